@@ -1,0 +1,247 @@
+// Trial-executor kernels for the resident (warm) trial runtime on MI355X (gfx950).
+//
+// The reference (Polyaxon 0.2.8) never touches the training step: each trial is a pod running user
+// code (polyaxon/scheduler/spawners/experiment_spawner.py:108-179).  The MI355X-native executor keeps
+// one warm process per GPU and replays a captured hipGraph for every trial, so everything that differs
+// between trials (hyper-parameters, weights, optimizer state, step counter) must live in device memory
+// and be (re)written by kernels, never by re-capturing.  This file provides those kernels:
+//
+//   plx_sgd_flat      fused SGD(momentum, nesterov, decoupled-from-BN weight decay) over ONE flat fp32
+//                     parameter/grad/momentum buffer; reads hyper-parameters from device memory and zeroes
+//                     the gradient in the same pass (no separate zero_grad memset).
+//   plx_adamw_flat    fused AdamW over flat buffers, bias correction from a device step counter.
+//   plx_init_flat     re-initialises every parameter segment in one launch (Philox4x32-10 normal /
+//                     uniform / constant) so a new trial starts from fresh random weights in-place.
+//   plx_record_metric appends the step loss to a device ring and advances the device step counter.
+//   plx_commit_metric reduces the last `window` ring entries into a slot of the HPO metric tensor.
+//
+// All memory-bound kernels use 16-byte (float4) accesses and a grid capped at 2048 blocks with a
+// grid-stride loop (cdna_hip_programming.md Guideline 11/13).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PLX_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kBlock = 256;
+
+inline int grid_for(int64_t n_vec) {
+  int64_t g = (n_vec + kBlock - 1) / kBlock;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+// ---------------------------------------------------------------- SGD
+// hp layout (fp32, device): [0] lr, [1] momentum, [2] weight_decay, [3] nesterov (0/1), [4] dampening
+// Elements [0, n_decay) receive weight decay (conv / linear weights), [n_decay, n) do not (BN, bias).
+__global__ __launch_bounds__(kBlock) void sgd_flat_kernel(float4* __restrict__ p, float4* __restrict__ g,
+                                                          float4* __restrict__ m, int64_t n_vec,
+                                                          int64_t n_decay_vec, const float* __restrict__ hp,
+                                                          const int* __restrict__ first_step) {
+  const float lr = hp[0], mom = hp[1], wd = hp[2], damp = hp[4];
+  const bool nesterov = hp[3] != 0.f;
+  // First step after (re)initialisation: momentum buffer := grad (torch.optim.SGD semantics).
+  const bool first = first_step != nullptr && *first_step == 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_vec; i += stride) {
+    float4 pv = p[i], gv = g[i], mv = m[i];
+    const float w = i < n_decay_vec ? wd : 0.f;
+    float gg[4] = {gv.x + w * pv.x, gv.y + w * pv.y, gv.z + w * pv.z, gv.w + w * pv.w};
+    float mm[4] = {mv.x, mv.y, mv.z, mv.w};
+    float pp[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mm[k] = first ? gg[k] : mom * mm[k] + (1.f - damp) * gg[k];
+      const float d = nesterov ? gg[k] + mom * mm[k] : mm[k];
+      pp[k] -= lr * d;
+    }
+    p[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    m[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+    g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// ---------------------------------------------------------------- AdamW
+// hp layout: [0] lr, [1] beta1, [2] beta2, [3] eps, [4] weight_decay. step = *step_ptr + 1.
+__global__ __launch_bounds__(kBlock) void adamw_flat_kernel(float4* __restrict__ p, float4* __restrict__ g,
+                                                            float4* __restrict__ m, float4* __restrict__ v,
+                                                            int64_t n_vec, int64_t n_decay_vec,
+                                                            const float* __restrict__ hp,
+                                                            const int* __restrict__ step_ptr) {
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
+  const float t = (float)(*step_ptr + 1);
+  const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
+  const float step_size = lr / bc1, inv_sqrt_bc2 = rsqrtf(bc2);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_vec; i += stride) {
+    float4 pv = p[i], gv = g[i], mv = m[i], vv = v[i];
+    const float decay = i < n_decay_vec ? (1.f - lr * wd) : 1.f;
+    float pp[4] = {pv.x, pv.y, pv.z, pv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
+    float mm[4] = {mv.x, mv.y, mv.z, mv.w}, vq[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mm[k] = b1 * mm[k] + (1.f - b1) * gg[k];
+      vq[k] = b2 * vq[k] + (1.f - b2) * gg[k] * gg[k];
+      const float denom = sqrtf(vq[k]) * inv_sqrt_bc2 + eps;
+      pp[k] = pp[k] * decay - step_size * mm[k] / denom;
+    }
+    p[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    m[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+    v[i] = make_float4(vq[0], vq[1], vq[2], vq[3]);
+    g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ float u01(uint32_t x) {  // (0, 1]
+  return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+// Segment table (device): per chunk -> (segment start, chunk begin, chunk end); per segment kind/scale.
+// kind 0: normal(0, scale); 1: constant(scale); 2: uniform(-scale, scale).
+__global__ __launch_bounds__(kBlock) void init_flat_kernel(float* __restrict__ p, const int64_t* __restrict__ chunk_lo,
+                                                           const int64_t* __restrict__ chunk_hi,
+                                                           const int* __restrict__ chunk_seg,
+                                                           const int* __restrict__ seg_kind,
+                                                           const float* __restrict__ seg_scale, uint64_t seed) {
+  const int c = blockIdx.x;
+  const int64_t lo = chunk_lo[c], hi = chunk_hi[c];
+  const int s = chunk_seg[c];
+  const int kind = seg_kind[s];
+  const float scale = seg_scale[s];
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  for (int64_t base = lo + 4 * (int64_t)threadIdx.x; base < hi; base += 4 * (int64_t)blockDim.x) {
+    float vals[4];
+    if (kind == 1) {
+      vals[0] = vals[1] = vals[2] = vals[3] = scale;
+    } else {
+      const uint64_t ctr = (uint64_t)base >> 2;
+      U4 r = philox(U4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0x5eedu, 0u}, k0, k1);
+      if (kind == 0) {
+        const float r1 = sqrtf(-2.f * __logf(u01(r.x))), r2 = sqrtf(-2.f * __logf(u01(r.z)));
+        float sn, cs, sn2, cs2;
+        __sincosf(6.2831853f * u01(r.y), &sn, &cs);
+        __sincosf(6.2831853f * u01(r.w), &sn2, &cs2);
+        vals[0] = scale * r1 * cs;
+        vals[1] = scale * r1 * sn;
+        vals[2] = scale * r2 * cs2;
+        vals[3] = scale * r2 * sn2;
+      } else {
+        vals[0] = scale * (2.f * u01(r.x) - 1.f);
+        vals[1] = scale * (2.f * u01(r.y) - 1.f);
+        vals[2] = scale * (2.f * u01(r.z) - 1.f);
+        vals[3] = scale * (2.f * u01(r.w) - 1.f);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (base + k < hi) p[base + k] = vals[k];
+  }
+}
+
+__global__ void zero_kernel(float4* __restrict__ x, int64_t n_vec) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_vec; i += stride)
+    x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// ---------------------------------------------------------------- metric ring
+// loss: one scalar (fp32 or bf16 bits selected by is_bf16). ring[step % ring_size] = loss; ++step.
+__global__ void record_metric_kernel(const void* __restrict__ loss, int is_bf16, float* __restrict__ ring,
+                                     int* __restrict__ step, int ring_size) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    float v;
+    if (is_bf16) {
+      const uint16_t b = *reinterpret_cast<const uint16_t*>(loss);
+      v = __uint_as_float(((uint32_t)b) << 16);
+    } else {
+      v = *reinterpret_cast<const float*>(loss);
+    }
+    const int s = *step;
+    ring[s % ring_size] = v;
+    *step = s + 1;
+  }
+}
+
+// out[slot] = mean of the last `window` ring entries ending at step-1 (NaN if no steps ran).
+__global__ void commit_metric_kernel(const float* __restrict__ ring, const int* __restrict__ step, int ring_size,
+                                     int window, float* __restrict__ out, int slot) {
+  __shared__ float part[64];
+  const int s = *step;
+  const int w = window < s ? window : s;
+  float acc = 0.f;
+  for (int j = threadIdx.x; j < w; j += blockDim.x) acc += ring[(s - 1 - j) % ring_size];
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t += part[k];
+    out[slot] = w > 0 ? t / (float)w : __builtin_nanf("");
+  }
+}
+
+}  // namespace
+
+PLX_API int plx_sgd_flat(float* p, float* g, float* m, int64_t n, int64_t n_decay, const float* hp,
+                         const int* first_step, hipStream_t stream) {
+  if ((n & 3) || (n_decay & 3)) return 1;  // caller pads flat buffers to a multiple of 4 floats
+  const int64_t nv = n >> 2;
+  hipLaunchKernelGGL(sgd_flat_kernel, dim3(grid_for(nv)), dim3(kBlock), 0, stream, (float4*)p, (float4*)g,
+                     (float4*)m, nv, n_decay >> 2, hp, first_step);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_adamw_flat(float* p, float* g, float* m, float* v, int64_t n, int64_t n_decay, const float* hp,
+                           const int* step, hipStream_t stream) {
+  if ((n & 3) || (n_decay & 3)) return 1;
+  const int64_t nv = n >> 2;
+  hipLaunchKernelGGL(adamw_flat_kernel, dim3(grid_for(nv)), dim3(kBlock), 0, stream, (float4*)p, (float4*)g,
+                     (float4*)m, (float4*)v, nv, n_decay >> 2, hp, step);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_init_flat(float* p, const int64_t* chunk_lo, const int64_t* chunk_hi, const int* chunk_seg,
+                          int n_chunks, const int* seg_kind, const float* seg_scale, uint64_t seed,
+                          hipStream_t stream) {
+  if (n_chunks <= 0) return 0;
+  hipLaunchKernelGGL(init_flat_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, p, chunk_lo, chunk_hi, chunk_seg,
+                     seg_kind, seg_scale, seed);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_zero_flat(float* x, int64_t n, hipStream_t stream) {
+  if (n & 3) return 1;
+  hipLaunchKernelGGL(zero_kernel, dim3(grid_for(n >> 2)), dim3(kBlock), 0, stream, (float4*)x, n >> 2);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_record_metric(const void* loss, int is_bf16, float* ring, int* step, int ring_size,
+                              hipStream_t stream) {
+  hipLaunchKernelGGL(record_metric_kernel, dim3(1), dim3(64), 0, stream, loss, is_bf16, ring, step, ring_size);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_commit_metric(const float* ring, const int* step, int ring_size, int window, float* out, int slot,
+                              hipStream_t stream) {
+  hipLaunchKernelGGL(commit_metric_kernel, dim3(1), dim3(256), 0, stream, ring, step, ring_size, window, out, slot);
+  return (int)hipGetLastError();
+}

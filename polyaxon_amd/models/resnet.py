@@ -1,0 +1,122 @@
+"""ResNet-50 (v1.5: stride on the 3x3 conv) for the Hyperband/ASHA north-star sweep (BASELINE.json config 3).
+
+The reference ships no models; the north-star workload names a ResNet-50 sweep on
+synthetic ImageNet-shape data, so the framework carries its own architecture definition.  It is laid out
+for MI355X: channels_last (NHWC) activations so MIOpen picks its NHWC implicit-GEMM convolutions that
+map onto MFMA, bf16 autocast compute, fp32 master weights living in one flat buffer (see
+``polyaxon_amd.ops.flat``) so the whole optimizer step is one fused HIP kernel.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Type
+
+import torch
+import torch.nn as nn
+
+from polyaxon_amd.ops.norm import BatchNormAct
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, in_ch: int, width: int, stride: int = 1, downsample: Optional[nn.Module] = None,
+                 fused: bool = True):
+        super().__init__()
+        out_ch = width * self.expansion
+        self.conv1 = nn.Conv2d(in_ch, width, 1, bias=False)
+        self.bn1 = BatchNormAct(width, act=True, fused=fused)
+        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = BatchNormAct(width, act=True, fused=fused)
+        self.conv3 = nn.Conv2d(width, out_ch, 1, bias=False)
+        # bn3 fuses the residual add and the final ReLU: y = relu(bn(x) + identity)
+        self.bn3 = BatchNormAct(out_ch, act=True, fused=fused, residual=True)
+        self.downsample = downsample
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), identity)
+
+
+class Downsample(nn.Module):
+    def __init__(self, in_ch: int, out_ch: int, stride: int, fused: bool = True):
+        super().__init__()
+        self.conv = nn.Conv2d(in_ch, out_ch, 1, stride=stride, bias=False)
+        self.bn = BatchNormAct(out_ch, act=False, fused=fused)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.bn(self.conv(x))
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers: List[int], num_classes: int = 1000, width: int = 64,
+                 zero_init_residual: bool = True, fused: bool = True):
+        super().__init__()
+        self.stem = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
+        self.stem_bn = BatchNormAct(width, act=True, fused=fused)
+        self.pool = nn.MaxPool2d(3, stride=2, padding=1)
+        stages = []
+        in_ch = width
+        for i, n in enumerate(layers):
+            w = width * (2 ** i)
+            stride = 1 if i == 0 else 2
+            blocks = []
+            for j in range(n):
+                ds = None
+                if j == 0 and (stride != 1 or in_ch != w * Bottleneck.expansion):
+                    ds = Downsample(in_ch, w * Bottleneck.expansion, stride, fused=fused)
+                blocks.append(Bottleneck(in_ch, w, stride if j == 0 else 1, ds, fused=fused))
+                in_ch = w * Bottleneck.expansion
+            stages.append(nn.Sequential(*blocks))
+        self.stages = nn.Sequential(*stages)
+        self.fc = nn.Linear(in_ch, num_classes)
+        self.zero_init_residual = zero_init_residual
+        self.reset_parameters()
+
+    def init_spec(self):
+        """(param, kind, scale) triples describing the per-tensor random init (used by the fused
+        in-place re-initialiser, ``plx_init_flat``): kaiming-normal fan_out for convs, BN gamma=1
+        (0 for the last BN of each residual branch when zero_init_residual), beta=0, fc uniform."""
+        spec = []
+        for name, mod in self.named_modules():
+            if isinstance(mod, nn.Conv2d):
+                fan_out = mod.out_channels * mod.kernel_size[0] * mod.kernel_size[1]
+                spec.append((mod.weight, "normal", (2.0 / fan_out) ** 0.5))
+            elif isinstance(mod, BatchNormAct):
+                gamma = 0.0 if (self.zero_init_residual and mod.residual) else 1.0
+                spec.append((mod.weight, "const", gamma))
+                spec.append((mod.bias, "const", 0.0))
+            elif isinstance(mod, nn.Linear):
+                bound = 1.0 / mod.in_features ** 0.5
+                spec.append((mod.weight, "uniform", bound))
+                spec.append((mod.bias, "uniform", bound))
+        return spec
+
+    @torch.no_grad()
+    def reset_parameters(self) -> None:
+        for p, kind, scale in self.init_spec():
+            if kind == "normal":
+                p.normal_(0.0, scale)
+            elif kind == "const":
+                p.fill_(scale)
+            else:
+                p.uniform_(-scale, scale)
+        for mod in self.modules():
+            if isinstance(mod, BatchNormAct):
+                mod.reset_running_stats()
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.pool(self.stem_bn(self.stem(x)))
+        x = self.stages(x)
+        x = torch.flatten(x.mean((2, 3)), 1) if x.is_contiguous() else x.mean((2, 3))
+        return self.fc(x)
+
+
+def resnet50(num_classes: int = 1000, fused: bool = True, **kw) -> ResNet:
+    return ResNet([3, 4, 6, 3], num_classes=num_classes, fused=fused, **kw)
+
+
+def resnet18ish(num_classes: int = 10, fused: bool = True, **kw) -> ResNet:
+    """Small bottleneck ResNet used by CPU tests (same code path, fewer blocks and channels)."""
+    return ResNet([1, 1, 1, 1], num_classes=num_classes, width=8, fused=fused, **kw)

@@ -1,0 +1,148 @@
+"""Build and load the in-tree native libraries (HIP kernels for gfx950 + C++ runtime pieces).
+
+Every library is compiled with ``hipcc --offload-arch=gfx950`` (or ``g++`` for host-only C++) straight
+into ``polyaxon_amd/_native/lib<name>.so`` and loaded with :mod:`ctypes`.  The kernels take raw device
+pointers and a ``hipStream_t`` (torch's current stream), so they are captured by hipGraphs like any other
+launch.  There is deliberately no pure-PyTorch fallback on a GPU box: if a library is missing there,
+:func:`lib` raises, so a silent eager path can never pass for the native one.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import shutil
+import subprocess
+import threading
+from pathlib import Path
+from typing import Dict, Iterable, List, Optional
+
+PKG_DIR = Path(__file__).resolve().parent.parent
+CSRC = PKG_DIR / "csrc"
+OUT = PKG_DIR / "_native"
+ARCH = os.environ.get("PLX_OFFLOAD_ARCH", "gfx950")
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+
+# name -> (sources, kind, extra link flags)
+LIBRARIES: Dict[str, dict] = {
+    "plx_train": {"sources": ["train_kernels.hip"], "kind": "hip", "link": []},
+    "plx_polytune": {"sources": ["polytune_kernels.hip"], "kind": "hip", "link": []},
+}
+
+_lock = threading.Lock()
+_loaded: Dict[str, ctypes.CDLL] = {}
+
+
+def _register(name: str, sources: List[str], kind: str, link: Optional[List[str]] = None) -> None:
+    LIBRARIES[name] = {"sources": sources, "kind": kind, "link": list(link or [])}
+
+
+def lib_path(name: str) -> Path:
+    return OUT / f"lib{name}.so"
+
+
+def _digest(sources: Iterable[Path], flags: List[str]) -> str:
+    h = hashlib.sha256()
+    for s in sources:
+        h.update(s.read_bytes())
+    for hdr in sorted(CSRC.glob("*.h")):
+        h.update(hdr.read_bytes())
+    h.update(" ".join(flags).encode())
+    return h.hexdigest()[:16]
+
+
+def _flags(kind: str) -> List[str]:
+    common = ["-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-function", f"-I{CSRC}"]
+    if kind == "hip":
+        return common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+    if kind == "hip_host":  # host C++ that links the HIP runtime (streams, events, pinned memory, RCCL)
+        return common + [f"-I{ROCM / 'include'}", "-D__HIP_PLATFORM_AMD__"]
+    return common  # plain host C++
+
+
+def build(name: str, force: bool = False, verbose: bool = False) -> Path:
+    """Compile one library if its sources changed. Returns the .so path."""
+    spec = LIBRARIES[name]
+    srcs = [CSRC / s for s in spec["sources"]]
+    flags = _flags(spec["kind"])
+    out = lib_path(name)
+    stamp = out.with_suffix(".so.sha")
+    digest = _digest(srcs, flags + spec["link"])
+    if not force and out.exists() and stamp.exists() and stamp.read_text().strip() == digest:
+        return out
+    OUT.mkdir(parents=True, exist_ok=True)
+    if spec["kind"] in ("hip", "hip_host"):
+        cc = shutil.which("hipcc") or str(ROCM / "bin" / "hipcc")
+    else:
+        cc = shutil.which("g++") or "g++"
+    link = list(spec["link"])
+    if spec["kind"] == "hip_host":
+        link = [f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}"] + link + ["-lamdhip64"]
+    tmp = out.with_suffix(f".so.tmp{os.getpid()}")
+    cmd = [cc, *flags, *map(str, srcs), "-o", str(tmp), *link]
+    if verbose:
+        print(" ".join(cmd))
+    proc = subprocess.run(cmd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError(f"native build of {name} failed:\n{' '.join(cmd)}\n{proc.stderr[-6000:]}")
+    os.replace(tmp, out)
+    stamp.write_text(digest)
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = False) -> List[Path]:
+    return [build(n, force=force, verbose=verbose) for n in LIBRARIES]
+
+
+def available(name: str) -> bool:
+    return lib_path(name).exists()
+
+
+def lib(name: str) -> ctypes.CDLL:
+    """Load (building on first use if a compiler is present) the named native library."""
+    with _lock:
+        if name in _loaded:
+            return _loaded[name]
+        path = lib_path(name)
+        if not path.exists() or os.environ.get("PLX_NATIVE_REBUILD") == "1":
+            build(name)
+        handle = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+        _declare(name, handle)
+        _loaded[name] = handle
+        return handle
+
+
+# ----------------------------------------------------------------------------- signatures
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_int64
+_U64 = ctypes.c_uint64
+_F = ctypes.c_float
+_D = ctypes.c_double
+
+SIGNATURES: Dict[str, Dict[str, list]] = {
+    "plx_train": {
+        "plx_sgd_flat": [_P, _P, _P, _L, _L, _P, _P, _P],
+        "plx_adamw_flat": [_P, _P, _P, _P, _L, _L, _P, _P, _P],
+        "plx_init_flat": [_P, _P, _P, _P, _I, _P, _P, _U64, _P],
+        "plx_zero_flat": [_P, _L, _P],
+        "plx_record_metric": [_P, _I, _P, _P, _I, _P],
+        "plx_commit_metric": [_P, _P, _I, _I, _P, _I, _P],
+    },
+    "plx_polytune": {
+        "plx_topk_brackets": [_P, _P, _I, _I, _I, _I, _P, _P],
+        "plx_early_stop_any": [_P, _I, _I, _P, _P, _P, _I, _P, _P],
+    },
+}
+
+
+def _declare(name: str, handle: ctypes.CDLL) -> None:
+    for fn, argtypes in SIGNATURES.get(name, {}).items():
+        f = getattr(handle, fn)
+        f.argtypes = argtypes
+        f.restype = _I
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with code {rc}")

@@ -1,0 +1,136 @@
+"""Flat parameter storage: every parameter of a module becomes a view into ONE fp32 buffer.
+
+Why (MI355X-first): the optimizer step then touches three contiguous buffers (params, grads, state) with
+one vectorised HIP kernel (``plx_sgd_flat`` / ``plx_adamw_flat``) instead of ~160 tensors × several
+foreach launches; re-initialising a trial's weights is one ``plx_init_flat`` launch; snapshotting a trial
+for Hyperband *resume* is one device-to-device copy of a contiguous buffer; and every pointer is fixed for
+the life of the executor, so a captured hipGraph stays valid across trials.
+
+Layout: parameters that take weight decay (ndim > 1: conv / linear weights) come first, the rest
+(BN affine, biases) after, each segment padded to 4 floats so the kernels can use float4 accesses.
+4-D conv weights get channels_last strides inside the flat buffer so MIOpen's NHWC kernels read them
+without a layout transform, and their ``.grad`` aliases the flat gradient buffer with the same strides.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Tuple
+
+import torch
+import torch.nn as nn
+
+_KIND = {"normal": 0, "const": 1, "uniform": 2}
+CHUNK = 16384
+
+
+def _contig_strides(shape) -> Tuple[int, ...]:
+    strides, acc = [], 1
+    for s in reversed(shape):
+        strides.append(acc)
+        acc *= s
+    return tuple(reversed(strides))
+
+
+def _cl_strides(shape) -> Tuple[int, ...]:
+    n, c, h, w = shape
+    return (h * w * c, 1, w * c, c)
+
+
+def _pad4(n: int) -> int:
+    return (n + 3) & ~3
+
+
+@dataclass
+class Segment:
+    name: str
+    offset: int
+    numel: int
+    shape: Tuple[int, ...]
+    strides: Tuple[int, ...]
+    decay: bool
+
+
+class FlatParams:
+    """Re-home ``module``'s parameters into flat fp32 ``params``/``grads`` buffers on ``device``."""
+
+    def __init__(self, module: nn.Module, device: torch.device, channels_last: bool = True):
+        named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
+        decay = [(n, p) for n, p in named if p.dim() > 1]
+        no_decay = [(n, p) for n, p in named if p.dim() <= 1]
+        self.segments: List[Segment] = []
+        off = 0
+        for group, is_decay in ((decay, True), (no_decay, False)):
+            for n, p in group:
+                strides = (_cl_strides(p.shape) if (channels_last and p.dim() == 4)
+                           else _contig_strides(p.shape))
+                self.segments.append(Segment(n, off, p.numel(), tuple(p.shape), strides, is_decay))
+                off += _pad4(p.numel())
+            if is_decay:
+                self.n_decay = off
+        self.numel = off
+        self.device = torch.device(device)
+        self.params = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.grads = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        by_name: Dict[str, nn.Parameter] = dict(named)
+        self._views: Dict[str, torch.Tensor] = {}
+        with torch.no_grad():
+            for seg in self.segments:
+                old = by_name[seg.name]
+                view = self.params.as_strided(seg.shape, seg.strides, seg.offset)
+                view.copy_(old.detach().to(self.device))
+                newp = nn.Parameter(view)
+                newp.grad = self.grads.as_strided(seg.shape, seg.strides, seg.offset)
+                self._set(module, seg.name, newp)
+                self._views[seg.name] = newp
+        module.to(self.device)  # buffers (BN running stats)
+
+    @staticmethod
+    def _set(module: nn.Module, dotted: str, value: nn.Parameter) -> None:
+        parts = dotted.split(".")
+        for part in parts[:-1]:
+            module = getattr(module, part)
+        setattr(module, parts[-1], value)
+
+    def parameter(self, name: str) -> nn.Parameter:
+        return self._views[name]
+
+    def segment_of(self, param: torch.Tensor) -> Segment:
+        for seg in self.segments:
+            if self._views[seg.name] is param:
+                return seg
+        raise KeyError("parameter is not part of this FlatParams")
+
+    # ------------------------------------------------------------------ fused re-init tables
+    def init_tables(self, init_spec) -> Dict[str, torch.Tensor]:
+        """Chunk tables for ``plx_init_flat`` from (param, kind, scale) triples (model.init_spec())."""
+        kinds, scales, lo, hi, seg_id = [], [], [], [], []
+        for i, (p, kind, scale) in enumerate(init_spec):
+            seg = self.segment_of(p)
+            kinds.append(_KIND[kind])
+            scales.append(float(scale))
+            start, end = seg.offset, seg.offset + seg.numel
+            for c in range(start, end, CHUNK):
+                lo.append(c)
+                hi.append(min(c + CHUNK, end))
+                seg_id.append(i)
+        dev = self.device
+        return {
+            "chunk_lo": torch.tensor(lo, dtype=torch.int64, device=dev),
+            "chunk_hi": torch.tensor(hi, dtype=torch.int64, device=dev),
+            "chunk_seg": torch.tensor(seg_id, dtype=torch.int32, device=dev),
+            "seg_kind": torch.tensor(kinds, dtype=torch.int32, device=dev),
+            "seg_scale": torch.tensor(scales, dtype=torch.float32, device=dev),
+        }
+
+    def init_reference(self, init_spec, seed: int) -> None:
+        """CPU / numerics-reference re-initialiser (torch RNG; distributions match the kernel)."""
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        with torch.no_grad():
+            for p, kind, scale in init_spec:
+                if kind == "normal":
+                    v = torch.randn(p.shape, generator=g) * scale
+                elif kind == "const":
+                    v = torch.full(p.shape, float(scale))
+                else:
+                    v = (torch.rand(p.shape, generator=g) * 2 - 1) * scale
+                p.copy_(v.to(p.device))

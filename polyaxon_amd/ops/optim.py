@@ -1,0 +1,138 @@
+"""Fused flat-buffer optimizers with device-resident hyper-parameters.
+
+The hyper-parameters (lr, momentum, weight decay, ...) live in a small fp32 device tensor that the kernel
+reads at run time.  A trial executor therefore changes a trial's hyper-parameters with one 32-byte H2D
+copy and keeps replaying the SAME captured hipGraph — the graph never has to be re-captured per trial,
+which is what makes a warm per-GPU trial executor cheap (SURVEY.md §7.1 polyflow; BASELINE.md "reference
+design constants": every reference trial pays pod start + 1 s task hops instead).
+
+On CPU (no native library) the same update is computed with torch ops; tests compare the two.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from polyaxon_amd.ops import _native
+from polyaxon_amd.ops.flat import FlatParams
+
+
+def _stream_ptr(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+class FusedSGD:
+    """SGD with momentum / nesterov / dampening and weight decay on the decay segment only."""
+
+    HP = ("lr", "momentum", "weight_decay", "nesterov", "dampening")
+
+    def __init__(self, flat: FlatParams, lr: float = 0.1, momentum: float = 0.9, weight_decay: float = 1e-4,
+                 nesterov: bool = False, dampening: float = 0.0, step_counter: Optional[torch.Tensor] = None):
+        self.flat = flat
+        dev = flat.device
+        self.momentum_buf = torch.zeros_like(flat.params)
+        self.hp = torch.zeros(8, dtype=torch.float32, device=dev)
+        # step counter shared with the metric ring: 0 right after reset() => momentum := grad
+        self.step = step_counter if step_counter is not None else torch.zeros(1, dtype=torch.int32, device=dev)
+        self.set_hparams(lr=lr, momentum=momentum, weight_decay=weight_decay, nesterov=nesterov,
+                         dampening=dampening)
+
+    def set_hparams(self, **hp) -> None:
+        vals = getattr(self, "_hp_host", {k: 0.0 for k in self.HP})
+        for k, v in hp.items():
+            if k not in self.HP:
+                raise KeyError(f"unknown SGD hyper-parameter {k!r}")
+            vals[k] = float(v)
+        self._hp_host = vals
+        host = torch.tensor([vals[k] for k in self.HP] + [0.0] * (8 - len(self.HP)), dtype=torch.float32)
+        self.hp.copy_(host.pin_memory() if self.hp.is_cuda else host, non_blocking=self.hp.is_cuda)
+
+    def reset_state(self) -> None:
+        if self.flat.params.is_cuda:
+            _native.check(_native.lib("plx_train").plx_zero_flat(
+                self.momentum_buf.data_ptr(), self.momentum_buf.numel(), _stream_ptr(self.hp)), "plx_zero_flat")
+        else:
+            self.momentum_buf.zero_()
+
+    def step_(self) -> None:
+        f = self.flat
+        if f.params.is_cuda:
+            rc = _native.lib("plx_train").plx_sgd_flat(
+                f.params.data_ptr(), f.grads.data_ptr(), self.momentum_buf.data_ptr(), f.numel, f.n_decay,
+                self.hp.data_ptr(), self.step.data_ptr(), _stream_ptr(f.params))
+            _native.check(rc, "plx_sgd_flat")
+        else:
+            self._step_reference()
+
+    @torch.no_grad()
+    def _step_reference(self) -> None:
+        f = self.flat
+        lr, mom, wd, nest, damp = (float(self.hp[i]) for i in range(5))
+        g = f.grads.clone()
+        g[: f.n_decay] += wd * f.params[: f.n_decay]
+        if int(self.step.item()) == 0:
+            self.momentum_buf.copy_(g)
+        else:
+            self.momentum_buf.mul_(mom).add_(g, alpha=1.0 - damp)
+        d = g + mom * self.momentum_buf if nest else self.momentum_buf
+        f.params.sub_(lr * d)
+        f.grads.zero_()
+
+    def state_buffers(self) -> Dict[str, torch.Tensor]:
+        return {"momentum": self.momentum_buf}
+
+
+class FusedAdamW:
+    HP = ("lr", "beta1", "beta2", "eps", "weight_decay")
+
+    def __init__(self, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-2, step_counter: Optional[torch.Tensor] = None):
+        self.flat = flat
+        dev = flat.device
+        self.exp_avg = torch.zeros_like(flat.params)
+        self.exp_avg_sq = torch.zeros_like(flat.params)
+        self.hp = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.step = step_counter if step_counter is not None else torch.zeros(1, dtype=torch.int32, device=dev)
+        self.set_hparams(lr=lr, beta1=betas[0], beta2=betas[1], eps=eps, weight_decay=weight_decay)
+
+    def set_hparams(self, **hp) -> None:
+        vals = getattr(self, "_hp_host", {k: 0.0 for k in self.HP})
+        for k, v in hp.items():
+            if k not in self.HP:
+                raise KeyError(f"unknown AdamW hyper-parameter {k!r}")
+            vals[k] = float(v)
+        self._hp_host = vals
+        host = torch.tensor([vals[k] for k in self.HP] + [0.0] * (8 - len(self.HP)), dtype=torch.float32)
+        self.hp.copy_(host.pin_memory() if self.hp.is_cuda else host, non_blocking=self.hp.is_cuda)
+
+    def reset_state(self) -> None:
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+
+    def step_(self) -> None:
+        f = self.flat
+        if f.params.is_cuda:
+            rc = _native.lib("plx_train").plx_adamw_flat(
+                f.params.data_ptr(), f.grads.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                f.numel, f.n_decay, self.hp.data_ptr(), self.step.data_ptr(), _stream_ptr(f.params))
+            _native.check(rc, "plx_adamw_flat")
+        else:
+            self._step_reference()
+
+    @torch.no_grad()
+    def _step_reference(self) -> None:
+        f = self.flat
+        lr, b1, b2, eps, wd = (float(self.hp[i]) for i in range(5))
+        t = int(self.step.item()) + 1
+        g = f.grads
+        f.params[: f.n_decay].mul_(1.0 - lr * wd)
+        self.exp_avg.mul_(b1).add_(g, alpha=1 - b1)
+        self.exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+        denom = (self.exp_avg_sq.sqrt() / bc2 ** 0.5).add_(eps)
+        f.params.addcdiv_(self.exp_avg, denom, value=-lr / bc1)
+        g.zero_()
+
+    def state_buffers(self) -> Dict[str, torch.Tensor]:
+        return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}

@@ -1,0 +1,220 @@
+"""Resident (warm) trial executor: one per GPU, runs trial after trial without leaving the process.
+
+The reference runs every trial — including every Hyperband promotion, which it models as a *new*
+experiment (``experiment.resume/restart``, polyaxon/hpsearch/iteration_managers/hyperband.py:94-113) —
+as a fresh Kubernetes pod: image check, pod create, container start, framework import, CUDA context,
+cuDNN autotune, and a 1–30 s chain of Celery hops around it (BASELINE.md "reference design constants").
+On a single MI355X node the expensive, trial-invariant parts are all reusable, so polyflow keeps them
+resident:
+
+* the model, its flat fp32 weights/grads and optimizer state are allocated once (``FlatParams``);
+* the full training step (forward, backward, fused optimizer, metric record) is captured once as a
+  hipGraph and replayed for every step of every trial;
+* everything trial-specific is device data rewritten by kernels: weights (``plx_init_flat``),
+  optimizer state (``plx_zero_flat``), hyper-parameters (one 32-byte H2D copy), step counter;
+* the step loss goes to a device ring (``plx_record_metric``); a trial's result is reduced on the device
+  into the HPO metric tensor (``plx_commit_metric``), so no host sync happens inside a trial;
+* Hyperband *resume* snapshots live in HBM (288 GB per GPU holds hundreds of ResNet-50 trial states), so
+  a promotion is a device-to-device copy instead of a checkpoint file round trip.
+
+The same class runs on CPU (no graph, reference kernels) for the unit tests.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import Callable, Dict, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from polyaxon_amd.ops import _native
+from polyaxon_amd.ops.flat import FlatParams
+from polyaxon_amd.ops.optim import FusedAdamW, FusedSGD
+
+
+def _stream_ptr(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+@dataclass
+class TrialState:
+    params: torch.Tensor
+    opt: Dict[str, torch.Tensor]
+    buffers: torch.Tensor
+    step: torch.Tensor
+
+
+class ResidentTrialExecutor:
+    def __init__(self, model: nn.Module, batch: Tuple[torch.Tensor, torch.Tensor], device,
+                 loss_fn: Optional[Callable] = None, optimizer: str = "sgd", use_graph: bool = True,
+                 amp_dtype: Optional[torch.dtype] = torch.bfloat16, channels_last: bool = True,
+                 ring_size: int = 4096, init_spec: Optional[Callable] = None):
+        self.device = torch.device(device)
+        self.is_cuda = self.device.type == "cuda"
+        if channels_last:
+            model = model.to(memory_format=torch.channels_last)
+        self.model = model
+        self.flat = FlatParams(model, self.device, channels_last=channels_last)
+        self._flatten_buffers()
+        self.step = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if optimizer == "sgd":
+            self.opt = FusedSGD(self.flat, step_counter=self.step)
+        elif optimizer == "adamw":
+            self.opt = FusedAdamW(self.flat, step_counter=self.step)
+        else:
+            raise ValueError(f"unknown optimizer {optimizer!r}")
+        self.loss_fn = loss_fn or (lambda out, y: F.cross_entropy(out.float(), y))
+        self.x, self.y = batch[0].to(self.device), batch[1].to(self.device)
+        self.amp_dtype = amp_dtype if self.is_cuda else None
+        self.ring_size = ring_size
+        self.ring = torch.zeros(ring_size, dtype=torch.float32, device=self.device)
+        spec = init_spec() if init_spec is not None else (model.init_spec() if hasattr(model, "init_spec") else None)
+        self._init_spec = spec
+        self._init_tables = self.flat.init_tables(spec) if (spec is not None and self.is_cuda) else None
+        self.use_graph = use_graph and self.is_cuda
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.snapshots: Dict[object, TrialState] = {}
+        self.model.train()
+
+    # ------------------------------------------------------------------ buffers (BN running stats)
+    def _flatten_buffers(self) -> None:
+        bufs = [(n, b) for n, b in self.model.named_buffers() if b.dtype == torch.float32]
+        total = sum(b.numel() for _, b in bufs)
+        self.buffers = torch.zeros(max(total, 1), dtype=torch.float32, device=self.device)
+        self._buffer_init = torch.zeros_like(self.buffers)
+        off = 0
+        for name, b in bufs:
+            view = self.buffers[off: off + b.numel()].view_as(b)
+            view.copy_(b)
+            self._buffer_init[off: off + b.numel()].copy_(b.reshape(-1))
+            mod = self.model
+            parts = name.split(".")
+            for p in parts[:-1]:
+                mod = getattr(mod, p)
+            mod._buffers[parts[-1]] = view
+            off += b.numel()
+
+    # ------------------------------------------------------------------ the step
+    def _train_step(self) -> None:
+        if self.amp_dtype is not None:
+            with torch.autocast("cuda", dtype=self.amp_dtype):
+                out = self.model(self.x)
+                loss = self.loss_fn(out, self.y)
+        else:
+            out = self.model(self.x)
+            loss = self.loss_fn(out, self.y)
+        loss.backward()
+        self.opt.step_()
+        self._record(loss.detach())
+
+    def _record(self, loss: torch.Tensor) -> None:
+        if self.is_cuda:
+            loss = loss.float().contiguous()
+            rc = _native.lib("plx_train").plx_record_metric(loss.data_ptr(), 0, self.ring.data_ptr(),
+                                                             self.step.data_ptr(), self.ring_size,
+                                                             _stream_ptr(self.device))
+            _native.check(rc, "plx_record_metric")
+            self._last_loss = loss  # keep alive for the graph's lifetime
+        else:
+            s = int(self.step.item())
+            self.ring[s % self.ring_size] = float(loss)
+            self.step += 1
+
+    def capture(self, warmup: int = 3) -> None:
+        """Warm up (MIOpen find, allocator) and capture the training step as a hipGraph."""
+        if not self.use_graph:
+            return
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._train_step()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._train_step()
+        torch.cuda.synchronize(self.device)
+        self.graph = g
+
+    # ------------------------------------------------------------------ trial lifecycle
+    def reset(self, seed: int) -> None:
+        """Fresh random weights + zero optimizer state + step 0 (a new trial, reference RESTART)."""
+        with torch.no_grad():
+            if self.is_cuda and self._init_tables is not None:
+                t = self._init_tables
+                rc = _native.lib("plx_train").plx_init_flat(
+                    self.flat.params.data_ptr(), t["chunk_lo"].data_ptr(), t["chunk_hi"].data_ptr(),
+                    t["chunk_seg"].data_ptr(), int(t["chunk_lo"].numel()), t["seg_kind"].data_ptr(),
+                    t["seg_scale"].data_ptr(), int(seed) & 0xFFFFFFFFFFFFFFFF, _stream_ptr(self.device))
+                _native.check(rc, "plx_init_flat")
+            elif self._init_spec is not None:
+                self.flat.init_reference(self._init_spec, seed)
+            self.opt.reset_state()
+            self.flat.grads.zero_()
+            self.buffers.copy_(self._buffer_init)
+            self.step.zero_()
+
+    def set_hparams(self, **hp) -> None:
+        self.opt.set_hparams(**{k: v for k, v in hp.items() if k in self.opt.HP})
+
+    def run(self, n_steps: int) -> None:
+        for _ in range(n_steps):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self._train_step()
+
+    def commit(self, out: torch.Tensor, slot: int, window: int = 10) -> None:
+        """out[slot] = mean loss over the last ``window`` steps, computed on the device."""
+        if self.is_cuda:
+            rc = _native.lib("plx_train").plx_commit_metric(self.ring.data_ptr(), self.step.data_ptr(),
+                                                             self.ring_size, window, out.data_ptr(), slot,
+                                                             _stream_ptr(self.device))
+            _native.check(rc, "plx_commit_metric")
+        else:
+            s = int(self.step.item())
+            w = min(window, s)
+            if w == 0:
+                out.view(-1)[slot] = float("nan")
+            else:
+                idx = [(s - 1 - j) % self.ring_size for j in range(w)]
+                out.view(-1)[slot] = self.ring[idx].mean()
+
+    def losses(self) -> torch.Tensor:
+        s = int(self.step.item())
+        n = min(s, self.ring_size)
+        idx = [(s - n + j) % self.ring_size for j in range(n)]
+        return self.ring[idx].cpu()
+
+    # ------------------------------------------------------------------ HBM-resident snapshots
+    def snapshot(self, key) -> None:
+        st = self.snapshots.get(key)
+        bufs = self.opt.state_buffers()
+        if st is None:
+            st = TrialState(torch.empty_like(self.flat.params), {k: torch.empty_like(v) for k, v in bufs.items()},
+                            torch.empty_like(self.buffers), torch.empty_like(self.step))
+            self.snapshots[key] = st
+        st.params.copy_(self.flat.params, non_blocking=True)
+        for k, v in bufs.items():
+            st.opt[k].copy_(v, non_blocking=True)
+        st.buffers.copy_(self.buffers, non_blocking=True)
+        st.step.copy_(self.step, non_blocking=True)
+
+    def restore(self, key) -> None:
+        st = self.snapshots[key]
+        self.flat.params.copy_(st.params, non_blocking=True)
+        for k, v in self.opt.state_buffers().items():
+            v.copy_(st.opt[k], non_blocking=True)
+        self.buffers.copy_(st.buffers, non_blocking=True)
+        self.step.copy_(st.step, non_blocking=True)
+        self.flat.grads.zero_()
+
+    def drop(self, key) -> None:
+        self.snapshots.pop(key, None)
+
+    def snapshot_bytes(self) -> int:
+        n = self.flat.params.numel() * (1 + len(self.opt.state_buffers())) + self.buffers.numel()
+        return 4 * n

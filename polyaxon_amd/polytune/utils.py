@@ -1,0 +1,68 @@
+"""Suggestion bookkeeping and random sampling shared by the search managers.
+
+Behaviour parity with polyaxon/hpsearch/search_managers/utils.py:9-64:
+  * a suggestion is a dict of params; two suggestions are equal iff same keys and values; its hash is
+    the hash of the sorted ``key:value`` rendering, its uuid the uuid5 of that rendering;
+  * random suggestions are drawn with ``numpy.random.RandomState(seed)`` (global ``np.random`` when no
+    seed), de-duplicated, and capped at the size of the space when every matrix entry is discrete.
+"""
+from __future__ import annotations
+
+import copy
+import uuid
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from polyaxon_amd.spec.matrix import space_size
+
+
+class Suggestion:
+    __slots__ = ("params",)
+
+    def __init__(self, params: Dict[str, Any]):
+        self.params = params
+
+    def __eq__(self, other) -> bool:
+        if not isinstance(other, Suggestion) or self.params.keys() != other.params.keys():
+            return False
+        return all(v == other.params[k] for k, v in self.params.items())
+
+    def __repr__(self) -> str:
+        return ",".join(f"{k}:{v}" for k, v in sorted(self.params.items()))
+
+    def __hash__(self) -> int:
+        return hash(repr(self))
+
+    def uuid(self) -> uuid.UUID:
+        return uuid.uuid5(uuid.NAMESPACE_DNS, repr(self))
+
+
+def get_random_generator(seed: Optional[int] = None):
+    return np.random.RandomState(seed) if seed else np.random
+
+
+def _plain(v):
+    return v.item() if hasattr(v, "item") else v
+
+
+def get_random_suggestions(matrix, n_suggestions: int, suggestion_params: Optional[Dict] = None,
+                           seed: Optional[int] = None, rand_generator=None) -> List[Dict[str, Any]]:
+    if not n_suggestions:
+        raise ValueError("This search algorithm requires `n_experiments`.")
+    suggestion_params = suggestion_params or {}
+    rng = rand_generator if rand_generator is not None else get_random_generator(seed)
+    size = space_size(matrix)
+    if size is not None:
+        n_suggestions = min(n_suggestions, size)
+    seen = set()
+    out: List[Dict[str, Any]] = []
+    while n_suggestions > 0:
+        params = copy.deepcopy(suggestion_params)
+        params.update({k: _plain(v.sample(rand_generator=rng)) for k, v in matrix.items()})
+        s = Suggestion(params)
+        if s not in seen:
+            seen.add(s)
+            out.append(params)
+            n_suggestions -= 1
+    return out
