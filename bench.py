@@ -66,6 +66,7 @@ def main() -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--unfused", action="store_true", help="PyTorch BN/ReLU instead of the HIP kernels")
     ap.add_argument("--tune", action="store_true", help="exhaustive MIOpen find (cudnn.benchmark)")
+    ap.add_argument("--verbose", action="store_true", help="print every trial's record to stderr")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,6 +137,10 @@ def main() -> int:
         if r.metric <= args.target and r.end_event is not None:
             t_target = min(t_target, start_ev.elapsed_time(r.end_event) / 1000.0)
     best = min((r.metric for r in records if r.metric is not None), default=math.nan)
+    if args.verbose:
+        for r in records:
+            log(f"trial {r.trial} cfg {r.config_id} it {r.iteration}/{r.bracket_iteration} res {r.resource} "
+                f"steps {r.steps} metric {r.metric} params {r.params}")
     t = torch.tensor([elapsed, -t_target if math.isfinite(t_target) else -math.inf, train_steps, best],
                      dtype=torch.float64, device=dev)
     if world > 1:

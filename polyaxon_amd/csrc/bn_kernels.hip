@@ -1,0 +1,419 @@
+// Fused BatchNorm(+residual add)(+ReLU) for NHWC bf16 activations on MI355X (gfx950).
+//
+// A ResNet-50 training step runs 53 BatchNorms, 49 of them followed by ReLU and 16 by a residual add
+// first.  Unfused, that is stats + normalise + add + relu in the forward and relu-backward + BN-backward
+// (+ the add's gradient copy) in the backward: 7-9 full passes over each activation, all HBM-bound.
+// These kernels do it in 2 passes forward (stats, apply) and 2 backward (reduce, dx), 16-byte vectors
+// (8 x bf16) per lane, fp32 math, fp32 per-channel partials.
+//
+// Layout: x viewed as [M, C] row-major, M = N*H*W (channels_last), C % 8 == 0 and C/8 a power of two.
+// Thread t of a 256-thread block owns channel group cg = t % Gb (8 channels, Gb = min(C/8, 256)) and row
+// lane t / Gb, so its per-channel state (shift, scale, bias, mean, invstd) stays in registers while it
+// walks rows; one wave reads 64 x 16 B = 1 KiB contiguous per instruction.
+//
+//   plx_bn_fwd_stats     per-block shifted sum / sum-of-squares partials  [nblk, C] (+ level-2 reduce)
+//   plx_bn_fwd_finalize  mean, invstd, fused scale/bias, running-stat update (unbiased var)
+//   plx_bn_fwd_apply     y = act(x*scale + bias [+ res])
+//   plx_bn_bwd_reduce    partial sums of dz and dz*xhat   (dz = dy * [y > 0] when act)
+//   plx_bn_bwd_finalize  dgamma, dbeta and the dx coefficients  dx = A*dz + B*x + D
+//   plx_bn_bwd_dx        dx (and d_residual = dz) in one pass
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PLX_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct alignas(16) bf16x8 {
+  uint16_t v[8];
+};
+
+__device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {  // round-to-nearest-even
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // NaN stays NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ void load8(const bf16x8* p, float* f) {
+  const bf16x8 v = *p;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) f[k] = bf2f(v.v[k]);
+}
+
+__device__ __forceinline__ void store8(bf16x8* p, const float* f) {
+  bf16x8 v;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v.v[k] = f2bf(f[k]);
+  *p = v;
+}
+
+// ------------------------------------------------------------------------------- forward stats
+__global__ __launch_bounds__(kBlock) void bn_stats_kernel(const bf16x8* __restrict__ x, int64_t M, int G, int Gb,
+                                                          int64_t rows_per_block, float* __restrict__ psum,
+                                                          float* __restrict__ psq) {
+  __shared__ float s_sum[kBlock * 8];
+  __shared__ float s_sq[kBlock * 8];
+  const int tid = threadIdx.x;
+  const int cg_local = tid % Gb, rlane = tid / Gb, R = kBlock / Gb;
+  const int cg = blockIdx.y * Gb + cg_local;
+  const int C = G * 8;
+  float shift[8], s[8], q[8];
+  load8(x + cg, shift);  // row 0 as the shift: var = E[(x-k)^2] - E[x-k]^2 stays well conditioned
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = q[k] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  int64_t r1 = r0 + rows_per_block;
+  if (r1 > M) r1 = M;
+#pragma unroll 4
+  for (int64_t r = r0 + rlane; r < r1; r += R) {
+    float v[8];
+    load8(x + r * G + cg, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float d = v[k] - shift[k];
+      s[k] += d;
+      q[k] = fmaf(d, d, q[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s_sum[tid * 8 + k] = s[k];
+    s_sq[tid * 8 + k] = q[k];
+  }
+  __syncthreads();
+  if (rlane == 0) {
+    for (int j = 1; j < R; ++j) {
+      const int o = (j * Gb + cg_local) * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s[k] += s_sum[o + k];
+        q[k] += s_sq[o + k];
+      }
+    }
+    float* ps = psum + (int64_t)blockIdx.x * C + cg * 8;
+    float* pq = psq + (int64_t)blockIdx.x * C + cg * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ps[k] = s[k];
+      pq[k] = q[k];
+    }
+  }
+}
+
+// Level-2 reduction of the per-block partials: [2][nblk][C] -> [2][S][C], S = ceil(nblk / 64).
+// Block = 64 channels x 4 row lanes (one wave reads 64 consecutive channels = 256 B per row), grid
+// (ceil(C/64), S, 2): parallel over channels AND partial rows, so neither a large C (layer4) nor a
+// large nblk (stem) leaves the reduction on a handful of CUs.
+constexpr int kRowsPerSplit = 64;
+
+__global__ __launch_bounds__(256) void bn_partial_reduce_kernel(const float* __restrict__ part, int nblk, int C,
+                                                                float* __restrict__ out, int S) {
+  __shared__ float sh[256];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane = threadIdx.x >> 6;
+  const int s = blockIdx.y, which = blockIdx.z;
+  const float* src = part + (int64_t)which * nblk * C;
+  const int b0 = s * kRowsPerSplit;
+  int b1 = b0 + kRowsPerSplit;
+  if (b1 > nblk) b1 = nblk;
+  float acc = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (int b = b0 + lane; b < b1; b += 4) acc += src[(int64_t)b * C + c];
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  if (lane == 0 && c < C) {
+    const int t = threadIdx.x;
+    out[((int64_t)which * S + s) * C + c] = sh[t] + sh[t + 64] + sh[t + 128] + sh[t + 192];
+  }
+}
+
+__global__ void bn_fwd_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq, int nblk,
+                                       const uint16_t* __restrict__ x_row0, int C, int64_t M,
+                                       const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                                       float momentum, float* __restrict__ running_mean,
+                                       float* __restrict__ running_var, float* __restrict__ save_mean,
+                                       float* __restrict__ save_invstd, float* __restrict__ scale,
+                                       float* __restrict__ bias) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double S = 0.0, Q = 0.0;  // <= 32 level-2 partials per channel, summed in fp64
+  for (int b = 0; b < nblk; ++b) {
+    S += psum[(int64_t)b * C + c];
+    Q += psq[(int64_t)b * C + c];
+  }
+  const double m = S / (double)M;
+  double var = Q / (double)M - m * m;
+  if (var < 0.0) var = 0.0;
+  const float mean = bf2f(x_row0[c]) + (float)m;
+  const float invstd = rsqrtf((float)var + eps);
+  const float g = gamma[c];
+  save_mean[c] = mean;
+  save_invstd[c] = invstd;
+  scale[c] = g * invstd;
+  bias[c] = beta[c] - mean * g * invstd;
+  if (running_mean != nullptr) {
+    const float unbiased = M > 1 ? (float)(var * (double)M / (double)(M - 1)) : (float)var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+  }
+}
+
+// ------------------------------------------------------------------------------- forward apply
+__global__ __launch_bounds__(kBlock) void bn_apply_kernel(const bf16x8* __restrict__ x, const bf16x8* __restrict__ res,
+                                                          bf16x8* __restrict__ y, const float* __restrict__ scale,
+                                                          const float* __restrict__ bias, int64_t n_vec, int G,
+                                                          int relu) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // multiple of G (G | 256 or G % 256 == 0 handled by host)
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_vec) return;
+  const int cg = (int)(i % G);
+  float a[8], b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    a[k] = scale[cg * 8 + k];
+    b[k] = bias[cg * 8 + k];
+  }
+  for (; i < n_vec; i += stride) {
+    float v[8];
+    load8(x + i, v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], a[k], b[k]);
+    if (res != nullptr) {
+      float r[8];
+      load8(res + i, r);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += r[k];
+    }
+    if (relu) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
+    }
+    store8(y + i, v);
+  }
+}
+
+// ------------------------------------------------------------------------------- backward reduce
+__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const bf16x8* __restrict__ x, const bf16x8* __restrict__ y,
+                                                               const bf16x8* __restrict__ dy, int64_t M, int G, int Gb,
+                                                               int64_t rows_per_block, const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd, int relu,
+                                                               float* __restrict__ pdz, float* __restrict__ pdzx) {
+  __shared__ float s_a[kBlock * 8];
+  __shared__ float s_b[kBlock * 8];
+  const int tid = threadIdx.x;
+  const int cg_local = tid % Gb, rlane = tid / Gb, R = kBlock / Gb;
+  const int cg = blockIdx.y * Gb + cg_local;
+  const int C = G * 8;
+  float mu[8], is[8], sa[8], sb[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mu[k] = mean[cg * 8 + k];
+    is[k] = invstd[cg * 8 + k];
+    sa[k] = sb[k] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  int64_t r1 = r0 + rows_per_block;
+  if (r1 > M) r1 = M;
+#pragma unroll 4
+  for (int64_t r = r0 + rlane; r < r1; r += R) {
+    const int64_t off = r * G + cg;
+    float xv[8], g[8];
+    load8(x + off, xv);
+    load8(dy + off, g);
+    if (relu) {
+      float yv[8];
+      load8(y + off, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sa[k] += g[k];
+      sb[k] = fmaf(g[k], (xv[k] - mu[k]) * is[k], sb[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s_a[tid * 8 + k] = sa[k];
+    s_b[tid * 8 + k] = sb[k];
+  }
+  __syncthreads();
+  if (rlane == 0) {
+    for (int j = 1; j < R; ++j) {
+      const int o = (j * Gb + cg_local) * 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        sa[k] += s_a[o + k];
+        sb[k] += s_b[o + k];
+      }
+    }
+    float* pa = pdz + (int64_t)blockIdx.x * C + cg * 8;
+    float* pb = pdzx + (int64_t)blockIdx.x * C + cg * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      pa[k] = sa[k];
+      pb[k] = sb[k];
+    }
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ pdz, const float* __restrict__ pdzx, int nblk, int C,
+                                       int64_t M, const float* __restrict__ gamma, const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, float* __restrict__ dgamma,
+                                       float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double A = 0.0, B = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    A += pdz[(int64_t)b * C + c];
+    B += pdzx[(int64_t)b * C + c];
+  }
+  const float db = (float)A, dg = (float)B;
+  dbeta[c] = db;
+  dgamma[c] = dg;
+  const float is = invstd[c], k1 = gamma[c] * is;
+  const float k2 = db / (float)M, k3 = dg / (float)M;
+  // dx = k1 * (dz - k2 - xhat*k3),  xhat = (x - mean) * is   =>  dx = A*dz + B*x + D
+  coef[c] = k1;                                  // A
+  coef[C + c] = -k1 * k3 * is;                   // B
+  coef[2 * C + c] = -k1 * k2 + k1 * k3 * is * mean[c];  // D
+}
+
+__global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restrict__ x, const bf16x8* __restrict__ y,
+                                                           const bf16x8* __restrict__ dy, bf16x8* __restrict__ dx,
+                                                           bf16x8* __restrict__ dres, const float* __restrict__ coef,
+                                                           int64_t n_vec, int G, int relu) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_vec) return;
+  const int cg = (int)(i % G);
+  const int C = G * 8;
+  float A[8], B[8], D[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    A[k] = coef[cg * 8 + k];
+    B[k] = coef[C + cg * 8 + k];
+    D[k] = coef[2 * C + cg * 8 + k];
+  }
+  for (; i < n_vec; i += stride) {
+    float xv[8], g[8];
+    load8(x + i, xv);
+    load8(dy + i, g);
+    if (relu) {
+      float yv[8];
+      load8(y + i, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+    }
+    if (dres != nullptr) store8(dres + i, g);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = fmaf(A[k], g[k], fmaf(B[k], xv[k], D[k]));
+    store8(dx + i, o);
+  }
+}
+
+struct Plan {
+  int G, Gb, gy, nblk, S;
+  int64_t rows_per_block;
+};
+
+inline bool plan_for(int64_t M, int C, Plan* p) {
+  if (C <= 0 || (C & 7)) return false;
+  const int G = C / 8;
+  if (G & (G - 1)) return false;  // power of two channel groups
+  p->G = G;
+  p->Gb = G < kBlock ? G : kBlock;
+  p->gy = G / p->Gb;
+  const int R = kBlock / p->Gb;
+  const int64_t cap = (2048 + p->gy - 1) / p->gy;
+  int64_t want = (M + 16 * R - 1) / (16 * R);  // every thread streams >= 16 rows
+  if (want > cap) want = cap;
+  if (want < 1) want = 1;
+  int64_t rpb = (M + want - 1) / want;
+  rpb = (rpb + R - 1) / R * R;
+  p->rows_per_block = rpb;
+  p->nblk = (int)((M + rpb - 1) / rpb);
+  p->S = (p->nblk + kRowsPerSplit - 1) / kRowsPerSplit;
+  return true;
+}
+
+// grid-stride must keep each thread on one channel group: grid*256 % G == 0
+inline int apply_grid(int64_t n_vec, int G) {
+  int64_t g = (n_vec + kBlock - 1) / kBlock;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  const int64_t mult = G > kBlock ? G / kBlock : 1;
+  g = (g + mult - 1) / mult * mult;
+  return (int)g;
+}
+
+}  // namespace
+
+// fp32 workspace the host must pass as `partials`: level-1 [2][nblk][C] + level-2 [2][S][C].
+PLX_API int64_t plx_bn_workspace(int64_t M, int C) {
+  Plan p;
+  if (!plan_for(M, C, &p)) return -1;
+  return 2 * (int64_t)(p.nblk + p.S) * C;
+}
+
+PLX_API int plx_bn_forward(const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
+                           const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                           float* save_mean, float* save_invstd, float* scale_bias /* [2C] */,
+                           float* partials /* plx_bn_workspace floats */, int relu, hipStream_t stream) {
+  Plan p;
+  if (!plan_for(M, C, &p) || M < 1) return 1;
+  float* psum = partials;
+  float* psq = partials + (int64_t)p.nblk * C;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(p.nblk, p.gy), dim3(kBlock), 0, stream, (const bf16x8*)x, M, p.G, p.Gb,
+                     p.rows_per_block, psum, psq);
+  float* l2 = partials + 2 * (int64_t)p.nblk * C;
+  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, p.S, 2), dim3(256), 0, stream, partials, p.nblk, C,
+                     l2, p.S);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, l2, l2 + (int64_t)p.S * C, p.S,
+                     (const uint16_t*)x, C, M, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
+                     save_invstd, scale_bias, scale_bias + C);
+  const int64_t n_vec = M * p.G;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
+                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_bn_apply(const void* x, const void* res, void* y, int64_t M, int C, const float* scale_bias, int relu,
+                         hipStream_t stream) {
+  Plan p;
+  if (!plan_for(M, C, &p)) return 1;
+  const int64_t n_vec = M * p.G;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
+                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_bn_backward(const void* x, const void* y, const void* dy, void* dx, void* dres, int64_t M, int C,
+                            const float* gamma, const float* save_mean, const float* save_invstd, float* dgamma,
+                            float* dbeta, float* coef /* [3C] */, float* partials /* plx_bn_workspace floats */, int relu,
+                            hipStream_t stream) {
+  Plan p;
+  if (!plan_for(M, C, &p) || M < 1) return 1;
+  float* pa = partials;
+  float* pb = partials + (int64_t)p.nblk * C;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(p.nblk, p.gy), dim3(kBlock), 0, stream, (const bf16x8*)x,
+                     (const bf16x8*)y, (const bf16x8*)dy, M, p.G, p.Gb, p.rows_per_block, save_mean, save_invstd,
+                     relu, pa, pb);
+  float* l2 = partials + 2 * (int64_t)p.nblk * C;
+  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, p.S, 2), dim3(256), 0, stream, partials, p.nblk, C,
+                     l2, p.S);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, l2, l2 + (int64_t)p.S * C, p.S, C, M,
+                     gamma, save_mean, save_invstd, dgamma, dbeta, coef);
+  const int64_t n_vec = M * p.G;
+  hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
+                     (const bf16x8*)y, (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, p.G, relu);
+  return (int)hipGetLastError();
+}

@@ -27,6 +27,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 LIBRARIES: Dict[str, dict] = {
     "plx_train": {"sources": ["train_kernels.hip"], "kind": "hip", "link": []},
     "plx_polytune": {"sources": ["polytune_kernels.hip"], "kind": "hip", "link": []},
+    "plx_bn": {"sources": ["bn_kernels.hip"], "kind": "hip", "link": []},
 }
 
 _lock = threading.Lock()
@@ -129,6 +130,12 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_record_metric": [_P, _I, _P, _P, _I, _P],
         "plx_commit_metric": [_P, _P, _I, _I, _P, _I, _P],
     },
+    "plx_bn": {
+        "plx_bn_workspace": [_L, _I],
+        "plx_bn_forward": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P],
+        "plx_bn_apply": [_P, _P, _P, _L, _I, _P, _I, _P],
+        "plx_bn_backward": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
+    },
     "plx_polytune": {
         "plx_topk_brackets": [_P, _P, _I, _I, _I, _I, _P, _P],
         "plx_early_stop_any": [_P, _I, _I, _P, _P, _P, _I, _P, _P],
@@ -136,11 +143,14 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
+RESTYPES: Dict[str, object] = {"plx_bn_workspace": _L}
+
+
 def _declare(name: str, handle: ctypes.CDLL) -> None:
     for fn, argtypes in SIGNATURES.get(name, {}).items():
         f = getattr(handle, fn)
         f.argtypes = argtypes
-        f.restype = _I
+        f.restype = RESTYPES.get(fn, _I)
 
 
 def check(rc: int, what: str) -> None:

@@ -1,12 +1,104 @@
-"""Dispatch for the fused NHWC BatchNorm(+add)(+ReLU) HIP kernels (filled in by csrc/bn_kernels.hip)."""
+"""Autograd wrapper for the fused NHWC bf16 BatchNorm(+add)(+ReLU) HIP kernels (csrc/bn_kernels.hip).
+
+Forward (training): stats → finalize (mean/invstd/scale/bias + running-stat update) → apply.
+Backward: reduce (Σdz, Σdz·x̂) → finalize (dγ, dβ, dx coefficients) → dx (+ d_residual) in one pass.
+The ReLU mask is taken from the saved output ``y`` — it is the next convolution's input and is kept by
+autograd anyway, so the fusion saves no extra activation memory.
+"""
 from __future__ import annotations
+
+from typing import Optional
 
 import torch
 
+from polyaxon_amd.ops import _native
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
+
 
 def supported(x: torch.Tensor) -> bool:
-    return False
+    if not x.is_cuda or x.dtype != torch.bfloat16 or x.dim() != 4:
+        return False
+    c = x.shape[1]
+    g = c // 8
+    return c % 8 == 0 and g > 0 and (g & (g - 1)) == 0 and x.numel() > 0
 
 
-def bn_act(*args, **kwargs):  # pragma: no cover - replaced once the kernels land
-    raise NotImplementedError
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
+        lib = _native.lib("plx_bn")
+        x = _cl(x)
+        n, c, h, w = x.shape
+        m = n * h * w
+        ws = lib.plx_bn_workspace(m, c)
+        if ws < 0:
+            raise RuntimeError("unsupported channel count for fused BN")
+        f32 = dict(dtype=torch.float32, device=x.device)
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        stats = torch.empty(4 * c, **f32)  # mean | invstd | scale | bias
+        partials = torch.empty(ws, **f32)
+        res = _cl(residual) if residual is not None else None
+        rc = lib.plx_bn_forward(
+            x.data_ptr(), res.data_ptr() if res is not None else None, y.data_ptr(), m, c,
+            weight.data_ptr(), bias.data_ptr(), float(eps), float(momentum),
+            running_mean.data_ptr() if running_mean is not None else None,
+            running_var.data_ptr() if running_var is not None else None,
+            stats.data_ptr(), stats[c:].data_ptr(), stats[2 * c:].data_ptr(), partials.data_ptr(), int(relu),
+            _stream())
+        _native.check(rc, "plx_bn_forward")
+        ctx.save_for_backward(x, y, weight, stats)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.ws = ws
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _native.lib("plx_bn")
+        x, y, weight, stats = ctx.saved_tensors
+        n, c, h, w = x.shape
+        m = n * h * w
+        dy = _cl(dy)
+        if dy.dtype != torch.bfloat16:
+            dy = dy.to(torch.bfloat16)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        dgb = torch.empty(2 * c, **f32)
+        coef = torch.empty(3 * c, **f32)
+        partials = torch.empty(ctx.ws, **f32)
+        rc = lib.plx_bn_backward(
+            x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else None,
+            m, c, weight.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(), dgb.data_ptr(), dgb[c:].data_ptr(),
+            coef.data_ptr(), partials.data_ptr(), int(ctx.relu), _stream())
+        _native.check(rc, "plx_bn_backward")
+        return dx, dgb[:c], dgb[c:], None, None, dres, None, None, None
+
+
+def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
+           running_var: Optional[torch.Tensor], training: bool, momentum: float, eps: float,
+           residual: Optional[torch.Tensor], act: bool) -> torch.Tensor:
+    if residual is not None and residual.dtype != x.dtype:
+        residual = residual.to(x.dtype)
+    if training:
+        return _BNAct.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, act)
+    # inference: fold running stats into scale/bias, one apply pass
+    lib = _native.lib("plx_bn")
+    x = _cl(x)
+    n, c, h, w = x.shape
+    inv = torch.rsqrt(running_var.float() + eps)
+    scale = weight.float() * inv
+    sb = torch.cat([scale, bias.float() - running_mean.float() * scale]).contiguous()
+    y = torch.empty_like(x, memory_format=torch.channels_last)
+    res = _cl(residual) if residual is not None else None
+    rc = lib.plx_bn_apply(x.data_ptr(), res.data_ptr() if res is not None else None, y.data_ptr(), n * h * w, c,
+                          sb.data_ptr(), int(act), _stream())
+    _native.check(rc, "plx_bn_apply")
+    return y

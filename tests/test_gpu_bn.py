@@ -1,0 +1,89 @@
+"""Fused NHWC bf16 BatchNorm(+add)(+ReLU) HIP kernels vs an fp32 PyTorch reference of the same op."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x, w, b, rm, rv, res, relu, momentum=0.1, eps=1e-5):
+    y = F.batch_norm(x.float(), rm, rv, w, b, True, momentum, eps)
+    if res is not None:
+        y = y + res.float()
+    return F.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 14, 14), (2, 256, 7, 9), (3, 2048, 3, 3), (2, 4096, 2, 2),
+                                   (2, 128, 1, 1), (8, 64, 56, 56)])
+@pytest.mark.parametrize("relu,residual", [(True, False), (True, True), (False, False)])
+def test_bn_act_forward_backward(cuda, shape, relu, residual):
+    from polyaxon_amd.ops.bn_fused import bn_act, supported
+
+    torch.manual_seed(0)
+    n, c, h, w = shape
+    x = (torch.randn(shape, device=cuda) * 2 + 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert supported(x)
+    res = (torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+           if residual else None)
+    wgt = (torch.rand(c, device=cuda) + 0.5).requires_grad_()
+    bias = (torch.randn(c, device=cuda) * 0.1).requires_grad_()
+    rm, rv = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
+    rm_ref, rv_ref = rm.clone(), rv.clone()
+
+    xa = x.clone().requires_grad_()
+    ra = res.clone().requires_grad_() if residual else None
+    y = bn_act(xa, wgt, bias, rm, rv, True, 0.1, 1e-5, ra, relu)
+    xr = x.float().clone().requires_grad_()
+    rr = res.float().clone().requires_grad_() if residual else None
+    wr = wgt.detach().clone().requires_grad_()
+    br = bias.detach().clone().requires_grad_()
+    yr = _ref(xr, wr, br, rm_ref, rv_ref, rr, relu)
+
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(rm, rm_ref, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(rv, rv_ref, rtol=1e-3, atol=1e-3)
+
+    g = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y.backward(g)
+    yr.backward(g.float())
+    scale = max(1.0, float(xr.grad.abs().max()))
+    torch.testing.assert_close(xa.grad.float(), xr.grad, rtol=3e-2, atol=3e-2 * scale)
+    m = n * h * w
+    torch.testing.assert_close(wgt.grad, wr.grad, rtol=2e-2, atol=2e-2 * m ** 0.5)
+    torch.testing.assert_close(bias.grad, br.grad, rtol=2e-2, atol=2e-2 * m ** 0.5)
+    if residual:
+        torch.testing.assert_close(ra.grad.float(), rr.grad, rtol=2e-2, atol=2e-2)
+
+
+def test_bn_act_eval_matches_reference(cuda):
+    from polyaxon_amd.ops.bn_fused import bn_act
+
+    x = torch.randn(2, 64, 5, 5, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w, b = torch.rand(64, device=cuda) + 0.5, torch.randn(64, device=cuda)
+    rm, rv = torch.randn(64, device=cuda), torch.rand(64, device=cuda) + 0.5
+    y = bn_act(x, w, b, rm, rv, False, 0.1, 1e-5, None, True)
+    yr = F.relu(F.batch_norm(x.float(), rm, rv, w, b, False, 0.1, 1e-5))
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+
+
+def test_resnet_fused_matches_unfused_loss(cuda):
+    """Fused bf16 path vs unfused bf16 path, both judged against an fp32 run of the same network."""
+    from polyaxon_amd.models.resnet import resnet18ish
+
+    torch.manual_seed(0)
+    x32 = torch.randn(8, 3, 32, 32, device=cuda).contiguous(memory_format=torch.channels_last)
+    x = x32.to(torch.bfloat16)
+    y = torch.randint(0, 10, (8,), device=cuda)
+    res = {}
+    for name, fused, amp in (("fused", True, True), ("unfused", False, True), ("fp32", False, False)):
+        torch.manual_seed(1)
+        m = resnet18ish(fused=fused).to(cuda).to(memory_format=torch.channels_last)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            out = m(x if amp else x32)
+        loss = F.cross_entropy(out.float(), y)
+        loss.backward()
+        res[name] = (float(loss.detach()), m.stem.weight.grad.flatten().float().clone())
+    assert abs(res["fused"][0] - res["fp32"][0]) < 3e-2
+    cos = {k: float(F.cosine_similarity(res[k][1], res["fp32"][1], dim=0)) for k in ("fused", "unfused")}
+    assert cos["fused"] > 0.9, cos
+    assert cos["fused"] >= cos["unfused"] - 0.01, cos
