@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 kernel trace over the steady-state training window.
+
+The window is the span of the last ``--steps`` optimizer launches (``sgd_flat_kernel`` / ``adamw_flat``
+mark one training step each), so MIOpen's first-use Find / compile kernels and the warm-up are excluded.
+Prints per-step time by kernel class and the top kernels, optionally as markdown for profiles/.
+"""
+import argparse
+import collections
+import csv
+import sys
+
+CLASSES = [
+    ("conv (MIOpen igemm/CK/naive)", ("igemm", "conv", "ck::tensor_operation", "naive_conv", "gtcx")),
+    ("fused BN+add+ReLU (plx)", ("bn_stats", "bn_apply", "bn_bwd", "bn_fwd", "bn_partial")),
+    ("BN (MIOpen)", ("MIOpenBatchNorm",)),
+    ("optimizer / trial kernels (plx)", ("sgd_flat", "adamw_flat", "record_metric", "commit_metric", "init_flat",
+                                         "zero_kernel")),
+    ("GEMM (hipBLASLt/rocBLAS)", ("Cijk", "gemm", "Gemm")),
+    ("pool", ("pool",)),
+    ("elementwise/other torch", ("at::native",)),
+]
+
+
+def classify(name: str) -> str:
+    for cls, keys in CLASSES:
+        if any(k in name for k in keys):
+            return cls
+    return "other"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--marker", default="sgd_flat_kernel")
+    ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--markdown", action="store_true")
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
+    if len(marks) < 2:
+        sys.exit("not enough step markers")
+    marks = marks[-(a.steps + 1):]
+    lo, hi = marks[0] + 1, marks[-1] + 1
+    n_steps = len(marks) - 1
+    win = rows[lo:hi]
+    t0, t1 = int(win[0]["Start_Timestamp"]), int(win[-1]["End_Timestamp"])
+    busy = collections.Counter()
+    calls = collections.Counter()
+    per_class = collections.Counter()
+    for r in win:
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        busy[r["Kernel_Name"]] += d
+        calls[r["Kernel_Name"]] += 1
+        per_class[classify(r["Kernel_Name"])] += d
+    total = sum(busy.values())
+    wall = (t1 - t0) / n_steps / 1e6
+    out = []
+    out.append(f"steady-state window: {n_steps} steps, wall {wall:.3f} ms/step, kernel-busy {total / n_steps / 1e6:.3f} "
+               f"ms/step, {len(win) / n_steps:.0f} launches/step")
+    out.append("")
+    out.append("| class | ms/step | share |")
+    out.append("|---|---|---|")
+    for cls, d in per_class.most_common():
+        out.append(f"| {cls} | {d / n_steps / 1e6:.3f} | {100 * d / total:.1f}% |")
+    out.append("")
+    out.append("| kernel | calls/step | us/call | ms/step | share |")
+    out.append("|---|---|---|---|---|")
+    for name, d in busy.most_common(a.top):
+        out.append(f"| `{name[:90]}` | {calls[name] / n_steps:.1f} | {d / calls[name] / 1e3:.1f} | "
+                   f"{d / n_steps / 1e6:.3f} | {100 * d / total:.1f}% |")
+    print("\n".join(out))
+
+
+if __name__ == "__main__":
+    main()
