@@ -63,7 +63,7 @@ def main() -> int:
     ap.add_argument("--max-iter", type=int, default=9)
     ap.add_argument("--eta", type=int, default=3)
     ap.add_argument("--target", type=float, default=2.0, help="loss target for wall-clock-to-target")
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph (slower for ResNet-50 on ROCm 7, see profiles/README.md)")
     ap.add_argument("--unfused", action="store_true", help="PyTorch BN/ReLU instead of the HIP kernels")
     ap.add_argument("--tune", action="store_true", help="exhaustive MIOpen find (cudnn.benchmark)")
     ap.add_argument("--verbose", action="store_true", help="print every trial's record to stderr")
@@ -89,7 +89,7 @@ def main() -> int:
     x = x.contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (args.batch,), generator=gen)
     model = resnet50(fused=not args.unfused)
-    ex = ResidentTrialExecutor(model, (x, y), dev, use_graph=not args.no_graph)
+    ex = ResidentTrialExecutor(model, (x, y), dev, use_graph=args.graph)
 
     log("model built; capturing training step")
     t_cap = time.perf_counter()

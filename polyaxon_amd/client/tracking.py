@@ -1,0 +1,335 @@
+"""In-trial tracking client + helper getters (reference external polyaxon-client/tracking and
+polyaxon-helper; contract in docs/templates/polyaxon_tracking/experiments.md and
+docs/templates/polyaxon_tracking/polyaxon_helper.md:47-141).
+
+``Experiment()`` inside a polyflow trial picks up its identity from the env contract (polyflow/env.py) and
+writes to the node's tracking store directly (``POLYAXON_STORE_PATH``, SQLite/WAL — no HTTP hop, no
+20 req/s throttle as in the reference's api/experiments/views.py:389) or, if only
+``POLYAXON_API_HTTP_HOST`` is set, through the REST API.  Outside a cluster it can also create a
+local experiment in a store of your choice (``Experiment(project=..., store_path=...)``).
+
+Metric values may be Python numbers or (GPU) tensors: tensors are handed to :class:`MetricStream`, which
+copies them device→pinned host on a low-priority side stream, records an event, and lets a background
+thread write the batch to the store once the event completes — the training stream never synchronises.
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+import time
+import urllib.request
+from typing import Any, Dict, List, Optional
+
+
+# ------------------------------------------------------------------ helper getters (polyaxon-helper API)
+def _env_json(name: str, default=None):
+    v = os.environ.get(name)
+    if v is None:
+        return default
+    try:
+        return json.loads(v)
+    except ValueError:
+        return default
+
+
+def get_cluster_def() -> Optional[Dict[str, List[str]]]:
+    return _env_json("POLYAXON_CLUSTER")
+
+
+def get_declarations() -> Optional[Dict[str, Any]]:
+    return _env_json("POLYAXON_DECLARATIONS")
+
+
+def get_experiment_info() -> Optional[Dict[str, Any]]:
+    return _env_json("POLYAXON_EXPERIMENT_INFO")
+
+
+def get_job_info() -> Optional[Dict[str, Any]]:
+    return _env_json("POLYAXON_JOB_INFO")
+
+
+def get_task_info() -> Optional[Dict[str, Any]]:
+    return _env_json("POLYAXON_TASK_INFO")
+
+
+def get_task_type() -> Optional[str]:
+    info = get_task_info()
+    return info.get("type") if info else None
+
+
+def get_task_index() -> Optional[int]:
+    info = get_task_info()
+    return info.get("index") if info else None
+
+
+def get_outputs_path() -> Optional[str]:
+    return os.environ.get("POLYAXON_RUN_OUTPUTS_PATH")
+
+
+def get_log_level() -> Optional[str]:
+    return os.environ.get("POLYAXON_LOG_LEVEL")
+
+
+def get_data_paths() -> Optional[Dict[str, str]]:
+    return _env_json("POLYAXON_RUN_DATA_PATHS")
+
+
+def get_outputs_refs_paths() -> Optional[Dict[str, List[str]]]:
+    return _env_json("POLYAXON_REFS_OUTPUTS_PATHS")
+
+
+def get_tf_config(envvar: str = "TF_CONFIG") -> Optional[Dict[str, Any]]:
+    return _env_json(envvar)
+
+
+def is_in_cluster() -> bool:
+    return os.environ.get("POLYAXON_IN_CLUSTER", "").lower() in ("1", "true")
+
+
+# ------------------------------------------------------------------ backends
+class _StoreBackend:
+    def __init__(self, path: str):
+        from polyaxon_amd.store import Store
+
+        self.store = Store(path)
+
+    def log_metrics(self, xid: int, rows):
+        self.store.add_metrics_batch([(xid, vals, step, ts) for vals, step, ts in rows])
+
+    def update(self, xid: int, **values):
+        rec = self.store.get_experiment(xid)
+        if "declarations" in values:
+            values["declarations"] = dict(rec["declarations"] or {}, **values["declarations"])
+        if "tags" in values:
+            values["tags"] = sorted(set(rec["tags"] or []) | set(values["tags"]))
+        self.store.update_experiment(xid, **values)
+
+    def status(self, xid: int, status: str, message: Optional[str] = None):
+        self.store.set_experiment_status(xid, status, message)
+
+
+class _HttpBackend:
+    def __init__(self, host: str, token: Optional[str], project: str, user: str):
+        self.host = host.rstrip("/")
+        self.token = token
+        self.base = f"{self.host}/api/v1/{user}/{project}"
+
+    def _req(self, method: str, path: str, payload=None):
+        data = json.dumps(payload).encode() if payload is not None else None
+        req = urllib.request.Request(self.base + path, data=data, method=method,
+                                     headers={"Content-Type": "application/json",
+                                              **({"Authorization": f"token {self.token}"} if self.token else {})})
+        with urllib.request.urlopen(req, timeout=10) as r:
+            return json.loads(r.read() or b"null")
+
+    def log_metrics(self, xid: int, rows):
+        self._req("POST", f"/experiments/{xid}/metrics",
+                  [{"values": vals, "step": step, "created_at": ts} for vals, step, ts in rows])
+
+    def update(self, xid: int, **values):
+        self._req("PATCH", f"/experiments/{xid}", values)
+
+    def status(self, xid: int, status: str, message: Optional[str] = None):
+        self._req("POST", f"/experiments/{xid}/statuses", {"status": status, "message": message})
+
+
+class MetricStream:
+    """Asynchronous device→store metric path: tensors are copied to pinned host memory on
+    a side stream; a flusher thread writes rows whose copy event has completed."""
+
+    def __init__(self, sink, xid: int, flush_every_s: float = 0.5):
+        self.sink = sink
+        self.xid = xid
+        self.flush_every_s = flush_every_s
+        self._pending: List = []  # (event|None, {name: value|pinned tensor}, step, ts)
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._side = None
+        self._thread = threading.Thread(target=self._run, name="plx-metrics", daemon=True)
+        self._thread.start()
+
+    def _stream_for(self, t):
+        import torch
+
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=t.device, priority=0)
+        return self._side
+
+    def put(self, values: Dict[str, Any], step: Optional[int]) -> None:
+        ts = time.time()
+        host: Dict[str, Any] = {}
+        event = None
+        tensors = {k: v for k, v in values.items() if hasattr(v, "is_cuda") and v.is_cuda}
+        if tensors:
+            import torch
+
+            first = next(iter(tensors.values()))
+            side = self._stream_for(first)
+            side.wait_stream(torch.cuda.current_stream(first.device))
+            with torch.cuda.stream(side):
+                for k, v in tensors.items():
+                    buf = torch.empty(v.shape, dtype=torch.float32, pin_memory=True)
+                    buf.copy_(v.detach().float(), non_blocking=True)
+                    v.record_stream(side)
+                    host[k] = buf
+                event = torch.cuda.Event()
+                event.record(side)
+        for k, v in values.items():
+            if k not in host:
+                host[k] = float(v.item()) if hasattr(v, "item") else float(v)
+        with self._lock:
+            self._pending.append((event, host, step, ts))
+
+    def _ready_rows(self, force: bool):
+        rows, keep = [], []
+        with self._lock:
+            for ev, host, step, ts in self._pending:
+                if ev is not None and not force and not ev.query():
+                    keep.append((ev, host, step, ts))
+                    continue
+                if ev is not None:
+                    ev.synchronize()
+                vals = {k: (float(v.reshape(-1)[0]) if hasattr(v, "reshape") else v) for k, v in host.items()}
+                rows.append((vals, step, ts))
+            self._pending = keep
+        return rows
+
+    def flush(self, force: bool = True) -> None:
+        rows = self._ready_rows(force)
+        if rows:
+            self.sink.log_metrics(self.xid, rows)
+
+    def _run(self) -> None:
+        while not self._stop.wait(self.flush_every_s):
+            try:
+                self.flush(force=False)
+            except Exception:
+                pass
+
+    def close(self) -> None:
+        self._stop.set()
+        self._thread.join(timeout=5)
+        self.flush(force=True)
+
+
+class Experiment:
+    """Tracking handle (reference ``polyaxon_client.tracking.Experiment``)."""
+
+    def __init__(self, experiment_id: Optional[int] = None, project: Optional[str] = None,
+                 store_path: Optional[str] = None, api_host: Optional[str] = None, token: Optional[str] = None,
+                 user: str = "root", track: bool = True, async_metrics: bool = True):
+        self.experiment_id = experiment_id or (int(os.environ["POLYAXON_EXPERIMENT_ID"])
+                                               if os.environ.get("POLYAXON_EXPERIMENT_ID") else None)
+        info = get_experiment_info() or {}
+        self.project = project or (info.get("project_name", "").split(".")[-1] or None)
+        self.user = user
+        store_path = store_path or os.environ.get("POLYAXON_STORE_PATH")
+        api_host = api_host or os.environ.get("POLYAXON_API_HTTP_HOST")
+        self.backend = None
+        if track and store_path:
+            self.backend = _StoreBackend(store_path)
+            if self.experiment_id is None:  # local, outside polyflow
+                st = self.backend.store
+                proj = st.get_or_create_project(self.project or "default", user)
+                self.experiment_id = st.create_experiment(proj["id"], {}, user=user, is_managed=False)
+                st.set_experiment_status(self.experiment_id, "scheduled")
+                st.set_experiment_status(self.experiment_id, "running")
+        elif track and api_host and self.experiment_id is not None:
+            self.backend = _HttpBackend(api_host, token or os.environ.get("POLYAXON_SECRET_USER_TOKEN"),
+                                        self.project or "default", user)
+        self._stream = MetricStream(self.backend, self.experiment_id) if (self.backend and async_metrics) else None
+        self._done = False
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def outputs_path(self) -> Optional[str]:
+        return get_outputs_path()
+
+    def get_outputs_path(self) -> Optional[str]:
+        return self.outputs_path
+
+    def get_cluster_def(self):
+        return get_cluster_def()
+
+    def get_declarations(self):
+        return get_declarations()
+
+    def get_data_paths(self):
+        return get_data_paths()
+
+    def get_outputs_refs_paths(self):
+        return get_outputs_refs_paths()
+
+    # ------------------------------------------------------------------ logging
+    def log_metrics(self, step: Optional[int] = None, **metrics) -> None:
+        if self.backend is None:
+            return
+        if self._stream is not None:
+            self._stream.put(metrics, step)
+        else:
+            vals = {k: float(v.item()) if hasattr(v, "item") else float(v) for k, v in metrics.items()}
+            self.backend.log_metrics(self.experiment_id, [(vals, step, time.time())])
+
+    def log_params(self, **params) -> None:
+        if self.backend is not None:
+            self.backend.update(self.experiment_id, declarations=params)
+
+    log_declarations = log_params
+
+    def log_tags(self, tags) -> None:
+        if self.backend is not None:
+            self.backend.update(self.experiment_id, tags=list(tags))
+
+    def set_description(self, description: str) -> None:
+        if self.backend is not None:
+            self.backend.update(self.experiment_id, description=description)
+
+    def set_name(self, name: str) -> None:
+        if self.backend is not None:
+            self.backend.update(self.experiment_id, name=name)
+
+    def log_status(self, status: str, message: Optional[str] = None) -> None:
+        if self.backend is not None:
+            self.backend.status(self.experiment_id, status, message)
+
+    def log_run_env(self, env: Dict[str, Any]) -> None:
+        if self.backend is not None:
+            self.backend.update(self.experiment_id, run_env=env)
+
+    def flush(self) -> None:
+        if self._stream is not None:
+            self._stream.flush(force=True)
+
+    def succeeded(self) -> None:
+        self._finish("succeeded")
+
+    def failed(self, message: Optional[str] = None) -> None:
+        self._finish("failed", message)
+
+    def _finish(self, status: str, message: Optional[str] = None) -> None:
+        self.close()
+        if self.backend is not None and isinstance(self.backend, _StoreBackend):
+            rec = self.backend.store.get_experiment(self.experiment_id)
+            if not rec.get("is_managed"):
+                self.log_status(status, message)
+
+    def close(self) -> None:
+        if self._stream is not None and not self._done:
+            self._stream.close()
+        self._done = True
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        if exc_type is None:
+            self.succeeded()
+        else:
+            self.failed(str(exc))
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass

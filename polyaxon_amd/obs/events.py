@@ -1,0 +1,234 @@
+"""Event bus = the reference's event_manager + auditor + activitylogs + notifier + tracker + stats.
+
+Reference: polyaxon/event_manager/ (typed event catalogue, 116 types, event.py:13-148), auditor/service.py
+(one ``record`` fanned out to notifier, tracker and activity logs), notifier/service.py, activitylogs/,
+tracker/publish_tracker.py (Segment analytics), stats/ (statsd/datadog counters), action_manager/ (email,
+Slack, Discord, Mattermost, HipChat, PagerDuty, generic webhooks).
+
+Here: event types are ``<subject>.<action>`` strings validated against :data:`EVENT_TYPES`;
+:class:`Auditor.record` synchronously writes the activity log row and the notification row (for
+notifying events) and hands webhook deliveries to a background thread so the scheduler loop never blocks
+on the network.  Subscribers (``subscribe(pattern, fn)``) get every matching event in-process (the
+websocket/SSE streams and tests use this).
+"""
+from __future__ import annotations
+
+import fnmatch
+import json
+import logging
+import queue
+import threading
+import time
+import urllib.request
+from collections import Counter
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+log = logging.getLogger("polyaxon_amd.events")
+
+SUBJECTS = {
+    "experiment": ["created", "updated", "deleted", "viewed", "stopped", "resumed", "restarted", "copied",
+                   "bookmarked", "unbookmarked", "new_status", "new_metric", "succeeded", "failed", "done",
+                   "resources_viewed", "logs_viewed", "outputs_downloaded", "statuses_viewed", "jobs_viewed",
+                   "metrics_viewed", "deleted_triggered", "stopped_triggered", "resumed_triggered",
+                   "restarted_triggered", "copied_triggered"],
+    "experiment_group": ["created", "updated", "deleted", "viewed", "stopped", "resumed", "bookmarked",
+                         "unbookmarked", "new_status", "experiments_viewed", "statuses_viewed", "metrics_viewed",
+                         "iteration", "random", "grid", "hyperband", "bo", "asha", "done", "succeeded", "failed",
+                         "deleted_triggered", "stopped_triggered"],
+    "experiment_job": ["viewed", "resources_viewed", "logs_viewed", "statuses_viewed", "new_status", "failed",
+                       "succeeded", "done"],
+    "job": ["created", "updated", "started", "started_triggered", "deleted", "deleted_triggered", "viewed",
+            "bookmarked", "unbookmarked", "stopped", "stopped_triggered", "restarted", "restarted_triggered",
+            "statuses_viewed", "logs_viewed", "new_status", "failed", "succeeded", "done", "outputs_downloaded"],
+    "build_job": ["created", "updated", "started", "started_triggered", "deleted", "deleted_triggered", "viewed",
+                  "bookmarked", "unbookmarked", "stopped", "stopped_triggered", "statuses_viewed", "logs_viewed",
+                  "new_status", "failed", "succeeded", "done"],
+    "notebook": ["started", "started_triggered", "stopped", "stopped_triggered", "viewed", "new_status", "failed",
+                 "succeeded"],
+    "tensorboard": ["started", "started_triggered", "stopped", "stopped_triggered", "viewed", "new_status",
+                    "failed", "succeeded"],
+    "project": ["created", "updated", "deleted", "viewed", "bookmarked", "unbookmarked", "set_public",
+                "set_private", "experiments_viewed", "jobs_viewed", "builds_viewed", "experiment_groups_viewed",
+                "tensorboards_viewed", "deleted_triggered"],
+    "pipeline": ["created", "started", "succeeded", "failed", "stopped", "done"],
+    "operation": ["created", "started", "succeeded", "failed", "upstream_failed", "retrying", "skipped", "stopped"],
+    "repo": ["created", "new_commit", "downloaded"],
+    "cluster": ["created", "updated", "resources_updated", "node_created", "node_updated", "node_deleted",
+                "node_gpu", "node_gpu_unhealthy"],
+    "user": ["registered", "updated", "activated", "deleted", "viewed", "password_changed"],
+    "superuser": ["role_granted", "role_revoked"],
+    "permission": ["project_denied", "repo_denied", "experiment_group_denied", "experiment_denied",
+                   "tensorboard_denied", "notebook_denied", "build_job_denied", "experiment_job_denied",
+                   "cluster_denied", "user_role_denied"],
+    "search": ["created", "deleted"],
+    "chart_view": ["created", "deleted"],
+    "bookmark": ["created", "deleted"],
+    "webhook_action": ["executed"],
+}
+EVENT_TYPES = frozenset(f"{s}.{a}" for s, acts in SUBJECTS.items() for a in acts)
+# events that also create a user-visible notification (reference notifier/service.py event list)
+NOTIFY = frozenset(e for e in EVENT_TYPES if e.endswith((".succeeded", ".failed", ".done", ".stopped",
+                                                         ".upstream_failed")))
+
+
+@dataclass
+class Event:
+    event_type: str
+    object_kind: Optional[str] = None
+    object_id: Optional[int] = None
+    actor: Optional[str] = None
+    context: Dict[str, Any] = field(default_factory=dict)
+    created_at: float = field(default_factory=time.time)
+
+    @property
+    def subject(self) -> str:
+        return self.event_type.split(".", 1)[0]
+
+    @property
+    def action(self) -> str:
+        return self.event_type.split(".", 1)[1]
+
+    def to_dict(self) -> Dict[str, Any]:
+        return {"event_type": self.event_type, "object_kind": self.object_kind, "object_id": self.object_id,
+                "actor": self.actor, "context": self.context, "created_at": self.created_at}
+
+    def readable(self) -> str:
+        who = f"{self.actor} " if self.actor else ""
+        obj = f"{self.object_kind} {self.object_id}" if self.object_kind else self.subject
+        return f"{who}{self.action.replace('_', ' ')}: {obj}"
+
+
+class Stats:
+    """Counters/timings (reference stats/: noop | statsd | datadog). Kept in-process; optional statsd UDP."""
+
+    def __init__(self, statsd_addr: Optional[Tuple[str, int]] = None, prefix: str = "polyaxon"):
+        self.counters: Counter = Counter()
+        self.timings: Dict[str, List[float]] = {}
+        self.prefix = prefix
+        self._addr = statsd_addr
+        self._sock = None
+        if statsd_addr:
+            import socket
+
+            self._sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+
+    def incr(self, key: str, value: int = 1) -> None:
+        self.counters[key] += value
+        self._send(f"{self.prefix}.{key}:{value}|c")
+
+    def timing(self, key: str, ms: float) -> None:
+        self.timings.setdefault(key, []).append(ms)
+        self._send(f"{self.prefix}.{key}:{ms:.3f}|ms")
+
+    def _send(self, payload: str) -> None:
+        if self._sock is not None:
+            try:
+                self._sock.sendto(payload.encode(), self._addr)
+            except OSError:
+                pass
+
+
+class WebhookAction:
+    """Generic webhook + chat integrations (Slack/Mattermost/Discord payload shapes; PagerDuty events v2)."""
+
+    KINDS = ("webhook", "slack", "mattermost", "discord", "hipchat", "pagerduty")
+
+    def __init__(self, url: str, kind: str = "webhook", method: str = "POST", events: Optional[List[str]] = None,
+                 timeout: float = 5.0):
+        if kind not in self.KINDS:
+            raise ValueError(f"unknown webhook kind {kind}")
+        if not url.startswith(("http://", "https://")):
+            raise ValueError(f"invalid webhook URL {url}")
+        if method.upper() not in ("GET", "POST"):
+            raise ValueError(f"unsupported webhook method {method}")
+        self.url, self.kind, self.method = url, kind, method.upper()
+        self.events = events or ["*"]
+        self.timeout = timeout
+
+    def matches(self, event_type: str) -> bool:
+        return any(fnmatch.fnmatch(event_type, p) for p in self.events)
+
+    def payload(self, ev: Event) -> Dict[str, Any]:
+        text = ev.readable()
+        if self.kind in ("slack", "mattermost"):
+            return {"text": text, "attachments": [{"fields": [{"title": k, "value": str(v), "short": True}
+                                                              for k, v in ev.context.items()]}]}
+        if self.kind == "discord":
+            return {"content": text}
+        if self.kind == "hipchat":
+            return {"message": text, "notify": True}
+        if self.kind == "pagerduty":
+            return {"event_action": "trigger", "payload": {"summary": text, "source": "polyaxon-mi355x",
+                                                           "severity": "error" if "failed" in ev.event_type
+                                                           else "info", "custom_details": ev.context}}
+        return {"subject": ev.event_type, "body": text, "datetime": ev.created_at, "context": ev.context}
+
+    def execute(self, ev: Event) -> bool:
+        data = json.dumps(self.payload(ev)).encode()
+        req = urllib.request.Request(self.url, data=data if self.method == "POST" else None, method=self.method,
+                                     headers={"Content-Type": "application/json"})
+        try:
+            with urllib.request.urlopen(req, timeout=self.timeout) as r:
+                return 200 <= r.status < 300
+        except Exception as e:  # delivery failures never break the platform (reference safe_request)
+            log.warning("webhook %s failed: %s", self.url, e)
+            return False
+
+
+class Auditor:
+    def __init__(self, store=None, stats: Optional[Stats] = None, strict: bool = True):
+        self.store = store
+        self.stats = stats or Stats()
+        self.strict = strict
+        self.actions: List[WebhookAction] = []
+        self._subs: List[Tuple[str, Callable[[Event], None]]] = []
+        self._q: "queue.Queue[Tuple[WebhookAction, Event]]" = queue.Queue()
+        self._worker: Optional[threading.Thread] = None
+        self.delivered: List[Tuple[str, bool]] = []
+
+    def subscribe(self, pattern: str, fn: Callable[[Event], None]) -> None:
+        self._subs.append((pattern, fn))
+
+    def add_action(self, action: WebhookAction) -> None:
+        self.actions.append(action)
+
+    def record(self, event_type: str, object_kind: Optional[str] = None, object_id: Optional[int] = None,
+               actor: Optional[str] = None, **context) -> Event:
+        if self.strict and event_type not in EVENT_TYPES:
+            raise ValueError(f"unknown event type {event_type!r}")
+        ev = Event(event_type, object_kind, object_id, actor, context)
+        self.stats.incr(event_type)
+        if self.store is not None:
+            self.store.add_activity(event_type, actor, object_kind, object_id, context)
+            if event_type in NOTIFY:
+                self.store.add_notification(event_type, object_kind, object_id, context, user=actor)
+        for pattern, fn in list(self._subs):
+            if fnmatch.fnmatch(event_type, pattern):
+                try:
+                    fn(ev)
+                except Exception:  # subscribers must not break the emitter
+                    log.exception("event subscriber failed")
+        for a in self.actions:
+            if a.matches(event_type):
+                self._ensure_worker()
+                self._q.put((a, ev))
+        return ev
+
+    def _ensure_worker(self) -> None:
+        if self._worker is None or not self._worker.is_alive():
+            self._worker = threading.Thread(target=self._deliver, name="plx-webhooks", daemon=True)
+            self._worker.start()
+
+    def _deliver(self) -> None:
+        while True:
+            a, ev = self._q.get()
+            ok = a.execute(ev)
+            self.delivered.append((a.url, ok))
+            self.stats.incr("webhook_action.executed")
+            self._q.task_done()
+
+    def flush(self, timeout: float = 10.0) -> None:
+        end = time.time() + timeout
+        while self._q.unfinished_tasks and time.time() < end:
+            time.sleep(0.01)

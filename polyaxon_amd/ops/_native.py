@@ -28,6 +28,8 @@ LIBRARIES: Dict[str, dict] = {
     "plx_train": {"sources": ["train_kernels.hip"], "kind": "hip", "link": []},
     "plx_polytune": {"sources": ["polytune_kernels.hip"], "kind": "hip", "link": []},
     "plx_bn": {"sources": ["bn_kernels.hip"], "kind": "hip", "link": []},
+    "plx_procmon": {"sources": ["procmon.cpp"], "kind": "cpp", "link": ["-lpthread"]},
+    "plx_gp": {"sources": ["gp_kernels.hip"], "kind": "hip", "link": []},
 }
 
 _lock = threading.Lock()
@@ -91,6 +93,18 @@ def build(name: str, force: bool = False, verbose: bool = False) -> Path:
     return out
 
 
+def _stale(name: str) -> bool:
+    spec = LIBRARIES[name]
+    stamp = lib_path(name).with_suffix(".so.sha")
+    if not stamp.exists():
+        return False  # shipped without a stamp: trust it
+    try:
+        digest = _digest([CSRC / s for s in spec["sources"]], _flags(spec["kind"]) + spec["link"])
+    except OSError:
+        return False
+    return stamp.read_text().strip() != digest
+
+
 def build_all(force: bool = False, verbose: bool = False) -> List[Path]:
     return [build(n, force=force, verbose=verbose) for n in LIBRARIES]
 
@@ -105,8 +119,9 @@ def lib(name: str) -> ctypes.CDLL:
         if name in _loaded:
             return _loaded[name]
         path = lib_path(name)
-        if not path.exists() or os.environ.get("PLX_NATIVE_REBUILD") == "1":
-            build(name)
+        # rebuild when the sources changed since the .so was built (digest stamp), or when forced
+        if not path.exists() or os.environ.get("PLX_NATIVE_REBUILD") == "1" or _stale(name):
+            build(name, force=os.environ.get("PLX_NATIVE_REBUILD") == "1")
         handle = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
         _declare(name, handle)
         _loaded[name] = handle
@@ -136,6 +151,21 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_bn_apply": [_P, _P, _P, _L, _I, _P, _I, _P],
         "plx_bn_backward": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     },
+    "plx_procmon": {
+        "plx_pm_create": [],
+        "plx_pm_destroy": [_P],
+        "plx_pm_spawn": [_P, _P, _P, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(_I)],
+        "plx_pm_wait": [_P, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)],
+        "plx_pm_wake": [_P],
+        "plx_pm_signal": [_P, _I, _I, _I],
+        "plx_pm_count": [_P],
+    },
+    "plx_gp": {
+        "plx_gp_kmat": [_P, _P, _I, _I, _I, _P, _I, _I, _F, _F, _F, _I, _F, _P],
+        "plx_gp_chol": [_P, _I, _I, _P, _P],
+        "plx_gp_predict_acq": [_P, _I, _P, _I, _I, _P, _I, _P, _I, _F, _F, _F, _F, _I, _F, _F, _F, _P, _P, _P, _P,
+                               _P, _P],
+    },
     "plx_polytune": {
         "plx_topk_brackets": [_P, _P, _I, _I, _I, _I, _P, _P],
         "plx_early_stop_any": [_P, _I, _I, _P, _P, _P, _I, _P, _P],
@@ -143,7 +173,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_bn_workspace": _L}
+RESTYPES: Dict[str, object] = {"plx_bn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
+                               "plx_pm_wake": None}
 
 
 def _declare(name: str, handle: ctypes.CDLL) -> None:

@@ -1,0 +1,802 @@
+"""polyflow: the event-driven node scheduler (replaces the reference's scheduler/ + spawners/ + Celery +
+monitors + crons for one 8×MI355X node).
+
+Reference call stacks collapsed here: run one experiment (API → signals → Celery
+build/start → spawner → K8s pods → status monitor → events worker → aggregation → stop), groups
+(§3.2-3.3, hpsearch tasks), distributed experiments (§3.6, per-framework spawners), generic jobs /
+builds / notebooks / tensorboards (scheduler/{job,dockerizer,notebook,tensorboard}_scheduler.py).
+
+Design (MI355X-first, single node):
+* one scheduler thread owns all mutable state (allocator, run table, group drivers) — no locks on the
+  hot path, no races on device accounting (reference: hpsearch/tasks/base.py:44-47 admits races);
+* the thread blocks in the native process monitor (csrc/procmon.cpp: epoll over pidfds + an eventfd),
+  so a replica exit, a submitted command and a timer deadline all wake it immediately: the gap between
+  a trial ending and the next one being spawned is the cost of one ``posix_spawn``, not a 1–30 s poll;
+* replicas are plain processes pinned with ``HIP_VISIBLE_DEVICES`` and the reference env contract
+  (polyflow/env.py); gangs (DP=2/4/8) are allocated all-or-nothing by the device allocator;
+* every status change goes through the lifecycle FSMs in the store; every lifecycle event goes to the
+  auditor (activity log, notifications, webhooks).
+"""
+from __future__ import annotations
+
+import hashlib
+import heapq
+import json
+import logging
+import os
+import signal
+import sys
+import threading
+import time
+import traceback
+import uuid
+from collections import deque
+from dataclasses import dataclass, field
+from typing import Any, Callable, Deque, Dict, List, Optional, Tuple
+
+from polyaxon_amd.fsm import ExperimentLifeCycle, JobLifeCycle
+from polyaxon_amd.obs.events import Auditor
+from polyaxon_amd.polyflow.devices import DeviceAllocator
+from polyaxon_amd.polyflow.env import cluster_def as make_cluster_def
+from polyaxon_amd.polyflow.env import free_port, trial_env
+from polyaxon_amd.polyflow.paths import Paths
+from polyaxon_amd.polyflow.process import ProcessMonitor
+from polyaxon_amd.spec import specification_for
+from polyaxon_amd.spec.specification import (BaseSpecification, ExperimentSpecification, GroupSpecification,
+                                             Kinds, PolyaxonfileError)
+from polyaxon_amd.store import Store
+
+log = logging.getLogger("polyaxon_amd.polyflow")
+
+BUILD_REUSE_S = 6 * 3600  # reference dockerizer_scheduler.py:48-50
+
+
+@dataclass
+class Replica:
+    role: str
+    index: int
+    job_id: int
+    gpus: float
+    devices: List[int] = field(default_factory=list)
+    pid: Optional[int] = None
+    exit_code: Optional[int] = None
+    done: bool = False
+
+
+@dataclass
+class Run:
+    kind: str  # "experiment" | "job"
+    id: int
+    spec: BaseSpecification
+    cwd: str
+    replicas: List[Replica] = field(default_factory=list)
+    stop_requested: bool = False
+    stop_reason: Optional[str] = None
+    final_status: Optional[str] = None
+    final_message: Optional[str] = None
+    created: float = field(default_factory=time.time)
+    started: Optional[float] = None
+    build_id: Optional[int] = None
+    port: Optional[int] = None
+    extra_env: Dict[str, str] = field(default_factory=dict)
+    on_done: List[Callable[[str], None]] = field(default_factory=list)
+
+    @property
+    def owner(self) -> str:
+        return f"{self.kind}:{self.id}"
+
+    @property
+    def active(self) -> bool:
+        return any(r.pid is not None and not r.done for r in self.replicas)
+
+
+def _replica_gpus(spec: BaseSpecification, role: str, index: int) -> float:
+    if role == "master":
+        res = spec.resources
+    elif role == "worker":
+        res = spec.get_worker_resources(index) or spec.resources
+    else:
+        res = spec.get_ps_resources(index)
+    if res is None or res.gpu is None:
+        return 0.0
+    return float(res.gpu.value)
+
+
+def _command(spec: BaseSpecification) -> str:
+    if spec.run is None:
+        raise PolyaxonfileError("nothing to run: the specification has no `run.cmd`")
+    return " && ".join(spec.run.commands)
+
+
+class Polyflow:
+    """Node scheduler. Public methods are thread-safe (they post commands to the scheduler thread)."""
+
+    def __init__(self, root: str, store: Optional[Store] = None, allocator: Optional[DeviceAllocator] = None,
+                 auditor: Optional[Auditor] = None, api_host: Optional[str] = None, stop_grace_s: float = 10.0,
+                 python: Optional[str] = None):
+        self.paths = Paths(root)
+        self.store_path = os.path.join(self.paths.root, "polyaxon.sqlite")
+        self.store = store or Store(self.store_path)
+        if store is not None and store.path != ":memory:":
+            self.store_path = store.path
+        self.alloc = allocator or DeviceAllocator()
+        self.auditor = auditor or Auditor(self.store)
+        self.api_host = api_host
+        self.stop_grace_s = stop_grace_s
+        self.python = python or sys.executable
+        self.pm = ProcessMonitor()
+        self.runs: Dict[str, Run] = {}
+        self.pending: Deque[str] = deque()
+        self.pid_index: Dict[int, Tuple[str, int]] = {}
+        self.groups: Dict[int, Any] = {}
+        self.pipelines: Dict[int, Any] = {}
+        self._cmds: Deque[Tuple[Callable, tuple, Optional["_Result"]]] = deque()
+        self._timers: List[Tuple[float, int, Callable]] = []
+        self._timer_seq = 0
+        self._thread: Optional[threading.Thread] = None
+        self._running = False
+        self._idle = threading.Event()
+        self.stats = {"spawned": 0, "exited": 0, "gaps_ms": []}
+        self._last_exit_t: Optional[float] = None
+
+    # ================================================================== lifecycle of the scheduler itself
+    def start(self) -> "Polyflow":
+        if self._thread is None:
+            self._running = True
+            self._thread = threading.Thread(target=self._loop, name="polyflow", daemon=True)
+            self._thread.start()
+            self.store.upsert_node("local", os.uname().nodename, float(os.cpu_count() or 1), 0.0, self.alloc.n_devices)
+        return self
+
+    def shutdown(self, stop_running: bool = True, timeout: float = 30.0) -> None:
+        if self._thread is None:
+            return
+        if stop_running:
+            self.call(self._stop_all)
+            end = time.time() + timeout
+            while time.time() < end and self.call(lambda: any(r.active for r in self.runs.values())):
+                time.sleep(0.05)
+        self._running = False
+        self.pm.wake()
+        self._thread.join(timeout=timeout)
+        self._thread = None
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.shutdown()
+
+    # ================================================================== command plumbing
+    def call(self, fn: Callable, *args, timeout: Optional[float] = 60.0):
+        """Run ``fn(*args)`` on the scheduler thread and return its result (or raise its exception)."""
+        if self._thread is None or threading.current_thread() is self._thread:
+            return fn(*args)
+        res = _Result()
+        self._cmds.append((fn, args, res))
+        self.pm.wake()
+        return res.get(timeout)
+
+    def post(self, fn: Callable, *args) -> None:
+        self._cmds.append((fn, args, None))
+        self.pm.wake()
+
+    def after(self, delay_s: float, fn: Callable) -> None:
+        """Timer on the scheduler thread."""
+        self._timer_seq += 1
+        heapq.heappush(self._timers, (time.time() + delay_s, self._timer_seq, fn))
+        self.pm.wake()
+
+    def _loop(self) -> None:
+        while self._running:
+            try:
+                self._drain_commands()
+                self._fire_timers()
+                self._schedule()
+                busy = any(r.active for r in self.runs.values()) or bool(self.pending) or bool(self._cmds)
+                if not busy:
+                    self._idle.set()
+                timeout = 1.0
+                if self._timers:
+                    timeout = max(0.0, min(timeout, self._timers[0][0] - time.time()))
+                if self._cmds:
+                    timeout = 0.0
+                got = self.pm.wait(timeout)
+                while got is not None:
+                    self._on_exit(*got)
+                    got = self.pm.wait(0)
+            except Exception:
+                log.exception("polyflow loop error")
+
+    def _drain_commands(self) -> None:
+        while self._cmds:
+            fn, args, res = self._cmds.popleft()
+            try:
+                out = fn(*args)
+                if res is not None:
+                    res.set(out)
+            except BaseException as e:  # noqa: BLE001 - forwarded to the caller
+                if res is not None:
+                    res.fail(e)
+                else:
+                    log.exception("polyflow command failed")
+
+    def _fire_timers(self) -> None:
+        now = time.time()
+        while self._timers and self._timers[0][0] <= now:
+            _, _, fn = heapq.heappop(self._timers)
+            try:
+                fn()
+            except Exception:
+                log.exception("polyflow timer failed")
+
+    # ================================================================== submission API
+    def submit(self, content, project: str = "default", user: str = "root", cwd: Optional[str] = None,
+               name: Optional[str] = None, description: Optional[str] = None) -> Dict[str, Any]:
+        """``polyaxon run -f polyaxonfile.yml`` equivalent. Returns {"kind", "id"}."""
+        spec = content if isinstance(content, BaseSpecification) else specification_for(content)
+        return self.call(self._submit, spec, project, user, cwd or os.getcwd(), name, description)
+
+    def _submit(self, spec: BaseSpecification, project: str, user: str, cwd: str, name, description):
+        proj = self.store.get_or_create_project(spec.project or project, user)
+        if spec.kind == Kinds.EXPERIMENT:
+            xid = self._create_experiment(spec, proj, user, cwd, name=name, description=description)
+            return {"kind": "experiment", "id": xid}
+        if spec.kind == Kinds.GROUP:
+            from polyaxon_amd.polyflow.groups import make_group_driver
+
+            gid = self.store.create_group(proj["id"], spec.raw_data, spec.hptuning.to_dict(), user=user,
+                                          name=name or spec.name, description=description, tags=spec.tags,
+                                          search_algorithm=spec.search_algorithm, concurrency=spec.concurrency)
+            self.auditor.record("experiment_group.created", "experiment_group", gid, user)
+            driver = make_group_driver(self, gid, spec, proj, user, cwd)
+            self.groups[gid] = driver
+            driver.start()
+            return {"kind": "group", "id": gid}
+        if spec.kind in (Kinds.JOB, Kinds.NOTEBOOK, Kinds.TENSORBOARD, Kinds.BUILD):
+            jid = self._create_job(spec, proj, user, cwd, name=name, description=description)
+            return {"kind": spec.kind, "id": jid}
+        if spec.kind == Kinds.PIPELINE:
+            from polyaxon_amd.polyflow.pipelines import PipelineRunner
+
+            pid = self.store.create_pipeline(proj["id"], name or spec.name or "pipeline", spec.raw_data, user,
+                                             spec.concurrency, spec.schedule)
+            runner = PipelineRunner(self, pid, spec, proj, user, cwd)
+            self.pipelines[pid] = runner
+            rid = runner.start()
+            return {"kind": "pipeline", "id": pid, "run_id": rid}
+        raise PolyaxonfileError(f"cannot run kind {spec.kind}")
+
+    # ------------------------------------------------------------------ experiments
+    def _create_experiment(self, spec: ExperimentSpecification, proj: Dict, user: str, cwd: str,
+                           group_id: Optional[int] = None, name=None, description=None,
+                           original_id: Optional[int] = None, strategy: Optional[str] = None,
+                           enqueue: bool = True) -> int:
+        xid = self.store.create_experiment(
+            proj["id"], spec.raw_data, group_id=group_id, user=user, name=name or spec.name, description=description,
+            declarations=spec.declarations, tags=spec.tags, original_experiment_id=original_id,
+            cloning_strategy=strategy, framework=spec.framework,
+            resources=spec.total_resources.to_dict() if spec.total_resources else None)
+        root = self._clone_root(original_id, strategy)
+        outputs = self.paths.experiment_outputs(user, proj["name"], root["id"] if root else xid,
+                                                root["group_id"] if root else group_id)
+        if strategy == "copy" and original_id:
+            orig = self.store.get_experiment(original_id)
+            outputs = self.paths.experiment_outputs(user, proj["name"], xid, group_id)
+            self.paths.prepare_outputs(outputs, "copy", orig["outputs_path"])
+        else:
+            self.paths.prepare_outputs(outputs, "resume" if strategy == "resume" else None)
+        logs = self.paths.experiment_logs(user, proj["name"], xid, group_id)
+        os.makedirs(logs, exist_ok=True)
+        self.store.update_experiment(xid, outputs_path=outputs, logs_path=logs)
+        self.auditor.record("experiment.created", "experiment", xid, user, group=group_id)
+        run = Run("experiment", xid, spec, cwd)
+        self.runs[run.owner] = run
+        if enqueue:
+            self._enqueue(run)
+        return xid
+
+    def _clone_root(self, original_id: Optional[int], strategy: Optional[str]) -> Optional[Dict]:
+        """Resuming a resumed experiment resumes the root (reference db/models/experiments.py:261-269)."""
+        if not original_id or strategy != "resume":
+            return None
+        x = self.store.get_experiment(original_id)
+        while x and x.get("cloning_strategy") == "resume" and x.get("original_experiment_id"):
+            x = self.store.get_experiment(x["original_experiment_id"])
+        return x
+
+    def _enqueue(self, run: Run) -> None:
+        spec = run.spec
+        if spec.build is not None and spec.build.build_steps and run.build_id is None:
+            bid = self._ensure_build(spec, run)
+            if bid is not None:
+                run.build_id = bid
+                return  # released by the build's completion callback
+        self.pending.append(run.owner)
+
+    # ------------------------------------------------------------------ builds (dockerizer equivalent)
+    def _build_hash(self, spec: BaseSpecification, cwd: str) -> str:
+        b = spec.build
+        h = hashlib.sha256(json.dumps({"image": b.image, "steps": b.build_steps, "env": b.env_vars,
+                                       "ref": b.ref, "cwd": cwd}, sort_keys=True).encode())
+        return h.hexdigest()[:20]
+
+    def _ensure_build(self, spec: BaseSpecification, dependent: Run) -> Optional[int]:
+        """Run ``build.build_steps`` once per (image, steps, env) hash, reusing a success within 6 h.
+        Returns the build job id the dependent must wait for, or None if a cached build exists."""
+        h = self._build_hash(spec, dependent.cwd)
+        cached = self.store.last_build_for_hash(h, BUILD_REUSE_S)
+        if cached and not spec.build.nocache:
+            dependent.extra_env.update({"PLX_BUILD_DIR": cached["outputs_path"] or ""})
+            if dependent.kind == "experiment":
+                self.store.update_experiment(dependent.id, build_job_id=cached["id"])
+            return None
+        owner = next((o for o, r in self.runs.items() if r.kind == "job" and r.spec.kind == Kinds.BUILD
+                      and r.extra_env.get("PLX_BUILD_HASH") == h and r.final_status is None), None)
+        if owner is None:
+            proj = self.store.get("projects", self._project_id(dependent))
+            bspec = specification_for({"version": 1, "kind": "build", "build": spec.build.to_dict()})
+            bid = self._create_job(bspec, proj, "root", dependent.cwd, build_hash=h)
+            owner = f"job:{bid}"
+        brun = self.runs[owner]
+        if dependent.kind == "experiment":
+            self.store.set_experiment_status(dependent.id, "building")
+            self.store.update_experiment(dependent.id, build_job_id=brun.id)
+
+        def release(status: str, dep=dependent, brun=brun):
+            if status == "succeeded":
+                dep.extra_env["PLX_BUILD_DIR"] = self.store.get_job(brun.id)["outputs_path"] or ""
+                self.pending.append(dep.owner)
+            else:
+                self._finish_unstarted(dep, "failed", f"build {brun.id} {status}")
+
+        brun.on_done.append(release)
+        return brun.id
+
+    def _project_id(self, run: Run) -> int:
+        rec = self.store.get_experiment(run.id) if run.kind == "experiment" else self.store.get_job(run.id)
+        return rec["project_id"]
+
+    # ------------------------------------------------------------------ generic jobs, notebooks, tensorboards
+    def _create_job(self, spec: BaseSpecification, proj: Dict, user: str, cwd: str, name=None, description=None,
+                    build_hash: Optional[str] = None) -> int:
+        jid = self.store.create_job(spec.kind, proj["id"], spec.raw_data, user=user, name=name or spec.name,
+                                    description=description, tags=spec.tags,
+                                    image=spec.build.image if spec.build else None, image_hash=build_hash)
+        kind_dir = {"job": "jobs", "build": "builds", "notebook": "notebooks", "tensorboard": "tensorboards"}[spec.kind]
+        outputs = self.paths.job_outputs(user, proj["name"], jid, kind_dir)
+        if spec.kind == Kinds.BUILD and build_hash:
+            outputs = os.path.join(self.paths.envs_root, build_hash)
+        os.makedirs(outputs, exist_ok=True)
+        logs = self.paths.job_logs(user, proj["name"], jid, kind_dir)
+        os.makedirs(logs, exist_ok=True)
+        self.store.update_job(jid, outputs_path=outputs, logs_path=logs)
+        subject = {"job": "job", "build": "build_job", "notebook": "notebook", "tensorboard": "tensorboard"}[spec.kind]
+        self.auditor.record(f"{subject}.created" if subject in ("job", "build_job") else f"{subject}.started",
+                            spec.kind, jid, user)
+        run = Run("job", jid, spec, cwd)
+        if build_hash:
+            run.extra_env["PLX_BUILD_HASH"] = build_hash
+        if spec.kind in (Kinds.NOTEBOOK, Kinds.TENSORBOARD):
+            run.port = free_port()
+            self.store.update_job(jid, port=run.port)
+        self.runs[run.owner] = run
+        if spec.kind == Kinds.BUILD:
+            self.pending.append(run.owner)
+        else:
+            self._enqueue(run)
+        return jid
+
+    def _job_command(self, run: Run) -> str:
+        spec = run.spec
+        if spec.kind == Kinds.BUILD:
+            steps = spec.build.build_steps or ["true"]
+            return " && ".join(steps)
+        if spec.kind == Kinds.NOTEBOOK:
+            return (f"{self.python} -m jupyter lab --no-browser --ip=127.0.0.1 --port={run.port} "
+                    f"--NotebookApp.token={uuid.uuid4().hex} --notebook-dir={run.cwd}")
+        if spec.kind == Kinds.TENSORBOARD:
+            return f"{self.python} -m tensorboard.main --logdir={self.paths.outputs_root} --port={run.port} --host=127.0.0.1"
+        return _command(spec)
+
+    # ================================================================== placement
+    def _requirements(self, run: Run) -> List[Tuple[str, int, float]]:
+        spec = run.spec
+        if run.kind == "job":
+            res = spec.resources
+            return [("master", 0, float(res.gpu.value) if res and res.gpu else 0.0)]
+        cluster, _ = spec.cluster_def
+        reqs = []
+        for role in ("master", "worker", "ps"):
+            for i in range(cluster.get(role, 0)):
+                reqs.append((role, i, _replica_gpus(spec, role, i)))
+        return reqs
+
+    def _schedule(self) -> None:
+        if not self.pending:
+            return
+        still: Deque[str] = deque()
+        while self.pending:
+            owner = self.pending.popleft()
+            run = self.runs.get(owner)
+            if run is None or run.final_status is not None or run.stop_requested:
+                continue
+            if not self._try_place(run):
+                still.append(owner)
+        self.pending = still
+
+    def _try_place(self, run: Run) -> bool:
+        reqs = self._requirements(run)
+        need = [g for _, _, g in reqs]
+        if any(g > self.alloc.n_devices + 1e-9 for g in need) or sum(g for g in need if g >= 1) > self.alloc.n_devices:
+            self._finish_unstarted(run, "failed", f"requests {need} GPUs but the node has {self.alloc.n_devices}")
+            return True
+        taken: List[str] = []
+        devices: List[List[int]] = []
+        for (role, idx, g) in reqs:
+            owner = f"{run.owner}:{role}.{idx}"
+            a = self.alloc.allocate(owner, g) if g > 0 else None
+            if g > 0 and a is None:
+                for o in taken:
+                    self.alloc.release(o)
+                return False
+            if a is not None:
+                taken.append(owner)
+            devices.append(a.devices if a else [])
+        self._spawn(run, reqs, devices)
+        return True
+
+    def _finish_unstarted(self, run: Run, status: str, message: str) -> None:
+        run.final_status = status
+        run.final_message = message
+        if run.kind == "experiment":
+            if status == "stopped":
+                self.store.set_experiment_status(run.id, "stopped", message)
+            else:
+                self.store.set_experiment_status(run.id, status, message)
+        else:
+            self.store.set_job_status(run.id, status, message)
+        self._after_done(run, status)
+
+    # ================================================================== spawning
+    def _spawn(self, run: Run, reqs, devices) -> None:
+        spec = run.spec
+        if run.kind == "experiment":
+            rec = self.store.get_experiment(run.id)
+            self.store.set_experiment_status(run.id, "scheduled")
+        else:
+            rec = self.store.get_job(run.id)
+            self.store.set_job_status(run.id, "scheduled")
+        proj = self.store.get("projects", rec["project_id"])
+        group = self.store.get_group(rec["group_id"]) if run.kind == "experiment" and rec.get("group_id") else None
+        base_port = free_port()
+        cluster, _ = spec.cluster_def if run.kind == "experiment" else ({"master": 1}, False)
+        cdef = make_cluster_def(spec.framework, cluster, base_port)
+        master_port = base_port
+        try:
+            cmd = self._job_command(run) if run.kind == "job" else _command(spec)
+        except PolyaxonfileError as e:
+            for role, idx, _ in reqs:
+                self.alloc.release(f"{run.owner}:{role}.{idx}")
+            self._finish_unstarted(run, "failed", str(e))
+            return
+        refs = self._refs_outputs(spec)
+        data_paths = {name: os.path.join(self.paths.data_root, name)
+                      for name in (spec.environment.persistence.get("data") or [])} if spec.environment else {}
+        if run.kind == "experiment":
+            self.store.set_experiment_status(run.id, "starting")
+        local_rank = 0
+        for (role, idx, g), devs in zip(reqs, devices):
+            if run.kind == "experiment":
+                jid = self.store.create_experiment_job(run.id, role, idx, definition={"cmd": cmd},
+                                                       resources={"gpu": g}, devices=devs)
+            else:
+                jid = run.id
+            rep = Replica(role, idx, jid, g, devs)
+            run.replicas.append(rep)
+            env = trial_env(experiment=rec if run.kind == "experiment" else {"id": rec["id"], "uuid": rec["uuid"]},
+                            project=proj["name"], user=rec["user"], group=group, role=role, index=idx,
+                            framework=spec.framework if run.kind == "experiment" else None, cluster=cdef,
+                            devices=devs, outputs_path=rec["outputs_path"], logs_path=rec["logs_path"],
+                            declarations=spec.declarations, data_paths=data_paths, refs_outputs=refs,
+                            log_level=(spec.logging or {}).get("level"), store_path=self.store_path,
+                            api_host=self.api_host, ephemeral_token=uuid.uuid4().hex, master_port=master_port,
+                            local_rank=local_rank)
+            env.update(run.extra_env)
+            if spec.kind == Kinds.BUILD:
+                env["PLX_BUILD_DIR"] = rec["outputs_path"]
+            if env.get("PLX_BUILD_DIR"):  # built environments install into <env>/site (pip --target)
+                site = os.path.join(env["PLX_BUILD_DIR"], "site")
+                env["PYTHONPATH"] = site + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+            for k, v in (spec.build.env_vars if spec.build else []):
+                env[str(k)] = str(v)
+            for k, v in spec.environment.env_vars if spec.environment else []:
+                env[str(k)] = str(v)
+            if run.kind == "job":
+                env["POLYAXON_JOB_INFO"] = json.dumps({"job_id": rec["id"], "job_uuid": rec["uuid"],
+                                                       "kind": spec.kind, "project_name": proj["name"]})
+            log_path = self.paths.replica_log(rec["logs_path"], role, idx)
+            try:
+                pid = self.pm.spawn(["/bin/bash", "-c", cmd], env, cwd=run.cwd, log_path=log_path)
+            except OSError as e:
+                rep.done = True
+                self._replica_status(run, rep, "failed", f"spawn failed: {e}")
+                self._stop_run(run, f"replica {role}.{idx} failed to start")
+                self._maybe_finalize(run)
+                return
+            rep.pid = pid
+            self.pid_index[pid] = (run.owner, len(run.replicas) - 1)
+            self.stats["spawned"] += 1
+            if self._last_exit_t is not None:
+                self.stats["gaps_ms"].append((time.time() - self._last_exit_t) * 1000.0)
+                self._last_exit_t = None
+            if run.kind == "experiment":
+                self.store.update_experiment_job(jid, pid=pid)
+                self.store.set_experiment_job_status(jid, "scheduled")
+                self.store.set_experiment_job_status(jid, "running")
+            else:
+                self.store.update_job(jid, pid=pid, devices=devs)
+                self.store.set_job_status(jid, "running")
+            local_rank += 1 if devs else 0
+        run.started = time.time()
+        if run.kind == "experiment":
+            self.store.set_experiment_status(run.id, "running")
+            self.auditor.record("experiment.new_status", "experiment", run.id, status="running")
+        else:
+            self.auditor.record(f"{self._subject(run)}.new_status", run.spec.kind, run.id, status="running")
+
+    def _subject(self, run: Run) -> str:
+        return {"job": "job", "build": "build_job", "notebook": "notebook", "tensorboard": "tensorboard"}.get(
+            run.spec.kind, "job")
+
+    def _refs_outputs(self, spec: BaseSpecification) -> Dict[str, List[str]]:
+        out: Dict[str, List[str]] = {}
+        refs = spec.environment.outputs if spec.environment else {}
+        for ref in refs.get("experiments", []) or []:
+            x = self._resolve_ref("experiments", ref)
+            if x:
+                out.setdefault("experiments", []).append(x["outputs_path"])
+        for ref in refs.get("jobs", []) or []:
+            j = self._resolve_ref("jobs", ref)
+            if j:
+                out.setdefault("jobs", []).append(j["outputs_path"])
+        return out
+
+    def _resolve_ref(self, table: str, ref) -> Optional[Dict]:
+        """Outputs references by id, name, project.name or user.project.name (reference signals/outputs.py)."""
+        if isinstance(ref, int) or (isinstance(ref, str) and ref.isdigit()):
+            return self.store.get(table, int(ref))
+        parts = str(ref).split(".")
+        name = parts[-1]
+        rows = self.store.execute(f"SELECT * FROM {table} WHERE name = ? ORDER BY id DESC", (name,)).fetchall()
+        return self.store._row(rows[0]) if rows else None
+
+    # ================================================================== exits and aggregation
+    def _replica_status(self, run: Run, rep: Replica, status: str, message: Optional[str] = None) -> None:
+        if run.kind == "experiment":
+            self.store.set_experiment_job_status(rep.job_id, status, message)
+            self.store.update_experiment_job(rep.job_id, exit_code=rep.exit_code)
+        else:
+            self.store.update_job(rep.job_id, exit_code=rep.exit_code)
+
+    def _on_exit(self, pid: int, status: int) -> None:
+        self.stats["exited"] += 1
+        self._last_exit_t = time.time()
+        key = self.pid_index.pop(pid, None)
+        if key is None:
+            return
+        owner, ri = key
+        run = self.runs.get(owner)
+        if run is None:
+            return
+        rep = run.replicas[ri]
+        rep.done = True
+        rep.exit_code = status
+        self.alloc.release(f"{run.owner}:{rep.role}.{rep.index}")
+        if run.stop_requested:
+            # replicas torn down after the master succeeded count as succeeded ("Master is done.")
+            jstatus = "succeeded" if run.final_status == "succeeded" else "stopped"
+            self._replica_status(run, rep, jstatus, run.stop_reason)
+        elif status == 0:
+            self._replica_status(run, rep, "succeeded")
+            if rep.role == "master":
+                run.final_status = "succeeded"  # master done wins (reference db/models/experiments.py:175-183)
+                self._stop_run(run, "Master is done.")
+        else:
+            msg = f"exit code {status}" if status > 0 else f"killed by signal {-status}"
+            self._replica_status(run, rep, "failed", msg)
+            run.final_status = "failed"
+            run.final_message = f"{rep.role}.{rep.index} {msg}"
+            self._stop_run(run, f"replica {rep.role}.{rep.index} failed")
+        self._maybe_finalize(run)
+
+    def _maybe_finalize(self, run: Run) -> None:
+        if any(not r.done for r in run.replicas):
+            return
+        if run.final_status is None:
+            run.final_status = "stopped" if run.stop_requested else "succeeded"
+        status = run.final_status
+        if run.kind == "experiment":
+            # remaining replicas that were stopped because the master finished count as succeeded
+            self.store.set_experiment_status(run.id, status, run.final_message)
+            self.auditor.record(f"experiment.{'done' if status == 'stopped' else status}", "experiment", run.id,
+                                status=status)
+        else:
+            self.store.set_job_status(run.id, status, run.final_message)
+            subj = self._subject(run)
+            ev = f"{subj}.{status}" if status in ("succeeded", "failed") else f"{subj}.stopped"
+            self.auditor.record(ev, run.spec.kind, run.id, status=status)
+        self._after_done(run, status)
+
+    def _after_done(self, run: Run, status: str) -> None:
+        for cb in run.on_done:
+            try:
+                cb(status)
+            except Exception:
+                log.exception("on_done callback failed")
+        if run.kind == "experiment":
+            rec = self.store.get_experiment(run.id)
+            gid = rec.get("group_id") if rec else None
+            if gid in self.groups:
+                self.groups[gid].on_experiment_done(run.id, status)
+
+    # ================================================================== stopping
+    def _stop_run(self, run: Run, reason: str) -> None:
+        """SIGTERM every live replica's process group now, SIGKILL whatever is left after the grace period."""
+        run.stop_requested = True
+        run.stop_reason = reason
+        live = [r for r in run.replicas if r.pid is not None and not r.done]
+        for r in live:
+            self.pm.signal(r.pid, signal.SIGTERM, group=True)
+        if live:
+            pids = [r.pid for r in live]
+
+            def kill(pids=pids, run=run):
+                for r in run.replicas:
+                    if r.pid in pids and not r.done:
+                        self.pm.signal(r.pid, signal.SIGKILL, group=True)
+
+            self.after(self.stop_grace_s, kill)
+
+    def _stop(self, kind: str, id_: int, message: str = "Stopped by user.") -> bool:
+        run = self.runs.get(f"{kind}:{id_}")
+        if run is None or run.final_status is not None and not run.active:
+            return False
+        if not run.replicas:  # never placed
+            self._finish_unstarted(run, "stopped", message)
+            return True
+        if run.final_status is None:
+            run.final_status = "stopped"
+            run.final_message = message
+        self._stop_run(run, message)
+        return True
+
+    def stop_experiment(self, xid: int, message: str = "Stopped by user.") -> bool:
+        self.auditor.record("experiment.stopped_triggered", "experiment", xid)
+        return self.call(self._stop, "experiment", xid, message)
+
+    def stop_job(self, jid: int) -> bool:
+        return self.call(self._stop, "job", jid, "Stopped by user.")
+
+    def stop_group(self, gid: int, pending: bool = False, message: str = "Stopped by user.") -> None:
+        self.auditor.record("experiment_group.stopped_triggered", "experiment_group", gid)
+        self.call(self._stop_group, gid, pending, message)
+
+    def _stop_group(self, gid: int, pending: bool, message: str) -> None:
+        driver = self.groups.get(gid)
+        if driver is not None:
+            driver.stop(pending_only=pending, message=message)
+
+    def _stop_all(self) -> None:
+        for run in list(self.runs.values()):
+            if run.final_status is None or run.active:
+                if run.replicas:
+                    if run.final_status is None:
+                        run.final_status = "stopped"
+                    self._stop_run(run, "Scheduler shutdown.")
+                elif run.final_status is None:
+                    self._finish_unstarted(run, "stopped", "Scheduler shutdown.")
+
+    # ================================================================== cloning: restart / resume / copy
+    def clone_experiment(self, xid: int, strategy: str, declarations: Optional[Dict[str, Any]] = None,
+                         content=None) -> int:
+        """Reference Experiment.restart/resume/copy (db/models/experiments.py:225-316)."""
+        if strategy not in ("restart", "resume", "copy"):
+            raise ValueError(f"unknown cloning strategy {strategy}")
+        return self.call(self._clone, xid, strategy, declarations, content)
+
+    def _clone(self, xid: int, strategy: str, declarations, content, group_id=None) -> int:
+        orig = self.store.get_experiment(xid)
+        if orig is None:
+            raise KeyError(f"experiment {xid} not found")
+        raw = dict(content) if content is not None else dict(orig["config"])
+        if declarations:
+            raw["declarations"] = dict(raw.get("declarations") or {}, **declarations)
+        spec = ExperimentSpecification(raw)
+        proj = self.store.get("projects", orig["project_id"])
+        old = self.runs.get(f"experiment:{xid}")
+        cwd = old.cwd if old else os.getcwd()
+        new = self._create_experiment(spec, proj, orig["user"], cwd,
+                                      group_id=orig["group_id"] if group_id is None else group_id,
+                                      original_id=xid, strategy=strategy)
+        self.auditor.record(f"experiment.{ {'restart': 'restarted', 'resume': 'resumed', 'copy': 'copied'}[strategy]}",
+                            "experiment", new, original=xid)
+        return new
+
+    # ================================================================== queries / waiting
+    def wait(self, kind: str, id_: int, timeout: Optional[float] = None, poll_s: float = 0.02) -> str:
+        end = None if timeout is None else time.time() + timeout
+        while True:
+            if kind == "experiment":
+                rec = self.store.get_experiment(id_)
+                st = rec["status"]
+                done = ExperimentLifeCycle.is_done(st)
+            elif kind == "group":
+                rec = self.store.get_group(id_)
+                st = rec["status"]
+                done = st in ("succeeded", "failed", "stopped")
+            elif kind == "pipeline_run":
+                rec = self.store.get("pipeline_runs", id_)
+                st = rec["status"]
+                done = st in ("finished", "stopped", "skipped")
+            else:
+                rec = self.store.get_job(id_)
+                st = rec["status"]
+                done = JobLifeCycle.is_done(st)
+            if done:
+                return st
+            if end is not None and time.time() > end:
+                raise TimeoutError(f"{kind} {id_} still {st}")
+            time.sleep(poll_s)
+
+    def wait_idle(self, timeout: float = 60.0) -> None:
+        end = time.time() + timeout
+        while time.time() < end:
+            busy = self.call(lambda: any(r.active for r in self.runs.values()) or bool(self.pending)
+                             or any(not d.done for d in self.groups.values()))
+            if not busy:
+                return
+            time.sleep(0.02)
+        raise TimeoutError("scheduler did not become idle")
+
+    def running_experiments(self) -> List[int]:
+        return self.call(lambda: [r.id for r in self.runs.values() if r.kind == "experiment" and r.active])
+
+    def logs(self, kind: str, id_: int, tail: Optional[int] = None) -> str:
+        """Experiment logs = every replica log prefixed ``role.index -- `` (reference events_handlers/tasks/logs.py)."""
+        if kind == "experiment":
+            rec = self.store.get_experiment(id_)
+            out = []
+            for j in self.store.experiment_jobs(id_):
+                path = self.paths.replica_log(rec["logs_path"], j["role"], j["idx"])
+                for line in Paths.read_log(path).splitlines():
+                    out.append(f"{j['role']}.{j['idx']} -- {line}")
+            lines = out
+        else:
+            rec = self.store.get_job(id_)
+            lines = Paths.read_log(self.paths.replica_log(rec["logs_path"], "master", 0)).splitlines()
+        if tail:
+            lines = lines[-tail:]
+        return "\n".join(lines)
+
+
+class _Result:
+    def __init__(self):
+        self._ev = threading.Event()
+        self._val = None
+        self._err: Optional[BaseException] = None
+
+    def set(self, v):
+        self._val = v
+        self._ev.set()
+
+    def fail(self, e: BaseException):
+        self._err = e
+        self._ev.set()
+
+    def get(self, timeout: Optional[float]):
+        if not self._ev.wait(timeout):
+            raise TimeoutError("polyflow command timed out")
+        if self._err is not None:
+            raise self._err
+        return self._val

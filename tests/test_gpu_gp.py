@@ -1,0 +1,77 @@
+"""GP / acquisition HIP kernels (csrc/gp_kernels.hip) vs the numpy/scipy fp64 reference of the same math."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("kind,nu", [("rbf", 0.0), ("matern05", 0.5), ("matern15", 1.5), ("matern25", 2.5),
+                                     ("matern_nu", 1.9), ("matern_nu", 0.7)])
+@pytest.mark.parametrize("n,m,d", [(7, 5, 3), (100, 130, 11), (64, 64, 64)])
+def test_kmat_matches_numpy(cuda, kind, nu, n, m, d):
+    from polyaxon_amd.polytune.bo import HipGP, kernel_np
+
+    rng = np.random.RandomState(0)
+    A = rng.uniform(-1, 1, size=(n, d)).astype(np.float32)
+    B = rng.uniform(-1, 1, size=(m, d)).astype(np.float32)
+    ls = 0.8 * np.sqrt(d)
+    K = HipGP(cuda).kmat(A, B, kind, ls, nu).cpu().numpy()
+    ref = kernel_np(A.astype(np.float64), B.astype(np.float64), kind, ls, nu)
+    np.testing.assert_allclose(K, ref, rtol=2e-4, atol=2e-5)
+
+
+def test_cholesky_matches_numpy(cuda):
+    import torch
+
+    from polyaxon_amd.polytune.bo import HipGP, kernel_np
+
+    rng = np.random.RandomState(1)
+    for n in (1, 5, 64, 128):
+        X = rng.uniform(0, 5, size=(n, 4))
+        K = kernel_np(X, X, "matern25", 1.0, 2.5) + 1e-4 * np.eye(n)
+        L = HipGP(cuda).cholesky(torch.tensor(K, dtype=torch.float32, device=cuda)).cpu().numpy()
+        np.testing.assert_allclose(L, np.linalg.cholesky(K), rtol=1e-3, atol=1e-4)
+    with pytest.raises(np.linalg.LinAlgError):
+        HipGP(cuda).cholesky(torch.tensor([[1.0, 2.0], [2.0, 1.0]], device=cuda))
+
+
+@pytest.mark.parametrize("n", [3, 20, 40, 64, 90])
+@pytest.mark.parametrize("acq", ["ucb", "ei", "poi"])
+def test_predict_acq_matches_numpy(cuda, n, acq):
+    from polyaxon_amd.polytune.bo import HipGP, acquisition_np, fit_gp, predict_np
+
+    rng = np.random.RandomState(2)
+    d = 5
+    X = rng.uniform(0, 3, size=(n, d))
+    y = np.sin(X).sum(1)
+    gp = fit_gp(X, y, kernel="matern", nu=2.5, length_scale=1.5, optimize=False)
+    Xc = rng.uniform(0, 3, size=(3000, d))
+    hip = HipGP(cuda)
+    dev = hip.fit(gp)
+    out, best, mean, std = hip.predict_acq(gp, dev, Xc, acq, float(y.max()), 1.3, 0.01, want_mean_std=True)
+    m_ref, s_ref = predict_np(gp, Xc)
+    a_ref = acquisition_np(m_ref, s_ref, acq, float(y.max()), 1.3, 0.01)
+    np.testing.assert_allclose(mean.cpu().numpy(), m_ref, rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(std.cpu().numpy(), s_ref, rtol=2e-2, atol=3e-3)
+    np.testing.assert_allclose(out.cpu().numpy(), a_ref, rtol=2e-2, atol=3e-3)
+    assert a_ref[best] >= a_ref.max() - 1e-2
+
+
+def test_bo_manager_hip_backend_end_to_end(cuda):
+    from polyaxon_amd.polytune.bo import BOOptimizer
+    from polyaxon_amd.spec.hptuning import HPTuningConfig
+
+    cfg = HPTuningConfig.from_dict({
+        "seed": 4,
+        "bo": {"n_iterations": 3, "n_initial_trials": 3, "metric": {"name": "loss", "optimization": "minimize"},
+               "utility_function": {"acquisition_function": "ei", "eps": 0.0,
+                                    "gaussian_process": {"kernel": "matern", "length_scale": 1.0, "nu": 1.9}}},
+        "matrix": {"x": {"uniform": [-3, 3]}, "z": {"uniform": [-3, 3]}, "c": {"values": ["a", "b"]}}})
+    rng = np.random.RandomState(0)
+    configs = [{"x": float(a), "z": float(b), "c": "ab"[i % 2]} for i, (a, b) in
+               enumerate(rng.uniform(-3, 3, size=(12, 2)))]
+    f = lambda c: (c["x"] - 1) ** 2 + (c["z"] + 0.5) ** 2 + (0.3 if c["c"] == "b" else 0)  # noqa: E731
+    opt = BOOptimizer(cfg, backend="hip")
+    opt.add_observations(configs, [f(c) for c in configs])
+    s = opt.get_suggestion()
+    assert f(s) < min(f(c) for c in configs) + 0.5

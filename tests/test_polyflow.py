@@ -1,0 +1,258 @@
+"""polyflow scheduler on CPU: trials are real subprocesses; devices are a fake pool (no GPU needed).
+
+Covers the reference's lifecycle tests (tests/test_experiments/test_models.py,
+tests/test_experiment_groups/test_models.py) with a real process backend instead of mocked spawners."""
+import json
+import os
+import sys
+import textwrap
+import time
+
+import pytest
+
+from polyaxon_amd.polyflow.devices import Device, DeviceAllocator
+from polyaxon_amd.polyflow.scheduler import Polyflow
+
+PY = sys.executable
+
+
+def _flow(tmp_path, n_gpus=2, grace=2.0):
+    alloc = DeviceAllocator([Device(i) for i in range(n_gpus)])
+    return Polyflow(str(tmp_path / "plx"), allocator=alloc, stop_grace_s=grace).start()
+
+
+def _xp(cmd, **env):
+    d = {"version": 1, "kind": "experiment", "run": {"cmd": cmd}}
+    if env:
+        d["environment"] = env
+    return d
+
+
+def test_experiment_success_env_contract_and_logs(tmp_path):
+    flow = _flow(tmp_path)
+    try:
+        script = ("import os,json; print('HIP', os.environ['HIP_VISIBLE_DEVICES']); "
+                  "print('DECL', os.environ['POLYAXON_DECLARATIONS']); print('OUT', os.environ['POLYAXON_RUN_OUTPUTS_PATH']);"
+                  "print('TASK', os.environ['POLYAXON_TASK_INFO'])")
+        spec = _xp(f"{PY} -c \"{script}\"", resources={"gpu": {"limits": 1}})
+        spec["declarations"] = {"lr": 0.5}
+        r = flow.submit(spec, project="p")
+        assert flow.wait("experiment", r["id"], timeout=30) == "succeeded"
+        logs = flow.logs("experiment", r["id"])
+        assert "master.0 -- HIP 0" in logs and '"lr": 0.5' in logs and '"type": "master"' in logs
+        x = flow.store.get_experiment(r["id"])
+        assert os.path.isdir(x["outputs_path"]) and "/root/p/experiments/" in x["outputs_path"]
+        sts = [s["status"] for s in flow.store.experiment_statuses(r["id"])]
+        assert sts == ["created", "scheduled", "starting", "running", "succeeded"]
+        jobs = flow.store.experiment_jobs(r["id"])
+        assert [j["status"] for j in jobs] == ["succeeded"] and jobs[0]["devices"] == [0]
+    finally:
+        flow.shutdown()
+
+
+def test_failure_and_stop(tmp_path):
+    flow = _flow(tmp_path)
+    try:
+        bad = flow.submit(_xp("exit 3"))
+        assert flow.wait("experiment", bad["id"], timeout=30) == "failed"
+        j = flow.store.experiment_jobs(bad["id"])[0]
+        assert j["exit_code"] == 3 and j["status"] == "failed"
+        slow = flow.submit(_xp("sleep 60"))
+        deadline = time.time() + 10
+        while flow.store.get_experiment(slow["id"])["status"] != "running" and time.time() < deadline:
+            time.sleep(0.02)
+        assert flow.stop_experiment(slow["id"])
+        assert flow.wait("experiment", slow["id"], timeout=15) == "stopped"
+    finally:
+        flow.shutdown()
+
+
+def test_distributed_pytorch_master_done_wins(tmp_path):
+    flow = _flow(tmp_path, n_gpus=4)
+    try:
+        script = ("import os,sys,time; print(os.environ['RANK'], os.environ['WORLD_SIZE'], os.environ['MASTER_ADDR'],"
+                  " os.environ['HIP_VISIBLE_DEVICES'], flush=True); "
+                  "time.sleep(1 if os.environ['RANK']=='0' else 30)")
+        spec = _xp(f"{PY} -c \"{script}\"", resources={"gpu": {"limits": 1}},
+                   pytorch={"n_workers": 2, "default_worker": {"resources": {"gpu": {"limits": 1}}}})
+        r = flow.submit(spec)
+        assert flow.wait("experiment", r["id"], timeout=30) == "succeeded"
+        jobs = flow.store.experiment_jobs(r["id"])
+        assert [(j["role"], j["idx"]) for j in jobs] == [("master", 0), ("worker", 0), ("worker", 1)]
+        assert all(j["status"] == "succeeded" for j in jobs)  # "Master is done."
+        assert sorted(d for j in jobs for d in j["devices"]) == [0, 1, 2]
+        logs = flow.logs("experiment", r["id"])
+        assert "master.0 -- 0 3 127.0.0.1" in logs and "worker.1 -- 2 3 127.0.0.1" in logs
+    finally:
+        flow.shutdown()
+
+
+def test_distributed_worker_failure_fails_experiment(tmp_path):
+    flow = _flow(tmp_path, n_gpus=2)
+    try:
+        script = "import os,sys,time; sys.exit(5) if os.environ['RANK']=='1' else time.sleep(30)"
+        r = flow.submit(_xp(f"{PY} -c \"{script}\"", pytorch={"n_workers": 1}))
+        assert flow.wait("experiment", r["id"], timeout=30) == "failed"
+        st = {j["role"]: j["status"] for j in flow.store.experiment_jobs(r["id"])}
+        assert st == {"master": "stopped", "worker": "failed"}
+    finally:
+        flow.shutdown()
+
+
+def test_gang_allocation_waits_for_devices(tmp_path):
+    flow = _flow(tmp_path, n_gpus=2)
+    try:
+        a = flow.submit(_xp("sleep 0.5", resources={"gpu": {"limits": 1}}))
+        b = flow.submit(_xp("true", resources={"gpu": {"limits": 2}}))
+        assert flow.wait("experiment", b["id"], timeout=30) == "succeeded"
+        xa, xb = flow.store.get_experiment(a["id"]), flow.store.get_experiment(b["id"])
+        assert xb["started_at"] >= xa["finished_at"] - 0.05
+        too_big = flow.submit(_xp("true", resources={"gpu": {"limits": 3}}))
+        assert flow.wait("experiment", too_big["id"], timeout=10) == "failed"
+    finally:
+        flow.shutdown()
+
+
+def _group(algo_block, matrix, cmd, concurrency=2, extra=None):
+    d = {"version": 1, "kind": "group", "hptuning": {"concurrency": concurrency, "matrix": matrix, **algo_block},
+         "run": {"cmd": cmd}}
+    if extra:
+        d.update(extra)
+    return d
+
+
+TRIAL = ("from polyaxon_amd.client import Experiment, get_declarations; import time; d = get_declarations(); "
+         "e = Experiment(); time.sleep(float(d.get('sleep', 0.05))); "
+         "e.log_metrics(step=1, loss=(d['lr'] - 0.3) ** 2 + 1.0 / float(d.get('steps', 1))); e.close()")
+
+
+def _trial_cmd():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return f"PYTHONPATH={root} {PY} -c \"{TRIAL}\""
+
+
+def test_grid_group_concurrency_and_metrics(tmp_path):
+    flow = _flow(tmp_path, n_gpus=1)
+    try:
+        spec = _group({}, {"lr": {"values": [0.1, 0.2, 0.3]}, "sleep": {"values": [0.3, 0.31]}}, _trial_cmd(),
+                      concurrency=2, extra={"environment": {"resources": {"gpu": {"limits": 0.25}}}})
+        g = flow.submit(spec)
+        assert flow.wait("group", g["id"], timeout=60) == "succeeded"
+        xps = flow.store.list_experiments(group_id=g["id"], sort="metric.loss")
+        assert len(xps) == 6 and all(x["status"] == "succeeded" for x in xps)
+        assert xps[0]["declarations"]["lr"] == 0.3
+        # never more than `concurrency` trials overlapping
+        spans = sorted((x["started_at"], x["finished_at"]) for x in xps)
+        for t, _ in spans:
+            assert sum(1 for s, f in spans if s <= t < f) <= 2
+        assert [s["status"] for s in flow.store.group_statuses(g["id"])] == ["created", "running", "succeeded"]
+    finally:
+        flow.shutdown()
+
+
+def test_hyperband_group_promotions(tmp_path):
+    flow = _flow(tmp_path, n_gpus=1)
+    try:
+        hb = {"hyperband": {"max_iter": 3, "eta": 3, "resource": {"name": "steps", "type": "int"},
+                            "metric": {"name": "loss", "optimization": "minimize"}, "resume": True}, "seed": 1}
+        spec = _group(hb, {"lr": {"values": [0.1, 0.2, 0.3, 0.4, 0.5]}}, _trial_cmd(), concurrency=3)
+        g = flow.submit(spec)
+        assert flow.wait("group", g["id"], timeout=120) == "succeeded"
+        its = flow.store.iterations(g["id"])
+        # max_iter=3, eta=3: s_max=1; bracket 1: 3 configs -> keep 1; bracket 0: 2 configs -> keep int(2/3)=0... +1
+        seq = [(i["data"]["iteration"], i["data"]["bracket_iteration"]) for i in its]
+        assert seq[0] == (0, 0) and (0, 1) in seq and (1, 0) in seq
+        promoted = [x for x in flow.store.list_experiments(group_id=g["id"]) if x["cloning_strategy"] == "resume"]
+        assert promoted and all(x["declarations"]["steps"] == 3 for x in promoted)
+        orig = flow.store.get_experiment(promoted[0]["original_experiment_id"])
+        assert promoted[0]["outputs_path"] == orig["outputs_path"]  # RESUME reuses the outputs
+    finally:
+        flow.shutdown()
+
+
+def test_random_group_early_stopping(tmp_path):
+    flow = _flow(tmp_path, n_gpus=1)
+    try:
+        spec = _group({"random_search": {"n_experiments": 6}, "seed": 2,
+                       "early_stopping": [{"metric": "loss", "value": 10.0, "optimization": "minimize"}]},
+                      {"lr": {"uniform": [0.0, 1.0]}}, _trial_cmd(), concurrency=1)
+        g = flow.submit(spec)
+        assert flow.wait("group", g["id"], timeout=60) in ("stopped", "succeeded")
+        xps = flow.store.list_experiments(group_id=g["id"])
+        assert len(xps) == 6
+        assert sum(x["status"] == "succeeded" for x in xps) == 1
+        assert sum(x["status"] == "stopped" for x in xps) == 5
+    finally:
+        flow.shutdown()
+
+
+def test_bo_and_asha_groups(tmp_path):
+    flow = _flow(tmp_path, n_gpus=1)
+    try:
+        bo = {"bo": {"n_iterations": 2, "n_initial_trials": 3, "metric": {"name": "loss", "optimization": "minimize"},
+                     "utility_function": {"acquisition_function": "ucb", "kappa": 1.0,
+                                          "gaussian_process": {"kernel": "matern", "nu": 2.5}}}, "seed": 3}
+        g = flow.submit(_group(bo, {"lr": {"uniform": [0.0, 1.0]}}, _trial_cmd(), concurrency=3))
+        assert flow.wait("group", g["id"], timeout=120) == "succeeded"
+        assert len(flow.store.list_experiments(group_id=g["id"])) == 3 + 2
+        asha = {"asha": {"min_resource": 1, "max_resource": 9, "eta": 3, "n_experiments": 6,
+                         "resource": {"name": "steps", "type": "int"},
+                         "metric": {"name": "loss", "optimization": "minimize"}}, "seed": 4}
+        g2 = flow.submit(_group(asha, {"lr": {"uniform": [0.0, 1.0]}}, _trial_cmd(), concurrency=2))
+        assert flow.wait("group", g2["id"], timeout=120) == "succeeded"
+        xps = flow.store.list_experiments(group_id=g2["id"])
+        assert len([x for x in xps if x["declarations"]["steps"] == 1]) == 6
+        assert any(x["declarations"]["steps"] == 3 for x in xps)
+    finally:
+        flow.shutdown()
+
+
+def test_clone_strategies(tmp_path):
+    flow = _flow(tmp_path)
+    try:
+        r = flow.submit(_xp("echo hi > $POLYAXON_RUN_OUTPUTS_PATH/ckpt.txt"))
+        assert flow.wait("experiment", r["id"], timeout=30) == "succeeded"
+        orig = flow.store.get_experiment(r["id"])
+        res = flow.clone_experiment(r["id"], "resume")
+        cp = flow.clone_experiment(r["id"], "copy")
+        rs = flow.clone_experiment(r["id"], "restart", declarations={"lr": 1})
+        for x in (res, cp, rs):
+            flow.wait("experiment", x, timeout=30)
+        assert flow.store.get_experiment(res)["outputs_path"] == orig["outputs_path"]
+        cpx = flow.store.get_experiment(cp)
+        assert cpx["outputs_path"] != orig["outputs_path"] and os.path.exists(os.path.join(cpx["outputs_path"], "ckpt.txt"))
+        assert flow.store.get_experiment(rs)["declarations"]["lr"] == 1
+        assert flow.store.get_experiment(rs)["original_experiment_id"] == r["id"]
+    finally:
+        flow.shutdown()
+
+
+def test_trial_to_trial_gap_is_small(tmp_path):
+    flow = _flow(tmp_path, n_gpus=1)
+    try:
+        g = flow.submit(_group({}, {"i": {"range": [0, 8, 1]}}, "true", concurrency=1))
+        assert flow.wait("group", g["id"], timeout=60) == "succeeded"
+        gaps = flow.stats["gaps_ms"]
+        assert len(gaps) >= 7
+        assert sorted(gaps)[len(gaps) // 2] < 100.0  # SURVEY.md §7.3 acceptance: < 100 ms
+    finally:
+        flow.shutdown()
+
+
+def test_jobs_and_builds(tmp_path):
+    flow = _flow(tmp_path)
+    try:
+        j = flow.submit({"version": 1, "kind": "job", "run": {"cmd": "echo job-ran"}})
+        assert flow.wait("job", j["id"], timeout=30) == "succeeded"
+        assert "job-ran" in flow.logs("job", j["id"])
+        spec = _xp("test -n \"$PLX_BUILD_DIR\" && cat $PLX_BUILD_DIR/marker")
+        spec["build"] = {"image": "rocm/pytorch", "build_steps": ["echo built > $PLX_BUILD_DIR/marker"]}
+        x1 = flow.submit(spec)
+        assert flow.wait("experiment", x1["id"], timeout=30) == "succeeded"
+        x2 = flow.submit(spec)
+        assert flow.wait("experiment", x2["id"], timeout=30) == "succeeded"
+        builds = flow.store.list_jobs(kind="build")
+        assert len(builds) == 1  # second experiment reused the build (6 h window)
+        assert "built" in flow.logs("experiment", x2["id"])
+    finally:
+        flow.shutdown()
