@@ -5,3 +5,4 @@ from polyaxon_amd.spec.specification import (BuildSpecification, ExperimentSpeci
                                              GroupSpecification, JobSpecification, Kinds, NotebookSpecification,
                                              PipelineSpecification, PolyaxonfileError, TensorboardSpecification,
                                              specification_for, validate)
+from polyaxon_amd.spec.specification import read_raw as read_raw_spec  # noqa: F401,E402

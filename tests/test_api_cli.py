@@ -1,0 +1,131 @@
+"""REST API (FastAPI TestClient, real scheduler underneath) and the plx CLI in local mode."""
+import json
+import os
+import sys
+
+import pytest
+
+from polyaxon_amd.polyflow.devices import Device, DeviceAllocator
+from polyaxon_amd.polyflow.scheduler import Polyflow
+
+TOKEN = "t0ken"
+
+
+@pytest.fixture
+def api(tmp_path):
+    from fastapi.testclient import TestClient
+
+    from polyaxon_amd.api.server import create_app
+
+    flow = Polyflow(str(tmp_path / "plx"), allocator=DeviceAllocator([Device(0), Device(1)])).start()
+    client = TestClient(create_app(flow, admin_token=TOKEN))
+    client.headers["Authorization"] = f"token {TOKEN}"
+    yield client, flow
+    flow.shutdown()
+
+
+def test_auth_required(api):
+    client, _ = api
+    r = client.get("/api/v1/projects", headers={"Authorization": "token wrong"})
+    assert r.status_code == 401
+    assert client.get("/_health").json() == {"status": "ok"}
+
+
+def test_experiment_lifecycle_over_rest(api):
+    client, flow = api
+    assert client.post("/api/v1/projects", json={"name": "mnist"}).status_code == 201
+    content = {"version": 1, "kind": "experiment", "declarations": {"lr": 0.1},
+               "run": {"cmd": "echo lr={{ lr }}"}}
+    r = client.post("/api/v1/root/mnist/experiments", json={"content": content})
+    assert r.status_code == 201, r.text
+    xid = r.json()["id"]
+    assert flow.wait("experiment", xid, timeout=30) == "succeeded"
+    x = client.get(f"/api/v1/root/mnist/experiments/{xid}").json()
+    assert x["status"] == "succeeded" and x["declarations"] == {"lr": 0.1}
+    assert "master.0 -- lr=0.1" in client.get(f"/api/v1/root/mnist/experiments/{xid}/logs").text
+    sts = client.get(f"/api/v1/root/mnist/experiments/{xid}/statuses").json()
+    assert [s["status"] for s in sts["results"]][-1] == "succeeded"
+    # metrics: single + batch, then query/sort through the list endpoint
+    assert client.post(f"/api/v1/root/mnist/experiments/{xid}/metrics", json={"values": {"loss": 0.5}}).status_code == 201
+    client.post(f"/api/v1/root/mnist/experiments/{xid}/metrics",
+                json=[{"values": {"loss": 0.3}, "step": 2}, {"values": {"acc": 0.9}, "step": 2}])
+    assert client.get(f"/api/v1/root/mnist/experiments/{xid}").json()["last_metric"] == {"loss": 0.3, "acc": 0.9}
+    lst = client.get("/api/v1/root/mnist/experiments", params={"query": "metric.loss:<0.4", "sort": "-created_at"})
+    assert [e["id"] for e in lst.json()["results"]] == [xid]
+    assert client.get("/api/v1/root/mnist/experiments", params={"query": "bogus:1"}).status_code == 400
+    # clone
+    r = client.post(f"/api/v1/root/mnist/experiments/{xid}/restart", json={"declarations": {"lr": 0.2}})
+    assert r.status_code == 201 and r.json()["original_experiment_id"] == xid
+    assert flow.wait("experiment", r.json()["id"], timeout=30) == "succeeded"
+    # update / bookmark / outputs / jobs
+    assert client.patch(f"/api/v1/root/mnist/experiments/{xid}", json={"tags": ["best"]}).json()["tags"] == ["best"]
+    assert client.post(f"/api/v1/root/mnist/experiments/{xid}/bookmark").json()["bookmarked"]
+    assert client.get(f"/api/v1/root/mnist/experiments/{xid}/outputs").status_code == 200
+    assert client.get(f"/api/v1/root/mnist/experiments/{xid}/jobs").json()["count"] == 1
+    assert client.get(f"/api/v1/root/mnist/experiments/999").status_code == 404
+    acts = client.get("/api/v1/activitylogs").json()
+    assert any(a["event_type"] == "experiment.created" for a in acts["results"])
+
+
+def test_ephemeral_token_exchange(api):
+    client, flow = api
+    r = client.post("/api/v1/root/p/experiments", json={"content": {"version": 1, "kind": "experiment",
+                                                                     "run": {"cmd": "true"}}})
+    xid = r.json()["id"]
+    eph = client.post(f"/api/v1/root/p/experiments/{xid}/ephemeraltoken").json()["token"]
+    r2 = client.post(f"/api/v1/root/p/experiments/{xid}/token", headers={"Authorization": f"token {eph}"})
+    assert r2.status_code == 200 and r2.json()["token"] == TOKEN
+    r3 = client.post(f"/api/v1/root/p/experiments/{xid + 1}/token", headers={"Authorization": f"token {eph}"})
+    assert r3.status_code in (403, 404)
+
+
+def test_group_over_rest_and_status(api):
+    client, flow = api
+    content = {"version": 1, "kind": "group",
+               "hptuning": {"concurrency": 2, "matrix": {"x": {"values": [1, 2, 3]}}},
+               "run": {"cmd": "echo {{ x }}"}}
+    r = client.post("/api/v1/root/g/groups", json={"content": content})
+    assert r.status_code == 201
+    gid = r.json()["id"]
+    assert flow.wait("group", gid, timeout=30) == "succeeded"
+    g = client.get(f"/api/v1/root/g/groups/{gid}").json()
+    assert g["num_experiments"] == 3 and g["status_counts"] == {"succeeded": 3}
+    assert client.get(f"/api/v1/root/g/groups/{gid}/experiments", params={"sort": "-id"}).json()["count"] == 3
+    st = client.get("/_status").json()
+    assert st["checks"]["store"]["status"] == "ok" and st["checks"]["scheduler"]["status"] == "ok"
+    assert client.post("/api/v1/root/g/groups", json={"content": {"version": 1, "kind": "group"}}).status_code == 400
+
+
+def test_sse_log_stream(api):
+    client, flow = api
+    r = client.post("/api/v1/root/s/experiments",
+                    json={"content": {"version": 1, "kind": "experiment", "run": {"cmd": "echo a; echo b"}}})
+    xid = r.json()["id"]
+    flow.wait("experiment", xid, timeout=30)
+    with client.stream("GET", f"/streams/v1/root/s/experiments/{xid}/logs") as s:
+        body = "".join(s.iter_text())
+    assert "data: master.0 -- a" in body and "event: done" in body
+
+
+def test_cli_local_mode(tmp_path, monkeypatch):
+    from click.testing import CliRunner
+
+    from polyaxon_amd.cli.main import cli
+
+    monkeypatch.setenv("PLX_ROOT", str(tmp_path / "root"))
+    monkeypatch.setenv("PLX_CONFIG", str(tmp_path / "cfg.yaml"))
+    monkeypatch.delenv("PLX_HOST", raising=False)
+    f = tmp_path / "xp.yml"
+    f.write_text("version: 1\nkind: experiment\ndeclarations: {lr: 0.3}\nrun: {cmd: 'echo lr={{ lr }}'}\n")
+    runner = CliRunner()
+    r = runner.invoke(cli, ["check", "-f", str(f)])
+    assert r.exit_code == 0 and "valid experiment" in r.output
+    r = runner.invoke(cli, ["-p", "demo", "run", "-f", str(f), "--gpus", "1"])
+    assert r.exit_code == 0, r.output
+    assert "succeeded" in r.output and "lr=0.3" in r.output
+    r = runner.invoke(cli, ["-p", "demo", "--json", "project", "experiments"])
+    assert json.loads(r.output)[0]["status"] == "succeeded"
+    r = runner.invoke(cli, ["-p", "demo", "experiment", "-xp", "1", "logs"])
+    assert "master.0 -- lr=0.3" in r.output
+    r = runner.invoke(cli, ["-p", "demo", "experiment", "-xp", "1", "statuses"])
+    assert "succeeded" in r.output

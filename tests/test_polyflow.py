@@ -256,3 +256,38 @@ def test_jobs_and_builds(tmp_path):
         assert "built" in flow.logs("experiment", x2["id"])
     finally:
         flow.shutdown()
+
+
+def test_pipeline_dag_triggers_and_retries(tmp_path):
+    from polyaxon_amd.polyflow.pipelines import sort_topologically, trigger_satisfied
+
+    assert sort_topologically({"a": {"b", "c"}, "b": {"d"}, "c": {"d"}, "d": set()}) == ["a", "b", "c", "d"]
+    with pytest.raises(ValueError):
+        sort_topologically({"a": {"b"}, "b": {"a"}})
+    assert trigger_satisfied("all_succeeded", ["succeeded", "running"]) is None
+    assert trigger_satisfied("all_succeeded", ["succeeded", "failed"]) is False
+    assert trigger_satisfied("one_failed", ["failed", "running"]) is True
+    assert trigger_satisfied("all_done", ["failed", "stopped"]) is True
+
+    flow = _flow(tmp_path)
+    try:
+        counter = tmp_path / "count"
+        flaky = f"n=$(cat {counter} 2>/dev/null || echo 0); echo $((n+1)) > {counter}; test $n -ge 1"
+        job = lambda cmd: {"version": 1, "kind": "job", "run": {"cmd": cmd}}  # noqa: E731
+        spec = {"version": 1, "kind": "pipeline", "concurrency": 2, "ops": [
+            {"name": "prep", "template": job("true")},
+            {"name": "flaky", "upstream": ["prep"], "max_retries": 2, "retry_delay": 0.05,
+             "template": job(flaky)},
+            {"name": "never", "upstream": ["prep"], "template": job("exit 1")},
+            {"name": "after_fail", "upstream": ["never"], "trigger": "all_succeeded", "template": job("true")},
+            {"name": "cleanup", "upstream": ["flaky", "never"], "trigger": "all_done", "template": job("true")}]}
+        r = flow.submit(spec)
+        assert flow.wait("pipeline_run", r["run_id"], timeout=60) == "finished"
+        ops = {o["name"]: o for o in flow.store.operation_runs(r["run_id"])}
+        assert ops["prep"]["status"] == "succeeded"
+        assert ops["flaky"]["status"] == "succeeded" and ops["flaky"]["retries"] == 1
+        assert ops["never"]["status"] == "failed"
+        assert ops["after_fail"]["status"] == "upstream_failed"
+        assert ops["cleanup"]["status"] == "succeeded"
+    finally:
+        flow.shutdown()
