@@ -1,0 +1,219 @@
+"""Decoder-only transformers for the BASELINE.json language-model configs:
+
+* GPT-2 125M — the Bayesian-GP search config (``gpt2_125m``: 12 layers, d=768, 12 heads, LayerNorm,
+  GELU MLP, learned positions, tied embeddings, vocab 50257, context 1024);
+* Llama-3 8B — the distributed PyTorchJob-equivalent config (``llama3_8b``: 32 layers, d=4096, 32 query /
+  8 KV heads (GQA), RMSNorm, SwiGLU 14336, RoPE theta 500000, vocab 128256).
+
+MI355X layout choices: bf16 autocast compute with fp32 master weights in a flat buffer (ops/flat.py) so
+the optimizer is one fused kernel; attention through ``scaled_dot_product_attention`` (the ROCm flash
+path); QKV and gate/up projections are single fused GEMMs (one hipBLASLt call instead of 3 / 2);
+RMSNorm in fp32 accumulate; optional activation checkpointing per block for long contexts.
+The reference ships no models: these exist so the framework's HPO and distributed paths
+can be exercised on the named configs with random weights and synthetic tokens.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.utils.checkpoint import checkpoint
+
+
+@dataclass
+class TransformerConfig:
+    vocab_size: int = 50257
+    n_layers: int = 12
+    d_model: int = 768
+    n_heads: int = 12
+    n_kv_heads: Optional[int] = None
+    d_ff: int = 3072
+    max_seq_len: int = 1024
+    norm: str = "layernorm"       # layernorm | rmsnorm
+    mlp: str = "gelu"             # gelu | swiglu
+    pos: str = "learned"          # learned | rope
+    rope_theta: float = 10000.0
+    tie_embeddings: bool = True
+    norm_eps: float = 1e-5
+    bias: bool = True
+    checkpoint: bool = False
+
+    @property
+    def kv_heads(self) -> int:
+        return self.n_kv_heads or self.n_heads
+
+    @property
+    def head_dim(self) -> int:
+        return self.d_model // self.n_heads
+
+
+def gpt2_125m(**kw) -> TransformerConfig:
+    return TransformerConfig(**kw)
+
+
+def llama3_8b(**kw) -> TransformerConfig:
+    base = dict(vocab_size=128256, n_layers=32, d_model=4096, n_heads=32, n_kv_heads=8, d_ff=14336,
+                max_seq_len=8192, norm="rmsnorm", mlp="swiglu", pos="rope", rope_theta=500000.0,
+                tie_embeddings=False, bias=False)
+    base.update(kw)
+    return TransformerConfig(**base)
+
+
+def tiny_llama(**kw) -> TransformerConfig:
+    base = dict(vocab_size=256, n_layers=2, d_model=64, n_heads=4, n_kv_heads=2, d_ff=128, max_seq_len=64,
+                norm="rmsnorm", mlp="swiglu", pos="rope", tie_embeddings=False, bias=False)
+    base.update(kw)
+    return TransformerConfig(**base)
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, d: int, eps: float = 1e-5):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(d))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        from polyaxon_amd.ops import rmsnorm as _rms
+
+        return _rms.rms_norm(x, self.weight, self.eps)
+
+
+def rope_cache(seq_len: int, head_dim: int, theta: float, device, dtype=torch.float32):
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, device=device, dtype=torch.float32) / head_dim))
+    t = torch.arange(seq_len, device=device, dtype=torch.float32)
+    freqs = torch.outer(t, inv)
+    return freqs.cos().to(dtype), freqs.sin().to(dtype)
+
+
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    # x: [B, H, S, D]; rotate pairs (even, odd) interleaved as two halves (Llama convention)
+    d = x.shape[-1] // 2
+    x1, x2 = x[..., :d], x[..., d:]
+    c, s = cos[None, None, : x.shape[2]], sin[None, None, : x.shape[2]]
+    return torch.cat([x1 * c - x2 * s, x1 * s + x2 * c], dim=-1)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: TransformerConfig):
+        super().__init__()
+        self.cfg = cfg
+        hd = cfg.head_dim
+        self.qkv = nn.Linear(cfg.d_model, (cfg.n_heads + 2 * cfg.kv_heads) * hd, bias=cfg.bias)
+        self.proj = nn.Linear(cfg.n_heads * hd, cfg.d_model, bias=cfg.bias)
+
+    def forward(self, x, rope=None):
+        B, S, _ = x.shape
+        cfg = self.cfg
+        hd = cfg.head_dim
+        qkv = self.qkv(x)
+        q, k, v = qkv.split([cfg.n_heads * hd, cfg.kv_heads * hd, cfg.kv_heads * hd], dim=-1)
+        q = q.view(B, S, cfg.n_heads, hd).transpose(1, 2)
+        k = k.view(B, S, cfg.kv_heads, hd).transpose(1, 2)
+        v = v.view(B, S, cfg.kv_heads, hd).transpose(1, 2)
+        if rope is not None:
+            q, k = apply_rope(q, *rope), apply_rope(k, *rope)
+        if cfg.kv_heads != cfg.n_heads:
+            rep = cfg.n_heads // cfg.kv_heads
+            k = k.repeat_interleave(rep, dim=1)
+            v = v.repeat_interleave(rep, dim=1)
+        y = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        return self.proj(y.transpose(1, 2).reshape(B, S, cfg.n_heads * hd))
+
+
+class MLP(nn.Module):
+    def __init__(self, cfg: TransformerConfig):
+        super().__init__()
+        self.kind = cfg.mlp
+        if cfg.mlp == "swiglu":
+            self.up = nn.Linear(cfg.d_model, 2 * cfg.d_ff, bias=cfg.bias)  # fused gate|up GEMM
+        else:
+            self.up = nn.Linear(cfg.d_model, cfg.d_ff, bias=cfg.bias)
+        self.down = nn.Linear(cfg.d_ff, cfg.d_model, bias=cfg.bias)
+
+    def forward(self, x):
+        h = self.up(x)
+        if self.kind == "swiglu":
+            g, u = h.chunk(2, dim=-1)
+            h = F.silu(g) * u
+        else:
+            h = F.gelu(h, approximate="tanh")
+        return self.down(h)
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: TransformerConfig):
+        super().__init__()
+        Norm = (lambda d: RMSNorm(d, cfg.norm_eps)) if cfg.norm == "rmsnorm" else (
+            lambda d: nn.LayerNorm(d, eps=cfg.norm_eps))
+        self.n1, self.n2 = Norm(cfg.d_model), Norm(cfg.d_model)
+        self.attn, self.mlp = Attention(cfg), MLP(cfg)
+
+    def forward(self, x, rope=None):
+        x = x + self.attn(self.n1(x), rope)
+        return x + self.mlp(self.n2(x))
+
+
+class Transformer(nn.Module):
+    def __init__(self, cfg: TransformerConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.embed = nn.Embedding(cfg.vocab_size, cfg.d_model)
+        self.pos = nn.Embedding(cfg.max_seq_len, cfg.d_model) if cfg.pos == "learned" else None
+        self.blocks = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layers)])
+        self.norm = RMSNorm(cfg.d_model, cfg.norm_eps) if cfg.norm == "rmsnorm" else nn.LayerNorm(cfg.d_model)
+        self.head = None if cfg.tie_embeddings else nn.Linear(cfg.d_model, cfg.vocab_size, bias=False)
+        self._rope = None
+        self.reset_parameters()
+
+    def init_spec(self):
+        """(param, kind, scale) for the fused in-place re-initialiser (GPT-2 / Llama conventions)."""
+        spec = []
+        resid_scale = 0.02 / math.sqrt(2 * self.cfg.n_layers)
+        for name, p in self.named_parameters():
+            if p.dim() == 1:
+                spec.append((p, "const", 0.0 if name.endswith("bias") else 1.0))
+            elif name.endswith("proj.weight") or name.endswith("down.weight"):
+                spec.append((p, "normal", resid_scale))
+            else:
+                spec.append((p, "normal", 0.02))
+        return spec
+
+    @torch.no_grad()
+    def reset_parameters(self):
+        for p, kind, scale in self.init_spec():
+            if kind == "normal":
+                p.normal_(0.0, scale)
+            else:
+                p.fill_(scale)
+
+    def forward(self, tokens: torch.Tensor) -> torch.Tensor:
+        B, S = tokens.shape
+        x = self.embed(tokens)
+        rope = None
+        if self.pos is not None:
+            x = x + self.pos(torch.arange(S, device=tokens.device))[None]
+        else:
+            if self._rope is None or self._rope[0].shape[0] < S or self._rope[0].device != tokens.device:
+                self._rope = rope_cache(max(S, 16), self.cfg.head_dim, self.cfg.rope_theta, tokens.device)
+            rope = (self._rope[0][:S].to(x.dtype if x.dtype != torch.float32 else torch.float32),
+                    self._rope[1][:S].to(x.dtype if x.dtype != torch.float32 else torch.float32))
+        for blk in self.blocks:
+            if self.cfg.checkpoint and self.training:
+                x = checkpoint(blk, x, rope, use_reentrant=False)
+            else:
+                x = blk(x, rope)
+        x = self.norm(x)
+        w = self.embed.weight if self.head is None else self.head.weight
+        return F.linear(x, w)
+
+    def num_params(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+
+def lm_loss(logits: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
+    """Next-token cross entropy (targets = tokens shifted left)."""
+    return F.cross_entropy(logits[:, :-1].reshape(-1, logits.shape[-1]).float(), tokens[:, 1:].reshape(-1))

@@ -30,6 +30,7 @@ LIBRARIES: Dict[str, dict] = {
     "plx_bn": {"sources": ["bn_kernels.hip"], "kind": "hip", "link": []},
     "plx_procmon": {"sources": ["procmon.cpp"], "kind": "cpp", "link": ["-lpthread"]},
     "plx_gp": {"sources": ["gp_kernels.hip"], "kind": "hip", "link": []},
+    "plx_rms": {"sources": ["rmsnorm.hip"], "kind": "hip", "link": []},
 }
 
 _lock = threading.Lock()
@@ -165,6 +166,11 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gp_chol": [_P, _I, _I, _P, _P],
         "plx_gp_predict_acq": [_P, _I, _P, _I, _I, _P, _I, _P, _I, _F, _F, _F, _F, _I, _F, _F, _F, _P, _P, _P, _P,
                                _P, _P],
+    },
+    "plx_rms": {
+        "plx_rms_forward": [_P, _P, _P, _P, _L, _I, _F, _P],
+        "plx_rms_bwd_blocks": [_L],
+        "plx_rms_backward": [_P, _P, _P, _P, _P, _P, _L, _I, _P],
     },
     "plx_polytune": {
         "plx_topk_brackets": [_P, _P, _I, _I, _I, _I, _P, _P],

@@ -1,0 +1,245 @@
+"""Trial entry points for the BASELINE.json configs (run under polyflow; read hyper-parameters from
+POLYAXON_DECLARATIONS / CLI flags, report metrics through the tracking client).
+
+    python -m polyaxon_amd.trainers mlp     --lr 0.01 --bs 256 --steps 200          (config 2)
+    python -m polyaxon_amd.trainers resnet  --lr 0.1 --steps 80                     (config 3, process mode)
+    python -m polyaxon_amd.trainers lm --model gpt2_125m --steps 50                  (config 4, DP=N ranks)
+    python -m polyaxon_amd.trainers lm --model llama3_8b --seq 2048 --bs 1           (config 5, DP=8)
+
+Every trainer: flat fp32 master weights + fused HIP optimizer, bf16 autocast, synthetic data of the real
+shape, metrics streamed from the GPU (tracking client MetricStream), DP through FlatDDP (RCCL) when
+WORLD_SIZE > 1, rank 0 reports.  ``--ckpt`` saves/loads ``model.pt`` under POLYAXON_RUN_OUTPUTS_PATH so
+Hyperband RESUME promotions continue training.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def _declared(args: argparse.Namespace) -> argparse.Namespace:
+    decl = json.loads(os.environ.get("POLYAXON_DECLARATIONS", "{}") or "{}")
+    for k, v in decl.items():
+        k = k.replace("-", "_")
+        if hasattr(args, k) and getattr(args, k) == args._defaults.get(k):
+            setattr(args, k, type(args._defaults[k])(v) if args._defaults.get(k) is not None else v)
+    return args
+
+
+def _parser(name: str) -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog=f"polyaxon_amd.trainers {name}")
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--weight_decay", type=float, default=0.0)
+    ap.add_argument("--momentum", type=float, default=0.9)
+    ap.add_argument("--bs", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--log_every", type=int, default=10)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--ckpt", action="store_true")
+    ap.add_argument("--cpu", action="store_true")
+    return ap
+
+
+def _parse(ap: argparse.ArgumentParser, argv):
+    args = ap.parse_args(argv)
+    args._defaults = {a.dest: a.default for a in ap._actions}
+    return _declared(args)
+
+
+def _device(args):
+    if args.cpu or not torch.cuda.is_available() or os.environ.get("PLX_CPU_ONLY") == "1":
+        return torch.device("cpu")
+    return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) if torch.cuda.device_count() > 1 else 0)
+
+
+def _tracker():
+    from polyaxon_amd.client import Experiment
+
+    return Experiment() if (os.environ.get("POLYAXON_EXPERIMENT_ID") or os.environ.get("POLYAXON_STORE_PATH")) \
+        else None
+
+
+def _ckpt_path():
+    out = os.environ.get("POLYAXON_RUN_OUTPUTS_PATH")
+    return os.path.join(out, "model.pt") if out else None
+
+
+# ------------------------------------------------------------------ config 2: 2-layer MLP
+class MLP(nn.Module):
+    def __init__(self, d_in=784, hidden=1024, classes=10):
+        super().__init__()
+        self.fc1 = nn.Linear(d_in, hidden)
+        self.fc2 = nn.Linear(hidden, classes)
+
+    def forward(self, x):
+        return self.fc2(F.relu(self.fc1(x)))
+
+    def init_spec(self):
+        return [(self.fc1.weight, "uniform", 1 / math.sqrt(self.fc1.in_features)),
+                (self.fc1.bias, "const", 0.0),
+                (self.fc2.weight, "uniform", 1 / math.sqrt(self.fc2.in_features)),
+                (self.fc2.bias, "const", 0.0)]
+
+
+def train_mlp(argv=None) -> float:
+    """Grid-search lr x bs over a 2-layer MLP; the whole step is a replayed hipGraph (launch-bound model)."""
+    from polyaxon_amd.polyflow.executor import ResidentTrialExecutor
+
+    args = _parse(_parser("mlp"), argv)
+    dev = _device(args)
+    g = torch.Generator().manual_seed(args.seed)
+    x = torch.randn(args.bs, 784, generator=g)
+    w_true = torch.randn(784, 10, generator=g)
+    y = (x @ w_true).argmax(1)
+    ex = ResidentTrialExecutor(MLP(), (x, y), dev, optimizer="sgd", use_graph=dev.type == "cuda",
+                               channels_last=False)
+    ex.capture(warmup=2)
+    ex.reset(seed=args.seed)
+    ex.set_hparams(lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay)
+    xp = _tracker()
+    steps_done = 0
+    while steps_done < args.steps:
+        n = min(args.log_every, args.steps - steps_done)
+        ex.run(n)
+        steps_done += n
+        if xp is not None:  # GPU tensor -> pinned side-stream copy, no sync on the training stream
+            xp.log_metrics(step=steps_done, loss=ex.ring[(int(steps_done) - 1) % ex.ring_size])
+    loss = float(ex.losses()[-1])
+    if xp is not None:
+        xp.log_metrics(step=steps_done, loss=loss)
+        xp.close()
+    print(json.dumps({"loss": loss, "steps": steps_done}))
+    return loss
+
+
+# ------------------------------------------------------------------ config 3 (process mode): ResNet-50 trial
+def train_resnet(argv=None) -> float:
+    from polyaxon_amd.models.resnet import resnet50
+    from polyaxon_amd.polyflow.executor import ResidentTrialExecutor
+
+    ap = _parser("resnet")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--units", type=int, default=1)
+    ap.add_argument("--unit_steps", type=int, default=8)
+    args = _parse(ap, argv)
+    dev = _device(args)
+    g = torch.Generator().manual_seed(args.seed)
+    x = torch.randn(args.bs, 3, args.image, args.image, generator=g).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (args.bs,), generator=g)
+    ex = ResidentTrialExecutor(resnet50(), (x, y), dev, use_graph=False)
+    ckpt = _ckpt_path() if args.ckpt else None
+    done_units = 0
+    ex.reset(seed=args.seed)
+    if ckpt and os.path.exists(ckpt):  # Hyperband RESUME: continue from the previous rung
+        st = torch.load(ckpt, map_location=dev, weights_only=True)
+        ex.flat.params.copy_(st["params"])
+        ex.opt.momentum_buf.copy_(st["momentum"])
+        ex.buffers.copy_(st["buffers"])
+        ex.step.fill_(int(st["step"]))
+        done_units = int(st["units"])
+    ex.set_hparams(lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay)
+    ex.run(max(0, args.units - done_units) * args.unit_steps)
+    out = torch.full((1,), float("nan"), device=dev)
+    ex.commit(out, 0, window=4)
+    loss = float(out[0])
+    if ckpt:
+        torch.save({"params": ex.flat.params, "momentum": ex.opt.momentum_buf, "buffers": ex.buffers,
+                    "step": int(ex.step.item()), "units": args.units}, ckpt)
+    xp = _tracker()
+    if xp is not None:
+        xp.log_metrics(step=int(ex.step.item()), loss=loss)
+        xp.close()
+    print(json.dumps({"loss": loss, "units": args.units}))
+    return loss
+
+
+# ------------------------------------------------------------------ configs 4 & 5: language models, DP over RCCL
+def train_lm(argv=None) -> float:
+    from polyaxon_amd.models.transformer import Transformer, gpt2_125m, llama3_8b, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.ops.optim import FusedAdamW
+    from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
+
+    ap = _parser("lm")
+    ap.add_argument("--model", default="gpt2_125m", choices=["gpt2_125m", "llama3_8b", "tiny"])
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--warmup_steps", type=int, default=0)
+    ap.add_argument("--bucket_mb", type=float, default=64.0)
+    ap.add_argument("--checkpoint_activations", action="store_true")
+    ap.add_argument("--beta2", type=float, default=0.95)
+    args = _parse(ap, argv)
+    backend = "gloo" if args.cpu or not torch.cuda.is_available() else "nccl"
+    info = init_from_env(backend)
+    dev = info["device"]
+    cfg = {"gpt2_125m": gpt2_125m, "llama3_8b": llama3_8b, "tiny": tiny_llama}[args.model](
+        checkpoint=args.checkpoint_activations)
+    seq = min(args.seq, cfg.max_seq_len)
+    torch.manual_seed(args.seed)
+    model = Transformer(cfg) if dev.type == "cpu" else _build_on_device(Transformer, cfg, dev)
+    flat = FlatParams(model, dev, channels_last=False)
+    step = torch.zeros(1, dtype=torch.int32, device=dev)
+    opt = FusedAdamW(flat, lr=args.lr, betas=(0.9, args.beta2), weight_decay=args.weight_decay, step_counter=step)
+    ddp = FlatDDP(flat, bucket_mb=args.bucket_mb)
+    ddp.broadcast_params()
+    g = torch.Generator(device="cpu").manual_seed(args.seed + 1000 * info["rank"])
+    tokens = torch.randint(0, cfg.vocab_size, (args.bs, seq), generator=g).to(dev)
+    xp = _tracker() if info["rank"] == 0 else None
+    amp = dev.type == "cuda"
+    t0 = time.time()
+    loss_val = float("nan")
+    for it in range(args.steps):
+        lr = args.lr * min(1.0, (it + 1) / args.warmup_steps) if args.warmup_steps else args.lr
+        opt.set_hparams(lr=lr)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            loss = lm_loss(model(tokens), tokens)
+        loss.backward()
+        ddp.finish()
+        opt.step_()
+        step += 1
+        if xp is not None and (it + 1) % args.log_every == 0:
+            xp.log_metrics(step=it + 1, loss=loss.detach())
+        if it == args.steps - 1:
+            loss_val = float(loss.detach())
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    dt = time.time() - t0
+    tok_s = args.steps * args.bs * seq * info["world"] / dt
+    if xp is not None:
+        xp.log_metrics(step=args.steps, loss=loss_val, tokens_per_s=tok_s)
+        xp.close()
+    if info["rank"] == 0:
+        print(json.dumps({"loss": loss_val, "tokens_per_s": round(tok_s, 1), "world": info["world"],
+                          "params_m": round(sum(s.numel for s in flat.segments) / 1e6, 1)}))
+    if info["world"] > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+    return loss_val
+
+
+def _build_on_device(cls, cfg, dev):
+    with torch.device(dev):
+        return cls(cfg)
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv:
+        print(__doc__)
+        return 2
+    which, rest = argv[0], argv[1:]
+    {"mlp": train_mlp, "resnet": train_resnet, "lm": train_lm}[which](rest)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
