@@ -31,6 +31,7 @@ LIBRARIES: Dict[str, dict] = {
     "plx_procmon": {"sources": ["procmon.cpp"], "kind": "cpp", "link": ["-lpthread"]},
     "plx_gp": {"sources": ["gp_kernels.hip"], "kind": "hip", "link": []},
     "plx_rms": {"sources": ["rmsnorm.hip"], "kind": "hip", "link": []},
+    "plx_rccl": {"sources": ["rccl_comm.cpp"], "kind": "hip_host", "link": ["-lrccl"]},
 }
 
 _lock = threading.Lock()
@@ -172,6 +173,17 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_rms_bwd_blocks": [_L],
         "plx_rms_backward": [_P, _P, _P, _P, _P, _P, _L, _I, _P],
     },
+    "plx_rccl": {
+        "plx_rccl_unique_id": [ctypes.c_char_p],
+        "plx_rccl_init": [ctypes.c_char_p, _I, _I, _I, ctypes.POINTER(_I)],
+        "plx_rccl_all_reduce": [_P, _P, _P, _L, _I, _I, _P],
+        "plx_rccl_all_gather": [_P, _P, _P, _L, _I, _P],
+        "plx_rccl_reduce_scatter": [_P, _P, _P, _L, _I, _I, _P],
+        "plx_rccl_broadcast": [_P, _P, _P, _L, _I, _I, _P],
+        "plx_rccl_bus_bw": [_P, _P, _L, _I, _P, ctypes.POINTER(_D), ctypes.POINTER(_D)],
+        "plx_rccl_destroy": [_P],
+        "plx_rccl_error": [_I],
+    },
     "plx_polytune": {
         "plx_topk_brackets": [_P, _P, _I, _I, _I, _I, _P, _P],
         "plx_early_stop_any": [_P, _I, _I, _P, _P, _P, _I, _P, _P],
@@ -180,7 +192,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 
 
 RESTYPES: Dict[str, object] = {"plx_bn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
-                               "plx_pm_wake": None}
+                               "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 
 def _declare(name: str, handle: ctypes.CDLL) -> None:
