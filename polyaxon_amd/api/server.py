@@ -262,6 +262,14 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
         ok = store.set_experiment_status(xid, body["status"], body.get("message"), body.get("traceback"))
         return {"accepted": ok, "status": store.get_experiment(xid)["status"]}
 
+    @app.post("/api/v1/{username}/{project}/experiments/{xid}/heartbeat")
+    def experiment_heartbeat(username: str, project: str, xid: int, user=Depends(auth)):
+        """Liveness from the tracking client (deadline: environment.heartbeat_timeout)."""
+        xp_or_404(username, project, xid)
+        now = time.time()
+        store.kv_set(f"heartbeat:experiment:{xid}", now)
+        return {"heartbeat": now}
+
     @app.get("/api/v1/{username}/{project}/experiments/{xid}/metrics")
     def experiment_metrics(username: str, project: str, xid: int, request: Request, user=Depends(auth)):
         xp_or_404(username, project, xid)
@@ -467,6 +475,31 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
                            if j["status"] not in ("succeeded", "failed", "stopped") and flow.stop_job(j["id"])]
                 return {"stopped": stopped}
         make_plugin()
+
+    # ------------------------------------------------------------------ repos (polyaxon upload)
+    @app.post("/api/v1/{username}/{project}/repo/upload")
+    async def repo_upload(username: str, project: str, request: Request, user=Depends(auth)):
+        from polyaxon_amd.polyflow.repos import ProjectRepo
+
+        store.get_or_create_project(project, username)
+        data = await request.body()
+        try:
+            sha = ProjectRepo(flow.paths.repos_root, username, project).upload_tarball(data)
+        except Exception as e:
+            raise HTTPException(400, f"invalid archive: {e}")
+        flow.auditor.record("repo.new_commit", "project", store.get_project(project, username)["id"], commit=sha)
+        return {"commit": sha, "path": ProjectRepo(flow.paths.repos_root, username, project).path}
+
+    @app.get("/api/v1/{username}/{project}/repo/download")
+    def repo_download(username: str, project: str, user=Depends(auth)):
+        from fastapi.responses import Response
+
+        from polyaxon_amd.polyflow.repos import ProjectRepo
+
+        repo = ProjectRepo(flow.paths.repos_root, username, project)
+        if not repo.last_commit:
+            raise HTTPException(404, "no repo uploaded")
+        return Response(repo.archive(), media_type="application/gzip")
 
     # ------------------------------------------------------------------ pipelines
     @app.get("/api/v1/{username}/{project}/pipelines/{pid}/runs/{rid}")

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import json
 import os
+import signal
 import threading
 import time
 import urllib.request
@@ -108,6 +109,9 @@ class _StoreBackend:
     def status(self, xid: int, status: str, message: Optional[str] = None):
         self.store.set_experiment_status(xid, status, message)
 
+    def heartbeat(self, xid: int):
+        self.store.kv_set(f"heartbeat:experiment:{xid}", time.time())
+
 
 class _HttpBackend:
     def __init__(self, host: str, token: Optional[str], project: str, user: str):
@@ -132,6 +136,9 @@ class _HttpBackend:
 
     def status(self, xid: int, status: str, message: Optional[str] = None):
         self._req("POST", f"/experiments/{xid}/statuses", {"status": status, "message": message})
+
+    def heartbeat(self, xid: int):
+        self._req("POST", f"/experiments/{xid}/heartbeat", {})
 
 
 class MetricStream:
@@ -213,6 +220,19 @@ class MetricStream:
         self.flush(force=True)
 
 
+def _step_fault() -> Optional[int]:
+    """Step of a ``POLYFLOW_FAULT=kill_rank:R@step:N`` targeting this replica on its first attempt."""
+    text = os.environ.get("POLYFLOW_FAULT")
+    if not text or os.environ.get("POLYAXON_RESTART_COUNT", "0") != "0":
+        return None
+    from polyaxon_amd.polyflow.faults import parse_fault
+
+    f = parse_fault(text)
+    if f is None or f["at"] != "step" or int(os.environ.get("RANK", "0")) != f["rank"]:
+        return None
+    return int(f["value"])
+
+
 class Experiment:
     """Tracking handle (reference ``polyaxon_client.tracking.Experiment``)."""
 
@@ -240,6 +260,8 @@ class Experiment:
                                         self.project or "default", user)
         self._stream = MetricStream(self.backend, self.experiment_id) if (self.backend and async_metrics) else None
         self._done = False
+        self._last_beat = 0.0
+        self._fault = _step_fault()
 
     # ------------------------------------------------------------------ properties
     @property
@@ -262,9 +284,23 @@ class Experiment:
         return get_outputs_refs_paths()
 
     # ------------------------------------------------------------------ logging
+    def heartbeat(self, force: bool = True) -> None:
+        """Liveness signal read by the scheduler's ``environment.heartbeat_timeout`` deadline."""
+        now = time.time()
+        if self.backend is None or (not force and now - self._last_beat < 1.0):
+            return
+        self._last_beat = now
+        try:
+            self.backend.heartbeat(self.experiment_id)
+        except Exception:  # a missed beat must never kill the trial
+            pass
+
     def log_metrics(self, step: Optional[int] = None, **metrics) -> None:
+        if self._fault is not None and step is not None and step >= self._fault:
+            os.kill(os.getpid(), signal.SIGKILL)  # POLYFLOW_FAULT=kill_rank:R@step:N (tests only)
         if self.backend is None:
             return
+        self.heartbeat(force=False)
         if self._stream is not None:
             self._stream.put(metrics, step)
         else:

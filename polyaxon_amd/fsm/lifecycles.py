@@ -97,7 +97,7 @@ JobLifeCycle = Lifecycle(
     done=(S.FAILED, S.STOPPED, S.SUCCEEDED), failed=(S.FAILED,))
 
 _XP_VALUES = (S.CREATED, S.RESUMING, S.BUILDING, S.SCHEDULED, S.STARTING, S.RUNNING, S.SUCCEEDED, S.FAILED,
-              S.STOPPED, S.UNKNOWN)
+              S.STOPPED, S.UNKNOWN, S.RETRYING)
 
 
 class _ExperimentLifecycle(Lifecycle):
@@ -127,15 +127,17 @@ ExperimentLifeCycle = _ExperimentLifecycle(
         S.CREATED: [None],
         S.RESUMING: [S.SUCCEEDED, S.STOPPED],
         S.BUILDING: [S.CREATED, S.RESUMING],
-        S.SCHEDULED: [S.CREATED, S.RESUMING, S.BUILDING],
+        S.SCHEDULED: [S.CREATED, S.RESUMING, S.BUILDING, S.RETRYING],
         S.STARTING: [S.SCHEDULED],
+        # opt-in retry (environment.max_restarts, an MI355X extension; the reference never retries)
+        S.RETRYING: [S.SCHEDULED, S.STARTING, S.RUNNING],
         S.RUNNING: [S.SCHEDULED, S.STARTING, S.UNKNOWN],
         S.SUCCEEDED: [S.SCHEDULED, S.STARTING, S.RUNNING, S.UNKNOWN],
-        S.FAILED: [S.CREATED, S.RESUMING, S.BUILDING, S.SCHEDULED, S.STARTING, S.RUNNING, S.UNKNOWN],
+        S.FAILED: [S.CREATED, S.RESUMING, S.BUILDING, S.SCHEDULED, S.STARTING, S.RUNNING, S.UNKNOWN, S.RETRYING],
         S.STOPPED: _all_but(_XP_VALUES, S.STOPPED),
         S.UNKNOWN: set(_XP_VALUES),
     },
-    pending=(S.CREATED, S.RESUMING), running=(S.SCHEDULED, S.BUILDING, S.STARTING, S.RUNNING),
+    pending=(S.CREATED, S.RESUMING), running=(S.SCHEDULED, S.BUILDING, S.STARTING, S.RUNNING, S.RETRYING),
     done=(S.FAILED, S.STOPPED, S.SUCCEEDED), failed=(S.FAILED,))
 
 _GROUP_VALUES = (S.CREATED, S.RUNNING, S.SUCCEEDED, S.FAILED, S.STOPPED)

@@ -39,6 +39,7 @@ from polyaxon_amd.obs.events import Auditor
 from polyaxon_amd.polyflow.devices import DeviceAllocator
 from polyaxon_amd.polyflow.env import cluster_def as make_cluster_def
 from polyaxon_amd.polyflow.env import free_port, trial_env
+from polyaxon_amd.polyflow.faults import parse_fault
 from polyaxon_amd.polyflow.paths import Paths
 from polyaxon_amd.polyflow.process import ProcessMonitor
 from polyaxon_amd.spec import specification_for
@@ -80,6 +81,7 @@ class Run:
     port: Optional[int] = None
     extra_env: Dict[str, str] = field(default_factory=dict)
     on_done: List[Callable[[str], None]] = field(default_factory=list)
+    attempt: int = 0  # opt-in retries (environment.max_restarts)
 
     @property
     def owner(self) -> str:
@@ -113,7 +115,8 @@ class Polyflow:
 
     def __init__(self, root: str, store: Optional[Store] = None, allocator: Optional[DeviceAllocator] = None,
                  auditor: Optional[Auditor] = None, api_host: Optional[str] = None, stop_grace_s: float = 10.0,
-                 python: Optional[str] = None):
+                 python: Optional[str] = None, reconcile_s: float = 5.0,
+                 health_check: Optional[Callable[[], List[int]]] = None):
         self.paths = Paths(root)
         self.store_path = os.path.join(self.paths.root, "polyaxon.sqlite")
         self.store = store or Store(self.store_path)
@@ -136,8 +139,11 @@ class Polyflow:
         self._thread: Optional[threading.Thread] = None
         self._running = False
         self._idle = threading.Event()
-        self.stats = {"spawned": 0, "exited": 0, "gaps_ms": []}
+        self.stats = {"spawned": 0, "exited": 0, "gaps_ms": [], "retries": 0, "heartbeat_kills": 0,
+                      "faults_injected": 0}
         self._last_exit_t: Optional[float] = None
+        self.reconcile_s = reconcile_s
+        self.health_check = health_check  # () -> indices of unhealthy devices (amd-smi RAS/ECC watchdog)
 
     # ================================================================== lifecycle of the scheduler itself
     def start(self) -> "Polyflow":
@@ -145,6 +151,8 @@ class Polyflow:
             self._running = True
             self._thread = threading.Thread(target=self._loop, name="polyflow", daemon=True)
             self._thread.start()
+            if self.reconcile_s > 0:
+                self.after(self.reconcile_s, self._reconcile)
             self.store.upsert_node("local", os.uname().nodename, float(os.cpu_count() or 1), 0.0, self.alloc.n_devices)
         return self
 
@@ -237,8 +245,25 @@ class Polyflow:
         spec = content if isinstance(content, BaseSpecification) else specification_for(content)
         return self.call(self._submit, spec, project, user, cwd or os.getcwd(), name, description)
 
+    def _code_ref(self, cwd: str) -> Optional[int]:
+        """One CodeReference per (submission dir, commit); reused by every trial of a group."""
+        from polyaxon_amd.polyflow.repos import code_reference
+
+        ref = code_reference(cwd)
+        if ref is None:
+            return None
+        key = f"coderef:{cwd}:{ref['commit']}:{hash(ref['diff'] or '')}"
+        cached = self.store.kv_get(key)
+        if cached:
+            return int(cached)
+        rid = self.store.create_code_reference(ref["commit"], ref["branch"], ref["git_url"], ref["is_dirty"],
+                                               ref["diff"])
+        self.store.kv_set(key, rid)
+        return rid
+
     def _submit(self, spec: BaseSpecification, project: str, user: str, cwd: str, name, description):
         proj = self.store.get_or_create_project(spec.project or project, user)
+        self._current_code_ref = self._code_ref(cwd)
         if spec.kind == Kinds.EXPERIMENT:
             xid = self._create_experiment(spec, proj, user, cwd, name=name, description=description)
             return {"kind": "experiment", "id": xid}
@@ -247,7 +272,8 @@ class Polyflow:
 
             gid = self.store.create_group(proj["id"], spec.raw_data, spec.hptuning.to_dict(), user=user,
                                           name=name or spec.name, description=description, tags=spec.tags,
-                                          search_algorithm=spec.search_algorithm, concurrency=spec.concurrency)
+                                          search_algorithm=spec.search_algorithm, concurrency=spec.concurrency,
+                                          code_reference_id=self._current_code_ref)
             self.auditor.record("experiment_group.created", "experiment_group", gid, user)
             driver = make_group_driver(self, gid, spec, proj, user, cwd)
             self.groups[gid] = driver
@@ -276,6 +302,7 @@ class Polyflow:
             proj["id"], spec.raw_data, group_id=group_id, user=user, name=name or spec.name, description=description,
             declarations=spec.declarations, tags=spec.tags, original_experiment_id=original_id,
             cloning_strategy=strategy, framework=spec.framework,
+            code_reference_id=self._group_code_ref(group_id),
             resources=spec.total_resources.to_dict() if spec.total_resources else None)
         root = self._clone_root(original_id, strategy)
         outputs = self.paths.experiment_outputs(user, proj["name"], root["id"] if root else xid,
@@ -295,6 +322,13 @@ class Polyflow:
         if enqueue:
             self._enqueue(run)
         return xid
+
+    def _group_code_ref(self, group_id: Optional[int]) -> Optional[int]:
+        if group_id:
+            g = self.store.get_group(group_id)
+            if g and g.get("code_reference_id"):
+                return g["code_reference_id"]
+        return getattr(self, "_current_code_ref", None)
 
     def _clone_root(self, original_id: Optional[int], strategy: Optional[str]) -> Optional[Dict]:
         """Resuming a resumed experiment resumes the root (reference db/models/experiments.py:261-269)."""
@@ -503,6 +537,7 @@ class Polyflow:
                             api_host=self.api_host, ephemeral_token=uuid.uuid4().hex, master_port=master_port,
                             local_rank=local_rank)
             env.update(run.extra_env)
+            env["POLYAXON_RESTART_COUNT"] = str(run.attempt)
             if spec.kind == Kinds.BUILD:
                 env["PLX_BUILD_DIR"] = rec["outputs_path"]
             if env.get("PLX_BUILD_DIR"):  # built environments install into <env>/site (pip --target)
@@ -539,6 +574,7 @@ class Polyflow:
                 self.store.set_job_status(jid, "running")
             local_rank += 1 if devs else 0
         run.started = time.time()
+        self._arm_fault(run)
         if run.kind == "experiment":
             self.store.set_experiment_status(run.id, "running")
             self.auditor.record("experiment.new_status", "experiment", run.id, status="running")
@@ -616,6 +652,8 @@ class Polyflow:
         if run.final_status is None:
             run.final_status = "stopped" if run.stop_requested else "succeeded"
         status = run.final_status
+        if status == "failed" and self._maybe_retry(run):
+            return
         if run.kind == "experiment":
             # remaining replicas that were stopped because the master finished count as succeeded
             self.store.set_experiment_status(run.id, status, run.final_message)
@@ -639,6 +677,80 @@ class Polyflow:
             gid = rec.get("group_id") if rec else None
             if gid in self.groups:
                 self.groups[gid].on_experiment_done(run.id, status)
+
+    # ================================================================== failure handling
+    def _max_restarts(self, run: Run) -> int:
+        env = getattr(run.spec, "environment", None)
+        return int(getattr(env, "max_restarts", 0) or 0) if run.kind == "experiment" else 0
+
+    def _maybe_retry(self, run: Run) -> bool:
+        """Opt-in retry: a failed experiment is re-queued whole (all replicas, fresh rendezvous port) up to
+        ``environment.max_restarts`` times; POLYAXON_RESTART_COUNT tells the trial which attempt it is."""
+        if run.attempt >= self._max_restarts(run):
+            return False
+        run.attempt += 1
+        self.stats["retries"] += 1
+        msg = f"retry {run.attempt}/{self._max_restarts(run)} after: {run.final_message}"
+        self.store.set_experiment_status(run.id, "retrying", msg)
+        self.auditor.record("experiment.new_status", "experiment", run.id, status="retrying")
+        run.replicas = []
+        run.stop_requested = False
+        run.stop_reason = None
+        run.final_status = None
+        run.final_message = None
+        run.started = None
+        self.pending.append(run.owner)
+        return True
+
+    def _arm_fault(self, run: Run) -> None:
+        """Fault injection for tests: ``POLYFLOW_FAULT=kill_rank:R@t:SECONDS`` SIGKILLs replica R of the
+        first attempt that long after spawn (``@step:N`` is handled by the tracking client inside the trial)."""
+        fault = run.extra_env.get("POLYFLOW_FAULT") or dict(
+            (str(k), str(v)) for k, v in (run.spec.environment.env_vars if run.spec.environment else [])
+        ).get("POLYFLOW_FAULT")
+        if not fault or run.attempt > 0:
+            return
+        spec = parse_fault(fault)
+        if spec is None or spec["at"] != "t":
+            return
+        replicas = list(run.replicas)
+
+        def fire():
+            if spec["rank"] < len(replicas):
+                r = replicas[spec["rank"]]
+                if r.pid is not None and not r.done:
+                    self.stats["faults_injected"] += 1
+                    self.pm.signal(r.pid, signal.SIGKILL, group=True)
+
+        self.after(spec["value"], fire)
+
+    def _reconcile(self) -> None:
+        """Periodic health pass (the reference's 30 s cron, crons/tasks/experiments.py:9-17, event-driven
+        here except for what cannot raise an event): heartbeat deadlines of hung trials and GPU health."""
+        try:
+            now = time.time()
+            for run in list(self.runs.values()):
+                if run.kind != "experiment" or not run.active or run.stop_requested or run.started is None:
+                    continue
+                env = run.spec.environment
+                timeout = getattr(env, "heartbeat_timeout", None) if env else None
+                if not timeout:
+                    continue
+                last = self.store.kv_get(f"heartbeat:experiment:{run.id}")
+                last = max(float(last), run.started) if last else run.started
+                if now - last > timeout:
+                    self.stats["heartbeat_kills"] += 1
+                    run.final_status = "failed"
+                    run.final_message = f"no heartbeat for {now - last:.1f}s (timeout {timeout}s)"
+                    self._stop_run(run, run.final_message)
+            if self.health_check is not None:
+                for idx in self.health_check() or []:
+                    self.alloc.mark_unhealthy(idx)
+        except Exception:
+            log.exception("reconcile failed")
+        finally:
+            if self._running and self.reconcile_s > 0:
+                self.after(self.reconcile_s, self._reconcile)
 
     # ================================================================== stopping
     def _stop_run(self, run: Run, reason: str) -> None:

@@ -23,6 +23,7 @@ from typing import Callable, Dict, List, Optional
 
 import torch
 
+from polyaxon_amd.obs.tracing import trace_range
 from polyaxon_amd.polytune.kernels import BracketMetrics
 from polyaxon_amd.polytune.managers import HyperbandIterationConfig, HyperbandSearchManager
 
@@ -76,6 +77,10 @@ class HyperbandSweep:
 
     def _run_trial(self, it: HyperbandIterationConfig, cid: int, params: Dict, slot: int,
                    prev_resource: Optional[float]) -> TrialRecord:
+        with trace_range(f"trial {self._trial} it{it.iteration}.{it.bracket_iteration} cfg{cid}"):
+            return self._run_trial_inner(it, cid, params, slot, prev_resource)
+
+    def _run_trial_inner(self, it, cid, params, slot, prev_resource) -> TrialRecord:
         r = params[self.resource_name]
         if self.resume and prev_resource is not None:
             self.ex.restore(cid)

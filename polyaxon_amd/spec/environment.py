@@ -184,6 +184,9 @@ class EnvironmentSpec:
     configmap_refs: List[str] = field(default_factory=list)
     env_vars: List[List[str]] = field(default_factory=list)
     framework: Optional[FrameworkSpec] = None
+    # MI355X extensions: opt-in trial retry and a heartbeat deadline for hung trials
+    max_restarts: int = 0
+    heartbeat_timeout: Optional[float] = None
 
     @classmethod
     def from_dict(cls, d: Optional[Dict[str, Any]]):
@@ -192,7 +195,7 @@ class EnvironmentSpec:
         if len(fws) > 1:
             raise MatrixValidationError(f"environment defines more than one framework: {fws}")
         known = {"resources", "outputs", "persistence", "node_selector", "tolerations", "affinity", "secret_refs",
-                 "configmap_refs", "env_vars", *FRAMEWORKS}
+                 "configmap_refs", "env_vars", "max_restarts", "heartbeat_timeout", *FRAMEWORKS}
         unknown = set(d) - known
         if unknown:
             raise MatrixValidationError(f"unknown environment keys {sorted(unknown)}")
@@ -205,7 +208,9 @@ class EnvironmentSpec:
                    tolerations=d.get("tolerations"), affinity=d.get("affinity"),
                    secret_refs=list(d.get("secret_refs") or []), configmap_refs=list(d.get("configmap_refs") or []),
                    env_vars=[list(e) for e in d.get("env_vars") or []],
-                   framework=FrameworkSpec.from_dict(fws[0], d[fws[0]]) if fws else None)
+                   framework=FrameworkSpec.from_dict(fws[0], d[fws[0]]) if fws else None,
+                   max_restarts=int(d.get("max_restarts") or 0),
+                   heartbeat_timeout=float(d["heartbeat_timeout"]) if d.get("heartbeat_timeout") else None)
 
     def to_dict(self):
         out: Dict[str, Any] = {}
@@ -219,4 +224,8 @@ class EnvironmentSpec:
                 out[k] = getattr(self, k)
         if self.framework:
             out[self.framework.framework] = self.framework.to_dict()
+        if self.max_restarts:
+            out["max_restarts"] = self.max_restarts
+        if self.heartbeat_timeout:
+            out["heartbeat_timeout"] = self.heartbeat_timeout
         return out

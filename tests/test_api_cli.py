@@ -129,3 +129,27 @@ def test_cli_local_mode(tmp_path, monkeypatch):
     assert "master.0 -- lr=0.3" in r.output
     r = runner.invoke(cli, ["-p", "demo", "experiment", "-xp", "1", "statuses"])
     assert "succeeded" in r.output
+
+
+def test_repo_upload_and_code_reference(api, tmp_path):
+    import io
+    import tarfile
+
+    client, flow = api
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w:gz") as tar:
+        data = b"print('hello from uploaded code')\n"
+        info = tarfile.TarInfo("train.py")
+        info.size = len(data)
+        tar.addfile(info, io.BytesIO(data))
+    r = client.post("/api/v1/root/up/repo/upload", content=buf.getvalue())
+    assert r.status_code == 200, r.text
+    sha, path = r.json()["commit"], r.json()["path"]
+    assert len(sha) == 40
+    content = {"version": 1, "kind": "experiment", "run": {"cmd": f"{sys.executable} train.py"}}
+    xid = client.post("/api/v1/root/up/experiments", json={"content": content, "cwd": path}).json()["id"]
+    assert flow.wait("experiment", xid, timeout=30) == "succeeded"
+    assert "hello from uploaded code" in client.get(f"/api/v1/root/up/experiments/{xid}/logs").text
+    ref = client.get(f"/api/v1/root/up/experiments/{xid}/coderef").json()
+    assert ref["commit_sha"] == sha and ref["is_dirty"] == 0
+    assert client.get("/api/v1/root/up/repo/download").status_code == 200
