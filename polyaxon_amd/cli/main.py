@@ -60,10 +60,10 @@ class Ctx:
         self._store = None
 
     # REST
-    def api(self, method: str, path: str, payload=None, raw: bool = False):
+    def api(self, method: str, path: str, payload=None, raw: bool = False, body: Optional[bytes] = None):
         url = self.host.rstrip("/") + path
-        data = json.dumps(payload).encode() if payload is not None else None
-        headers = {"Content-Type": "application/json"}
+        data = body if body is not None else (json.dumps(payload).encode() if payload is not None else None)
+        headers = {"Content-Type": "application/octet-stream" if body is not None else "application/json"}
         if self.cfg.get("token"):
             headers["Authorization"] = f"token {self.cfg['token']}"
         req = urllib.request.Request(url, data=data, method=method, headers=headers)
@@ -204,7 +204,7 @@ def check(c, files, definition):
 @click.option("--description", default=None)
 @click.option("-d", "--detach", is_flag=True, help="server mode: return immediately")
 @click.option("--gpus", type=int, default=None, help="local mode: number of HIP devices to manage")
-@click.option("-u", "--upload", is_flag=True, help="(accepted for compatibility; local code is used in place)")
+@click.option("-u", "--upload", is_flag=True, help="upload the current directory first and run that snapshot")
 @click.pass_obj
 def run(c, files, name, description, detach, gpus, upload):
     """Run an experiment, group, job, build or pipeline from polyaxonfile(s)."""
@@ -214,6 +214,7 @@ def run(c, files, name, description, detach, gpus, upload):
         content = read_raw_spec(list(files))
     except PolyaxonfileError as e:
         raise click.ClickException(str(e))
+    cwd = _upload(c)["path"] if upload else os.getcwd()
     if c.host:
         kind = content.get("kind")
         path = {"experiment": "experiments", "group": "groups", "job": "jobs", "build": "builds",
@@ -221,7 +222,7 @@ def run(c, files, name, description, detach, gpus, upload):
         if path is None:
             raise click.ClickException(f"cannot run kind {kind} remotely")
         res = c.api("POST", f"{c.base()}/{path}", {"content": content, "name": name, "description": description,
-                                                     "cwd": os.getcwd()})
+                                                     "cwd": cwd})
         click.echo(f"created {kind} {res.get('id')}")
         return
     from polyaxon_amd.polyflow.devices import Device, DeviceAllocator
@@ -230,7 +231,7 @@ def run(c, files, name, description, detach, gpus, upload):
     alloc = DeviceAllocator([Device(i) for i in range(gpus)]) if gpus is not None else None
     flow = Polyflow(os.path.expanduser(c.cfg["root"]), allocator=alloc).start()
     try:
-        res = flow.submit(content, project=c.project, user=c.user, name=name, description=description)
+        res = flow.submit(content, project=c.project, user=c.user, cwd=cwd, name=name, description=description)
         kind, rid = res["kind"], res["id"]
         click.echo(f"created {kind} {rid}; waiting (Ctrl-C to stop)")
         wait_kind = {"pipeline": "pipeline_run"}.get(kind, "group" if kind == "group" else
@@ -245,6 +246,53 @@ def run(c, files, name, description, detach, gpus, upload):
             click.echo(flow.logs("experiment", rid, tail=20))
     finally:
         flow.shutdown()
+
+
+def _tar_dir(path: str) -> bytes:
+    """Tarball of ``path`` minus .git/__pycache__ and the patterns in .polyaxonignore (reference CLI upload)."""
+    import fnmatch
+    import io
+    import tarfile
+
+    ignore = [".git", "__pycache__", "*.pyc", ".polyaxon"]
+    pi = os.path.join(path, ".polyaxonignore")
+    if os.path.exists(pi):
+        with open(pi) as f:
+            ignore += [ln.strip().rstrip("/") for ln in f if ln.strip() and not ln.startswith("#")]
+
+    def skip(rel: str) -> bool:
+        parts = rel.split(os.sep)
+        return any(fnmatch.fnmatch(rel, pat) or any(fnmatch.fnmatch(p, pat) for p in parts) for pat in ignore)
+
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w:gz") as tar:
+        for root, dirs, files in os.walk(path):
+            rel_root = os.path.relpath(root, path)
+            dirs[:] = sorted(d for d in dirs if not skip(os.path.normpath(os.path.join(rel_root, d))))
+            for fn in sorted(files):
+                rel = os.path.normpath(os.path.join(rel_root, fn))
+                if not skip(rel):
+                    tar.add(os.path.join(root, fn), arcname=rel, recursive=False)
+    return buf.getvalue()
+
+
+def _upload(c) -> Dict[str, Any]:
+    data = _tar_dir(os.getcwd())
+    if c.host:
+        return c.api("POST", f"{c.base()}/repo/upload", body=data)
+    from polyaxon_amd.polyflow.paths import Paths
+    from polyaxon_amd.polyflow.repos import ProjectRepo
+
+    repo = ProjectRepo(Paths(os.path.expanduser(c.cfg["root"])).repos_root, c.user, c.project)
+    return {"commit": repo.upload_tarball(data), "path": repo.path}
+
+
+@cli.command()
+@click.pass_obj
+def upload(c):
+    """Upload the current directory as the project's code (reference `polyaxon upload`)."""
+    res = _upload(c)
+    click.echo(f"uploaded {len(res['commit']) and res['commit'][:12]} -> {res['path']}")
 
 
 @cli.command()

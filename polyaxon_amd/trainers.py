@@ -196,7 +196,12 @@ def train_lm(argv=None) -> float:
     amp = dev.type == "cuda"
     t0 = time.time()
     loss_val = float("nan")
+    skip = 2 if args.steps > 4 else 0  # exclude allocator / kernel-selection warmup from tokens/s
     for it in range(args.steps):
+        if it == skip and skip:
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            t0 = time.time()
         lr = args.lr * min(1.0, (it + 1) / args.warmup_steps) if args.warmup_steps else args.lr
         opt.set_hparams(lr=lr)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
@@ -212,7 +217,7 @@ def train_lm(argv=None) -> float:
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     dt = time.time() - t0
-    tok_s = args.steps * args.bs * seq * info["world"] / dt
+    tok_s = (args.steps - skip) * args.bs * seq * info["world"] / dt
     if xp is not None:
         xp.log_metrics(step=args.steps, loss=loss_val, tokens_per_s=tok_s)
         xp.close()

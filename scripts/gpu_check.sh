@@ -13,6 +13,8 @@ echo "== build" && timeout -k 10 300 python __graft_entry__.py > gpurun_out/buil
 && echo "== bench" && timeout -k 10 900 python bench.py --steps $STEPS --warmup $WARM ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err \
 && cat gpurun_out/bench.json \
 && echo "== rocprof" && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 4 --warmup 1 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1 \
+&& echo "== gpt2" && timeout -k 10 600 python -m polyaxon_amd.trainers lm --model gpt2_125m --bs 16 --seq 1024 --steps 20 --log_every 100 > gpurun_out/gpt2.json 2> gpurun_out/gpt2.err \
+&& cat gpurun_out/gpt2.json \
 && echo "== done"
 rc=$?
 echo "exit $rc"

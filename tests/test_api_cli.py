@@ -153,3 +153,28 @@ def test_repo_upload_and_code_reference(api, tmp_path):
     ref = client.get(f"/api/v1/root/up/experiments/{xid}/coderef").json()
     assert ref["commit_sha"] == sha and ref["is_dirty"] == 0
     assert client.get("/api/v1/root/up/repo/download").status_code == 200
+
+
+def test_cli_upload_and_run_snapshot(tmp_path, monkeypatch):
+    from click.testing import CliRunner
+
+    from polyaxon_amd.cli.main import cli
+
+    monkeypatch.setenv("PLX_ROOT", str(tmp_path / "root"))
+    monkeypatch.setenv("PLX_CONFIG", str(tmp_path / "cfg.yaml"))
+    monkeypatch.delenv("PLX_HOST", raising=False)
+    code = tmp_path / "code"
+    code.mkdir()
+    (code / "train.py").write_text("print('snapshot v1')\n")
+    (code / "big.bin").write_text("x")
+    (code / ".polyaxonignore").write_text("*.bin\n")
+    (code / "xp.yml").write_text(f"version: 1\nkind: experiment\nrun: {{cmd: '{sys.executable} train.py'}}\n")
+    monkeypatch.chdir(code)
+    runner = CliRunner()
+    r = runner.invoke(cli, ["-p", "up", "upload"])
+    assert r.exit_code == 0 and "uploaded" in r.output, r.output
+    repo = tmp_path / "root" / "repos" / "root" / "up"
+    assert (repo / "train.py").exists() and not (repo / "big.bin").exists()
+    (code / "train.py").write_text("print('snapshot v2')\n")
+    r = runner.invoke(cli, ["-p", "up", "run", "-u", "-f", "xp.yml", "--gpus", "0"])
+    assert r.exit_code == 0 and "snapshot v2" in r.output, r.output
