@@ -65,6 +65,7 @@ def main() -> int:
     ap.add_argument("--target", type=float, default=2.0, help="loss target for wall-clock-to-target")
     ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph (slower for ResNet-50 on ROCm 7, see profiles/README.md)")
     ap.add_argument("--unfused", action="store_true", help="PyTorch BN/ReLU instead of the HIP kernels")
+    ap.add_argument("--miopen-1x1", action="store_true", help="MIOpen for the 1x1 convs instead of the MFMA GEMMs")
     ap.add_argument("--tune", action="store_true", help="exhaustive MIOpen find (cudnn.benchmark)")
     ap.add_argument("--verbose", action="store_true", help="print every trial's record to stderr")
     args = ap.parse_args()
@@ -88,7 +89,7 @@ def main() -> int:
     x = torch.randn(args.batch, 3, args.image, args.image, generator=gen).to(torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (args.batch,), generator=gen)
-    model = resnet50(fused=not args.unfused)
+    model = resnet50(fused=not args.unfused, native_conv=not args.miopen_1x1)
     ex = ResidentTrialExecutor(model, (x, y), dev, use_graph=args.graph)
 
     log("model built; capturing training step")
@@ -188,6 +189,7 @@ def main() -> int:
             "graph_capture_s": round(capture_s, 2),
             "hip_graph": ex.graph is not None,
             "fused_bn": not args.unfused,
+            "mfma_1x1_conv": not args.miopen_1x1,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

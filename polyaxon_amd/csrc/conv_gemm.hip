@@ -1,0 +1,407 @@
+// MFMA GEMMs for stride-1 1x1 convolutions on NHWC bf16 activations (ResNet-50 bottleneck conv1/conv3).
+//
+// On NHWC the three convolution passes are plain GEMMs over M = N*H*W pixel rows:
+//   forward      y[M][Cout]  = x[M][Cin]   . W[Cout][Cin]^T       -> plx_gemm_nt   (A = x,  B = W)
+//   data grad    dx[M][Cin]  = dy[M][Cout] . Wt[Cin][Cout]^T      -> plx_gemm_nt   (A = dy, B = W^T)
+//   weight grad  dW[Cout][Cin] = sum_m dy[m][Cout]^T x[m][Cin]    -> plx_gemm_tn   (split over m, fp32 out)
+// plx_gemm_nt needs both operands K-contiguous (row-major [rows][K]); plx_gemm_tn reads both operands
+// row-major over the reduction index m and feeds the MFMA through ds_read_b64_tr_b16 transposed LDS reads.
+//
+// Kernel structure (cdna_hip_programming.md §5): 256 threads = 4 waves, each wave owns a WT1 x WT2 output
+// sub-tile computed with v_mfma_f32_16x16x32_bf16; tiles are staged global -> LDS with 16-byte
+// global_load_lds (LDS image lane-linear, bank swizzle applied on the per-lane SOURCE address and on the
+// read, rule 21), double-buffered over BK = 64; blockIdx is remapped so blocks sharing an operand panel
+// run on one XCD (T1, bijective form).  Rows past the end of M read a zero page instead of being masked,
+// so partial tiles need no branches around the DMA.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_void;
+
+constexpr int BK = 64;          // reduction depth per LDS stage (bf16 elements)
+constexpr int NTHREADS = 256;   // 4 waves
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    // consecutive logical ids on one XCD (blocks are dealt round-robin over the 8 XCDs); bijective for any nwg
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + (bid >> 3);
+}
+
+__device__ __forceinline__ void glds16(const void* g, void* l) {
+    __builtin_amdgcn_global_load_lds((gbl_void*)g, (lds_void*)l, 16, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+    uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
+    ua += 0x7fffu + ((ua >> 16) & 1u);   // round to nearest even
+    ub += 0x7fffu + ((ub >> 16) & 1u);
+    return (ua >> 16) | (ub & 0xffff0000u);
+}
+
+// ------------------------------------------------------------------------------------------- NT GEMM
+// C[M][N] (bf16, ldc) = A[M][K] (lda) . B[N][K]^T (ldb).  N % BN == 0, K % 64 == 0 (host-checked).
+// LDS row = 64 bf16 = 128 B = 8 chunks of 16 B; physical chunk = logical ^ ((row >> 1) & 7), which puts the
+// 16 rows of a fragment read on 16 distinct bank slots.
+__device__ __forceinline__ int nt_swz(int row) { return (row >> 1) & 7; }
+
+template <int BM, int BN, int WGM, int WGN>
+__global__ void __launch_bounds__(NTHREADS, 2)
+gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
+               int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero) {
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
+    constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
+    constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ntn = N / BN, ntm = (M + BM - 1) / BM;
+    const int id = xcd_remap(blockIdx.x, ntm * ntn);
+    const int tn = id % ntn, tm = id / ntn;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int wm = wave / WGN, wn = wave % WGN;
+
+    // staging: each wave instruction moves 1024 B = 8 rows x 8 chunks; lane -> (row, physical chunk)
+    auto stage = [&](int buf, int k0) {
+        char* base = smem + buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < BM / 32; ++i) {                 // A: BM rows / 8 rows per instr / 4 waves
+            const int row = (i * 4 + wave) * 8 + (lane >> 3);
+            const int lc = (lane & 7) ^ nt_swz(row);
+            const int gm = m0 + row;
+            const __bf16* src = gm < M ? A + (size_t)gm * lda + k0 + lc * 8 : zero;
+            glds16(src, base + (i * 4 + wave) * 1024);
+        }
+#pragma unroll
+        for (int i = 0; i < BN / 32; ++i) {
+            const int row = (i * 4 + wave) * 8 + (lane >> 3);
+            const int lc = (lane & 7) ^ nt_swz(row);
+            glds16(B + (size_t)(n0 + row) * ldb + k0 + lc * 8, base + A_BYTES + (i * 4 + wave) * 1024);
+        }
+    };
+
+    f32x4 acc[RN][RM];
+#pragma unroll
+    for (int a = 0; a < RN; ++a)
+#pragma unroll
+        for (int b = 0; b < RM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BK;
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+        const char* As = smem + cur * STAGE;
+        const char* Bs = As + A_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {                    // two 32-deep MFMA steps per stage
+            bf16x8 fa[RN], fb[RM];
+#pragma unroll
+            for (int rn = 0; rn < RN; ++rn) {               // MFMA A operand = B rows (output channel n)
+                const int row = wn * WTN + rn * 16 + fr;
+                const int pc = (kk * 4 + fq) ^ nt_swz(row);
+                fa[rn] = *(const bf16x8*)(Bs + row * 128 + pc * 16);
+            }
+#pragma unroll
+            for (int rm = 0; rm < RM; ++rm) {               // MFMA B operand = A rows (pixel m)
+                const int row = wm * WTM + rm * 16 + fr;
+                const int pc = (kk * 4 + fq) ^ nt_swz(row);
+                fb[rm] = *(const bf16x8*)(As + row * 128 + pc * 16);
+            }
+#pragma unroll
+            for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+                for (int rm = 0; rm < RM; ++rm)
+                    acc[rn][rm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rn], fb[rm], acc[rn][rm], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    // D[n][m]: lane holds column m = fr, rows n = 4*fq + r -> 4 consecutive channels of one pixel (8 B store)
+#pragma unroll
+    for (int rm = 0; rm < RM; ++rm) {
+        const int gm = m0 + wm * WTM + rm * 16 + fr;
+        if (gm >= M) continue;
+#pragma unroll
+        for (int rn = 0; rn < RN; ++rn) {
+            const int gn = n0 + wn * WTN + rn * 16 + fq * 4;
+            const f32x4 v = acc[rn][rm];
+            uint2 packed;
+            packed.x = pack_bf16x2(v[0], v[1]);
+            packed.y = pack_bf16x2(v[2], v[3]);
+            *(uint2*)(C + (size_t)gm * ldc + gn) = packed;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------- TN GEMM
+// W[slice][N1][N2] (fp32 slab per m-slice, ld = N2) = sum_{m in slice} A[m][N1] (lda) * B[m][N2] (ldb).
+// The slabs are summed by slab_reduce_kernel (the guide's slab reducer).  The first version accumulated with
+// per-element fp32 atomics instead; on the 7x7 layers (16 slices into one 4 MB output) its weight gradient ran
+// at half the forward GEMM's rate.
+// LDS images are [BK rows = m][BNx cols] in natural row order; MFMA fragments come from ds_read_b64_tr_b16
+// (T10): lane 4q+p of a 16-lane group addresses row kb+q, columns c0+4p..4p+3 and receives column (lane&15)
+// of those 4 rows.  Physical 16-B chunk = logical ^ tr_swz(row) makes both 32-lane halves conflict-free.
+template <int ROWB>
+__device__ __forceinline__ int tr_swz(int row) {
+    if constexpr (ROWB >= 256) return 2 * ((row & 3) | (((row >> 3) & 1) << 2));
+    else return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
+}
+
+template <int ROWB>
+__device__ __forceinline__ s16x4 tr_read(const char* img, int row, int col /* element */) {
+    const int lc = col >> 3, half = (col >> 2) & 1;
+    const int pc = lc ^ tr_swz<ROWB>(row);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + row * ROWB + pc * 16 + half * 8));
+}
+
+template <int ROWB>
+__device__ __forceinline__ void stage_rows(char* img, const __bf16* __restrict__ G, int ld, int r0, int rend,
+                                           int c0, const __bf16* __restrict__ zero, int wave, int lane) {
+    // BK rows x ROWB bytes, lane-linear image; 1024 B per wave instruction
+    constexpr int INSTR = BK * ROWB / 1024;
+#pragma unroll
+    for (int i = 0; i < INSTR / 4; ++i) {
+        const int off = (i * 4 + wave) * 1024 + lane * 16;
+        const int row = off / ROWB, pc = (off % ROWB) >> 4;
+        const int lc = pc ^ tr_swz<ROWB>(row);
+        const int gr = r0 + row;
+        const __bf16* src = gr < rend ? G + (size_t)gr * ld + c0 + lc * 8 : zero;
+        glds16(src, img + (i * 4 + wave) * 1024);
+    }
+}
+
+template <int BN1, int BN2, int WG1, int WG2>
+__global__ void __launch_bounds__(NTHREADS, 2)
+gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float* __restrict__ W,
+               int M, int N1, int N2, int lda, int ldb, int kchunk, const __bf16* __restrict__ zero) {
+    constexpr int WT1 = BN1 / WG1, WT2 = BN2 / WG2, R1 = WT1 / 16, R2 = WT2 / 16;
+    constexpr int ROWA = BN1 * 2, ROWB_ = BN2 * 2;
+    constexpr int A_BYTES = BK * ROWA, STAGE = BK * (ROWA + ROWB_);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nt1 = N1 / BN1, nt2 = N2 / BN2, ntiles = nt1 * nt2;
+    const int nslices = (M + kchunk - 1) / kchunk;
+    const int id = xcd_remap(blockIdx.x, ntiles * nslices);
+    const int tile = id % ntiles, slice = id / ntiles;
+    const int t1 = tile / nt2, t2 = tile % nt2;
+    const int n10 = t1 * BN1, n20 = t2 * BN2;
+    const int kbeg = slice * kchunk, kend = min(M, kbeg + kchunk);
+    const int w1 = wave / WG2, w2 = wave % WG2;
+
+    f32x4 acc[R1][R2];
+#pragma unroll
+    for (int a = 0; a < R1; ++a)
+#pragma unroll
+        for (int b = 0; b < R2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = (kend - kbeg + BK - 1) / BK;
+    auto stage = [&](int buf, int k0) {
+        char* base = smem + buf * STAGE;
+        stage_rows<ROWA>(base, A, lda, k0, kend, n10, zero, wave, lane);
+        stage_rows<ROWB_>(base + A_BYTES, B, ldb, k0, kend, n20, zero, wave, lane);
+    };
+    if (nk > 0) {
+        stage(0, kbeg);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    const int gi = lane & 15, g = lane >> 4, q = gi >> 2, p = gi & 3;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) stage(cur ^ 1, kbeg + (kt + 1) * BK);
+        const char* As = smem + cur * STAGE;
+        const char* Bs = As + A_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int kb = kk * 32 + 8 * g + q;             // this lane's address row for the first tr read
+            bf16x8 fa[R1], fb[R2];
+#pragma unroll
+            for (int r = 0; r < R1; ++r) {
+                const int c = w1 * WT1 + r * 16 + 4 * p;
+                const s16x4 lo = tr_read<ROWA>(As, kb, c), hi = tr_read<ROWA>(As, kb + 4, c);
+                fa[r] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+#pragma unroll
+            for (int r = 0; r < R2; ++r) {
+                const int c = w2 * WT2 + r * 16 + 4 * p;
+                const s16x4 lo = tr_read<ROWB_>(Bs, kb, c), hi = tr_read<ROWB_>(Bs, kb + 4, c);
+                fb[r] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+#pragma unroll
+            for (int a = 0; a < R1; ++a)
+#pragma unroll
+                for (int b = 0; b < R2; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    // D[n1][n2]: lane holds column n2 = lane&15, rows n1 = 4*(lane>>4) + r
+    float* slab = W + (size_t)slice * N1 * N2;
+#pragma unroll
+    for (int a = 0; a < R1; ++a)
+#pragma unroll
+        for (int b = 0; b < R2; ++b) {
+            const int c2 = n20 + w2 * WT2 + b * 16 + gi;
+            const int r1 = n10 + w1 * WT1 + a * 16 + 4 * g;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) slab[(size_t)(r1 + r) * N2 + c2] = acc[a][b][r];
+        }
+}
+
+// C[i][j] (ldc) = (accumulate ? C : 0) + sum_s W[s][i][j]; one float4 per thread
+__global__ void slab_reduce_kernel(const float* __restrict__ W, float* __restrict__ C, int N1, int N2, int ldc,
+                                   int slices, int accumulate) {
+    const long total4 = (long)N1 * N2 / 4;
+    const long plane = (long)N1 * N2;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int s = 0; s < slices; ++s) {
+            const float4 v = ((const float4*)(W + s * plane))[i];
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+        const long e = i * 4;
+        const int r = (int)(e / N2), c = (int)(e % N2);
+        float4* dst = (float4*)(C + (size_t)r * ldc + c);
+        if (accumulate) {
+            const float4 o = *dst;
+            acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+        }
+        *dst = acc;
+    }
+}
+
+// fp32 W[Cout][Cin] -> bf16 W[Cout][Cin] and bf16 W^T[Cin][Cout] (both used by the 1x1 conv passes)
+__global__ void weight_prep_kernel(const float* __restrict__ w, __bf16* __restrict__ wb, __bf16* __restrict__ wt,
+                                   int cout, int cin) {
+    __shared__ float tile[32][33];
+    const int c0 = blockIdx.x * 32, o0 = blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 256 threads: 32 x 8
+    for (int j = ty; j < 32; j += 8) {
+        const int o = o0 + j, c = c0 + tx;
+        float v = (o < cout && c < cin) ? w[(size_t)o * cin + c] : 0.f;
+        tile[j][tx] = v;
+        if (o < cout && c < cin) wb[(size_t)o * cin + c] = (__bf16)v;
+    }
+    __syncthreads();
+    for (int j = ty; j < 32; j += 8) {
+        const int c = c0 + j, o = o0 + tx;
+        if (o < cout && c < cin) wt[(size_t)c * cout + o] = (__bf16)tile[tx][j];
+    }
+}
+
+template <typename KernelT>
+int set_lds(KernelT k, int bytes) {
+    return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess ? 0
+                                                                                                                 : -2;
+}
+
+template <int BM, int BN, int WGM, int WGN>
+int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+              const void* zero, hipStream_t s) {
+    constexpr int LDS = 2 * (BM + BN) * BK * 2;
+    auto k = gemm_nt_kernel<BM, BN, WGM, WGN>;
+    static int attr = set_lds(k, LDS);
+    if (attr) return attr;
+    const int nwg = ((M + BM - 1) / BM) * (N / BN);
+    hipLaunchKernelGGL(k, dim3(nwg), dim3(NTHREADS), LDS, s, (const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N,
+                       K, lda, ldb, ldc, (const __bf16*)zero);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// m-slicing of the weight-gradient GEMM: ~2 blocks per CU, >= 8 k-stages per block, slabs <= 16 MB
+struct TnPlan { int kchunk, slices; };
+
+inline void tn_tile(int N1, int N2, int& bn1, int& bn2) {
+    bn1 = N1 % 128 == 0 ? 128 : 64;
+    bn2 = N2 % 128 == 0 ? 128 : 64;
+}
+
+inline TnPlan tn_plan(int M, int N1, int N2, int num_cus) {
+    int bn1, bn2;
+    tn_tile(N1, N2, bn1, bn2);
+    const int ntiles = (N1 / bn1) * (N2 / bn2);
+    const long plane = (long)N1 * N2;
+    int slices = (2 * (num_cus > 0 ? num_cus : 256)) / ntiles;
+    const int by_depth = M / (8 * BK);
+    const int by_bytes = (int)((16l << 20) / (plane * 4));
+    if (slices > by_depth) slices = by_depth;
+    if (slices > by_bytes) slices = by_bytes;
+    if (slices < 1) slices = 1;
+    int kchunk = (M + slices - 1) / slices;
+    kchunk = ((kchunk + BK - 1) / BK) * BK;
+    return {kchunk, (M + kchunk - 1) / kchunk};
+}
+
+template <int BN1, int BN2, int WG1, int WG2>
+int launch_tn(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
+              const void* zero, hipStream_t s) {
+    constexpr int LDS = 2 * BK * (BN1 + BN2) * 2;
+    auto k = gemm_tn_kernel<BN1, BN2, WG1, WG2>;
+    static int attr = set_lds(k, LDS);
+    if (attr) return attr;
+    const int ntiles = (N1 / BN1) * (N2 / BN2);
+    hipLaunchKernelGGL(k, dim3(ntiles * plan.slices), dim3(NTHREADS), LDS, s, (const __bf16*)A, (const __bf16*)B, W,
+                       M, N1, N2, lda, ldb, plan.kchunk, (const __bf16*)zero);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace
+
+extern "C" {
+
+// tile selection: wide-N problems use 128x128, N == 64 uses 256x64 (pixels x channels)
+int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                const void* zero, void* stream) {
+    if (M <= 0 || N % 64 || K % BK || lda % 8 || ldb % 8 || ldc % 4) return -1;
+    hipStream_t s = (hipStream_t)stream;
+    if (N % 128 == 0) return launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, s);
+    return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, s);
+}
+
+// floats of slab workspace plx_gemm_tn needs for this problem
+long plx_gemm_tn_workspace(int M, int N1, int N2, int num_cus) {
+    if (M <= 0 || N1 % 64 || N2 % 64) return -1;
+    const TnPlan p = tn_plan(M, N1, N2, num_cus);
+    return (long)p.slices * N1 * N2;
+}
+
+// C[N1][N2] (ldc, fp32) = (accumulate ? C : 0) + A^T B over M rows; ws holds plx_gemm_tn_workspace floats
+int plx_gemm_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int N2, int lda, int ldb, int ldc,
+                const void* zero, int num_cus, int accumulate, void* stream) {
+    if (M <= 0 || N1 % 64 || N2 % 64 || lda % 8 || ldb % 8 || ldc % 4) return -1;
+    hipStream_t s = (hipStream_t)stream;
+    const TnPlan plan = tn_plan(M, N1, N2, num_cus);
+    int rc;
+    if (N1 % 128 == 0 && N2 % 128 == 0) rc = launch_tn<128, 128, 2, 2>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s);
+    else if (N1 % 128 == 0) rc = launch_tn<128, 64, 4, 1>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s);
+    else if (N2 % 128 == 0) rc = launch_tn<64, 128, 1, 4>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s);
+    else rc = launch_tn<64, 64, 2, 2>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s);
+    if (rc) return rc;
+    const long total4 = (long)N1 * N2 / 4;
+    int blocks = (int)((total4 + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, C, N1, N2, ldc, plan.slices, accumulate);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int plx_weight_prep(const float* w, void* wb, void* wt, int cout, int cin, void* stream) {
+    dim3 grid((cin + 31) / 32, (cout + 31) / 32);
+    hipLaunchKernelGGL(weight_prep_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, (__bf16*)wb, (__bf16*)wt, cout,
+                       cin);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // extern "C"

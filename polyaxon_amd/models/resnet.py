@@ -13,6 +13,7 @@ from typing import List, Optional, Type
 import torch
 import torch.nn as nn
 
+from polyaxon_amd.ops.conv1x1 import Conv1x1
 from polyaxon_amd.ops.norm import BatchNormAct
 
 
@@ -20,14 +21,15 @@ class Bottleneck(nn.Module):
     expansion = 4
 
     def __init__(self, in_ch: int, width: int, stride: int = 1, downsample: Optional[nn.Module] = None,
-                 fused: bool = True):
+                 fused: bool = True, native_conv: bool = True):
         super().__init__()
         out_ch = width * self.expansion
-        self.conv1 = nn.Conv2d(in_ch, width, 1, bias=False)
+        # stride-1 1x1 convs run as MFMA GEMMs on the NHWC rows (ops/conv1x1.py); the 3x3 stays on MIOpen
+        self.conv1 = Conv1x1(in_ch, width, native=native_conv)
         self.bn1 = BatchNormAct(width, act=True, fused=fused)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
         self.bn2 = BatchNormAct(width, act=True, fused=fused)
-        self.conv3 = nn.Conv2d(width, out_ch, 1, bias=False)
+        self.conv3 = Conv1x1(width, out_ch, native=native_conv)
         # bn3 fuses the residual add and the final ReLU: y = relu(bn(x) + identity)
         self.bn3 = BatchNormAct(out_ch, act=True, fused=fused, residual=True)
         self.downsample = downsample
@@ -51,7 +53,7 @@ class Downsample(nn.Module):
 
 class ResNet(nn.Module):
     def __init__(self, layers: List[int], num_classes: int = 1000, width: int = 64,
-                 zero_init_residual: bool = True, fused: bool = True):
+                 zero_init_residual: bool = True, fused: bool = True, native_conv: bool = True):
         super().__init__()
         self.stem = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
         self.stem_bn = BatchNormAct(width, act=True, fused=fused)
@@ -66,7 +68,7 @@ class ResNet(nn.Module):
                 ds = None
                 if j == 0 and (stride != 1 or in_ch != w * Bottleneck.expansion):
                     ds = Downsample(in_ch, w * Bottleneck.expansion, stride, fused=fused)
-                blocks.append(Bottleneck(in_ch, w, stride if j == 0 else 1, ds, fused=fused))
+                blocks.append(Bottleneck(in_ch, w, stride if j == 0 else 1, ds, fused=fused, native_conv=native_conv))
                 in_ch = w * Bottleneck.expansion
             stages.append(nn.Sequential(*blocks))
         self.stages = nn.Sequential(*stages)

@@ -31,6 +31,7 @@ LIBRARIES: Dict[str, dict] = {
     "plx_procmon": {"sources": ["procmon.cpp"], "kind": "cpp", "link": ["-lpthread"]},
     "plx_gp": {"sources": ["gp_kernels.hip"], "kind": "hip", "link": []},
     "plx_rms": {"sources": ["rmsnorm.hip"], "kind": "hip", "link": []},
+    "plx_conv": {"sources": ["conv_gemm.hip"], "kind": "hip", "link": []},
     "plx_rccl": {"sources": ["rccl_comm.cpp"], "kind": "hip_host", "link": ["-lrccl"]},
 }
 
@@ -168,6 +169,12 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gp_predict_acq": [_P, _I, _P, _I, _I, _P, _I, _P, _I, _F, _F, _F, _F, _I, _F, _F, _F, _P, _P, _P, _P,
                                _P, _P],
     },
+    "plx_conv": {
+        "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
+        "plx_gemm_tn_workspace": [_I, _I, _I, _I],
+        "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
+        "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
+    },
     "plx_rms": {
         "plx_rms_forward": [_P, _P, _P, _P, _L, _I, _F, _P],
         "plx_rms_bwd_blocks": [_L],
@@ -191,7 +198,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_bn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
+RESTYPES: Dict[str, object] = {"plx_bn_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

@@ -1,0 +1,73 @@
+"""Time the ResNet-50 1x1 convolutions: MIOpen (F.conv2d fwd+bwd) vs the plx MFMA GEMM op, per pass.
+
+Interleaved rounds in one process (guide §5.4 rule 24); random bf16 data; CUDA events."""
+import sys
+
+import torch
+import torch.nn.functional as F
+
+from polyaxon_amd.ops.conv1x1 import conv1x1, gemm_nt, gemm_tn, weight_prep
+
+dev = torch.device("cuda", 0)
+SHAPES = [(256, 64, 56, 56, 256), (256, 256, 56, 56, 64), (256, 64, 56, 56, 64), (256, 512, 28, 28, 128),
+          (256, 128, 28, 28, 512), (256, 1024, 14, 14, 256), (256, 256, 14, 14, 1024), (256, 2048, 7, 7, 512),
+          (256, 512, 7, 7, 2048)]
+
+
+def timeit(fn, it=10):
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it
+
+
+def main():
+    tot = {"miopen": 0.0, "plx": 0.0}
+    for n, cin, h, w, cout in SHAPES:
+        x = torch.randn(n, cin, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        wt32 = torch.randn(cout, cin, 1, 1, device=dev) * 0.05
+        g = torch.randn(n, cout, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        xm = x.clone().requires_grad_()
+        wm = wt32.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_()
+        xp = x.clone().requires_grad_()
+        wp = wt32.clone().requires_grad_()
+
+        def miopen():
+            xm.grad = None
+            wm.grad = None
+            F.conv2d(xm, wm).backward(g)
+
+        def plx():
+            xp.grad = None
+            wp.grad = None
+            conv1x1(xp, wp).backward(g)
+
+        m = n * h * w
+        xr = x.permute(0, 2, 3, 1).reshape(m, cin)
+        gr = g.permute(0, 2, 3, 1).reshape(m, cout)
+        wb, wtt = weight_prep(wt32)
+        parts = {"fwd": lambda: gemm_nt(xr, wb), "dgrad": lambda: gemm_nt(gr, wtt), "wgrad": lambda: gemm_tn(gr, xr)}
+        res = {"miopen": [], "plx": []}
+        for _ in range(3):
+            res["miopen"].append(timeit(miopen))
+            res["plx"].append(timeit(plx))
+        a, b = min(res["miopen"]), min(res["plx"])
+        tot["miopen"] += a
+        tot["plx"] += b
+        pt = {k: timeit(f) for k, f in parts.items()}
+        fl = 3 * 2 * m * cin * cout
+        byts = 2 * (2 * m * cin + 3 * m * cout)  # fwd: x r, y w; dgrad: dy r, dx w; wgrad: dy r, x r (+y rewritten)
+        # correctness spot check vs MIOpen result
+        torch.testing.assert_close(xp.grad.float(), xm.grad.float(), rtol=5e-2, atol=1.0)
+        print(f"{(n, cin, h, w, cout)}  miopen {a:.3f} ms  plx {b:.3f} ms  ({b / a:.2f}x)  "
+              f"plx {fl / b / 1e9:.0f} TF  parts " + " ".join(f"{k}={v:.3f}" for k, v in pt.items())
+              + f"  roofline~{byts / 6.3e9:.3f} ms", flush=True)
+    print(f"total miopen {tot['miopen']:.3f} ms  plx {tot['plx']:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,92 @@
+"""MFMA GEMM kernels for 1x1 convolutions (csrc/conv_gemm.hip) vs fp32 PyTorch references."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(*shape, dev):
+    return torch.randn(*shape, device=dev).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("m,n,k", [(1024, 128, 64), (1000, 256, 192), (777, 64, 128), (4096, 192, 256),
+                                   (300, 512, 1024), (64, 64, 64)])
+def test_gemm_nt(cuda, m, n, k):
+    from polyaxon_amd.ops.conv1x1 import gemm_nt
+
+    torch.manual_seed(0)
+    a, b = _bf(m, k, dev=cuda), _bf(n, k, dev=cuda)
+    out = gemm_nt(a, b)
+    ref = a.float() @ b.float().t()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2 * k ** 0.5)
+
+
+def test_gemm_nt_strided_rows(cuda):
+    from polyaxon_amd.ops.conv1x1 import gemm_nt
+
+    a = _bf(512, 320, dev=cuda)[:, 64:192]          # lda = 320, K = 128
+    b = _bf(128, 128, dev=cuda)
+    out = torch.zeros(512, 256, dtype=torch.bfloat16, device=cuda)
+    gemm_nt(a, b, out[:, 128:])                      # ldc = 256
+    torch.testing.assert_close(out[:, 128:].float(), a.float() @ b.float().t(), rtol=2e-2, atol=0.25)
+    assert out[:, :128].abs().max() == 0
+
+
+@pytest.mark.parametrize("m,n1,n2", [(1024, 128, 128), (1000, 256, 64), (777, 64, 256), (333, 64, 64),
+                                     (50000, 128, 128), (200, 512, 1024)])
+def test_gemm_tn(cuda, m, n1, n2):
+    from polyaxon_amd.ops.conv1x1 import gemm_tn
+
+    torch.manual_seed(1)
+    a, b = _bf(m, n1, dev=cuda), _bf(m, n2, dev=cuda)
+    out = gemm_tn(a, b)
+    ref = a.float().t() @ b.float()
+    torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-3 * m ** 0.5)
+
+
+def test_weight_prep(cuda):
+    from polyaxon_amd.ops.conv1x1 import weight_prep
+
+    w = torch.randn(192, 320, 1, 1, device=cuda)
+    wb, wt = weight_prep(w)
+    assert torch.equal(wb, w.view(192, 320).to(torch.bfloat16))
+    assert torch.equal(wt, w.view(192, 320).t().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("shape,cout", [((2, 64, 7, 9), 128), ((4, 256, 14, 14), 64), ((3, 128, 5, 5), 512)])
+def test_conv1x1_autograd(cuda, shape, cout):
+    from polyaxon_amd.ops.conv1x1 import Conv1x1, supported
+
+    torch.manual_seed(2)
+    conv = Conv1x1(shape[1], cout).to(cuda)
+    x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert supported(x, conv)
+    xa = x.clone().requires_grad_()
+    y = conv(xa)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.float().clone().requires_grad_()
+    wr = conv.weight.detach().clone().requires_grad_()
+    yr = F.conv2d(xr, wr.to(torch.bfloat16).float())
+    yr.backward(g.float())
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=5e-2)
+    torch.testing.assert_close(xa.grad.float(), xr.grad, rtol=2e-2, atol=5e-2)
+    assert conv.weight.grad.dtype == torch.float32
+    torch.testing.assert_close(conv.weight.grad, wr.grad, rtol=2e-2, atol=0.1)
+
+
+def test_conv1x1_in_autocast_graph(cuda):
+    """Inside autocast with an fp32 master weight, as the ResNet executor runs it."""
+    from polyaxon_amd.ops.conv1x1 import Conv1x1
+
+    conv = Conv1x1(64, 256).to(cuda).to(memory_format=torch.channels_last)
+    x = torch.randn(8, 64, 16, 16, device=cuda).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = conv(x)
+        loss = y.float().square().mean()
+    loss.backward()
+    ref = F.conv2d(x.to(torch.bfloat16), conv.weight.to(torch.bfloat16))
+    torch.testing.assert_close(y.float(), ref.float(), rtol=2e-2, atol=5e-2)
+    assert conv.weight.grad is not None and torch.isfinite(conv.weight.grad).all()
