@@ -151,7 +151,7 @@ __global__ void bn_fwd_finalize_kernel(const float* __restrict__ psum, const flo
   const double m = S / (double)M;
   double var = Q / (double)M - m * m;
   if (var < 0.0) var = 0.0;
-  const float mean = bf2f(x_row0[c]) + (float)m;
+  const float mean = (x_row0 != nullptr ? bf2f(x_row0[c]) : 0.f) + (float)m;  // no shift: producer-fused stats
   const float invstd = rsqrtf((float)var + eps);
   const float g = gamma[c];
   save_mean[c] = mean;
@@ -379,6 +379,33 @@ PLX_API int plx_bn_forward(const void* x, const void* res, void* y, int64_t M, i
                      l2, p.S);
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, l2, l2 + (int64_t)p.S * C, p.S,
                      (const uint16_t*)x, C, M, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
+                     save_invstd, scale_bias, scale_bias + C);
+  const int64_t n_vec = M * p.G;
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
+                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu);
+  return (int)hipGetLastError();
+}
+
+// Level-2 workspace for externally produced level-1 partials ([2][nblk][C], e.g. from the 1x1-conv GEMM
+// epilogue, csrc/conv_gemm.hip): 2 * ceil(nblk / 64) * C floats.
+PLX_API int64_t plx_bn_l2_workspace(int nblk, int C) {
+  return 2 * (int64_t)((nblk + kRowsPerSplit - 1) / kRowsPerSplit) * C;
+}
+
+// Forward with the per-channel sums already produced by the op that wrote x (unshifted sums over nblk row
+// blocks): skips the stats pass over x.  l2 holds plx_bn_l2_workspace(nblk, C) floats.
+PLX_API int plx_bn_forward_from_partials(const void* x, const void* res, void* y, int64_t M, int C,
+                                         const float* gamma, const float* beta, float eps, float momentum,
+                                         float* running_mean, float* running_var, float* save_mean,
+                                         float* save_invstd, float* scale_bias, const float* partials, int nblk,
+                                         float* l2, int relu, hipStream_t stream) {
+  Plan p;
+  if (!plan_for(M, C, &p) || M < 1 || nblk < 1) return 1;
+  const int S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
+  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, S, 2), dim3(256), 0, stream, partials, nblk, C, l2,
+                     S);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S,
+                     (const uint16_t*)nullptr, C, M, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
                      save_invstd, scale_bias, scale_bias + C);
   const int64_t n_vec = M * p.G;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,

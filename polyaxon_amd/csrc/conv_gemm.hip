@@ -54,7 +54,8 @@ __device__ __forceinline__ int nt_swz(int row) { return (row >> 1) & 7; }
 template <int BM, int BN, int WGM, int WGN>
 __global__ void __launch_bounds__(NTHREADS, 2)
 gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
-               int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero) {
+               int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
+               float* __restrict__ stats) {
     constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
     constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -126,19 +127,54 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    // D[n][m]: lane holds column m = fr, rows n = 4*fq + r -> 4 consecutive channels of one pixel (8 B store)
+    // Epilogue through LDS (the k-loop's last barrier freed it): D[n][m] has column m = fr and rows
+    // n = 4*fq + r in each lane, i.e. 4 consecutive channels of one pixel.  Stage the bf16 tile as [m][n] rows
+    // padded by 16 B, then store whole output rows with 16 B per lane (a wave instruction writes contiguous
+    // row segments instead of 32-B pieces of 16 different rows).
+    constexpr int CROW = BN * 2 + 16;
 #pragma unroll
     for (int rm = 0; rm < RM; ++rm) {
-        const int gm = m0 + wm * WTM + rm * 16 + fr;
-        if (gm >= M) continue;
+        const int ml = wm * WTM + rm * 16 + fr;
 #pragma unroll
         for (int rn = 0; rn < RN; ++rn) {
-            const int gn = n0 + wn * WTN + rn * 16 + fq * 4;
+            const int nl = wn * WTN + rn * 16 + fq * 4;
             const f32x4 v = acc[rn][rm];
             uint2 packed;
             packed.x = pack_bf16x2(v[0], v[1]);
             packed.y = pack_bf16x2(v[2], v[3]);
-            *(uint2*)(C + (size_t)gm * ldc + gn) = packed;
+            *(uint2*)(smem + ml * CROW + nl * 2) = packed;
+        }
+    }
+    __syncthreads();
+    constexpr int CHUNKS = BN / 8;                          // 16-B chunks per output row
+    const int rows = min(BM, M - m0);
+    for (int i = tid; i < BM * CHUNKS; i += NTHREADS) {
+        const int r = i / CHUNKS, c = i % CHUNKS;
+        if (r < rows)
+            *(uint4*)(C + (size_t)(m0 + r) * ldc + n0 + c * 8) = *(const uint4*)(smem + r * CROW + c * 16);
+    }
+    if (stats != nullptr) {
+        // per-channel partial sum / sum of squares of the bf16-rounded outputs over this block's rows:
+        // stats[0][tm][n] and stats[1][tm][n] (the BatchNorm that consumes this conv skips its stats pass)
+        constexpr int TPC = NTHREADS / BN;                  // threads per channel
+        const int c = tid % BN, part = tid / BN;
+        float s1 = 0.f, s2 = 0.f;
+        for (int r = part; r < rows; r += TPC) {
+            const float v = (float)*(const __bf16*)(smem + r * CROW + c * 2);
+            s1 += v;
+            s2 = fmaf(v, v, s2);
+        }
+        float* red = (float*)(smem + BM * CROW);            // [2][NTHREADS]
+        red[tid] = s1;
+        red[NTHREADS + tid] = s2;
+        __syncthreads();
+        if (part == 0) {
+            for (int j = 1; j < TPC; ++j) {
+                s1 += red[j * BN + c];
+                s2 += red[NTHREADS + j * BN + c];
+            }
+            stats[(size_t)tm * N + n0 + c] = s1;
+            stats[(size_t)(ntm + tm) * N + n0 + c] = s2;
         }
     }
 }
@@ -261,25 +297,35 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
         }
 }
 
-// C[i][j] (ldc) = (accumulate ? C : 0) + sum_s W[s][i][j]; one float4 per thread
+// C[i][j] (ldc) (+)= sum_s W[s][i][j]; one float4 per thread.  blockIdx.y picks a group of `per_group`
+// slices so a small output with many slices still spreads over the chip; with more than one group the
+// groups combine with fp32 atomics into C (zeroed by the host unless accumulating).
 __global__ void slab_reduce_kernel(const float* __restrict__ W, float* __restrict__ C, int N1, int N2, int ldc,
-                                   int slices, int accumulate) {
+                                   int slices, int per_group, int direct, int accumulate) {
     const long total4 = (long)N1 * N2 / 4;
     const long plane = (long)N1 * N2;
+    const int s0 = blockIdx.y * per_group, s1 = min(slices, s0 + per_group);
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int s = 0; s < slices; ++s) {
+        for (int s = s0; s < s1; ++s) {
             const float4 v = ((const float4*)(W + s * plane))[i];
             acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
         }
         const long e = i * 4;
         const int r = (int)(e / N2), c = (int)(e % N2);
-        float4* dst = (float4*)(C + (size_t)r * ldc + c);
-        if (accumulate) {
-            const float4 o = *dst;
-            acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+        float* dst = C + (size_t)r * ldc + c;
+        if (direct) {
+            if (accumulate) {
+                const float4 o = *(const float4*)dst;
+                acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+            }
+            *(float4*)dst = acc;
+        } else {
+            unsafeAtomicAdd(dst, acc.x);
+            unsafeAtomicAdd(dst + 1, acc.y);
+            unsafeAtomicAdd(dst + 2, acc.z);
+            unsafeAtomicAdd(dst + 3, acc.w);
         }
-        *dst = acc;
     }
 }
 
@@ -310,14 +356,15 @@ int set_lds(KernelT k, int bytes) {
 
 template <int BM, int BN, int WGM, int WGN>
 int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-              const void* zero, hipStream_t s) {
+              const void* zero, float* stats, hipStream_t s) {
     constexpr int LDS = 2 * (BM + BN) * BK * 2;
+    static_assert(BM * (BN * 2 + 16) + 2 * NTHREADS * 4 <= LDS, "epilogue staging must fit the k-loop LDS");
     auto k = gemm_nt_kernel<BM, BN, WGM, WGN>;
     static int attr = set_lds(k, LDS);
     if (attr) return attr;
     const int nwg = ((M + BM - 1) / BM) * (N / BN);
     hipLaunchKernelGGL(k, dim3(nwg), dim3(NTHREADS), LDS, s, (const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N,
-                       K, lda, ldb, ldc, (const __bf16*)zero);
+                       K, lda, ldb, ldc, (const __bf16*)zero, stats);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -334,8 +381,8 @@ inline TnPlan tn_plan(int M, int N1, int N2, int num_cus) {
     tn_tile(N1, N2, bn1, bn2);
     const int ntiles = (N1 / bn1) * (N2 / bn2);
     const long plane = (long)N1 * N2;
-    int slices = (2 * (num_cus > 0 ? num_cus : 256)) / ntiles;
-    const int by_depth = M / (8 * BK);
+    int slices = (4 * (num_cus > 0 ? num_cus : 256)) / ntiles;
+    const int by_depth = M / (4 * BK);
     const int by_bytes = (int)((16l << 20) / (plane * 4));
     if (slices > by_depth) slices = by_depth;
     if (slices > by_bytes) slices = by_bytes;
@@ -363,12 +410,15 @@ int launch_tn(const void* A, const void* B, float* W, int M, int N1, int N2, int
 extern "C" {
 
 // tile selection: wide-N problems use 128x128, N == 64 uses 256x64 (pixels x channels)
+int plx_gemm_nt_rows_per_block(int N) { return N % 128 == 0 ? 128 : 256; }
+
+// stats (nullable): fp32 [2][ceil(M / rows_per_block)][N] per-block channel sums / sums of squares of C
 int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                const void* zero, void* stream) {
-    if (M <= 0 || N % 64 || K % BK || lda % 8 || ldb % 8 || ldc % 4) return -1;
+                const void* zero, float* stats, void* stream) {
+    if (M <= 0 || N % 64 || K % BK || lda % 8 || ldb % 8 || ldc % 8) return -1;
     hipStream_t s = (hipStream_t)stream;
-    if (N % 128 == 0) return launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, s);
-    return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, s);
+    if (N % 128 == 0) return launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s);
+    return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s);
 }
 
 // floats of slab workspace plx_gemm_tn needs for this problem
@@ -393,7 +443,17 @@ int plx_gemm_tn(const void* A, const void* B, float* C, float* ws, int M, int N1
     const long total4 = (long)N1 * N2 / 4;
     int blocks = (int)((total4 + 255) / 256);
     if (blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, C, N1, N2, ldc, plan.slices, accumulate);
+    int groups = 1024 / blocks;                             // aim for ~1024 reducer blocks
+    if (groups > plan.slices / 8) groups = plan.slices / 8;  // but >= 8 slabs per group
+    if (groups < 1) groups = 1;
+    const int per_group = (plan.slices + groups - 1) / groups;
+    groups = (plan.slices + per_group - 1) / per_group;
+    const int direct = groups == 1;
+    if (!direct && !accumulate) {
+        if (hipMemset2DAsync(C, (size_t)ldc * 4, 0, (size_t)N2 * 4, N1, s) != hipSuccess) return -3;
+    }
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks, groups), dim3(256), 0, s, ws, C, N1, N2, ldc, plan.slices,
+                       per_group, direct, accumulate);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

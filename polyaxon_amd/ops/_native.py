@@ -152,6 +152,9 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_bn_workspace": [_L, _I],
         "plx_bn_forward": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P],
         "plx_bn_apply": [_P, _P, _P, _L, _I, _P, _I, _P],
+        "plx_bn_l2_workspace": [_I, _I],
+        "plx_bn_forward_from_partials": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P, _I,
+                                         _P],
         "plx_bn_backward": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     },
     "plx_procmon": {
@@ -170,7 +173,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
                                _P, _P],
     },
     "plx_conv": {
-        "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
+        "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P],
+        "plx_gemm_nt_rows_per_block": [_I],
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
@@ -198,7 +202,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_bn_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
+RESTYPES: Dict[str, object] = {"plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

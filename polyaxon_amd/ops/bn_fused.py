@@ -32,7 +32,7 @@ def supported(x: torch.Tensor) -> bool:
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, ext=None):
         lib = _native.lib("plx_bn")
         x = _cl(x)
         n, c, h, w = x.shape
@@ -43,16 +43,26 @@ class _BNAct(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=x.device)
         y = torch.empty_like(x, memory_format=torch.channels_last)
         stats = torch.empty(4 * c, **f32)  # mean | invstd | scale | bias
-        partials = torch.empty(ws, **f32)
         res = _cl(residual) if residual is not None else None
-        rc = lib.plx_bn_forward(
-            x.data_ptr(), res.data_ptr() if res is not None else None, y.data_ptr(), m, c,
-            weight.data_ptr(), bias.data_ptr(), float(eps), float(momentum),
-            running_mean.data_ptr() if running_mean is not None else None,
-            running_var.data_ptr() if running_var is not None else None,
-            stats.data_ptr(), stats[c:].data_ptr(), stats[2 * c:].data_ptr(), partials.data_ptr(), int(relu),
-            _stream())
-        _native.check(rc, "plx_bn_forward")
+        rm = running_mean.data_ptr() if running_mean is not None else None
+        rv = running_var.data_ptr() if running_var is not None else None
+        if ext is not None:
+            # channel sums came from the producing conv's GEMM epilogue: no stats pass over x
+            part, nblk = ext
+            l2 = torch.empty(int(lib.plx_bn_l2_workspace(nblk, c)), **f32)
+            rc = lib.plx_bn_forward_from_partials(
+                x.data_ptr(), res.data_ptr() if res is not None else None, y.data_ptr(), m, c, weight.data_ptr(),
+                bias.data_ptr(), float(eps), float(momentum), rm, rv, stats.data_ptr(), stats[c:].data_ptr(),
+                stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(), int(relu), _stream())
+            _native.check(rc, "plx_bn_forward_from_partials")
+        else:
+            partials = torch.empty(ws, **f32)
+            rc = lib.plx_bn_forward(
+                x.data_ptr(), res.data_ptr() if res is not None else None, y.data_ptr(), m, c,
+                weight.data_ptr(), bias.data_ptr(), float(eps), float(momentum), rm, rv,
+                stats.data_ptr(), stats[c:].data_ptr(), stats[2 * c:].data_ptr(), partials.data_ptr(), int(relu),
+                _stream())
+            _native.check(rc, "plx_bn_forward")
         ctx.save_for_backward(x, y, weight, stats)
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -79,16 +89,18 @@ class _BNAct(torch.autograd.Function):
             m, c, weight.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(), dgb.data_ptr(), dgb[c:].data_ptr(),
             coef.data_ptr(), partials.data_ptr(), int(ctx.relu), _stream())
         _native.check(rc, "plx_bn_backward")
-        return dx, dgb[:c], dgb[c:], None, None, dres, None, None, None
+        return dx, dgb[:c], dgb[c:], None, None, dres, None, None, None, None
 
 
 def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
            running_var: Optional[torch.Tensor], training: bool, momentum: float, eps: float,
-           residual: Optional[torch.Tensor], act: bool) -> torch.Tensor:
+           residual: Optional[torch.Tensor], act: bool, ext_stats=None) -> torch.Tensor:
+    """``ext_stats`` = (fp32 [2][nblk][C] channel sums / sums of squares of ``x``, nblk) from the op that
+    produced ``x`` (the 1x1-conv GEMM epilogue); training mode then skips the stats pass."""
     if residual is not None and residual.dtype != x.dtype:
         residual = residual.to(x.dtype)
     if training:
-        return _BNAct.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, act)
+        return _BNAct.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, act, ext_stats)
     # inference: fold running stats into scale/bias, one apply pass
     lib = _native.lib("plx_bn")
     x = _cl(x)

@@ -45,16 +45,26 @@ def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
-def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
-    """out[M][N] = a[M][K] · b[N][K]ᵀ, bf16 (rows may be strided, K contiguous)."""
+def nt_stats_rows(n: int) -> int:
+    """Rows per block of plx_gemm_nt for an N-wide output (the granularity of its BN-stats partials)."""
+    return int(_native.lib("plx_conv").plx_gemm_nt_rows_per_block(n))
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, stats: torch.Tensor = None) -> torch.Tensor:
+    """out[M][N] = a[M][K] · b[N][K]ᵀ, bf16 (rows may be strided, K contiguous).  ``stats`` (fp32
+    [2][ceil(M / nt_stats_rows(N))][N]) receives per-block channel sums and sums of squares of ``out``."""
     m, k = a.shape
     n = b.shape[0]
     if out is None:
         out = torch.empty(m, n, dtype=torch.bfloat16, device=a.device)
     assert a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1 and b.shape[1] == k
-    assert a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and out.data_ptr() % 8 == 0
+    assert a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0
+    if stats is not None:
+        nblk = -(-m // nt_stats_rows(n))
+        assert stats.dtype == torch.float32 and stats.is_contiguous() and stats.numel() >= 2 * nblk * n
     rc = _native.lib("plx_conv").plx_gemm_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0),
-                                             b.stride(0), out.stride(0), _zero_page(a.device).data_ptr(), _stream())
+                                             b.stride(0), out.stride(0), _zero_page(a.device).data_ptr(),
+                                             stats.data_ptr() if stats is not None else None, _stream())
     _native.check(rc, "plx_gemm_nt")
     return out
 
@@ -99,13 +109,13 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, stats):
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         wb, wt = weight_prep(weight)
         y = torch.empty((n, cout, h, w), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-        gemm_nt(_rows(x), wb, _rows(y))
+        gemm_nt(_rows(x), wb, _rows(y), stats)
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
         ctx.wdtype = weight.dtype
@@ -121,28 +131,47 @@ class _Conv1x1(torch.autograd.Function):
             gemm_nt(_rows(dy), wt, _rows(dx))
         if ctx.needs_input_grad[1]:
             dw = gemm_tn(_rows(dy), _rows(x)).view(ctx.wshape).to(ctx.wdtype)
-        return dx, dw
+        return dx, dw, None
+
+
+def _bf16_context(x: torch.Tensor) -> bool:
+    """bf16 activations, or fp32 ones inside a bf16 autocast region (an fp32 network keeps fp32 convs)."""
+    if x.dtype == torch.bfloat16:
+        return True
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
 
 
 def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
-    return (x.is_cuda and x.dim() == 4 and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+    return (x.is_cuda and x.dim() == 4 and _bf16_context(x) and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
             and conv.padding == (0, 0) and conv.groups == 1 and conv.bias is None
             and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0 and x.numel() > 0)
 
 
-def conv1x1(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    return _Conv1x1.apply(x, weight)
+def conv1x1(x: torch.Tensor, weight: torch.Tensor, with_stats: bool = False) -> torch.Tensor:
+    """With ``with_stats`` the output carries ``_plx_channel_stats`` = (fp32 [2][nblk][Cout] per-block channel
+    sums / sums of squares, nblk), which a following fused BatchNorm uses instead of its own stats pass."""
+    stats = None
+    if with_stats:
+        n, _, h, w = x.shape
+        m, cout = n * h * w, weight.shape[0]
+        nblk = -(-m // nt_stats_rows(cout))
+        stats = torch.empty(2 * nblk * cout, dtype=torch.float32, device=x.device)
+    y = _Conv1x1.apply(x, weight, stats)
+    if stats is not None:
+        y._plx_channel_stats = (stats, nblk)
+    return y
 
 
 class Conv1x1(nn.Conv2d):
     """``nn.Conv2d(in, out, 1, bias=False)`` whose GPU path is the MFMA GEMM op above (same parameter, same
     init; falls back to ``F.conv2d`` on CPU or for unsupported channel counts)."""
 
-    def __init__(self, in_ch: int, out_ch: int, stride: int = 1, native: bool = True):
+    def __init__(self, in_ch: int, out_ch: int, stride: int = 1, native: bool = True, bn_stats: bool = True):
         super().__init__(in_ch, out_ch, 1, stride=stride, bias=False)
         self.native = native
+        self.bn_stats = bn_stats  # emit channel stats for the BatchNorm that follows (training only)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.native and supported(x, self):
-            return conv1x1(x, self.weight)
+            return conv1x1(x, self.weight, with_stats=self.bn_stats and self.training)
         return F.conv2d(x, self.weight, None, self.stride)

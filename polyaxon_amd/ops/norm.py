@@ -55,8 +55,9 @@ class BatchNormAct(nn.Module):
         if self.fused and x.is_cuda:
             from polyaxon_amd.ops import bn_fused
             if bn_fused.supported(x):
+                ext = getattr(x, "_plx_channel_stats", None)  # set by ops.conv1x1 on its output
                 return bn_fused.bn_act(x, self.weight, self.bias, self.running_mean, self.running_var,
-                                       self.training, self.momentum, self.eps, identity, self.act)
+                                       self.training, self.momentum, self.eps, identity, self.act, ext)
         if x.is_cuda and torch.is_autocast_enabled("cuda"):
             # keep BN math in the activation dtype like the fused kernel (fp32 stats inside)
             pass

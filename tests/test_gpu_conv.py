@@ -90,3 +90,44 @@ def test_conv1x1_in_autocast_graph(cuda):
     ref = F.conv2d(x.to(torch.bfloat16), conv.weight.to(torch.bfloat16))
     torch.testing.assert_close(y.float(), ref.float(), rtol=2e-2, atol=5e-2)
     assert conv.weight.grad is not None and torch.isfinite(conv.weight.grad).all()
+
+
+@pytest.mark.parametrize("m,n,k", [(1000, 128, 64), (777, 64, 128), (4096, 256, 64)])
+def test_gemm_nt_channel_stats(cuda, m, n, k):
+    from polyaxon_amd.ops.conv1x1 import gemm_nt, nt_stats_rows
+
+    torch.manual_seed(3)
+    a, b = _bf(m, k, dev=cuda), _bf(n, k, dev=cuda)
+    rows = nt_stats_rows(n)
+    nblk = -(-m // rows)
+    stats = torch.full((2 * nblk * n,), float("nan"), device=cuda)
+    out = gemm_nt(a, b, stats=stats)
+    st = stats.view(2, nblk, n)
+    o = out.float()
+    torch.testing.assert_close(st[0].sum(0), o.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(st[1].sum(0), o.square().sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(st[0][0], o[:rows].sum(0), rtol=1e-4, atol=1e-2)
+
+
+def test_conv_stats_feed_batchnorm(cuda):
+    """conv1x1 -> BatchNormAct with the GEMM-epilogue stats == the same BN running its own stats pass."""
+    from polyaxon_amd.ops.conv1x1 import Conv1x1
+    from polyaxon_amd.ops.norm import BatchNormAct
+
+    torch.manual_seed(4)
+    x = torch.randn(4, 128, 20, 20, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for use_stats in (True, False):
+        conv = Conv1x1(128, 256, bn_stats=use_stats).to(cuda)
+        torch.manual_seed(5)
+        conv.weight.data.normal_(0, 0.05)
+        bn = BatchNormAct(256).to(cuda)
+        xa = x.clone().requires_grad_()
+        z = conv(xa)
+        assert (getattr(z, "_plx_channel_stats", None) is not None) == use_stats
+        y = bn(z)
+        y.float().square().mean().backward()
+        outs.append((y.float(), bn.running_mean.clone(), bn.running_var.clone(), xa.grad.float(),
+                     conv.weight.grad.clone()))
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=1e-2, atol=2e-2)
