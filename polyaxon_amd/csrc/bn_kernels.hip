@@ -169,7 +169,7 @@ __global__ void bn_fwd_finalize_kernel(const float* __restrict__ psum, const flo
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const bf16x8* __restrict__ x, const bf16x8* __restrict__ res,
                                                           bf16x8* __restrict__ y, const float* __restrict__ scale,
                                                           const float* __restrict__ bias, int64_t n_vec, int G,
-                                                          int relu) {
+                                                          int relu, uint8_t* __restrict__ mask) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // multiple of G (G | 256 or G % 256 == 0 handled by host)
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_vec) return;
@@ -196,11 +196,19 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const bf16x8* __restri
       for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
     }
     store8(y + i, v);
+    if (mask != nullptr) {
+      // ReLU mask, 1 bit per element (bit k of byte i = channel 8*cg+k of vector i): the backward reads this
+      // 1/16-size tensor instead of y (a positive float stays positive after bf16 rounding, so bit == y > 0).
+      uint32_t bits = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bits |= (uint32_t)(v[k] > 0.f) << k;
+      mask[i] = (uint8_t)bits;
+    }
   }
 }
 
 // ------------------------------------------------------------------------------- backward reduce
-__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const bf16x8* __restrict__ x, const bf16x8* __restrict__ y,
+__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const bf16x8* __restrict__ x, const uint8_t* __restrict__ mask,
                                                                const bf16x8* __restrict__ dy, int64_t M, int G, int Gb,
                                                                int64_t rows_per_block, const float* __restrict__ mean,
                                                                const float* __restrict__ invstd, int relu,
@@ -228,10 +236,9 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const bf16x8* __r
     load8(x + off, xv);
     load8(dy + off, g);
     if (relu) {
-      float yv[8];
-      load8(y + off, yv);
+      const uint32_t mb = mask[off];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+      for (int k = 0; k < 8; ++k) g[k] = (mb >> k) & 1u ? g[k] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -286,7 +293,7 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ pdz, const floa
   coef[2 * C + c] = -k1 * k2 + k1 * k3 * is * mean[c];  // D
 }
 
-__global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restrict__ x, const bf16x8* __restrict__ y,
+__global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restrict__ x, const uint8_t* __restrict__ mask,
                                                            const bf16x8* __restrict__ dy, bf16x8* __restrict__ dx,
                                                            bf16x8* __restrict__ dres, const float* __restrict__ coef,
                                                            int64_t n_vec, int G, int relu) {
@@ -307,10 +314,9 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restr
     load8(x + i, xv);
     load8(dy + i, g);
     if (relu) {
-      float yv[8];
-      load8(y + i, yv);
+      const uint32_t mb = mask[i];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+      for (int k = 0; k < 8; ++k) g[k] = (mb >> k) & 1u ? g[k] : 0.f;
     }
     if (dres != nullptr) store8(dres + i, g);
     float o[8];
@@ -367,7 +373,8 @@ PLX_API int64_t plx_bn_workspace(int64_t M, int C) {
 PLX_API int plx_bn_forward(const void* x, const void* res, void* y, int64_t M, int C, const float* gamma,
                            const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                            float* save_mean, float* save_invstd, float* scale_bias /* [2C] */,
-                           float* partials /* plx_bn_workspace floats */, int relu, hipStream_t stream) {
+                           float* partials /* plx_bn_workspace floats */, uint8_t* mask /* M*C/8 bytes or null */,
+                           int relu, hipStream_t stream) {
   Plan p;
   if (!plan_for(M, C, &p) || M < 1) return 1;
   float* psum = partials;
@@ -382,7 +389,7 @@ PLX_API int plx_bn_forward(const void* x, const void* res, void* y, int64_t M, i
                      save_invstd, scale_bias, scale_bias + C);
   const int64_t n_vec = M * p.G;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu);
+                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu, relu ? mask : nullptr);
   return (int)hipGetLastError();
 }
 
@@ -398,7 +405,7 @@ PLX_API int plx_bn_forward_from_partials(const void* x, const void* res, void* y
                                          const float* gamma, const float* beta, float eps, float momentum,
                                          float* running_mean, float* running_var, float* save_mean,
                                          float* save_invstd, float* scale_bias, const float* partials, int nblk,
-                                         float* l2, int relu, hipStream_t stream) {
+                                         float* l2, uint8_t* mask, int relu, hipStream_t stream) {
   Plan p;
   if (!plan_for(M, C, &p) || M < 1 || nblk < 1) return 1;
   const int S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
@@ -409,7 +416,7 @@ PLX_API int plx_bn_forward_from_partials(const void* x, const void* res, void* y
                      save_invstd, scale_bias, scale_bias + C);
   const int64_t n_vec = M * p.G;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu);
+                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu, relu ? mask : nullptr);
   return (int)hipGetLastError();
 }
 
@@ -419,20 +426,21 @@ PLX_API int plx_bn_apply(const void* x, const void* res, void* y, int64_t M, int
   if (!plan_for(M, C, &p)) return 1;
   const int64_t n_vec = M * p.G;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu);
+                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu, nullptr);
   return (int)hipGetLastError();
 }
 
-PLX_API int plx_bn_backward(const void* x, const void* y, const void* dy, void* dx, void* dres, int64_t M, int C,
+// mask: the ReLU bit mask written by the forward (required when relu)
+PLX_API int plx_bn_backward(const void* x, const uint8_t* mask, const void* dy, void* dx, void* dres, int64_t M, int C,
                             const float* gamma, const float* save_mean, const float* save_invstd, float* dgamma,
                             float* dbeta, float* coef /* [3C] */, float* partials /* plx_bn_workspace floats */, int relu,
                             hipStream_t stream) {
   Plan p;
-  if (!plan_for(M, C, &p) || M < 1) return 1;
+  if (!plan_for(M, C, &p) || M < 1 || (relu && mask == nullptr)) return 1;
   float* pa = partials;
   float* pb = partials + (int64_t)p.nblk * C;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(p.nblk, p.gy), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     (const bf16x8*)y, (const bf16x8*)dy, M, p.G, p.Gb, p.rows_per_block, save_mean, save_invstd,
+                     mask, (const bf16x8*)dy, M, p.G, p.Gb, p.rows_per_block, save_mean, save_invstd,
                      relu, pa, pb);
   float* l2 = partials + 2 * (int64_t)p.nblk * C;
   hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, p.S, 2), dim3(256), 0, stream, partials, p.nblk, C,
@@ -441,6 +449,6 @@ PLX_API int plx_bn_backward(const void* x, const void* y, const void* dy, void* 
                      gamma, save_mean, save_invstd, dgamma, dbeta, coef);
   const int64_t n_vec = M * p.G;
   hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     (const bf16x8*)y, (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, p.G, relu);
+                     mask, (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, p.G, relu);
   return (int)hipGetLastError();
 }

@@ -15,6 +15,7 @@ import torch.nn as nn
 
 from polyaxon_amd.ops.conv1x1 import Conv1x1
 from polyaxon_amd.ops.norm import BatchNormAct
+from polyaxon_amd.ops.pool import MaxPool3s2
 
 
 class Bottleneck(nn.Module):
@@ -57,7 +58,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.stem = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
         self.stem_bn = BatchNormAct(width, act=True, fused=fused)
-        self.pool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.pool = MaxPool3s2(native=native_conv)
         stages = []
         in_ch = width
         for i, n in enumerate(layers):

@@ -32,6 +32,7 @@ LIBRARIES: Dict[str, dict] = {
     "plx_gp": {"sources": ["gp_kernels.hip"], "kind": "hip", "link": []},
     "plx_rms": {"sources": ["rmsnorm.hip"], "kind": "hip", "link": []},
     "plx_conv": {"sources": ["conv_gemm.hip"], "kind": "hip", "link": []},
+    "plx_pool": {"sources": ["pool_kernels.hip"], "kind": "hip", "link": []},
     "plx_rccl": {"sources": ["rccl_comm.cpp"], "kind": "hip_host", "link": ["-lrccl"]},
 }
 
@@ -150,11 +151,11 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
     },
     "plx_bn": {
         "plx_bn_workspace": [_L, _I],
-        "plx_bn_forward": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P],
+        "plx_bn_forward": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _P],
         "plx_bn_apply": [_P, _P, _P, _L, _I, _P, _I, _P],
         "plx_bn_l2_workspace": [_I, _I],
-        "plx_bn_forward_from_partials": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P, _I,
-                                         _P],
+        "plx_bn_forward_from_partials": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P, _P,
+                                         _I, _P],
         "plx_bn_backward": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     },
     "plx_procmon": {
@@ -178,6 +179,10 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
+    },
+    "plx_pool": {
+        "plx_maxpool3s2_forward": [_P, _P, _P, _I, _I, _I, _I, _P],
+        "plx_maxpool3s2_backward": [_P, _P, _P, _I, _I, _I, _I, _P],
     },
     "plx_rms": {
         "plx_rms_forward": [_P, _P, _P, _P, _L, _I, _F, _P],

@@ -2,8 +2,8 @@
 
 Forward (training): stats → finalize (mean/invstd/scale/bias + running-stat update) → apply.
 Backward: reduce (Σdz, Σdz·x̂) → finalize (dγ, dβ, dx coefficients) → dx (+ d_residual) in one pass.
-The ReLU mask is taken from the saved output ``y`` — it is the next convolution's input and is kept by
-autograd anyway, so the fusion saves no extra activation memory.
+With ReLU the forward also writes a 1-bit-per-element mask (1/16 of ``y``); the backward reads it instead of
+``y``, one fewer full activation stream in each of its two passes.
 """
 from __future__ import annotations
 
@@ -46,6 +46,8 @@ class _BNAct(torch.autograd.Function):
         res = _cl(residual) if residual is not None else None
         rm = running_mean.data_ptr() if running_mean is not None else None
         rv = running_var.data_ptr() if running_var is not None else None
+        mask = torch.empty(m * c // 8, dtype=torch.uint8, device=x.device) if relu else None
+        mp = mask.data_ptr() if mask is not None else None
         if ext is not None:
             # channel sums came from the producing conv's GEMM epilogue: no stats pass over x
             part, nblk = ext
@@ -53,17 +55,17 @@ class _BNAct(torch.autograd.Function):
             rc = lib.plx_bn_forward_from_partials(
                 x.data_ptr(), res.data_ptr() if res is not None else None, y.data_ptr(), m, c, weight.data_ptr(),
                 bias.data_ptr(), float(eps), float(momentum), rm, rv, stats.data_ptr(), stats[c:].data_ptr(),
-                stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(), int(relu), _stream())
+                stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(), mp, int(relu), _stream())
             _native.check(rc, "plx_bn_forward_from_partials")
         else:
             partials = torch.empty(ws, **f32)
             rc = lib.plx_bn_forward(
                 x.data_ptr(), res.data_ptr() if res is not None else None, y.data_ptr(), m, c,
                 weight.data_ptr(), bias.data_ptr(), float(eps), float(momentum), rm, rv,
-                stats.data_ptr(), stats[c:].data_ptr(), stats[2 * c:].data_ptr(), partials.data_ptr(), int(relu),
+                stats.data_ptr(), stats[c:].data_ptr(), stats[2 * c:].data_ptr(), partials.data_ptr(), mp, int(relu),
                 _stream())
             _native.check(rc, "plx_bn_forward")
-        ctx.save_for_backward(x, y, weight, stats)
+        ctx.save_for_backward(x, mask, weight, stats)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.ws = ws
@@ -72,7 +74,7 @@ class _BNAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         lib = _native.lib("plx_bn")
-        x, y, weight, stats = ctx.saved_tensors
+        x, mask, weight, stats = ctx.saved_tensors
         n, c, h, w = x.shape
         m = n * h * w
         dy = _cl(dy)
@@ -85,7 +87,7 @@ class _BNAct(torch.autograd.Function):
         coef = torch.empty(3 * c, **f32)
         partials = torch.empty(ctx.ws, **f32)
         rc = lib.plx_bn_backward(
-            x.data_ptr(), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else None,
+            x.data_ptr(), mask.data_ptr() if mask is not None else None, dy.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else None,
             m, c, weight.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(), dgb.data_ptr(), dgb[c:].data_ptr(),
             coef.data_ptr(), partials.data_ptr(), int(ctx.relu), _stream())
         _native.check(rc, "plx_bn_backward")

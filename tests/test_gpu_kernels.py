@@ -187,3 +187,21 @@ def test_executor_snapshot_restore_is_exact(cuda):
     torch.cuda.synchronize()
     torch.testing.assert_close(ex.flat.params, p1, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(ex.losses()[-3:], l1, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 112, 112), (3, 16, 9, 7), (1, 8, 2, 2)])
+def test_maxpool3s2_matches_torch(cuda, shape):
+    from polyaxon_amd.ops.pool import _MaxPool3s2
+
+    torch.manual_seed(0)
+    x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x[0, 0, 0, :2] = 3.0  # a tie inside one window: both implementations keep the first maximum
+    xa = x.clone().requires_grad_()
+    y = _MaxPool3s2.apply(xa)
+    xr = x.clone().requires_grad_()
+    yr = torch.nn.functional.max_pool2d(xr, 3, 2, 1)
+    assert torch.equal(y, yr)
+    g = torch.randn_like(yr)
+    y.backward(g)
+    yr.backward(g)
+    torch.testing.assert_close(xa.grad.float(), xr.grad.float(), rtol=1e-2, atol=1e-2)
