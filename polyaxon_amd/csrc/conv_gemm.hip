@@ -25,6 +25,20 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void gbl_void;
 
 constexpr int BK = 64;          // reduction depth per LDS stage (bf16 elements)
+
+// Implicit-GEMM geometry of a 3x3 / stride-1 / pad-1 convolution on NHWC rows: pixel row m = (n*H + h)*W + w,
+// reduction index k = tap*C + c with tap = 3*kh + kw.  The operand row for (m, tap) is the pixel shifted by
+// (kh-1, kw-1) (or by (1-kh, 1-kw) when `flip`, the data-gradient direction); out-of-image rows read the
+// zero page, which is exactly the zero padding.
+struct ConvGeom {
+    int H, W, C, flip;
+};
+
+__device__ __forceinline__ void tap_shift(int tap, int flip, int& dh, int& dw) {
+    const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+    dh = flip ? 1 - kh : kh - 1;
+    dw = flip ? 1 - kw : kw - 1;
+}
 constexpr int NTHREADS = 256;   // 4 waves
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
@@ -51,11 +65,11 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 // 16 rows of a fragment read on 16 distinct bank slots.
 __device__ __forceinline__ int nt_swz(int row) { return (row >> 1) & 7; }
 
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, bool CONV>
 __global__ void __launch_bounds__(NTHREADS, 2)
 gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
                int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
-               float* __restrict__ stats) {
+               float* __restrict__ stats, ConvGeom geo) {
     constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
     constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -68,15 +82,40 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     const int m0 = tm * BM, n0 = tn * BN;
     const int wm = wave / WGN, wn = wave % WGN;
 
+    // conv mode: (h, w) of the A rows this thread stages, fixed over the whole k loop
+    int row_h[BM / 32], row_w[BM / 32];
+    if constexpr (CONV) {
+#pragma unroll
+        for (int i = 0; i < BM / 32; ++i) {
+            const int gm = m0 + (i * 4 + wave) * 8 + (lane >> 3);
+            const int q = gm / geo.W;
+            row_w[i] = gm - q * geo.W;
+            row_h[i] = q - (q / geo.H) * geo.H;
+        }
+    }
+
     // staging: each wave instruction moves 1024 B = 8 rows x 8 chunks; lane -> (row, physical chunk)
     auto stage = [&](int buf, int k0) {
         char* base = smem + buf * STAGE;
+        int dh = 0, dw = 0, c0 = k0;
+        if constexpr (CONV) {
+            const int tap = k0 / geo.C;
+            c0 = k0 - tap * geo.C;
+            tap_shift(tap, geo.flip, dh, dw);
+        }
 #pragma unroll
         for (int i = 0; i < BM / 32; ++i) {                 // A: BM rows / 8 rows per instr / 4 waves
             const int row = (i * 4 + wave) * 8 + (lane >> 3);
             const int lc = (lane & 7) ^ nt_swz(row);
             const int gm = m0 + row;
-            const __bf16* src = gm < M ? A + (size_t)gm * lda + k0 + lc * 8 : zero;
+            const __bf16* src;
+            if constexpr (CONV) {
+                const int ih = row_h[i] + dh, iw = row_w[i] + dw;
+                const bool ok = gm < M && (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
+                src = ok ? A + (size_t)(gm + dh * geo.W + dw) * lda + c0 + lc * 8 : zero;
+            } else {
+                src = gm < M ? A + (size_t)gm * lda + k0 + lc * 8 : zero;
+            }
             glds16(src, base + (i * 4 + wave) * 1024);
         }
 #pragma unroll
@@ -201,10 +240,12 @@ __device__ __forceinline__ s16x4 tr_read(const char* img, int row, int col /* el
         (__attribute__((address_space(3))) s16x4*)(img + row * ROWB + pc * 16 + half * 8));
 }
 
-template <int ROWB>
+template <int ROWB, bool GATHER = false>
 __device__ __forceinline__ void stage_rows(char* img, const __bf16* __restrict__ G, int ld, int r0, int rend,
-                                           int c0, const __bf16* __restrict__ zero, int wave, int lane) {
-    // BK rows x ROWB bytes, lane-linear image; 1024 B per wave instruction
+                                           int c0, const __bf16* __restrict__ zero, int wave, int lane,
+                                           ConvGeom geo = {}, int dh = 0, int dw = 0) {
+    // BK rows x ROWB bytes, lane-linear image; 1024 B per wave instruction.  GATHER: row gr is the pixel
+    // shifted by (dh, dw) (zero page outside the image), for the weight gradient of a 3x3 convolution.
     constexpr int INSTR = BK * ROWB / 1024;
 #pragma unroll
     for (int i = 0; i < INSTR / 4; ++i) {
@@ -212,15 +253,24 @@ __device__ __forceinline__ void stage_rows(char* img, const __bf16* __restrict__
         const int row = off / ROWB, pc = (off % ROWB) >> 4;
         const int lc = pc ^ tr_swz<ROWB>(row);
         const int gr = r0 + row;
-        const __bf16* src = gr < rend ? G + (size_t)gr * ld + c0 + lc * 8 : zero;
+        const __bf16* src;
+        if constexpr (GATHER) {
+            const int q = gr / geo.W;
+            const int w = gr - q * geo.W, h = q - (q / geo.H) * geo.H;
+            const bool ok = gr < rend && (unsigned)(h + dh) < (unsigned)geo.H && (unsigned)(w + dw) < (unsigned)geo.W;
+            src = ok ? G + (size_t)(gr + dh * geo.W + dw) * ld + c0 + lc * 8 : zero;
+        } else {
+            src = gr < rend ? G + (size_t)gr * ld + c0 + lc * 8 : zero;
+        }
         glds16(src, img + (i * 4 + wave) * 1024);
     }
 }
 
-template <int BN1, int BN2, int WG1, int WG2>
+template <int BN1, int BN2, int WG1, int WG2, bool CONV>
 __global__ void __launch_bounds__(NTHREADS, 2)
 gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float* __restrict__ W,
-               int M, int N1, int N2, int lda, int ldb, int kchunk, const __bf16* __restrict__ zero) {
+               int M, int N1, int N2, int lda, int ldb, int kchunk, const __bf16* __restrict__ zero,
+               ConvGeom geo) {
     constexpr int WT1 = BN1 / WG1, WT2 = BN2 / WG2, R1 = WT1 / 16, R2 = WT2 / 16;
     constexpr int ROWA = BN1 * 2, ROWB_ = BN2 * 2;
     constexpr int A_BYTES = BK * ROWA, STAGE = BK * (ROWA + ROWB_);
@@ -243,10 +293,17 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
         for (int b = 0; b < R2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nk = (kend - kbeg + BK - 1) / BK;
+    // conv mode: N2 = 9*C and a BN2 tile lies inside one tap (C % BN2 == 0, host-checked)
+    int bc0 = n20, dh = 0, dw = 0;
+    if constexpr (CONV) {
+        const int tap = n20 / geo.C;
+        bc0 = n20 - tap * geo.C;
+        tap_shift(tap, 0, dh, dw);
+    }
     auto stage = [&](int buf, int k0) {
         char* base = smem + buf * STAGE;
         stage_rows<ROWA>(base, A, lda, k0, kend, n10, zero, wave, lane);
-        stage_rows<ROWB_>(base + A_BYTES, B, ldb, k0, kend, n20, zero, wave, lane);
+        stage_rows<ROWB_, CONV>(base + A_BYTES, B, ldb, k0, kend, bc0, zero, wave, lane, geo, dh, dw);
     };
     if (nk > 0) {
         stage(0, kbeg);
@@ -354,17 +411,17 @@ int set_lds(KernelT k, int bytes) {
                                                                                                                  : -2;
 }
 
-template <int BM, int BN, int WGM, int WGN>
+template <int BM, int BN, int WGM, int WGN, bool CONV = false>
 int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-              const void* zero, float* stats, hipStream_t s) {
+              const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}) {
     constexpr int LDS = 2 * (BM + BN) * BK * 2;
     static_assert(BM * (BN * 2 + 16) + 2 * NTHREADS * 4 <= LDS, "epilogue staging must fit the k-loop LDS");
-    auto k = gemm_nt_kernel<BM, BN, WGM, WGN>;
+    auto k = gemm_nt_kernel<BM, BN, WGM, WGN, CONV>;
     static int attr = set_lds(k, LDS);
     if (attr) return attr;
     const int nwg = ((M + BM - 1) / BM) * (N / BN);
     hipLaunchKernelGGL(k, dim3(nwg), dim3(NTHREADS), LDS, s, (const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N,
-                       K, lda, ldb, ldc, (const __bf16*)zero, stats);
+                       K, lda, ldb, ldc, (const __bf16*)zero, stats, geo);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -392,16 +449,16 @@ inline TnPlan tn_plan(int M, int N1, int N2, int num_cus) {
     return {kchunk, (M + kchunk - 1) / kchunk};
 }
 
-template <int BN1, int BN2, int WG1, int WG2>
+template <int BN1, int BN2, int WG1, int WG2, bool CONV = false>
 int launch_tn(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
-              const void* zero, hipStream_t s) {
+              const void* zero, hipStream_t s, ConvGeom geo = {}) {
     constexpr int LDS = 2 * BK * (BN1 + BN2) * 2;
-    auto k = gemm_tn_kernel<BN1, BN2, WG1, WG2>;
+    auto k = gemm_tn_kernel<BN1, BN2, WG1, WG2, CONV>;
     static int attr = set_lds(k, LDS);
     if (attr) return attr;
     const int ntiles = (N1 / BN1) * (N2 / BN2);
     hipLaunchKernelGGL(k, dim3(ntiles * plan.slices), dim3(NTHREADS), LDS, s, (const __bf16*)A, (const __bf16*)B, W,
-                       M, N1, N2, lda, ldb, plan.kchunk, (const __bf16*)zero);
+                       M, N1, N2, lda, ldb, plan.kchunk, (const __bf16*)zero, geo);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -428,17 +485,22 @@ long plx_gemm_tn_workspace(int M, int N1, int N2, int num_cus) {
     return (long)p.slices * N1 * N2;
 }
 
-// C[N1][N2] (ldc, fp32) = (accumulate ? C : 0) + A^T B over M rows; ws holds plx_gemm_tn_workspace floats
-int plx_gemm_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int N2, int lda, int ldb, int ldc,
-                const void* zero, int num_cus, int accumulate, void* stream) {
-    if (M <= 0 || N1 % 64 || N2 % 64 || lda % 8 || ldb % 8 || ldc % 4) return -1;
-    hipStream_t s = (hipStream_t)stream;
+}  // extern "C"
+
+namespace {
+template <bool CONV>
+int run_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int N2, int lda, int ldb, int ldc,
+           const void* zero, int num_cus, int accumulate, hipStream_t s, ConvGeom geo) {
     const TnPlan plan = tn_plan(M, N1, N2, num_cus);
     int rc;
-    if (N1 % 128 == 0 && N2 % 128 == 0) rc = launch_tn<128, 128, 2, 2>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s);
-    else if (N1 % 128 == 0) rc = launch_tn<128, 64, 4, 1>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s);
-    else if (N2 % 128 == 0) rc = launch_tn<64, 128, 1, 4>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s);
-    else rc = launch_tn<64, 64, 2, 2>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s);
+    if (N1 % 128 == 0 && N2 % 128 == 0)
+        rc = launch_tn<128, 128, 2, 2, CONV>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
+    else if (N1 % 128 == 0)
+        rc = launch_tn<128, 64, 4, 1, CONV>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
+    else if (N2 % 128 == 0)
+        rc = launch_tn<64, 128, 1, 4, CONV>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
+    else
+        rc = launch_tn<64, 64, 2, 2, CONV>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
     if (rc) return rc;
     const long total4 = (long)N1 * N2 / 4;
     int blocks = (int)((total4 + 255) / 256);
@@ -454,6 +516,80 @@ int plx_gemm_tn(const void* A, const void* B, float* C, float* ws, int M, int N1
     }
     hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks, groups), dim3(256), 0, s, ws, C, N1, N2, ldc, plan.slices,
                        per_group, direct, accumulate);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// fp32 weight [Cout][Cin][3][3] (any strides) -> bf16 Wf[Cout][tap][Cin] (forward B operand) and
+// Wd[Cin][tap][Cout] (data-gradient B operand; the tap flip lives in the gather, not in the copy)
+__global__ void weight_prep3_kernel(const float* __restrict__ w, long s_co, long s_ci, long s_kh, long s_kw,
+                                    __bf16* __restrict__ wf, __bf16* __restrict__ wd, int cout, int cin) {
+    const long total = (long)cout * cin * 9;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int ci = (int)(i % cin);
+        const long r = i / cin;
+        const int tap = (int)(r % 9), co = (int)(r / 9);
+        const __bf16 v = (__bf16)w[co * s_co + ci * s_ci + (tap / 3) * s_kh + (tap % 3) * s_kw];
+        wf[i] = v;                                            // [co][tap][ci]
+        wd[((long)ci * 9 + tap) * cout + co] = v;             // [ci][tap][co]
+    }
+}
+}  // namespace
+
+extern "C" {
+
+// C[N1][N2] (ldc, fp32) = (accumulate ? C : 0) + A^T B over M rows; ws holds plx_gemm_tn_workspace floats
+int plx_gemm_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int N2, int lda, int ldb, int ldc,
+                const void* zero, int num_cus, int accumulate, void* stream) {
+    if (M <= 0 || N1 % 64 || N2 % 64 || lda % 8 || ldb % 8 || ldc % 4) return -1;
+    return run_tn<false>(A, B, C, ws, M, N1, N2, lda, ldb, ldc, zero, num_cus, accumulate, (hipStream_t)stream, {});
+}
+
+// ---- 3x3 / stride 1 / pad 1 convolution on NHWC bf16 (Cin, Cout multiples of 64) as implicit GEMMs
+// y[M][Cout] = sum_{tap, ci} x[shift_tap(m)][ci] * Wf[co][tap][ci]; stats as in plx_gemm_nt
+int plx_conv3x3_fwd(const void* x, const void* wf, void* y, int Nb, int H, int W, int Cin, int Cout,
+                    const void* zero, float* stats, void* stream) {
+    const int M = Nb * H * W;
+    if (M <= 0 || Cin % 64 || Cout % 64) return -1;
+    const ConvGeom g{H, W, Cin, 0};
+    hipStream_t s = (hipStream_t)stream;
+    if (Cout % 128 == 0)
+        return launch_nt<128, 128, 2, 2, true>(x, wf, y, M, Cout, 9 * Cin, Cin, 9 * Cin, Cout, zero, stats, s, g);
+    return launch_nt<256, 64, 4, 1, true>(x, wf, y, M, Cout, 9 * Cin, Cin, 9 * Cin, Cout, zero, stats, s, g);
+}
+
+// dx[M][Cin] = sum_{tap, co} dy[shift_-tap(m)][co] * Wd[ci][tap][co]
+int plx_conv3x3_dgrad(const void* dy, const void* wd, void* dx, int Nb, int H, int W, int Cin, int Cout,
+                      const void* zero, void* stream) {
+    const int M = Nb * H * W;
+    if (M <= 0 || Cin % 64 || Cout % 64) return -1;
+    const ConvGeom g{H, W, Cout, 1};
+    hipStream_t s = (hipStream_t)stream;
+    if (Cin % 128 == 0)
+        return launch_nt<128, 128, 2, 2, true>(dy, wd, dx, M, Cin, 9 * Cout, Cout, 9 * Cout, Cin, zero, nullptr, s, g);
+    return launch_nt<256, 64, 4, 1, true>(dy, wd, dx, M, Cin, 9 * Cout, Cout, 9 * Cout, Cin, zero, nullptr, s, g);
+}
+
+long plx_conv3x3_wgrad_workspace(int Nb, int H, int W, int Cin, int Cout, int num_cus) {
+    return plx_gemm_tn_workspace(Nb * H * W, Cout, 9 * Cin, num_cus);
+}
+
+// dW[co][tap][ci] (fp32, (+)=) = sum_m dy[m][co] * x[shift_tap(m)][ci]
+int plx_conv3x3_wgrad(const void* dy, const void* x, float* dw, float* ws, int Nb, int H, int W, int Cin, int Cout,
+                      const void* zero, int num_cus, int accumulate, void* stream) {
+    const int M = Nb * H * W;
+    if (M <= 0 || Cin % 64 || Cout % 64) return -1;
+    const ConvGeom g{H, W, Cin, 0};
+    return run_tn<true>(dy, x, dw, ws, M, Cout, 9 * Cin, Cout, Cin, 9 * Cin, zero, num_cus, accumulate,
+                        (hipStream_t)stream, g);
+}
+
+int plx_weight_prep3(const float* w, long s_co, long s_ci, long s_kh, long s_kw, void* wf, void* wd, int cout, int cin,
+                     void* stream) {
+    const long total = (long)cout * cin * 9;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(weight_prep3_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, s_co, s_ci, s_kh, s_kw,
+                       (__bf16*)wf, (__bf16*)wd, cout, cin);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

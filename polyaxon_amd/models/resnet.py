@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 
 from polyaxon_amd.ops.conv1x1 import Conv1x1
+from polyaxon_amd.ops.conv3x3 import Conv3x3
 from polyaxon_amd.ops.norm import BatchNormAct
 from polyaxon_amd.ops.pool import MaxPool3s2
 
@@ -25,10 +26,11 @@ class Bottleneck(nn.Module):
                  fused: bool = True, native_conv: bool = True):
         super().__init__()
         out_ch = width * self.expansion
-        # stride-1 1x1 convs run as MFMA GEMMs on the NHWC rows (ops/conv1x1.py); the 3x3 stays on MIOpen
+        # stride-1 1x1 and 3x3 convs run as (implicit) MFMA GEMMs on the NHWC rows (ops/conv1x1.py, conv3x3.py);
+        # the strided 3x3, the downsample and the stem stay on MIOpen
         self.conv1 = Conv1x1(in_ch, width, native=native_conv)
         self.bn1 = BatchNormAct(width, act=True, fused=fused)
-        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.conv2 = Conv3x3(width, width, stride, native=native_conv)
         self.bn2 = BatchNormAct(width, act=True, fused=fused)
         self.conv3 = Conv1x1(width, out_ch, native=native_conv)
         # bn3 fuses the residual add and the final ReLU: y = relu(bn(x) + identity)

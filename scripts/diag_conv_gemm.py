@@ -67,6 +67,49 @@ def main():
               f"plx {fl / b / 1e9:.0f} TF  parts " + " ".join(f"{k}={v:.3f}" for k, v in pt.items())
               + f"  roofline~{byts / 6.3e9:.3f} ms", flush=True)
     print(f"total miopen {tot['miopen']:.3f} ms  plx {tot['plx']:.3f} ms")
+    conv3()
+
+
+def conv3():
+    """3x3 stride-1 convs of ResNet-50: MIOpen vs the implicit-GEMM kernels (kernel time per pass)."""
+    from polyaxon_amd.ops import _native
+    from polyaxon_amd.ops.conv1x1 import _num_cus, _stream, _zero_page
+    from polyaxon_amd.ops.conv3x3 import conv3x3, weight_prep3
+
+    lib = _native.lib("plx_conv")
+    for n, c, h, w in [(256, 64, 56, 56), (256, 128, 28, 28), (256, 256, 14, 14), (256, 512, 7, 7)]:
+        x = torch.randn(n, c, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        wt = (torch.randn(c, c, 3, 3, device=dev) * 0.05).contiguous(memory_format=torch.channels_last)
+        g = torch.randn(n, c, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        xm = x.clone().requires_grad_()
+        wm = wt.to(torch.bfloat16).requires_grad_()
+
+        def miopen():
+            xm.grad = None
+            wm.grad = None
+            F.conv2d(xm, wm, padding=1).backward(g)
+
+        wf, wd = weight_prep3(wt)
+        y = torch.empty_like(x)
+        dx = torch.empty_like(x)
+        z = _zero_page(dev).data_ptr()
+        cus = _num_cus(dev)
+        ws = torch.empty(int(lib.plx_conv3x3_wgrad_workspace(n, h, w, c, c, cus)), device=dev)
+        dw = torch.empty(c, 9, c, device=dev)
+        parts = {
+            "fwd": lambda: lib.plx_conv3x3_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), n, h, w, c, c, z, None,
+                                               _stream()),
+            "dgrad": lambda: lib.plx_conv3x3_dgrad(g.data_ptr(), wd.data_ptr(), dx.data_ptr(), n, h, w, c, c, z,
+                                                   _stream()),
+            "wgrad": lambda: lib.plx_conv3x3_wgrad(g.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), n, h, w,
+                                                   c, c, z, cus, 0, _stream()),
+        }
+        a = min(timeit(miopen) for _ in range(3))
+        pt = {k: min(timeit(f) for _ in range(2)) for k, f in parts.items()}
+        fl = 2 * n * h * w * c * c * 9
+        print(f"3x3 {(n, c, h, w)}  miopen fwd+bwd {a:.3f} ms  plx " +
+              " ".join(f"{k}={v:.3f}({fl / v / 1e9:.0f}TF)" for k, v in pt.items()) + f"  sum {sum(pt.values()):.3f}",
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -131,3 +131,37 @@ def test_conv_stats_feed_batchnorm(cuda):
                      conv.weight.grad.clone()))
     for a, b in zip(*outs):
         torch.testing.assert_close(a, b, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("shape,cout", [((2, 64, 7, 9), 64), ((3, 128, 10, 6), 128), ((2, 64, 5, 5), 256),
+                                        ((4, 256, 14, 14), 64), ((1, 64, 1, 1), 128)])
+def test_conv3x3_autograd(cuda, shape, cout):
+    from polyaxon_amd.ops.conv3x3 import Conv3x3, supported
+
+    torch.manual_seed(6)
+    conv = Conv3x3(shape[1], cout).to(cuda)
+    conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
+    x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert supported(x, conv)
+    xa = x.clone().requires_grad_()
+    y = conv(xa)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.float().clone().requires_grad_()
+    wr = conv.weight.detach().clone().requires_grad_()
+    yr = F.conv2d(xr, wr.to(torch.bfloat16).float(), padding=1)
+    yr.backward(g.float())
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=8e-2)
+    torch.testing.assert_close(xa.grad.float(), xr.grad, rtol=2e-2, atol=8e-2)
+    torch.testing.assert_close(conv.weight.grad, wr.grad, rtol=2e-2, atol=0.2)
+
+
+def test_conv3x3_stats(cuda):
+    from polyaxon_amd.ops.conv3x3 import conv3x3
+
+    x = torch.randn(2, 64, 9, 11, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(128, 64, 3, 3, device=cuda) * 0.05
+    y = conv3x3(x, w, with_stats=True)
+    st, nblk = y._plx_channel_stats
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, 128)
+    torch.testing.assert_close(st.view(2, nblk, 128)[0].sum(0), yf.sum(0), rtol=1e-4, atol=1e-2)
