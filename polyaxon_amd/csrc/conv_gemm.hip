@@ -69,7 +69,7 @@ template <int BM, int BN, int WGM, int WGN, bool CONV>
 __global__ void __launch_bounds__(NTHREADS, 2)
 gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
                int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
-               float* __restrict__ stats, ConvGeom geo) {
+               float* __restrict__ stats, ConvGeom geo, const __bf16* __restrict__ D, int ldd) {
     constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
     constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -189,8 +189,22 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     const int rows = min(BM, M - m0);
     for (int i = tid; i < BM * CHUNKS; i += NTHREADS) {
         const int r = i / CHUNKS, c = i % CHUNKS;
-        if (r < rows)
-            *(uint4*)(C + (size_t)(m0 + r) * ldc + n0 + c * 8) = *(const uint4*)(smem + r * CROW + c * 16);
+        if (r >= rows) continue;
+        uint4 v = *(const uint4*)(smem + r * CROW + c * 16);
+        if (D != nullptr) {
+            // C = A.B^T + D (a second gradient into the same tensor, e.g. the residual branch's): added in fp32
+            // and rounded once, instead of a separate bf16 add pass over both tensors
+            const uint4 d = *(const uint4*)(D + (size_t)(m0 + r) * ldd + n0 + c * 8);
+            uint32_t* pv = (uint32_t*)&v;
+            const uint32_t* pd = (const uint32_t*)&d;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float lo = __uint_as_float(pv[j] << 16) + __uint_as_float(pd[j] << 16);
+                const float hi = __uint_as_float(pv[j] & 0xffff0000u) + __uint_as_float(pd[j] & 0xffff0000u);
+                pv[j] = pack_bf16x2(lo, hi);
+            }
+        }
+        *(uint4*)(C + (size_t)(m0 + r) * ldc + n0 + c * 8) = v;
     }
     if (stats != nullptr) {
         // per-channel partial sum / sum of squares of the bf16-rounded outputs over this block's rows:
@@ -413,7 +427,8 @@ int set_lds(KernelT k, int bytes) {
 
 template <int BM, int BN, int WGM, int WGN, bool CONV = false>
 int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-              const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}) {
+              const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}, const void* D = nullptr,
+              int ldd = 0) {
     constexpr int LDS = 2 * (BM + BN) * BK * 2;
     static_assert(BM * (BN * 2 + 16) + 2 * NTHREADS * 4 <= LDS, "epilogue staging must fit the k-loop LDS");
     auto k = gemm_nt_kernel<BM, BN, WGM, WGN, CONV>;
@@ -421,11 +436,11 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
     if (attr) return attr;
     const int nwg = ((M + BM - 1) / BM) * (N / BN);
     hipLaunchKernelGGL(k, dim3(nwg), dim3(NTHREADS), LDS, s, (const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N,
-                       K, lda, ldb, ldc, (const __bf16*)zero, stats, geo);
+                       K, lda, ldb, ldc, (const __bf16*)zero, stats, geo, (const __bf16*)D, ldd);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-// m-slicing of the weight-gradient GEMM: ~2 blocks per CU, >= 8 k-stages per block, slabs <= 16 MB
+// m-slicing of the weight-gradient GEMM
 struct TnPlan { int kchunk, slices; };
 
 inline void tn_tile(int N1, int N2, int& bn1, int& bn2) {
@@ -438,9 +453,11 @@ inline TnPlan tn_plan(int M, int N1, int N2, int num_cus) {
     tn_tile(N1, N2, bn1, bn2);
     const int ntiles = (N1 / bn1) * (N2 / bn2);
     const long plane = (long)N1 * N2;
+    // ~4 blocks per CU (one 4-wave block per CU leaves each SIMD a single wave: latency-bound), >= 4
+    // k-stages per block, slabs <= 32 MB (they are re-read by the reducer, mostly from the infinity cache)
     int slices = (4 * (num_cus > 0 ? num_cus : 256)) / ntiles;
     const int by_depth = M / (4 * BK);
-    const int by_bytes = (int)((16l << 20) / (plane * 4));
+    const int by_bytes = (int)((32l << 20) / (plane * 4));
     if (slices > by_depth) slices = by_depth;
     if (slices > by_bytes) slices = by_bytes;
     if (slices < 1) slices = 1;
@@ -470,12 +487,13 @@ extern "C" {
 int plx_gemm_nt_rows_per_block(int N) { return N % 128 == 0 ? 128 : 256; }
 
 // stats (nullable): fp32 [2][ceil(M / rows_per_block)][N] per-block channel sums / sums of squares of C
+// D (nullable, bf16 [M][N], ldd): added to the product (C = A.B^T + D); not reflected in stats
 int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                const void* zero, float* stats, void* stream) {
-    if (M <= 0 || N % 64 || K % BK || lda % 8 || ldb % 8 || ldc % 8) return -1;
+                const void* zero, float* stats, const void* D, int ldd, void* stream) {
+    if (M <= 0 || N % 64 || K % BK || lda % 8 || ldb % 8 || ldc % 8 || (D != nullptr && ldd % 8)) return -1;
     hipStream_t s = (hipStream_t)stream;
-    if (N % 128 == 0) return launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s);
-    return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s);
+    if (N % 128 == 0) return launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd);
+    return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd);
 }
 
 // floats of slab workspace plx_gemm_tn needs for this problem

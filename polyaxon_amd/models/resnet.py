@@ -13,7 +13,7 @@ from typing import List, Optional, Type
 import torch
 import torch.nn as nn
 
-from polyaxon_amd.ops.conv1x1 import Conv1x1
+from polyaxon_amd.ops.conv1x1 import Conv1x1, GradMailbox
 from polyaxon_amd.ops.conv3x3 import Conv3x3
 from polyaxon_amd.ops.norm import BatchNormAct
 from polyaxon_amd.ops.pool import MaxPool3s2
@@ -38,7 +38,13 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
+        if self.downsample is None:
+            # identity block: bn3's residual gradient is added inside conv1's dgrad GEMM (ops.conv1x1.GradMailbox)
+            box = GradMailbox() if (self.training and torch.is_grad_enabled() and x.requires_grad) else None
+            out = self.bn1(self.conv1(x, grad_box=box))
+            out = self.bn2(self.conv2(out))
+            return self.bn3(self.conv3(out), x, residual_grad_box=box)
+        identity = self.downsample(x)
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))
         return self.bn3(self.conv3(out), identity)

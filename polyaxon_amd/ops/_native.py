@@ -174,7 +174,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
                                _P, _P],
     },
     "plx_conv": {
-        "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P],
+        "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P],
         "plx_gemm_nt_rows_per_block": [_I],
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],

@@ -32,7 +32,7 @@ def supported(x: torch.Tensor) -> bool:
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, ext=None):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, ext=None, box=None):
         lib = _native.lib("plx_bn")
         x = _cl(x)
         n, c, h, w = x.shape
@@ -68,6 +68,7 @@ class _BNAct(torch.autograd.Function):
         ctx.save_for_backward(x, mask, weight, stats)
         ctx.relu = relu
         ctx.has_res = residual is not None
+        ctx.box = box if (box is not None and box.armed and residual is not None) else None
         ctx.ws = ws
         return y
 
@@ -91,18 +92,22 @@ class _BNAct(torch.autograd.Function):
             m, c, weight.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(), dgb.data_ptr(), dgb[c:].data_ptr(),
             coef.data_ptr(), partials.data_ptr(), int(ctx.relu), _stream())
         _native.check(rc, "plx_bn_backward")
-        return dx, dgb[:c], dgb[c:], None, None, dres, None, None, None, None
+        if ctx.box is not None:  # the residual's gradient rides into conv1's dgrad epilogue (ops.conv1x1)
+            ctx.box.put(dres)
+            dres = None
+        return dx, dgb[:c], dgb[c:], None, None, dres, None, None, None, None, None
 
 
 def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
            running_var: Optional[torch.Tensor], training: bool, momentum: float, eps: float,
-           residual: Optional[torch.Tensor], act: bool, ext_stats=None) -> torch.Tensor:
+           residual: Optional[torch.Tensor], act: bool, ext_stats=None, residual_grad_box=None) -> torch.Tensor:
     """``ext_stats`` = (fp32 [2][nblk][C] channel sums / sums of squares of ``x``, nblk) from the op that
     produced ``x`` (the 1x1-conv GEMM epilogue); training mode then skips the stats pass."""
     if residual is not None and residual.dtype != x.dtype:
         residual = residual.to(x.dtype)
     if training:
-        return _BNAct.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, act, ext_stats)
+        return _BNAct.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, act, ext_stats,
+                            residual_grad_box)
     # inference: fold running stats into scale/bias, one apply pass
     lib = _native.lib("plx_bn")
     x = _cl(x)

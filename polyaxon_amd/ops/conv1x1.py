@@ -50,9 +50,11 @@ def nt_stats_rows(n: int) -> int:
     return int(_native.lib("plx_conv").plx_gemm_nt_rows_per_block(n))
 
 
-def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, stats: torch.Tensor = None) -> torch.Tensor:
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, stats: torch.Tensor = None,
+            add: torch.Tensor = None) -> torch.Tensor:
     """out[M][N] = a[M][K] · b[N][K]ᵀ, bf16 (rows may be strided, K contiguous).  ``stats`` (fp32
-    [2][ceil(M / nt_stats_rows(N))][N]) receives per-block channel sums and sums of squares of ``out``."""
+    [2][ceil(M / nt_stats_rows(N))][N]) receives per-block channel sums and sums of squares of ``out``;
+    ``add`` (bf16 [M][N]) is summed into the product in the epilogue."""
     m, k = a.shape
     n = b.shape[0]
     if out is None:
@@ -62,9 +64,13 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, stats: t
     if stats is not None:
         nblk = -(-m // nt_stats_rows(n))
         assert stats.dtype == torch.float32 and stats.is_contiguous() and stats.numel() >= 2 * nblk * n
+    if add is not None:
+        assert add.shape == (m, n) and add.stride(1) == 1 and add.dtype == torch.bfloat16 and add.data_ptr() % 16 == 0
     rc = _native.lib("plx_conv").plx_gemm_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0),
                                              b.stride(0), out.stride(0), _zero_page(a.device).data_ptr(),
-                                             stats.data_ptr() if stats is not None else None, _stream())
+                                             stats.data_ptr() if stats is not None else None,
+                                             add.data_ptr() if add is not None else None,
+                                             add.stride(0) if add is not None else 0, _stream())
     _native.check(rc, "plx_gemm_nt")
     return out
 
@@ -101,6 +107,30 @@ def weight_prep(w: torch.Tensor):
     return wb, wt
 
 
+class GradMailbox:
+    """Hands a gradient from a later op's backward to an earlier op's backward that consumes the same tensor.
+
+    In a ResNet identity block the block input feeds conv1 and the residual add of bn3; autograd would sum the
+    two gradients with a separate bf16 add over the whole activation.  Instead bn3's backward ``put``s its
+    residual gradient here and conv1's backward adds it in its data-gradient GEMM epilogue.  conv1 runs before
+    bn3 in the forward, so it ``arm``s the box only when it took the native path that will consume it; bn3
+    defers its gradient only into an armed box.  Reverse-topological backward order guarantees bn3's backward
+    (later in the forward) runs before conv1's."""
+
+    __slots__ = ("armed", "grad")
+
+    def __init__(self):
+        self.armed = False
+        self.grad = None
+
+    def put(self, g: torch.Tensor) -> None:
+        self.grad = g if self.grad is None else self.grad + g
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
 def _rows(t: torch.Tensor) -> torch.Tensor:
     """[N,C,H,W] channels_last -> [N*H*W, C] view."""
     n, c, h, w = t.shape
@@ -109,8 +139,9 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stats):
+    def forward(ctx, x, weight, stats, box):
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        ctx.box = box
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         wb, wt = weight_prep(weight)
@@ -126,12 +157,15 @@ class _Conv1x1(torch.autograd.Function):
         x, wt = ctx.saved_tensors
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
+        extra = ctx.box.take() if ctx.box is not None else None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            gemm_nt(_rows(dy), wt, _rows(dx))
+            if extra is not None:
+                extra = extra.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            gemm_nt(_rows(dy), wt, _rows(dx), add=_rows(extra) if extra is not None else None)
         if ctx.needs_input_grad[1]:
             dw = gemm_tn(_rows(dy), _rows(x)).view(ctx.wshape).to(ctx.wdtype)
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 def _bf16_context(x: torch.Tensor) -> bool:
@@ -147,7 +181,8 @@ def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
             and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0 and x.numel() > 0)
 
 
-def conv1x1(x: torch.Tensor, weight: torch.Tensor, with_stats: bool = False) -> torch.Tensor:
+def conv1x1(x: torch.Tensor, weight: torch.Tensor, with_stats: bool = False,
+            grad_box: "GradMailbox" = None) -> torch.Tensor:
     """With ``with_stats`` the output carries ``_plx_channel_stats`` = (fp32 [2][nblk][Cout] per-block channel
     sums / sums of squares, nblk), which a following fused BatchNorm uses instead of its own stats pass."""
     stats = None
@@ -156,7 +191,9 @@ def conv1x1(x: torch.Tensor, weight: torch.Tensor, with_stats: bool = False) -> 
         m, cout = n * h * w, weight.shape[0]
         nblk = -(-m // nt_stats_rows(cout))
         stats = torch.empty(2 * nblk * cout, dtype=torch.float32, device=x.device)
-    y = _Conv1x1.apply(x, weight, stats)
+    if grad_box is not None:
+        grad_box.armed = True
+    y = _Conv1x1.apply(x, weight, stats, grad_box)
     if stats is not None:
         y._plx_channel_stats = (stats, nblk)
     return y
@@ -171,7 +208,7 @@ class Conv1x1(nn.Conv2d):
         self.native = native
         self.bn_stats = bn_stats  # emit channel stats for the BatchNorm that follows (training only)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, grad_box: GradMailbox = None) -> torch.Tensor:
         if self.native and supported(x, self):
-            return conv1x1(x, self.weight, with_stats=self.bn_stats and self.training)
+            return conv1x1(x, self.weight, with_stats=self.bn_stats and self.training, grad_box=grad_box)
         return F.conv2d(x, self.weight, None, self.stride)
