@@ -11,6 +11,9 @@ import csv
 import sys
 
 CLASSES = [
+    ("conv GEMM (plx MFMA: 1x1, 3x3 implicit, wgrad slabs)", ("gemm_nt_kernel", "gemm_tn_kernel", "slab_reduce",
+                                                           "weight_prep")),
+    ("pool (plx)", ("maxpool_fwd", "maxpool_bwd")),
     ("conv (MIOpen igemm/CK/naive)", ("igemm", "conv", "ck::tensor_operation", "naive_conv", "gtcx")),
     ("fused BN+add+ReLU (plx)", ("bn_stats", "bn_apply", "bn_bwd", "bn_fwd", "bn_partial")),
     ("BN (MIOpen)", ("MIOpenBatchNorm",)),
