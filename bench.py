@@ -188,6 +188,7 @@ def main() -> int:
             "train_images_per_s": round(total_steps * args.batch / elapsed_max, 1),
             "graph_capture_s": round(capture_s, 2),
             "hip_graph": ex.graph is not None,
+            "graph_check_error": ex.graph_check_error,
             "fused_bn": not args.unfused,
             "mfma_1x1_conv": not args.miopen_1x1,
         }

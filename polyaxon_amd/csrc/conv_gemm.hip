@@ -234,7 +234,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
 
 // ------------------------------------------------------------------------------------------- TN GEMM
 // W[slice][N1][N2] (fp32 slab per m-slice, ld = N2) = sum_{m in slice} A[m][N1] (lda) * B[m][N2] (ldb).
-// The slabs are summed by slab_reduce_kernel (the guide's slab reducer).  The first version accumulated with
+// The slabs are summed by slab_partial_kernel / slab_final_kernel (the guide's slab reducer).  The first version accumulated with
 // per-element fp32 atomics instead; on the 7x7 layers (16 slices into one 4 MB output) its weight gradient ran
 // at half the forward GEMM's rate.
 // LDS images are [BK rows = m][BNx cols] in natural row order; MFMA fragments come from ds_read_b64_tr_b16
@@ -368,13 +368,13 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
         }
 }
 
-// C[i][j] (ldc) (+)= sum_s W[s][i][j]; one float4 per thread.  blockIdx.y picks a group of `per_group`
-// slices so a small output with many slices still spreads over the chip; with more than one group the
-// groups combine with fp32 atomics into C (zeroed by the host unless accumulating).
-__global__ void slab_reduce_kernel(const float* __restrict__ W, float* __restrict__ C, int N1, int N2, int ldc,
-                                   int slices, int per_group, int direct, int accumulate) {
-    const long total4 = (long)N1 * N2 / 4;
-    const long plane = (long)N1 * N2;
+// Slab reduction, deterministic and graph-capturable (no memset, no atomics):
+//   slab_partial_kernel  P[g][i] = sum of slabs [g*per_group, (g+1)*per_group)   (only when many slabs)
+//   slab_final_kernel    C[i][j] (ldc) (+)= sum_s S[s][i][j]
+// one float4 per thread; blockIdx.y = group in the partial pass.
+__global__ void slab_partial_kernel(const float* __restrict__ W, float* __restrict__ P, long plane, int slices,
+                                    int per_group) {
+    const long total4 = plane / 4;
     const int s0 = blockIdx.y * per_group, s1 = min(slices, s0 + per_group);
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -382,21 +382,28 @@ __global__ void slab_reduce_kernel(const float* __restrict__ W, float* __restric
             const float4 v = ((const float4*)(W + s * plane))[i];
             acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
         }
+        ((float4*)(P + blockIdx.y * plane))[i] = acc;
+    }
+}
+
+__global__ void slab_final_kernel(const float* __restrict__ S, float* __restrict__ C, int N1, int N2, int ldc,
+                                  int nslabs, int accumulate) {
+    const long total4 = (long)N1 * N2 / 4;
+    const long plane = (long)N1 * N2;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total4; i += (long)gridDim.x * blockDim.x) {
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int s = 0; s < nslabs; ++s) {
+            const float4 v = ((const float4*)(S + s * plane))[i];
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
         const long e = i * 4;
         const int r = (int)(e / N2), c = (int)(e % N2);
         float* dst = C + (size_t)r * ldc + c;
-        if (direct) {
-            if (accumulate) {
-                const float4 o = *(const float4*)dst;
-                acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
-            }
-            *(float4*)dst = acc;
-        } else {
-            unsafeAtomicAdd(dst, acc.x);
-            unsafeAtomicAdd(dst + 1, acc.y);
-            unsafeAtomicAdd(dst + 2, acc.z);
-            unsafeAtomicAdd(dst + 3, acc.w);
+        if (accumulate) {
+            const float4 o = *(const float4*)dst;
+            acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
         }
+        *(float4*)dst = acc;
     }
 }
 
@@ -441,7 +448,7 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
 }
 
 // m-slicing of the weight-gradient GEMM
-struct TnPlan { int kchunk, slices; };
+struct TnPlan { int kchunk, slices, groups, per_group, blocks; };
 
 inline void tn_tile(int N1, int N2, int& bn1, int& bn2) {
     bn1 = N1 % 128 == 0 ? 128 : 64;
@@ -463,7 +470,17 @@ inline TnPlan tn_plan(int M, int N1, int N2, int num_cus) {
     if (slices < 1) slices = 1;
     int kchunk = (M + slices - 1) / slices;
     kchunk = ((kchunk + BK - 1) / BK) * BK;
-    return {kchunk, (M + kchunk - 1) / kchunk};
+    slices = (M + kchunk - 1) / kchunk;
+    // reducer: ~1024 blocks; many slabs are first summed in groups of >= 8 so a small plane still spreads out
+    const long total4 = plane / 4;
+    int blocks = (int)((total4 + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    int groups = 1024 / blocks;
+    if (groups > slices / 8) groups = slices / 8;
+    if (groups < 1) groups = 1;
+    const int per_group = (slices + groups - 1) / groups;
+    groups = (slices + per_group - 1) / per_group;
+    return {kchunk, slices, groups, per_group, blocks};
 }
 
 template <int BN1, int BN2, int WG1, int WG2, bool CONV = false>
@@ -500,7 +517,7 @@ int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int 
 long plx_gemm_tn_workspace(int M, int N1, int N2, int num_cus) {
     if (M <= 0 || N1 % 64 || N2 % 64) return -1;
     const TnPlan p = tn_plan(M, N1, N2, num_cus);
-    return (long)p.slices * N1 * N2;
+    return (long)(p.slices + (p.groups > 1 ? p.groups : 0)) * N1 * N2;
 }
 
 }  // extern "C"
@@ -520,20 +537,17 @@ int run_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int
     else
         rc = launch_tn<64, 64, 2, 2, CONV>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
     if (rc) return rc;
-    const long total4 = (long)N1 * N2 / 4;
-    int blocks = (int)((total4 + 255) / 256);
-    if (blocks > 2048) blocks = 2048;
-    int groups = 1024 / blocks;                             // aim for ~1024 reducer blocks
-    if (groups > plan.slices / 8) groups = plan.slices / 8;  // but >= 8 slabs per group
-    if (groups < 1) groups = 1;
-    const int per_group = (plan.slices + groups - 1) / groups;
-    groups = (plan.slices + per_group - 1) / per_group;
-    const int direct = groups == 1;
-    if (!direct && !accumulate) {
-        if (hipMemset2DAsync(C, (size_t)ldc * 4, 0, (size_t)N2 * 4, N1, s) != hipSuccess) return -3;
+    const long plane = (long)N1 * N2;
+    const float* slabs = ws;
+    int nslabs = plan.slices;
+    if (plan.groups > 1) {
+        float* part = ws + (long)plan.slices * plane;
+        hipLaunchKernelGGL(slab_partial_kernel, dim3(plan.blocks, plan.groups), dim3(256), 0, s, ws, part, plane,
+                           plan.slices, plan.per_group);
+        slabs = part;
+        nslabs = plan.groups;
     }
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks, groups), dim3(256), 0, s, ws, C, N1, N2, ldc, plan.slices,
-                       per_group, direct, accumulate);
+    hipLaunchKernelGGL(slab_final_kernel, dim3(plan.blocks), dim3(256), 0, s, slabs, C, N1, N2, ldc, nslabs, accumulate);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -75,6 +75,8 @@ class ResidentTrialExecutor:
         self._init_tables = self.flat.init_tables(spec) if (spec is not None and self.is_cuda) else None
         self.use_graph = use_graph and self.is_cuda
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.graph_rejected = False
+        self.graph_check_error: Optional[float] = None
         self.snapshots: Dict[object, TrialState] = {}
         self.model.train()
 
@@ -122,10 +124,16 @@ class ResidentTrialExecutor:
             self.ring[s % self.ring_size] = float(loss)
             self.step += 1
 
-    def capture(self, warmup: int = 3) -> None:
-        """Warm up (MIOpen find, allocator) and capture the training step as a hipGraph."""
+    def capture(self, warmup: int = 3, verify: bool = True, tol: float = 0.05) -> bool:
+        """Warm up (MIOpen find, allocator) and capture the training step as a hipGraph.
+
+        With ``verify`` the graph is checked before it is trusted: one eager step and one replay run from the
+        same saved state and their parameter updates must agree to ``tol`` (relative, and finite).  A library
+        kernel that is not capture-safe (e.g. one relying on an uncaptured memset) shows up here as a diverging
+        update, and the executor stays eager instead of training on garbage.  Returns whether the graph is used.
+        """
         if not self.use_graph:
-            return
+            return False
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -138,6 +146,28 @@ class ResidentTrialExecutor:
             self._train_step()
         torch.cuda.synchronize(self.device)
         self.graph = g
+        if verify and not self._verify_graph(tol):
+            self.graph = None
+            self.graph_rejected = True
+        return self.graph is not None
+
+    def _verify_graph(self, tol: float) -> bool:
+        key = "__graph_check__"
+        self.snapshot(key)
+        p0 = self.flat.params.detach().clone()
+        self.graph, g = None, self.graph
+        self.run(1)  # eager
+        d_eager = self.flat.params.detach() - p0
+        self.restore(key)
+        self.graph = g
+        self.run(1)  # replay
+        d_graph = self.flat.params.detach() - p0
+        self.restore(key)
+        self.drop(key)
+        torch.cuda.synchronize(self.device)
+        err = float((d_eager - d_graph).norm() / (d_eager.norm() + 1e-12))
+        self.graph_check_error = err
+        return bool(torch.isfinite(d_graph).all()) and err < tol
 
     # ------------------------------------------------------------------ trial lifecycle
     def reset(self, seed: int) -> None:

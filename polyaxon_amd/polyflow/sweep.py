@@ -128,15 +128,16 @@ class HyperbandSweep:
                     configs[cid] = dict(configs[cid], **{self.resource_name: r})
             self.metrics.reset_bracket(0, len(active))
             it.experiment_ids = list(active)
+            rung: List[TrialRecord] = []
             for slot, cid in enumerate(active):
-                self._run_trial(it, cid, configs[cid], slot, prev_r.get(cid))
+                rung.append(self._run_trial(it, cid, configs[cid], slot, prev_r.get(cid)))
                 if max_trials is not None and self._trial >= max_trials:
                     return self.result
             # rung decision on the device: one top-k launch, one small D2H read
             order = self.metrics.order(self.maximize)[0].cpu().tolist()
             vals = self.metrics.values[0, : len(active)].cpu().tolist()
             it.experiments_metrics = [(cid, vals[i]) for i, cid in enumerate(active) if not math.isnan(vals[i])]
-            for rec in self.result.trials[-len(active):]:
+            for rec in rung:
                 rec.metric = vals[rec.slot]
             self._update_best(active, vals, configs)
             if m.is_done(it):

@@ -11,7 +11,7 @@ import csv
 import sys
 
 CLASSES = [
-    ("conv GEMM (plx MFMA: 1x1, 3x3 implicit, wgrad slabs)", ("gemm_nt_kernel", "gemm_tn_kernel", "slab_reduce",
+    ("conv GEMM (plx MFMA: 1x1, 3x3 implicit, wgrad slabs)", ("gemm_nt_kernel", "gemm_tn_kernel", "slab_partial", "slab_final",
                                                            "weight_prep")),
     ("pool (plx)", ("maxpool_fwd", "maxpool_bwd")),
     ("conv (MIOpen igemm/CK/naive)", ("igemm", "conv", "ck::tensor_operation", "naive_conv", "gtcx")),
