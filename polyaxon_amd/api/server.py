@@ -19,7 +19,7 @@ import os
 import time
 from typing import Any, Dict, List, Optional
 
-from fastapi import Depends, FastAPI, Header, HTTPException, Request
+from fastapi import Depends, FastAPI, Header, HTTPException, Query, Request
 from fastapi.responses import FileResponse, JSONResponse, PlainTextResponse, StreamingResponse
 
 from polyaxon_amd import __version__
@@ -41,10 +41,11 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
     internal = internal_token or os.environ.get("POLYAXON_SECRET_INTERNAL_TOKEN")
 
     # ------------------------------------------------------------------ auth
-    def auth(authorization: Optional[str] = Header(None),
-             x_polyaxon_internal: Optional[str] = Header(None)) -> Dict[str, Any]:
+    def identify(authorization: Optional[str], x_polyaxon_internal: Optional[str], token: Optional[str]):
         if not require_auth:
             return {"username": "root", "is_superuser": 1}
+        if authorization is None and token:  # EventSource (dashboard streams) cannot set headers
+            authorization = f"token {token}"
         if x_polyaxon_internal and internal and authorization == f"token {internal}":
             return {"username": "internal", "is_superuser": 1}
         if authorization and authorization.lower().startswith("token "):
@@ -56,6 +57,30 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
             if eph:
                 return {"username": eph["user"], "is_superuser": 0, "scope": eph}
         raise HTTPException(401, "Authentication credentials were not provided or are invalid.")
+
+    def auth(request: Request, authorization: Optional[str] = Header(None),
+             x_polyaxon_internal: Optional[str] = Header(None),
+             token: Optional[str] = Query(None)) -> Dict[str, Any]:
+        """Authenticate, then authorise project-scoped routes (reference libs/permissions/projects.py):
+        superusers and the owner may do anything; other users may only read public projects; an ephemeral
+        token may only touch its own experiment."""
+        user = identify(authorization, x_polyaxon_internal, token)
+        pp = request.path_params
+        if user.get("is_superuser") or "username" not in pp or "project" not in pp:
+            return user
+        scope = user.get("scope")
+        if scope is not None:
+            xid = pp.get("xid")
+            if xid is None or int(xid) != int(scope.get("experiment", -1)):
+                raise HTTPException(403, "ephemeral token is scoped to another experiment")
+            return user
+        owner = pp["username"]
+        if user.get("username") == owner:
+            return user
+        proj = store.get_project(pp["project"], owner)
+        if request.method in ("GET", "HEAD") and (proj is None or proj.get("is_public")):
+            return user
+        raise HTTPException(403, "You do not have permission to perform this action.")
 
     def project_or_404(user: str, project: str) -> Dict[str, Any]:
         p = store.get_project(project, user)
@@ -92,6 +117,14 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
             rows = rows[offset: offset + limit]
         return {"count": total, "results": rows}
 
+    # ------------------------------------------------------------------ dashboard (static page over this API)
+    static = os.path.join(os.path.dirname(os.path.abspath(__file__)), "static", "index.html")
+
+    @app.get("/", include_in_schema=False)
+    @app.get("/ui", include_in_schema=False)
+    def dashboard():
+        return FileResponse(static, media_type="text/html")
+
     # ------------------------------------------------------------------ health / status / versions
     @app.get("/_health")
     def health():
@@ -116,6 +149,26 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
     @app.get("/api/v1/users")
     def me(user=Depends(auth)):
         return {k: v for k, v in user.items() if k != "token"}
+
+    def superuser(user=Depends(auth)):
+        if not user.get("is_superuser"):
+            raise HTTPException(403, "superuser only")
+        return user
+
+    @app.post("/api/v1/users", status_code=201)
+    async def create_user(request: Request, user=Depends(superuser)):
+        """Create a user and return its API token (reference `createuser` management command)."""
+        body = await request.json()
+        if not body.get("username") or store.get_user(body["username"]):
+            raise HTTPException(400, "missing or existing username")
+        u = store.create_user(body["username"], body.get("email", ""), bool(body.get("is_superuser")))
+        flow.auditor.record("user.registered", "user", u["id"], user.get("username"))
+        return u
+
+    @app.get("/api/v1/users/list")
+    def list_users(user=Depends(superuser)):
+        rows = store.execute("SELECT id, username, email, is_superuser, created_at FROM users ORDER BY id").fetchall()
+        return {"results": [dict(r) for r in rows]}
 
     @app.get("/api/v1/projects")
     def list_projects(request: Request, user=Depends(auth)):

@@ -625,6 +625,36 @@ for _plugin in ("notebook", "tensorboard"):
     _mk_plugin()
 
 
+@cli.command()
+@click.pass_obj
+def whoami(c):
+    """Show the authenticated user (server mode) or the configured local user."""
+    if c.host:
+        out(c.api("GET", "/api/v1/users"), c.fmt)
+    else:
+        out({"username": c.user, "mode": "local", "root": c.cfg["root"]}, c.fmt)
+
+
+@cli.group()
+def user():
+    """Users (reference `createuser` management command)."""
+
+
+@user.command("create")
+@click.argument("username")
+@click.option("--email", default="")
+@click.option("--superuser", is_flag=True)
+@click.pass_obj
+def user_create(c, username, email, superuser):
+    if c.host:
+        u = c.api("POST", "/api/v1/users", {"username": username, "email": email, "is_superuser": superuser})
+    else:
+        if c.store.get_user(username):
+            raise click.ClickException(f"user {username} exists")
+        u = c.store.create_user(username, email, superuser)
+    click.echo(f"created user {u['username']} token={u['token']}")
+
+
 @cli.group()
 def cluster():
     """Cluster (node + HIP devices)."""

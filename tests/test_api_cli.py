@@ -178,3 +178,40 @@ def test_cli_upload_and_run_snapshot(tmp_path, monkeypatch):
     (code / "train.py").write_text("print('snapshot v2')\n")
     r = runner.invoke(cli, ["-p", "up", "run", "-u", "-f", "xp.yml", "--gpus", "0"])
     assert r.exit_code == 0 and "snapshot v2" in r.output, r.output
+
+
+def test_dashboard_page_and_query_token(api):
+    client, flow = api
+    r = client.get("/", headers={"Authorization": ""})
+    assert r.status_code == 200 and "polyaxon-mi355x" in r.text and "EventSource" in r.text
+    # streams accept ?token= (EventSource cannot send headers)
+    xid = client.post("/api/v1/root/d/experiments",
+                      json={"content": {"version": 1, "kind": "experiment", "run": {"cmd": "echo hi"}}}).json()["id"]
+    flow.wait("experiment", xid, timeout=30)
+    del client.headers["Authorization"]
+    assert client.get("/api/v1/projects").status_code == 401
+    with client.stream("GET", f"/streams/v1/root/d/experiments/{xid}/logs", params={"token": TOKEN}) as s:
+        body = "".join(s.iter_text())
+    assert "hi" in body
+
+
+def test_users_and_project_permissions(api):
+    client, flow = api
+    assert client.post("/api/v1/projects", json={"name": "priv", "is_public": False}).status_code == 201
+    assert client.post("/api/v1/projects", json={"name": "pub"}).status_code == 201
+    r = client.post("/api/v1/users", json={"username": "alice"})
+    assert r.status_code == 201
+    alice = {"Authorization": f"token {r.json()['token']}"}
+    assert client.get("/api/v1/users", headers=alice).json()["username"] == "alice"
+    # alice: read public, not private; no writes into root's projects; not a superuser
+    assert client.get("/api/v1/root/pub/experiments", headers=alice).status_code == 200
+    assert client.get("/api/v1/root/priv/experiments", headers=alice).status_code == 403
+    content = {"version": 1, "kind": "experiment", "run": {"cmd": "true"}}
+    assert client.post("/api/v1/root/pub/experiments", json={"content": content}, headers=alice).status_code == 403
+    assert client.post("/api/v1/users", json={"username": "eve"}, headers=alice).status_code == 403
+    # her own project is fully hers
+    assert client.post("/api/v1/projects", json={"name": "mine"}, headers=alice).status_code == 201
+    r = client.post("/api/v1/alice/mine/experiments", json={"content": content}, headers=alice)
+    assert r.status_code == 201
+    assert flow.wait("experiment", r.json()["id"], timeout=30) == "succeeded"
+    assert [u["username"] for u in client.get("/api/v1/users/list").json()["results"]] == ["root", "alice"]
