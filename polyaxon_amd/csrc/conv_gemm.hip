@@ -26,18 +26,34 @@ typedef __attribute__((address_space(1))) const void gbl_void;
 
 constexpr int BK = 64;          // reduction depth per LDS stage (bf16 elements)
 
-// Implicit-GEMM geometry of a 3x3 / stride-1 / pad-1 convolution on NHWC rows: pixel row m = (n*H + h)*W + w,
-// reduction index k = tap*C + c with tap = 3*kh + kw.  The operand row for (m, tap) is the pixel shifted by
-// (kh-1, kw-1) (or by (1-kh, 1-kw) when `flip`, the data-gradient direction); out-of-image rows read the
-// zero page, which is exactly the zero padding.
+// Implicit-GEMM geometry of a convolution on NHWC rows (1x1 or 3x3, stride 1 or 2).
+// GEMM rows are pixels of a row grid (Hr x Wr per image): row m = (n*Hr + r)*Wr + c.  The reduction index is
+// k = t*C + ch over `ntaps` taps; for tap t the operand row is the source pixel (r*S + offh[t], c*S + offw[t])
+// of an H x W image (out-of-image -> the zero page, i.e. the zero padding), and the B operand column is
+// btap[t]*C + ch (B holds all 9 (or 1) taps).  Forward / weight-gradient use S = stride, off = tap - pad;
+// the stride-1 data gradient flips the taps (off = pad - tap); the stride-2 data gradient is split into the
+// four (ih, iw) parity classes of the input, each a stride-1 gather over the taps of matching parity, whose
+// output rows are scattered back to input pixels (2r + ph, 2c + pw) of an Hc x Wc grid (OS = 2).
 struct ConvGeom {
-    int H, W, C, flip;
+    int H, W;        // gathered (source) image
+    int Hr, Wr;      // row grid
+    int C, S, ntaps;
+    int Hc, Wc, OS, oph, opw;  // output-row scatter (OS == 0: row m is output row m)
+    signed char offh[9], offw[9], btap[9];
 };
 
-__device__ __forceinline__ void tap_shift(int tap, int flip, int& dh, int& dw) {
-    const int kh = tap / 3, kw = tap - 3 * (tap / 3);
-    dh = flip ? 1 - kh : kh - 1;
-    dw = flip ? 1 - kw : kw - 1;
+__device__ __forceinline__ void row_coords(int m, int Hr, int Wr, int& n, int& r, int& c) {
+    const int q = m / Wr;
+    c = m - q * Wr;
+    n = q / Hr;
+    r = q - n * Hr;
+}
+
+__device__ __forceinline__ size_t out_row(const ConvGeom& g, int m) {
+    if (g.OS == 0) return (size_t)m;
+    int n, r, c;
+    row_coords(m, g.Hr, g.Wr, n, r, c);
+    return ((size_t)n * g.Hc + r * g.OS + g.oph) * g.Wc + c * g.OS + g.opw;
 }
 constexpr int NTHREADS = 256;   // 4 waves
 
@@ -82,26 +98,30 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     const int m0 = tm * BM, n0 = tn * BN;
     const int wm = wave / WGN, wn = wave % WGN;
 
-    // conv mode: (h, w) of the A rows this thread stages, fixed over the whole k loop
-    int row_h[BM / 32], row_w[BM / 32];
+    // conv mode: image base and (r, c) of the A rows this thread stages, fixed over the whole k loop
+    int row_n[BM / 32], row_h[BM / 32], row_w[BM / 32];
     if constexpr (CONV) {
 #pragma unroll
         for (int i = 0; i < BM / 32; ++i) {
             const int gm = m0 + (i * 4 + wave) * 8 + (lane >> 3);
-            const int q = gm / geo.W;
-            row_w[i] = gm - q * geo.W;
-            row_h[i] = q - (q / geo.H) * geo.H;
+            int n, r, c;
+            row_coords(gm, geo.Hr, geo.Wr, n, r, c);
+            row_n[i] = n * geo.H * geo.W;
+            row_h[i] = r * geo.S;
+            row_w[i] = c * geo.S;
         }
     }
 
     // staging: each wave instruction moves 1024 B = 8 rows x 8 chunks; lane -> (row, physical chunk)
     auto stage = [&](int buf, int k0) {
         char* base = smem + buf * STAGE;
-        int dh = 0, dw = 0, c0 = k0;
+        int dh = 0, dw = 0, c0 = k0, bk0 = k0;
         if constexpr (CONV) {
-            const int tap = k0 / geo.C;
-            c0 = k0 - tap * geo.C;
-            tap_shift(tap, geo.flip, dh, dw);
+            const int t = k0 / geo.C;
+            c0 = k0 - t * geo.C;
+            dh = geo.offh[t];
+            dw = geo.offw[t];
+            bk0 = geo.btap[t] * geo.C + c0;
         }
 #pragma unroll
         for (int i = 0; i < BM / 32; ++i) {                 // A: BM rows / 8 rows per instr / 4 waves
@@ -112,7 +132,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
             if constexpr (CONV) {
                 const int ih = row_h[i] + dh, iw = row_w[i] + dw;
                 const bool ok = gm < M && (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
-                src = ok ? A + (size_t)(gm + dh * geo.W + dw) * lda + c0 + lc * 8 : zero;
+                src = ok ? A + ((size_t)row_n[i] + ih * geo.W + iw) * lda + c0 + lc * 8 : zero;
             } else {
                 src = gm < M ? A + (size_t)gm * lda + k0 + lc * 8 : zero;
             }
@@ -122,7 +142,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         for (int i = 0; i < BN / 32; ++i) {
             const int row = (i * 4 + wave) * 8 + (lane >> 3);
             const int lc = (lane & 7) ^ nt_swz(row);
-            glds16(B + (size_t)(n0 + row) * ldb + k0 + lc * 8, base + A_BYTES + (i * 4 + wave) * 1024);
+            glds16(B + (size_t)(n0 + row) * ldb + bk0 + lc * 8, base + A_BYTES + (i * 4 + wave) * 1024);
         }
     };
 
@@ -191,6 +211,8 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         const int r = i / CHUNKS, c = i % CHUNKS;
         if (r >= rows) continue;
         uint4 v = *(const uint4*)(smem + r * CROW + c * 16);
+        size_t orow = (size_t)(m0 + r);
+        if constexpr (CONV) orow = out_row(geo, m0 + r);
         if (D != nullptr) {
             // C = A.B^T + D (a second gradient into the same tensor, e.g. the residual branch's): added in fp32
             // and rounded once, instead of a separate bf16 add pass over both tensors
@@ -204,7 +226,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                 pv[j] = pack_bf16x2(lo, hi);
             }
         }
-        *(uint4*)(C + (size_t)(m0 + r) * ldc + n0 + c * 8) = v;
+        *(uint4*)(C + orow * ldc + n0 + c * 8) = v;
     }
     if (stats != nullptr) {
         // per-channel partial sum / sum of squares of the bf16-rounded outputs over this block's rows:
@@ -257,7 +279,7 @@ __device__ __forceinline__ s16x4 tr_read(const char* img, int row, int col /* el
 template <int ROWB, bool GATHER = false>
 __device__ __forceinline__ void stage_rows(char* img, const __bf16* __restrict__ G, int ld, int r0, int rend,
                                            int c0, const __bf16* __restrict__ zero, int wave, int lane,
-                                           ConvGeom geo = {}, int dh = 0, int dw = 0) {
+                                           const ConvGeom* geo = nullptr, int dh = 0, int dw = 0) {
     // BK rows x ROWB bytes, lane-linear image; 1024 B per wave instruction.  GATHER: row gr is the pixel
     // shifted by (dh, dw) (zero page outside the image), for the weight gradient of a 3x3 convolution.
     constexpr int INSTR = BK * ROWB / 1024;
@@ -269,10 +291,11 @@ __device__ __forceinline__ void stage_rows(char* img, const __bf16* __restrict__
         const int gr = r0 + row;
         const __bf16* src;
         if constexpr (GATHER) {
-            const int q = gr / geo.W;
-            const int w = gr - q * geo.W, h = q - (q / geo.H) * geo.H;
-            const bool ok = gr < rend && (unsigned)(h + dh) < (unsigned)geo.H && (unsigned)(w + dw) < (unsigned)geo.W;
-            src = ok ? G + (size_t)(gr + dh * geo.W + dw) * ld + c0 + lc * 8 : zero;
+            int n, r, c;
+            row_coords(gr, geo->Hr, geo->Wr, n, r, c);
+            const int ih = r * geo->S + dh, iw = c * geo->S + dw;
+            const bool ok = gr < rend && (unsigned)ih < (unsigned)geo->H && (unsigned)iw < (unsigned)geo->W;
+            src = ok ? G + (((size_t)n * geo->H + ih) * geo->W + iw) * ld + c0 + lc * 8 : zero;
         } else {
             src = gr < rend ? G + (size_t)gr * ld + c0 + lc * 8 : zero;
         }
@@ -310,14 +333,15 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
     // conv mode: N2 = 9*C and a BN2 tile lies inside one tap (C % BN2 == 0, host-checked)
     int bc0 = n20, dh = 0, dw = 0;
     if constexpr (CONV) {
-        const int tap = n20 / geo.C;
-        bc0 = n20 - tap * geo.C;
-        tap_shift(tap, 0, dh, dw);
+        const int t = n20 / geo.C;
+        bc0 = n20 - t * geo.C;
+        dh = geo.offh[t];
+        dw = geo.offw[t];
     }
     auto stage = [&](int buf, int k0) {
         char* base = smem + buf * STAGE;
         stage_rows<ROWA>(base, A, lda, k0, kend, n10, zero, wave, lane);
-        stage_rows<ROWB_, CONV>(base + A_BYTES, B, ldb, k0, kend, bc0, zero, wave, lane, geo, dh, dw);
+        stage_rows<ROWB_, CONV>(base + A_BYTES, B, ldb, k0, kend, bc0, zero, wave, lane, &geo, dh, dw);
     };
     if (nk > 0) {
         stage(0, kbeg);
@@ -551,18 +575,19 @@ int run_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-// fp32 weight [Cout][Cin][3][3] (any strides) -> bf16 Wf[Cout][tap][Cin] (forward B operand) and
-// Wd[Cin][tap][Cout] (data-gradient B operand; the tap flip lives in the gather, not in the copy)
-__global__ void weight_prep3_kernel(const float* __restrict__ w, long s_co, long s_ci, long s_kh, long s_kw,
-                                    __bf16* __restrict__ wf, __bf16* __restrict__ wd, int cout, int cin) {
-    const long total = (long)cout * cin * 9;
+// fp32 weight [Cout][Cin][K][K] (any strides) -> bf16 Wf[Cout][tap][Cin] (forward B operand) and
+// Wd[Cin][tap][Cout] (data-gradient B operand; tap flips / parity classes live in the gather, not in the copy)
+__global__ void weight_prepk_kernel(const float* __restrict__ w, long s_co, long s_ci, long s_kh, long s_kw,
+                                    __bf16* __restrict__ wf, __bf16* __restrict__ wd, int cout, int cin, int K) {
+    const int taps = K * K;
+    const long total = (long)cout * cin * taps;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         const int ci = (int)(i % cin);
         const long r = i / cin;
-        const int tap = (int)(r % 9), co = (int)(r / 9);
-        const __bf16 v = (__bf16)w[co * s_co + ci * s_ci + (tap / 3) * s_kh + (tap % 3) * s_kw];
+        const int tap = (int)(r % taps), co = (int)(r / taps);
+        const __bf16 v = (__bf16)w[co * s_co + ci * s_ci + (tap / K) * s_kh + (tap % K) * s_kw];
         wf[i] = v;                                            // [co][tap][ci]
-        wd[((long)ci * 9 + tap) * cout + co] = v;             // [ci][tap][co]
+        wd[((long)ci * taps + tap) * cout + co] = v;          // [ci][tap][co]
     }
 }
 }  // namespace
@@ -576,52 +601,112 @@ int plx_gemm_tn(const void* A, const void* B, float* C, float* ws, int M, int N1
     return run_tn<false>(A, B, C, ws, M, N1, N2, lda, ldb, ldc, zero, num_cus, accumulate, (hipStream_t)stream, {});
 }
 
-// ---- 3x3 / stride 1 / pad 1 convolution on NHWC bf16 (Cin, Cout multiples of 64) as implicit GEMMs
-// y[M][Cout] = sum_{tap, ci} x[shift_tap(m)][ci] * Wf[co][tap][ci]; stats as in plx_gemm_nt
-int plx_conv3x3_fwd(const void* x, const void* wf, void* y, int Nb, int H, int W, int Cin, int Cout,
-                    const void* zero, float* stats, void* stream) {
-    const int M = Nb * H * W;
-    if (M <= 0 || Cin % 64 || Cout % 64) return -1;
-    const ConvGeom g{H, W, Cin, 0};
-    hipStream_t s = (hipStream_t)stream;
-    if (Cout % 128 == 0)
-        return launch_nt<128, 128, 2, 2, true>(x, wf, y, M, Cout, 9 * Cin, Cin, 9 * Cin, Cout, zero, stats, s, g);
-    return launch_nt<256, 64, 4, 1, true>(x, wf, y, M, Cout, 9 * Cin, Cin, 9 * Cin, Cout, zero, stats, s, g);
+// ---- KxK (K = 1 or 3, pad = K/2) convolutions with stride 1 or 2 on NHWC bf16 (Cin, Cout multiples of 64)
+}  // extern "C"
+
+namespace {
+inline int out_dim(int H, int K, int S) { return (H + 2 * (K / 2) - K) / S + 1; }
+
+// forward / weight-gradient gather: rows = output pixels, tap t -> source (r*S + kh - p, c*S + kw - p)
+inline ConvGeom fwd_geom(int H, int W, int C, int K, int S) {
+    ConvGeom g{};
+    g.H = H; g.W = W; g.Hr = out_dim(H, K, S); g.Wr = out_dim(W, K, S);
+    g.C = C; g.S = S; g.ntaps = K * K; g.OS = 0;
+    for (int t = 0; t < K * K; ++t) {
+        g.offh[t] = (signed char)(t / K - K / 2);
+        g.offw[t] = (signed char)(t % K - K / 2);
+        g.btap[t] = (signed char)t;
+    }
+    return g;
 }
 
-// dx[M][Cin] = sum_{tap, co} dy[shift_-tap(m)][co] * Wd[ci][tap][co]
-int plx_conv3x3_dgrad(const void* dy, const void* wd, void* dx, int Nb, int H, int W, int Cin, int Cout,
-                      const void* zero, void* stream) {
-    const int M = Nb * H * W;
-    if (M <= 0 || Cin % 64 || Cout % 64) return -1;
-    const ConvGeom g{H, W, Cout, 1};
-    hipStream_t s = (hipStream_t)stream;
-    if (Cin % 128 == 0)
-        return launch_nt<128, 128, 2, 2, true>(dy, wd, dx, M, Cin, 9 * Cout, Cout, 9 * Cout, Cin, zero, nullptr, s, g);
-    return launch_nt<256, 64, 4, 1, true>(dy, wd, dx, M, Cin, 9 * Cout, Cout, 9 * Cout, Cin, zero, nullptr, s, g);
+template <int BM_, int BN_, int WGM_, int WGN_>
+int nt_conv(const void* A, const void* B, void* C, int M, int N, const ConvGeom& g, int ldb, int ldc,
+            const void* zero, float* stats, hipStream_t s) {
+    return launch_nt<BM_, BN_, WGM_, WGN_, true>(A, B, C, M, N, g.ntaps * g.C, g.C, ldb, ldc, zero, stats, s, g);
 }
 
-long plx_conv3x3_wgrad_workspace(int Nb, int H, int W, int Cin, int Cout, int num_cus) {
-    return plx_gemm_tn_workspace(Nb * H * W, Cout, 9 * Cin, num_cus);
+int nt_conv_any(const void* A, const void* B, void* C, int M, int N, const ConvGeom& g, int ldb, int ldc,
+                const void* zero, float* stats, hipStream_t s) {
+    if (N % 128 == 0) return nt_conv<128, 128, 2, 2>(A, B, C, M, N, g, ldb, ldc, zero, stats, s);
+    return nt_conv<256, 64, 4, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s);
+}
+}  // namespace
+
+extern "C" {
+
+// y[Nb*Ho*Wo][Cout] = conv(x[Nb*H*W][Cin], Wf[Cout][K*K][Cin]); stats as in plx_gemm_nt
+int plx_conv_fwd(const void* x, const void* wf, void* y, int Nb, int H, int W, int Cin, int Cout, int K, int S,
+                 const void* zero, float* stats, void* stream) {
+    if (Nb <= 0 || Cin % 64 || Cout % 64 || (K != 1 && K != 3) || (S != 1 && S != 2)) return -1;
+    const ConvGeom g = fwd_geom(H, W, Cin, K, S);
+    return nt_conv_any(x, wf, y, Nb * g.Hr * g.Wr, Cout, g, K * K * Cin, Cout, zero, stats, (hipStream_t)stream);
 }
 
-// dW[co][tap][ci] (fp32, (+)=) = sum_m dy[m][co] * x[shift_tap(m)][ci]
-int plx_conv3x3_wgrad(const void* dy, const void* x, float* dw, float* ws, int Nb, int H, int W, int Cin, int Cout,
-                      const void* zero, int num_cus, int accumulate, void* stream) {
-    const int M = Nb * H * W;
-    if (M <= 0 || Cin % 64 || Cout % 64) return -1;
-    const ConvGeom g{H, W, Cin, 0};
-    return run_tn<true>(dy, x, dw, ws, M, Cout, 9 * Cin, Cout, Cin, 9 * Cin, zero, num_cus, accumulate,
+// dx[Nb*H*W][Cin] = conv^T(dy[Nb*Ho*Wo][Cout], Wd[Cin][K*K][Cout]).  For S == 2 and K == 1 the caller passes a
+// zeroed dx (only the even-even pixels receive a value).
+int plx_conv_dgrad(const void* dy, const void* wd, void* dx, int Nb, int H, int W, int Cin, int Cout, int K, int S,
+                   const void* zero, void* stream) {
+    if (Nb <= 0 || Cin % 64 || Cout % 64 || (K != 1 && K != 3) || (S != 1 && S != 2)) return -1;
+    hipStream_t st = (hipStream_t)stream;
+    const int Ho = out_dim(H, K, S), Wo = out_dim(W, K, S), p = K / 2;
+    if (S == 1) {  // flipped taps over the same grid
+        ConvGeom g = fwd_geom(Ho, Wo, Cout, K, 1);
+        g.Hr = H; g.Wr = W;
+        for (int t = 0; t < K * K; ++t) {
+            g.offh[t] = (signed char)(p - t / K);
+            g.offw[t] = (signed char)(p - t % K);
+        }
+        return nt_conv_any(dy, wd, dx, Nb * H * W, Cin, g, K * K * Cout, Cin, zero, nullptr, st);
+    }
+    // stride 2: input pixel (ih, iw) = (2a + ph, 2b + pw) receives dy at ho = (ih + p - kh) / 2 for the taps kh
+    // with (ih + p - kh) even; one GEMM per parity class, rows scattered back into dx.
+    for (int ph = 0; ph < 2; ++ph)
+        for (int pw = 0; pw < 2; ++pw) {
+            ConvGeom g{};
+            g.H = Ho; g.W = Wo; g.C = Cout; g.S = 1;
+            g.Hr = (H - ph + 1) / 2; g.Wr = (W - pw + 1) / 2;
+            g.Hc = H; g.Wc = W; g.OS = 2; g.oph = ph; g.opw = pw;
+            int nt = 0;
+            for (int kh = 0; kh < K; ++kh) {
+                if ((ph + p - kh) & 1) continue;
+                for (int kw = 0; kw < K; ++kw) {
+                    if ((pw + p - kw) & 1) continue;
+                    g.offh[nt] = (signed char)((ph + p - kh) / 2);  // ho = a + offh
+                    g.offw[nt] = (signed char)((pw + p - kw) / 2);
+                    g.btap[nt] = (signed char)(kh * K + kw);
+                    ++nt;
+                }
+            }
+            g.ntaps = nt;
+            if (nt == 0 || g.Hr <= 0 || g.Wr <= 0) continue;
+            const int rc = nt_conv_any(dy, wd, dx, Nb * g.Hr * g.Wr, Cin, g, K * K * Cout, Cin, zero, nullptr, st);
+            if (rc) return rc;
+        }
+    return 0;
+}
+
+long plx_conv_wgrad_workspace(int Nb, int H, int W, int Cin, int Cout, int K, int S, int num_cus) {
+    return plx_gemm_tn_workspace(Nb * out_dim(H, K, S) * out_dim(W, K, S), Cout, K * K * Cin, num_cus);
+}
+
+// dW[co][tap][ci] (fp32, (+)=) = sum over output pixels m of dy[m][co] * x[gather_tap(m)][ci]
+int plx_conv_wgrad(const void* dy, const void* x, float* dw, float* ws, int Nb, int H, int W, int Cin, int Cout, int K,
+                   int S, const void* zero, int num_cus, int accumulate, void* stream) {
+    if (Nb <= 0 || Cin % 64 || Cout % 64 || (K != 1 && K != 3) || (S != 1 && S != 2)) return -1;
+    const ConvGeom g = fwd_geom(H, W, Cin, K, S);
+    const int M = Nb * g.Hr * g.Wr;
+    return run_tn<true>(dy, x, dw, ws, M, Cout, K * K * Cin, Cout, Cin, K * K * Cin, zero, num_cus, accumulate,
                         (hipStream_t)stream, g);
 }
 
-int plx_weight_prep3(const float* w, long s_co, long s_ci, long s_kh, long s_kw, void* wf, void* wd, int cout, int cin,
-                     void* stream) {
-    const long total = (long)cout * cin * 9;
+int plx_weight_prepk(const float* w, long s_co, long s_ci, long s_kh, long s_kw, void* wf, void* wd, int cout, int cin,
+                     int K, void* stream) {
+    const long total = (long)cout * cin * K * K;
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(weight_prep3_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, s_co, s_ci, s_kh, s_kw,
-                       (__bf16*)wf, (__bf16*)wd, cout, cin);
+    hipLaunchKernelGGL(weight_prepk_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, s_co, s_ci, s_kh, s_kw,
+                       (__bf16*)wf, (__bf16*)wd, cout, cin, K);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -14,7 +14,7 @@ import torch
 import torch.nn as nn
 
 from polyaxon_amd.ops.conv1x1 import Conv1x1, GradMailbox
-from polyaxon_amd.ops.conv3x3 import Conv3x3
+from polyaxon_amd.ops.conv import Conv3x3, ConvKxK
 from polyaxon_amd.ops.norm import BatchNormAct
 from polyaxon_amd.ops.pool import MaxPool3s2
 
@@ -26,8 +26,7 @@ class Bottleneck(nn.Module):
                  fused: bool = True, native_conv: bool = True):
         super().__init__()
         out_ch = width * self.expansion
-        # stride-1 1x1 and 3x3 convs run as (implicit) MFMA GEMMs on the NHWC rows (ops/conv1x1.py, conv3x3.py);
-        # the strided 3x3, the downsample and the stem stay on MIOpen
+        # every conv but the stem runs as an (implicit) MFMA GEMM on the NHWC rows (ops/conv1x1.py, ops/conv.py)
         self.conv1 = Conv1x1(in_ch, width, native=native_conv)
         self.bn1 = BatchNormAct(width, act=True, fused=fused)
         self.conv2 = Conv3x3(width, width, stride, native=native_conv)
@@ -51,9 +50,10 @@ class Bottleneck(nn.Module):
 
 
 class Downsample(nn.Module):
-    def __init__(self, in_ch: int, out_ch: int, stride: int, fused: bool = True):
+    def __init__(self, in_ch: int, out_ch: int, stride: int, fused: bool = True, native_conv: bool = True):
         super().__init__()
-        self.conv = nn.Conv2d(in_ch, out_ch, 1, stride=stride, bias=False)
+        self.conv = (Conv1x1(in_ch, out_ch, native=native_conv) if stride == 1
+                     else ConvKxK(in_ch, out_ch, 1, stride, native=native_conv))
         self.bn = BatchNormAct(out_ch, act=False, fused=fused)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -76,7 +76,7 @@ class ResNet(nn.Module):
             for j in range(n):
                 ds = None
                 if j == 0 and (stride != 1 or in_ch != w * Bottleneck.expansion):
-                    ds = Downsample(in_ch, w * Bottleneck.expansion, stride, fused=fused)
+                    ds = Downsample(in_ch, w * Bottleneck.expansion, stride, fused=fused, native_conv=native_conv)
                 blocks.append(Bottleneck(in_ch, w, stride if j == 0 else 1, ds, fused=fused, native_conv=native_conv))
                 in_ch = w * Bottleneck.expansion
             stages.append(nn.Sequential(*blocks))

@@ -179,11 +179,11 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
-        "plx_weight_prep3": [_P, _L, _L, _L, _L, _P, _P, _I, _I, _P],
-        "plx_conv3x3_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P],
-        "plx_conv3x3_dgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _P, _P],
-        "plx_conv3x3_wgrad_workspace": [_I, _I, _I, _I, _I, _I],
-        "plx_conv3x3_wgrad": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _I, _I, _P],
+        "plx_weight_prepk": [_P, _L, _L, _L, _L, _P, _P, _I, _I, _I, _P],
+        "plx_conv_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
+        "plx_conv_dgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P],
+        "plx_conv_wgrad_workspace": [_I, _I, _I, _I, _I, _I, _I, _I],
+        "plx_conv_wgrad": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
     },
     "plx_pool": {
         "plx_maxpool3s2_forward": [_P, _P, _P, _I, _I, _I, _I, _P],
@@ -212,7 +212,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_conv3x3_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
+RESTYPES: Dict[str, object] = {"plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

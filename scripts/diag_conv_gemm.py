@@ -74,7 +74,7 @@ def conv3():
     """3x3 stride-1 convs of ResNet-50: MIOpen vs the implicit-GEMM kernels (kernel time per pass)."""
     from polyaxon_amd.ops import _native
     from polyaxon_amd.ops.conv1x1 import _num_cus, _stream, _zero_page
-    from polyaxon_amd.ops.conv3x3 import conv3x3, weight_prep3
+    from polyaxon_amd.ops.conv import weight_prep_k
 
     lib = _native.lib("plx_conv")
     for n, c, h, w in [(256, 64, 56, 56), (256, 128, 28, 28), (256, 256, 14, 14), (256, 512, 7, 7)]:
@@ -89,20 +89,20 @@ def conv3():
             wm.grad = None
             F.conv2d(xm, wm, padding=1).backward(g)
 
-        wf, wd = weight_prep3(wt)
+        wf, wd = weight_prep_k(wt)
         y = torch.empty_like(x)
         dx = torch.empty_like(x)
         z = _zero_page(dev).data_ptr()
         cus = _num_cus(dev)
-        ws = torch.empty(int(lib.plx_conv3x3_wgrad_workspace(n, h, w, c, c, cus)), device=dev)
+        ws = torch.empty(int(lib.plx_conv_wgrad_workspace(n, h, w, c, c, 3, 1, cus)), device=dev)
         dw = torch.empty(c, 9, c, device=dev)
         parts = {
-            "fwd": lambda: lib.plx_conv3x3_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), n, h, w, c, c, z, None,
-                                               _stream()),
-            "dgrad": lambda: lib.plx_conv3x3_dgrad(g.data_ptr(), wd.data_ptr(), dx.data_ptr(), n, h, w, c, c, z,
-                                                   _stream()),
-            "wgrad": lambda: lib.plx_conv3x3_wgrad(g.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), n, h, w,
-                                                   c, c, z, cus, 0, _stream()),
+            "fwd": lambda: lib.plx_conv_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), n, h, w, c, c, 3, 1, z, None,
+                                            _stream()),
+            "dgrad": lambda: lib.plx_conv_dgrad(g.data_ptr(), wd.data_ptr(), dx.data_ptr(), n, h, w, c, c, 3, 1, z,
+                                                _stream()),
+            "wgrad": lambda: lib.plx_conv_wgrad(g.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), n, h, w,
+                                                c, c, 3, 1, z, cus, 0, _stream()),
         }
         a = min(timeit(miopen) for _ in range(3))
         pt = {k: min(timeit(f) for _ in range(2)) for k, f in parts.items()}
@@ -112,5 +112,52 @@ def conv3():
               flush=True)
 
 
+def strided():
+    """Strided convs of ResNet-50 (3x3 s2 in conv2 of each stage's first block, 1x1 s2 downsample):
+    MIOpen fwd+bwd vs the implicit-GEMM passes."""
+    from polyaxon_amd.ops import _native
+    from polyaxon_amd.ops.conv import weight_prep_k
+    from polyaxon_amd.ops.conv1x1 import _num_cus, _stream, _zero_page
+
+    lib = _native.lib("plx_conv")
+    for n, cin, h, w, cout, k in [(256, 128, 56, 56, 128, 3), (256, 256, 28, 28, 256, 3), (256, 512, 14, 14, 512, 3),
+                                  (256, 256, 56, 56, 512, 1), (256, 512, 28, 28, 1024, 1),
+                                  (256, 1024, 14, 14, 2048, 1)]:
+        ho, wo = (h + 2 * (k // 2) - k) // 2 + 1, (w + 2 * (k // 2) - k) // 2 + 1
+        x = torch.randn(n, cin, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        wt = (torch.randn(cout, cin, k, k, device=dev) * 0.05).contiguous(memory_format=torch.channels_last)
+        g = torch.randn(n, cout, ho, wo, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        xm = x.clone().requires_grad_()
+        wm = wt.to(torch.bfloat16).requires_grad_()
+
+        def miopen():
+            xm.grad = None
+            wm.grad = None
+            F.conv2d(xm, wm, stride=2, padding=k // 2).backward(g)
+
+        wf, wd = weight_prep_k(wt)
+        y = torch.empty(n, cout, ho, wo, device=dev, dtype=torch.bfloat16)
+        dx = torch.zeros_like(x)
+        z = _zero_page(dev).data_ptr()
+        cus = _num_cus(dev)
+        ws = torch.empty(int(lib.plx_conv_wgrad_workspace(n, h, w, cin, cout, k, 2, cus)), device=dev)
+        dw = torch.empty(cout, k * k, cin, device=dev)
+        parts = {
+            "fwd": lambda: lib.plx_conv_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), n, h, w, cin, cout, k, 2, z,
+                                            None, _stream()),
+            "dgrad": lambda: lib.plx_conv_dgrad(g.data_ptr(), wd.data_ptr(), dx.data_ptr(), n, h, w, cin, cout, k, 2,
+                                                z, _stream()),
+            "wgrad": lambda: lib.plx_conv_wgrad(g.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr(), n, h, w,
+                                                cin, cout, k, 2, z, cus, 0, _stream()),
+        }
+        a = min(timeit(miopen) for _ in range(3))
+        pt = {kk: min(timeit(f) for _ in range(2)) for kk, f in parts.items()}
+        print(f"s2 k{k} {(n, cin, h, w, cout)}  miopen fwd+bwd {a:.3f} ms  plx " +
+              " ".join(f"{kk}={v:.3f}" for kk, v in pt.items()) + f"  sum {sum(pt.values()):.3f}", flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if "--strided" in sys.argv:
+        strided()
+    else:
+        main()

@@ -136,7 +136,7 @@ def test_conv_stats_feed_batchnorm(cuda):
 @pytest.mark.parametrize("shape,cout", [((2, 64, 7, 9), 64), ((3, 128, 10, 6), 128), ((2, 64, 5, 5), 256),
                                         ((4, 256, 14, 14), 64), ((1, 64, 1, 1), 128)])
 def test_conv3x3_autograd(cuda, shape, cout):
-    from polyaxon_amd.ops.conv3x3 import Conv3x3, supported
+    from polyaxon_amd.ops.conv import Conv3x3, supported
 
     torch.manual_seed(6)
     conv = Conv3x3(shape[1], cout).to(cuda)
@@ -157,11 +157,11 @@ def test_conv3x3_autograd(cuda, shape, cout):
 
 
 def test_conv3x3_stats(cuda):
-    from polyaxon_amd.ops.conv3x3 import conv3x3
+    from polyaxon_amd.ops.conv import conv_k
 
     x = torch.randn(2, 64, 9, 11, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = torch.randn(128, 64, 3, 3, device=cuda) * 0.05
-    y = conv3x3(x, w, with_stats=True)
+    y = conv_k(x, w, 1, with_stats=True)
     st, nblk = y._plx_channel_stats
     yf = y.float().permute(0, 2, 3, 1).reshape(-1, 128)
     torch.testing.assert_close(st.view(2, nblk, 128)[0].sum(0), yf.sum(0), rtol=1e-4, atol=1e-2)
@@ -191,3 +191,28 @@ def test_resnet_native_convs_match_miopen(cuda):
         cn = float(F.cosine_similarity(res["native"][1][pname], g, dim=0))
         cm = float(F.cosine_similarity(res["miopen"][1][pname], g, dim=0))
         assert cn > 0.8 and cn >= cm - 0.02, (pname, cn, cm)  # stem grads sit near 0.87 for both bf16 paths
+
+
+@pytest.mark.parametrize("k,stride,shape,cout", [(3, 2, (2, 64, 14, 14), 64), (3, 2, (2, 128, 9, 7), 128),
+                                                 (1, 2, (2, 256, 14, 14), 512), (1, 2, (3, 64, 7, 9), 128),
+                                                 (1, 1, (2, 64, 6, 6), 64)])
+def test_convk_strided_autograd(cuda, k, stride, shape, cout):
+    from polyaxon_amd.ops.conv import ConvKxK, supported
+
+    torch.manual_seed(7)
+    conv = ConvKxK(shape[1], cout, k, stride).to(cuda)
+    conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
+    x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert supported(x, conv)
+    xa = x.clone().requires_grad_()
+    y = conv(xa)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr = x.float().clone().requires_grad_()
+    wr = conv.weight.detach().clone().requires_grad_()
+    yr = F.conv2d(xr, wr.to(torch.bfloat16).float(), stride=stride, padding=k // 2)
+    yr.backward(g.float())
+    assert y.shape == yr.shape
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=8e-2)
+    torch.testing.assert_close(xa.grad.float(), xr.grad, rtol=2e-2, atol=8e-2)
+    torch.testing.assert_close(conv.weight.grad, wr.grad, rtol=2e-2, atol=0.2)
