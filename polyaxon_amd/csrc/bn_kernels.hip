@@ -274,7 +274,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const bf16x8* __r
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ pdz, const float* __restrict__ pdzx, int nblk, int C,
                                        int64_t M, const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ invstd, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, float* __restrict__ coef) {
+                                       float* __restrict__ dbeta, float* __restrict__ coef, int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double A = 0.0, B = 0.0;
@@ -283,8 +283,9 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ pdz, const floa
     B += pdzx[(int64_t)b * C + c];
   }
   const float db = (float)A, dg = (float)B;
-  dbeta[c] = db;
-  dgamma[c] = dg;
+  // accumulate: dgamma / dbeta are the parameters' own (flat) gradient slots, summed into like autograd would
+  dbeta[c] = accumulate ? dbeta[c] + db : db;
+  dgamma[c] = accumulate ? dgamma[c] + dg : dg;
   const float is = invstd[c], k1 = gamma[c] * is;
   const float k2 = db / (float)M, k3 = dg / (float)M;
   // dx = k1 * (dz - k2 - xhat*k3),  xhat = (x - mean) * is   =>  dx = A*dz + B*x + D
@@ -430,11 +431,11 @@ PLX_API int plx_bn_apply(const void* x, const void* res, void* y, int64_t M, int
   return (int)hipGetLastError();
 }
 
-// mask: the ReLU bit mask written by the forward (required when relu)
+// mask: the ReLU bit mask written by the forward (required when relu); accumulate: dgamma/dbeta += (else =)
 PLX_API int plx_bn_backward(const void* x, const uint8_t* mask, const void* dy, void* dx, void* dres, int64_t M, int C,
                             const float* gamma, const float* save_mean, const float* save_invstd, float* dgamma,
                             float* dbeta, float* coef /* [3C] */, float* partials /* plx_bn_workspace floats */, int relu,
-                            hipStream_t stream) {
+                            int accumulate, hipStream_t stream) {
   Plan p;
   if (!plan_for(M, C, &p) || M < 1 || (relu && mask == nullptr)) return 1;
   float* pa = partials;
@@ -446,7 +447,28 @@ PLX_API int plx_bn_backward(const void* x, const uint8_t* mask, const void* dy, 
   hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, p.S, 2), dim3(256), 0, stream, partials, p.nblk, C,
                      l2, p.S);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, l2, l2 + (int64_t)p.S * C, p.S, C, M,
-                     gamma, save_mean, save_invstd, dgamma, dbeta, coef);
+                     gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
+  const int64_t n_vec = M * p.G;
+  hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
+                     mask, (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, p.G, relu);
+  return (int)hipGetLastError();
+}
+
+// Backward whose per-block partials ([2][nblk][C]: sum dz, sum dz*xhat) were produced by the op that wrote dy
+// (the data-gradient GEMM epilogue, csrc/conv_gemm.hip BnBwd): skips the reduce pass over x and dy.  l2 holds
+// plx_bn_l2_workspace(nblk, C) floats.
+PLX_API int plx_bn_backward_from_partials(const void* x, const uint8_t* mask, const void* dy, void* dx, void* dres,
+                                          int64_t M, int C, const float* gamma, const float* save_mean,
+                                          const float* save_invstd, float* dgamma, float* dbeta, float* coef,
+                                          const float* partials, int nblk, float* l2, int relu, int accumulate,
+                                          hipStream_t stream) {
+  Plan p;
+  if (!plan_for(M, C, &p) || M < 1 || nblk < 1 || (relu && mask == nullptr)) return 1;
+  const int S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
+  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, S, 2), dim3(256), 0, stream, partials, nblk, C, l2,
+                     S);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S, C,
+                     M, gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
   const int64_t n_vec = M * p.G;
   hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
                      mask, (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, p.G, relu);

@@ -42,6 +42,20 @@ struct ConvGeom {
     signed char offh[9], offw[9], btap[9];
 };
 
+// BatchNorm-backward channel reduction fused into a data-gradient GEMM's epilogue.  The GEMM's output C is
+// dy of a BatchNorm(+ReLU) whose input x (same [rows][ldc] layout as C) and 1-bit ReLU mask the forward kept;
+// the epilogue adds per-block partials of  sum dz  and  sum dz * (x - mean) * invstd  (dz = dy * mask) to
+// part[blk_off + tm][n] and part[part_ld + blk_off + tm][n], so the BatchNorm backward skips its reduce pass
+// (one full read of dy) -- the same hand-off the forward does with its channel stats.
+struct BnBwd {
+    const __bf16* x;
+    const uint8_t* mask;   // nullptr: no ReLU
+    const float* mean;
+    const float* invstd;
+    float* part;           // nullptr: disabled
+    int part_ld, blk_off;
+};
+
 __device__ __forceinline__ void row_coords(int m, int Hr, int Wr, int& n, int& r, int& c) {
     const int q = m / Wr;
     c = m - q * Wr;
@@ -85,7 +99,7 @@ template <int BM, int BN, int WGM, int WGN, bool CONV>
 __global__ void __launch_bounds__(NTHREADS, 2)
 gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
                int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
-               float* __restrict__ stats, ConvGeom geo, const __bf16* __restrict__ D, int ldd) {
+               float* __restrict__ stats, ConvGeom geo, const __bf16* __restrict__ D, int ldd, BnBwd bnr) {
     constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
     constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -189,8 +203,49 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     // Epilogue through LDS (the k-loop's last barrier freed it): D[n][m] has column m = fr and rows
     // n = 4*fq + r in each lane, i.e. 4 consecutive channels of one pixel.  Stage the bf16 tile as [m][n] rows
     // padded by 16 B, then store whole output rows with 16 B per lane (a wave instruction writes contiguous
-    // row segments instead of 32-B pieces of 16 different rows).
+    // row segments instead of 32-B pieces of 16 different rows).  Thread tid owns chunk column tid % CHUNKS of
+    // rows tid / CHUNKS + it * RSTEP; the epilogue's global operands (D, and x / mask of the fused BatchNorm
+    // backward) are loaded for all of its rows BEFORE the tile is staged, so their latency hides behind the LDS
+    // pass (rows past M are clamped to a valid row and discarded: no per-row branch around a load).
     constexpr int CROW = BN * 2 + 16;
+    constexpr int CHUNKS = BN / 8;                          // 16-B chunks per output row
+    static_assert(NTHREADS % CHUNKS == 0, "a thread keeps one chunk column over the store loop");
+    constexpr int RSTEP = NTHREADS / CHUNKS, ITERS = BM / RSTEP;
+    const int rows = min(BM, M - m0);
+    const int cc = tid % CHUNKS, r0 = tid / CHUNKS;
+    const int ch0 = n0 + cc * 8;                            // this thread's 8 channels
+    const bool bnr_on = bnr.part != nullptr;
+    size_t orow[ITERS];
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+        const int gm = min(m0 + r0 + it * RSTEP, M - 1);
+        if constexpr (CONV) orow[it] = out_row(geo, gm);
+        else orow[it] = (size_t)gm;
+    }
+    uint4 dpre[ITERS], xpre[ITERS];
+    uint32_t mpre[ITERS];
+    if (D != nullptr) {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) dpre[it] = *(const uint4*)(D + orow[it] * ldd + ch0);
+    }
+    float sa[8], sb[8], mu[8], is[8];
+    if (bnr_on) {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) xpre[it] = *(const uint4*)(bnr.x + orow[it] * ldc + ch0);
+        if (bnr.mask != nullptr) {
+#pragma unroll
+            for (int it = 0; it < ITERS; ++it) mpre[it] = bnr.mask[(orow[it] * ldc + ch0) >> 3];
+        } else {
+#pragma unroll
+            for (int it = 0; it < ITERS; ++it) mpre[it] = 0xffu;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            sa[k] = sb[k] = 0.f;
+            mu[k] = bnr.mean[ch0 + k];
+            is[k] = bnr.invstd[ch0 + k];
+        }
+    }
 #pragma unroll
     for (int rm = 0; rm < RM; ++rm) {
         const int ml = wm * WTM + rm * 16 + fr;
@@ -205,20 +260,17 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         }
     }
     __syncthreads();
-    constexpr int CHUNKS = BN / 8;                          // 16-B chunks per output row
-    const int rows = min(BM, M - m0);
-    for (int i = tid; i < BM * CHUNKS; i += NTHREADS) {
-        const int r = i / CHUNKS, c = i % CHUNKS;
-        if (r >= rows) continue;
-        uint4 v = *(const uint4*)(smem + r * CROW + c * 16);
-        size_t orow = (size_t)(m0 + r);
-        if constexpr (CONV) orow = out_row(geo, m0 + r);
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+        const int r = r0 + it * RSTEP;
+        if (r >= rows) break;
+        uint4 v = *(const uint4*)(smem + r * CROW + cc * 16);
         if (D != nullptr) {
             // C = A.B^T + D (a second gradient into the same tensor, e.g. the residual branch's): added in fp32
-            // and rounded once, instead of a separate bf16 add pass over both tensors
-            const uint4 d = *(const uint4*)(D + (size_t)(m0 + r) * ldd + n0 + c * 8);
+            // and rounded once, instead of a separate bf16 add pass over both tensors.  D is indexed like C, so
+            // D == C (in place) is allowed.
             uint32_t* pv = (uint32_t*)&v;
-            const uint32_t* pd = (const uint32_t*)&d;
+            const uint32_t* pd = (const uint32_t*)&dpre[it];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const float lo = __uint_as_float(pv[j] << 16) + __uint_as_float(pd[j] << 16);
@@ -226,7 +278,50 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                 pv[j] = pack_bf16x2(lo, hi);
             }
         }
-        *(uint4*)(C + orow * ldc + n0 + c * 8) = v;
+        *(uint4*)(C + orow[it] * ldc + ch0) = v;
+        if (bnr_on) {
+            const uint32_t mb = mpre[it];
+            const uint32_t* pv = (const uint32_t*)&v;
+            const uint32_t* px = (const uint32_t*)&xpre[it];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float g0 = (mb >> (2 * j)) & 1u ? __uint_as_float(pv[j] << 16) : 0.f;
+                const float g1 = (mb >> (2 * j + 1)) & 1u ? __uint_as_float(pv[j] & 0xffff0000u) : 0.f;
+                const float x0 = __uint_as_float(px[j] << 16), x1 = __uint_as_float(px[j] & 0xffff0000u);
+                sa[2 * j] += g0;
+                sa[2 * j + 1] += g1;
+                sb[2 * j] = fmaf(g0, (x0 - mu[2 * j]) * is[2 * j], sb[2 * j]);
+                sb[2 * j + 1] = fmaf(g1, (x1 - mu[2 * j + 1]) * is[2 * j + 1], sb[2 * j + 1]);
+            }
+        }
+    }
+    if (bnr_on) {
+        // threads tid, tid + CHUNKS, ... share a chunk column: sum them through LDS past the staged tile
+        float* red = (float*)(smem + BM * CROW);            // [NTHREADS][16]
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            red[tid * 16 + k] = sa[k];
+            red[tid * 16 + 8 + k] = sb[k];
+        }
+        __syncthreads();
+        if (tid < CHUNKS) {
+            for (int j = 1; j < NTHREADS / CHUNKS; ++j) {
+                const float* o = red + (j * CHUNKS + tid) * 16;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    sa[k] += o[k];
+                    sb[k] += o[8 + k];
+                }
+            }
+            float* pa = bnr.part + (size_t)(bnr.blk_off + tm) * ldc + ch0;
+            float* pb = bnr.part + (size_t)(bnr.part_ld + bnr.blk_off + tm) * ldc + ch0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                pa[k] = sa[k];
+                pb[k] = sb[k];
+            }
+        }
+        __syncthreads();                                    // red aliases the stats scratch below
     }
     if (stats != nullptr) {
         // per-channel partial sum / sum of squares of the bf16-rounded outputs over this block's rows:
@@ -459,15 +554,15 @@ int set_lds(KernelT k, int bytes) {
 template <int BM, int BN, int WGM, int WGN, bool CONV = false>
 int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
               const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}, const void* D = nullptr,
-              int ldd = 0) {
+              int ldd = 0, BnBwd bnr = {}) {
     constexpr int LDS = 2 * (BM + BN) * BK * 2;
-    static_assert(BM * (BN * 2 + 16) + 2 * NTHREADS * 4 <= LDS, "epilogue staging must fit the k-loop LDS");
+    static_assert(BM * (BN * 2 + 16) + NTHREADS * 16 * 4 <= LDS, "epilogue staging must fit the k-loop LDS");
     auto k = gemm_nt_kernel<BM, BN, WGM, WGN, CONV>;
     static int attr = set_lds(k, LDS);
     if (attr) return attr;
     const int nwg = ((M + BM - 1) / BM) * (N / BN);
     hipLaunchKernelGGL(k, dim3(nwg), dim3(NTHREADS), LDS, s, (const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N,
-                       K, lda, ldb, ldc, (const __bf16*)zero, stats, geo, (const __bf16*)D, ldd);
+                       K, lda, ldb, ldc, (const __bf16*)zero, stats, geo, (const __bf16*)D, ldd, bnr);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -529,12 +624,16 @@ int plx_gemm_nt_rows_per_block(int N) { return N % 128 == 0 ? 128 : 256; }
 
 // stats (nullable): fp32 [2][ceil(M / rows_per_block)][N] per-block channel sums / sums of squares of C
 // D (nullable, bf16 [M][N], ldd): added to the product (C = A.B^T + D); not reflected in stats
+// bnr (nullable host struct): fused BatchNorm-backward partials of C (see BnBwd; needs ldc == N)
 int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                const void* zero, float* stats, const void* D, int ldd, void* stream) {
+                const void* zero, float* stats, const void* D, int ldd, const BnBwd* bnr, void* stream) {
     if (M <= 0 || N % 64 || K % BK || lda % 8 || ldb % 8 || ldc % 8 || (D != nullptr && ldd % 8)) return -1;
+    if (bnr != nullptr && (ldc != N || bnr->part == nullptr)) return -1;
+    const BnBwd b = bnr != nullptr ? *bnr : BnBwd{};
     hipStream_t s = (hipStream_t)stream;
-    if (N % 128 == 0) return launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd);
-    return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd);
+    if (N % 128 == 0)
+        return launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b);
+    return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b);
 }
 
 // floats of slab workspace plx_gemm_tn needs for this problem
@@ -622,33 +721,22 @@ inline ConvGeom fwd_geom(int H, int W, int C, int K, int S) {
 
 template <int BM_, int BN_, int WGM_, int WGN_>
 int nt_conv(const void* A, const void* B, void* C, int M, int N, const ConvGeom& g, int ldb, int ldc,
-            const void* zero, float* stats, hipStream_t s) {
-    return launch_nt<BM_, BN_, WGM_, WGN_, true>(A, B, C, M, N, g.ntaps * g.C, g.C, ldb, ldc, zero, stats, s, g);
+            const void* zero, float* stats, hipStream_t s, const void* D, const BnBwd& bnr) {
+    return launch_nt<BM_, BN_, WGM_, WGN_, true>(A, B, C, M, N, g.ntaps * g.C, g.C, ldb, ldc, zero, stats, s, g, D,
+                                                 D != nullptr ? ldc : 0, bnr);
 }
+
+inline int nt_rows_per_block(int N) { return N % 128 == 0 ? 128 : 256; }
 
 int nt_conv_any(const void* A, const void* B, void* C, int M, int N, const ConvGeom& g, int ldb, int ldc,
-                const void* zero, float* stats, hipStream_t s) {
-    if (N % 128 == 0) return nt_conv<128, 128, 2, 2>(A, B, C, M, N, g, ldb, ldc, zero, stats, s);
-    return nt_conv<256, 64, 4, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s);
-}
-}  // namespace
-
-extern "C" {
-
-// y[Nb*Ho*Wo][Cout] = conv(x[Nb*H*W][Cin], Wf[Cout][K*K][Cin]); stats as in plx_gemm_nt
-int plx_conv_fwd(const void* x, const void* wf, void* y, int Nb, int H, int W, int Cin, int Cout, int K, int S,
-                 const void* zero, float* stats, void* stream) {
-    if (Nb <= 0 || Cin % 64 || Cout % 64 || (K != 1 && K != 3) || (S != 1 && S != 2)) return -1;
-    const ConvGeom g = fwd_geom(H, W, Cin, K, S);
-    return nt_conv_any(x, wf, y, Nb * g.Hr * g.Wr, Cout, g, K * K * Cin, Cout, zero, stats, (hipStream_t)stream);
+                const void* zero, float* stats, hipStream_t s, const void* D = nullptr, const BnBwd& bnr = {}) {
+    if (N % 128 == 0) return nt_conv<128, 128, 2, 2>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
+    return nt_conv<256, 64, 4, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
 }
 
-// dx[Nb*H*W][Cin] = conv^T(dy[Nb*Ho*Wo][Cout], Wd[Cin][K*K][Cout]).  For S == 2 and K == 1 the caller passes a
-// zeroed dx (only the even-even pixels receive a value).
-int plx_conv_dgrad(const void* dy, const void* wd, void* dx, int Nb, int H, int W, int Cin, int Cout, int K, int S,
-                   const void* zero, void* stream) {
-    if (Nb <= 0 || Cin % 64 || Cout % 64 || (K != 1 && K != 3) || (S != 1 && S != 2)) return -1;
-    hipStream_t st = (hipStream_t)stream;
+// the GEMMs of a data gradient: (row grid geometry, ntaps) per launch; S == 2 gives one per parity class
+template <typename F>
+int for_each_dgrad_gemm(int Nb, int H, int W, int Cin, int Cout, int K, int S, F&& f) {
     const int Ho = out_dim(H, K, S), Wo = out_dim(W, K, S), p = K / 2;
     if (S == 1) {  // flipped taps over the same grid
         ConvGeom g = fwd_geom(Ho, Wo, Cout, K, 1);
@@ -657,7 +745,7 @@ int plx_conv_dgrad(const void* dy, const void* wd, void* dx, int Nb, int H, int 
             g.offh[t] = (signed char)(p - t / K);
             g.offw[t] = (signed char)(p - t % K);
         }
-        return nt_conv_any(dy, wd, dx, Nb * H * W, Cin, g, K * K * Cout, Cin, zero, nullptr, st);
+        return f(g, Nb * H * W);
     }
     // stride 2: input pixel (ih, iw) = (2a + ph, 2b + pw) receives dy at ho = (ih + p - kh) / 2 for the taps kh
     // with (ih + p - kh) even; one GEMM per parity class, rows scattered back into dx.
@@ -680,10 +768,50 @@ int plx_conv_dgrad(const void* dy, const void* wd, void* dx, int Nb, int H, int 
             }
             g.ntaps = nt;
             if (nt == 0 || g.Hr <= 0 || g.Wr <= 0) continue;
-            const int rc = nt_conv_any(dy, wd, dx, Nb * g.Hr * g.Wr, Cin, g, K * K * Cout, Cin, zero, nullptr, st);
+            const int rc = f(g, Nb * g.Hr * g.Wr);
             if (rc) return rc;
         }
     return 0;
+}
+}  // namespace
+
+extern "C" {
+
+// y[Nb*Ho*Wo][Cout] = conv(x[Nb*H*W][Cin], Wf[Cout][K*K][Cin]); stats as in plx_gemm_nt
+int plx_conv_fwd(const void* x, const void* wf, void* y, int Nb, int H, int W, int Cin, int Cout, int K, int S,
+                 const void* zero, float* stats, void* stream) {
+    if (Nb <= 0 || Cin % 64 || Cout % 64 || (K != 1 && K != 3) || (S != 1 && S != 2)) return -1;
+    const ConvGeom g = fwd_geom(H, W, Cin, K, S);
+    return nt_conv_any(x, wf, y, Nb * g.Hr * g.Wr, Cout, g, K * K * Cin, Cout, zero, stats, (hipStream_t)stream);
+}
+
+// dx[Nb*H*W][Cin] = conv^T(dy[Nb*Ho*Wo][Cout], Wd[Cin][K*K][Cout]) (+ D, bf16 [Nb*H*W][Cin], may alias dx).
+// For S == 2 and K == 1 only the even-even pixels are written: the caller passes a zeroed dx, or D == dx (the
+// other rows then keep D).  bnr (nullable): fused BatchNorm-backward partials of dx, one block row per GEMM
+// block over all launches (plx_conv_dgrad_blocks of them); only valid when every pixel is written (not S2/K1).
+int plx_conv_dgrad(const void* dy, const void* wd, void* dx, int Nb, int H, int W, int Cin, int Cout, int K, int S,
+                   const void* zero, const void* D, const BnBwd* bnr, void* stream) {
+    if (Nb <= 0 || Cin % 64 || Cout % 64 || (K != 1 && K != 3) || (S != 1 && S != 2)) return -1;
+    if (bnr != nullptr && (S == 2 && K == 1)) return -1;
+    hipStream_t st = (hipStream_t)stream;
+    BnBwd b = bnr != nullptr ? *bnr : BnBwd{};
+    const int rpb = nt_rows_per_block(Cin);
+    return for_each_dgrad_gemm(Nb, H, W, Cin, Cout, K, S, [&](const ConvGeom& g, int M) {
+        const int rc = nt_conv_any(dy, wd, dx, M, Cin, g, K * K * Cout, Cin, zero, nullptr, st, D, b);
+        b.blk_off += (M + rpb - 1) / rpb;
+        return rc;
+    });
+}
+
+// number of BatchNorm-partial block rows plx_conv_dgrad writes (part_ld for its bnr)
+int plx_conv_dgrad_blocks(int Nb, int H, int W, int Cin, int Cout, int K, int S) {
+    int total = 0;
+    const int rpb = nt_rows_per_block(Cin);
+    const int rc = for_each_dgrad_gemm(Nb, H, W, Cin, Cout, K, S, [&](const ConvGeom&, int M) {
+        total += (M + rpb - 1) / rpb;
+        return 0;
+    });
+    return rc ? rc : total;
 }
 
 long plx_conv_wgrad_workspace(int Nb, int H, int W, int Cin, int Cout, int K, int S, int num_cus) {

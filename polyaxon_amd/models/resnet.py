@@ -37,16 +37,19 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        train = self.training and torch.is_grad_enabled() and x.requires_grad
+        box = GradMailbox() if train else None
         if self.downsample is None:
-            # identity block: bn3's residual gradient is added inside conv1's dgrad GEMM (ops.conv1x1.GradMailbox)
-            box = GradMailbox() if (self.training and torch.is_grad_enabled() and x.requires_grad) else None
-            out = self.bn1(self.conv1(x, grad_box=box))
-            out = self.bn2(self.conv2(out))
-            return self.bn3(self.conv3(out), x, residual_grad_box=box)
-        identity = self.downsample(x)
-        out = self.bn1(self.conv1(x))
-        out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), identity)
+            # identity block: bn3's residual gradient is added inside conv1's dgrad GEMM (ops.conv1x1.GradMailbox),
+            # so conv1's dgrad is x's whole gradient and serves the previous block's bn3 its backward partials
+            out = self.bn1(self.conv1(x, grad_box=box, bn_link=True))
+            out = self.bn2(self.conv2(out, bn_link=True))
+            return self.bn3(self.conv3(out, bn_link=True), x, residual_grad_box=box)
+        # downsampling block: conv1's data gradient is deferred into the downsample conv's dgrad epilogue
+        identity = self.downsample(x, grad_box=box)
+        out = self.bn1(self.conv1(x, grad_sink=box))
+        out = self.bn2(self.conv2(out, bn_link=True))
+        return self.bn3(self.conv3(out, bn_link=True), identity)
 
 
 class Downsample(nn.Module):
@@ -56,8 +59,8 @@ class Downsample(nn.Module):
                      else ConvKxK(in_ch, out_ch, 1, stride, native=native_conv))
         self.bn = BatchNormAct(out_ch, act=False, fused=fused)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.bn(self.conv(x))
+    def forward(self, x: torch.Tensor, grad_box: Optional[GradMailbox] = None) -> torch.Tensor:
+        return self.bn(self.conv(x, grad_box=grad_box))
 
 
 class ResNet(nn.Module):

@@ -156,7 +156,9 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_bn_l2_workspace": [_I, _I],
         "plx_bn_forward_from_partials": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P, _P,
                                          _I, _P],
-        "plx_bn_backward": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P],
+        "plx_bn_backward": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P],
+        "plx_bn_backward_from_partials": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I,
+                                          _P],
     },
     "plx_procmon": {
         "plx_pm_create": [],
@@ -174,14 +176,15 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
                                _P, _P],
     },
     "plx_conv": {
-        "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P],
+        "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
         "plx_gemm_nt_rows_per_block": [_I],
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
         "plx_weight_prepk": [_P, _L, _L, _L, _L, _P, _P, _I, _I, _I, _P],
         "plx_conv_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
-        "plx_conv_dgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P],
+        "plx_conv_dgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
+        "plx_conv_dgrad_blocks": [_I, _I, _I, _I, _I, _I, _I],
         "plx_conv_wgrad_workspace": [_I, _I, _I, _I, _I, _I, _I, _I],
         "plx_conv_wgrad": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
     },
@@ -221,6 +224,12 @@ def _declare(name: str, handle: ctypes.CDLL) -> None:
         f = getattr(handle, fn)
         f.argtypes = argtypes
         f.restype = RESTYPES.get(fn, _I)
+
+
+class BnBwdArgs(ctypes.Structure):
+    """Host image of ``BnBwd`` (csrc/conv_gemm.hip): fused BatchNorm-backward partials in a dgrad GEMM epilogue."""
+    _fields_ = [("x", _P), ("mask", _P), ("mean", _P), ("invstd", _P), ("part", _P), ("part_ld", _I),
+                ("blk_off", _I)]
 
 
 def check(rc: int, what: str) -> None:

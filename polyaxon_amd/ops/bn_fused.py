@@ -12,6 +12,8 @@ from typing import Optional
 import torch
 
 from polyaxon_amd.ops import _native
+from polyaxon_amd.ops.conv1x1 import BnLink
+from polyaxon_amd.ops.flat import direct_grad
 
 
 def _stream() -> int:
@@ -32,7 +34,8 @@ def supported(x: torch.Tensor) -> bool:
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, ext=None, box=None):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, ext=None, box=None,
+                link=None):
         lib = _native.lib("plx_bn")
         x = _cl(x)
         n, c, h, w = x.shape
@@ -69,7 +72,16 @@ class _BNAct(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.box = box if (box is not None and box.armed and residual is not None) else None
+        if ctx.box is not None:
+            ctx.box.expect = True
         ctx.ws = ws
+        # direct gradients: dgamma / dbeta accumulate into the flat gradient slots (ops.flat.direct_grad)
+        gw, gb = direct_grad(weight), direct_grad(bias)
+        ctx.direct = (gw, gb) if (gw is not None and gb is not None) else None
+        # the consumer conv may produce this BN's backward partials in its dgrad epilogue (ops.conv1x1.BnLink)
+        ctx.link = link
+        if link is not None:
+            link.x, link.mask, link.mean, link.invstd = x, mask, stats[:c], stats[c:2 * c]
         return y
 
     @staticmethod
@@ -84,18 +96,36 @@ class _BNAct(torch.autograd.Function):
         f32 = dict(dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
-        dgb = torch.empty(2 * c, **f32)
+        if ctx.direct is not None:
+            dg_ptr, db_ptr, acc = ctx.direct[0].data_ptr(), ctx.direct[1].data_ptr(), 1
+            dgb = None
+        else:
+            dgb = torch.empty(2 * c, **f32)
+            dg_ptr, db_ptr, acc = dgb.data_ptr(), dgb[c:].data_ptr(), 0
         coef = torch.empty(3 * c, **f32)
-        partials = torch.empty(ctx.ws, **f32)
-        rc = lib.plx_bn_backward(
-            x.data_ptr(), mask.data_ptr() if mask is not None else None, dy.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else None,
-            m, c, weight.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(), dgb.data_ptr(), dgb[c:].data_ptr(),
-            coef.data_ptr(), partials.data_ptr(), int(ctx.relu), _stream())
-        _native.check(rc, "plx_bn_backward")
+        part, nblk = ctx.link.take() if ctx.link is not None else (None, 0)
+        if part is not None:  # the consumer's dgrad epilogue already reduced dz and dz*xhat per block
+            l2 = torch.empty(int(lib.plx_bn_l2_workspace(nblk, c)), **f32)
+            rc = lib.plx_bn_backward_from_partials(
+                x.data_ptr(), mask.data_ptr() if mask is not None else None, dy.data_ptr(), dx.data_ptr(),
+                dres.data_ptr() if dres is not None else None, m, c, weight.data_ptr(), stats.data_ptr(),
+                stats[c:].data_ptr(), dg_ptr, db_ptr, coef.data_ptr(), part.data_ptr(), nblk, l2.data_ptr(),
+                int(ctx.relu), acc, _stream())
+            _native.check(rc, "plx_bn_backward_from_partials")
+        else:
+            partials = torch.empty(ctx.ws, **f32)
+            rc = lib.plx_bn_backward(
+                x.data_ptr(), mask.data_ptr() if mask is not None else None, dy.data_ptr(), dx.data_ptr(),
+                dres.data_ptr() if dres is not None else None, m, c, weight.data_ptr(), stats.data_ptr(),
+                stats[c:].data_ptr(), dg_ptr, db_ptr, coef.data_ptr(), partials.data_ptr(), int(ctx.relu), acc,
+                _stream())
+            _native.check(rc, "plx_bn_backward")
         if ctx.box is not None:  # the residual's gradient rides into conv1's dgrad epilogue (ops.conv1x1)
             ctx.box.put(dres)
             dres = None
-        return dx, dgb[:c], dgb[c:], None, None, dres, None, None, None, None, None
+        dgamma = dgb[:c] if dgb is not None else None
+        dbeta = dgb[c:] if dgb is not None else None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None
 
 
 def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
@@ -106,8 +136,11 @@ def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_me
     if residual is not None and residual.dtype != x.dtype:
         residual = residual.to(x.dtype)
     if training:
-        return _BNAct.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, act, ext_stats,
-                            residual_grad_box)
+        link = BnLink()
+        y = _BNAct.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, act, ext_stats,
+                         residual_grad_box, link)
+        y._plx_bn_link = link
+        return y
     # inference: fold running stats into scale/bias, one apply pass
     lib = _native.lib("plx_bn")
     x = _cl(x)

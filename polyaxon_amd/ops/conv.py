@@ -20,8 +20,11 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import ctypes
+
 from polyaxon_amd.ops import _native
-from polyaxon_amd.ops.conv1x1 import _bf16_context, _num_cus, _stream, _zero_page, nt_stats_rows
+from polyaxon_amd.ops.conv1x1 import GradMailbox, _bf16_context, _num_cus, _stream, _zero_page, bn_link_of, nt_stats_rows
+from polyaxon_amd.ops.flat import direct_grad
 
 
 def _out(h: int, k: int, s: int) -> int:
@@ -44,7 +47,7 @@ def weight_prep_k(w: torch.Tensor):
 
 class _ConvK(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stats, stride):
+    def forward(ctx, x, weight, stats, stride, box, link):
         lib = _native.lib("plx_conv")
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         n, cin, h, w = x.shape
@@ -59,6 +62,10 @@ class _ConvK(torch.autograd.Function):
         ctx.save_for_backward(x, wd)
         ctx.wshape = weight.shape
         ctx.stride = stride
+        ctx.box = box
+        ctx.link = link if not (stride == 2 and k == 1) else None  # that dgrad never writes the odd pixels
+        g = direct_grad(weight)
+        ctx.wgrad = g if (g is not None and g.stride() == (k * k * cin, 1, k * cin, cin)) else None
         return y
 
     @staticmethod
@@ -71,22 +78,38 @@ class _ConvK(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         zero = _zero_page(x.device).data_ptr()
         dx = dw = None
+        extra = ctx.box.take() if ctx.box is not None else None
         if ctx.needs_input_grad[0]:
-            # a strided 1x1 only reaches the even-even pixels: the rest of dx is zero
-            dx = (torch.zeros_like if (s == 2 and k == 1) else torch.empty_like)(x, memory_format=torch.channels_last)
+            add = None
+            if extra is not None:
+                extra = extra.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+                if s == 2 and k == 1:
+                    dx = add = extra  # in place: the even pixels get += dgrad, the rest keep the deferred gradient
+                else:
+                    add = extra
+            if dx is None:
+                # a strided 1x1 only reaches the even-even pixels: the rest of dx is zero
+                dx = (torch.zeros_like if (s == 2 and k == 1) else torch.empty_like)(x, memory_format=torch.channels_last)
+            bnr = None
+            if ctx.link is not None and (ctx.box is None or extra is not None):
+                nblk = int(lib.plx_conv_dgrad_blocks(n, h, w, cin, cout, k, s))
+                bnr = ctx.link.request(nblk)
             rc = lib.plx_conv_dgrad(dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), n, h, w, cin, cout, k, s, zero,
-                                    _stream())
+                                    add.data_ptr() if add is not None else None,
+                                    ctypes.addressof(bnr) if bnr is not None else None, _stream())
             _native.check(rc, "plx_conv_dgrad")
         if ctx.needs_input_grad[1]:
             cus = _num_cus(x.device)
             ws = torch.empty(int(lib.plx_conv_wgrad_workspace(n, h, w, cin, cout, k, s, cus)), dtype=torch.float32,
                              device=x.device)
-            g = torch.empty(cout, k, k, cin, dtype=torch.float32, device=x.device)  # [co][kh][kw][ci]
+            direct = ctx.wgrad is not None
+            g = ctx.wgrad if direct else torch.empty(cout, k, k, cin, dtype=torch.float32, device=x.device)
             rc = lib.plx_conv_wgrad(dy.data_ptr(), x.data_ptr(), g.data_ptr(), ws.data_ptr(), n, h, w, cin, cout, k,
-                                    s, zero, cus, 0, _stream())
+                                    s, zero, cus, int(direct), _stream())
             _native.check(rc, "plx_conv_wgrad")
-            dw = g.permute(0, 3, 1, 2)  # [co][ci][kh][kw] view with channels_last strides
-        return dx, dw, None, None
+            if not direct:
+                dw = g.permute(0, 3, 1, 2)  # [co][ci][kh][kw] view with channels_last strides
+        return dx, dw, None, None, None, None
 
 
 def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -97,7 +120,10 @@ def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
             and conv.in_channels % 64 == 0 and conv.out_channels % 64 == 0 and x.numel() > 0)
 
 
-def conv_k(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, with_stats: bool = False) -> torch.Tensor:
+def conv_k(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, with_stats: bool = False,
+           grad_box: GradMailbox = None, bn_link: bool = False) -> torch.Tensor:
+    """``grad_box``: add the box's deferred gradient into dx (see ops.conv1x1.GradMailbox); ``bn_link``: dx is the
+    complete gradient of ``x`` — serve the producing BatchNorm its backward partials (ops.conv1x1.BnLink)."""
     stats = None
     if with_stats:
         n, _, h, w = x.shape
@@ -105,7 +131,9 @@ def conv_k(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, with_stats: b
         m, cout = n * _out(h, k, stride) * _out(w, k, stride), weight.shape[0]
         nblk = -(-m // nt_stats_rows(cout))
         stats = torch.empty(2 * nblk * cout, dtype=torch.float32, device=x.device)
-    y = _ConvK.apply(x, weight, stats, stride)
+    if grad_box is not None:
+        grad_box.armed = True
+    y = _ConvK.apply(x, weight, stats, stride, grad_box, bn_link_of(x, bn_link))
     if stats is not None:
         y._plx_channel_stats = (stats, nblk)
     return y
@@ -121,9 +149,10 @@ class ConvKxK(nn.Conv2d):
         self.native = native
         self.bn_stats = bn_stats
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, grad_box: GradMailbox = None, bn_link: bool = False) -> torch.Tensor:
         if self.native and supported(x, self):
-            return conv_k(x, self.weight, self.stride[0], with_stats=self.bn_stats and self.training)
+            return conv_k(x, self.weight, self.stride[0], with_stats=self.bn_stats and self.training,
+                          grad_box=grad_box, bn_link=bn_link)
         return F.conv2d(x, self.weight, None, self.stride, self.padding)
 
 

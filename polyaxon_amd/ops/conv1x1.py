@@ -14,6 +14,7 @@ gradient comes back in fp32, so autocast's bf16 weight copy and its backward cas
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict
 
 import torch
@@ -21,6 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from polyaxon_amd.ops import _native
+from polyaxon_amd.ops.flat import direct_grad
 
 _ZERO: Dict[int, torch.Tensor] = {}
 _CUS: Dict[int, int] = {}
@@ -51,10 +53,11 @@ def nt_stats_rows(n: int) -> int:
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, stats: torch.Tensor = None,
-            add: torch.Tensor = None) -> torch.Tensor:
+            add: torch.Tensor = None, bnr: "_native.BnBwdArgs" = None) -> torch.Tensor:
     """out[M][N] = a[M][K] · b[N][K]ᵀ, bf16 (rows may be strided, K contiguous).  ``stats`` (fp32
     [2][ceil(M / nt_stats_rows(N))][N]) receives per-block channel sums and sums of squares of ``out``;
-    ``add`` (bf16 [M][N]) is summed into the product in the epilogue."""
+    ``add`` (bf16 [M][N]) is summed into the product in the epilogue; ``bnr`` (from :meth:`BnLink.request`)
+    makes the epilogue emit the BatchNorm-backward partials of ``out``."""
     m, k = a.shape
     n = b.shape[0]
     if out is None:
@@ -70,7 +73,8 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, stats: t
                                              b.stride(0), out.stride(0), _zero_page(a.device).data_ptr(),
                                              stats.data_ptr() if stats is not None else None,
                                              add.data_ptr() if add is not None else None,
-                                             add.stride(0) if add is not None else 0, _stream())
+                                             add.stride(0) if add is not None else 0,
+                                             ctypes.addressof(bnr) if bnr is not None else None, _stream())
     _native.check(rc, "plx_gemm_nt")
     return out
 
@@ -112,23 +116,59 @@ class GradMailbox:
 
     In a ResNet identity block the block input feeds conv1 and the residual add of bn3; autograd would sum the
     two gradients with a separate bf16 add over the whole activation.  Instead bn3's backward ``put``s its
-    residual gradient here and conv1's backward adds it in its data-gradient GEMM epilogue.  conv1 runs before
-    bn3 in the forward, so it ``arm``s the box only when it took the native path that will consume it; bn3
-    defers its gradient only into an armed box.  Reverse-topological backward order guarantees bn3's backward
-    (later in the forward) runs before conv1's."""
+    residual gradient here and conv1's backward adds it in its data-gradient GEMM epilogue.  In a downsampling
+    block the input feeds the downsample conv and conv1: conv1's backward ``put``s its data gradient and the
+    downsample conv's dgrad adds it (in place, for the strided 1x1 whose GEMM only reaches the even pixels).
+    The consumer runs first in the forward and ``arm``s the box only on the native path that will drain it;
+    the producer defers only into an armed box and sets ``expect``.  Reverse-topological backward order (higher
+    autograd sequence number first) runs the producer's backward before the consumer's; ``take`` fails loudly
+    if that ever does not hold instead of silently dropping a gradient."""
 
-    __slots__ = ("armed", "grad")
+    __slots__ = ("armed", "grad", "expect")
 
     def __init__(self):
         self.armed = False
         self.grad = None
+        self.expect = False
 
     def put(self, g: torch.Tensor) -> None:
         self.grad = g if self.grad is None else self.grad + g
 
     def take(self):
         g, self.grad = self.grad, None
+        if g is None and self.expect:
+            raise RuntimeError("GradMailbox: the deferred gradient did not arrive before its consumer's backward")
         return g
+
+
+class BnLink:
+    """A fused BatchNorm(+ReLU)'s output → the convolution whose data gradient is that output's COMPLETE gradient.
+
+    The BatchNorm forward attaches one to its output (``y._plx_bn_link``) holding what its backward reduction
+    reads (x, ReLU mask, mean, invstd).  A consumer conv that the model marks as the sole gradient source
+    (``bn_link=True``) ``request``s a partials buffer and its dgrad GEMM epilogue writes the per-block
+    Σdz and Σdz·x̂ (csrc/conv_gemm.hip ``BnBwd``); the BatchNorm backward then skips its reduce pass."""
+
+    __slots__ = ("x", "mask", "mean", "invstd", "part", "nblk", "_args")
+
+    def __init__(self, x=None, mask=None, mean=None, invstd=None):
+        self.x, self.mask, self.mean, self.invstd = x, mask, mean, invstd
+        self.part = None
+        self.nblk = 0
+        self._args = None
+
+    def request(self, nblk: int) -> "_native.BnBwdArgs":
+        c = self.x.shape[1]
+        self.part = torch.empty(2 * nblk * c, dtype=torch.float32, device=self.x.device)
+        self.nblk = nblk
+        self._args = _native.BnBwdArgs(self.x.data_ptr(), self.mask.data_ptr() if self.mask is not None else None,
+                                       self.mean.data_ptr(), self.invstd.data_ptr(), self.part.data_ptr(), nblk, 0)
+        return self._args
+
+    def take(self):
+        part, nblk = self.part, self.nblk
+        self.part, self._args = None, None
+        return part, nblk
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -137,11 +177,21 @@ def _rows(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
 
 
+def bn_link_of(x: torch.Tensor, want: bool):
+    link = getattr(x, "_plx_bn_link", None) if want else None
+    return link if (link is not None and link.x is not None and link.x.shape == x.shape) else None
+
+
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stats, box):
+    def forward(ctx, x, weight, stats, box, sink, link):
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         ctx.box = box
+        ctx.sink = sink if (sink is not None and sink.armed) else None
+        if ctx.sink is not None:
+            ctx.sink.expect = True
+        ctx.link = link
+        ctx.wgrad = direct_grad(weight)
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         wb, wt = weight_prep(weight)
@@ -155,6 +205,7 @@ class _Conv1x1(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, wt = ctx.saved_tensors
+        n, cin, h, w = x.shape
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         extra = ctx.box.take() if ctx.box is not None else None
@@ -162,10 +213,22 @@ class _Conv1x1(torch.autograd.Function):
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             if extra is not None:
                 extra = extra.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-            gemm_nt(_rows(dy), wt, _rows(dx), add=_rows(extra) if extra is not None else None)
+            bnr = None
+            # the link is only served when dx (+ the box's gradient) is the whole gradient of x: with a box, the
+            # producer must actually have deferred into it; a sink means dx is only part of it
+            if ctx.link is not None and ctx.sink is None and (ctx.box is None or extra is not None):
+                bnr = ctx.link.request(-(-(n * h * w) // nt_stats_rows(cin)))
+            gemm_nt(_rows(dy), wt, _rows(dx), add=_rows(extra) if extra is not None else None, bnr=bnr)
+            if ctx.sink is not None:  # the downsample conv's dgrad adds this gradient in its epilogue
+                ctx.sink.put(dx)
+                dx = None
         if ctx.needs_input_grad[1]:
-            dw = gemm_tn(_rows(dy), _rows(x)).view(ctx.wshape).to(ctx.wdtype)
-        return dx, dw, None, None
+            cout = ctx.wshape[0]
+            if ctx.wgrad is not None:  # accumulate into the flat gradient slot, autograd sees no weight grad
+                gemm_tn(_rows(dy), _rows(x), out=ctx.wgrad.as_strided((cout, cin), (cin, 1)), accumulate=True)
+            else:
+                dw = gemm_tn(_rows(dy), _rows(x)).view(ctx.wshape).to(ctx.wdtype)
+        return dx, dw, None, None, None, None
 
 
 def _bf16_context(x: torch.Tensor) -> bool:
@@ -182,9 +245,12 @@ def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, with_stats: bool = False,
-            grad_box: "GradMailbox" = None) -> torch.Tensor:
+            grad_box: "GradMailbox" = None, grad_sink: "GradMailbox" = None, bn_link: bool = False) -> torch.Tensor:
     """With ``with_stats`` the output carries ``_plx_channel_stats`` = (fp32 [2][nblk][Cout] per-block channel
-    sums / sums of squares, nblk), which a following fused BatchNorm uses instead of its own stats pass."""
+    sums / sums of squares, nblk), which a following fused BatchNorm uses instead of its own stats pass.
+    ``grad_box``: add the box's deferred gradient into dx; ``grad_sink``: defer dx into that (armed) box;
+    ``bn_link``: dx (+ ``grad_box``'s gradient) is the complete gradient of ``x`` — serve the BatchNorm that
+    produced ``x`` its backward partials (:class:`BnLink`)."""
     stats = None
     if with_stats:
         n, _, h, w = x.shape
@@ -193,7 +259,7 @@ def conv1x1(x: torch.Tensor, weight: torch.Tensor, with_stats: bool = False,
         stats = torch.empty(2 * nblk * cout, dtype=torch.float32, device=x.device)
     if grad_box is not None:
         grad_box.armed = True
-    y = _Conv1x1.apply(x, weight, stats, grad_box)
+    y = _Conv1x1.apply(x, weight, stats, grad_box, grad_sink, bn_link_of(x, bn_link))
     if stats is not None:
         y._plx_channel_stats = (stats, nblk)
     return y
@@ -208,7 +274,9 @@ class Conv1x1(nn.Conv2d):
         self.native = native
         self.bn_stats = bn_stats  # emit channel stats for the BatchNorm that follows (training only)
 
-    def forward(self, x: torch.Tensor, grad_box: GradMailbox = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, grad_box: GradMailbox = None, grad_sink: GradMailbox = None,
+                bn_link: bool = False) -> torch.Tensor:
         if self.native and supported(x, self):
-            return conv1x1(x, self.weight, with_stats=self.bn_stats and self.training, grad_box=grad_box)
+            return conv1x1(x, self.weight, with_stats=self.bn_stats and self.training, grad_box=grad_box,
+                           grad_sink=grad_sink, bn_link=bn_link)
         return F.conv2d(x, self.weight, None, self.stride)

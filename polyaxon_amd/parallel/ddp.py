@@ -48,6 +48,7 @@ def init_from_env(backend: Optional[str] = None, device: Optional[torch.device] 
 class FlatDDP:
     def __init__(self, flat: FlatParams, process_group=None, bucket_mb: float = 64.0, overlap: bool = True):
         self.flat = flat
+        flat.enable_direct_grads(False)  # bucket readiness needs autograd's post-accumulate hooks
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.overlap = overlap and self.world > 1

@@ -57,6 +57,7 @@ class ResidentTrialExecutor:
             model = model.to(memory_format=torch.channels_last)
         self.model = model
         self.flat = FlatParams(model, self.device, channels_last=channels_last)
+        self.flat.enable_direct_grads(True)  # native ops accumulate weight grads straight into flat.grads
         self._flatten_buffers()
         self.step = torch.zeros(1, dtype=torch.int32, device=self.device)
         if optimizer == "sgd":

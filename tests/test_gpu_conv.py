@@ -218,3 +218,90 @@ def test_convk_strided_autograd(cuda, k, stride, shape, cout):
     torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=8e-2)
     torch.testing.assert_close(xa.grad.float(), xr.grad, rtol=2e-2, atol=8e-2)
     torch.testing.assert_close(conv.weight.grad, wr.grad, rtol=2e-2, atol=0.2)
+
+
+def _bn_chain_grads(cuda, conv_ctor, shape, link, seed=3):
+    """x -> fused BN+ReLU -> conv (bn_link on/off) -> sum(g * y); grads of x, gamma, beta and the conv weight."""
+    from polyaxon_amd.ops.norm import BatchNormAct
+
+    torch.manual_seed(seed)
+    bn = BatchNormAct(shape[1], act=True).to(cuda)
+    conv = conv_ctor().to(cuda)
+    conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    x = (torch.randn(shape, device=cuda) + 0.3).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
+    y = conv(bn(x), bn_link=link)
+    g = torch.randn_like(y.float()).to(torch.bfloat16)
+    y.backward(g)
+    return x.grad.float(), bn.weight.grad.clone(), bn.bias.grad.clone(), conv.weight.grad.clone()
+
+
+@pytest.mark.parametrize("kind,shape,cout", [("1x1", (2, 128, 10, 12), 256), ("1x1", (3, 64, 7, 9), 64),
+                                             ("3x3s1", (2, 64, 9, 11), 128), ("3x3s2", (2, 128, 14, 14), 128),
+                                             ("3x3s2", (2, 64, 9, 7), 64)])
+def test_bn_backward_partials_from_dgrad_epilogue(cuda, kind, shape, cout):
+    """The BN-backward channel reduction fused into the consumer conv's dgrad GEMM epilogue (BnLink) gives the
+    same gradients as the BN's own reduce pass."""
+    from polyaxon_amd.ops.conv import ConvKxK
+    from polyaxon_amd.ops.conv1x1 import Conv1x1
+
+    cin = shape[1]
+    ctor = {"1x1": lambda: Conv1x1(cin, cout), "3x3s1": lambda: ConvKxK(cin, cout, 3, 1),
+            "3x3s2": lambda: ConvKxK(cin, cout, 3, 2)}[kind]
+    ref = _bn_chain_grads(cuda, ctor, shape, link=False)
+    got = _bn_chain_grads(cuda, ctor, shape, link=True)
+    for a, b, name in zip(got, ref, ("dx", "dgamma", "dbeta", "dw")):
+        torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2 * float(b.abs().max()), msg=name)
+
+
+def test_direct_flat_grads_match_autograd(cuda):
+    """FlatParams.enable_direct_grads: the native convs / BN accumulate straight into the flat gradient buffer
+    (returning no weight grad to autograd) and produce the same gradients as autograd's accumulation."""
+    from polyaxon_amd.models.resnet import ResNet
+    from polyaxon_amd.ops.flat import FlatParams
+
+    torch.manual_seed(0)
+    x = torch.randn(4, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (4,), device=cuda)
+    grads = []
+    for direct in (False, True):
+        torch.manual_seed(1)
+        m = ResNet([2, 1, 1, 1], num_classes=10, width=64, zero_init_residual=False).to(memory_format=torch.channels_last)
+        flat = FlatParams(m, cuda)
+        flat.enable_direct_grads(direct)
+        for _ in range(2):  # two backwards accumulate
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x).float(), y)
+            loss.backward()
+        grads.append(flat.grads.clone())
+    torch.testing.assert_close(grads[1], grads[0], rtol=2e-2, atol=2e-2 * float(grads[0].abs().max()))
+    assert float(grads[0].abs().sum()) > 0
+
+
+def test_downsample_mailbox_matches_autograd_sum(cuda):
+    """Downsampling block: conv1's dgrad deferred into the (strided) downsample conv's dgrad epilogue equals
+    autograd summing the two branch gradients."""
+    from polyaxon_amd.models.resnet import Bottleneck, Downsample
+
+    for stride, cin in ((2, 256), (1, 64)):
+        torch.manual_seed(5)
+        ds = Downsample(cin, 256 if stride == 1 else 512, stride)
+        blk = Bottleneck(cin, 64 if stride == 1 else 128, stride, ds).to(cuda).to(memory_format=torch.channels_last)
+        x = torch.randn(2, cin, 14, 14, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        outs = []
+        for fused in (True, False):
+            xa = x.clone().requires_grad_()
+            if fused:
+                out = blk(xa)
+            else:  # the same block with no mailbox: autograd sums the branch gradients
+                identity = blk.downsample(xa)
+                o = blk.bn2(blk.conv2(blk.bn1(blk.conv1(xa))))
+                out = blk.bn3(blk.conv3(o), identity)
+            torch.manual_seed(9)
+            out.backward(torch.randn_like(out.float()).to(torch.bfloat16))
+            outs.append(xa.grad.float())
+            blk.zero_grad(set_to_none=True)
+        torch.testing.assert_close(outs[0], outs[1], rtol=2e-2, atol=2e-2 * float(outs[1].abs().max()))
