@@ -119,6 +119,69 @@ __global__ __launch_bounds__(256) void gp_kmat_kernel(const float* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------------------------------ batched fp64 Gram
+// Length-scale fit (log marginal likelihood over a batch of scales): K[b][i][j] = k(|X_i - X_j| / ls_b) + diag
+// in fp64 end to end.  The fp32 MFMA Gram above is exact enough for the posterior, but a long length scale
+// makes K nearly singular (entries 1 - O(r^2)) and fp32 rounding turns it indefinite, so the LML search would
+// wrongly reject the scales the fp64 objective prefers.  One thread per (i, j <= i) pair: the distance is
+// summed once in fp64 from direct differences and every scale of the batch is written (mirrored to (j, i)).
+__device__ __forceinline__ double bessel_k_nu_f64(double z, double nu) {
+  const double tmax = acosh(fmax(1.0, 40.0 / fmax(z, 1e-12))) + 2.5;
+  const int n = 160;
+  const double h = tmax / n;
+  double s = 0.5 * exp(-z);
+  for (int i = 1; i <= n; ++i) {
+    const double t = i * h;
+    const double et = exp(t), ei = 1.0 / et;
+    const double w = (i == n) ? 0.5 : 1.0;
+    s += w * exp(-z * 0.5 * (et + ei)) * 0.5 * (exp(nu * t) + exp(-nu * t));
+  }
+  return s * h;
+}
+
+__device__ __forceinline__ double kernel_from_sq_f64(double r2, int kind, double nu, double matern_c) {
+  if (kind == kRBF) return exp(-0.5 * r2);
+  const double r = sqrt(r2);
+  if (kind == kMatern05) return exp(-r);
+  if (kind == kMatern15) {
+    const double a = 1.7320508075688772 * r;
+    return (1.0 + a) * exp(-a);
+  }
+  if (kind == kMatern25) {
+    const double a = 2.23606797749979 * r;
+    return (1.0 + a + a * a / 3.0) * exp(-a);
+  }
+  const double s = sqrt(2.0 * nu) * r;
+  if (s < 1e-12) return 1.0;
+  if (s > 700.0) return 0.0;
+  return matern_c * pow(s, nu) * bessel_k_nu_f64(s, nu);
+}
+
+__global__ __launch_bounds__(256) void gp_kmat_batch_f64_kernel(const double* __restrict__ X, int n, int d,
+                                                                const double* __restrict__ inv_ls2, int nb,
+                                                                double* __restrict__ K, int kind, double nu,
+                                                                double matern_c, double diag) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // packed lower-triangle index
+  const int64_t total = (int64_t)n * (n + 1) / 2;
+  if (p >= total) return;
+  int i = (int)((sqrt(8.0 * (double)p + 1.0) - 1.0) * 0.5);
+  while ((int64_t)i * (i + 1) / 2 > p) --i;
+  while ((int64_t)(i + 1) * (i + 2) / 2 <= p) ++i;
+  const int j = (int)(p - (int64_t)i * (i + 1) / 2);
+  double sq = 0.0;
+  for (int k = 0; k < d; ++k) {
+    const double t = X[(int64_t)i * d + k] - X[(int64_t)j * d + k];
+    sq = fma(t, t, sq);
+  }
+  for (int b = 0; b < nb; ++b) {
+    double v = kernel_from_sq_f64(sq * inv_ls2[b], kind, nu, matern_c);
+    if (i == j) v += diag;
+    double* Kb = K + (int64_t)b * n * n;
+    Kb[(int64_t)i * n + j] = v;
+    Kb[(int64_t)j * n + i] = v;
+  }
+}
+
 // ------------------------------------------------------------------------------------------ cholesky
 constexpr int CHOL_MAX = 128;
 
@@ -261,6 +324,16 @@ PLX_API int plx_gp_kmat(const float* A, const float* B, int n, int m, int d, flo
   dim3 grid((m + KB - 1) / KB, (n + KB - 1) / KB);
   hipLaunchKernelGGL(gp_kmat_kernel, grid, dim3(256), 0, stream, A, B, n, m, d, K, ldk, kind, inv_ls2, nu, matern_c,
                      add_diag, diag);
+  return (int)hipGetLastError();
+}
+
+// K: fp64 [nb][n][n]; inv_ls2: device fp64 [nb] (1 / length_scale^2 per batch entry)
+PLX_API int plx_gp_kmat_batch_f64(const double* X, int n, int d, const double* inv_ls2, int nb, double* K, int kind,
+                                  double nu, double matern_c, double diag, hipStream_t stream) {
+  if (n <= 0 || d <= 0 || nb <= 0) return 1;
+  const int64_t total = (int64_t)n * (n + 1) / 2;
+  hipLaunchKernelGGL(gp_kmat_batch_f64_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, X, n, d,
+                     inv_ls2, nb, K, kind, nu, matern_c, diag);
   return (int)hipGetLastError();
 }
 

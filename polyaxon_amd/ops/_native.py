@@ -172,6 +172,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
     "plx_gp": {
         "plx_gp_kmat": [_P, _P, _I, _I, _I, _P, _I, _I, _F, _F, _F, _I, _F, _P],
         "plx_gp_chol": [_P, _I, _I, _P, _P],
+        "plx_gp_kmat_batch_f64": [_P, _I, _I, _P, _I, _P, _I, _D, _D, _D, _P],
         "plx_gp_predict_acq": [_P, _I, _P, _I, _I, _P, _I, _P, _I, _F, _F, _F, _F, _I, _F, _F, _F, _P, _P, _P, _P,
                                _P, _P],
     },

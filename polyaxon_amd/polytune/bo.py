@@ -13,8 +13,9 @@ Two execution paths, same semantics:
   single-workgroup fp64 LDS Cholesky, fused predict+UCB/EI/POI+argmax over every candidate in one launch.
   Because a candidate costs nanoseconds there, acquisition maximisation evaluates the docstring's intended
   effort (1e5 random candidates, acquisition_function.py:75) plus rounds of batched local refinement around
-  the best points instead of sequential scipy restarts.  The length scale is still fit by maximising the
-  log marginal likelihood (1-D bounded search on log ls, host side: n is tens to hundreds).
+  the best points instead of sequential scipy restarts.  The length scale is fit by maximising the log
+  marginal likelihood on the device too: batched Gram kernels + one batched fp64 Cholesky per zoom round
+  (``HipGP.fit_length_scale``), so an n ~ 1000 suggestion is not bound by host O(n^3) factorisations.
 * ``backend="numpy"`` — the same math as the HIP path in numpy (CPU-only hosts, and the kernels' parity
   reference).
 """
@@ -227,7 +228,13 @@ def acquisition_np(mean, std, acq: str, y_max: float, kappa: float, eps: float) 
 
 # ================================================================================ HIP path
 class HipGP:
-    """GP posterior + acquisition on the MI355X kernels. Training data and factors stay on the device."""
+    """GP posterior + acquisition on the MI355X kernels. Training data and factors stay on the device.
+
+    Gram matrices are always built by our kernels; fp64 factorisations above ``DEVICE_FACTOR_MAX`` rows run
+    through LAPACK on the host (a one-off D2H of the Gram): torch's device Cholesky faulted the GPU at n = 1000
+    on this ROCm build (scripts/diag_bo1000.py), while n <= 128 goes through our LDS Cholesky or torch."""
+
+    DEVICE_FACTOR_MAX = 128
 
     def __init__(self, device=None):
         import torch
@@ -258,7 +265,11 @@ class HipGP:
         t = self.torch
         n = K.shape[0]
         if n > 128:
-            return t.linalg.cholesky(K.double()).float()
+            try:
+                L = np.linalg.cholesky(K.double().cpu().numpy())
+            except np.linalg.LinAlgError as e:
+                raise np.linalg.LinAlgError(str(e))
+            return t.as_tensor(L, dtype=t.float32, device=self.device)
         status = t.zeros(1, dtype=t.int32, device=self.device)
         out = K.clone()
         rc = self.lib.plx_gp_chol(out.data_ptr(), n, n, status.data_ptr(), self._stream())
@@ -267,8 +278,75 @@ class HipGP:
             raise np.linalg.LinAlgError(f"not positive definite at column {int(status.item())}")
         return out
 
+    def lml_batch(self, X, y, kind: str, nu: float, log_ls, alpha: float = 1e-10):
+        """Log marginal likelihood at every length scale exp(log_ls): ONE fp64 Gram launch for the whole batch
+        (plx_gp_kmat_batch_f64), fp64 Cholesky per scale, one batched solve."""
+        t = self.torch
+        Xd = t.as_tensor(np.ascontiguousarray(X, dtype=np.float64), device=self.device)
+        yd = t.as_tensor(y, dtype=t.float64, device=self.device)
+        n, d = Xd.shape
+        nb = len(log_ls)
+        inv = t.tensor([math.exp(-2.0 * float(l)) for l in log_ls], dtype=t.float64, device=self.device)
+        Ks = t.empty((nb, n, n), dtype=t.float64, device=self.device)
+        rc = self.lib.plx_gp_kmat_batch_f64(Xd.data_ptr(), n, d, inv.data_ptr(), nb, Ks.data_ptr(), KIND_IDS[kind],
+                                            float(nu), float(matern_c(nu)) if kind == "matern_nu" else 0.0,
+                                            float(alpha), self._stream())
+        self._native.check(rc, "plx_gp_kmat_batch_f64")
+        if n > self.DEVICE_FACTOR_MAX:
+            return self._lml_host(Ks.cpu().numpy(), np.asarray(y, dtype=np.float64))
+        # one factorisation per scale: a batched cholesky_ex on ROCm does not keep the other batch entries
+        # valid once one of them is not positive definite (measured: wrong LMLs beside a failing entry)
+        Ls, oks = [], []
+        for b in range(nb):
+            Lb, ib = t.linalg.cholesky_ex(Ks[b])
+            Ls.append(Lb)
+            oks.append(ib == 0)
+        L, ok = t.stack(Ls), t.stack(oks)
+        L = t.where(ok[:, None, None], L, t.eye(n, dtype=L.dtype, device=self.device).expand_as(L))
+        a = t.cholesky_solve(yd[None, :, None].expand(nb, n, 1).contiguous(), L)[..., 0]
+        lml = -0.5 * (a * yd[None]).sum(1) - t.log(t.diagonal(L, dim1=1, dim2=2)).sum(1) - 0.5 * n * math.log(2 * math.pi)
+        lml = t.where(ok & t.isfinite(lml), lml, t.full_like(lml, -math.inf))
+        return lml.cpu().numpy()
+
+    @staticmethod
+    def _lml_host(Ks: np.ndarray, y: np.ndarray) -> np.ndarray:
+        """fp64 LAPACK factorisations of device-built Gram matrices (sklearn semantics: not PD -> -inf)."""
+        out = np.full(Ks.shape[0], -np.inf)
+        n = Ks.shape[1]
+        for b in range(Ks.shape[0]):
+            try:
+                L = np.linalg.cholesky(Ks[b])
+            except np.linalg.LinAlgError:
+                continue
+            from scipy.linalg import cho_solve
+
+            a = cho_solve((L, True), y)
+            v = -0.5 * float(y @ a) - float(np.log(np.diag(L)).sum()) - 0.5 * n * math.log(2 * math.pi)
+            out[b] = v if math.isfinite(v) else -np.inf
+        return out
+
+    def fit_length_scale(self, X, y, kind: str, nu: float, length_scale: float, alpha: float = 1e-10,
+                         bounds=(1e-5, 1e5), coarse: int = 24, rounds: int = 3) -> float:
+        """Maximise the LML over log length scale on the device: a coarse batched grid over the bounds (plus the
+        configured initial value, as sklearn always tries it), then batched zoom rounds around the best point.
+        Replaces the host 1-D search, whose O(n^3) factorisations dominate a suggestion at n ~ 1000."""
+        lo, hi = math.log(bounds[0]), math.log(bounds[1])
+        grid = list(np.linspace(lo, hi, coarse)) + [math.log(length_scale)]
+        vals = self.lml_batch(X, y, kind, nu, grid, alpha)
+        best = int(np.argmax(vals))
+        x_best, f_best = grid[best], vals[best]
+        step = (hi - lo) / (coarse - 1)
+        for _ in range(rounds):
+            g = list(np.linspace(max(lo, x_best - step), min(hi, x_best + step), 9))
+            v = self.lml_batch(X, y, kind, nu, g, alpha)
+            i = int(np.argmax(v))
+            if v[i] > f_best:
+                x_best, f_best = g[i], v[i]
+            step /= 4.0
+        return math.exp(x_best) if math.isfinite(f_best) else float(length_scale)
+
     def fit(self, gp: GPState):
-        """Device factors for a host-fitted GP (length scale from the LML search)."""
+        """Device factors for a fitted GP (length scale from the LML search)."""
         t = self.torch
         K = self.kmat(gp.X, gp.X, gp.kind, gp.ls, gp.nu, diag=1e-10)
         jitter = 0.0
@@ -365,11 +443,16 @@ class UtilityFunction:
                                                              random_state=self.random_generator)
             self.gaussian_process.fit(X, y)
             return
-        self._gp = fit_gp(X, y, kernel=g.kernel, nu=g.nu, length_scale=g.length_scale)
         if self.backend == "hip":
             if self._hip is None:
                 self._hip = HipGP()
+            kind = _kind(g.kernel, g.nu)
+            ls = self._hip.fit_length_scale(X, y, kind, g.nu, g.length_scale) if len(X) > 1 else float(g.length_scale)
+            self._gp = GPState(np.asarray(X, dtype=np.float64), np.asarray(y, dtype=np.float64), ls, kind, g.nu,
+                               None, None, float("nan"))
             self._dev = self._hip.fit(self._gp)
+            return
+        self._gp = fit_gp(X, y, kernel=g.kernel, nu=g.nu, length_scale=g.length_scale)
 
     def compute(self, x: np.ndarray, y_max: float) -> np.ndarray:
         acq = self.acquisition_function
