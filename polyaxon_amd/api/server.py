@@ -20,7 +20,7 @@ import time
 from typing import Any, Dict, List, Optional
 
 from fastapi import Depends, FastAPI, Header, HTTPException, Query, Request
-from fastapi.responses import FileResponse, JSONResponse, PlainTextResponse, StreamingResponse
+from fastapi.responses import FileResponse, JSONResponse, PlainTextResponse, Response, StreamingResponse
 
 from polyaxon_amd import __version__
 from polyaxon_amd.spec import PolyaxonfileError, specification_for
@@ -169,6 +169,76 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
     def list_users(user=Depends(superuser)):
         rows = store.execute("SELECT id, username, email, is_superuser, created_at FROM users ORDER BY id").fetchall()
         return {"results": [dict(r) for r in rows]}
+
+    # ------------------------------------------------------------------ admin (reference db/admin/*.py)
+    # The reference registers every model with the Django admin; here a superuser gets a generic table
+    # browser over the store: list tables with counts, page through rows, edit or delete a row.  Secrets
+    # (API tokens, kv values holding ephemeral tokens) are never returned.
+    _SECRET_COLS = {"token"}
+
+    def _admin_tables() -> List[str]:
+        rows = store.execute("SELECT name FROM sqlite_master WHERE type='table' AND name NOT LIKE 'sqlite_%' "
+                             "ORDER BY name").fetchall()
+        return [r[0] for r in rows]
+
+    def _admin_table(name: str) -> List[str]:
+        if name not in _admin_tables():
+            raise HTTPException(404, f"table {name} not found")
+        return [r[1] for r in store.execute(f"PRAGMA table_info({name})").fetchall()]
+
+    def _redact(table: str, row: Dict[str, Any]) -> Dict[str, Any]:
+        out = {k: ("***" if k in _SECRET_COLS else v) for k, v in row.items()}
+        if table == "kv" and "v" in out:
+            out["v"] = "***"
+        return out
+
+    @app.get("/api/v1/admin/tables")
+    def admin_tables(user=Depends(superuser)):
+        out = []
+        for t in _admin_tables():
+            n = store.execute(f"SELECT COUNT(*) FROM {t}").fetchone()[0]
+            out.append({"table": t, "rows": n, "columns": _admin_table(t)})
+        return {"results": out}
+
+    @app.get("/api/v1/admin/tables/{table}")
+    def admin_rows(table: str, request: Request, user=Depends(superuser)):
+        cols = _admin_table(table)
+        limit = min(int(request.query_params.get("limit", 50) or 50), 1000)
+        offset = int(request.query_params.get("offset", 0) or 0)
+        order = "id DESC" if "id" in cols else "rowid DESC"
+        rows = store.execute(f"SELECT * FROM {table} ORDER BY {order} LIMIT ? OFFSET ?", (limit, offset)).fetchall()
+        total = store.execute(f"SELECT COUNT(*) FROM {table}").fetchone()[0]
+        return {"count": total, "columns": cols, "results": [_redact(table, dict(r)) for r in rows]}
+
+    @app.patch("/api/v1/admin/tables/{table}/{rid}")
+    async def admin_update(table: str, rid: int, request: Request, user=Depends(superuser)):
+        cols = _admin_table(table)
+        body = await request.json()
+        bad = [k for k in body if k not in cols or k in ("id",) or k in _SECRET_COLS]
+        if bad or not body or "id" not in cols:
+            raise HTTPException(400, f"columns not editable: {bad or 'none given'}")
+        sets = ", ".join(f"{k} = ?" for k in body)
+        vals = [json.dumps(v) if isinstance(v, (dict, list)) else v for v in body.values()]
+        cur = store.execute(f"UPDATE {table} SET {sets} WHERE id = ?", (*vals, rid))
+        if cur.rowcount == 0:
+            raise HTTPException(404, f"{table} row {rid} not found")
+        flow.auditor.record("admin.updated", table, rid, user.get("username"))
+        row = store.execute(f"SELECT * FROM {table} WHERE id = ?", (rid,)).fetchone()
+        return _redact(table, dict(row))
+
+    @app.delete("/api/v1/admin/tables/{table}/{rid}", status_code=204)
+    def admin_delete(table: str, rid: int, user=Depends(superuser)):
+        cols = _admin_table(table)
+        if "id" not in cols:
+            raise HTTPException(400, "table has no id column")
+        if table == "users" and store.execute("SELECT username FROM users WHERE id = ?", (rid,)).fetchone() is not None \
+                and store.execute("SELECT username FROM users WHERE id = ?", (rid,)).fetchone()[0] == user.get("username"):
+            raise HTTPException(400, "cannot delete yourself")
+        cur = store.execute(f"DELETE FROM {table} WHERE id = ?", (rid,))
+        if cur.rowcount == 0:
+            raise HTTPException(404, f"{table} row {rid} not found")
+        flow.auditor.record("admin.deleted", table, rid, user.get("username"))
+        return Response(status_code=204)
 
     @app.get("/api/v1/projects")
     def list_projects(request: Request, user=Depends(auth)):

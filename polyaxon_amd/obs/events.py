@@ -65,6 +65,8 @@ SUBJECTS = {
     "chart_view": ["created", "deleted"],
     "bookmark": ["created", "deleted"],
     "webhook_action": ["executed"],
+    "email_action": ["executed"],
+    "admin": ["updated", "deleted"],
 }
 EVENT_TYPES = frozenset(f"{s}.{a}" for s, acts in SUBJECTS.items() for a in acts)
 # events that also create a user-visible notification (reference notifier/service.py event list)
@@ -176,12 +178,92 @@ class WebhookAction:
             return False
 
 
+class EmailAction:
+    """E-mail notification (reference action_manager/actions/email.py): one message per matching event over
+    SMTP (optional STARTTLS + login).  Delivery failures are logged, never raised."""
+
+    kind = "email"
+
+    def __init__(self, host: str, to: List[str], port: int = 25, sender: str = "polyaxon@localhost",
+                 events: Optional[List[str]] = None, use_tls: bool = False, username: Optional[str] = None,
+                 password: Optional[str] = None, timeout: float = 5.0, subject_prefix: str = "[polyaxon]"):
+        if not to:
+            raise ValueError("email action needs at least one recipient")
+        self.host, self.port, self.to, self.sender = host, int(port), list(to), sender
+        self.events = events or ["*.succeeded", "*.failed", "*.stopped"]
+        self.use_tls, self.username, self.password = use_tls, username, password
+        self.timeout, self.subject_prefix = timeout, subject_prefix
+        self.url = f"smtp://{host}:{port}"
+
+    def matches(self, event_type: str) -> bool:
+        return any(fnmatch.fnmatch(event_type, p) for p in self.events)
+
+    def message(self, ev: Event):
+        from email.message import EmailMessage
+
+        msg = EmailMessage()
+        msg["Subject"] = f"{self.subject_prefix} {ev.readable()}"
+        msg["From"] = self.sender
+        msg["To"] = ", ".join(self.to)
+        body = [ev.readable(), "", f"event: {ev.event_type}", f"at: {time.ctime(ev.created_at)}"]
+        body += [f"{k}: {v}" for k, v in ev.context.items()]
+        msg.set_content("\n".join(body))
+        return msg
+
+    def execute(self, ev: Event) -> bool:
+        import smtplib
+
+        try:
+            with smtplib.SMTP(self.host, self.port, timeout=self.timeout) as smtp:
+                if self.use_tls:
+                    smtp.starttls()
+                if self.username:
+                    smtp.login(self.username, self.password or "")
+                smtp.send_message(self.message(ev))
+            return True
+        except Exception as e:
+            log.warning("email to %s via %s failed: %s", self.to, self.url, e)
+            return False
+
+
+def actions_from_config(cfg: Dict[str, Any]) -> List[Any]:
+    """``{"webhooks": [{"url", "kind", "method", "events"}...], "email": {"host", "port", "to", "sender",
+    "events", "use_tls", "username", "password"}}`` -> action objects (reference INTEGRATIONS_* settings)."""
+    out: List[Any] = []
+    for w in cfg.get("webhooks", []) or []:
+        out.append(WebhookAction(w["url"], kind=w.get("kind", "webhook"), method=w.get("method", "POST"),
+                                 events=w.get("events")))
+    em = cfg.get("email")
+    if em:
+        out.append(EmailAction(em["host"], em["to"] if isinstance(em["to"], list) else [em["to"]],
+                               port=em.get("port", 25), sender=em.get("sender", "polyaxon@localhost"),
+                               events=em.get("events"), use_tls=bool(em.get("use_tls")),
+                               username=em.get("username"), password=em.get("password")))
+    return out
+
+
+def load_notification_config(value: Optional[str]) -> Dict[str, Any]:
+    """PLX_NOTIFICATIONS: inline JSON, or a path to a JSON / YAML file."""
+    if not value:
+        return {}
+    value = value.strip()
+    if value.startswith("{"):
+        return json.loads(value)
+    with open(value) as f:
+        text = f.read()
+    if value.endswith((".yml", ".yaml")):
+        import yaml
+
+        return yaml.safe_load(text) or {}
+    return json.loads(text)
+
+
 class Auditor:
     def __init__(self, store=None, stats: Optional[Stats] = None, strict: bool = True):
         self.store = store
         self.stats = stats or Stats()
         self.strict = strict
-        self.actions: List[WebhookAction] = []
+        self.actions: List[Any] = []
         self._subs: List[Tuple[str, Callable[[Event], None]]] = []
         self._q: "queue.Queue[Tuple[WebhookAction, Event]]" = queue.Queue()
         self._worker: Optional[threading.Thread] = None
@@ -190,8 +272,12 @@ class Auditor:
     def subscribe(self, pattern: str, fn: Callable[[Event], None]) -> None:
         self._subs.append((pattern, fn))
 
-    def add_action(self, action: WebhookAction) -> None:
+    def add_action(self, action) -> None:
         self.actions.append(action)
+
+    def configure(self, cfg: Dict[str, Any]) -> None:
+        for a in actions_from_config(cfg):
+            self.add_action(a)
 
     def record(self, event_type: str, object_kind: Optional[str] = None, object_id: Optional[int] = None,
                actor: Optional[str] = None, **context) -> Event:
@@ -225,7 +311,7 @@ class Auditor:
             a, ev = self._q.get()
             ok = a.execute(ev)
             self.delivered.append((a.url, ok))
-            self.stats.incr("webhook_action.executed")
+            self.stats.incr("email_action.executed" if getattr(a, "kind", "") == "email" else "webhook_action.executed")
             self._q.task_done()
 
     def flush(self, timeout: float = 10.0) -> None:

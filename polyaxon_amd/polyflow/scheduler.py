@@ -124,6 +124,10 @@ class Polyflow:
             self.store_path = store.path
         self.alloc = allocator or DeviceAllocator()
         self.auditor = auditor or Auditor(self.store)
+        if auditor is None and os.environ.get("PLX_NOTIFICATIONS"):
+            from polyaxon_amd.obs.events import load_notification_config
+
+            self.auditor.configure(load_notification_config(os.environ["PLX_NOTIFICATIONS"]))
         self.api_host = api_host
         self.stop_grace_s = stop_grace_s
         self.python = python or sys.executable

@@ -346,9 +346,33 @@ class HipGP:
         return math.exp(x_best) if math.isfinite(f_best) else float(length_scale)
 
     def fit(self, gp: GPState):
-        """Device factors for a fitted GP (length scale from the LML search)."""
+        """Device factors for a fitted GP (length scale from the LML search): (X, L, alpha, L^-1 or None).
+
+        n <= DEVICE_FACTOR_MAX: our LDS Cholesky + device triangular solves.  Larger n: the Gram comes from our
+        kernel, the fp64 factorisation, alpha and the explicit L^-1 from LAPACK; the posterior variance then
+        needs only a GEMM (v = L^-1 k*^T) on the device instead of a triangular solve."""
         t = self.torch
+        n = len(gp.X)
         K = self.kmat(gp.X, gp.X, gp.kind, gp.ls, gp.nu, diag=1e-10)
+        Xd = t.as_tensor(gp.X, dtype=t.float32, device=self.device).contiguous()
+        if n > self.DEVICE_FACTOR_MAX:
+            from scipy.linalg import cho_solve, solve_triangular
+
+            Kh = K.double().cpu().numpy()
+            jitter = 0.0
+            for _ in range(8):
+                try:
+                    Lh = np.linalg.cholesky(Kh + jitter * np.eye(n) if jitter else Kh)
+                    break
+                except np.linalg.LinAlgError:
+                    jitter = max(jitter * 10, 1e-8)
+            else:
+                raise np.linalg.LinAlgError("GP Gram matrix not positive definite")
+            ah = cho_solve((Lh, True), np.asarray(gp.y, dtype=np.float64))
+            Linv = solve_triangular(Lh, np.eye(n), lower=True)
+            f32 = dict(dtype=t.float32, device=self.device)
+            return Xd, t.as_tensor(Lh, **f32).contiguous(), t.as_tensor(ah, **f32).contiguous(), \
+                t.as_tensor(Linv, **f32).contiguous()
         jitter = 0.0
         for _ in range(6):
             try:
@@ -358,13 +382,12 @@ class HipGP:
                 jitter = max(jitter * 10, 1e-8)
         y = t.as_tensor(gp.y, dtype=t.float32, device=self.device)
         alpha = t.cholesky_solve(y[:, None], L)[:, 0]
-        Xd = t.as_tensor(gp.X, dtype=t.float32, device=self.device).contiguous()
-        return Xd, L.contiguous(), alpha.contiguous()
+        return Xd, L.contiguous(), alpha.contiguous(), None
 
     def predict_acq(self, gp: GPState, dev_state, Xc, acq: str, y_max: float, kappa: float, eps: float,
                     want_mean_std: bool = False):
         t = self.torch
-        Xd, L, alpha = dev_state
+        Xd, L, alpha, Linv = dev_state
         Xc = t.as_tensor(Xc, dtype=t.float32, device=self.device).contiguous()
         m, n, d = Xc.shape[0], Xd.shape[0], Xd.shape[1]
         acq_id = {"ucb": 0, "ei": 1, "poi": 2}[acq]
@@ -385,7 +408,7 @@ class HipGP:
         else:  # large n: MFMA cross-kernel + TRSM, acquisition in torch
             Ks = self.kmat(Xc, Xd, gp.kind, gp.ls, gp.nu)
             mu = Ks @ alpha
-            v = t.linalg.solve_triangular(L, Ks.T, upper=False)
+            v = Linv @ Ks.T if Linv is not None else t.linalg.solve_triangular(L, Ks.T, upper=False)
             sd = (1.0 - (v * v).sum(0)).clamp_min(0).sqrt()
             out = self._acq_torch(mu, sd, acq, y_max, kappa, eps)
             best = int(t.argmax(out).item())
@@ -501,7 +524,33 @@ class UtilityFunction:
                 x_max, max_acq = pert[order[0]], yp[order[0]]
             top = np.concatenate([top, pert[order[:64]]])[: 128]
             scale *= 0.7
+        # batched multi-start projected gradient ascent (the reference's L-BFGS-B restarts, all seeds at once):
+        # central differences for every seed and coordinate are ONE acquisition launch per step
+        seeds = np.concatenate([x_max[None], top[:15]])
+        xs, fx = self._ascend(seeds, y_max, lo, hi, width)
+        i = int(np.argmax(fx))
+        if fx[i] >= max_acq:
+            x_max = xs[i]
         return np.clip(x_max, lo, hi)
+
+    def _ascend(self, xs: np.ndarray, y_max: float, lo, hi, width, steps: int = 25):
+        k, d = xs.shape
+        h = 1e-4 * width
+        step = 0.05 * width
+        fx = self.compute(xs, y_max)
+        eye = np.eye(d)
+        for _ in range(steps):
+            probe = np.concatenate([(xs[:, None, :] + eye[None] * h), (xs[:, None, :] - eye[None] * h)], axis=1)
+            fp = self.compute(np.clip(probe.reshape(-1, d), lo, hi), y_max).reshape(k, 2 * d)
+            grad = (fp[:, :d] - fp[:, d:]) / (2 * h)
+            gn = np.linalg.norm(grad / width, axis=1, keepdims=True)
+            cand = np.clip(xs + step * grad / width / np.maximum(gn, 1e-30) * width, lo, hi)
+            fc = self.compute(cand, y_max)
+            better = fc > fx
+            xs = np.where(better[:, None], cand, xs)
+            fx = np.where(better, fc, fx)
+            step = np.where(better[:, None], step * 1.2, step * 0.5)
+        return xs, fx
 
 
 class BOOptimizer:

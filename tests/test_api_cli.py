@@ -215,3 +215,24 @@ def test_users_and_project_permissions(api):
     assert r.status_code == 201
     assert flow.wait("experiment", r.json()["id"], timeout=30) == "succeeded"
     assert [u["username"] for u in client.get("/api/v1/users/list").json()["results"]] == ["root", "alice"]
+
+
+def test_admin_table_browser(api):
+    """Superuser admin (reference db/admin/*.py): tables with counts, paged rows with secrets redacted,
+    edit and delete a row; non-superusers are refused."""
+    client = api[0] if isinstance(api, tuple) else api
+    r = client.post("/api/v1/projects", json={"name": "adm"})
+    assert r.status_code == 201
+    tables = {t["table"]: t for t in client.get("/api/v1/admin/tables").json()["results"]}
+    assert {"projects", "experiments", "users", "kv"} <= set(tables)
+    rows = client.get("/api/v1/admin/tables/users").json()
+    assert rows["count"] >= 1 and all(u.get("token") in (None, "***") for u in rows["results"])
+    proj = [p for p in client.get("/api/v1/admin/tables/projects").json()["results"] if p["name"] == "adm"][0]
+    r = client.patch(f"/api/v1/admin/tables/projects/{proj['id']}", json={"description": "edited by admin"})
+    assert r.status_code == 200 and r.json()["description"] == "edited by admin"
+    assert client.patch(f"/api/v1/admin/tables/projects/{proj['id']}", json={"nope": 1}).status_code == 400
+    assert client.get("/api/v1/admin/tables/not_a_table").status_code == 404
+    assert client.delete(f"/api/v1/admin/tables/projects/{proj['id']}").status_code == 204
+    assert client.delete(f"/api/v1/admin/tables/projects/{proj['id']}").status_code == 404
+    tok = client.post("/api/v1/users", json={"username": "bob"}).json()["token"]
+    assert client.get("/api/v1/admin/tables", headers={"Authorization": f"token {tok}"}).status_code == 403

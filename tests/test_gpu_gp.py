@@ -35,7 +35,7 @@ def test_cholesky_matches_numpy(cuda):
         HipGP(cuda).cholesky(torch.tensor([[1.0, 2.0], [2.0, 1.0]], device=cuda))
 
 
-@pytest.mark.parametrize("n", [3, 20, 40, 64, 90])
+@pytest.mark.parametrize("n", [3, 20, 40, 64, 90, 200])
 @pytest.mark.parametrize("acq", ["ucb", "ei", "poi"])
 def test_predict_acq_matches_numpy(cuda, n, acq):
     from polyaxon_amd.polytune.bo import HipGP, acquisition_np, fit_gp, predict_np
