@@ -20,9 +20,12 @@ import time
 from typing import Any, Dict, List, Optional
 
 from fastapi import Depends, FastAPI, Header, HTTPException, Query, Request
-from fastapi.responses import FileResponse, JSONResponse, PlainTextResponse, Response, StreamingResponse
+from fastapi.responses import (FileResponse, JSONResponse, PlainTextResponse, RedirectResponse, Response,
+                               StreamingResponse)
 
 from polyaxon_amd import __version__
+from polyaxon_amd.auth import Accounts, AuthError, validate_name
+from polyaxon_amd.conf import Settings
 from polyaxon_amd.spec import PolyaxonfileError, specification_for
 from polyaxon_amd.store import QueryError
 
@@ -30,8 +33,10 @@ INTERNAL_HEADER = "x-polyaxon-internal"
 
 
 def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional[str] = None,
-               require_auth: bool = True) -> FastAPI:
+               require_auth: bool = True, settings: Optional[Settings] = None, sso_transport=None) -> FastAPI:
     store = flow.store
+    settings = settings or Settings.load(env={})
+    accounts = Accounts(store, settings, transport=sso_transport)
     app = FastAPI(title="polyaxon-mi355x", version=__version__)
     if admin_token and not store.user_for_token(admin_token):
         if store.get_user("root"):
@@ -52,6 +57,8 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
             tok = authorization.split(" ", 1)[1].strip()
             user = store.user_for_token(tok)
             if user:
+                if not accounts.token_valid(user):
+                    raise HTTPException(401, "Token expired or account inactive.")
                 return user
             eph = store.kv_get(f"ephemeral:{tok}")
             if eph:
@@ -161,9 +168,93 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
         body = await request.json()
         if not body.get("username") or store.get_user(body["username"]):
             raise HTTPException(400, "missing or existing username")
+        try:
+            validate_name(body["username"], settings.get("blacklist.extra"))
+        except ValueError as e:
+            raise HTTPException(400, str(e))
         u = store.create_user(body["username"], body.get("email", ""), bool(body.get("is_superuser")))
+        if body.get("password"):
+            _auth_call(accounts.set_password, u["username"], body["password"])
         flow.auditor.record("user.registered", "user", u["id"], user.get("username"))
         return u
+
+    def _auth_call(fn, *args):
+        try:
+            return fn(*args)
+        except AuthError as e:
+            raise HTTPException(e.status, str(e))
+
+    @app.post("/api/v1/users/token")
+    async def login(request: Request):
+        """Exchange username + password (local or LDAP) for an API token (reference users/token + login)."""
+        body = await request.json()
+        u = _auth_call(accounts.login, body.get("username", ""), body.get("password", ""))
+        flow.auditor.record("user.logged_in", "user", u["id"], u["username"])
+        return {"token": u["token"], "username": u["username"]}
+
+    @app.post("/api/v1/users/logout")
+    def logout(user=Depends(auth)):
+        if user.get("scope") is None and user.get("username") != "internal":
+            accounts.logout(user["username"])
+            flow.auditor.record("user.logged_out", "user", user.get("id"), user["username"])
+        return {"ok": True}
+
+    @app.post("/api/v1/users/password")
+    async def change_password(request: Request, user=Depends(auth)):
+        body = await request.json()
+        _auth_call(accounts.change_password, user["username"], body.get("old_password"), body.get("new_password"))
+        flow.auditor.record("user.password_changed", "user", user.get("id"), user["username"])
+        return {"ok": True}
+
+    @app.post("/api/v1/users/register", status_code=201)
+    async def register(request: Request):
+        """Self-registration (reference SimpleRegistrationView): ``auth.registration`` = ``open`` returns a
+        token at once; ``superuser_validation`` parks the account until ``/users/<name>/activate``."""
+        body = await request.json()
+        out = _auth_call(accounts.register, body.get("username", ""), body.get("email", ""),
+                         body.get("password", ""))
+        flow.auditor.record("user.registered", "user", None, body.get("username"))
+        return out
+
+    @app.get("/api/v1/users/pending")
+    def pending_users(user=Depends(superuser)):
+        return {"results": accounts.pending()}
+
+    @app.post("/api/v1/users/{username}/activate")
+    def activate_user(username: str, user=Depends(superuser)):
+        _auth_call(accounts.activate, username)
+        flow.auditor.record("user.activated", "user", None, user.get("username"))
+        return {"ok": True}
+
+    @app.post("/api/v1/users/{username}/deactivate")
+    def deactivate_user(username: str, user=Depends(superuser)):
+        _auth_call(accounts.deactivate, username)
+        flow.auditor.record("user.deactivated", "user", None, user.get("username"))
+        return {"ok": True}
+
+    @app.post("/api/v1/users/{username}/password")
+    async def set_password(username: str, request: Request, user=Depends(superuser)):
+        body = await request.json()
+        _auth_call(accounts.set_password, username, body.get("password", ""))
+        return {"ok": True}
+
+    @app.get("/api/v1/sso/providers")
+    def sso_providers():
+        return {"providers": accounts.sso_providers(), "ldap": bool(settings.get("auth.ldap.enabled"))}
+
+    def _redirect_uri(request: Request, provider: str) -> str:
+        return str(request.url_for("sso_complete", provider=provider))
+
+    @app.get("/oauth/{provider}/login")
+    def sso_login(provider: str, request: Request):
+        url = _auth_call(accounts.sso_login_url, provider, _redirect_uri(request, provider))
+        return RedirectResponse(url, status_code=302)
+
+    @app.get("/oauth/{provider}/complete", name="sso_complete")
+    def sso_complete(provider: str, request: Request, code: str = "", state: str = ""):
+        out = _auth_call(accounts.sso_complete, provider, code, state, _redirect_uri(request, provider))
+        flow.auditor.record("user.sso_logged_in", "user", None, out["username"])
+        return out
 
     @app.get("/api/v1/users/list")
     def list_users(user=Depends(superuser)):
@@ -248,6 +339,7 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
     async def create_project(request: Request, user=Depends(auth)):
         body = await request.json()
         try:
+            validate_name(body.get("name", ""), settings.get("blacklist.extra"))
             p = store.create_project(body["name"], user.get("username", "root"), body.get("description", ""),
                                      body.get("is_public", True), body.get("tags"))
         except Exception as e:

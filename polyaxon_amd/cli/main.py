@@ -300,23 +300,33 @@ def upload(c):
 @click.option("--port", default=8000, type=int)
 @click.option("--token", default=None, help="admin token (default: generated and printed)")
 @click.option("--gpus", type=int, default=None)
+@click.option("--set", "sets", multiple=True, help="settings override key=value (see `plx settings`)")
 @click.pass_obj
-def server(c, host, port, token, gpus):
+def server(c, host, port, token, gpus, sets):
     """Run the scheduler + REST API (reference api/ + scheduler services in one process)."""
     import uuid
 
     import uvicorn
 
     from polyaxon_amd.api.server import create_app
+    from polyaxon_amd.conf import ConfigError, Settings, set_settings
     from polyaxon_amd.polyflow.devices import Device, DeviceAllocator
     from polyaxon_amd.polyflow.scheduler import Polyflow
 
-    token = token or c.cfg.get("token") or uuid.uuid4().hex
+    try:
+        st = Settings.load(overrides=dict(kv.split("=", 1) for kv in sets))
+    except ConfigError as e:
+        raise click.ClickException(str(e))
+    set_settings(st)
+    gpus = gpus if gpus is not None else st.get("scheduler.gpus")
+    token = token or st.get("api.admin_token") or c.cfg.get("token") or uuid.uuid4().hex
     alloc = DeviceAllocator([Device(i) for i in range(gpus)]) if gpus is not None else None
     flow = Polyflow(os.path.expanduser(c.cfg["root"]), allocator=alloc, api_host=f"http://{host}:{port}").start()
     click.echo(f"plx server on http://{host}:{port}  token={token}")
     try:
-        uvicorn.run(create_app(flow, admin_token=token), host=host, port=port, log_level="warning")
+        uvicorn.run(create_app(flow, admin_token=token, settings=st, internal_token=st.get("secret.internal_token"),
+                               require_auth=st.get("api.require_auth")),
+                    host=host, port=port, log_level="warning")
     finally:
         flow.shutdown()
 
@@ -653,6 +663,125 @@ def user_create(c, username, email, superuser):
             raise click.ClickException(f"user {username} exists")
         u = c.store.create_user(username, email, superuser)
     click.echo(f"created user {u['username']} token={u['token']}")
+
+
+@user.command("password")
+@click.argument("username")
+@click.option("--password", prompt=True, hide_input=True, confirmation_prompt=True)
+@click.pass_obj
+def user_password(c, username, password):
+    """Set a user's password (superuser; server mode)."""
+    _need_host(c, "user password")
+    c.api("POST", f"/api/v1/users/{username}/password", {"password": password})
+    click.echo("password set")
+
+
+@user.command("activate")
+@click.argument("username")
+@click.pass_obj
+def user_activate(c, username):
+    """Validate a pending registration (reference superuser-validation workflow)."""
+    _need_host(c, "user activate")
+    c.api("POST", f"/api/v1/users/{username}/activate", {})
+    click.echo(f"activated {username}")
+
+
+@user.command("pending")
+@click.pass_obj
+def user_pending(c):
+    _need_host(c, "user pending")
+    out(c.api("GET", "/api/v1/users/pending")["results"], c.fmt)
+
+
+def _need_host(c, what: str) -> None:
+    if not c.host:
+        raise click.ClickException(f"`{what}` needs a running `plx server` (set PLX_HOST)")
+
+
+@cli.command()
+@click.option("--username", "-u", prompt=True)
+@click.option("--password", "-p", prompt=True, hide_input=True)
+@click.pass_obj
+def login(c, username, password):
+    """Log in (local password or LDAP) and store the API token in the CLI config."""
+    _need_host(c, "login")
+    res = c.api("POST", "/api/v1/users/token", {"username": username, "password": password})
+    cfg = load_config()
+    cfg.update({"token": res["token"], "user": res["username"], "host": c.host})
+    save_config(cfg)
+    click.echo(f"logged in as {res['username']}")
+
+
+@cli.command()
+@click.pass_obj
+def logout(c):
+    """Invalidate the stored token."""
+    if c.host and c.cfg.get("token"):
+        c.api("POST", "/api/v1/users/logout", {})
+    cfg = load_config()
+    cfg.pop("token", None)
+    save_config(cfg)
+    click.echo("logged out")
+
+
+@cli.command()
+@click.option("--username", "-u", prompt=True)
+@click.option("--email", "-e", default="")
+@click.option("--password", "-p", prompt=True, hide_input=True, confirmation_prompt=True)
+@click.pass_obj
+def register(c, username, email, password):
+    """Self-register (when the server allows it)."""
+    _need_host(c, "register")
+    res = c.api("POST", "/api/v1/users/register", {"username": username, "email": email, "password": password})
+    click.echo("registered; " + ("token=" + res["token"] if res.get("token") else "awaiting activation"))
+
+
+@cli.command("settings")
+@click.option("--set", "sets", multiple=True, help="key=value override to validate")
+@click.pass_obj
+def settings_show(c, sets):
+    """Show the resolved platform settings with each value's origin (secrets redacted)."""
+    from polyaxon_amd.conf import ConfigError, Settings
+
+    try:
+        st = Settings.load(overrides=dict(kv.split("=", 1) for kv in sets))
+    except ConfigError as e:
+        raise click.ClickException(str(e))
+    rows = st.describe()
+    if c.fmt == "json":
+        out(rows, "json")
+    else:
+        out(rows, "table", ["key", "value", "origin", "env"])
+
+
+@cli.group()
+def admin():
+    """Management commands (reference commands/management/commands/*.py)."""
+
+
+@admin.command("clean")
+@click.argument("what", type=click.Choice(["stale", "experiments", "groups", "jobs", "outputs"]))
+@click.option("--older-than", default="7d", help="outputs: age cutoff, e.g. 3600s, 12h, 7d")
+@click.option("--dry-run", is_flag=True)
+@click.option("--force", is_flag=True, help="clean even though a scheduler looks alive")
+@click.pass_obj
+def admin_clean(c, what, older_than, dry_run, force):
+    """Stop runs the store still calls running (after a crash), or delete old outputs."""
+    from polyaxon_amd.polyflow.cleaning import clean_outputs, clean_stale, scheduler_alive
+
+    if c.host:
+        raise click.ClickException("`admin clean` runs against the node's store: unset PLX_HOST")
+    if what != "outputs" and not force and scheduler_alive(os.path.expanduser(c.cfg["root"])):
+        raise click.ClickException("a scheduler is running on this root; its runs are live (use --force)")
+    if what == "outputs":
+        mult = {"s": 1, "m": 60, "h": 3600, "d": 86400}
+        unit = older_than[-1] if older_than[-1] in mult else "s"
+        secs = float(older_than.rstrip("smhd")) * mult[unit]
+        paths = clean_outputs(c.store, secs, dry_run=dry_run)
+        out({"deleted": paths, "dry_run": dry_run}, "json")
+        return
+    kinds = ("experiments", "groups", "jobs") if what == "stale" else (what,)
+    out(clean_stale(c.store, kinds=kinds), "json")
 
 
 @cli.group()

@@ -56,7 +56,8 @@ SUBJECTS = {
     "repo": ["created", "new_commit", "downloaded"],
     "cluster": ["created", "updated", "resources_updated", "node_created", "node_updated", "node_deleted",
                 "node_gpu", "node_gpu_unhealthy"],
-    "user": ["registered", "updated", "activated", "deleted", "viewed", "password_changed"],
+    "user": ["registered", "updated", "activated", "deactivated", "deleted", "viewed", "password_changed",
+             "logged_in", "logged_out", "sso_logged_in"],
     "superuser": ["role_granted", "role_revoked"],
     "permission": ["project_denied", "repo_denied", "experiment_group_denied", "experiment_denied",
                    "tensorboard_denied", "notebook_denied", "build_job_denied", "experiment_job_denied",

@@ -116,8 +116,9 @@ class Polyflow:
     def __init__(self, root: str, store: Optional[Store] = None, allocator: Optional[DeviceAllocator] = None,
                  auditor: Optional[Auditor] = None, api_host: Optional[str] = None, stop_grace_s: float = 10.0,
                  python: Optional[str] = None, reconcile_s: float = 5.0,
-                 health_check: Optional[Callable[[], List[int]]] = None):
+                 health_check: Optional[Callable[[], List[int]]] = None, clean_on_start: bool = True):
         self.paths = Paths(root)
+        self.clean_on_start = clean_on_start
         self.store_path = os.path.join(self.paths.root, "polyaxon.sqlite")
         self.store = store or Store(self.store_path)
         if store is not None and store.path != ":memory:":
@@ -152,6 +153,14 @@ class Polyflow:
     # ================================================================== lifecycle of the scheduler itself
     def start(self) -> "Polyflow":
         if self._thread is None:
+            if self.clean_on_start:  # runs a previous scheduler process left non-terminal
+                from polyaxon_amd.polyflow.cleaning import clean_stale
+
+                cleaned = clean_stale(self.store)
+                if any(cleaned.values()):
+                    log.warning("cleaning hook stopped orphaned runs: %s", cleaned)
+            with open(os.path.join(self.paths.root, "scheduler.pid"), "w") as f:
+                f.write(str(os.getpid()))
             self._running = True
             self._thread = threading.Thread(target=self._loop, name="polyflow", daemon=True)
             self._thread.start()
@@ -172,6 +181,10 @@ class Polyflow:
         self.pm.wake()
         self._thread.join(timeout=timeout)
         self._thread = None
+        try:
+            os.unlink(os.path.join(self.paths.root, "scheduler.pid"))
+        except OSError:
+            pass
 
     def __enter__(self):
         return self.start()
