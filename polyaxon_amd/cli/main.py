@@ -755,6 +755,61 @@ def settings_show(c, sets):
 
 
 @cli.group()
+def deploy():
+    """Node deployment wizard (reference deploy/ web wizard -> Helm values)."""
+
+
+def _deploy_cfg(root, host, port, gpus, registration, service_user):
+    from polyaxon_amd.deploy import DeployConfig
+
+    return DeployConfig(root=root, host=host, port=port, gpus=gpus, registration=registration,
+                        service_user=service_user)
+
+
+_deploy_opts = [
+    click.option("--root", default="/var/lib/polyaxon-mi355x"),
+    click.option("--host", default="0.0.0.0"),
+    click.option("--port", default=8000, type=int),
+    click.option("--gpus", default=None, type=int),
+    click.option("--registration", default="disabled",
+                 type=click.Choice(["disabled", "superuser_validation", "open"])),
+    click.option("--service-user", default="polyaxon"),
+]
+
+
+def _with_deploy_opts(f):
+    for o in reversed(_deploy_opts):
+        f = o(f)
+    return f
+
+
+@deploy.command("check")
+@_with_deploy_opts
+@click.pass_obj
+def deploy_check(c, root, host, port, gpus, registration, service_user):
+    """Preflight: /dev/kfd, gfx950 agents, RCCL, port, disk, writable root."""
+    from dataclasses import asdict
+
+    from polyaxon_amd.deploy import preflight
+
+    checks = preflight(_deploy_cfg(root, host, port, gpus, registration, service_user))
+    out([asdict(ch) for ch in checks], c.fmt, ["name", "ok", "required", "detail"])
+    if any(not ch.ok and ch.required for ch in checks):
+        raise click.ClickException("preflight failed")
+
+
+@deploy.command("generate")
+@_with_deploy_opts
+@click.option("--out", "out_dir", default="./plx-deploy")
+@click.pass_obj
+def deploy_generate(c, root, host, port, gpus, registration, service_user, out_dir):
+    """Write settings.yaml, a systemd unit and the client env for this node."""
+    from polyaxon_amd.deploy import generate
+
+    out(generate(_deploy_cfg(root, host, port, gpus, registration, service_user), out_dir), "json")
+
+
+@cli.group()
 def admin():
     """Management commands (reference commands/management/commands/*.py)."""
 

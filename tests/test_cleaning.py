@@ -91,3 +91,27 @@ def test_clean_outputs(tmp_path):
     assert clean_outputs(store, 86400) == [str(old_dir)]
     assert not old_dir.exists() and new_dir.exists()
     assert store.get_experiment(ids[0])["outputs_path"] is None
+
+
+def test_deploy_generate_and_check(tmp_path, monkeypatch, capsys):
+    import json as _json
+
+    from polyaxon_amd.cli.main import main
+    from polyaxon_amd.conf import Settings
+    from polyaxon_amd.deploy import DeployConfig, preflight
+
+    monkeypatch.setenv("PLX_CONFIG", str(tmp_path / "c.yaml"))
+    out_dir = tmp_path / "dep"
+    assert main(["deploy", "generate", "--root", str(tmp_path / "root"), "--port", "8123", "--gpus", "8",
+                 "--out", str(out_dir)]) == 0
+    res = _json.loads(capsys.readouterr().out)
+    assert res["files"] == ["deploy.json", "plx.env", "polyaxon-mi355x.service", "settings.yaml"]
+    st = Settings.load(env={}, files=[str(out_dir / "settings.yaml")])
+    assert st["api.port"] == 8123 and st["scheduler.gpus"] == 8 and st["root"] == str(tmp_path / "root")
+    tok = st["api.admin_token"]
+    assert f"PLX_TOKEN={tok}" in (out_dir / "plx.env").read_text()
+    assert oct((out_dir / "plx.env").stat().st_mode & 0o777) == "0o600"
+    unit = (out_dir / "polyaxon-mi355x.service").read_text()
+    assert "HSA_ENABLE_IPC_MODE_LEGACY=0" in unit and "--port 8123" in unit
+    names = {c.name for c in preflight(DeployConfig(root=str(tmp_path), port=0, host="127.0.0.1"))}
+    assert {"dev_kfd", "gfx950_agents", "rccl", "port", "disk", "root_writable"} <= names
