@@ -574,6 +574,10 @@ inline void tn_tile(int N1, int N2, int& bn1, int& bn2) {
     bn2 = N2 % 128 == 0 ? 128 : 64;
 }
 
+// slicing knobs (plx_set_tn_plan): target resident blocks per CU, cap on the fp32 slab bytes
+int g_tn_blocks_per_cu = 3;   // swept 1..12 x 8..256 MB on MI355X (scripts/diag_wgrad_plan.py): 3 / 32 MB best
+long g_tn_slab_bytes = 32l << 20;
+
 inline TnPlan tn_plan(int M, int N1, int N2, int num_cus) {
     int bn1, bn2;
     tn_tile(N1, N2, bn1, bn2);
@@ -581,9 +585,9 @@ inline TnPlan tn_plan(int M, int N1, int N2, int num_cus) {
     const long plane = (long)N1 * N2;
     // ~4 blocks per CU (one 4-wave block per CU leaves each SIMD a single wave: latency-bound), >= 4
     // k-stages per block, slabs <= 32 MB (they are re-read by the reducer, mostly from the infinity cache)
-    int slices = (4 * (num_cus > 0 ? num_cus : 256)) / ntiles;
+    int slices = (g_tn_blocks_per_cu * (num_cus > 0 ? num_cus : 256)) / ntiles;
     const int by_depth = M / (4 * BK);
-    const int by_bytes = (int)((32l << 20) / (plane * 4));
+    const int by_bytes = (int)(g_tn_slab_bytes / (plane * 4));
     if (slices > by_depth) slices = by_depth;
     if (slices > by_bytes) slices = by_bytes;
     if (slices < 1) slices = 1;
@@ -634,6 +638,12 @@ int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int 
     if (N % 128 == 0)
         return launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b);
     return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b);
+}
+
+// weight-gradient slicing knobs; workspace sizes follow them, so set before sizing / launching
+void plx_set_tn_plan(int blocks_per_cu, int slab_mb) {
+    if (blocks_per_cu > 0) g_tn_blocks_per_cu = blocks_per_cu;
+    if (slab_mb > 0) g_tn_slab_bytes = (long)slab_mb << 20;
 }
 
 // floats of slab workspace plx_gemm_tn needs for this problem

@@ -1,0 +1,211 @@
+// Fused elementwise/layout kernels of the decoder-only language models (Llama-3 8B, GPT-2) on MI355X.
+//
+//   plx_qkv_rope_fwd   qkv[T][(H+2KV)*D] (the fused QKV GEMM's output, T = B*S rows)
+//                        -> q[B][H][S][D], k[B][KV][S][D] rotated by RoPE, v[B][KV][S][D]
+//                      one pass instead of split / view / transpose / 2x(cat, 4 mul, add, sub) / contiguous:
+//                      the rotation is fused into the head-major relayout attention wants.
+//   plx_qkv_rope_bwd   dq, dk, dv -> dqkv[T][(H+2KV)*D] (inverse rotation + the transpose back)
+//   plx_swiglu_fwd     h[T][2F] (gate | up halves of the fused gate/up GEMM) -> a[T][F] = silu(g) * u
+//   plx_swiglu_bwd     da, h -> dh[T][2F]: dg = da*u*silu'(g), du = da*silu(g)
+//
+// Llama RoPE convention (rotate the two halves of each head): for j < D/2
+//   y[j] = x[j] c_j - x[j+D/2] s_j,  y[j+D/2] = x[j] s_j + x[j+D/2] c_j,  c_j = cos(pos * theta^(-2j/D)).
+// cos / sin come from an fp32 [S][D/2] table.  `rot_heads` = number of leading heads that rotate (H + KV for
+// RoPE models, 0 for GPT-2's learned positions: the kernel is then the pure relayout).
+//
+// Memory-bound: every lane moves 16-byte vectors (8 bf16) and computes in fp32; a lane owns one 8-wide chunk of
+// the first half of a head row and the matching chunk of the second half, so the pair it rotates is in
+// registers.  Grid-strided, 256-thread blocks, capped at 8192 blocks (>> 256 CUs x 8 waves).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PLX_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct alignas(16) bf16x8 {
+  uint16_t v[8];
+};
+
+__device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+inline int grid_for(int64_t items) {
+  int64_t g = (items + kBlock - 1) / kBlock;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+// work item i -> (row t, head h, chunk c of the first half); head-major destination row (b, h, s)
+__global__ __launch_bounds__(kBlock) void qkv_rope_fwd_kernel(const bf16x8* __restrict__ qkv,
+                                                              const float* __restrict__ cosv,
+                                                              const float* __restrict__ sinv,
+                                                              bf16x8* __restrict__ q, bf16x8* __restrict__ k,
+                                                              bf16x8* __restrict__ v, int64_t T, int S, int H,
+                                                              int KV, int D, int rot_heads) {
+  const int NH = H + 2 * KV, half8 = D / 16, row8 = D / 8;
+  const int64_t items = T * NH * half8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < items; i += stride) {
+    const int c = (int)(i % half8);
+    const int64_t th = i / half8;
+    const int h = (int)(th % NH);
+    const int64_t t = th / NH;
+    const int s = (int)(t % S);
+    const int64_t b = t / S;
+    const bf16x8* src = qkv + (t * NH + h) * row8;
+    bf16x8 x1 = src[c], x2 = src[c + half8];
+    if (h < rot_heads) {
+      const float* cs = cosv + (int64_t)s * (D / 2) + c * 8;
+      const float* sn = sinv + (int64_t)s * (D / 2) + c * 8;
+      bf16x8 y1, y2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float a = bf2f(x1.v[e]), bb = bf2f(x2.v[e]), co = cs[e], si = sn[e];
+        y1.v[e] = f2bf(a * co - bb * si);
+        y2.v[e] = f2bf(a * si + bb * co);
+      }
+      x1 = y1;
+      x2 = y2;
+    }
+    bf16x8* dst;
+    if (h < H) {
+      dst = q + ((b * H + h) * S + s) * row8;
+    } else if (h < H + KV) {
+      dst = k + ((b * KV + (h - H)) * S + s) * row8;
+    } else {
+      dst = v + ((b * KV + (h - H - KV)) * S + s) * row8;
+    }
+    dst[c] = x1;
+    dst[c + half8] = x2;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void qkv_rope_bwd_kernel(const bf16x8* __restrict__ dq,
+                                                              const bf16x8* __restrict__ dk,
+                                                              const bf16x8* __restrict__ dv,
+                                                              const float* __restrict__ cosv,
+                                                              const float* __restrict__ sinv,
+                                                              bf16x8* __restrict__ dqkv, int64_t T, int S, int H,
+                                                              int KV, int D, int rot_heads) {
+  const int NH = H + 2 * KV, half8 = D / 16, row8 = D / 8;
+  const int64_t items = T * NH * half8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < items; i += stride) {
+    const int c = (int)(i % half8);
+    const int64_t th = i / half8;
+    const int h = (int)(th % NH);
+    const int64_t t = th / NH;
+    const int s = (int)(t % S);
+    const int64_t b = t / S;
+    const bf16x8* src;
+    if (h < H) {
+      src = dq + ((b * H + h) * S + s) * row8;
+    } else if (h < H + KV) {
+      src = dk + ((b * KV + (h - H)) * S + s) * row8;
+    } else {
+      src = dv + ((b * KV + (h - H - KV)) * S + s) * row8;
+    }
+    bf16x8 g1 = src[c], g2 = src[c + half8];
+    if (h < rot_heads) {  // transpose of the rotation: [c s; -s c]
+      const float* cs = cosv + (int64_t)s * (D / 2) + c * 8;
+      const float* sn = sinv + (int64_t)s * (D / 2) + c * 8;
+      bf16x8 y1, y2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float a = bf2f(g1.v[e]), bb = bf2f(g2.v[e]), co = cs[e], si = sn[e];
+        y1.v[e] = f2bf(a * co + bb * si);
+        y2.v[e] = f2bf(bb * co - a * si);
+      }
+      g1 = y1;
+      g2 = y2;
+    }
+    bf16x8* dst = dqkv + (t * NH + h) * row8;
+    dst[c] = g1;
+    dst[c + half8] = g2;
+  }
+}
+
+__device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + __expf(-x)); }
+
+__global__ __launch_bounds__(kBlock) void swiglu_fwd_kernel(const bf16x8* __restrict__ h, bf16x8* __restrict__ a,
+                                                            int64_t T, int F8) {
+  const int64_t items = T * F8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < items; i += stride) {
+    const int64_t t = i / F8;
+    const int c = (int)(i - t * F8);
+    const bf16x8 g = h[t * 2 * F8 + c], u = h[t * 2 * F8 + F8 + c];
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gf = bf2f(g.v[e]);
+      o.v[e] = f2bf(gf * sigmoidf(gf) * bf2f(u.v[e]));
+    }
+    a[i] = o;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void swiglu_bwd_kernel(const bf16x8* __restrict__ da,
+                                                            const bf16x8* __restrict__ h,
+                                                            bf16x8* __restrict__ dh, int64_t T, int F8) {
+  const int64_t items = T * F8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < items; i += stride) {
+    const int64_t t = i / F8;
+    const int c = (int)(i - t * F8);
+    const bf16x8 g = h[t * 2 * F8 + c], u = h[t * 2 * F8 + F8 + c], d = da[i];
+    bf16x8 dg, du;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gf = bf2f(g.v[e]), uf = bf2f(u.v[e]), df = bf2f(d.v[e]);
+      const float sg = sigmoidf(gf), si = gf * sg;
+      du.v[e] = f2bf(df * si);
+      dg.v[e] = f2bf(df * uf * sg * (1.f + gf * (1.f - sg)));
+    }
+    dh[t * 2 * F8 + c] = dg;
+    dh[t * 2 * F8 + F8 + c] = du;
+  }
+}
+
+}  // namespace
+
+PLX_API int plx_qkv_rope_fwd(const void* qkv, const float* cosv, const float* sinv, void* q, void* k, void* v,
+                             int64_t T, int S, int H, int KV, int D, int rot_heads, hipStream_t stream) {
+  if (T <= 0 || S <= 0 || T % S || D % 16 || rot_heads < 0 || rot_heads > H + KV) return 1;
+  const int64_t items = T * (H + 2 * KV) * (D / 16);
+  hipLaunchKernelGGL(qkv_rope_fwd_kernel, dim3(grid_for(items)), dim3(kBlock), 0, stream, (const bf16x8*)qkv, cosv,
+                     sinv, (bf16x8*)q, (bf16x8*)k, (bf16x8*)v, T, S, H, KV, D, rot_heads);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_qkv_rope_bwd(const void* dq, const void* dk, const void* dv, const float* cosv, const float* sinv,
+                             void* dqkv, int64_t T, int S, int H, int KV, int D, int rot_heads, hipStream_t stream) {
+  if (T <= 0 || S <= 0 || T % S || D % 16 || rot_heads < 0 || rot_heads > H + KV) return 1;
+  const int64_t items = T * (H + 2 * KV) * (D / 16);
+  hipLaunchKernelGGL(qkv_rope_bwd_kernel, dim3(grid_for(items)), dim3(kBlock), 0, stream, (const bf16x8*)dq,
+                     (const bf16x8*)dk, (const bf16x8*)dv, cosv, sinv, (bf16x8*)dqkv, T, S, H, KV, D, rot_heads);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_swiglu_fwd(const void* h, void* a, int64_t T, int F, hipStream_t stream) {
+  if (T <= 0 || F % 8) return 1;
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(grid_for(T * (F / 8))), dim3(kBlock), 0, stream, (const bf16x8*)h,
+                     (bf16x8*)a, T, F / 8);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_swiglu_bwd(const void* da, const void* h, void* dh, int64_t T, int F, hipStream_t stream) {
+  if (T <= 0 || F % 8) return 1;
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(T * (F / 8))), dim3(kBlock), 0, stream, (const bf16x8*)da,
+                     (const bf16x8*)h, (bf16x8*)dh, T, F / 8);
+  return (int)hipGetLastError();
+}

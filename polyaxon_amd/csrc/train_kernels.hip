@@ -94,6 +94,64 @@ __global__ __launch_bounds__(kBlock) void adamw_flat_kernel(float4* __restrict__
   }
 }
 
+// Mixed-precision AdamW for the language models (ops/flat.py lp mode): the model computes with bf16 weights
+// (views into `plp`) and produces bf16 gradients (`g`, zeroed here after use); the fp32 master copy `p` and the
+// moments stay fp32.  One pass: read p, g, m, v (14 B/elem), write p, m, v, plp and g (16 B/elem) -- no
+// separate fp32->bf16 weight cast per forward and no bf16->fp32 gradient cast per backward.
+// `decay` applies weight decay to the whole range (callers pass the decay segment only).
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf16_to_f(unsigned short h) { return __uint_as_float((uint32_t)h << 16); }
+
+__device__ __forceinline__ unsigned short f_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (finite inputs)
+  return (unsigned short)(u >> 16);
+}
+
+__global__ __launch_bounds__(kBlock) void adamw_mixed_kernel(float4* __restrict__ p, u16x4* __restrict__ g,
+                                                             float4* __restrict__ m, float4* __restrict__ v,
+                                                             u16x4* __restrict__ plp, int64_t n_vec, int decay_on,
+                                                             const float* __restrict__ hp,
+                                                             const int* __restrict__ step_ptr) {
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
+  const float t = (float)(*step_ptr + 1);
+  const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
+  const float step_size = lr / bc1, inv_sqrt_bc2 = rsqrtf(bc2);
+  const float decay = decay_on ? (1.f - lr * wd) : 1.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_vec; i += stride) {
+    const float4 pv = p[i], mv = m[i], vv = v[i];
+    const u16x4 gv = g[i];
+    float pp[4] = {pv.x, pv.y, pv.z, pv.w}, mm[4] = {mv.x, mv.y, mv.z, mv.w}, vq[4] = {vv.x, vv.y, vv.z, vv.w};
+    u16x4 lo;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gg = bf16_to_f(gv[k]);
+      mm[k] = b1 * mm[k] + (1.f - b1) * gg;
+      vq[k] = b2 * vq[k] + (1.f - b2) * gg * gg;
+      const float denom = sqrtf(vq[k]) * inv_sqrt_bc2 + eps;
+      pp[k] = pp[k] * decay - step_size * mm[k] / denom;
+      lo[k] = f_to_bf16(pp[k]);
+    }
+    p[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    m[i] = make_float4(mm[0], mm[1], mm[2], mm[3]);
+    v[i] = make_float4(vq[0], vq[1], vq[2], vq[3]);
+    plp[i] = lo;
+    g[i] = u16x4{0, 0, 0, 0};
+  }
+}
+
+// fp32 master -> bf16 model copy (after re-initialisation, checkpoint load or a parameter broadcast)
+__global__ __launch_bounds__(kBlock) void cast_lp_kernel(const float4* __restrict__ p, u16x4* __restrict__ plp,
+                                                         int64_t n_vec) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_vec; i += stride) {
+    const float4 pv = p[i];
+    plp[i] = u16x4{f_to_bf16(pv.x), f_to_bf16(pv.y), f_to_bf16(pv.z), f_to_bf16(pv.w)};
+  }
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 struct U4 {
   uint32_t x, y, z, w;
@@ -216,6 +274,22 @@ PLX_API int plx_adamw_flat(float* p, float* g, float* m, float* v, int64_t n, in
   const int64_t nv = n >> 2;
   hipLaunchKernelGGL(adamw_flat_kernel, dim3(grid_for(nv)), dim3(kBlock), 0, stream, (float4*)p, (float4*)g,
                      (float4*)m, (float4*)v, nv, n_decay >> 2, hp, step);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_adamw_mixed(float* p, void* g, float* m, float* v, void* plp, int64_t n, int decay_on,
+                            const float* hp, const int* step, hipStream_t stream) {
+  if (n & 3) return 1;
+  const int64_t nv = n >> 2;
+  hipLaunchKernelGGL(adamw_mixed_kernel, dim3(grid_for(nv)), dim3(kBlock), 0, stream, (float4*)p, (u16x4*)g,
+                     (float4*)m, (float4*)v, (u16x4*)plp, nv, decay_on, hp, step);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_cast_lp(const float* p, void* plp, int64_t n, hipStream_t stream) {
+  if (n & 3) return 1;
+  hipLaunchKernelGGL(cast_lp_kernel, dim3(grid_for(n >> 2)), dim3(kBlock), 0, stream, (const float4*)p,
+                     (u16x4*)plp, n >> 2);
   return (int)hipGetLastError();
 }
 

@@ -33,6 +33,7 @@ LIBRARIES: Dict[str, dict] = {
     "plx_rms": {"sources": ["rmsnorm.hip"], "kind": "hip", "link": []},
     "plx_conv": {"sources": ["conv_gemm.hip"], "kind": "hip", "link": []},
     "plx_pool": {"sources": ["pool_kernels.hip"], "kind": "hip", "link": []},
+    "plx_lm": {"sources": ["lm_kernels.hip"], "kind": "hip", "link": []},
     "plx_rccl": {"sources": ["rccl_comm.cpp"], "kind": "hip_host", "link": ["-lrccl"]},
 }
 
@@ -144,6 +145,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
     "plx_train": {
         "plx_sgd_flat": [_P, _P, _P, _L, _L, _P, _P, _P],
         "plx_adamw_flat": [_P, _P, _P, _P, _L, _L, _P, _P, _P],
+        "plx_adamw_mixed": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P],
+        "plx_cast_lp": [_P, _P, _L, _P],
         "plx_init_flat": [_P, _P, _P, _P, _I, _P, _P, _U64, _P],
         "plx_zero_flat": [_P, _L, _P],
         "plx_record_metric": [_P, _I, _P, _P, _I, _P],
@@ -180,6 +183,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
         "plx_gemm_nt_rows_per_block": [_I],
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
+        "plx_set_tn_plan": [_I, _I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
         "plx_weight_prepk": [_P, _L, _L, _L, _L, _P, _P, _I, _I, _I, _P],
@@ -188,6 +192,12 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_conv_dgrad_blocks": [_I, _I, _I, _I, _I, _I, _I],
         "plx_conv_wgrad_workspace": [_I, _I, _I, _I, _I, _I, _I, _I],
         "plx_conv_wgrad": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
+    },
+    "plx_lm": {
+        "plx_qkv_rope_fwd": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _I, _P],
+        "plx_qkv_rope_bwd": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _I, _P],
+        "plx_swiglu_fwd": [_P, _P, _L, _I, _P],
+        "plx_swiglu_bwd": [_P, _P, _P, _L, _I, _P],
     },
     "plx_pool": {
         "plx_maxpool3s2_forward": [_P, _P, _P, _I, _I, _I, _I, _P],

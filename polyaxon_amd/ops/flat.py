@@ -58,9 +58,19 @@ def direct_grad(p: torch.Tensor):
 
 
 class FlatParams:
-    """Re-home ``module``'s parameters into flat fp32 ``params``/``grads`` buffers on ``device``."""
+    """Re-home ``module``'s parameters into flat fp32 ``params``/``grads`` buffers on ``device``.
 
-    def __init__(self, module: nn.Module, device: torch.device, channels_last: bool = True):
+    ``lp_dtype=torch.bfloat16`` (the language models): the weight-decayed segment (every matrix: embeddings,
+    projections) is presented to the model as bf16 views into ``lp_params`` with bf16 gradients in
+    ``lp_grads``; ``params`` stays the fp32 master copy the optimizer updates (``plx_adamw_mixed`` rewrites
+    ``lp_params`` in the same pass).  The 1-D tail (norm weights, biases) keeps fp32 params and fp32 grads
+    (``grads`` then holds only that tail: ``grad_view`` maps flat offsets).  Autocast then has no weight to
+    cast and autograd no gradient to cast back: per Llama-3 8B step that removes ~580 cast kernels and a
+    fp32 read-modify-write of every gradient (profiles/r1_llama3_8b_*), and DP all-reduces move bf16.
+    """
+
+    def __init__(self, module: nn.Module, device: torch.device, channels_last: bool = True,
+                 lp_dtype: torch.dtype = None):
         named = [(n, p) for n, p in module.named_parameters() if p.requires_grad]
         decay = [(n, p) for n, p in named if p.dim() > 1]
         no_decay = [(n, p) for n, p in named if p.dim() <= 1]
@@ -74,22 +84,87 @@ class FlatParams:
                 off += _pad4(p.numel())
             if is_decay:
                 self.n_decay = off
+        if not decay:
+            self.n_decay = 0
         self.numel = off
         self.device = torch.device(device)
+        self.lp_dtype = lp_dtype
         self.params = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
-        self.grads = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        if lp_dtype is not None:
+            self.lp_params = torch.zeros(self.n_decay, dtype=lp_dtype, device=self.device)
+            self.lp_grads = torch.zeros(self.n_decay, dtype=lp_dtype, device=self.device)
+            self.grad_base = self.n_decay
+        else:
+            self.lp_params = self.lp_grads = None
+            self.grad_base = 0
+        self.grads = torch.zeros(self.numel - self.grad_base, dtype=torch.float32, device=self.device)
         by_name: Dict[str, nn.Parameter] = dict(named)
         self._views: Dict[str, torch.Tensor] = {}
+        self._master: Dict[str, torch.Tensor] = {}
         with torch.no_grad():
             for seg in self.segments:
                 old = by_name[seg.name]
-                view = self.params.as_strided(seg.shape, seg.strides, seg.offset)
-                view.copy_(old.detach().to(self.device))
-                newp = nn.Parameter(view)
-                newp.grad = self.grads.as_strided(seg.shape, seg.strides, seg.offset)
+                master = self.params.as_strided(seg.shape, seg.strides, seg.offset)
+                master.copy_(old.detach().to(self.device))
+                self._master[seg.name] = master
+                if lp_dtype is not None and seg.decay:
+                    newp = nn.Parameter(self.lp_params.as_strided(seg.shape, seg.strides, seg.offset))
+                    newp.grad = self.lp_grads.as_strided(seg.shape, seg.strides, seg.offset)
+                else:
+                    newp = nn.Parameter(master)
+                    newp.grad = self.grads.as_strided(seg.shape, seg.strides, seg.offset - self.grad_base)
+                newp._plx_flat = self
                 self._set(module, seg.name, newp)
                 self._views[seg.name] = newp
+        self._written = set()
+        self.sync_lp()
         module.to(self.device)  # buffers (BN running stats)
+
+    # ------------------------------------------------------------------ mixed precision (lp mode)
+    def sync_lp(self) -> None:
+        """Refresh the bf16 model weights from the fp32 master (after init / load / broadcast)."""
+        if self.lp_params is None or self.n_decay == 0:
+            return
+        if self.params.is_cuda:
+            from polyaxon_amd.ops import _native
+
+            _native.check(_native.lib("plx_train").plx_cast_lp(
+                self.params.data_ptr(), self.lp_params.data_ptr(), self.n_decay,
+                torch.cuda.current_stream(self.device).cuda_stream), "plx_cast_lp")
+        else:
+            with torch.no_grad():
+                self.lp_params.copy_(self.params[: self.n_decay])
+
+    def grad_view(self, lo: int, hi: int) -> torch.Tensor:
+        """Gradient elements [lo, hi) of the flat layout (never straddling the bf16 / fp32 boundary)."""
+        if self.lp_grads is None:
+            return self.grads[lo:hi]
+        if hi <= self.n_decay:
+            return self.lp_grads[lo:hi]
+        if lo >= self.n_decay:
+            return self.grads[lo - self.n_decay: hi - self.n_decay]
+        raise ValueError(f"grad range [{lo}, {hi}) straddles the bf16/fp32 boundary at {self.n_decay}")
+
+    def zero_grads(self) -> None:
+        self.grads.zero_()
+        if self.lp_grads is not None:
+            self.lp_grads.zero_()
+        self._written.clear()
+
+    def mark_written(self, slot: torch.Tensor) -> bool:
+        """Direct-gradient GEMMs (ops/lm.py): record that ``slot`` holds this step's gradient; True if it
+        already did (then the GEMM accumulates)."""
+        key = slot.data_ptr()
+        seen = key in self._written
+        self._written.add(key)
+        return seen
+
+    def grads_consumed(self) -> None:
+        """The optimizer zeroed the gradient buffers: the next direct write of every slot overwrites."""
+        self._written.clear()
+
+    def master(self, name: str) -> torch.Tensor:
+        return self._master[name]
 
     @staticmethod
     def _set(module: nn.Module, dotted: str, value: nn.Parameter) -> None:
@@ -148,4 +223,5 @@ class FlatParams:
                     v = torch.full(p.shape, float(scale))
                 else:
                     v = (torch.rand(p.shape, generator=g) * 2 - 1) * scale
-                p.copy_(v.to(p.device))
+                self._master[self.segment_of(p).name].copy_(v.to(p.device))
+        self.sync_lp()

@@ -1,0 +1,168 @@
+"""Language-model hot ops: fused QKV split + RoPE + head-major relayout, fused SwiGLU, and a Linear whose
+weight gradient is written by the GEMM straight into the flat (bf16) gradient buffer.
+
+HIP kernels in csrc/lm_kernels.hip for bf16 CUDA tensors; every op has a plain PyTorch composition used on
+CPU (tests, gloo runs) and as the numerics reference of the GPU tests.  On a GPU a bf16 input that the
+kernel cannot take (odd head size, ...) raises instead of silently falling back.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from polyaxon_amd.ops import _native
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _native_ok(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.dtype == torch.bfloat16
+
+
+# ---------------------------------------------------------------------------------------------- QKV + RoPE
+def qkv_rope_reference(qkv: torch.Tensor, B: int, S: int, H: int, KV: int, D: int,
+                       rope: Optional[Tuple[torch.Tensor, torch.Tensor]]):
+    q, k, v = qkv.view(B, S, H + 2 * KV, D).split([H, KV, KV], dim=2)
+    q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+    if rope is not None:
+        cos, sin = rope
+        c, s = cos[None, None, :S].to(q.dtype), sin[None, None, :S].to(q.dtype)
+
+        def rot(x):
+            d = x.shape[-1] // 2
+            x1, x2 = x[..., :d], x[..., d:]
+            return torch.cat([x1 * c - x2 * s, x1 * s + x2 * c], dim=-1)
+        q, k = rot(q), rot(k)
+    return q.contiguous(), k.contiguous(), v.contiguous()
+
+
+class _QKVRope(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, B, S, H, KV, D, rot):
+        lib = _native.lib("plx_lm")
+        qkv = qkv.contiguous()
+        q = torch.empty((B, H, S, D), dtype=qkv.dtype, device=qkv.device)
+        k = torch.empty((B, KV, S, D), dtype=qkv.dtype, device=qkv.device)
+        v = torch.empty_like(k)
+        _native.check(lib.plx_qkv_rope_fwd(qkv.data_ptr(), cos.data_ptr(), sin.data_ptr(), q.data_ptr(), k.data_ptr(),
+                                           v.data_ptr(), B * S, S, H, KV, D, rot, _stream()), "plx_qkv_rope_fwd")
+        ctx.save_for_backward(cos, sin)
+        ctx.dims = (B, S, H, KV, D, rot, qkv.shape)
+        return q, k, v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        lib = _native.lib("plx_lm")
+        cos, sin = ctx.saved_tensors
+        B, S, H, KV, D, rot, shape = ctx.dims
+        dq = dq.contiguous() if dq is not None else torch.zeros((B, H, S, D), dtype=torch.bfloat16, device=cos.device)
+        dk = dk.contiguous() if dk is not None else torch.zeros((B, KV, S, D), dtype=torch.bfloat16, device=cos.device)
+        dv = dv.contiguous() if dv is not None else torch.zeros((B, KV, S, D), dtype=torch.bfloat16, device=cos.device)
+        dqkv = torch.empty(shape, dtype=dq.dtype, device=dq.device)
+        _native.check(lib.plx_qkv_rope_bwd(dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), cos.data_ptr(), sin.data_ptr(),
+                                           dqkv.data_ptr(), B * S, S, H, KV, D, rot, _stream()), "plx_qkv_rope_bwd")
+        return dqkv, None, None, None, None, None, None, None, None
+
+
+def qkv_rope(qkv: torch.Tensor, B: int, S: int, H: int, KV: int, D: int,
+             rope: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+    """qkv [B, S, (H+2KV)*D] -> q [B,H,S,D], k/v [B,KV,S,D] (contiguous), q and k rotated when ``rope``
+    = (cos, sin) fp32 [>=S, D/2] is given."""
+    if not _native_ok(qkv):
+        return qkv_rope_reference(qkv, B, S, H, KV, D, rope)
+    if D % 16:
+        raise ValueError(f"plx_qkv_rope needs head_dim % 16 == 0, got {D}")
+    if rope is not None:
+        cos = rope[0][:S].float().contiguous()
+        sin = rope[1][:S].float().contiguous()
+        rot = H + KV
+    else:
+        cos = sin = torch.zeros(1, dtype=torch.float32, device=qkv.device)
+        rot = 0
+    return _QKVRope.apply(qkv, cos, sin, B, S, H, KV, D, rot)
+
+
+# ---------------------------------------------------------------------------------------------- SwiGLU
+def swiglu_reference(h: torch.Tensor) -> torch.Tensor:
+    g, u = h.chunk(2, dim=-1)
+    return F.silu(g) * u
+
+
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h):
+        lib = _native.lib("plx_lm")
+        h = h.contiguous()
+        F2 = h.shape[-1]
+        T = h.numel() // F2
+        a = torch.empty(h.shape[:-1] + (F2 // 2,), dtype=h.dtype, device=h.device)
+        _native.check(lib.plx_swiglu_fwd(h.data_ptr(), a.data_ptr(), T, F2 // 2, _stream()), "plx_swiglu_fwd")
+        ctx.save_for_backward(h)
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        lib = _native.lib("plx_lm")
+        (h,) = ctx.saved_tensors
+        da = da.contiguous()
+        F2 = h.shape[-1]
+        dh = torch.empty_like(h)
+        _native.check(lib.plx_swiglu_bwd(da.data_ptr(), h.data_ptr(), dh.data_ptr(), h.numel() // F2, F2 // 2,
+                                         _stream()), "plx_swiglu_bwd")
+        return dh
+
+
+def swiglu(h: torch.Tensor) -> torch.Tensor:
+    """h [..., 2F] = gate | up -> silu(gate) * up."""
+    if not _native_ok(h):
+        return swiglu_reference(h)
+    if h.shape[-1] % 16:
+        raise ValueError("plx_swiglu needs the hidden size % 8 == 0")
+    return _SwiGLU.apply(h)
+
+
+# ---------------------------------------------------------------------------------------------- direct-grad Linear
+class _LinearDirect(torch.autograd.Function):
+    """y = x W^T (+ b).  Backward writes dW = dy^T x with the GEMM's output pointer on the parameter's flat
+    gradient slot (``p.grad``, bf16 in lp mode): no separate gradient tensor and no autograd ``grad += g``
+    read-modify-write.  The flat buffer is zeroed by the optimizer, so the first write of a step is a plain
+    GEMM (beta = 0) and any later one (a weight used twice) accumulates (beta = 1)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, slot, flat):
+        ctx.save_for_backward(x, weight)
+        ctx.slot, ctx.flat, ctx.has_bias = slot, flat, bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dx = dy @ weight if ctx.needs_input_grad[0] else None
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1]).to(dy2.dtype)
+        g = ctx.slot
+        if ctx.flat.mark_written(g):
+            torch.addmm(g, dy2.t(), x2, out=g)
+        else:
+            torch.mm(dy2.t(), x2, out=g)
+        db = dy2.sum(0) if ctx.has_bias else None
+        cb = getattr(weight, "_plx_ready_cb", None)
+        if cb is not None:
+            cb(weight)
+        return dx, None, db, None, None
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """F.linear, or the direct-gradient form when ``weight`` is a flat parameter whose grad slot has the
+    compute dtype (FlatParams lp mode with direct grads enabled)."""
+    slot = getattr(weight, "grad", None)
+    flat = getattr(weight, "_plx_flat", None)
+    if (flat is not None and getattr(weight, "_plx_direct_grad", False) and slot is not None and weight.requires_grad
+            and torch.is_grad_enabled() and slot.dtype == weight.dtype and x.dtype == weight.dtype
+            and slot.is_contiguous()):
+        return _LinearDirect.apply(x, weight, bias, slot, flat)
+    return F.linear(x, weight, bias)

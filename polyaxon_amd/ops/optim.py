@@ -57,6 +57,9 @@ class FusedSGD:
 
     def step_(self) -> None:
         f = self.flat
+        f.grads_consumed()
+        if f.lp_params is not None:
+            raise NotImplementedError("FusedSGD has no mixed-precision (lp) flat mode; use FusedAdamW")
         if f.params.is_cuda:
             rc = _native.lib("plx_train").plx_sgd_flat(
                 f.params.data_ptr(), f.grads.data_ptr(), self.momentum_buf.data_ptr(), f.numel, f.n_decay,
@@ -112,27 +115,45 @@ class FusedAdamW:
 
     def step_(self) -> None:
         f = self.flat
-        if f.params.is_cuda:
-            rc = _native.lib("plx_train").plx_adamw_flat(
-                f.params.data_ptr(), f.grads.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
-                f.numel, f.n_decay, self.hp.data_ptr(), self.step.data_ptr(), _stream_ptr(f.params))
-            _native.check(rc, "plx_adamw_flat")
-        else:
+        f.grads_consumed()  # every kernel below zeroes the gradients it reads
+        if not f.params.is_cuda:
             self._step_reference()
+            return
+        lib = _native.lib("plx_train")
+        st = _stream_ptr(f.params)
+        if f.lp_params is None:
+            rc = lib.plx_adamw_flat(
+                f.params.data_ptr(), f.grads.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                f.numel, f.n_decay, self.hp.data_ptr(), self.step.data_ptr(), st)
+            _native.check(rc, "plx_adamw_flat")
+            return
+        # lp mode: bf16 decay segment (master fp32 + bf16 model copy) and the fp32 tail
+        nd = f.n_decay
+        if nd:
+            _native.check(lib.plx_adamw_mixed(
+                f.params.data_ptr(), f.lp_grads.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                f.lp_params.data_ptr(), nd, 1, self.hp.data_ptr(), self.step.data_ptr(), st), "plx_adamw_mixed")
+        if f.numel > nd:
+            off = nd * 4
+            _native.check(lib.plx_adamw_flat(
+                f.params.data_ptr() + off, f.grads.data_ptr(), self.exp_avg.data_ptr() + off,
+                self.exp_avg_sq.data_ptr() + off, f.numel - nd, 0, self.hp.data_ptr(), self.step.data_ptr(), st),
+                "plx_adamw_flat")
 
     @torch.no_grad()
     def _step_reference(self) -> None:
         f = self.flat
         lr, b1, b2, eps, wd = (float(self.hp[i]) for i in range(5))
         t = int(self.step.item()) + 1
-        g = f.grads
+        g = f.grads if f.lp_grads is None else torch.cat([f.lp_grads.float(), f.grads])
         f.params[: f.n_decay].mul_(1.0 - lr * wd)
         self.exp_avg.mul_(b1).add_(g, alpha=1 - b1)
         self.exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
         bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
         denom = (self.exp_avg_sq.sqrt() / bc2 ** 0.5).add_(eps)
         f.params.addcdiv_(self.exp_avg, denom, value=-lr / bc1)
-        g.zero_()
+        f.zero_grads()
+        f.sync_lp()
 
     def state_buffers(self) -> Dict[str, torch.Tensor]:
         return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}

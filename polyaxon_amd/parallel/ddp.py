@@ -48,7 +48,10 @@ def init_from_env(backend: Optional[str] = None, device: Optional[torch.device] 
 class FlatDDP:
     def __init__(self, flat: FlatParams, process_group=None, bucket_mb: float = 64.0, overlap: bool = True):
         self.flat = flat
-        flat.enable_direct_grads(False)  # bucket readiness needs autograd's post-accumulate hooks
+        if flat.lp_params is None:
+            # the ResNet native ops write weight grads without telling anyone: bucket readiness then needs
+            # autograd's post-accumulate hooks.  lp-mode direct-gradient GEMMs (ops/lm.py) call _plx_ready_cb.
+            flat.enable_direct_grads(False)
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.overlap = overlap and self.world > 1
@@ -60,6 +63,9 @@ class FlatDDP:
         cur: List = []
         size = 0
         for seg in segs:
+            if cur and flat.lp_grads is not None and cur[-1].decay != seg.decay:
+                self._close(cur)  # a bucket never spans the fp32 tail and the bf16 gradients
+                cur, size = [], 0
             cur.append(seg)
             size += seg.numel
             if size >= bucket_elems:
@@ -73,7 +79,9 @@ class FlatDDP:
         if self.overlap:
             for seg in flat.segments:
                 p = flat.parameter(seg.name)
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(self.seg_bucket[seg.name])))
+                hook = self._make_hook(self.seg_bucket[seg.name])
+                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+                p._plx_ready_cb = hook
         self.reset()
 
     def _close(self, segs) -> None:
@@ -97,7 +105,7 @@ class FlatDDP:
 
     def _launch(self, b: int) -> None:
         lo, hi, _ = self.buckets[b]
-        view = self.flat.grads[lo:hi]
+        view = self.flat.grad_view(lo, hi)
         if self.avg_supported:
             h = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)
             self._handles.append((h, None))
@@ -126,8 +134,11 @@ class FlatDDP:
         """Make every rank start from rank ``src``'s weights (one collective over the flat buffer)."""
         if self.world > 1:
             dist.broadcast(self.flat.params, src=src, group=self.pg)
+            self.flat.sync_lp()
 
     def remove_hooks(self) -> None:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        for seg in self.flat.segments:
+            self.flat.parameter(seg.name).__dict__.pop("_plx_ready_cb", None)

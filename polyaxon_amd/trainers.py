@@ -176,6 +176,10 @@ def train_lm(argv=None) -> float:
     ap.add_argument("--bucket_mb", type=float, default=64.0)
     ap.add_argument("--checkpoint_activations", action="store_true")
     ap.add_argument("--beta2", type=float, default=0.95)
+    ap.add_argument("--fp32_weights", action="store_true",
+                    help="model computes from fp32 weights under autocast (default on GPU: bf16 weights/grads with "
+                         "an fp32 master copy in the optimizer)")
+    ap.add_argument("--fixed_batch", action="store_true", help="reuse one synthetic batch every step")
     args = _parse(ap, argv)
     backend = "gloo" if args.cpu or not torch.cuda.is_available() else "nccl"
     info = init_from_env(backend)
@@ -185,13 +189,20 @@ def train_lm(argv=None) -> float:
     seq = min(args.seq, cfg.max_seq_len)
     torch.manual_seed(args.seed)
     model = Transformer(cfg) if dev.type == "cpu" else _build_on_device(Transformer, cfg, dev)
-    flat = FlatParams(model, dev, channels_last=False)
+    lp = torch.bfloat16 if (dev.type == "cuda" and not args.fp32_weights) else None
+    flat = FlatParams(model, dev, channels_last=False, lp_dtype=lp)
+    if lp is not None:
+        flat.enable_direct_grads(True)  # weight-gradient GEMMs write into the flat bf16 grads (ops/lm.py)
     step = torch.zeros(1, dtype=torch.int32, device=dev)
     opt = FusedAdamW(flat, lr=args.lr, betas=(0.9, args.beta2), weight_decay=args.weight_decay, step_counter=step)
     ddp = FlatDDP(flat, bucket_mb=args.bucket_mb)
     ddp.broadcast_params()
-    g = torch.Generator(device="cpu").manual_seed(args.seed + 1000 * info["rank"])
-    tokens = torch.randint(0, cfg.vocab_size, (args.bs, seq), generator=g).to(dev)
+    g = torch.Generator(device=dev).manual_seed(args.seed + 1000 * info["rank"])
+
+    def batch():  # synthetic tokens drawn on the device: a fresh batch per step costs one tiny kernel
+        return torch.randint(0, cfg.vocab_size, (args.bs, seq), generator=g, device=dev)
+
+    tokens = batch()
     xp = _tracker() if info["rank"] == 0 else None
     amp = dev.type == "cuda"
     t0 = time.time()
@@ -204,6 +215,8 @@ def train_lm(argv=None) -> float:
             t0 = time.time()
         lr = args.lr * min(1.0, (it + 1) / args.warmup_steps) if args.warmup_steps else args.lr
         opt.set_hparams(lr=lr)
+        if it and not args.fixed_batch:
+            tokens = batch()
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             loss = lm_loss(model(tokens), tokens)
         loss.backward()

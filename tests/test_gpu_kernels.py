@@ -62,6 +62,36 @@ def test_adamw_flat_matches_torch(cuda):
     torch.testing.assert_close(p, torch.cat([pa.detach(), pb.detach()]), rtol=1e-5, atol=1e-6)
 
 
+def test_adamw_mixed_matches_torch(cuda):
+    """bf16 grads + fp32 master: same update as torch AdamW fed the (bf16-exact) grads; the bf16 model copy is
+    the round-to-nearest-even of the master; the bf16 grads are zeroed."""
+    lib = _native.lib("plx_train")
+    n = 4096 * 9 + 4
+    p = torch.randn(n, device=cuda)
+    m = torch.zeros(n, device=cuda)
+    v = torch.zeros(n, device=cuda)
+    plp = torch.empty(n, dtype=torch.bfloat16, device=cuda)
+    hp = torch.tensor([1e-3, 0.9, 0.95, 1e-8, 0.1, 0, 0, 0], device=cuda)
+    step = torch.zeros(1, dtype=torch.int32, device=cuda)
+    pa = torch.nn.Parameter(p.clone())
+    opt = torch.optim.AdamW([pa], lr=1e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    for it in range(3):
+        g = torch.randn(n, device=cuda).to(torch.bfloat16)
+        pa.grad = g.float()
+        _native.check(lib.plx_adamw_mixed(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), plp.data_ptr(), n,
+                                          1, hp.data_ptr(), step.data_ptr(), _stream()), "adamw_mixed")
+        step += 1
+        opt.step()
+        torch.cuda.synchronize()
+        assert float(g.float().abs().max()) == 0.0
+    torch.testing.assert_close(p, pa.detach(), rtol=1e-5, atol=1e-6)
+    assert torch.equal(plp, p.to(torch.bfloat16))
+    q = torch.empty_like(plp)
+    _native.check(lib.plx_cast_lp(p.data_ptr(), q.data_ptr(), n, _stream()), "cast_lp")
+    torch.cuda.synchronize()
+    assert torch.equal(q, p.to(torch.bfloat16))
+
+
 def test_init_flat_statistics(cuda):
     from polyaxon_amd.ops.flat import FlatParams
     from polyaxon_amd.models.resnet import resnet50

@@ -1,0 +1,87 @@
+"""GPU tests of the language-model HIP kernels (csrc/lm_kernels.hip) against plain PyTorch fp32 references, and
+of the lp-mode (bf16 weights/grads + fp32 master, direct weight-gradient GEMMs) model against the fp32 model."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from polyaxon_amd.ops import _native
+
+pytestmark = pytest.mark.gpu
+
+
+def _rope_tables(S, D, theta, dev):
+    from polyaxon_amd.models.transformer import rope_cache
+
+    return rope_cache(S, D, theta, dev)
+
+
+@pytest.mark.parametrize("B,S,H,KV,D,use_rope", [(2, 64, 4, 2, 128, True), (1, 128, 32, 8, 128, True),
+                                                 (2, 32, 12, 12, 64, False), (3, 16, 2, 1, 16, True)])
+def test_qkv_rope_matches_fp32(cuda, B, S, H, KV, D, use_rope):
+    from polyaxon_amd.ops.lm import qkv_rope, qkv_rope_reference
+
+    assert _native.lib("plx_lm") is not None
+    torch.manual_seed(0)
+    qkv = torch.randn(B, S, (H + 2 * KV) * D, device=cuda).to(torch.bfloat16).requires_grad_()
+    rope = _rope_tables(S, D, 500000.0, cuda) if use_rope else None
+    q, k, v = qkv_rope(qkv, B, S, H, KV, D, rope)
+    assert q.shape == (B, H, S, D) and k.shape == (B, KV, S, D) and v.is_contiguous()
+    ref_in = qkv.detach().float().requires_grad_()
+    qr, kr, vr = qkv_rope_reference(ref_in, B, S, H, KV, D, rope)
+    for a, b in ((q, qr), (k, kr), (v, vr)):
+        torch.testing.assert_close(a.float(), b, rtol=1e-2, atol=1e-2)
+    gq, gk, gv = (torch.randn_like(t) for t in (q, k, v))
+    torch.autograd.backward([q, k, v], [gq, gk, gv])
+    torch.autograd.backward([qr, kr, vr], [gq.float(), gk.float(), gv.float()])
+    torch.testing.assert_close(qkv.grad.float(), ref_in.grad, rtol=1e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("T,Fh", [(1, 8), (37, 1376), (4096, 14336)])
+def test_swiglu_matches_fp32(cuda, T, Fh):
+    from polyaxon_amd.ops.lm import swiglu, swiglu_reference
+
+    torch.manual_seed(1)
+    h = (torch.randn(T, 2 * Fh, device=cuda) * 2).to(torch.bfloat16).requires_grad_()
+    a = swiglu(h)
+    hr = h.detach().float().requires_grad_()
+    ar = swiglu_reference(hr)
+    torch.testing.assert_close(a.float(), ar, rtol=1e-2, atol=1e-2)
+    g = torch.randn_like(a)
+    a.backward(g)
+    ar.backward(g.float())
+    torch.testing.assert_close(h.grad.float(), hr.grad, rtol=2e-2, atol=2e-2)
+
+
+def test_lp_model_matches_fp32_model(cuda):
+    """tiny Llama: loss and master-weight gradients of the lp path (HIP RoPE/SwiGLU/RMSNorm kernels, bf16 flat
+    weights, direct weight-gradient GEMMs) vs the same model in fp32 without any of them."""
+    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+
+    cfg = tiny_llama(d_model=128, n_heads=4, n_kv_heads=2, d_ff=256, vocab_size=512)
+    tokens = torch.randint(0, 512, (2, 64), device=cuda)
+    torch.manual_seed(0)
+    with torch.device(cuda):
+        m32 = Transformer(cfg)
+    torch.manual_seed(0)
+    with torch.device(cuda):
+        mlp = Transformer(cfg)
+    f32 = FlatParams(m32, cuda, channels_last=False)
+    flp = FlatParams(mlp, cuda, channels_last=False, lp_dtype=torch.bfloat16)
+    flp.enable_direct_grads(True)
+    torch.testing.assert_close(f32.params, flp.params)
+    l32 = lm_loss(m32(tokens), tokens)
+    l32.backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        llp = lm_loss(mlp(tokens), tokens)
+    llp.backward()
+    assert abs(float(l32) - float(llp)) < 0.05
+    assert len(flp._written) > 0  # the direct-gradient GEMMs ran
+    g32 = f32.grads
+    glp = torch.cat([flp.lp_grads.float(), flp.grads])
+    cos = F.cosine_similarity(g32, glp, dim=0)
+    assert float(cos) > 0.99, float(cos)
+    for seg in f32.segments:  # every parameter gets a gradient of the right size
+        a = g32[seg.offset: seg.offset + seg.numel]
+        b = glp[seg.offset: seg.offset + seg.numel]
+        assert float(b.norm()) > 0 and abs(float(a.norm()) - float(b.norm())) <= 0.1 * float(a.norm()) + 1e-4, seg.name

@@ -70,3 +70,103 @@ def test_ddp_matches_single_process_average():
     loss = sum(lm_loss(m(t), t) for t in toks) / 2
     loss.backward()
     assert all(p.grad is not None for p in m.parameters())
+
+
+def _lp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
+
+    init_from_env("gloo")
+    torch.manual_seed(0)
+    model = Transformer(tiny_llama())
+    flat = FlatParams(model, "cpu", channels_last=False, lp_dtype=torch.bfloat16)
+    flat.enable_direct_grads(True)  # weight grads written by the GEMM; buckets counted down by _plx_ready_cb
+    ddp = FlatDDP(flat, bucket_mb=0.01)
+    torch.manual_seed(100 + rank)
+    tokens = torch.randint(0, 256, (4, 16))
+    ddp.broadcast_params()
+    lm_loss(model(tokens), tokens).backward()
+    ddp.finish()
+    g = torch.cat([flat.lp_grads.float(), flat.grads])
+    gathered = [torch.zeros_like(g) for _ in range(world)]
+    dist.all_gather(gathered, g)
+    # no bucket straddles the bf16 / fp32 boundary
+    ok_buckets = all(hi <= flat.n_decay or lo >= flat.n_decay for lo, hi, _ in ddp.buckets)
+    q.put((rank, ok_buckets, all(torch.equal(gathered[0], x) for x in gathered), float(g.norm())))
+    dist.destroy_process_group()
+
+
+def test_flat_ddp_lp_mode_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(r[1] and r[2] for r in res) and res[0][3] > 0
+
+
+def test_lp_mode_matches_fp32_training():
+    """bf16 model weights + fp32 master (lp mode) track the all-fp32 flat path within bf16 tolerance."""
+    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.ops.optim import FusedAdamW
+
+    tokens = torch.randint(0, 256, (4, 16), generator=torch.Generator().manual_seed(3))
+    out = {}
+    for lp in (None, torch.bfloat16):
+        torch.manual_seed(0)
+        model = Transformer(tiny_llama())
+        flat = FlatParams(model, "cpu", channels_last=False, lp_dtype=lp)
+        if lp is not None:
+            assert model.embed.weight.dtype == torch.bfloat16 and model.norm.weight.dtype == torch.float32
+            assert flat.grads.numel() == flat.numel - flat.n_decay
+        opt = FusedAdamW(flat, lr=1e-2, weight_decay=0.1)
+        losses = []
+        for _ in range(3):
+            loss = lm_loss(model(tokens), tokens)
+            loss.backward()
+            opt.step_()
+            opt.step += 1
+            losses.append(float(loss))
+        if lp is not None:
+            assert float(flat.lp_grads.abs().max()) == 0.0  # zeroed by the step
+            assert torch.equal(flat.lp_params, flat.params[: flat.n_decay].to(torch.bfloat16))
+        out[lp] = (losses, flat.params.clone())
+    (l32, p32), (l16, p16) = out[None], out[torch.bfloat16]
+    assert abs(l32[0] - l16[0]) < 0.05 and l16[-1] < l16[0]
+    assert (p32 - p16).abs().max() < 0.05
+
+
+def test_direct_grad_linear_matches_autograd():
+    """lp mode: the direct-gradient GEMM path (ops/lm.linear) leaves exactly autograd's gradients in the flat
+    buffer, also across two backward passes (accumulation) and an optimizer step (overwrite again)."""
+    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+
+    tokens = torch.randint(0, 256, (2, 16), generator=torch.Generator().manual_seed(5))
+    grads = {}
+    for direct in (False, True):
+        torch.manual_seed(0)
+        model = Transformer(tiny_llama())
+        flat = FlatParams(model, "cpu", channels_last=False, lp_dtype=torch.bfloat16)
+        flat.enable_direct_grads(direct)
+        for _ in range(2):
+            lm_loss(model(tokens), tokens).backward()
+        grads[direct] = (flat.lp_grads.float().clone(), flat.grads.clone())
+        if direct:
+            assert len(flat._written) > 0
+            flat.zero_grads()
+            lm_loss(model(tokens), tokens).backward()
+            torch.testing.assert_close(flat.lp_grads.float() * 2, grads[True][0], rtol=0.02, atol=2e-3)
+    torch.testing.assert_close(grads[True][0], grads[False][0], rtol=0.02, atol=2e-3)
+    torch.testing.assert_close(grads[True][1], grads[False][1], rtol=1e-3, atol=1e-5)
