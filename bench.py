@@ -103,6 +103,10 @@ def main() -> int:
                           args.unit_steps, seed=10_000 + rank)
     if args.warmup > 0:
         warm.run(max_trials=args.warmup)
+        # plus one short bracket with a rung promotion (snapshot -> top-k reduction -> resume): the first
+        # promotion of a cold process otherwise pays ~0.8 s of lazily paged-in library code inside the timed
+        # region (measured on a fresh box: trial 9 took 1.2 s instead of 0.42 s)
+        HyperbandSweep(HyperbandSearchManager(hptuning(20_000 + rank, 3, 3)), ex, 1, seed=20_000 + rank).run()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -139,9 +143,12 @@ def main() -> int:
             t_target = min(t_target, start_ev.elapsed_time(r.end_event) / 1000.0)
     best = min((r.metric for r in records if r.metric is not None), default=math.nan)
     if args.verbose:
+        prev = 0.0
         for r in records:
+            t_end = start_ev.elapsed_time(r.end_event) if r.end_event is not None else float("nan")
             log(f"trial {r.trial} cfg {r.config_id} it {r.iteration}/{r.bracket_iteration} res {r.resource} "
-                f"steps {r.steps} metric {r.metric} params {r.params}")
+                f"steps {r.steps} ends {t_end:.1f} ms (+{t_end - prev:.1f}) metric {r.metric}")
+            prev = t_end
     t = torch.tensor([elapsed, -t_target if math.isfinite(t_target) else -math.inf, train_steps, best],
                      dtype=torch.float64, device=dev)
     if world > 1:
