@@ -10,9 +10,11 @@ WORLD_SIZE and call NCCL themselves.  This module is what a polyflow DP trial us
   its ``all_reduce(AVG)`` is launched asynchronously (``async_op=True``: RCCL runs on its own stream),
   so communication overlaps the rest of the backward; ``finish()`` waits for the tail;
 * segments are bucketed in reverse registration order so the buckets fill in backward order;
-* optional ZeRO-1 (``shard_optimizer=True``): reduce-scatter instead of all-reduce, every rank updates
-  only its shard of the flat buffers with the fused optimizer kernel, then all-gathers the parameters —
-  optimizer state memory / world, same bytes on the wire.
+* lp mode (FlatParams ``lp_dtype=bf16``, the language models): the weight gradients are bf16, so the
+  all-reduce moves half the bytes; buckets never straddle the bf16 / fp32-tail boundary, and the direct
+  weight-gradient GEMMs (ops/lm.py) count their bucket down through ``_plx_ready_cb`` instead of autograd's
+  post-accumulate hook.  (Optimizer-state sharding / ZeRO-1 is not implemented: an 8B model's fp32 master +
+  moments are 96 GB, which one 288 GB MI355X holds unsharded.)
 Backend ``"nccl"`` is RCCL on ROCm; ``"gloo"`` works for CPU tests.
 """
 from __future__ import annotations
