@@ -37,6 +37,7 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
     store = flow.store
     settings = settings or Settings.load(env={})
     accounts = Accounts(store, settings, transport=sso_transport)
+    _metric_buckets: Dict[int, Any] = {}  # xid -> (tokens, last refill) for api.throttle_metrics_per_s
     app = FastAPI(title="polyaxon-mi355x", version=__version__)
     if admin_token and not store.user_for_token(admin_token):
         if store.get_user("root"):
@@ -492,8 +493,18 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
 
     @app.post("/api/v1/{username}/{project}/experiments/{xid}/metrics", status_code=201)
     async def create_metrics(username: str, project: str, xid: int, request: Request, user=Depends(auth)):
-        """Single ``{"values": {...}}`` or a list of them (batched ingestion, no per-request throttle)."""
+        """Single ``{"values": {...}}`` or a list of them (batched ingestion).  ``api.throttle_metrics_per_s``
+        > 0 caps requests per experiment (reference throttle scope 'high', config_settings/rest.py:20); a batch
+        counts as one request, so batching clients are never slowed down."""
         xp_or_404(username, project, xid)
+        rate = settings.get("api.throttle_metrics_per_s")
+        if rate:
+            now = time.monotonic()
+            tokens, last = _metric_buckets.get(xid, (rate, now))
+            tokens = min(rate, tokens + (now - last) * rate)
+            if tokens < 1.0:
+                raise HTTPException(429, "Request was throttled.", headers={"Retry-After": f"{(1 - tokens) / rate:.2f}"})
+            _metric_buckets[xid] = (tokens - 1.0, now)
         body = await request.json()
         rows = body if isinstance(body, list) else [body]
         store.add_metrics_batch([(xid, r.get("values", {}), r.get("step"), r.get("created_at")) for r in rows])
@@ -800,7 +811,7 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
         async def gen():
             for _ in range(int(os.environ.get("PLX_STREAM_MAX_TICKS", "1000000"))):
                 yield f"data: {json.dumps(experiment_resources(flow, xid))}\n\n"
-                await asyncio.sleep(1.0)
+                await asyncio.sleep(settings.get("telemetry.interval_s"))
         return StreamingResponse(gen(), media_type="text/event-stream")
 
     return app

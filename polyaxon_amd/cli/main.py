@@ -321,7 +321,11 @@ def server(c, host, port, token, gpus, sets):
     gpus = gpus if gpus is not None else st.get("scheduler.gpus")
     token = token or st.get("api.admin_token") or c.cfg.get("token") or uuid.uuid4().hex
     alloc = DeviceAllocator([Device(i) for i in range(gpus)]) if gpus is not None else None
-    flow = Polyflow(os.path.expanduser(c.cfg["root"]), allocator=alloc, api_host=f"http://{host}:{port}").start()
+    import logging
+
+    logging.basicConfig(level=getattr(logging, st.get("logs.level")))
+    root = st.get("root") if st.origins.get("root") != "default" else os.path.expanduser(c.cfg["root"])
+    flow = Polyflow(root, allocator=alloc, api_host=f"http://{host}:{port}", settings=st).start()
     click.echo(f"plx server on http://{host}:{port}  token={token}")
     try:
         uvicorn.run(create_app(flow, admin_token=token, settings=st, internal_token=st.get("secret.internal_token"),

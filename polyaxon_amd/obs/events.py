@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import fnmatch
 import json
+import os
 import logging
 import queue
 import threading
@@ -103,12 +104,17 @@ class Event:
 
 
 class Stats:
-    """Counters/timings (reference stats/: noop | statsd | datadog). Kept in-process; optional statsd UDP."""
+    """Counters/timings (reference stats/: noop | statsd | datadog). Always kept in-process; ``statsd_addr``
+    also sends them over UDP, as plain statsd lines or, with ``backend="datadog"``, DogStatsD lines carrying
+    ``tags`` (reference stats/datadog.py:11-35)."""
 
-    def __init__(self, statsd_addr: Optional[Tuple[str, int]] = None, prefix: str = "polyaxon"):
+    def __init__(self, statsd_addr: Optional[Tuple[str, int]] = None, prefix: str = "polyaxon",
+                 backend: str = "statsd", tags: Optional[List[str]] = None):
         self.counters: Counter = Counter()
         self.timings: Dict[str, List[float]] = {}
         self.prefix = prefix
+        self.backend = backend
+        self.tags = list(tags or [])
         self._addr = statsd_addr
         self._sock = None
         if statsd_addr:
@@ -116,13 +122,19 @@ class Stats:
 
             self._sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
 
+    def _line(self, key: str, value: str, kind: str) -> str:
+        line = f"{self.prefix}.{key}:{value}|{kind}"
+        if self.backend == "datadog" and self.tags:
+            line += "|#" + ",".join(self.tags)
+        return line
+
     def incr(self, key: str, value: int = 1) -> None:
         self.counters[key] += value
-        self._send(f"{self.prefix}.{key}:{value}|c")
+        self._send(self._line(key, str(value), "c"))
 
     def timing(self, key: str, ms: float) -> None:
         self.timings.setdefault(key, []).append(ms)
-        self._send(f"{self.prefix}.{key}:{ms:.3f}|ms")
+        self._send(self._line(key, f"{ms:.3f}", "ms"))
 
     def _send(self, payload: str) -> None:
         if self._sock is not None:
@@ -227,6 +239,22 @@ class EmailAction:
             return False
 
 
+class JsonlTracker:
+    """Product-analytics sink (reference tracker/publish_tracker.py sends every event to Segment).  The node
+    has no egress, so events are appended as JSON lines to a local file an operator can ship elsewhere."""
+
+    def __init__(self, path: str):
+        self.path = path
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        self._lock = threading.Lock()
+
+    def __call__(self, ev: Event) -> None:
+        line = json.dumps({"event": ev.event_type, "actor": ev.actor, "object_kind": ev.object_kind,
+                           "object_id": ev.object_id, "ts": ev.created_at}, default=str)
+        with self._lock, open(self.path, "a") as f:
+            f.write(line + "\n")
+
+
 def actions_from_config(cfg: Dict[str, Any]) -> List[Any]:
     """``{"webhooks": [{"url", "kind", "method", "events"}...], "email": {"host", "port", "to", "sender",
     "events", "use_tls", "username", "password"}}`` -> action objects (reference INTEGRATIONS_* settings)."""
@@ -269,6 +297,22 @@ class Auditor:
         self._q: "queue.Queue[Tuple[WebhookAction, Event]]" = queue.Queue()
         self._worker: Optional[threading.Thread] = None
         self.delivered: List[Tuple[str, bool]] = []
+
+    @classmethod
+    def from_settings(cls, store, settings, root: Optional[str] = None) -> "Auditor":
+        """Stats backend, tracker and notification actions from :mod:`polyaxon_amd.conf` settings."""
+        backend = settings.get("stats.backend")
+        addr = (settings.get("stats.host"), settings.get("stats.port")) if backend in ("statsd", "datadog") else None
+        a = cls(store, Stats(addr, prefix=settings.get("stats.prefix"), backend=backend or "statsd",
+                             tags=[f"service:{settings.get('service')}", f"env:{settings.get('environment')}"]))
+        if settings.get("tracker.backend") == "memory":
+            a.tracked = []
+            a.subscribe("*", a.tracked.append)
+        elif settings.get("tracker.backend") == "jsonl":
+            a.subscribe("*", JsonlTracker(os.path.join(root or settings.get("root"), "tracker", "events.jsonl")))
+        if settings.get("notifications"):
+            a.configure(load_notification_config(settings.get("notifications")))
+        return a
 
     def subscribe(self, pattern: str, fn: Callable[[Event], None]) -> None:
         self._subs.append((pattern, fn))

@@ -116,7 +116,15 @@ class Polyflow:
     def __init__(self, root: str, store: Optional[Store] = None, allocator: Optional[DeviceAllocator] = None,
                  auditor: Optional[Auditor] = None, api_host: Optional[str] = None, stop_grace_s: float = 10.0,
                  python: Optional[str] = None, reconcile_s: float = 5.0,
-                 health_check: Optional[Callable[[], List[int]]] = None, clean_on_start: bool = True):
+                 health_check: Optional[Callable[[], List[int]]] = None, clean_on_start: bool = True,
+                 settings=None):
+        """``settings`` (polyaxon_amd.conf.Settings, e.g. from ``plx server``) supplies the reconcile period,
+        stop grace, build reuse window, stats / tracker / notification backends; explicit arguments win."""
+        if settings is not None:
+            reconcile_s = settings.get("scheduler.reconcile_interval_s") if reconcile_s == 5.0 else reconcile_s
+            stop_grace_s = settings.get("scheduler.stop_grace_s") if stop_grace_s == 10.0 else stop_grace_s
+        self.settings = settings
+        self.build_reuse_s = settings.get("scheduler.build_reuse_s") if settings is not None else BUILD_REUSE_S
         self.paths = Paths(root)
         self.clean_on_start = clean_on_start
         self.store_path = os.path.join(self.paths.root, "polyaxon.sqlite")
@@ -124,6 +132,8 @@ class Polyflow:
         if store is not None and store.path != ":memory:":
             self.store_path = store.path
         self.alloc = allocator or DeviceAllocator()
+        if auditor is None and settings is not None:
+            auditor = Auditor.from_settings(self.store, settings, root=self.paths.root)
         self.auditor = auditor or Auditor(self.store)
         if auditor is None and os.environ.get("PLX_NOTIFICATIONS"):
             from polyaxon_amd.obs.events import load_notification_config
@@ -376,7 +386,7 @@ class Polyflow:
         """Run ``build.build_steps`` once per (image, steps, env) hash, reusing a success within 6 h.
         Returns the build job id the dependent must wait for, or None if a cached build exists."""
         h = self._build_hash(spec, dependent.cwd)
-        cached = self.store.last_build_for_hash(h, BUILD_REUSE_S)
+        cached = self.store.last_build_for_hash(h, self.build_reuse_s)
         if cached and not spec.build.nocache:
             dependent.extra_env.update({"PLX_BUILD_DIR": cached["outputs_path"] or ""})
             if dependent.kind == "experiment":

@@ -323,3 +323,42 @@ def test_settings_cli(tmp_path, monkeypatch, capsys):
     rows = {r["key"]: r for r in json.loads(capsys.readouterr().out)}
     assert rows["api.port"]["value"] == 8123 and rows["api.port"]["origin"] == "env"
     assert main(["settings", "--set", "api.port=abc"]) == 1
+
+
+def test_settings_drive_scheduler_and_observability(tmp_path):
+    import socket as _s
+
+    from polyaxon_amd.obs.events import Stats
+
+    recv = _s.socket(_s.AF_INET, _s.SOCK_DGRAM)
+    recv.bind(("127.0.0.1", 0))
+    recv.settimeout(5)
+    st = Settings.load(env={"PLX_STATS_BACKEND": "datadog", "PLX_STATS_PORT": str(recv.getsockname()[1]),
+                            "PLX_TRACKER_BACKEND": "jsonl", "PLX_SCHEDULER_RECONCILE_INTERVAL_S": "0.5",
+                            "PLX_SCHEDULER_BUILD_REUSE_S": "60"})
+    flow = Polyflow(str(tmp_path / "plx"), allocator=DeviceAllocator([Device(0)]), settings=st)
+    try:
+        assert flow.reconcile_s == 0.5 and flow.build_reuse_s == 60.0
+        flow.auditor.record("project.created", "project", 1, "ann")
+        line = recv.recv(4096).decode()
+        assert line.startswith("polyaxon.project.created:1|c|#") and "service:monolith" in line
+        ev = json.loads((tmp_path / "plx" / "tracker" / "events.jsonl").read_text().splitlines()[0])
+        assert ev["event"] == "project.created" and ev["actor"] == "ann"
+    finally:
+        recv.close()
+    assert Stats(None)._line("a", "1", "c") == "polyaxon.a:1|c"
+
+
+def test_metric_throttle(make_api):
+    c = make_api({"PLX_API_THROTTLE_METRICS_PER_S": "2"})
+    assert c.post("/api/v1/projects", json={"name": "p1"}, headers=_h(TOKEN)).status_code == 201
+    x = c.post("/api/v1/root/p1/experiments", json={"content": {"version": 1, "kind": "experiment",
+                                                               "run": {"cmd": "true"}}}, headers=_h(TOKEN)).json()
+    url = f"/api/v1/root/p1/experiments/{x['id']}/metrics"
+    codes = [c.post(url, json={"values": {"loss": 1.0}}, headers=_h(TOKEN)).status_code for _ in range(4)]
+    assert codes[:2] == [201, 201] and 429 in codes[2:]
+    # a batch is one request: 50 points go through in one call once the bucket refills
+    import time as _t
+    _t.sleep(0.6)
+    r = c.post(url, json=[{"values": {"loss": float(i)}, "step": i} for i in range(50)], headers=_h(TOKEN))
+    assert r.status_code == 201 and r.json()["created"] == 50
