@@ -22,7 +22,7 @@ import torch.nn.functional as F
 
 import ctypes
 
-from polyaxon_amd.ops import _native
+from polyaxon_amd.ops import _native, side_stream
 from polyaxon_amd.ops.conv1x1 import GradMailbox, _bf16_context, _num_cus, _stream, _zero_page, bn_link_of, nt_stats_rows
 from polyaxon_amd.ops.flat import direct_grad
 
@@ -100,13 +100,19 @@ class _ConvK(torch.autograd.Function):
             _native.check(rc, "plx_conv_dgrad")
         if ctx.needs_input_grad[1]:
             cus = _num_cus(x.device)
-            ws = torch.empty(int(lib.plx_conv_wgrad_workspace(n, h, w, cin, cout, k, s, cus)), dtype=torch.float32,
-                             device=x.device)
             direct = ctx.wgrad is not None
             g = ctx.wgrad if direct else torch.empty(cout, k, k, cin, dtype=torch.float32, device=x.device)
-            rc = lib.plx_conv_wgrad(dy.data_ptr(), x.data_ptr(), g.data_ptr(), ws.data_ptr(), n, h, w, cin, cout, k,
-                                    s, zero, cus, int(direct), _stream())
-            _native.check(rc, "plx_conv_wgrad")
+
+            def wgrad():
+                ws = torch.empty(int(lib.plx_conv_wgrad_workspace(n, h, w, cin, cout, k, s, cus)),
+                                 dtype=torch.float32, device=x.device)
+                rc = lib.plx_conv_wgrad(dy.data_ptr(), x.data_ptr(), g.data_ptr(), ws.data_ptr(), n, h, w, cin, cout,
+                                        k, s, zero, cus, int(direct), _stream())
+                _native.check(rc, "plx_conv_wgrad")
+            if direct:  # only the optimizer reads the flat slot: overlap with the data-gradient chain
+                side_stream.run(wgrad, (dy, x), x.device)
+            else:
+                wgrad()
             if not direct:
                 dw = g.permute(0, 3, 1, 2)  # [co][ci][kh][kw] view with channels_last strides
         return dx, dw, None, None, None, None

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from polyaxon_amd.ops import _native
+from polyaxon_amd.ops import _native, side_stream
 from polyaxon_amd.ops.flat import direct_grad
 
 _ZERO: Dict[int, torch.Tensor] = {}
@@ -225,7 +225,8 @@ class _Conv1x1(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             cout = ctx.wshape[0]
             if ctx.wgrad is not None:  # accumulate into the flat gradient slot, autograd sees no weight grad
-                gemm_tn(_rows(dy), _rows(x), out=ctx.wgrad.as_strided((cout, cin), (cin, 1)), accumulate=True)
+                slot = ctx.wgrad.as_strided((cout, cin), (cin, 1))
+                side_stream.run(lambda: gemm_tn(_rows(dy), _rows(x), out=slot, accumulate=True), (dy, x), x.device)
             else:
                 dw = gemm_tn(_rows(dy), _rows(x)).view(ctx.wshape).to(ctx.wdtype)
         return dx, dw, None, None, None, None

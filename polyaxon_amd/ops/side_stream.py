@@ -1,0 +1,62 @@
+"""Weight-gradient GEMMs on a side HIP stream, overlapped with the memory-bound BatchNorm / data-gradient chain.
+
+In a ResNet backward the data gradient of layer L is on the critical path (layer L-1 needs it) while layer L's
+weight gradient is only needed by the optimizer at the end of the step.  The direct-gradient convolutions
+(ops/conv.py, ops/conv1x1.py) hand their weight-gradient launch to :func:`run`: it forks from the current
+stream with an event, runs the launch on the device's side stream, and pins the operand tensors to that stream
+(``record_stream``) so the caching allocator does not recycle them early.  :func:`join`, queued as an autograd
+end-of-backward callback (and called again by the executor before the optimizer), makes the main stream wait
+for every side launch.  Inside hipGraph capture, or with
+``PLX_WGRAD_STREAM=0``, launches run inline.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Dict, Iterable
+
+import torch
+
+_side: Dict[int, "torch.cuda.Stream"] = {}
+_pending: Dict[int, bool] = {}
+
+
+def enabled() -> bool:
+    return os.environ.get("PLX_WGRAD_STREAM", "1") != "0"
+
+
+def _stream_for(dev: torch.device) -> "torch.cuda.Stream":
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _side.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _side[idx] = s
+    return s
+
+
+def run(fn: Callable[[], None], tensors: Iterable[torch.Tensor], dev: torch.device) -> None:
+    if not enabled() or dev.type != "cuda" or torch.cuda.is_current_stream_capturing():
+        fn()
+        return
+    main = torch.cuda.current_stream(dev)
+    side = _stream_for(dev)
+    side.wait_stream(main)  # operands (dy, x) and the gradient slot are ready in main-stream order
+    with torch.cuda.stream(side):
+        fn()
+    for t in tensors:
+        t.record_stream(side)
+    idx = side.device.index
+    if not _pending.get(idx):
+        _pending[idx] = True
+        # join at the end of this backward pass, so every caller (executor, tests, user loops) reads complete
+        # gradients; the executor's explicit join() before the optimizer is then a no-op
+        torch.autograd.Variable._execution_engine.queue_callback(lambda d=dev: join(d))
+
+
+def join(dev: torch.device) -> None:
+    """Main stream waits for every side-stream weight-gradient launch of this device."""
+    if dev.type != "cuda":
+        return
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if _pending.get(idx):
+        torch.cuda.current_stream(dev).wait_stream(_side[idx])
+        _pending[idx] = False

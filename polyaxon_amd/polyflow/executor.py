@@ -29,7 +29,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from polyaxon_amd.ops import _native
+from polyaxon_amd.ops import _native, side_stream
 from polyaxon_amd.ops.flat import FlatParams
 from polyaxon_amd.ops.optim import FusedAdamW, FusedSGD
 
@@ -109,6 +109,7 @@ class ResidentTrialExecutor:
             out = self.model(self.x)
             loss = self.loss_fn(out, self.y)
         loss.backward()
+        side_stream.join(self.device)  # weight-gradient GEMMs overlapped on the side stream (ops/side_stream.py)
         self.opt.step_()
         self._record(loss.detach())
 
