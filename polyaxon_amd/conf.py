@@ -141,6 +141,7 @@ OPTIONS: List[Option] = [
            "(reference dockerizer_scheduler.py:48-50)", minimum=0),
     Option("scheduler.gpus", "int", None, "number of devices to schedule on (default: all visible)", minimum=0),
     Option("scheduler.stop_grace_s", "float", 10.0, "SIGTERM -> SIGKILL grace when stopping runs", minimum=0),
+    Option("scheduler.numa_bind", "bool", True, "pin each replica to the CPUs local to its GPUs"),
     Option("scheduler.clean_after_s", "float", 0.0, "delete outputs of finished runs older than this; 0 = keep",
            minimum=0),
     # auth (reference config_settings/auth.py, registration.py, sso)

@@ -106,7 +106,12 @@ PLX_API int plx_pm_spawn(void* h, char* const* argv, char* const* envp, const ch
   posix_spawnattr_destroy(&attr);
   if (rc != 0) return rc;
   int pfd = pidfd_open(pid);
-  if (pfd < 0) return errno ? errno : -1;
+  if (pfd < 0) {  // cannot supervise it: do not leak an unreaped child
+    const int e = errno ? errno : -1;
+    kill(pid, SIGKILL);
+    waitpid(pid, nullptr, 0);
+    return e;
+  }
   {
     std::lock_guard<std::mutex> lk(m->mu);
     m->fd_to_pid[pfd] = pid;

@@ -19,6 +19,7 @@ Backend ``"nccl"`` is RCCL on ROCm; ``"gloo"`` works for CPU tests.
 """
 from __future__ import annotations
 
+import datetime
 import os
 from typing import List, Optional
 
@@ -43,6 +44,11 @@ def init_from_env(backend: Optional[str] = None, device: Optional[torch.device] 
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {"device_id": device} if backend == "nccl" else {}
+        # collective watchdog: polyflow sets PLX_COLLECTIVE_TIMEOUT_S (+ TORCH_NCCL_ASYNC_ERROR_HANDLING) for
+        # multi-rank trials so a dead peer fails this rank instead of hanging it (polyflow/env.py)
+        timeout = float(os.environ.get("PLX_COLLECTIVE_TIMEOUT_S", "0") or 0)
+        if timeout > 0:
+            kw["timeout"] = datetime.timedelta(seconds=timeout)
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     return {"rank": rank, "world": world, "local_rank": local, "device": device, "backend": backend}
 

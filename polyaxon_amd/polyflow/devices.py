@@ -47,6 +47,43 @@ class Allocation:
     mem_gb: float
 
 
+def parse_cpulist(text: str) -> List[int]:
+    """``"0-3,8,10-11"`` -> [0, 1, 2, 3, 8, 10, 11] (sysfs cpulist format)."""
+    out: List[int] = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        out.extend(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+def device_cpus(index: int, sysfs: str = "/sys") -> Optional[List[int]]:
+    """CPUs local to HIP device ``index`` (the NUMA node of its PCIe root), read from the KFD topology (GPU nodes
+    in enumeration order -> ``drm_render_minor``) and DRM sysfs -- no GPU runtime call, so the scheduler can
+    use it before any trial starts.  None when the topology is not readable."""
+    import glob
+
+    gpus = []
+    paths = glob.glob(os.path.join(sysfs, "class", "kfd", "kfd", "topology", "nodes", "*", "properties"))
+    for p in sorted(paths, key=lambda s: int(os.path.basename(os.path.dirname(s)))):
+        try:
+            with open(p) as f:
+                props = dict(line.split(None, 1) for line in f.read().splitlines() if " " in line)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) > 0:
+            gpus.append(props.get("drm_render_minor", "").strip())
+    if index >= len(gpus) or not gpus[index]:
+        return None
+    try:
+        with open(os.path.join(sysfs, "class", "drm", f"renderD{gpus[index]}", "device", "local_cpulist")) as f:
+            cpus = parse_cpulist(f.read())
+    except (OSError, ValueError):
+        return None
+    return cpus or None
+
+
 def detect_devices() -> List[Device]:
     """Visible HIP devices without initialising the GPU runtime (``device_count`` only)."""
     n = os.environ.get("PLX_NUM_GPUS")

@@ -113,6 +113,13 @@ def trial_env(*, base_env: Optional[Dict[str, str]] = None, experiment: Dict[str
     env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devices)
     env["LOCAL_RANK"] = str(local_rank)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    n_ranks = sum(len(v) for v in cluster.values()) if cluster else 1
+    if n_ranks > 1:
+        # RCCL watchdog: a rank that dies or hangs inside a collective tears the process group
+        # down after PLX_COLLECTIVE_TIMEOUT_S (parallel/ddp.init_from_env) instead of blocking its peers forever;
+        # the scheduler then sees the failure and tears down the surviving ranks.
+        env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        env.setdefault("PLX_COLLECTIVE_TIMEOUT_S", "600")
     if not devices:
         env["PLX_CPU_ONLY"] = "1"
     return env

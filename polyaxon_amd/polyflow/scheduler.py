@@ -24,6 +24,8 @@ import heapq
 import json
 import logging
 import os
+import shlex
+import shutil
 import signal
 import sys
 import threading
@@ -36,7 +38,7 @@ from typing import Any, Callable, Deque, Dict, List, Optional, Tuple
 
 from polyaxon_amd.fsm import ExperimentLifeCycle, JobLifeCycle
 from polyaxon_amd.obs.events import Auditor
-from polyaxon_amd.polyflow.devices import DeviceAllocator
+from polyaxon_amd.polyflow.devices import DeviceAllocator, device_cpus
 from polyaxon_amd.polyflow.env import cluster_def as make_cluster_def
 from polyaxon_amd.polyflow.env import free_port, trial_env
 from polyaxon_amd.polyflow.faults import parse_fault
@@ -104,6 +106,26 @@ def _replica_gpus(spec: BaseSpecification, role: str, index: int) -> float:
     return float(res.gpu.value)
 
 
+_SHELL_OPS = ("&&", "||", ";", "|", ">", "<", "`", "$(", "\n")
+
+
+def profile_argv(cmd: str, out_dir: str) -> Optional[List[str]]:
+    """``rocprofv3 --kernel-trace --stats ... -- <argv>`` for a plain command line, else None.  The profiler must
+    start the program itself (its preloaded library initialises the GPU first, so a shell or env wrapper that
+    later execs the program is not allowed): commands with shell operators or leading ``VAR=`` assignments are
+    run unprofiled."""
+    if any(op in cmd for op in _SHELL_OPS):
+        return None
+    try:
+        argv = shlex.split(cmd)
+    except ValueError:
+        return None
+    if not argv or "=" in argv[0]:
+        return None
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    return [exe, "--kernel-trace", "--stats", "--output-format", "csv", "-d", out_dir, "-o", "trial", "--", *argv]
+
+
 def _command(spec: BaseSpecification) -> str:
     if spec.run is None:
         raise PolyaxonfileError("nothing to run: the specification has no `run.cmd`")
@@ -124,6 +146,7 @@ class Polyflow:
             reconcile_s = settings.get("scheduler.reconcile_interval_s") if reconcile_s == 5.0 else reconcile_s
             stop_grace_s = settings.get("scheduler.stop_grace_s") if stop_grace_s == 10.0 else stop_grace_s
         self.settings = settings
+        self.numa_bind = settings.get("scheduler.numa_bind") if settings is not None else True
         self.build_reuse_s = settings.get("scheduler.build_reuse_s") if settings is not None else BUILD_REUSE_S
         self.paths = Paths(root)
         self.clean_on_start = clean_on_start
@@ -414,6 +437,22 @@ class Polyflow:
         brun.on_done.append(release)
         return brun.id
 
+    @staticmethod
+    def _bind_cpus(pid: int, devs: List[int]) -> None:
+        """Pin a replica to the CPUs local to its GPUs (NUMA-near host threads for the HIP
+        runtime, RCCL proxies and data loading).  Set right after spawn; the trial's own children inherit it."""
+        cpus = set()
+        for d in devs:
+            cpus.update(device_cpus(d) or [])
+        if not cpus:
+            return
+        try:
+            target = cpus & os.sched_getaffinity(0)
+            if target:
+                os.sched_setaffinity(pid, target)
+        except OSError:
+            pass
+
     def _project_id(self, run: Run) -> int:
         rec = self.store.get_experiment(run.id) if run.kind == "experiment" else self.store.get_job(run.id)
         return rec["project_id"]
@@ -578,8 +617,16 @@ class Polyflow:
                 env["POLYAXON_JOB_INFO"] = json.dumps({"job_id": rec["id"], "job_uuid": rec["uuid"],
                                                        "kind": spec.kind, "project_name": proj["name"]})
             log_path = self.paths.replica_log(rec["logs_path"], role, idx)
+            argv = ["/bin/bash", "-c", cmd]
+            if spec.environment is not None and spec.environment.profile and rec.get("outputs_path"):
+                prof = profile_argv(cmd, os.path.join(rec["outputs_path"], "rocprof", f"{role}.{idx}"))
+                if prof is not None:
+                    argv = prof
+                else:
+                    with open(log_path, "a") as f:
+                        f.write("[polyflow] environment.profile: command uses shell syntax, running unprofiled\n")
             try:
-                pid = self.pm.spawn(["/bin/bash", "-c", cmd], env, cwd=run.cwd, log_path=log_path)
+                pid = self.pm.spawn(argv, env, cwd=run.cwd, log_path=log_path)
             except OSError as e:
                 rep.done = True
                 self._replica_status(run, rep, "failed", f"spawn failed: {e}")
@@ -587,6 +634,8 @@ class Polyflow:
                 self._maybe_finalize(run)
                 return
             rep.pid = pid
+            if devs and self.numa_bind:
+                self._bind_cpus(pid, devs)
             self.pid_index[pid] = (run.owner, len(run.replicas) - 1)
             self.stats["spawned"] += 1
             if self._last_exit_t is not None:
@@ -708,7 +757,10 @@ class Polyflow:
     # ================================================================== failure handling
     def _max_restarts(self, run: Run) -> int:
         env = getattr(run.spec, "environment", None)
-        return int(getattr(env, "max_restarts", 0) or 0) if run.kind == "experiment" else 0
+        if run.kind != "experiment":
+            return 0
+        n = int(getattr(env, "max_restarts", 0) or 0)
+        return n or (int(self.settings.get("scheduler.max_restarts")) if self.settings is not None else 0)
 
     def _maybe_retry(self, run: Run) -> bool:
         """Opt-in retry: a failed experiment is re-queued whole (all replicas, fresh rendezvous port) up to
@@ -761,6 +813,8 @@ class Polyflow:
                     continue
                 env = run.spec.environment
                 timeout = getattr(env, "heartbeat_timeout", None) if env else None
+                if not timeout and self.settings is not None:
+                    timeout = self.settings.get("scheduler.heartbeat_timeout_s") or None
                 if not timeout:
                     continue
                 last = self.store.kv_get(f"heartbeat:experiment:{run.id}")
@@ -773,6 +827,14 @@ class Polyflow:
             if self.health_check is not None:
                 for idx in self.health_check() or []:
                     self.alloc.mark_unhealthy(idx)
+            keep = self.settings.get("scheduler.clean_after_s") if self.settings is not None else 0
+            if keep and now - getattr(self, "_last_clean", 0.0) > 600.0:  # outputs retention, at most every 10 min
+                from polyaxon_amd.polyflow.cleaning import clean_outputs
+
+                self._last_clean = now
+                removed = clean_outputs(self.store, keep)
+                if removed:
+                    log.info("outputs retention removed %d paths", len(removed))
         except Exception:
             log.exception("reconcile failed")
         finally:

@@ -187,6 +187,8 @@ class EnvironmentSpec:
     # MI355X extensions: opt-in trial retry and a heartbeat deadline for hung trials
     max_restarts: int = 0
     heartbeat_timeout: Optional[float] = None
+    # wrap every replica in `rocprofv3 --kernel-trace --stats` (outputs/rocprof/<role>.<index>)
+    profile: bool = False
 
     @classmethod
     def from_dict(cls, d: Optional[Dict[str, Any]]):
@@ -195,10 +197,12 @@ class EnvironmentSpec:
         if len(fws) > 1:
             raise MatrixValidationError(f"environment defines more than one framework: {fws}")
         known = {"resources", "outputs", "persistence", "node_selector", "tolerations", "affinity", "secret_refs",
-                 "configmap_refs", "env_vars", "max_restarts", "heartbeat_timeout", *FRAMEWORKS}
+                 "configmap_refs", "env_vars", "max_restarts", "heartbeat_timeout", "profile", *FRAMEWORKS}
         unknown = set(d) - known
         if unknown:
             raise MatrixValidationError(f"unknown environment keys {sorted(unknown)}")
+        if not isinstance(d.get("profile", False), bool):
+            raise MatrixValidationError("environment.profile must be true or false")
         outputs = d.get("outputs") or {}
         bad = set(outputs) - {"jobs", "experiments"}
         if bad:
@@ -210,7 +214,8 @@ class EnvironmentSpec:
                    env_vars=[list(e) for e in d.get("env_vars") or []],
                    framework=FrameworkSpec.from_dict(fws[0], d[fws[0]]) if fws else None,
                    max_restarts=int(d.get("max_restarts") or 0),
-                   heartbeat_timeout=float(d["heartbeat_timeout"]) if d.get("heartbeat_timeout") else None)
+                   heartbeat_timeout=float(d["heartbeat_timeout"]) if d.get("heartbeat_timeout") else None,
+                   profile=bool(d.get("profile", False)))
 
     def to_dict(self):
         out: Dict[str, Any] = {}
@@ -228,4 +233,6 @@ class EnvironmentSpec:
             out["max_restarts"] = self.max_restarts
         if self.heartbeat_timeout:
             out["heartbeat_timeout"] = self.heartbeat_timeout
+        if self.profile:
+            out["profile"] = True
         return out
