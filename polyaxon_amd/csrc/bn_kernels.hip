@@ -134,20 +134,45 @@ __global__ __launch_bounds__(256) void bn_partial_reduce_kernel(const float* __r
   }
 }
 
-__global__ void bn_fwd_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq, int nblk,
+// Level-2 -> per-channel totals for the finalize kernels: block = 64 channels x 4 split lanes-groups, each group
+// sums every 4th of the S partial rows (independent loads, fp64 accumulation), then the 4 group sums are combined
+// through LDS in a fixed order (deterministic).  One thread per channel walking all S rows serially was 19 us per
+// backward BatchNorm on the 56x56 layers (S ~ 100 dependent-latency iterations on a single 256-thread block).
+constexpr int kFinSplit = 4;
+__device__ __forceinline__ bool fin_sum2(const float* __restrict__ pa, const float* __restrict__ pb, int nblk, int C,
+                                         double& A, double& B) {
+  __shared__ double sh[2][kFinSplit][64];
+  const int lc = threadIdx.x & 63, sp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  double a0 = 0.0, b0 = 0.0, a1 = 0.0, b1 = 0.0;
+  if (c < C) {
+    int b = sp;
+    for (; b + kFinSplit < nblk; b += 2 * kFinSplit) {
+      const float x0 = pa[(int64_t)b * C + c], y0 = pb[(int64_t)b * C + c];
+      const float x1 = pa[(int64_t)(b + kFinSplit) * C + c], y1 = pb[(int64_t)(b + kFinSplit) * C + c];
+      a0 += x0; b0 += y0; a1 += x1; b1 += y1;
+    }
+    if (b < nblk) { a0 += pa[(int64_t)b * C + c]; b0 += pb[(int64_t)b * C + c]; }
+  }
+  sh[0][sp][lc] = a0 + a1;
+  sh[1][sp][lc] = b0 + b1;
+  __syncthreads();
+  if (sp != 0 || c >= C) return false;
+  A = ((sh[0][0][lc] + sh[0][1][lc]) + sh[0][2][lc]) + sh[0][3][lc];
+  B = ((sh[1][0][lc] + sh[1][1][lc]) + sh[1][2][lc]) + sh[1][3][lc];
+  return true;
+}
+
+__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq, int nblk,
                                        const uint16_t* __restrict__ x_row0, int C, int64_t M,
                                        const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
                                        float momentum, float* __restrict__ running_mean,
                                        float* __restrict__ running_var, float* __restrict__ save_mean,
                                        float* __restrict__ save_invstd, float* __restrict__ scale,
                                        float* __restrict__ bias) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double S = 0.0, Q = 0.0;  // <= 32 level-2 partials per channel, summed in fp64
-  for (int b = 0; b < nblk; ++b) {
-    S += psum[(int64_t)b * C + c];
-    Q += psq[(int64_t)b * C + c];
-  }
+  double S, Q;  // level-2 partials per channel, summed in fp64
+  if (!fin_sum2(psum, psq, nblk, C, S, Q)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const double m = S / (double)M;
   double var = Q / (double)M - m * m;
   if (var < 0.0) var = 0.0;
@@ -271,17 +296,13 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const bf16x8* __r
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ pdz, const float* __restrict__ pdzx, int nblk, int C,
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ pdz, const float* __restrict__ pdzx, int nblk, int C,
                                        int64_t M, const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ invstd, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta, float* __restrict__ coef, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double A = 0.0, B = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    A += pdz[(int64_t)b * C + c];
-    B += pdzx[(int64_t)b * C + c];
-  }
+  double A, B;
+  if (!fin_sum2(pdz, pdzx, nblk, C, A, B)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const float db = (float)A, dg = (float)B;
   // accumulate: dgamma / dbeta are the parameters' own (flat) gradient slots, summed into like autograd would
   dbeta[c] = accumulate ? dbeta[c] + db : db;
@@ -385,7 +406,7 @@ PLX_API int plx_bn_forward(const void* x, const void* res, void* y, int64_t M, i
   float* l2 = partials + 2 * (int64_t)p.nblk * C;
   hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, p.S, 2), dim3(256), 0, stream, partials, p.nblk, C,
                      l2, p.S);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, l2, l2 + (int64_t)p.S * C, p.S,
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)p.S * C, p.S,
                      (const uint16_t*)x, C, M, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
                      save_invstd, scale_bias, scale_bias + C);
   const int64_t n_vec = M * p.G;
@@ -412,7 +433,7 @@ PLX_API int plx_bn_forward_from_partials(const void* x, const void* res, void* y
   const int S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
   hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, S, 2), dim3(256), 0, stream, partials, nblk, C, l2,
                      S);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S,
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S,
                      (const uint16_t*)nullptr, C, M, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
                      save_invstd, scale_bias, scale_bias + C);
   const int64_t n_vec = M * p.G;
@@ -446,7 +467,7 @@ PLX_API int plx_bn_backward(const void* x, const uint8_t* mask, const void* dy, 
   float* l2 = partials + 2 * (int64_t)p.nblk * C;
   hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, p.S, 2), dim3(256), 0, stream, partials, p.nblk, C,
                      l2, p.S);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, l2, l2 + (int64_t)p.S * C, p.S, C, M,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)p.S * C, p.S, C, M,
                      gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
   const int64_t n_vec = M * p.G;
   hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
@@ -467,7 +488,7 @@ PLX_API int plx_bn_backward_from_partials(const void* x, const uint8_t* mask, co
   const int S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
   hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, S, 2), dim3(256), 0, stream, partials, nblk, C, l2,
                      S);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S, C,
                      M, gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
   const int64_t n_vec = M * p.G;
   hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
