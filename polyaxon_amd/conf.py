@@ -139,6 +139,11 @@ OPTIONS: List[Option] = [
            minimum=0),
     Option("scheduler.build_reuse_s", "float", 6 * 3600.0, "built-environment reuse window "
            "(reference dockerizer_scheduler.py:48-50)", minimum=0),
+    Option("build.backend", "str", "native", "build jobs: native environment dir, container image (docker/podman), "
+           "or auto (container when an engine is installed)", choices=("native", "container", "auto")),
+    Option("build.registry", "str", "localhost:5000", "image registry prefix for container builds "
+           "(reference REGISTRY_HOST, docker_images/image_info.py:68-80)"),
+    Option("build.push", "bool", False, "push container builds to build.registry"),
     Option("scheduler.gpus", "int", None, "number of devices to schedule on (default: all visible)", minimum=0),
     Option("scheduler.stop_grace_s", "float", 10.0, "SIGTERM -> SIGKILL grace when stopping runs", minimum=0),
     Option("scheduler.numa_bind", "bool", True, "pin each replica to the CPUs local to its GPUs"),

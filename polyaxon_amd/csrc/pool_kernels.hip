@@ -24,18 +24,20 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// Grid: x = 8-channel groups of one image row (256 per block), y = image rows (n, h) with a stride loop.  All
+// index math is 32-bit and the row split is per block (scalar): the first version decoded a flat int64 element
+// index with three 64-bit div/mods per thread, which made the stem-pool backward ALU-bound (380 us against a
+// ~100 us HBM floor on 256x112x112x64).
+
 // one thread = 8 channels of one output pixel
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16x8* __restrict__ x, bf16x8* __restrict__ y,
                                                           u8x8* __restrict__ idx, int N, int H, int W, int G, int OH,
                                                           int OW) {
-  const int64_t total = (int64_t)N * OH * OW * G;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int g = (int)(t % G);
-    int64_t p = t / G;
-    const int ow = (int)(p % OW);
-    p /= OW;
-    const int oh = (int)(p % OH);
-    const int n = (int)(p / OH);
+  const unsigned j = blockIdx.x * 256u + threadIdx.x;
+  if (j >= (unsigned)(OW * G)) return;
+  const unsigned g = j % (unsigned)G, ow = j / (unsigned)G;
+  for (int row = blockIdx.y; row < N * OH; row += gridDim.y) {
+    const int n = row / OH, oh = row - n * OH;
     float best[8];
     uint8_t arg[8];
 #pragma unroll
@@ -47,11 +49,12 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16x8* __restri
     for (int kh = 0; kh < 3; ++kh) {
       const int ih = oh * 2 - 1 + kh;
       if (ih < 0 || ih >= H) continue;
+      const bf16x8* xr = x + ((size_t)(n * H + ih) * W) * G + g;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        const int iw = ow * 2 - 1 + kw;
+        const int iw = (int)ow * 2 - 1 + kw;
         if (iw < 0 || iw >= W) continue;
-        const bf16x8 v = x[(((int64_t)n * H + ih) * W + iw) * G + g];
+        const bf16x8 v = xr[(size_t)iw * G];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float f = bf2f(v.v[k]);
@@ -69,59 +72,69 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16x8* __restri
       o.v[k] = f2bf(best[k]);
       a.v[k] = arg[k];
     }
+    const size_t t = (size_t)row * OW * G + j;
     y[t] = o;
     idx[t] = a;
   }
 }
 
-// one thread = 8 channels of one input pixel
+// one thread = 8 channels of one input pixel.  Input row ih is covered by output rows oh = (ih+1-kh)/2 for the
+// kh in 0..2 of matching parity: ih even -> (ih/2, kh=1); ih odd -> ((ih+1)/2, kh=0) and ((ih-1)/2, kh=2).
+__device__ __forceinline__ int pool_cover(int i, int O, int* o, int* k) {
+  int n = 0;
+  if (i & 1) {
+    if ((i + 1) >> 1 < O) { o[n] = (i + 1) >> 1; k[n++] = 0; }
+    o[n] = (i - 1) >> 1; k[n++] = 2;
+  } else if ((i >> 1) < O) {
+    o[n] = i >> 1; k[n++] = 1;
+  }
+  return n;
+}
+
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16x8* __restrict__ dy, const u8x8* __restrict__ idx,
                                                           bf16x8* __restrict__ dx, int N, int H, int W, int G, int OH,
                                                           int OW) {
-  const int64_t total = (int64_t)N * H * W * G;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
-    const int g = (int)(t % G);
-    int64_t p = t / G;
-    const int iw = (int)(p % W);
-    p /= W;
-    const int ih = (int)(p % H);
-    const int n = (int)(p / H);
+  const unsigned j = blockIdx.x * 256u + threadIdx.x;
+  if (j >= (unsigned)(W * G)) return;
+  const unsigned g = j % (unsigned)G;
+  const int iw = (int)(j / (unsigned)G);
+  int ows[2], kws[2];
+  const int nw = pool_cover(iw, OW, ows, kws);
+  for (int row = blockIdx.y; row < N * H; row += gridDim.y) {
+    const int n = row / H, ih = row - n * H;
+    int ohs[2], khs[2];
+    const int nh = pool_cover(ih, OH, ohs, khs);
     float acc[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-    // ih = 2*oh - 1 + kh  =>  oh = (ih + 1 - kh) / 2 for kh in 0..2 with (ih + 1 - kh) even
-    const int oh_hi = (ih + 1) >> 1, oh_lo = ih >= 1 ? (ih) >> 1 : 0;
-    const int ow_hi = (iw + 1) >> 1, ow_lo = iw >= 1 ? (iw) >> 1 : 0;
-    for (int oh = oh_lo; oh <= oh_hi && oh < OH; ++oh) {
-      const int kh = ih + 1 - 2 * oh;
-      if (kh < 0 || kh > 2) continue;
-      for (int ow = ow_lo; ow <= ow_hi && ow < OW; ++ow) {
-        const int kw = iw + 1 - 2 * ow;
-        if (kw < 0 || kw > 2) continue;
-        const int64_t o = (((int64_t)n * OH + oh) * OW + ow) * G + g;
-        const u8x8 a = idx[o];
-        const uint8_t me = (uint8_t)(kh * 3 + kw);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      if (a >= nh) break;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if (b >= nw) break;
+        const size_t o = ((size_t)(n * OH + ohs[a]) * OW + ows[b]) * G + g;
+        const u8x8 am = idx[o];
+        const uint8_t me = (uint8_t)(khs[a] * 3 + kws[b]);
         bool any = false;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) any |= a.v[k] == me;
+        for (int k = 0; k < 8; ++k) any |= am.v[k] == me;
         if (!any) continue;
         const bf16x8 d = dy[o];
 #pragma unroll
         for (int k = 0; k < 8; ++k)
-          if (a.v[k] == me) acc[k] += bf2f(d.v[k]);
+          if (am.v[k] == me) acc[k] += bf2f(d.v[k]);
       }
     }
     bf16x8 out;
 #pragma unroll
     for (int k = 0; k < 8; ++k) out.v[k] = f2bf(acc[k]);
-    dx[t] = out;
+    dx[(size_t)row * W * G + j] = out;
   }
 }
 
-inline int grid_for(int64_t total) {
-  int64_t g = (total + 255) / 256;
-  if (g > 8192) g = 8192;
-  return (int)(g < 1 ? 1 : g);
+inline dim3 grid_for(int row_elems, int rows) {
+  return dim3((row_elems + 255) / 256, rows < 65535 ? rows : 65535);
 }
 
 }  // namespace
@@ -129,7 +142,7 @@ inline int grid_for(int64_t total) {
 PLX_API int plx_maxpool3s2_forward(const void* x, void* y, void* idx, int N, int H, int W, int C, hipStream_t s) {
   if (C % 8 || N <= 0 || H <= 0 || W <= 0) return 1;
   const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1, G = C / 8;
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((int64_t)N * OH * OW * G)), dim3(256), 0, s,
+  hipLaunchKernelGGL(maxpool_fwd_kernel, grid_for(OW * G, N * OH), dim3(256), 0, s,
                      (const bf16x8*)x, (bf16x8*)y, (u8x8*)idx, N, H, W, G, OH, OW);
   return (int)hipGetLastError();
 }
@@ -138,7 +151,7 @@ PLX_API int plx_maxpool3s2_backward(const void* dy, const void* idx, void* dx, i
                                     hipStream_t s) {
   if (C % 8 || N <= 0 || H <= 0 || W <= 0) return 1;
   const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1, G = C / 8;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((int64_t)N * H * W * G)), dim3(256), 0, s,
+  hipLaunchKernelGGL(maxpool_bwd_kernel, grid_for(W * G, N * H), dim3(256), 0, s,
                      (const bf16x8*)dy, (const u8x8*)idx, (bf16x8*)dx, N, H, W, G, OH, OW);
   return (int)hipGetLastError();
 }

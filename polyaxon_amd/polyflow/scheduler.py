@@ -38,6 +38,7 @@ from typing import Any, Callable, Deque, Dict, List, Optional, Tuple
 
 from polyaxon_amd.fsm import ExperimentLifeCycle, JobLifeCycle
 from polyaxon_amd.obs.events import Auditor
+from polyaxon_amd.polyflow import dockerizer
 from polyaxon_amd.polyflow.devices import DeviceAllocator, device_cpus
 from polyaxon_amd.polyflow.env import cluster_def as make_cluster_def
 from polyaxon_amd.polyflow.env import free_port, trial_env
@@ -148,6 +149,9 @@ class Polyflow:
         self.settings = settings
         self.numa_bind = settings.get("scheduler.numa_bind") if settings is not None else True
         self.build_reuse_s = settings.get("scheduler.build_reuse_s") if settings is not None else BUILD_REUSE_S
+        self.build_backend = settings.get("build.backend") if settings is not None else "native"
+        self.build_registry = settings.get("build.registry") if settings is not None else dockerizer.DEFAULT_REGISTRY
+        self.build_push = settings.get("build.push") if settings is not None else False
         self.paths = Paths(root)
         self.clean_on_start = clean_on_start
         self.store_path = os.path.join(self.paths.root, "polyaxon.sqlite")
@@ -402,7 +406,8 @@ class Polyflow:
     def _build_hash(self, spec: BaseSpecification, cwd: str) -> str:
         b = spec.build
         h = hashlib.sha256(json.dumps({"image": b.image, "steps": b.build_steps, "env": b.env_vars,
-                                       "ref": b.ref, "cwd": cwd}, sort_keys=True).encode())
+                                       "dockerfile": b.dockerfile, "ref": b.ref, "cwd": cwd},
+                                      sort_keys=True).encode())
         return h.hexdigest()[:20]
 
     def _ensure_build(self, spec: BaseSpecification, dependent: Run) -> Optional[int]:
@@ -487,11 +492,29 @@ class Polyflow:
             self._enqueue(run)
         return jid
 
+    def _build_command(self, run: Run) -> str:
+        """Dockerizer equivalent (polyflow/dockerizer.py): the Dockerfile is always rendered into the build's
+        environment directory; the command either runs the steps natively or builds the image."""
+        b = run.spec.build
+        rec = self.store.get_job(run.id)
+        env_dir = rec["outputs_path"]
+        backend = dockerizer.resolve_backend(self.build_backend)
+        dockerfile = os.path.join(run.cwd, b.dockerfile) if b.dockerfile else None
+        if b.image:
+            written = dockerizer.write_dockerfile(env_dir, b.image, b.build_steps, b.env_vars, run.cwd)
+            dockerfile = dockerfile or written
+        if backend == "native":
+            return dockerizer.native_build_command(b.build_steps)
+        proj = self.store.get("projects", rec["project_id"])
+        tag = dockerizer.tagged_image(proj["name"], proj["id"], run.extra_env.get("PLX_BUILD_HASH") or str(run.id),
+                                      self.build_registry)
+        self.store.update_job(run.id, image=tag)
+        return dockerizer.container_build_command(dockerfile, run.cwd, tag, nocache=b.nocache, push=self.build_push)
+
     def _job_command(self, run: Run) -> str:
         spec = run.spec
         if spec.kind == Kinds.BUILD:
-            steps = spec.build.build_steps or ["true"]
-            return " && ".join(steps)
+            return self._build_command(run)
         if spec.kind == Kinds.NOTEBOOK:
             return (f"{self.python} -m jupyter lab --no-browser --ip=127.0.0.1 --port={run.port} "
                     f"--NotebookApp.token={uuid.uuid4().hex} --notebook-dir={run.cwd}")

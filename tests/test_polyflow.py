@@ -254,6 +254,60 @@ def test_jobs_and_builds(tmp_path):
         builds = flow.store.list_jobs(kind="build")
         assert len(builds) == 1  # second experiment reused the build (6 h window)
         assert "built" in flow.logs("experiment", x2["id"])
+        # the rendered Dockerfile lands in the build's environment directory (reproducible as an image)
+        dockerfile = open(os.path.join(builds[0]["outputs_path"], "Dockerfile")).read()
+        assert dockerfile.startswith("FROM rocm/pytorch\n")
+        assert "RUN echo built > $PLX_BUILD_DIR/marker" in dockerfile
+    finally:
+        flow.shutdown()
+
+
+def test_dockerfile_and_image_naming(tmp_path):
+    from polyaxon_amd.polyflow import dockerizer
+
+    (tmp_path / "requirements.txt").write_text("numpy\n")
+    text = dockerizer.render_dockerfile("rocm/pytorch:latest", ["pip install -r requirements.txt", "make"],
+                                        [["LR", "0.1"], ["MSG", "two words"]], context=str(tmp_path))
+    lines = text.splitlines()
+    assert lines[0] == "FROM rocm/pytorch:latest"
+    assert "ENV LR=0.1" in lines and 'ENV MSG="two words"' in lines
+    # manifests are copied before the steps (cache-friendly), the code after them
+    assert lines.index("COPY requirements.txt /code/") < lines.index("RUN pip install -r requirements.txt")
+    assert lines.index("RUN make") < lines.index("COPY . /code")
+    assert dockerizer.tagged_image("MyProj", 7, "abc") == "localhost:5000/myproj_7:abc"
+    assert dockerizer.resolve_backend("native") == "native"
+    with pytest.raises(ValueError):
+        dockerizer.resolve_backend("kaniko")
+    with pytest.raises(ValueError):
+        dockerizer.render_dockerfile("", [])
+
+
+def test_container_build_backend(tmp_path, monkeypatch):
+    """build.backend=container: the scheduler builds the rendered Dockerfile with the engine on PATH (a fake
+    docker here that records its argv) and records the tagged image on the build job."""
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    argv_log = tmp_path / "docker_argv"
+    fake = bindir / "docker"
+    fake.write_text(f"#!/bin/sh\necho \"$@\" >> {argv_log}\n")
+    fake.chmod(0o755)
+    monkeypatch.setenv("PATH", f"{bindir}:{os.environ['PATH']}")
+    from polyaxon_amd.polyflow import dockerizer
+
+    assert dockerizer.resolve_backend("auto") == "container"
+    flow = _flow(tmp_path)
+    flow.build_backend, flow.build_push = "container", True
+    try:
+        spec = _xp("true")
+        spec["build"] = {"image": "rocm/pytorch", "build_steps": ["pip install einops"], "nocache": True}
+        x = flow.submit(spec)
+        assert flow.wait("experiment", x["id"], timeout=30) == "succeeded"
+        b = flow.store.list_jobs(kind="build")[0]
+        assert b["image"].startswith("localhost:5000/") and ":" in b["image"].split("/", 1)[1]
+        calls = argv_log.read_text().splitlines()
+        assert calls[0].startswith(f"build -t {b['image']} -f ") and "--no-cache" in calls[0]
+        assert calls[0].split(" -f ")[1].split()[0].endswith("Dockerfile")
+        assert calls[1] == f"push {b['image']}"
     finally:
         flow.shutdown()
 
