@@ -104,27 +104,37 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16x8* __restri
     const int n = row / H, ih = row - n * H;
     int ohs[2], khs[2];
     const int nh = pool_cover(ih, OH, ohs, khs);
-    float acc[8];
+    // all (<= 4) covering windows' argmax bytes and dy vectors are loaded up front as independent loads (a
+    // missing window re-reads a valid one and is masked out): the load -> test -> dependent-load chain per
+    // window left the kernel latency-bound at ~1.4 TB/s
+    size_t off[4];
+    bool valid[4];
+    uint8_t me[4];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-#pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      if (a >= nh) break;
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        if (b >= nw) break;
-        const size_t o = ((size_t)(n * OH + ohs[a]) * OW + ows[b]) * G + g;
-        const u8x8 am = idx[o];
-        const uint8_t me = (uint8_t)(khs[a] * 3 + kws[b]);
-        bool any = false;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) any |= am.v[k] == me;
-        if (!any) continue;
-        const bf16x8 d = dy[o];
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (am.v[k] == me) acc[k] += bf2f(d.v[k]);
+        const int q = a * 2 + b;
+        valid[q] = a < nh && b < nw;
+        const int oh = ohs[a < nh ? a : 0], ow = ows[b < nw ? b : 0];
+        off[q] = ((size_t)(n * OH + oh) * OW + ow) * G + g;
+        me[q] = (uint8_t)(khs[a < nh ? a : 0] * 3 + kws[b < nw ? b : 0]);
       }
+    u8x8 am[4];
+    bf16x8 d[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      am[q] = idx[off[q]];
+      d[q] = dy[off[q]];
+    }
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (valid[q] && am[q].v[k] == me[q]) v += bf2f(d[q].v[k]);
+      acc[k] = v;
     }
     bf16x8 out;
 #pragma unroll
