@@ -72,6 +72,8 @@ def parse_scalar(expr: str, number=True) -> Tuple[bool, str, Any]:
     if neg:
         expr = expr[1:].strip()
     m = _SCALAR.match(expr)
+    if m is None:
+        raise QueryError("empty scalar condition")
     op = m.group(1) or "="
     raw = m.group(2).strip()
     val = _parse_number(raw) if number else raw
@@ -96,6 +98,8 @@ def parse_datetime_op(expr: str) -> Tuple[bool, str, Any]:
         a, b = [p.strip() for p in expr.split("..", 1)]
         return neg, "range", (parse_datetime(a), parse_datetime(b))
     m = _SCALAR.match(expr)
+    if m is None:
+        raise QueryError("empty datetime condition")
     op = m.group(1) or "="
     return neg, op, parse_datetime(m.group(2))
 
