@@ -2,17 +2,26 @@
 """Headline benchmark: HPO trials/hour (whole node) + wall-clock-to-target, ResNet-50 Hyperband sweep.
 
 BASELINE.json config 3 ("Hyperband/ASHA sweep of ResNet-50 on synthetic ImageNet-shape data, 8×MI355X,
-64 brackets").  One rank per GPU (torchrun); every rank is a resident polyflow trial executor running its
-own Hyperband brackets (brackets are independent successive-halving runs, so they are spread over GPUs
-with no cross-GPU barrier; weak scaling: per-GPU work is fixed as N grows).
+64 brackets"), measured through the real control plane:
 
-A benchmark "step" is ONE trial = one Polyaxon experiment: a ResNet-50 config trained for its rung's
-resource (1 resource unit = ``--unit-steps`` full training steps: bf16 forward + backward + fused SGD
-update at ``--batch`` 224×224 images), with fresh random weights (restart) or its HBM snapshot (resume
-promotion), its metric reduced on the device, and the rung's top-k decided by the HIP kernel.  The timed
-region is exactly K trials per rank after W untimed warm-up trials; value = N·K / max-rank-time · 3600.
+* one rank per GPU (``torchrun``, or ``--gpus N`` spawns the N ranks itself before anything touches a GPU);
+  every rank builds a **resident trial executor** (polyflow/resident.py) for the ResNet-50 program and
+  attaches it to the **polyflow scheduler** that rank 0 runs (SQLite store, FSMs, group drivers);
+* the timed work is ``--steps K`` complete Hyperband sweeps **per GPU**: rank 0 submits ``K × N`` Polyaxonfile
+  groups (``hyperband: max_iter 9, eta 3, resume: true``; 3 brackets and 23 trials each, reference-exact
+  bracket arithmetic) with ``environment.executor: resident``; the scheduler spreads their ``3·K·N`` brackets
+  over the N executors (``--steps 3`` at 8 GPUs = 72 brackets, ``--steps 20`` = 480), every executor interleaves
+  its brackets and decides each round's promotions with one HIP top-k launch, and every trial is an experiment
+  row with its status history, metric and RESUME lineage.  The timed region starts after a barrier (after
+  ``--warmup W`` untimed sweeps per GPU through the same path) and ends when every group has SUCCEEDED and
+  every rank passed the final barrier: only whole sweeps are timed, never a prefix;
+* one Hyperband resource unit = ``--unit-steps`` full training steps (bf16 forward + backward + fused SGD) at
+  ``--batch`` 224×224 images; the data is a fresh, learnable synthetic batch generated on the device every step
+  (ops/synth.py), so ``wall_clock_to_target_s`` (first trial whose committed loss is below ``--target``,
+  measured from the start of the timed region) reflects real learning, not memorisation.
 
-Data: synthetic ImageNet-shape tensors, random-init weights (no datasets / checkpoints available).
+``value`` = trials completed in the timed region (all GPUs) / elapsed (max over ranks) × 3600.
+Data: synthetic ImageNet-shape tensors generated on the device, random-init weights (no datasets available).
 """
 from __future__ import annotations
 
@@ -20,186 +29,319 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
+import tempfile
+import threading
 import time
-
-import torch
-import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-from polyaxon_amd.models.resnet import resnet50  # noqa: E402
-from polyaxon_amd.polyflow.executor import ResidentTrialExecutor  # noqa: E402
-from polyaxon_amd.polyflow.sweep import HyperbandSweep  # noqa: E402
-from polyaxon_amd.polytune.managers import HyperbandSearchManager  # noqa: E402
-from polyaxon_amd.spec.hptuning import HPTuningConfig  # noqa: E402
-
 T0 = time.perf_counter()
 METRIC = "HPO trials/hour (whole node) + wall-clock-to-target, ResNet-50 Hyperband sweep"
+MAX_ITER, ETA = 9, 3
 
 
-def hptuning(seed: int, max_iter: int, eta: int) -> HPTuningConfig:
-    return HPTuningConfig.from_dict({
-        "seed": seed,
-        "concurrency": 1,
-        "hyperband": {"max_iter": max_iter, "eta": eta, "resource": {"name": "units", "type": "int"},
-                      "metric": {"name": "loss", "optimization": "minimize"}, "resume": True},
-        "matrix": {
-            "lr": {"loguniform": [math.log(0.02), math.log(0.8)]},
-            "momentum": {"uniform": [0.8, 0.95]},
-            "weight_decay": {"loguniform": [math.log(1e-5), math.log(1e-3)]},
+def _args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3, help="timed Hyperband sweeps per GPU (3 brackets, 23 trials each)")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed sweeps per GPU through the same path")
+    ap.add_argument("--batch", type=int, default=256, help="per-trial batch (one trial per GPU at a time)")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--unit-steps", type=int, default=4, help="training steps per Hyperband resource unit")
+    ap.add_argument("--target", type=float, default=3.0, help="loss target for wall-clock-to-target")
+    ap.add_argument("--signal", type=float, default=0.5, help="class-pattern amplitude of the synthetic data")
+    ap.add_argument("--max-active", type=int, default=8, help="brackets one executor interleaves")
+    ap.add_argument("--cpu", action="store_true", help="CPU rehearsal (gloo, small ResNet, tiny images)")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args(argv)
+
+
+def group_spec(seed: int, program: str, params: dict, concurrency: int, max_active: int) -> dict:
+    return {
+        "version": 1, "kind": "group", "project": "bench_resnet50_hyperband",
+        "hptuning": {
+            "seed": seed, "concurrency": concurrency,
+            "hyperband": {"max_iter": MAX_ITER, "eta": ETA, "resource": {"name": "units", "type": "int"},
+                          "metric": {"name": "loss", "optimization": "minimize"}, "resume": True},
+            "matrix": {"lr": {"loguniform": [math.log(0.02), math.log(1.0)]},
+                       "momentum": {"uniform": [0.8, 0.95]},
+                       "weight_decay": {"loguniform": [math.log(1e-5), math.log(1e-3)]}},
         },
-    })
+        "environment": {"resources": {"gpu": 1},
+                        "executor": {"kind": "resident", "program": program, "params": params,
+                                     "max_active_brackets": max_active}},
+    }
+
+
+# ----------------------------------------------------------------------------- launcher (no GPU calls here)
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """``--gpus N`` without torchrun: start N rank processes (one per GPU) and wait for them.  The parent never
+    initialises the GPU runtime, so starting children is safe."""
+    env = dict(os.environ)
+    env.update({"WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port()),
+                "LOCAL_WORLD_SIZE": str(n)})
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=e))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+# ----------------------------------------------------------------------------- rank 0: scheduler + control
+class Control(threading.Thread):
+    def __init__(self, args, world: int, listener: socket.socket, program: str, params: dict, log):
+        super().__init__(name="bench-control", daemon=True)
+        from polyaxon_amd.polyflow.devices import Device, DeviceAllocator
+        from polyaxon_amd.polyflow.scheduler import Polyflow
+
+        self.args, self.world, self.listener = args, world, listener
+        self.program, self.params, self.log = program, params, log
+        self.root = tempfile.mkdtemp(prefix="plx_bench_")
+        self.flow = Polyflow(self.root, allocator=DeviceAllocator([Device(i) for i in range(world)]),
+                             reconcile_s=0, clean_on_start=False).start()
+        self.t0_set = threading.Event()
+        self.t0_wall = 0.0
+        self.result = None
+        self.error = None
+
+    def _attach_all(self) -> None:
+        from polyaxon_amd.polyflow.resident import Channel
+
+        for _ in range(self.world):
+            sock, _ = self.listener.accept()
+            sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            chan = Channel(sock)
+            hello = chan.recv(timeout=600)
+            self.flow.attach_resident(chan, int(hello["rank"]), self.program, self.params,
+                                      max_active=self.args.max_active)
+        end = time.time() + 600
+        while time.time() < end:
+            snap = self.flow.call(lambda: self.flow.resident_pool().snapshot())
+            if sum(1 for w in snap if w["ready"]) == self.world:
+                return
+            time.sleep(0.05)
+        raise TimeoutError("resident executors did not become ready")
+
+    def _sweeps(self, n: int, seed0: int):
+        gids = []
+        for i in range(n):
+            spec = group_spec(seed0 + i, self.program, self.params, self.world, self.args.max_active)
+            gids.append(self.flow.submit(spec)["id"])
+        for g in gids:
+            st = self.flow.wait("group", g, timeout=3600, poll_s=0.05)
+            if st != "succeeded":
+                raise RuntimeError(f"group {g} ended {st}")
+        return gids
+
+    def _pause(self, tag: str) -> None:
+        done = threading.Event()
+        left = [self.world]
+
+        def on_paused(_msg):
+            left[0] -= 1
+            if left[0] == 0:
+                done.set()
+
+        self.flow.call(lambda: self.flow.resident_pool().pause_all(tag, on_paused))
+        if not done.wait(600):
+            raise TimeoutError(f"executors did not pause ({tag})")
+
+    def run(self) -> None:
+        try:
+            self._attach_all()
+            self.log(f"{self.world} resident executors ready; warm-up: {self.args.warmup} sweep(s)/GPU")
+            if self.args.warmup:
+                self._sweeps(self.args.warmup * self.world, 10_000)
+            self._pause("warm")
+            self.t0_set.wait()
+            gids = self._sweeps(self.args.steps * self.world, 1)
+            self._pause("timed")
+            self.result = self._summarise(gids)
+        except BaseException as e:  # surfaced by the main thread
+            self.error = e
+            self.t0_set.set()
+            try:
+                self.flow.call(lambda: self.flow.resident_pool().pause_all("abort"))
+            except Exception:
+                pass
+
+    def _summarise(self, gids) -> dict:
+        st = self.flow.store
+        q = ",".join("?" * len(gids))
+        xs = st.list_experiments(ids=[r["id"] for r in st.execute(
+            f"SELECT id FROM experiments WHERE group_id IN ({q})", gids).fetchall()])
+        trials = len(xs)
+        ok = sum(1 for x in xs if x["status"] == "succeeded")
+        steps = sum(int(r["step"] or 0) for r in st.execute(
+            f"SELECT m.step FROM experiment_metrics m JOIN experiments e ON e.id = m.experiment_id "
+            f"WHERE e.group_id IN ({q})", gids).fetchall())
+        hit = [x["finished_at"] for x in xs
+               if (x.get("last_metric") or {}).get("loss") is not None and x["last_metric"]["loss"] <= self.args.target]
+        ttt = (min(hit) - self.t0_wall) if hit else None
+        best = min((x["last_metric"]["loss"] for x in xs if (x.get("last_metric") or {}).get("loss") is not None),
+                   default=None)
+        # the status history every trial must show (reference ExperimentLifeCycle)
+        want = ["created", "scheduled", "starting", "running", "succeeded"]
+        sample = xs[:: max(1, len(xs) // 50)]
+        fsm_ok = all([s["status"] for s in st.experiment_statuses(x["id"])] == want
+                     for x in sample if x["status"] == "succeeded")
+        resumed = sum(1 for x in xs if x["cloning_strategy"] == "resume")
+        brackets = sum(1 for it in st.execute(
+            f"SELECT data FROM experiment_group_iterations WHERE group_id IN ({q})", gids).fetchall()
+            if json.loads(it["data"]).get("bracket_iteration") == 0)
+        pool = self.flow.call(lambda: self.flow.resident_pool().snapshot())
+        return {"trials": trials, "succeeded": ok, "train_steps": steps, "ttt": ttt, "best": best,
+                "fsm_ok": fsm_ok, "resumed": resumed, "brackets": brackets, "groups": len(gids), "pool": pool}
 
 
 def main() -> int:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=13, help="timed trials per GPU")
-    ap.add_argument("--warmup", type=int, default=2, help="untimed warm-up trials per GPU")
-    ap.add_argument("--batch", type=int, default=256, help="per-trial batch (one trial per GPU)")
-    ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--unit-steps", type=int, default=8, help="training steps per Hyperband resource unit")
-    ap.add_argument("--max-iter", type=int, default=9)
-    ap.add_argument("--eta", type=int, default=3)
-    ap.add_argument("--target", type=float, default=2.0, help="loss target for wall-clock-to-target")
-    ap.add_argument("--graph", action="store_true", help="replay the step as a hipGraph (slower for ResNet-50 on ROCm 7, see profiles/README.md)")
-    ap.add_argument("--unfused", action="store_true", help="PyTorch BN/ReLU instead of the HIP kernels")
-    ap.add_argument("--miopen-1x1", action="store_true", help="MIOpen for the 1x1 convs instead of the MFMA GEMMs")
-    ap.add_argument("--tune", action="store_true", help="exhaustive MIOpen find (cudnn.benchmark)")
-    ap.add_argument("--verbose", action="store_true", help="print every trial's record to stderr")
-    args = ap.parse_args()
-
+    args = _args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    torch.backends.cudnn.benchmark = args.tune
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+
+    import torch
+    import torch.distributed as dist
+
+    from polyaxon_amd.polyflow.resident import Channel, ResidentWorker
 
     def log(msg):
         if rank == 0:
             print(f"[bench +{time.perf_counter() - T0:.1f}s] {msg}", file=sys.stderr, flush=True)
 
-    gen = torch.Generator(device="cpu").manual_seed(1234 + rank)
-    x = torch.randn(args.batch, 3, args.image, args.image, generator=gen).to(torch.bfloat16)
-    x = x.contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (args.batch,), generator=gen)
-    model = resnet50(fused=not args.unfused, native_conv=not args.miopen_1x1)
-    ex = ResidentTrialExecutor(model, (x, y), dev, use_graph=args.graph)
-
-    log("model built; capturing training step")
-    t_cap = time.perf_counter()
-    ex.capture()
-    capture_s = time.perf_counter() - t_cap
-    log(f"captured in {capture_s:.1f}s; warm-up trials")
-
-    # ---- warm-up trials (untimed): same code path as the sweep
-    warm = HyperbandSweep(HyperbandSearchManager(hptuning(10_000 + rank, args.max_iter, args.eta)), ex,
-                          args.unit_steps, seed=10_000 + rank)
-    if args.warmup > 0:
-        warm.run(max_trials=args.warmup)
-        # plus one short bracket with a rung promotion (snapshot -> top-k reduction -> resume): the first
-        # promotion of a cold process otherwise pays ~0.8 s of lazily paged-in library code inside the timed
-        # region (measured on a fresh box: trial 9 took 1.2 s instead of 0.42 s)
-        HyperbandSweep(HyperbandSearchManager(hptuning(20_000 + rank, 3, 3)), ex, 1, seed=20_000 + rank).run()
-    torch.cuda.synchronize(dev)
+    if args.cpu:
+        dev = torch.device("cpu")
+        torch.set_num_threads(max(1, (os.cpu_count() or 2) // (2 * world)))  # ranks must not oversubscribe the CPU
+        program = "resnet_tiny"
+        params = {"batch": min(args.batch, 8), "image": min(args.image, 32), "unit_steps": min(args.unit_steps, 1),
+                  "grid": 4, "signal": args.signal}
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        program = "resnet50"
+        params = {"batch": args.batch, "image": args.image, "unit_steps": args.unit_steps, "signal": args.signal}
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+        if dev.type == "cuda":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
-    log("timed region")
-    # ---- timed region: exactly K trials per rank
-    start_ev = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    start_ev.record()
-    done, p = 0, 0
-    records = []
-    while done < args.steps:
-        sweep = HyperbandSweep(HyperbandSearchManager(hptuning(rank * 1000 + p + 1, args.max_iter, args.eta)), ex,
-                               args.unit_steps, seed=rank * 1000 + p + 1)
-        res = sweep.run(max_trials=args.steps - done)
-        done += len(res.trials)
-        records.extend(res.trials)
-        p += 1
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
+    def barrier():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
 
-    # ---- post-processing (outside the timed region)
-    train_steps = sum(r.steps for r in records)
-    # wall-clock to target: first trial (by device end time) whose committed metric is <= target
-    t_target = math.inf
-    for r in records:
-        if r.metric is None:
-            continue
-        if r.metric <= args.target and r.end_event is not None:
-            t_target = min(t_target, start_ev.elapsed_time(r.end_event) / 1000.0)
-    best = min((r.metric for r in records if r.metric is not None), default=math.nan)
-    if args.verbose:
-        prev = 0.0
-        for r in records:
-            t_end = start_ev.elapsed_time(r.end_event) if r.end_event is not None else float("nan")
-            log(f"trial {r.trial} cfg {r.config_id} it {r.iteration}/{r.bracket_iteration} res {r.resource} "
-                f"steps {r.steps} ends {t_end:.1f} ms (+{t_end - prev:.1f}) metric {r.metric}")
-            prev = t_end
-    t = torch.tensor([elapsed, -t_target if math.isfinite(t_target) else -math.inf, train_steps, best],
-                     dtype=torch.float64, device=dev)
-    if world > 1:
-        mx = t.clone()
-        dist.all_reduce(mx[:2], op=dist.ReduceOp.MAX)  # max elapsed, min time-to-target
-        tot = t[2:3].clone()
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        bst = t[3:4].clone()
-        dist.all_reduce(bst, op=dist.ReduceOp.MIN)
-        t = torch.cat([mx[:2], tot, bst])
-    elapsed_max = float(t[0])
-    ttt = -float(t[1])
-    total_steps = float(t[2])
-    n = world
-    value = n * args.steps / elapsed_max * 3600.0
+    # rank 0 listens for the executors (its own included) before anybody connects
+    listener = None
+    port = [0]
     if rank == 0:
+        listener = socket.socket()
+        listener.bind(("127.0.0.1", 0))
+        listener.listen(world)
+        port[0] = listener.getsockname()[1]
+    if world > 1:
+        dist.broadcast_object_list(port, src=0)
+
+    params["data_seed"] = 1234  # one task (class patterns) for every trial; the samples are fresh every step
+    worker = ResidentWorker(program, params, device=dev, max_active=args.max_active)
+    log(f"building {program} executors (batch {params['batch']}, image {params['image']})")
+    worker._ready_info = worker.build()
+    log(f"executor ready in {worker._ready_info['build_s']} s")
+    control = None
+    if rank == 0:
+        control = Control(args, world, listener, program, params, log)
+        control.start()
+    chan = Channel.connect("127.0.0.1", port[0])
+    chan.send({"rank": local if world > 1 else 0})
+
+    r = worker.serve(chan)                      # warm-up sweeps, until paused
+    if r != "pause:warm":
+        raise RuntimeError(f"executor stopped during warm-up: {r} ({control.error if control else ''})")
+    barrier()
+    t0 = time.perf_counter()
+    if control is not None:
+        control.t0_wall = time.time()
+        control.t0_set.set()
+        log("timed region")
+    r = worker.serve(chan)                      # timed sweeps, until paused
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if r != "pause:timed":
+        raise RuntimeError(f"executor stopped during the timed region: {r} ({control.error if control else ''})")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t[0])
+    if rank == 0:
+        control.join(timeout=600)
+        if control.error is not None:
+            raise control.error
+        res = control.result
+        value = res["trials"] / elapsed_max * 3600.0
         out = {
             "metric": METRIC,
             "value": round(value, 2),
             "unit": "trials/hour",
-            "n_gpus": n,
+            "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1000.0, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic ImageNet-shape (224x224x3, 1000 classes), random-init weights",
+            "dtype": "bf16" if dev.type == "cuda" else "fp32",
+            "data": "synthetic ImageNet-shape (224x224x3, 1000 classes), fresh learnable batch generated on the "
+                    "device every step (ops/synth.py); random-init weights",
             "config": {
-                "model": "resnet50",
-                "global_batch": args.batch * n,
-                "per_trial_batch": args.batch,
+                "model": "resnet50" if dev.type == "cuda" else "resnet18ish (CPU rehearsal)",
+                "global_batch": params["batch"] * world,
+                "per_trial_batch": params["batch"],
                 "seq_len": None,
-                "image_size": args.image,
-                "parallelism": f"trial-parallel x{n} (1 resident trial executor per GPU, independent brackets)",
-                "search": f"hyperband max_iter={args.max_iter} eta={args.eta} resume=true",
-                "unit_steps": args.unit_steps,
-                "brackets_per_gpu": "repeat",
+                "image_size": params["image"],
+                "parallelism": f"trial-parallel x{world} (resident executor per GPU, brackets balanced by polyflow)",
+                "search": f"hyperband max_iter={MAX_ITER} eta={ETA} resume=true, 3 brackets / 23 trials per sweep",
+                "unit_steps": params["unit_steps"],
+                "step": "one complete Hyperband sweep per GPU",
+                "sweeps": res["groups"],
+                "brackets": res["brackets"],
             },
-            "wall_clock_to_target_s": round(ttt, 3) if math.isfinite(ttt) else None,
+            "trials": res["trials"],
+            "trials_succeeded": res["succeeded"],
+            "trials_resumed": res["resumed"],
+            "train_images_per_s": round(res["train_steps"] * params["batch"] / elapsed_max, 1),
+            "wall_clock_to_target_s": round(res["ttt"], 3) if res["ttt"] is not None else None,
             "target_loss": args.target,
-            "best_loss": round(float(t[3]), 4),
-            "train_images_per_s": round(total_steps * args.batch / elapsed_max, 1),
-            "graph_capture_s": round(capture_s, 2),
-            "hip_graph": ex.graph is not None,
-            "graph_check_error": ex.graph_check_error,
-            "fused_bn": not args.unfused,
-            "mfma_1x1_conv": not args.miopen_1x1,
+            "best_loss": round(res["best"], 4) if res["best"] is not None else None,
+            "store_fsm_history_ok": res["fsm_ok"],
+            "path": "polyflow scheduler + SQLite store + resident executors (same path as plx run)",
         }
+        if args.verbose:
+            print(json.dumps(res["pool"]), file=sys.stderr)
         print(json.dumps(out), flush=True)
+        control.flow.shutdown(stop_running=False, timeout=10)
+    chan.close()
     if world > 1:
         dist.destroy_process_group()
     return 0

@@ -149,6 +149,12 @@ OPTIONS: List[Option] = [
     Option("scheduler.numa_bind", "bool", True, "pin each replica to the CPUs local to its GPUs"),
     Option("scheduler.clean_after_s", "float", 0.0, "delete outputs of finished runs older than this; 0 = keep",
            minimum=0),
+    Option("scheduler.gang_reserve_s", "float", 30.0, "after a multi-GPU run has waited this long, smaller runs "
+           "may not take the devices it needs (no starvation of DP gangs)", minimum=0),
+    Option("scheduler.resident_idle_s", "float", 300.0, "shut an idle resident executor down after this long",
+           minimum=0),
+    Option("scheduler.health_probe", "bool", True, "probe GPU health (amd-smi RAS/ECC, KFD) on every reconcile and "
+           "stop placing work on unhealthy devices"),
     # auth (reference config_settings/auth.py, registration.py, sso)
     Option("auth.registration", "str", "disabled", "self-registration workflow",
            choices=("disabled", "superuser_validation", "open")),

@@ -215,6 +215,65 @@ __global__ __launch_bounds__(kBlock) void init_flat_kernel(float* __restrict__ p
   }
 }
 
+// ---------------------------------------------------------------- synthetic learnable ImageNet-shape batches
+// A fresh batch per training step, generated on the device (no host->device copy, no fixed batch to memorise):
+//   y[b]          = Philox(seed; b, step) mod n_cls
+//   x[b,h,w,c]    = signal * proto[y[b]][h*G/H][w*G/W][c] + N(0, 1)        (NHWC / channels_last, bf16)
+// so the label is a function of a coarse G x G x 3 class pattern buried in unit noise: learnable, never repeated.
+// `counter` (device int) is the data-stream position; it is read here and advanced by counter_add_kernel, so the
+// pair is graph-capturable.  Each thread writes 8 consecutive bf16 (16-B store); H*W*3 % 8 == 0 is required so
+// an 8-element chunk never straddles two images (the host entry point checks it).
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+__global__ __launch_bounds__(kBlock) void synth_images_kernel(u16x8* __restrict__ x, int64_t* __restrict__ y, int B,
+                                                              int H, int W, const float* __restrict__ proto,
+                                                              int n_cls, int G, float signal, uint64_t seed,
+                                                              const int* __restrict__ counter) {
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const uint32_t step = (uint32_t)(*counter);
+  const int64_t per_img = (int64_t)H * W * 3;
+  const int64_t n8 = (int64_t)B * per_img / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n8; t += stride) {
+    const int64_t i0 = t * 8;
+    const int b = (int)(i0 / per_img);
+    const U4 lr = philox(U4{(uint32_t)b, step, 0x1abe1u, 0u}, k0, k1);
+    const int label = (int)(lr.x % (uint32_t)n_cls);
+    const int64_t rem = i0 - (int64_t)b * per_img;
+    if (rem == 0) y[b] = label;
+    const U4 r0 = philox(U4{(uint32_t)t, (uint32_t)(t >> 32), step, 0xda7a0u}, k0, k1);
+    const U4 r1 = philox(U4{(uint32_t)t, (uint32_t)(t >> 32), step, 0xda7a1u}, k0, k1);
+    const uint32_t ur[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    float nz[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // Box-Muller: 2 normals per pair of uniforms
+      const float rad = sqrtf(-2.f * __logf(u01(ur[2 * k])));
+      float sn, cs;
+      __sincosf(6.2831853f * u01(ur[2 * k + 1]), &sn, &cs);
+      nz[2 * k] = rad * cs;
+      nz[2 * k + 1] = rad * sn;
+    }
+    const float* pl = proto + (int64_t)label * G * G * 3;
+    u16x8 out;
+    int pix = (int)(rem / 3), c = (int)(rem - (int64_t)pix * 3);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int h = pix / W, w = pix - h * W;
+      const int gh = h * G / H, gw = w * G / W;
+      out[k] = f_to_bf16(signal * pl[(gh * G + gw) * 3 + c] + nz[k]);
+      if (++c == 3) {
+        c = 0;
+        ++pix;
+      }
+    }
+    x[t] = out;
+  }
+}
+
+__global__ void counter_add_kernel(int* __restrict__ c, int v) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *c += v;
+}
+
 __global__ void zero_kernel(float4* __restrict__ x, int64_t n_vec) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_vec; i += stride)
@@ -299,6 +358,17 @@ PLX_API int plx_init_flat(float* p, const int64_t* chunk_lo, const int64_t* chun
   if (n_chunks <= 0) return 0;
   hipLaunchKernelGGL(init_flat_kernel, dim3(n_chunks), dim3(kBlock), 0, stream, p, chunk_lo, chunk_hi, chunk_seg,
                      seg_kind, seg_scale, seed);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_synth_images(void* x, int64_t* y, int B, int H, int W, const float* proto, int n_cls, int G,
+                             float signal, uint64_t seed, int* counter, hipStream_t stream) {
+  const int64_t per_img = (int64_t)H * W * 3;
+  if (B <= 0 || per_img % 8 || n_cls <= 0 || G <= 0 || G > H || G > W) return 1;
+  const int64_t n8 = (int64_t)B * per_img / 8;
+  hipLaunchKernelGGL(synth_images_kernel, dim3(grid_for(n8)), dim3(kBlock), 0, stream, (u16x8*)x, y, B, H, W, proto,
+                     n_cls, G, signal, seed, (const int*)counter);
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, stream, counter, 1);
   return (int)hipGetLastError();
 }
 

@@ -151,6 +151,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_zero_flat": [_P, _L, _P],
         "plx_record_metric": [_P, _I, _P, _P, _I, _P],
         "plx_commit_metric": [_P, _P, _I, _I, _P, _I, _P],
+        "plx_synth_images": [_P, _P, _I, _I, _I, _P, _I, _I, _F, _U64, _P, _P],
     },
     "plx_bn": {
         "plx_bn_workspace": [_L, _I],

@@ -156,6 +156,29 @@ class DeviceAllocator:
         self.allocations[owner] = a
         return a
 
+    def allocate_on(self, owner: str, devices: List[int], gpus: float = 1.0,
+                    mem_gb: float = 0.0) -> Optional[Allocation]:
+        """Reserve specific devices (a process that already owns them registers with the scheduler, e.g. an
+        attached resident executor).  None if any of them cannot take the share / HBM."""
+        if owner in self.allocations:
+            raise ValueError(f"{owner} already holds an allocation")
+        share = 1.0 if gpus >= 1.0 - EPS else gpus
+        per_dev_mem = mem_gb / max(len(devices), 1)
+        for i in devices:
+            if i >= len(self.devices):
+                return None
+            d = self.devices[i]
+            if not d.healthy or d.share_free < share - EPS or d.memory_gb - d.mem_used_gb < per_dev_mem - EPS:
+                return None
+        for i in devices:
+            d = self.devices[i]
+            d.share_used += share
+            d.mem_used_gb += per_dev_mem
+            d.owners[owner] = share
+        a = Allocation(owner, list(devices), share, mem_gb)
+        self.allocations[owner] = a
+        return a
+
     def release(self, owner: str) -> None:
         a = self.allocations.pop(owner, None)
         if a is None:

@@ -67,7 +67,13 @@ class ResidentTrialExecutor:
         else:
             raise ValueError(f"unknown optimizer {optimizer!r}")
         self.loss_fn = loss_fn or (lambda out, y: F.cross_entropy(out.float(), y))
-        self.x, self.y = batch[0].to(self.device), batch[1].to(self.device)
+        # ``batch`` is either a fixed (x, y) pair or a data source with in-place ``next()`` (ops/synth.py) that the
+        # step refills before every forward: a fresh device-generated batch per step, inside the captured graph
+        self.data = batch if hasattr(batch, "next") else None
+        if self.data is not None:
+            self.x, self.y = self.data.x, self.data.y
+        else:
+            self.x, self.y = batch[0].to(self.device), batch[1].to(self.device)
         self.amp_dtype = amp_dtype if self.is_cuda else None
         self.ring_size = ring_size
         self.ring = torch.zeros(ring_size, dtype=torch.float32, device=self.device)
@@ -101,6 +107,8 @@ class ResidentTrialExecutor:
 
     # ------------------------------------------------------------------ the step
     def _train_step(self) -> None:
+        if self.data is not None:
+            self.data.next()
         if self.amp_dtype is not None:
             with torch.autocast("cuda", dtype=self.amp_dtype):
                 out = self.model(self.x)

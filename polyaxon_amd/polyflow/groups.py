@@ -21,8 +21,10 @@ Semantics kept from the reference:
 """
 from __future__ import annotations
 
+import json
 import logging
 import math
+import time
 from typing import Any, Dict, List, Optional
 
 from polyaxon_amd.fsm import ExperimentLifeCycle
@@ -116,19 +118,30 @@ class GroupDriver:
                                  "experiment_group", self.gid)
 
     def _should_stop_early(self) -> bool:
+        """Reference ExperimentGroup.should_stop_early (db/models/experiment_groups.py:211-221): any experiment whose
+        ``last_metric`` crosses any rule.  The group's metrics are pulled in one query into an [experiments x
+        metrics] matrix and every rule is evaluated in one ``early_stop_any`` call (HIP kernel for device tensors,
+        the same vectorised reduction on the host otherwise)."""
         rules = self.hp.early_stopping
         if not rules:
             return False
-        xps = self.store.list_experiments(group_id=self.gid)
-        for r in rules:
-            for x in xps:
-                v = (x.get("last_metric") or {}).get(r.metric)
-                if v is None:
-                    continue
-                if (Optimization.maximize(r.optimization) and v >= r.value) or (
-                        Optimization.minimize(r.optimization) and v <= r.value):
-                    return True
-        return False
+        import numpy as np
+        import torch
+
+        from polyaxon_amd.polytune.kernels import early_stop_any
+
+        names = sorted({r.metric for r in rules})
+        rows = self.store.execute("SELECT last_metric FROM experiments WHERE group_id = ?", (self.gid,)).fetchall()
+        mat = np.full((max(len(rows), 1), len(names)), np.nan, dtype=np.float32)
+        for i, r in enumerate(rows):
+            last = json.loads(r["last_metric"] or "{}")
+            for j, n in enumerate(names):
+                v = last.get(n)
+                if isinstance(v, (int, float)):
+                    mat[i, j] = v
+        flags = early_stop_any(torch.from_numpy(mat), [(names.index(r.metric), float(r.value),
+                                                        Optimization.maximize(r.optimization)) for r in rules])
+        return any(flags)
 
     def stop(self, pending_only: bool = False, message: str = "Stopped") -> None:
         self.stopped = True
@@ -226,8 +239,6 @@ class BODriver(GroupDriver):
             self.queue.append(xid)
         self.iteration_id = self.store.create_iteration(self.gid, {"iteration": 0, "experiment_ids": self.cur_ids})
 
-    def has_more_work(self) -> bool:
-        return self.manager.should_reschedule(self.iteration) and not self.stopped and bool(self.cur_ids) and False
 
     def advance(self, xid: int, status: str) -> None:
         if any(x not in self.finished for x in self.cur_ids):
@@ -297,8 +308,206 @@ class AshaDriver(GroupDriver):
         self._fill()
 
 
+class ResidentHyperbandDriver(GroupDriver):
+    """Hyperband on resident executors (``environment.executor: resident``; polyflow/resident.py, pool.py).
+
+    The reference runs the brackets one after another with a synchronous rung barrier and a 30 s poll
+    (polyaxon/hpsearch/tasks/hyperband.py:7-83), every trial a pod.  Here all ``s_max + 1`` brackets are created
+    up front (same suggestions as the reference: ``get_suggestions`` per iteration, same seed) and handed to the
+    group's executors -- at most ``concurrency`` of them, balanced by training units -- which run them
+    concurrently; each executor decides its rungs on the device.  This driver mirrors what the executors report
+    into the store, so every trial is an experiment row with its FSM history, metrics and ``last_metric``;
+    promotions are RESUME (or RESTART) clones of the previous rung's experiment with the resource declaration
+    patched (iteration_managers/hyperband.py:79-113); every finished rung is an iteration row.
+    """
+
+    def begin(self) -> None:
+        from polyaxon_amd.polyflow.programs import bracket_units, program_key
+
+        self.m: HyperbandSearchManager = self.manager
+        self.hb = self.hp.hyperband
+        self.ex = self.spec.environment.executor
+        self.program_key = program_key(self.ex.program, self.ex.params)
+        res = self.spec.environment.resources
+        g = res.gpu.value if (res is not None and res.gpu is not None) else 1.0
+        self.gpu = g if g > 0 else 1.0
+        if self.gpu > 1:
+            raise ValueError("a resident executor runs on one device (resources.gpu <= 1)")
+        self.hbm = res.hbm_gb if res is not None else 0.0
+        self.brackets: Dict[str, Dict[str, Any]] = {}
+        self.pending_keys: List[str] = []
+        self.used_workers: set = set()
+        self._xspec_cache: Dict[str, Any] = {}
+        rname = self.hb.resource.name
+        for it in range(self.m.s_max + 1):
+            sugg = self.m.get_suggestions(HyperbandIterationConfig(iteration=it))
+            key = f"{self.gid}.{it}"
+            configs = [{"cid": i, "params": {k: v for k, v in s.items() if k != rname}} for i, s in enumerate(sugg)]
+            self.brackets[key] = {"iteration": it, "configs": configs, "status": None, "wid": None, "xids": {},
+                                  "root": {}, "open": set(),
+                                  "units": bracket_units(self.hb.max_iter, self.hb.eta, it, self.hb.resume)}
+            self.pending_keys.append(key)
+        self._dispatch()
+
+    # ------------------------------------------------------------------ placement
+    def _dispatch(self) -> None:
+        if self.stopped or self.done or not self.pending_keys:
+            return
+        pool = self.flow.resident_pool()
+        pool.ensure(self.program_key, self.ex.program, self.ex.params, want=self.concurrency, gpu=self.gpu,
+                    hbm_gb=self.hbm, max_active=self.ex.max_active_brackets)
+        early = [{"metric": r.metric, "value": r.value, "optimization": r.optimization}
+                 for r in self.hp.early_stopping]
+        while self.pending_keys:
+            key = self.pending_keys[0]
+            br = self.brackets[key]
+            msg = {"op": "bracket", "key": key, "hptuning": self.hp.to_dict(), "iteration": br["iteration"],
+                   "configs": br["configs"], "seed": int(self.hp.seed or 0) + 7919 * self.gid,
+                   "early_stopping": early}
+            allowed = sorted(self.used_workers) if len(self.used_workers) >= self.concurrency else None
+            w = pool.assign(self, msg, br["units"], allowed=allowed, key=self.program_key)
+            if w is None:
+                break
+            self.used_workers.add(w.wid)
+            br["wid"] = w.wid
+            self.pending_keys.pop(0)
+        if self.pending_keys:  # every device is busy: try again shortly (an executor or device will free up)
+            self.flow.after(0.5, self._dispatch)
+
+    def has_more_work(self) -> bool:
+        return any(b["status"] is None for b in self.brackets.values())
+
+    # ------------------------------------------------------------------ executor events (scheduler thread)
+    def on_resident_event(self, h, msg: Dict[str, Any]) -> None:
+        br = self.brackets.get(msg.get("key"))
+        if br is None:
+            return
+        ev = msg["ev"]
+        if ev == "trial_start":
+            self._trial_start(h, br, msg)
+        elif ev == "trial_end":
+            self._trial_end(br, msg)
+        elif ev == "rung_done":
+            self._rung_done(br, msg)
+        elif ev == "bracket_done":
+            self._close_open(br, "failed" if msg.get("status") == "failed" else "stopped",
+                             f"bracket {msg.get('status')}")
+            br["status"] = msg.get("status") or "succeeded"
+            self._dispatch()
+            self._check_finished()
+        elif ev == "error":
+            log.warning("group %s bracket %s: %s", self.gid, msg.get("key"), msg.get("message"))
+
+    def on_bracket_lost(self, h, key: str, reason: str) -> None:
+        br = self.brackets.get(key)
+        if br is None or br["status"] is not None:
+            return
+        self._close_open(br, "failed", f"resident executor {h.wid} lost: {reason}")
+        br["status"] = "failed"
+        self._check_finished()
+
+    def _close_open(self, br, status: str, message: str) -> None:
+        for xid in list(br["open"]):
+            self.store.set_experiment_status(xid, status, message)
+            jid = br.get("jobs", {}).pop(xid, None)
+            if jid is not None:
+                self.store.set_experiment_job_status(jid, status, message)
+            self.finished[xid] = status
+            self.active.discard(xid)
+        br["open"].clear()
+
+    def _experiment_data(self, params: Dict[str, Any]) -> Dict[str, Any]:
+        return self.spec.experiment_data(params)
+
+    def _trial_start(self, h, br, msg) -> None:
+        rung, cid, params = int(msg["rung"]), int(msg["cid"]), msg["params"]
+        prev = br["xids"].get((rung - 1, cid)) if rung > 0 else None
+        strategy = ("resume" if self.hb.resume else "restart") if prev is not None else None
+        xid = self.store.create_experiment(
+            self.project["id"], self._experiment_data(params), group_id=self.gid, user=self.user,
+            declarations=params, original_experiment_id=prev, cloning_strategy=strategy,
+            code_reference_id=self.flow._group_code_ref(self.gid), resources={"gpu": self.gpu})
+        root = br["root"].get(cid) if strategy == "resume" else None
+        if root is None:
+            br["root"][cid] = xid
+            outputs = self.flow.paths.experiment_outputs(self.user, self.project["name"], xid, self.gid)
+        else:
+            outputs = self.store.get_experiment(root)["outputs_path"]
+        logs = self.flow.paths.experiment_logs(self.user, self.project["name"], xid, self.gid)
+        self.store.update_experiment(xid, outputs_path=outputs, logs_path=logs)
+        br["xids"][(rung, cid)] = xid
+        br["open"].add(xid)
+        for st in ("scheduled", "starting", "running"):
+            self.store.set_experiment_status(xid, st)
+        jid = self.store.create_experiment_job(xid, "master", 0, definition={"executor": f"resident:{h.wid}"},
+                                               resources={"gpu": self.gpu}, devices=h.devices)
+        self.store.set_experiment_job_status(jid, "running")
+        br.setdefault("jobs", {})[xid] = jid
+        self.flow.auditor.record("experiment.created", "experiment", xid, self.user, group=self.gid)
+        self.active.add(xid)
+
+    def _trial_end(self, br, msg) -> None:
+        xid = br["xids"].get((int(msg["rung"]), int(msg["cid"])))
+        if xid is None:
+            return
+        v = msg.get("metric")
+        name = self.hb.metric.name
+        if v is not None:
+            self.store.add_metrics(xid, {name: v}, step=int(msg.get("steps", 0)), created_at=msg.get("t_end"))
+            status, message = "succeeded", None
+        else:
+            status, message = "failed", f"{name} is not finite (diverged)"
+        self.store.set_experiment_status(xid, status, message)
+        self.store.update_experiment(xid, started_at=msg.get("t_start"), finished_at=msg.get("t_end"))
+        jid = br.get("jobs", {}).pop(xid, None)
+        if jid is not None:
+            self.store.set_experiment_job_status(jid, status, message)
+        br["open"].discard(xid)
+        self.active.discard(xid)
+        self.finished[xid] = status
+        self.flow.auditor.record(f"experiment.{status}", "experiment", xid, status=status)
+        if self.hp.early_stopping and not self.stopped and self._should_stop_early():
+            self.flow.auditor.record("experiment_group.stopped", "experiment_group", self.gid, reason="early_stopping")
+            self.stop(pending_only=not self.stop_running_on_early_stop, message="Early stopping")
+
+    def _rung_done(self, br, msg) -> None:
+        rung = int(msg["rung"])
+        ids = [x for (r, _c), x in sorted(br["xids"].items()) if r == rung]
+        metrics = [[br["xids"][(rung, int(c))], float(v)] for c, v in msg.get("metrics") or []
+                   if (rung, int(c)) in br["xids"]]
+        promoted = [br["xids"][(rung, int(c))] for c in msg.get("promoted") or [] if (rung, int(c)) in br["xids"]]
+        self.store.create_iteration(self.gid, {"iteration": br["iteration"], "bracket_iteration": rung,
+                                               "experiment_ids": ids, "experiments_metrics": metrics,
+                                               "promoted": promoted, "executor": br["wid"]})
+        if msg.get("early_stop") and not self.stopped:
+            self.flow.auditor.record("experiment_group.stopped", "experiment_group", self.gid, reason="early_stopping")
+            self.stop(pending_only=not self.stop_running_on_early_stop, message="Early stopping")
+
+    def stop(self, pending_only: bool = False, message: str = "Stopped") -> None:
+        self.stopped = True
+        pool = self.flow.resident_pool()
+        for key in list(self.pending_keys):
+            self.brackets[key]["status"] = "stopped"
+        self.pending_keys.clear()
+        for key, br in self.brackets.items():
+            if br["status"] is None and br["wid"] is not None:
+                if not pool.send(br["wid"], {"op": "stop_bracket", "key": key}):
+                    self._close_open(br, "stopped", message)
+                    br["status"] = "stopped"
+        if self.store.get_group(self.gid)["status"] not in ("stopped", "succeeded", "failed"):
+            self.store.set_group_status(self.gid, "stopped", message)
+        self._check_finished()
+
+
 def make_group_driver(flow, gid: int, spec: GroupSpecification, project: Dict, user: str, cwd: str) -> GroupDriver:
     algo = spec.search_algorithm
+    ex = spec.environment.executor if spec.environment is not None else None
+    if ex is not None and ex.resident:
+        if algo != SearchAlgorithms.HYPERBAND:
+            from polyaxon_amd.spec.specification import PolyaxonfileError
+
+            raise PolyaxonfileError(f"resident executors run hyperband groups; {algo} groups use executor: process")
+        return ResidentHyperbandDriver(flow, gid, spec, project, user, cwd)
     cls = {SearchAlgorithms.GRID: GridRandomDriver, SearchAlgorithms.RANDOM: GridRandomDriver,
            SearchAlgorithms.HYPERBAND: HyperbandDriver, SearchAlgorithms.BO: BODriver,
            SearchAlgorithms.ASHA: AshaDriver}[algo]

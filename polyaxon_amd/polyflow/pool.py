@@ -1,0 +1,318 @@
+"""Scheduler-side pool of resident executors (one warm worker process per GPU, see polyflow/resident.py).
+
+The pool lives on the polyflow thread.  It
+
+* spawns workers on demand for a program (``environment.executor``), each on a device it reserves in the
+  allocator under owner ``resident:<wid>`` (whole GPU, or a fraction + HBM budget for small programs), pinned
+  with ``HIP_VISIBLE_DEVICES`` and the NUMA-local CPUs like any trial replica;
+* accepts externally started workers (``attach``: bench.py's ranks, or a worker on a GPU another launcher owns);
+* balances brackets over the workers of a program by outstanding training units (longest-processing-time
+  greedy: every new bracket goes to the least-loaded executor the group may use);
+* turns worker messages into calls on the owning group driver (reader thread per worker -> ``flow.post``), and
+  a lost worker (process died, socket closed) into failed trials and released devices;
+* shuts idle spawned workers down after ``idle_s`` so their GPUs return to process-mode runs.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import socket
+import subprocess
+import sys
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+from polyaxon_amd.polyflow.resident import Channel, ChannelClosed
+
+log = logging.getLogger("polyaxon_amd.polyflow.pool")
+
+
+@dataclass
+class WorkerHandle:
+    wid: int
+    key: str                          # program key (name + params)
+    program: str
+    params: Dict[str, Any]
+    devices: List[int]
+    chan: Channel
+    proc: Optional[subprocess.Popen] = None
+    external: bool = False
+    ready: bool = False
+    alive: bool = True
+    info: Dict[str, Any] = field(default_factory=dict)
+    brackets: Dict[str, Any] = field(default_factory=dict)   # bracket key -> driver
+    units: Dict[str, float] = field(default_factory=dict)    # bracket key -> outstanding units
+    idle_since: float = field(default_factory=time.time)
+    closing: bool = False
+    waiters: Dict[str, Callable[[Dict[str, Any]], None]] = field(default_factory=dict)
+
+    @property
+    def owner(self) -> str:
+        return f"resident:{self.wid}"
+
+    @property
+    def load(self) -> float:
+        return sum(self.units.values())
+
+
+class ResidentPool:
+    def __init__(self, flow, idle_s: float = 300.0):
+        self.flow = flow
+        self.idle_s = idle_s
+        self.workers: Dict[int, WorkerHandle] = {}
+        self._next = 1
+        self._reaper_armed = False
+
+    # ------------------------------------------------------------------ queries
+    def workers_for(self, key: str) -> List[WorkerHandle]:
+        return [w for w in self.workers.values() if w.alive and w.key == key]
+
+    def snapshot(self) -> List[Dict[str, Any]]:
+        return [{"wid": w.wid, "program": w.program, "devices": w.devices, "external": w.external, "ready": w.ready,
+                 "alive": w.alive, "brackets": sorted(w.brackets), "load_units": w.load,
+                 "pid": w.proc.pid if w.proc else w.info.get("pid")} for w in self.workers.values()]
+
+    # ------------------------------------------------------------------ creation
+    def ensure(self, key: str, program: str, params: Dict[str, Any], want: int, gpu: float = 1.0,
+               hbm_gb: float = 0.0, max_active: int = 8) -> List[WorkerHandle]:
+        """Make sure up to ``want`` workers run ``program`` (spawning on free devices); returns the live ones."""
+        have = self.workers_for(key)
+        while len(have) < want:
+            h = self._spawn(key, program, params, gpu, hbm_gb, max_active)
+            if h is None:
+                break
+            have.append(h)
+        return have
+
+    def _spawn(self, key, program, params, gpu, hbm_gb, max_active) -> Optional[WorkerHandle]:
+        wid = self._next
+        owner = f"resident:{wid}"
+        try:
+            a = self.flow.alloc.allocate(owner, gpu, hbm_gb)
+        except ValueError as e:
+            log.warning("resident executor allocation rejected: %s", e)
+            return None
+        if a is None:
+            return None
+        self._next += 1
+        parent, child = socket.socketpair()
+        env = dict(os.environ)
+        env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in a.devices)
+        env.pop("ROCR_VISIBLE_DEVICES", None)
+        env["PYTHONUNBUFFERED"] = "1"
+        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = pkg_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        log_dir = os.path.join(self.flow.paths.root, "executors")
+        os.makedirs(log_dir, exist_ok=True)
+        log_path = os.path.join(log_dir, f"worker{wid}.log")
+        argv = [self.flow.python, "-m", "polyaxon_amd.polyflow.resident", "--fd", str(child.fileno())]
+        if self.flow.alloc.n_devices and os.environ.get("PLX_CPU_ONLY") == "1":
+            argv.append("--cpu")
+        try:
+            with open(log_path, "ab") as logf:
+                proc = subprocess.Popen(argv, env=env, pass_fds=(child.fileno(),), stdout=logf,
+                                        stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, start_new_session=True)
+        except OSError as e:
+            child.close()
+            parent.close()
+            self.flow.alloc.release(owner)
+            log.error("cannot start resident executor: %s", e)
+            self.flow.store.add_cluster_event("resident_executor", "error", f"spawn failed: {e}")
+            return None
+        child.close()
+        if a.devices and getattr(self.flow, "numa_bind", False):
+            self.flow._bind_cpus(proc.pid, a.devices)
+        h = WorkerHandle(wid, key, program, dict(params), list(a.devices), Channel(parent), proc=proc)
+        h.info["log_path"] = log_path
+        self.workers[wid] = h
+        h.chan.send({"op": "init", "program": program, "params": params, "max_active": max_active})
+        self._start_reader(h)
+        self._arm_reaper()
+        self.flow.auditor.record("resident_executor.started", "executor", wid, devices=a.devices, program=program)
+        return h
+
+    def attach(self, chan: Channel, device: int, program: str, params: Optional[Dict[str, Any]] = None,
+               max_active: int = 8, gpu: float = 1.0) -> WorkerHandle:
+        """Register an already running worker (it was built by another launcher, e.g. a bench.py rank) that owns
+        ``device``.  Runs on the scheduler thread."""
+        from polyaxon_amd.polyflow.programs import program_key
+
+        wid = self._next
+        self._next += 1
+        owner = f"resident:{wid}"
+        if self.flow.alloc.allocate_on(owner, [device], gpu) is None:
+            raise RuntimeError(f"device {device} is not free for a resident executor")
+        h = WorkerHandle(wid, program_key(program, params), program, dict(params or {}), [device], chan,
+                         external=True)
+        self.workers[wid] = h
+        chan.send({"op": "init", "program": program, "params": params or {}, "max_active": max_active})
+        self._start_reader(h)
+        return h
+
+    # ------------------------------------------------------------------ dispatch
+    def assign(self, driver, msg: Dict[str, Any], units: float,
+               allowed: Optional[List[int]] = None, key: Optional[str] = None) -> Optional[WorkerHandle]:
+        cands = [w for w in self.workers.values() if w.alive and (key is None or w.key == key)
+                 and (allowed is None or w.wid in allowed)]
+        if not cands:
+            return None
+        w = min(cands, key=lambda h: (h.load, h.wid))
+        w.brackets[msg["key"]] = driver
+        w.units[msg["key"]] = units
+        try:
+            w.chan.send(msg)
+        except OSError:
+            self._lost(w, "send failed")
+            return None
+        return w
+
+    def send(self, wid: int, msg: Dict[str, Any]) -> bool:
+        w = self.workers.get(wid)
+        if w is None or not w.alive:
+            return False
+        try:
+            w.chan.send(msg)
+            return True
+        except OSError:
+            self._lost(w, "send failed")
+            return False
+
+    def pause_all(self, tag: str, on_paused: Optional[Callable[[Dict[str, Any]], None]] = None,
+                  key: Optional[str] = None) -> int:
+        n = 0
+        for w in self.workers.values():
+            if w.alive and (key is None or w.key == key):
+                if on_paused is not None:
+                    w.waiters[f"paused:{tag}"] = on_paused
+                self.send(w.wid, {"op": "pause", "tag": tag})
+                n += 1
+        return n
+
+    def shutdown(self, wid: Optional[int] = None) -> None:
+        for w in list(self.workers.values()):
+            if wid is not None and w.wid != wid:
+                continue
+            if w.alive:
+                w.closing = True
+                self.send(w.wid, {"op": "shutdown"})
+
+    def close(self, timeout: float = 10.0) -> None:
+        """Scheduler shutdown: ask every worker to exit, wait for the spawned ones, release every device."""
+        self.shutdown()
+        end = time.time() + timeout
+        for w in list(self.workers.values()):
+            if w.proc is not None:
+                try:
+                    w.proc.wait(timeout=max(0.1, end - time.time()))
+                except subprocess.TimeoutExpired:
+                    pass
+            w.closing = True
+            self._lost(w, "scheduler shutdown")
+
+    # ------------------------------------------------------------------ messages (scheduler thread)
+    def _start_reader(self, h: WorkerHandle) -> None:
+        def reader():
+            while True:
+                try:
+                    msg = h.chan.recv()
+                except (ChannelClosed, OSError, ValueError):
+                    break
+                if msg is None:
+                    continue
+                self.flow.post(self._on_message, h, msg)
+            if h.proc is not None:
+                try:
+                    h.proc.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    h.proc.kill()
+            self.flow.post(self._lost, h, "worker exited" if h.proc is None else f"worker exited ({h.proc.returncode})")
+
+        threading.Thread(target=reader, name=f"resident-reader-{h.wid}", daemon=True).start()
+
+    def _on_message(self, h: WorkerHandle, msg: Dict[str, Any]) -> None:
+        ev = msg.get("ev")
+        if ev == "ready":
+            h.ready = True
+            h.info.update(msg)
+            self.flow.store.kv_set(f"resident:{h.wid}", {k: v for k, v in msg.items() if k != "ev"})
+            return
+        if ev == "paused":
+            cb = h.waiters.pop(f"paused:{msg.get('tag')}", None)
+            if cb is not None:
+                cb(dict(msg, wid=h.wid))
+            return
+        if ev == "pong":
+            cb = h.waiters.pop("pong", None)
+            if cb is not None:
+                cb(dict(msg, wid=h.wid))
+            return
+        if ev == "error" and msg.get("fatal"):
+            log.error("resident executor %d failed: %s", h.wid, msg.get("message"))
+            self.flow.store.add_cluster_event("resident_executor", "error",
+                                              f"executor {h.wid} on devices {h.devices}: {msg.get('message')}",
+                                              {"traceback": msg.get("traceback")})
+            self._lost(h, msg.get("message") or "fatal error")
+            return
+        key = msg.get("key")
+        driver = h.brackets.get(key) if key is not None else None
+        if driver is None:
+            if ev == "error":
+                log.warning("resident executor %d: %s", h.wid, msg.get("message"))
+            return
+        try:
+            driver.on_resident_event(h, msg)
+        finally:
+            if ev == "trial_end":
+                # outstanding work shrinks as trials finish (keeps the balancing estimate honest)
+                h.units[key] = max(0.0, h.units.get(key, 0.0) - float(msg.get("steps", 0)) /
+                                   max(1.0, float(h.info.get("unit_steps", 1) or 1)))
+            if ev == "bracket_done":
+                h.brackets.pop(key, None)
+                h.units.pop(key, None)
+                if not h.brackets:
+                    h.idle_since = time.time()
+
+    def _lost(self, h: WorkerHandle, reason: str) -> None:
+        if not h.alive:
+            return
+        h.alive = False
+        self.flow.alloc.release(h.owner)
+        try:
+            h.chan.close()
+        except Exception:
+            pass
+        if h.proc is not None and h.proc.poll() is None:
+            try:
+                os.killpg(h.proc.pid, 9)
+            except OSError:
+                pass
+        lost = dict(h.brackets)
+        h.brackets.clear()
+        h.units.clear()
+        if lost or not (h.external or h.closing):
+            self.flow.store.add_cluster_event("resident_executor", "warning" if not lost else "error",
+                                              f"executor {h.wid} on devices {h.devices} gone: {reason}",
+                                              {"brackets": sorted(lost)})
+        for key, driver in lost.items():
+            try:
+                driver.on_bracket_lost(h, key, reason)
+            except Exception:
+                log.exception("bracket loss handler failed")
+
+    # ------------------------------------------------------------------ idle reaping
+    def _arm_reaper(self) -> None:
+        if self._reaper_armed or self.idle_s <= 0:
+            return
+        self._reaper_armed = True
+        self.flow.after(min(self.idle_s, 30.0), self._reap)
+
+    def _reap(self) -> None:
+        self._reaper_armed = False
+        now = time.time()
+        for w in list(self.workers.values()):
+            if w.alive and not w.external and not w.brackets and now - w.idle_since > self.idle_s:
+                self.shutdown(w.wid)
+        if any(w.alive and not w.external for w in self.workers.values()):
+            self._arm_reaper()

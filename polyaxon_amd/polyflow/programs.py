@@ -1,0 +1,133 @@
+"""Trial programs for resident executors: what a warm worker builds once and then trains trial after trial.
+
+A *program* is the trial-invariant part of an experiment -- model architecture, batch shape, data stream,
+optimizer kind, the step (eager or captured as a hipGraph) -- and is named in the Polyaxonfile as
+``environment.executor: {kind: resident, program: <name>, params: {...}}``.  Everything that varies between
+trials (hyper-parameters, random init seed, Hyperband resource) is device data the executor rewrites in place
+(polyflow/executor.py).  In the reference every trial is a pod running ``run.cmd`` from scratch
+(polyaxon/scheduler/spawners/experiment_spawner.py:108-179); the program is what stays warm instead.
+
+Registry: ``resnet50`` (BASELINE.json config 3), ``resnet_tiny`` (same code path, CPU-test sized), ``mlp``
+(config 2).  ``module:callable`` names any user factory with the same signature ``(params, device) -> TrialProgram``.
+"""
+from __future__ import annotations
+
+import importlib
+import math
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, Optional, Tuple
+
+import torch
+
+
+@dataclass
+class TrialProgram:
+    executor: Any                     # ResidentTrialExecutor
+    unit_steps: int = 1               # training steps per Hyperband / ASHA resource unit
+    metric: str = "loss"              # the metric the executor commits (mean loss over the last `window` steps)
+    window: int = 4
+    hp_keys: Tuple[str, ...] = ()     # hyper-parameters the program understands
+    info: Dict[str, Any] = field(default_factory=dict)
+
+    def warm(self, steps: int = 2) -> None:
+        """Pay one-time costs (kernel selection, allocator growth, library page-in) before the first trial."""
+        ex = self.executor
+        if ex.use_graph:
+            ex.capture(warmup=steps)
+        else:
+            ex.reset(seed=0)
+            ex.set_hparams(**{k: v for k, v in self.info.get("warm_hparams", {}).items()})
+            ex.run(steps)
+            ex.snapshot("__warm__")
+            ex.restore("__warm__")
+            ex.drop("__warm__")
+        if ex.is_cuda:
+            torch.cuda.synchronize(ex.device)
+
+
+def _resnet(params: Dict[str, Any], device, tiny: bool) -> TrialProgram:
+    from polyaxon_amd.models.resnet import resnet18ish, resnet50
+    from polyaxon_amd.ops.synth import SyntheticImages
+    from polyaxon_amd.polyflow.executor import ResidentTrialExecutor
+
+    dev = torch.device(device)
+    batch = int(params.get("batch", 8 if tiny else 256))
+    image = int(params.get("image", 32 if tiny else 224))
+    classes = int(params.get("classes", 10 if tiny else 1000))
+    data = SyntheticImages(batch, image, dev, classes=classes,
+                           active_classes=int(params.get("active_classes", min(classes, 100))),
+                           grid=int(params.get("grid", 4 if tiny else 7)), signal=float(params.get("signal", 0.5)),
+                           seed=int(params.get("data_seed", 0)))
+    model = resnet18ish(num_classes=classes) if tiny else resnet50(num_classes=classes)
+    ex = ResidentTrialExecutor(model, data, dev, optimizer="sgd", use_graph=bool(params.get("graph", False)))
+    return TrialProgram(ex, unit_steps=int(params.get("unit_steps", 1 if tiny else 4)),
+                        window=int(params.get("window", 4)), hp_keys=("lr", "momentum", "weight_decay", "nesterov"),
+                        info={"model": "resnet18ish" if tiny else "resnet50", "batch": batch, "image": image,
+                              "classes": classes, "data": "synthetic, fresh per step (ops/synth.py)",
+                              "warm_hparams": {"lr": 0.01, "momentum": 0.9, "weight_decay": 1e-4},
+                              "images_per_step": batch})
+
+
+def _mlp(params: Dict[str, Any], device) -> TrialProgram:
+    from polyaxon_amd.polyflow.executor import ResidentTrialExecutor
+    from polyaxon_amd.trainers import MLP
+
+    dev = torch.device(device)
+    bs = int(params.get("batch", 256))
+    g = torch.Generator().manual_seed(int(params.get("data_seed", 0)))
+    x = torch.randn(bs, 784, generator=g)
+    y = (x @ torch.randn(784, 10, generator=g)).argmax(1)
+    ex = ResidentTrialExecutor(MLP(), (x, y), dev, optimizer="sgd", use_graph=dev.type == "cuda", channels_last=False)
+    return TrialProgram(ex, unit_steps=int(params.get("unit_steps", 10)), window=int(params.get("window", 4)),
+                        hp_keys=("lr", "momentum", "weight_decay"),
+                        info={"model": "mlp", "batch": bs, "warm_hparams": {"lr": 0.01, "momentum": 0.9},
+                              "images_per_step": bs})
+
+
+PROGRAMS: Dict[str, Callable[[Dict[str, Any], Any], TrialProgram]] = {
+    "resnet50": lambda p, d: _resnet(p, d, tiny=False),
+    "resnet_tiny": lambda p, d: _resnet(p, d, tiny=True),
+    "mlp": _mlp,
+}
+
+
+def resolve(name: str) -> Callable[[Dict[str, Any], Any], TrialProgram]:
+    if name in PROGRAMS:
+        return PROGRAMS[name]
+    if ":" in name:
+        mod, _, attr = name.partition(":")
+        return getattr(importlib.import_module(mod), attr)
+    raise KeyError(f"unknown resident program {name!r}; known: {sorted(PROGRAMS)} or module:callable")
+
+
+def build_program(name: str, params: Optional[Dict[str, Any]], device) -> TrialProgram:
+    prog = resolve(name)(dict(params or {}), device)
+    if not isinstance(prog, TrialProgram):
+        raise TypeError(f"program {name} returned {type(prog).__name__}, expected TrialProgram")
+    return prog
+
+
+def program_key(name: str, params: Optional[Dict[str, Any]]) -> str:
+    """Executors are shared by every group whose program (name + build params) is identical."""
+    import json
+
+    return f"{name}:{json.dumps(params or {}, sort_keys=True)}"
+
+
+def bracket_units(max_iter: float, eta: float, iteration: int, resume: bool) -> float:
+    """Training resource (in units) one Hyperband bracket costs -- the load the pool balances across executors."""
+    s_max = int(math.log(max_iter) / math.log(eta))
+    s = s_max - iteration
+    B = (s_max + 1) * max_iter
+    n0 = int(math.ceil((B / max_iter) * (eta ** s) / (s + 1)))
+    r = max_iter * eta ** (-s)
+    total, prev, n, i = 0.0, 0.0, n0, 0
+    while n > 0:
+        ri = r * eta ** i
+        total += n * ((ri - prev) if (resume and i) else ri)
+        prev = ri
+        # keep after rung i, exactly as HyperbandSearchManager.get_n_config_to_keep_for_iteration (including the
+        # reference quirk that the last bracket, s = 0, still reduces once: keep(n0, 0) = int(n0 / eta) > 0)
+        n = 0 if i == s + 1 else int(n0 * (eta ** -i) / eta)
+        i += 1
+    return total

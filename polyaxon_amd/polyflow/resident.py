@@ -1,0 +1,446 @@
+"""Resident trial executors: warm per-GPU worker processes that polyflow feeds Hyperband brackets over a socket.
+
+Reference behaviour being replaced: every Hyperband trial -- including every promotion, which
+the reference models as a *new* experiment resumed from the previous rung's outputs
+(polyaxon/hpsearch/iteration_managers/hyperband.py:79-113) -- is a pod: build check, pod create, container start,
+framework import, CUDA context, then user code, with a 1 s Celery hop per step and a 30 s poll at every rung
+barrier (polyaxon/hpsearch/tasks/hyperband.py:48-83).  On one 8×MI355X node everything trial-invariant can stay
+warm, so polyflow keeps **one resident executor per GPU**:
+
+* the worker process (``python -m polyaxon_amd.polyflow.resident``) builds its *program* once
+  (polyflow/programs.py: model, flat fp32 weights, fused optimizer, device data stream, optional hipGraph) and
+  then trains trial after trial, re-initialising weights/optimizer state in place (polyflow/executor.py);
+* the scheduler assigns whole **brackets** to executors (brackets are independent successive-halving runs, so
+  they spread over GPUs with no cross-GPU barrier); an executor interleaves up to ``max_active_brackets`` of
+  them in *rounds*: the current rung of every active bracket, then ONE ``plx_topk_brackets`` launch over the
+  device-resident ``[brackets × configs]`` metric tensor decides every promotion of the round (and one
+  ``plx_early_stop_any`` launch per rule set evaluates early stopping), with a single small D2H read;
+* promotions with ``resume: true`` restore the config's HBM snapshot (the reference RESUME clone,
+  db/models/experiments.py:225-316) instead of a checkpoint file round trip -- 288 GB of HBM holds hundreds of
+  ResNet-50 trial states;
+* every trial is still a Polyaxon experiment: the worker streams ``trial_start``/``trial_end``/``rung_done``
+  events, and the scheduler thread (polyflow/groups.py ``ResidentHyperbandDriver``) writes the experiment rows,
+  RESUME clones, FSM status history, metrics/``last_metric`` and iteration rows, while the GPU keeps running.
+
+Protocol (length-prefixed JSON over a stream socket; ``Channel``):
+
+  scheduler -> worker  {"op": "init", "program", "params", "max_active"} | {"op": "bracket", ...} |
+                       {"op": "stop_bracket", "key"} | {"op": "pause", "tag"} | {"op": "shutdown"}
+  worker -> scheduler  {"ev": "ready", ...} | {"ev": "trial_start", ...} | {"ev": "trial_end", ...} |
+                       {"ev": "rung_done", ...} | {"ev": "bracket_done", ...} | {"ev": "paused", "tag"} |
+                       {"ev": "error", ...}
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import select
+import socket
+import struct
+import sys
+import threading
+import time
+import traceback
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Tuple
+
+_HDR = struct.Struct("!I")
+
+
+class ChannelClosed(EOFError):
+    pass
+
+
+class Channel:
+    """Length-prefixed JSON messages over a connected stream socket.  ``send`` is thread-safe; ``recv`` is meant
+    for one reader."""
+
+    def __init__(self, sock: socket.socket):
+        self.sock = sock
+        self._wlock = threading.Lock()
+        self._buf = b""
+        self.closed = False
+
+    @classmethod
+    def connect(cls, host: str, port: int, timeout: float = 60.0) -> "Channel":
+        end = time.time() + timeout
+        while True:
+            try:
+                s = socket.create_connection((host, port), timeout=5.0)
+                s.settimeout(None)
+                s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                return cls(s)
+            except OSError:
+                if time.time() > end:
+                    raise
+                time.sleep(0.1)
+
+    def fileno(self) -> int:
+        return self.sock.fileno()
+
+    def send(self, msg: Dict[str, Any]) -> None:
+        data = json.dumps(msg, allow_nan=True).encode()
+        with self._wlock:
+            self.sock.sendall(_HDR.pack(len(data)) + data)
+
+    def _read_exact(self, n: int, timeout: Optional[float]) -> Optional[bytes]:
+        while len(self._buf) < n:
+            if timeout is not None:
+                r, _, _ = select.select([self.sock], [], [], timeout)
+                if not r:
+                    return None
+            chunk = self.sock.recv(max(65536, n - len(self._buf)))
+            if not chunk:
+                self.closed = True
+                raise ChannelClosed("peer closed the channel")
+            self._buf += chunk
+        out, self._buf = self._buf[:n], self._buf[n:]
+        return out
+
+    def recv(self, timeout: Optional[float] = None) -> Optional[Dict[str, Any]]:
+        """Next message; None if ``timeout`` (seconds, 0 = poll) passed without a complete header.  Once a
+        header has arrived the body is read to completion.  Raises ChannelClosed at EOF."""
+        hdr = self._read_exact(_HDR.size, timeout)
+        if hdr is None:
+            return None
+        (n,) = _HDR.unpack(hdr)
+        body = self._read_exact(n, None)
+        return json.loads(body)
+
+    def close(self) -> None:
+        self.closed = True
+        try:
+            self.sock.close()
+        except OSError:
+            pass
+
+
+# ============================================================================ worker side
+@dataclass
+class _Bracket:
+    key: str
+    manager: Any                      # HyperbandSearchManager of the owning group (reference-exact arithmetic)
+    iteration: int                    # Hyperband iteration = bracket index (bracket s = s_max - iteration)
+    configs: Dict[int, Dict[str, Any]]
+    resource_name: str
+    resource: Any                     # ResourceConfig (cast_value)
+    maximize: bool
+    resume: bool
+    seed: int
+    rules: List[Tuple[int, float, bool]] = field(default_factory=list)   # early stopping on the program metric
+    rung: int = 0
+    active: List[int] = field(default_factory=list)
+    prev_r: Dict[int, float] = field(default_factory=dict)
+    stopped: bool = False
+    early_stopped: bool = False
+
+
+class ResidentWorker:
+    """The GPU side.  Owns one TrialProgram; runs the brackets it is handed, in rounds."""
+
+    def __init__(self, program: str, params: Optional[Dict[str, Any]] = None, device=None, max_active: int = 8):
+        self.program_name = program
+        self.params = dict(params or {})
+        self.device = device
+        self.max_active = max(1, int(max_active))
+        self.program = None
+        self.queue: List[_Bracket] = []
+        self.active: List[_Bracket] = []
+        self.pause_tag: Optional[str] = None
+        self.metrics = None
+        self.stats = {"trials": 0, "train_steps": 0, "rounds": 0, "topk_launches": 0, "early_stop_launches": 0}
+        self._base_ev = None
+        self._base_wall = 0.0
+        self._shutdown: Optional[str] = None
+
+    # ------------------------------------------------------------------ build
+    def build(self) -> Dict[str, Any]:
+        import torch
+
+        from polyaxon_amd.polyflow.programs import build_program
+        from polyaxon_amd.polytune.kernels import BracketMetrics
+
+        t0 = time.time()
+        if self.device is None:
+            self.device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        self.program = build_program(self.program_name, self.params, self.device)
+        self.program.warm()
+        ex = self.program.executor
+        self.metrics = BracketMetrics(self.max_active, 32, ex.device)
+        self._reset_clock()
+        return {"ev": "ready", "program": self.program_name, "device": str(ex.device), "pid": os.getpid(),
+                "build_s": round(time.time() - t0, 3), "snapshot_bytes": ex.snapshot_bytes(),
+                "metric": self.program.metric, "unit_steps": self.program.unit_steps, "info": self.program.info,
+                "device_name": torch.cuda.get_device_name(ex.device) if ex.is_cuda else "cpu"}
+
+    def _reset_clock(self) -> None:
+        import torch
+
+        ex = self.program.executor
+        if ex.is_cuda:
+            torch.cuda.synchronize(ex.device)
+            self._base_ev = torch.cuda.Event(enable_timing=True)
+            self._base_ev.record()
+            torch.cuda.synchronize(ex.device)
+        self._base_wall = time.time()
+
+    def _event(self):
+        import torch
+
+        if not self.program.executor.is_cuda:
+            return time.time()
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def _wall(self, ev) -> float:
+        if isinstance(ev, float):
+            return ev
+        return self._base_wall + self._base_ev.elapsed_time(ev) / 1000.0
+
+    # ------------------------------------------------------------------ messages
+    def handle(self, msg: Dict[str, Any], chan: Channel) -> Optional[str]:
+        op = msg.get("op")
+        if op == "bracket":
+            self.queue.append(self._make_bracket(msg))
+        elif op == "stop_bracket":
+            for br in list(self.queue):
+                if br.key == msg["key"]:
+                    self.queue.remove(br)
+                    chan.send({"ev": "bracket_done", "key": br.key, "status": "stopped"})
+            for br in self.active:
+                if br.key == msg["key"]:
+                    br.stopped = True
+        elif op == "pause":
+            self.pause_tag = str(msg.get("tag", ""))
+        elif op == "shutdown":
+            return "shutdown"
+        elif op == "ping":
+            chan.send({"ev": "pong", "stats": dict(self.stats)})
+        elif op == "init":
+            if msg.get("program") != self.program_name:
+                chan.send({"ev": "error", "fatal": True,
+                           "message": f"worker runs {self.program_name}, asked for {msg.get('program')}"})
+                return "shutdown"
+            chan.send(self._ready_info)
+        else:
+            chan.send({"ev": "error", "fatal": False, "message": f"unknown op {op!r}"})
+        return None
+
+    def _make_bracket(self, msg: Dict[str, Any]) -> _Bracket:
+        from polyaxon_amd.polytune.managers import HyperbandSearchManager
+        from polyaxon_amd.spec.hptuning import HPTuningConfig, Optimization
+
+        hp = HPTuningConfig.from_dict(msg["hptuning"])
+        hb = hp.hyperband
+        m = HyperbandSearchManager(hp)
+        rules = []
+        for r in msg.get("early_stopping") or []:
+            if r["metric"] == self.program.metric:
+                rules.append((0, float(r["value"]), Optimization.maximize(r["optimization"])))
+        if hb.metric.name != self.program.metric:
+            raise ValueError(f"hyperband metric {hb.metric.name!r} is not what program {self.program_name} "
+                             f"reports ({self.program.metric!r})")
+        configs = {int(c["cid"]): dict(c["params"]) for c in msg["configs"]}
+        br = _Bracket(key=msg["key"], manager=m, iteration=int(msg["iteration"]), configs=configs,
+                      resource_name=hb.resource.name, resource=hb.resource,
+                      maximize=Optimization.maximize(hb.metric.optimization), resume=hb.resume,
+                      seed=int(msg.get("seed", 0)), rules=rules)
+        br.active = sorted(configs)
+        return br
+
+    # ------------------------------------------------------------------ serve loop
+    def serve(self, chan: Channel) -> str:
+        """Process messages and run rounds until paused (returns ``pause:<tag>``), shut down or disconnected."""
+        self._ready_info = getattr(self, "_ready_info", None) or {"ev": "ready", "program": self.program_name}
+        while True:
+            busy = bool(self.active or self.queue)
+            try:
+                msg = chan.recv(timeout=0 if busy else (None if self.pause_tag is None else 0))
+            except ChannelClosed:
+                return "eof"
+            if msg is not None:
+                try:
+                    r = self.handle(msg, chan)
+                except Exception as e:  # bad bracket message: report, keep serving
+                    chan.send({"ev": "error", "fatal": False, "key": msg.get("key"), "message": repr(e),
+                               "traceback": traceback.format_exc()})
+                    if msg.get("op") == "bracket":
+                        chan.send({"ev": "bracket_done", "key": msg.get("key"), "status": "failed"})
+                    r = None
+                if r is not None:
+                    return r
+                continue
+            if self.active or self.queue:
+                self._shutdown = None
+                self.run_round(chan)
+                if self._shutdown is not None:
+                    return self._shutdown
+            elif self.pause_tag is not None:
+                tag, self.pause_tag = self.pause_tag, None
+                chan.send({"ev": "paused", "tag": tag, "stats": dict(self.stats)})
+                return f"pause:{tag}"
+
+    def _poll_control(self, chan: Channel) -> None:
+        """Between trials: take in new brackets, stop requests and pauses without blocking, in arrival order
+        (a shutdown is honoured at the end of the round)."""
+        while True:
+            try:
+                msg = chan.recv(timeout=0)
+            except ChannelClosed:
+                self._shutdown = "eof"
+                return
+            if msg is None:
+                return
+            try:
+                r = self.handle(msg, chan)
+            except Exception as e:
+                chan.send({"ev": "error", "fatal": False, "key": msg.get("key"), "message": repr(e),
+                           "traceback": traceback.format_exc()})
+                if msg.get("op") == "bracket":
+                    chan.send({"ev": "bracket_done", "key": msg.get("key"), "status": "failed"})
+                r = None
+            if r is not None:
+                self._shutdown = r
+
+    # ------------------------------------------------------------------ one round
+    def run_round(self, chan: Channel) -> None:
+        import torch
+
+        from polyaxon_amd.polytune.kernels import BracketMetrics, early_stop_any
+
+        while len(self.active) < self.max_active and self.queue:
+            self.active.append(self.queue.pop(0))
+        brs = list(self.active)
+        ex = self.program.executor
+        width = max(len(br.active) for br in brs)
+        if self.metrics.values.shape[1] < width or self.metrics.values.shape[0] < len(brs):
+            self.metrics = BracketMetrics(max(self.max_active, len(brs)), max(width, self.metrics.values.shape[1]),
+                                          ex.device)
+        for row, br in enumerate(brs):
+            self.metrics.reset_bracket(row, len(br.active))
+        records = []
+        for row, br in enumerate(brs):
+            m = br.manager
+            r = br.resource.cast_value(m.get_n_resources_for_iteration(br.iteration, br.rung))
+            more = m.get_n_config_to_keep_for_iteration(br.iteration, br.rung) > 0
+            for slot, cid in enumerate(br.active):
+                self._poll_control(chan)
+                if br.stopped:
+                    break
+                params = dict(br.configs[cid])
+                params[br.resource_name] = r
+                chan.send({"ev": "trial_start", "key": br.key, "rung": br.rung, "cid": cid, "params": params,
+                           "t": time.time()})
+                t_start = self._event()
+                if br.resume and br.rung > 0 and cid in br.prev_r:
+                    ex.restore((br.key, cid))
+                    steps = int(round((r - br.prev_r[cid]) * self.program.unit_steps))
+                else:
+                    ex.reset(seed=(br.seed * 1000003 + br.iteration * 1009 + cid) & 0x7FFFFFFF)
+                    steps = int(round(r * self.program.unit_steps))
+                ex.set_hparams(**{k: v for k, v in params.items() if k in self.program.hp_keys})
+                ex.run(steps)
+                ex.commit(self.metrics.values[row], slot, self.program.window)
+                if br.resume and more:
+                    ex.snapshot((br.key, cid))
+                records.append((row, br, slot, cid, steps, t_start, self._event()))
+        # ---- the round's decision: one top-k launch per optimisation direction over every active bracket
+        n = len(brs)
+        vals_dev = self.metrics.values[:n]
+        orders = {}
+        for mx in sorted({br.maximize for br in brs}):
+            orders[mx] = self.metrics.order(mx, rows=n)
+            self.stats["topk_launches"] += 1
+        early = {}
+        by_rules: Dict[Tuple, List[int]] = {}
+        for row, br in enumerate(brs):
+            if br.rules:
+                by_rules.setdefault(tuple(br.rules), []).append(row)
+        for rules, rows in by_rules.items():
+            idx = torch.tensor(rows, device=vals_dev.device)
+            flags = early_stop_any(vals_dev.index_select(0, idx).reshape(-1, 1), list(rules))
+            self.stats["early_stop_launches"] += 1
+            for row in rows:
+                early[row] = any(flags)
+        vals = vals_dev.detach().cpu().tolist()          # the round's one D2H read (synchronises)
+        orders_h = {mx: o[:n].cpu().tolist() for mx, o in orders.items()}
+        for row, br, slot, cid, steps, t0, t1 in records:
+            v = vals[row][slot]
+            self.stats["trials"] += 1
+            self.stats["train_steps"] += steps
+            chan.send({"ev": "trial_end", "key": br.key, "rung": br.rung, "cid": cid, "steps": steps,
+                       "metric": None if math.isnan(v) else v, "t_start": self._wall(t0), "t_end": self._wall(t1)})
+        self.stats["rounds"] += 1
+        for row, br in enumerate(brs):
+            m = br.manager
+            ran = [rec for rec in records if rec[1] is br]
+            metrics = [[cid, vals[row][slot]] for (_, _, slot, cid, _, _, _) in ran if not math.isnan(vals[row][slot])]
+            keep = m.get_n_config_to_keep_for_iteration(br.iteration, br.rung)
+            ranked = [br.active[i] for i in orders_h[br.maximize][row]
+                      if 0 <= i < len(br.active) and not math.isnan(vals[row][i])]
+            br.early_stopped = br.early_stopped or early.get(row, False)
+            stop = br.stopped or br.early_stopped or len(ran) < len(br.active)
+            promoted = [] if stop else ranked[:keep]
+            chan.send({"ev": "rung_done", "key": br.key, "rung": br.rung, "metrics": metrics, "promoted": promoted,
+                       "early_stop": br.early_stopped})
+            for cid in br.active:
+                if cid not in promoted:
+                    ex.drop((br.key, cid))
+            if promoted:
+                br.prev_r = {cid: br.resource.cast_value(m.get_n_resources_for_iteration(br.iteration, br.rung))
+                             for cid in promoted}
+                br.active = promoted
+                br.rung += 1
+            else:
+                self.active.remove(br)
+                status = "stopped" if (br.stopped or br.early_stopped) else "succeeded"
+                chan.send({"ev": "bracket_done", "key": br.key, "status": status})
+
+
+def serve_forever(worker: ResidentWorker, chan: Channel) -> str:
+    """Worker process main loop: first message must be ``init``; then serve until shutdown / EOF."""
+    msg = chan.recv()
+    if msg is None or msg.get("op") != "init":
+        chan.send({"ev": "error", "fatal": True, "message": "expected init"})
+        return "error"
+    worker.program_name = msg.get("program", worker.program_name)
+    worker.params = dict(msg.get("params") or {})
+    worker.max_active = int(msg.get("max_active", worker.max_active))
+    try:
+        worker._ready_info = worker.build()
+    except Exception as e:
+        chan.send({"ev": "error", "fatal": True, "message": f"program build failed: {e!r}",
+                   "traceback": traceback.format_exc()})
+        return "error"
+    chan.send(worker._ready_info)
+    while True:
+        r = worker.serve(chan)
+        if r in ("shutdown", "eof"):
+            return r
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="polyaxon_amd.polyflow.resident")
+    ap.add_argument("--fd", type=int, help="inherited connected socket")
+    ap.add_argument("--connect", help="host:port of the scheduler")
+    ap.add_argument("--cpu", action="store_true")
+    args = ap.parse_args(argv)
+    if args.fd is not None:
+        chan = Channel(socket.socket(fileno=args.fd))
+    elif args.connect:
+        host, _, port = args.connect.rpartition(":")
+        chan = Channel.connect(host, int(port))
+    else:
+        ap.error("need --fd or --connect")
+    device = "cpu" if args.cpu or os.environ.get("PLX_CPU_ONLY") == "1" else None
+    worker = ResidentWorker("", device=device)
+    r = serve_forever(worker, chan)
+    chan.close()
+    return 0 if r in ("shutdown", "eof") else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -85,6 +85,8 @@ class Run:
     extra_env: Dict[str, str] = field(default_factory=dict)
     on_done: List[Callable[[str], None]] = field(default_factory=list)
     attempt: int = 0  # opt-in retries (environment.max_restarts)
+    alloc_owners: List[str] = field(default_factory=list)  # allocator owners of the current placement
+    waiting_since: Optional[float] = None  # first time a gang failed to place (gang reservation)
 
     @property
     def owner(self) -> str:
@@ -186,6 +188,21 @@ class Polyflow:
         self._last_exit_t: Optional[float] = None
         self.reconcile_s = reconcile_s
         self.health_check = health_check  # () -> indices of unhealthy devices (amd-smi RAS/ECC watchdog)
+        self._pool = None  # resident executors (polyflow/pool.py), created on first use
+
+    def resident_pool(self):
+        """The pool of warm resident trial executors (scheduler thread only)."""
+        if self._pool is None:
+            from polyaxon_amd.polyflow.pool import ResidentPool
+
+            idle = self.settings.get("scheduler.resident_idle_s") if self.settings is not None else 300.0
+            self._pool = ResidentPool(self, idle_s=float(idle))
+        return self._pool
+
+    def attach_resident(self, chan, device: int, program: str, params=None, max_active: int = 8) -> int:
+        """Register an already running resident executor that owns ``device`` (bench.py ranks, external
+        launchers).  Returns its worker id."""
+        return self.call(lambda: self.resident_pool().attach(chan, device, program, params, max_active).wid)
 
     # ================================================================== lifecycle of the scheduler itself
     def start(self) -> "Polyflow":
@@ -214,6 +231,8 @@ class Polyflow:
             end = time.time() + timeout
             while time.time() < end and self.call(lambda: any(r.active for r in self.runs.values())):
                 time.sleep(0.05)
+        if self._pool is not None:
+            self.call(self._pool.close, timeout=timeout + 5)
         self._running = False
         self.pm.wake()
         self._thread.join(timeout=timeout)
@@ -323,6 +342,14 @@ class Polyflow:
             return {"kind": "experiment", "id": xid}
         if spec.kind == Kinds.GROUP:
             from polyaxon_amd.polyflow.groups import make_group_driver
+
+            ex = spec.environment.executor
+            if ex is not None and ex.resident:
+                if spec.search_algorithm != "hyperband":
+                    raise PolyaxonfileError(f"resident executors run hyperband groups; {spec.search_algorithm} "
+                                            "groups use executor: process")
+                if spec.resources is not None and spec.resources.gpu is not None and spec.resources.gpu.value > 1:
+                    raise PolyaxonfileError("a resident executor runs on one device (resources.gpu <= 1)")
 
             gid = self.store.create_group(proj["id"], spec.raw_data, spec.hptuning.to_dict(), user=user,
                                           name=name or spec.name, description=description, tags=spec.tags,
@@ -536,38 +563,96 @@ class Polyflow:
         return reqs
 
     def _schedule(self) -> None:
+        """Place pending runs in FIFO order.  A run that cannot be placed is kept in order; once the oldest
+        waiting gang (a multi-device run) has waited ``scheduler.gang_reserve_s``, smaller runs behind it may only
+        use devices the gang cannot need (gang reservation -- a stream of 1-GPU trials cannot starve a DP=8 run)."""
         if not self.pending:
             return
         still: Deque[str] = deque()
-        while self.pending:
-            owner = self.pending.popleft()
-            run = self.runs.get(owner)
-            if run is None or run.final_status is not None or run.stop_requested:
-                continue
-            if not self._try_place(run):
-                still.append(owner)
-        self.pending = still
+        reserve = self._gang_reservation()
+        try:
+            while self.pending:
+                owner = self.pending.popleft()
+                run = self.runs.get(owner)
+                if run is None or run.final_status is not None or run.stop_requested:
+                    continue
+                try:
+                    placed = self._try_place(run, reserve)
+                except Exception as e:  # never lose the run (or the queue behind it) to a placement error
+                    log.exception("placement of %s failed", owner)
+                    self._release_run(run)
+                    self._finish_unstarted(run, "failed", f"placement failed: {e}")
+                    placed = True
+                if not placed:
+                    still.append(owner)
+        finally:
+            still.extend(self.pending)
+            self.pending = still
 
-    def _try_place(self, run: Run) -> bool:
+    def _gang_reservation(self) -> Optional[Tuple[str, int]]:
+        """(owner, devices) of the gang that holds a reservation, if one has waited long enough."""
+        wait = self.settings.get("scheduler.gang_reserve_s") if self.settings is not None else 30.0
+        now = time.time()
+        for owner in self.pending:
+            run = self.runs.get(owner)
+            if run is None or run.final_status is not None:
+                continue
+            whole = sum(int(round(g)) for _, _, g in self._requirements(run) if g >= 1.0 - 1e-9)
+            if whole > 1:
+                run.waiting_since = run.waiting_since or now
+                if now - run.waiting_since >= wait:
+                    return owner, whole
+                return None  # only the oldest gang may reserve
+        return None
+
+    def _try_place(self, run: Run, reserve: Optional[Tuple[str, int]] = None) -> bool:
         reqs = self._requirements(run)
         need = [g for _, _, g in reqs]
         if any(g > self.alloc.n_devices + 1e-9 for g in need) or sum(g for g in need if g >= 1) > self.alloc.n_devices:
             self._finish_unstarted(run, "failed", f"requests {need} GPUs but the node has {self.alloc.n_devices}")
             return True
+        if reserve is not None and reserve[0] != run.owner and any(g > 0 for g in need):
+            # keep enough whole devices free for the reserved gang: placing this run must leave them idle
+            free_whole = len(self.alloc.free_whole())
+            mine = sum(int(round(g)) if g >= 1 else 0 for g in need)
+            frac = any(0 < g < 1 for g in need)
+            if free_whole - mine - (1 if frac and not self._fraction_fits_shared(need) else 0) < reserve[1]:
+                return False
         taken: List[str] = []
         devices: List[List[int]] = []
-        for (role, idx, g) in reqs:
-            owner = f"{run.owner}:{role}.{idx}"
-            a = self.alloc.allocate(owner, g) if g > 0 else None
-            if g > 0 and a is None:
-                for o in taken:
-                    self.alloc.release(o)
-                return False
-            if a is not None:
-                taken.append(owner)
-            devices.append(a.devices if a else [])
+        hbm = run.spec.resources.hbm_gb if run.spec.resources is not None else 0.0
+        try:
+            for (role, idx, g) in reqs:
+                owner = f"{run.owner}:{role}.{idx}"
+                a = self.alloc.allocate(owner, g, hbm) if g > 0 else None
+                if g > 0 and a is None:
+                    for o in taken:
+                        self.alloc.release(o)
+                    return False
+                if a is not None:
+                    taken.append(owner)
+                devices.append(a.devices if a else [])
+        except Exception:
+            for o in taken:
+                self.alloc.release(o)
+            raise
+        run.alloc_owners = list(taken)
         self._spawn(run, reqs, devices)
         return True
+
+    def _fraction_fits_shared(self, need) -> bool:
+        """Would the run's fractional replicas fit on devices that already have fractional tenants?"""
+        for g in need:
+            if 0 < g < 1 and not any(d.healthy and 0 < d.share_used and d.share_free >= g - 1e-9
+                                     for d in self.alloc.devices):
+                return False
+        return True
+
+    def _release_run(self, run: Run) -> None:
+        """Release every device allocation the run holds (spawn failures, retries, final states)."""
+        for o in getattr(run, "alloc_owners", []) or []:
+            self.alloc.release(o)
+        run.alloc_owners = []
 
     def _finish_unstarted(self, run: Run, status: str, message: str) -> None:
         run.final_status = status
@@ -652,7 +737,16 @@ class Polyflow:
                 pid = self.pm.spawn(argv, env, cwd=run.cwd, log_path=log_path)
             except OSError as e:
                 rep.done = True
+                # replicas after this one were never spawned: release their devices now (they have no pid,
+                # so no exit will ever release them)
+                for (r2, i2, _g2) in reqs[len(run.replicas):]:
+                    self.alloc.release(f"{run.owner}:{r2}.{i2}")
+                self.alloc.release(f"{run.owner}:{role}.{idx}")
+                self.store.add_cluster_event("spawn_failure", "error", f"{run.owner} {role}.{idx}: {e}",
+                                             {"owner": run.owner, "role": role, "index": idx})
                 self._replica_status(run, rep, "failed", f"spawn failed: {e}")
+                run.final_status = "failed"
+                run.final_message = f"{role}.{idx} spawn failed: {e}"
                 self._stop_run(run, f"replica {role}.{idx} failed to start")
                 self._maybe_finalize(run)
                 return
@@ -748,6 +842,7 @@ class Polyflow:
     def _maybe_finalize(self, run: Run) -> None:
         if any(not r.done for r in run.replicas):
             return
+        self._release_run(run)
         if run.final_status is None:
             run.final_status = "stopped" if run.stop_requested else "succeeded"
         status = run.final_status

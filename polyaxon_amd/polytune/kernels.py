@@ -8,7 +8,7 @@ parity reference for the GPU tests.
 from __future__ import annotations
 
 import math
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -20,16 +20,19 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def topk_order(metrics: torch.Tensor, counts: torch.Tensor, maximize: bool) -> torch.Tensor:
+def topk_order(metrics: torch.Tensor, counts: torch.Tensor, maximize: bool,
+               host_counts: Optional[Sequence[int]] = None) -> torch.Tensor:
     """Per-row stable ordering (best first) of the first ``counts[b]`` entries of ``metrics[b]``.
-    NaN entries sort last; slots beyond ``counts[b]`` are -1."""
+    NaN entries sort last; slots beyond ``counts[b]`` are -1.  ``host_counts`` (the same counts, known on the
+    host) lets the bound check skip a device->host read, so the launch does not synchronise."""
     if metrics.dim() != 2:
         raise ValueError("metrics must be [brackets, configs]")
     B, C = metrics.shape
     if metrics.is_cuda:
         metrics = metrics.contiguous().float()
         counts = counts.to(device=metrics.device, dtype=torch.int32).contiguous()
-        if counts.numel() != B or int(counts.max().item() if B else 0) > C:
+        top = max(host_counts, default=0) if host_counts is not None else int(counts.max().item() if B else 0)
+        if counts.numel() != B or top > C:
             raise ValueError("counts must have one entry <= configs per bracket")
         order = torch.empty((B, C), dtype=torch.int32, device=metrics.device)
         rc = _native.lib("plx_polytune").plx_topk_brackets(
@@ -108,5 +111,7 @@ class BracketMetrics:
     def slot_ptr(self, b: int) -> int:
         return self.values[b].data_ptr()
 
-    def order(self, maximize: bool) -> torch.Tensor:
-        return topk_order(self.values, self.counts, maximize)
+    def order(self, maximize: bool, rows: Optional[int] = None) -> torch.Tensor:
+        """One launch over the first ``rows`` brackets (all by default)."""
+        n = self.values.shape[0] if rows is None else rows
+        return topk_order(self.values[:n], self.counts[:n], maximize, host_counts=self._host_counts[:n])

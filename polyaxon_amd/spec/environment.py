@@ -51,19 +51,36 @@ class PodResources:
     cpu: Optional[ResourceSpec] = None
     memory: Optional[ResourceSpec] = None
     gpu: Optional[ResourceSpec] = None
+    # MI355X extension: HBM budget (GB) a replica reserves on each of its devices, so fractional-GPU trials
+    # (``gpu: 0.25``) are packed by memory as well as by compute share (288 GB per MI355X)
+    hbm: Optional[ResourceSpec] = None
+
+    KEYS = ("cpu", "memory", "gpu", "hbm")
 
     @classmethod
     def from_dict(cls, d):
         if not d:
             return None
-        unknown = set(d) - {"cpu", "memory", "gpu"}
+        unknown = set(d) - set(cls.KEYS)
         if unknown:
             raise MatrixValidationError(f"unknown resources {sorted(unknown)}")
-        return cls(cpu=ResourceSpec.from_dict(d.get("cpu")), memory=ResourceSpec.from_dict(d.get("memory")),
-                   gpu=ResourceSpec.from_dict(d.get("gpu")))
+        out = cls(cpu=ResourceSpec.from_dict(d.get("cpu")), memory=ResourceSpec.from_dict(d.get("memory")),
+                  gpu=ResourceSpec.from_dict(d.get("gpu")), hbm=ResourceSpec.from_dict(d.get("hbm")))
+        if out.gpu is not None:
+            g = out.gpu.value
+            if g < 0 or (g > 1 and abs(g - round(g)) > 1e-9):
+                # a fraction shares one device; more than one device is a gang of whole devices
+                raise MatrixValidationError(f"resources.gpu must be a fraction <= 1 or a whole number, got {g}")
+        if out.hbm is not None and out.hbm.value < 0:
+            raise MatrixValidationError("resources.hbm must be >= 0 (GB)")
+        return out
 
     def to_dict(self):
-        return {k: getattr(self, k).to_dict() for k in ("cpu", "memory", "gpu") if getattr(self, k) is not None}
+        return {k: getattr(self, k).to_dict() for k in self.KEYS if getattr(self, k) is not None}
+
+    @property
+    def hbm_gb(self) -> float:
+        return self.hbm.value if self.hbm else 0.0
 
     @property
     def gpus(self) -> int:
@@ -82,7 +99,7 @@ class PodResources:
             return ResourceSpec(requests=total(a.requests, b.requests), limits=total(a.limits, b.limits))
 
         return PodResources(cpu=add(self.cpu, other.cpu), memory=add(self.memory, other.memory),
-                            gpu=add(self.gpu, other.gpu))
+                            gpu=add(self.gpu, other.gpu), hbm=add(self.hbm, other.hbm))
 
 
 @dataclass
@@ -173,6 +190,58 @@ class FrameworkSpec:
 
 
 @dataclass
+class ExecutorSpec:
+    """``environment.executor`` (MI355X extension): how polyflow runs the trials of an experiment or group.
+
+    * ``kind: process`` (default) -- every experiment is a fresh process tree running ``run.cmd``, exactly the
+      reference's one-pod-per-trial model.
+    * ``kind: resident`` -- trials run on warm resident executors (polyflow/resident.py): one long-lived worker
+      process per GPU holds the model, its flat weights, the captured step and the HBM snapshots, and receives
+      trials over a socket.  ``program`` names the trial program (polyflow/programs.py registry or
+      ``module:callable``), ``params`` are its build arguments (batch, image size, ``unit_steps`` = training steps
+      per Hyperband resource unit ...), ``max_active_brackets`` bounds how many brackets one executor
+      interleaves (each keeps its promotion snapshots in HBM).
+    """
+    kind: str = "process"
+    program: Optional[str] = None
+    params: Dict[str, Any] = field(default_factory=dict)
+    max_active_brackets: int = 8
+
+    @classmethod
+    def from_dict(cls, d):
+        if d is None:
+            return None
+        if isinstance(d, str):
+            d = {"kind": d}
+        unknown = set(d) - {"kind", "program", "params", "max_active_brackets"}
+        if unknown:
+            raise MatrixValidationError(f"unknown executor keys {sorted(unknown)}")
+        kind = d.get("kind", "process")
+        if kind not in ("process", "resident"):
+            raise MatrixValidationError(f"executor.kind must be process or resident, got {kind!r}")
+        if kind == "resident" and not d.get("program"):
+            raise MatrixValidationError("a resident executor needs `program`")
+        n = int(d.get("max_active_brackets", 8))
+        if n < 1:
+            raise MatrixValidationError("executor.max_active_brackets must be >= 1")
+        return cls(kind=kind, program=d.get("program"), params=dict(d.get("params") or {}), max_active_brackets=n)
+
+    def to_dict(self):
+        out: Dict[str, Any] = {"kind": self.kind}
+        if self.program:
+            out["program"] = self.program
+        if self.params:
+            out["params"] = dict(self.params)
+        if self.max_active_brackets != 8:
+            out["max_active_brackets"] = self.max_active_brackets
+        return out
+
+    @property
+    def resident(self) -> bool:
+        return self.kind == "resident"
+
+
+@dataclass
 class EnvironmentSpec:
     resources: Optional[PodResources] = None
     outputs: Dict[str, List[Any]] = field(default_factory=dict)
@@ -189,6 +258,7 @@ class EnvironmentSpec:
     heartbeat_timeout: Optional[float] = None
     # wrap every replica in `rocprofv3 --kernel-trace --stats` (outputs/rocprof/<role>.<index>)
     profile: bool = False
+    executor: Optional[ExecutorSpec] = None
 
     @classmethod
     def from_dict(cls, d: Optional[Dict[str, Any]]):
@@ -197,7 +267,7 @@ class EnvironmentSpec:
         if len(fws) > 1:
             raise MatrixValidationError(f"environment defines more than one framework: {fws}")
         known = {"resources", "outputs", "persistence", "node_selector", "tolerations", "affinity", "secret_refs",
-                 "configmap_refs", "env_vars", "max_restarts", "heartbeat_timeout", "profile", *FRAMEWORKS}
+                 "configmap_refs", "env_vars", "max_restarts", "heartbeat_timeout", "profile", "executor", *FRAMEWORKS}
         unknown = set(d) - known
         if unknown:
             raise MatrixValidationError(f"unknown environment keys {sorted(unknown)}")
@@ -215,7 +285,8 @@ class EnvironmentSpec:
                    framework=FrameworkSpec.from_dict(fws[0], d[fws[0]]) if fws else None,
                    max_restarts=int(d.get("max_restarts") or 0),
                    heartbeat_timeout=float(d["heartbeat_timeout"]) if d.get("heartbeat_timeout") else None,
-                   profile=bool(d.get("profile", False)))
+                   profile=bool(d.get("profile", False)),
+                   executor=ExecutorSpec.from_dict(d.get("executor")))
 
     def to_dict(self):
         out: Dict[str, Any] = {}
@@ -235,4 +306,6 @@ class EnvironmentSpec:
             out["heartbeat_timeout"] = self.heartbeat_timeout
         if self.profile:
             out["profile"] = True
+        if self.executor is not None:
+            out["executor"] = self.executor.to_dict()
         return out

@@ -257,8 +257,9 @@ class ExperimentSpecification(BaseSpecification):
         super()._parse(d)
         if d.get("hptuning") is not None:
             raise PolyaxonfileError("an experiment cannot define `hptuning`; use kind: group")
-        if self.run is None and d.get("model") is None:
-            raise PolyaxonfileError("an experiment requires a `run` section")
+        ex = self.environment.executor
+        if self.run is None and d.get("model") is None and not (ex is not None and ex.resident):
+            raise PolyaxonfileError("an experiment requires a `run` section (or `environment.executor: resident`)")
 
 
 class JobSpecification(BaseSpecification):

@@ -1,0 +1,315 @@
+"""Resident executors inside polyflow (polyflow/resident.py, pool.py, groups.ResidentHyperbandDriver) on CPU.
+
+The reference runs every Hyperband trial as a pod and reduces rungs with a Python sort after a 30 s poll
+(polyaxon/hpsearch/tasks/hyperband.py:7-83, iteration_managers/hyperband.py:52-113).  These tests check that the
+resident path keeps the reference's observable semantics -- same suggestions, same bracket/rung arithmetic,
+promotions = top-k of the rung, RESUME clones, FSM history per trial, iteration rows -- while running brackets
+concurrently on warm executors.
+"""
+import math
+import os
+import socket
+import subprocess
+import sys
+import threading
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _hp(seed=3, max_iter=9, eta=3, resume=True, concurrency=2, early=None):
+    hp = {"seed": seed, "concurrency": concurrency,
+          "hyperband": {"max_iter": max_iter, "eta": eta, "resource": {"name": "units", "type": "int"},
+                        "metric": {"name": "loss", "optimization": "minimize"}, "resume": resume},
+          "matrix": {"lr": {"loguniform": [-4, -1]}, "momentum": {"uniform": [0.8, 0.95]}}}
+    if early:
+        hp["early_stopping"] = early
+    return hp
+
+
+TINY = {"unit_steps": 1, "batch": 4, "image": 16, "grid": 4}
+
+
+def _group(**kw):
+    params = kw.pop("params", TINY)
+    return {"version": 1, "kind": "group", "project": "rt", "hptuning": _hp(**kw),
+            "environment": {"resources": {"gpu": 1},
+                            "executor": {"kind": "resident", "program": "resnet_tiny", "params": params}}}
+
+
+def test_channel_roundtrip():
+    from polyaxon_amd.polyflow.resident import Channel, ChannelClosed
+
+    a, b = socket.socketpair()
+    ca, cb = Channel(a), Channel(b)
+    assert cb.recv(timeout=0) is None
+    big = {"x": list(range(20000)), "s": "é" * 100, "nan": float("nan")}
+    ca.send({"op": "ping"})
+    ca.send(big)
+    assert cb.recv() == {"op": "ping"}
+    got = cb.recv()
+    assert got["x"] == big["x"] and got["s"] == big["s"] and math.isnan(got["nan"])
+    ca.close()
+    with pytest.raises(ChannelClosed):
+        cb.recv()
+
+
+def test_bracket_units_follow_reference_arithmetic():
+    from polyaxon_amd.polyflow.programs import bracket_units
+    from polyaxon_amd.polytune.managers import HyperbandSearchManager
+    from polyaxon_amd.spec.hptuning import HPTuningConfig
+
+    for max_iter, eta, resume in ((9, 3, True), (9, 3, False), (81, 3, True), (10, 3, False), (27, 3, True)):
+        m = HyperbandSearchManager(HPTuningConfig.from_dict(_hp(max_iter=max_iter, eta=eta, resume=resume)))
+        for it in range(m.s_max + 1):
+            # walk the reference state machine for this bracket
+            n, rung, total, prev = m.get_n_configs(m.get_bracket(it)), 0, 0.0, 0.0
+            while n > 0:
+                r = m.get_n_resources_for_iteration(it, rung)
+                total += n * ((r - prev) if (resume and rung) else r)
+                prev = r
+                n = m.get_n_config_to_keep_for_iteration(it, rung)
+                rung += 1
+            assert bracket_units(max_iter, eta, it, resume) == pytest.approx(total)
+
+
+def _worker_thread(program="resnet_tiny", params=TINY, max_active=8):
+    from polyaxon_amd.polyflow.resident import Channel, ResidentWorker, serve_forever
+
+    a, b = socket.socketpair()
+    sched, wchan = Channel(a), Channel(b)
+    w = ResidentWorker(program, device="cpu", max_active=max_active)
+    t = threading.Thread(target=serve_forever, args=(w, wchan), daemon=True)
+    t.start()
+    sched.send({"op": "init", "program": program, "params": params, "max_active": max_active})
+    ready = sched.recv(timeout=120)
+    assert ready["ev"] == "ready", ready
+    return w, sched, t
+
+
+def _collect(sched, n_brackets, timeout=120):
+    evs = []
+    done = 0
+    end = time.time() + timeout
+    while done < n_brackets:
+        m = sched.recv(timeout=max(0.1, end - time.time()))
+        assert m is not None, "worker stalled"
+        evs.append(m)
+        if m["ev"] == "bracket_done":
+            done += 1
+        assert m["ev"] != "error", m
+    return evs
+
+
+def test_worker_runs_concurrent_brackets_with_reference_promotions():
+    from polyaxon_amd.polytune.managers import HyperbandIterationConfig, HyperbandSearchManager
+    from polyaxon_amd.spec.hptuning import HPTuningConfig
+
+    hp = _hp()
+    m = HyperbandSearchManager(HPTuningConfig.from_dict(hp))
+    w, sched, t = _worker_thread()
+    for it in range(m.s_max + 1):
+        sugg = m.get_suggestions(HyperbandIterationConfig(iteration=it))
+        sched.send({"op": "bracket", "key": f"b{it}", "hptuning": hp, "iteration": it, "seed": 5,
+                    "configs": [{"cid": i, "params": {k: v for k, v in s.items() if k != "units"}}
+                                for i, s in enumerate(sugg)]})
+    evs = _collect(sched, m.s_max + 1)
+    starts = [e for e in evs if e["ev"] == "trial_start"]
+    ends = [e for e in evs if e["ev"] == "trial_end"]
+    rungs = [e for e in evs if e["ev"] == "rung_done"]
+    assert len(starts) == len(ends) == 23  # 13 + 6 + 4 trials (reference arithmetic, incl. the s=0 reduction)
+    for e in rungs:
+        it = int(e["key"][1:])
+        keep = m.get_n_config_to_keep_for_iteration(it, e["rung"])
+        ranked = [c for c, v in sorted(e["metrics"], key=lambda cv: (cv[1], cv[0]))]
+        assert e["promoted"] == ranked[:keep]  # device top-k == reference sort + keep
+        # resources follow the reference schedule
+        res = {s["params"]["units"] for s in starts if s["key"] == e["key"] and s["rung"] == e["rung"]}
+        assert res == {int(m.get_n_resources_for_iteration(it, e["rung"]))}
+    # the brackets were interleaved: one decision launch per round covered all of them
+    assert w.stats["rounds"] < len(rungs)
+    assert w.stats["topk_launches"] == w.stats["rounds"]
+    # resumed trials train only the additional resource
+    by = {(e["key"], e["rung"], e["cid"]): e for e in ends}
+    for (key, rung, cid), e in by.items():
+        if rung:
+            it = int(key[1:])
+            extra = m.get_n_resources_for_iteration(it, rung) - m.get_n_resources_for_iteration(it, rung - 1)
+            assert e["steps"] == int(extra) * TINY["unit_steps"]
+    sched.send({"op": "shutdown"})
+    t.join(10)
+
+
+def test_worker_stop_bracket_and_pause():
+    from polyaxon_amd.polytune.managers import HyperbandIterationConfig, HyperbandSearchManager
+    from polyaxon_amd.spec.hptuning import HPTuningConfig
+
+    hp = _hp()
+    m = HyperbandSearchManager(HPTuningConfig.from_dict(hp))
+    w, sched, t = _worker_thread(max_active=1)
+    for it in range(2):
+        sugg = m.get_suggestions(HyperbandIterationConfig(iteration=it))
+        sched.send({"op": "bracket", "key": f"b{it}", "hptuning": hp, "iteration": it, "seed": 1,
+                    "configs": [{"cid": i, "params": {"lr": s["lr"], "momentum": s["momentum"]}}
+                                for i, s in enumerate(sugg)]})
+    sched.send({"op": "stop_bracket", "key": "b1"})  # still queued (max_active=1): stopped without running
+    sched.send({"op": "pause", "tag": "p"})
+    evs = _collect(sched, 2)
+    done = {e["key"]: e["status"] for e in evs if e["ev"] == "bracket_done"}
+    assert done == {"b0": "succeeded", "b1": "stopped"}
+    assert not any(e["ev"] == "trial_start" and e["key"] == "b1" for e in evs)
+    paused = sched.recv(timeout=30)
+    assert paused["ev"] == "paused" and paused["tag"] == "p"
+    sched.send({"op": "shutdown"})
+    t.join(10)
+
+
+def test_worker_early_stopping_on_device_metric():
+    from polyaxon_amd.polytune.managers import HyperbandIterationConfig, HyperbandSearchManager
+    from polyaxon_amd.spec.hptuning import HPTuningConfig
+
+    hp = _hp(early=[{"metric": "loss", "value": 100.0, "optimization": "minimize"}])  # trips on the first rung
+    m = HyperbandSearchManager(HPTuningConfig.from_dict(hp))
+    w, sched, t = _worker_thread()
+    sugg = m.get_suggestions(HyperbandIterationConfig(iteration=0))
+    sched.send({"op": "bracket", "key": "b0", "hptuning": hp, "iteration": 0, "seed": 1,
+                "early_stopping": hp["early_stopping"],
+                "configs": [{"cid": i, "params": {"lr": s["lr"]}} for i, s in enumerate(sugg)]})
+    evs = _collect(sched, 1)
+    rung = [e for e in evs if e["ev"] == "rung_done"]
+    assert len(rung) == 1 and rung[0]["early_stop"] and rung[0]["promoted"] == []
+    assert [e["status"] for e in evs if e["ev"] == "bracket_done"] == ["stopped"]
+    assert w.stats["early_stop_launches"] == 1
+    sched.send({"op": "shutdown"})
+    t.join(10)
+
+
+@pytest.fixture
+def cpu_pool_env(monkeypatch):
+    monkeypatch.setenv("PLX_NUM_GPUS", "2")
+    monkeypatch.setenv("PLX_CPU_ONLY", "1")
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
+
+
+def test_polyflow_resident_group_end_to_end(tmp_path, cpu_pool_env):
+    from polyaxon_amd.polyflow.scheduler import Polyflow
+
+    with Polyflow(str(tmp_path), reconcile_s=0) as flow:
+        r = flow.submit(_group())
+        assert flow.wait("group", r["id"], timeout=300) == "succeeded"
+        st = flow.store
+        xs = st.list_experiments(group_id=r["id"])
+        assert len(xs) == 23 and {x["status"] for x in xs} == {"succeeded"}
+        for x in xs:
+            assert [s["status"] for s in st.experiment_statuses(x["id"])] == [
+                "created", "scheduled", "starting", "running", "succeeded"]
+            assert "loss" in x["last_metric"] and x["started_at"] <= x["finished_at"]
+            jobs = st.experiment_jobs(x["id"])
+            assert len(jobs) == 1 and jobs[0]["status"] == "succeeded" and jobs[0]["devices"] in ([0], [1])
+        resumed = [x for x in xs if x["cloning_strategy"] == "resume"]
+        assert len(resumed) == 6
+        for x in resumed:  # RESUME: same outputs as the root, one more resource level
+            orig = st.get_experiment(x["original_experiment_id"])
+            assert x["declarations"]["units"] > orig["declarations"]["units"]
+            assert x["outputs_path"] == orig["outputs_path"] or orig["cloning_strategy"] == "resume"
+            assert x["declarations"]["lr"] == orig["declarations"]["lr"]
+        its = st.iterations(r["id"])
+        assert len(its) == 7  # 3 + 2 + 2 rungs
+        for it in its:
+            d = it["data"]
+            vals = dict((int(a), b) for a, b in d["experiments_metrics"])
+            keep = len(d["promoted"])
+            assert d["promoted"] == sorted(vals, key=lambda k: vals[k])[:keep]
+        # both executors were used (brackets run concurrently) and stay warm for the next group
+        pool = flow.call(lambda: flow.resident_pool().snapshot())
+        assert len(pool) == 2 and all(p["ready"] and p["alive"] for p in pool)
+        assert {tuple(j["devices"]) for x in xs for j in st.experiment_jobs(x["id"])} == {(0,), (1,)}
+        # a second group reuses the warm executors (no new processes)
+        pids = {p["pid"] for p in pool}
+        r2 = flow.submit(_group(seed=11, concurrency=1))
+        assert flow.wait("group", r2["id"], timeout=300) == "succeeded"
+        pool2 = flow.call(lambda: flow.resident_pool().snapshot())
+        assert {p["pid"] for p in pool2} == pids
+        used = {tuple(j["devices"]) for x in st.list_experiments(group_id=r2["id"]) for j in st.experiment_jobs(x["id"])}
+        assert len(used) == 1  # concurrency: 1 -> one executor
+    # shutdown released every device
+    assert flow.alloc.allocations == {}
+
+
+def test_resident_executor_crash_fails_trials_and_frees_device(tmp_path, cpu_pool_env):
+    from polyaxon_amd.polyflow.scheduler import Polyflow
+
+    params = dict(TINY, unit_steps=3)
+    with Polyflow(str(tmp_path), reconcile_s=0) as flow:
+        r = flow.submit(_group(concurrency=1, params=params))
+        end = time.time() + 120
+        pid = None
+        while time.time() < end and pid is None:
+            snap = flow.call(lambda: flow.resident_pool().snapshot())
+            running = flow.store.list_experiments(group_id=r["id"])
+            if snap and snap[0]["ready"] and any(x["status"] == "running" for x in running):
+                pid = snap[0]["pid"]
+            time.sleep(0.05)
+        assert pid is not None
+        os.kill(pid, 9)
+        assert flow.wait("group", r["id"], timeout=120) == "succeeded"  # the group ends; trials are failed
+        xs = flow.store.list_experiments(group_id=r["id"])
+        assert any(x["status"] == "failed" for x in xs)
+        assert all(x["status"] in ("succeeded", "failed") for x in xs)
+        ev = flow.store.cluster_events()
+        assert any(e["kind"] == "resident_executor" and "gone" in e["message"] for e in ev)
+        assert not any(o.startswith("resident:") for o in flow.alloc.allocations)
+
+
+def test_resident_spec_validation():
+    from polyaxon_amd.spec import specification_for
+    from polyaxon_amd.spec.specification import PolyaxonfileError
+
+    spec = specification_for(_group())
+    assert spec.environment.executor.resident and spec.environment.executor.program == "resnet_tiny"
+    assert spec.environment.to_dict()["executor"]["kind"] == "resident"
+    bad = _group()
+    bad["environment"]["executor"] = {"kind": "resident"}
+    with pytest.raises(PolyaxonfileError):
+        specification_for(bad)
+    bad = _group()
+    bad["environment"]["executor"]["kind"] = "magic"
+    with pytest.raises(PolyaxonfileError):
+        specification_for(bad)
+    bad = _group()
+    bad["environment"]["resources"] = {"gpu": 1.5}
+    with pytest.raises(PolyaxonfileError):
+        specification_for(bad)
+
+
+def test_resident_rejects_non_hyperband(tmp_path, cpu_pool_env):
+    from polyaxon_amd.polyflow.scheduler import Polyflow
+    from polyaxon_amd.spec.specification import PolyaxonfileError
+
+    g = _group()
+    del g["hptuning"]["hyperband"]
+    g["hptuning"]["random_search"] = {"n_experiments": 3}
+    with Polyflow(str(tmp_path), reconcile_s=0) as flow:
+        with pytest.raises(PolyaxonfileError):
+            flow.submit(g)
+        assert flow.store.list_groups() == []
+
+
+def test_bench_cpu_two_ranks_complete_sweeps():
+    """bench.py --gpus 2 spawns its own two ranks, times whole sweeps through polyflow and reports n_gpus: 2."""
+    import json
+
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "2", "--steps", "1",
+                          "--warmup", "0"], capture_output=True, text=True, timeout=600, env=env, cwd="/tmp")
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 2 and res["steps"] == 1
+    assert res["config"]["sweeps"] == 2 and res["config"]["brackets"] == 6
+    assert res["trials"] == 46 and res["trials_succeeded"] == 46
+    assert res["store_fsm_history_ok"] is True
+    assert res["value"] > 0 and res["ms_per_step"] > 0
