@@ -51,7 +51,7 @@ def _args(argv=None):
     ap.add_argument("--batch", type=int, default=256, help="per-trial batch (one trial per GPU at a time)")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--unit-steps", type=int, default=4, help="training steps per Hyperband resource unit")
-    ap.add_argument("--target", type=float, default=3.0, help="loss target for wall-clock-to-target")
+    ap.add_argument("--target", type=float, default=1.0, help="loss target for wall-clock-to-target")
     ap.add_argument("--signal", type=float, default=0.5, help="class-pattern amplitude of the synthetic data")
     ap.add_argument("--max-active", type=int, default=8, help="brackets one executor interleaves")
     ap.add_argument("--cpu", action="store_true", help="CPU rehearsal (gloo, small ResNet, tiny images)")

@@ -107,18 +107,27 @@ def clean_stale(store, live: Iterable[Tuple[str, int]] = (), kinds: Iterable[str
 
 def clean_outputs(store, older_than_s: float, now: Optional[float] = None, dry_run: bool = False) -> List[str]:
     """Delete outputs and logs of finished experiments/jobs whose ``finished_at`` is older than the cutoff
-    (reference crons/tasks/cleaning.py).  Returns the deleted paths."""
+    (reference crons/tasks/cleaning.py).  Returns the deleted paths.
+
+    RESUME clones share their root's outputs directory (reference libs/paths/experiments.py:17-18), so an outputs
+    path is only removed once EVERY row that points at it is finished and past the retention window: a Hyperband
+    root that finished long ago keeps its checkpoints while a resumed promotion still uses (or just used) them."""
     cutoff = (now if now is not None else time.time()) - older_than_s
     deleted: List[str] = []
     for table in ("experiments", "jobs"):
         rows = store.execute(f"SELECT id, outputs_path, logs_path FROM {table} WHERE finished_at IS NOT NULL "
                              f"AND finished_at < ?", (cutoff,)).fetchall()
         for rid, outputs, logs in rows:
+            if outputs and store.execute(
+                    f"SELECT 1 FROM {table} WHERE outputs_path = ? AND id != ? AND "
+                    f"(finished_at IS NULL OR finished_at >= ?) LIMIT 1", (outputs, rid, cutoff)).fetchone():
+                outputs = None  # still shared with a live or recent run
             for p in (outputs, logs):
                 if p and os.path.isdir(p):
                     if not dry_run:
                         shutil.rmtree(p, ignore_errors=True)
                     deleted.append(p)
-            if not dry_run:
-                store.execute(f"UPDATE {table} SET outputs_path = NULL WHERE id = ?", (rid,))
+            if not dry_run and outputs:
+                store.execute(f"UPDATE {table} SET outputs_path = NULL WHERE outputs_path = ? AND finished_at IS NOT "
+                              f"NULL AND finished_at < ?", (outputs, cutoff))
     return deleted

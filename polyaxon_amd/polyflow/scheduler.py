@@ -597,7 +597,10 @@ class Polyflow:
             run = self.runs.get(owner)
             if run is None or run.final_status is not None:
                 continue
-            whole = sum(int(round(g)) for _, _, g in self._requirements(run) if g >= 1.0 - 1e-9)
+            try:
+                whole = sum(int(round(g)) for _, _, g in self._requirements(run) if g >= 1.0 - 1e-9)
+            except Exception:  # a malformed run is failed by _try_place; it never reserves
+                continue
             if whole > 1:
                 run.waiting_since = run.waiting_since or now
                 if now - run.waiting_since >= wait:

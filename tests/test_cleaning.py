@@ -93,6 +93,31 @@ def test_clean_outputs(tmp_path):
     assert store.get_experiment(ids[0])["outputs_path"] is None
 
 
+def test_clean_outputs_keeps_paths_shared_with_live_resume_clones(tmp_path):
+    """A Hyperband root finished long ago shares its outputs with a RESUME clone that is still running (or
+    finished recently): the checkpoints must survive until every row using them is past the window."""
+    store = Store(str(tmp_path / "s.sqlite"))
+    pid = store.create_project("p")["id"]
+    shared = tmp_path / "root_outputs"
+    shared.mkdir()
+    (shared / "model.pt").write_text("ckpt")
+    root = store.create_experiment(pid, {})
+    store.update_experiment(root, outputs_path=str(shared), logs_path=str(tmp_path / "logs_root"))
+    store.set_experiment_status(root, "succeeded", force=True)
+    store.update_experiment(root, finished_at=time.time() - 3 * 86400)
+    clone = store.create_experiment(pid, {}, original_experiment_id=root, cloning_strategy="resume")
+    store.update_experiment(clone, outputs_path=str(shared))
+    store.set_experiment_status(clone, "running", force=True)  # still training from the root's checkpoint
+    assert clean_outputs(store, 86400) == []
+    assert (shared / "model.pt").exists() and store.get_experiment(root)["outputs_path"] == str(shared)
+    store.set_experiment_status(clone, "succeeded")  # finished just now: still inside the window
+    assert clean_outputs(store, 86400) == [] and shared.exists()
+    store.update_experiment(clone, finished_at=time.time() - 2 * 86400)  # both past the window: now it goes
+    assert clean_outputs(store, 86400) == [str(shared)]
+    assert not shared.exists()
+    assert store.get_experiment(root)["outputs_path"] is None and store.get_experiment(clone)["outputs_path"] is None
+
+
 def test_deploy_generate_and_check(tmp_path, monkeypatch, capsys):
     import json as _json
 
