@@ -6,8 +6,9 @@
   8 KV heads (GQA), RMSNorm, SwiGLU 14336, RoPE theta 500000, vocab 128256).
 
 MI355X layout choices: bf16 autocast compute with fp32 master weights in a flat buffer (ops/flat.py) so
-the optimizer is one fused kernel; attention through ``scaled_dot_product_attention`` (the ROCm flash
-path); QKV and gate/up projections are single fused GEMMs (one hipBLASLt call instead of 3 / 2);
+the optimizer is one fused kernel; attention on the hand-written CDNA4 flash attention (csrc/attn_kernels.hip,
+GQA-native, output already in [B, S, H, D]); QKV and gate/up projections are single fused GEMMs (one
+hipBLASLt call instead of 3 / 2);
 RMSNorm in fp32 accumulate; optional activation checkpointing per block for long contexts.
 The reference ships no models: these exist so the framework's HPO and distributed paths
 can be exercised on the named configs with random weights and synthetic tokens.
@@ -24,6 +25,7 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 from polyaxon_amd.ops import lm as lm_ops
+from polyaxon_amd.ops.attention import flash_attention
 
 
 @dataclass
@@ -123,10 +125,10 @@ class Attention(nn.Module):
             if rope is not None:
                 cs = (rope[0].to(q.dtype), rope[1].to(q.dtype))
                 q, k = apply_rope(q, *cs), apply_rope(k, *cs)
-        # GQA straight into the attention kernel (no repeat_interleave copies of K/V and their backward
-        # reductions): 2.31 vs 3.62 ms fwd+bwd per Llama-3 8B layer at S=4096 (scripts/diag_gqa_sdpa.py)
-        y = F.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=cfg.kv_heads != cfg.n_heads)
-        return lm_ops.linear(y.transpose(1, 2).reshape(B, S, cfg.n_heads * hd), self.proj.weight, self.proj.bias)
+        # hand-written CDNA4 flash attention (ops/attention.py, csrc/attn_kernels.hip): GQA straight into the
+        # kernel (no repeat_interleave of K/V), output written in [B, S, H, D] so the projection reads it as is
+        y = flash_attention(q, k, v, causal=True)
+        return lm_ops.linear(y.reshape(B, S, cfg.n_heads * hd), self.proj.weight, self.proj.bias)
 
 
 class MLP(nn.Module):

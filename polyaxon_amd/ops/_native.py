@@ -34,6 +34,7 @@ LIBRARIES: Dict[str, dict] = {
     "plx_conv": {"sources": ["conv_gemm.hip"], "kind": "hip", "link": []},
     "plx_pool": {"sources": ["pool_kernels.hip"], "kind": "hip", "link": []},
     "plx_lm": {"sources": ["lm_kernels.hip"], "kind": "hip", "link": []},
+    "plx_attn": {"sources": ["attn_kernels.hip"], "kind": "hip", "link": []},
     "plx_rccl": {"sources": ["rccl_comm.cpp"], "kind": "hip_host", "link": ["-lrccl"]},
 }
 
@@ -200,6 +201,12 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_swiglu_fwd": [_P, _P, _L, _I, _P],
         "plx_swiglu_bwd": [_P, _P, _P, _L, _I, _P],
     },
+    "plx_attn": {
+        "plx_attn_fwd": [_P, _I, _P],
+        "plx_attn_bwd": [_P, _I, _P, _P],
+        "plx_attn_bwd_workspace": [_I, _I, _I, _I, _I],
+        "plx_attn_args_size": [],
+    },
     "plx_pool": {
         "plx_maxpool3s2_forward": [_P, _P, _P, _I, _I, _I, _I, _P],
         "plx_maxpool3s2_backward": [_P, _P, _P, _I, _I, _I, _I, _P],
@@ -227,7 +234,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 
