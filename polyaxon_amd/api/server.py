@@ -736,6 +736,21 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
         r["operations"] = store.operation_runs(rid)
         return r
 
+    @app.get("/api/v1/{username}/{project}/pipelines/{pid}")
+    def pipeline_detail(username: str, project: str, pid: int, user=Depends(auth)):
+        p = store.get("pipelines", pid)
+        if p is None:
+            raise HTTPException(404, "pipeline not found")
+        p["runs"] = store._rows(store.execute("SELECT * FROM pipeline_runs WHERE pipeline_id = ? ORDER BY id", (pid,)))
+        p["schedule_state"] = store.kv_get(f"pipeline_schedule:{pid}")
+        return p
+
+    @app.post("/api/v1/{username}/{project}/pipelines/{pid}/stop")
+    def pipeline_stop(username: str, project: str, pid: int, user=Depends(auth)):
+        if not flow.stop_pipeline(pid):
+            raise HTTPException(404, "pipeline not running in this scheduler")
+        return {"stopped": pid}
+
     # ------------------------------------------------------------------ cluster / nodes / activity / searches
     @app.get("/api/v1/cluster")
     def cluster(user=Depends(auth)):

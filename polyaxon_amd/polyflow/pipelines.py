@@ -108,6 +108,10 @@ class PipelineRunner:
                 self.dag[u].add(name)
         sort_topologically(self.dag)  # validates acyclicity
         self.concurrency = spec.concurrency
+        self.on_finished: List[Any] = []  # callbacks(runner) when the run is finished / stopped (schedules)
+        self.finished = False
+        self.succeeded = False
+        self.run_id: Optional[int] = None
 
     def start(self) -> int:
         self.run_id = self.store.create_pipeline_run(self.pipeline_id)
@@ -232,6 +236,14 @@ class PipelineRunner:
                 self.flow.auditor.record("pipeline.succeeded" if ok else "pipeline.failed", "pipeline",
                                          self.pipeline_id, run=self.run_id)
                 self.flow.auditor.record("pipeline.done", "pipeline", self.pipeline_id, run=self.run_id)
+                self._finish(ok)
+
+    def _finish(self, ok: bool) -> None:
+        if self.finished:
+            return
+        self.finished, self.succeeded = True, ok
+        for cb in list(self.on_finished):
+            cb(self)
 
     def stop(self) -> None:
         for name in self.ops:
@@ -245,3 +257,4 @@ class PipelineRunner:
                 else:
                     self.flow._stop("experiment" if kind == "experiment" else "job", eid, "pipeline stopped")
         self.store.set_pipeline_run_status(self.run_id, "stopped")
+        self._finish(False)

@@ -334,8 +334,26 @@ class Polyflow:
         self.store.kv_set(key, rid)
         return rid
 
+    def _external_checkout(self, spec: BaseSpecification, proj: Dict, user: str) -> Optional[str]:
+        """``build.git``: fetch the external repository and check out ``build.ref``; the run executes there."""
+        b = spec.build
+        if b is None or not b.git:
+            return None
+        from polyaxon_amd.polyflow.repos import ExternalRepo, GitError
+
+        repo = ExternalRepo(self.paths.repos_root, user, proj["name"], str(b.git))
+        try:
+            repo.fetch()
+            sha = repo.checkout(str(b.ref) if b.ref else None)
+        except GitError as e:
+            raise PolyaxonfileError(f"external repo {b.git}: {e}") from None
+        self.store.upsert_external_repo(proj["id"], str(b.git), repo.path, sha)
+        self.auditor.record("repo.new_commit", "repo", proj["id"], git_url=str(b.git), commit=sha)
+        return repo.path
+
     def _submit(self, spec: BaseSpecification, project: str, user: str, cwd: str, name, description):
         proj = self.store.get_or_create_project(spec.project or project, user)
+        cwd = self._external_checkout(spec, proj, user) or cwd
         self._current_code_ref = self._code_ref(cwd)
         if spec.kind == Kinds.EXPERIMENT:
             xid = self._create_experiment(spec, proj, user, cwd, name=name, description=description)
@@ -368,6 +386,14 @@ class Polyflow:
 
             pid = self.store.create_pipeline(proj["id"], name or spec.name or "pipeline", spec.raw_data, user,
                                              spec.concurrency, spec.schedule)
+            from polyaxon_amd.polyflow.schedules import PipelineSchedule, Schedule
+
+            sched = Schedule.from_dict(spec.schedule)
+            if sched is not None and (sched.periodic or sched.start_at is not None):
+                ps = PipelineSchedule(self, pid, spec, proj, user, cwd, sched)
+                self.pipelines[pid] = ps
+                rid = ps.start()
+                return {"kind": "pipeline", "id": pid, "run_id": rid, "next_at": ps.next_at}
             runner = PipelineRunner(self, pid, spec, proj, user, cwd)
             self.pipelines[pid] = runner
             rid = runner.start()
@@ -1003,6 +1029,17 @@ class Polyflow:
     def stop_group(self, gid: int, pending: bool = False, message: str = "Stopped by user.") -> None:
         self.auditor.record("experiment_group.stopped_triggered", "experiment_group", gid)
         self.call(self._stop_group, gid, pending, message)
+
+    def stop_pipeline(self, pid: int) -> bool:
+        """Stop a pipeline: its running run(s) and, for a scheduled pipeline, every future firing."""
+        def stop():
+            p = self.pipelines.get(pid)
+            if p is None:
+                return False
+            p.stop()
+            return True
+
+        return self.call(stop)
 
     def _stop_group(self, gid: int, pending: bool, message: str) -> None:
         driver = self.groups.get(gid)

@@ -96,8 +96,8 @@ class BuildConfig:
         self.ref = d.get("ref")
         self.nocache = bool(d.get("nocache", False))
         self.dockerfile = d.get("dockerfile")
-        if not self.image and not self.dockerfile:
-            raise PolyaxonfileError("build requires an `image` (or a `dockerfile`)")
+        if not self.image and not self.dockerfile and not self.git:
+            raise PolyaxonfileError("build requires an `image` (or a `dockerfile`, or a `git` source)")
         for e in self.env_vars:
             if len(e) != 2:
                 raise PolyaxonfileError(f"build.env_vars entries are [key, value] pairs, got {e}")
@@ -368,7 +368,8 @@ class PipelineSpecification(BaseSpecification):
     ops: [{name, upstream: [names], trigger: all_succeeded|all_failed|all_done|one_succeeded|one_failed|one_done,
            max_retries, retry_delay, retry_exponential_backoff, max_retry_delay, timeout, concurrency,
            template: <inline Polyaxonfile of kind experiment|job|group>}]
-    plus pipeline-level ``concurrency`` and optional ``schedule: {frequency: seconds | cron: '...'}``.
+    plus pipeline-level ``concurrency`` and optional ``schedule: {frequency | cron, start_at, end_at,
+    depends_on_past, max_runs}`` (polyflow/schedules.py).
     """
     KIND = Kinds.PIPELINE
     TRIGGERS = ("all_succeeded", "all_failed", "all_done", "one_succeeded", "one_failed", "one_done")
@@ -399,6 +400,13 @@ class PipelineSpecification(BaseSpecification):
                 raise PolyaxonfileError(f"op {op['name']} depends on unknown ops {missing}")
         self.concurrency = int(d.get("concurrency") or 0) or None
         self.schedule = d.get("schedule")
+        if self.schedule is not None:
+            from polyaxon_amd.polyflow.schedules import Schedule, ScheduleError
+
+            try:
+                Schedule.from_dict(self.schedule)
+            except (ScheduleError, ValueError, TypeError) as e:
+                raise PolyaxonfileError(f"invalid schedule: {e}") from None
 
 
 _KIND_TO_SPEC = {

@@ -91,6 +91,8 @@ CREATE TABLE IF NOT EXISTS node_gpus (id INTEGER PRIMARY KEY, node_id INTEGER, i
 CREATE TABLE IF NOT EXISTS cluster_events (id INTEGER PRIMARY KEY, kind TEXT, level TEXT, message TEXT, data TEXT,
     created_at REAL);
 CREATE TABLE IF NOT EXISTS kv (k TEXT PRIMARY KEY, v TEXT, expires_at REAL);
+CREATE TABLE IF NOT EXISTS external_repos (id INTEGER PRIMARY KEY, project_id INTEGER, git_url TEXT, path TEXT,
+    last_commit TEXT, created_at REAL, updated_at REAL, UNIQUE(project_id, git_url));
 """
 
 JSON_COLS = {"config", "declarations", "tags", "last_metric", "resources", "run_env", "content", "hptuning", "data",
@@ -672,6 +674,22 @@ class Store:
         return self._rows(self.execute("SELECT * FROM cluster_events ORDER BY id DESC LIMIT ?", (limit,)))
 
     # ------------------------------------------------------------------ ephemeral key/value (Redis replacement)
+    def upsert_external_repo(self, project_id: int, git_url: str, path: str, last_commit: Optional[str]) -> int:
+        """Reference ExternalRepo (db/models/repos.py): one row per (project, git url)."""
+        row = self.execute("SELECT id FROM external_repos WHERE project_id = ? AND git_url = ?",
+                           (project_id, git_url)).fetchone()
+        if row:
+            self._update("external_repos", row["id"], {"path": path, "last_commit": last_commit,
+                                                        "updated_at": _now()})
+            return int(row["id"])
+        return self._insert("external_repos", dict(project_id=project_id, git_url=git_url, path=path,
+                                                   last_commit=last_commit, created_at=_now(), updated_at=_now()))
+
+    def external_repos(self, project_id: Optional[int] = None) -> List[Dict[str, Any]]:
+        if project_id is None:
+            return self._rows(self.execute("SELECT * FROM external_repos ORDER BY id"))
+        return self._rows(self.execute("SELECT * FROM external_repos WHERE project_id = ? ORDER BY id", (project_id,)))
+
     def kv_set(self, key: str, value: Any, ttl: Optional[float] = None) -> None:
         exp = _now() + ttl if ttl else None
         self.execute("INSERT INTO kv (k, v, expires_at) VALUES (?, ?, ?) ON CONFLICT(k) DO UPDATE SET "
