@@ -187,7 +187,15 @@ class Polyflow:
                       "faults_injected": 0}
         self._last_exit_t: Optional[float] = None
         self.reconcile_s = reconcile_s
-        self.health_check = health_check  # () -> indices of unhealthy devices (amd-smi RAS/ECC watchdog)
+        # () -> indices of unhealthy devices.  Default (auto-detected devices only): the RAS/ECC + KFD probe of
+        # obs/nodes.py; a test that injects its own allocator keeps the probe off unless it passes one.
+        probe_on = settings.get("scheduler.health_probe") if settings is not None else True
+        if health_check is None and allocator is None and probe_on:
+            from polyaxon_amd.obs.nodes import GpuHealthProbe
+
+            health_check = GpuHealthProbe(events=self.cluster_event)
+        self.health_check = health_check
+        self._unhealthy: set = set()
         self._pool = None  # resident executors (polyflow/pool.py), created on first use
 
     def resident_pool(self):
@@ -220,8 +228,36 @@ class Polyflow:
             self._thread.start()
             if self.reconcile_s > 0:
                 self.after(self.reconcile_s, self._reconcile)
-            self.store.upsert_node("local", os.uname().nodename, float(os.cpu_count() or 1), 0.0, self.alloc.n_devices)
+            self.sync_inventory()
         return self
+
+    def sync_inventory(self) -> Dict[str, Any]:
+        """Node row + one NodeGPU row per device (KFD topology / amd-smi; reference crons/tasks/nodes.py)."""
+        from polyaxon_amd.obs.nodes import sync_node_inventory
+
+        try:
+            inv = sync_node_inventory(self.store, self.alloc.n_devices)
+        except Exception as e:  # inventory must never keep the scheduler from starting
+            log.warning("node inventory failed: %s", e)
+            self.store.upsert_node("local", os.uname().nodename, float(os.cpu_count() or 1), 0.0,
+                                   self.alloc.n_devices)
+            return {}
+        by_index = {g["index"]: g for g in inv.get("gpus", [])}
+        for d in self.alloc.devices:
+            g = by_index.get(d.index)
+            if g is not None:
+                d.name = g["name"]
+                if g["memory_gb"]:
+                    d.memory_gb = float(g["memory_gb"])
+        return inv
+
+    def cluster_event(self, kind: str, level: str, message: str, data: Optional[Dict[str, Any]] = None) -> None:
+        """Persist a node-level event (reference monitor_namespace: k8s warnings -> ClusterEvent rows)."""
+        try:
+            self.store.add_cluster_event(kind, level, message, data or {})
+            self.auditor.record("cluster.event", "cluster", None, kind=kind, level=level, message=message)
+        except Exception:
+            log.exception("cluster event %s failed", kind)
 
     def shutdown(self, stop_running: bool = True, timeout: float = 30.0) -> None:
         if self._thread is None:
@@ -638,6 +674,9 @@ class Polyflow:
         reqs = self._requirements(run)
         need = [g for _, _, g in reqs]
         if any(g > self.alloc.n_devices + 1e-9 for g in need) or sum(g for g in need if g >= 1) > self.alloc.n_devices:
+            self.cluster_event("failed_scheduling", "warning",
+                               f"{run.owner} requests {need} GPUs but the node has {self.alloc.n_devices}",
+                               {"owner": run.owner, "requested": need})
             self._finish_unstarted(run, "failed", f"requests {need} GPUs but the node has {self.alloc.n_devices}")
             return True
         if reserve is not None and reserve[0] != run.owner and any(g > 0 for g in need):
@@ -862,11 +901,32 @@ class Polyflow:
                 self._stop_run(run, "Master is done.")
         else:
             msg = f"exit code {status}" if status > 0 else f"killed by signal {-status}"
+            self._replica_event(run, rep, status)
             self._replica_status(run, rep, "failed", msg)
             run.final_status = "failed"
             run.final_message = f"{rep.role}.{rep.index} {msg}"
             self._stop_run(run, f"replica {rep.role}.{rep.index} failed")
         self._maybe_finalize(run)
+
+    def _replica_event(self, run: Run, rep: Replica, status: int) -> None:
+        """Cluster events for abnormal replica exits (the k8s events the reference's namespace monitor records:
+        OOMKilled, Error): an unrequested SIGKILL (the kernel OOM killer's signal), and a GPU fault the HIP runtime
+        printed into the replica's log (page fault / illegal address / hang)."""
+        from polyaxon_amd.obs.nodes import gpu_fault_in_log
+
+        rec = self.store.get_experiment(run.id) if run.kind == "experiment" else self.store.get_job(run.id)
+        logs = rec.get("logs_path") if rec else None
+        fault = gpu_fault_in_log(self.paths.replica_log(logs, rep.role, rep.index)) if logs else None
+        data = {"owner": run.owner, "replica": f"{rep.role}.{rep.index}", "devices": rep.devices, "status": status}
+        if fault:
+            self.cluster_event("gpu_fault", "error", f"{run.owner} {rep.role}.{rep.index} on devices "
+                                                     f"{rep.devices}: {fault}", data)
+        elif status == -signal.SIGKILL:
+            self.cluster_event("process_killed", "warning", f"{run.owner} {rep.role}.{rep.index} killed by SIGKILL "
+                                                            "(not requested by polyflow; OOM killer?)", data)
+        elif status < 0:
+            self.cluster_event("process_killed", "warning",
+                               f"{run.owner} {rep.role}.{rep.index} killed by signal {-status}", data)
 
     def _maybe_finalize(self, run: Run) -> None:
         if any(not r.done for r in run.replicas):
@@ -973,7 +1033,10 @@ class Polyflow:
                     self._stop_run(run, run.final_message)
             if self.health_check is not None:
                 for idx in self.health_check() or []:
-                    self.alloc.mark_unhealthy(idx)
+                    if idx < self.alloc.n_devices and idx not in self._unhealthy:
+                        self._unhealthy.add(idx)
+                        self.alloc.mark_unhealthy(idx)
+                        self.auditor.record("cluster.node_gpu_unhealthy", "cluster", None, device=idx)
             keep = self.settings.get("scheduler.clean_after_s") if self.settings is not None else 0
             if keep and now - getattr(self, "_last_clean", 0.0) > 600.0:  # outputs retention, at most every 10 min
                 from polyaxon_amd.polyflow.cleaning import clean_outputs
