@@ -74,9 +74,12 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
         token may only touch its own experiment."""
         user = identify(authorization, x_polyaxon_internal, token)
         pp = request.path_params
+        scope = user.get("scope")
+        if scope is not None and ("xid" not in pp or "username" not in pp or "project" not in pp):
+            # an ephemeral (per-trial) token only reaches its own experiment's routes
+            raise HTTPException(403, "ephemeral token is scoped to one experiment")
         if user.get("is_superuser") or "username" not in pp or "project" not in pp:
             return user
-        scope = user.get("scope")
         if scope is not None:
             xid = pp.get("xid")
             if xid is None or int(xid) != int(scope.get("experiment", -1)):
@@ -266,7 +269,7 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
     # The reference registers every model with the Django admin; here a superuser gets a generic table
     # browser over the store: list tables with counts, page through rows, edit or delete a row.  Secrets
     # (API tokens, kv values holding ephemeral tokens) are never returned.
-    _SECRET_COLS = {"token"}
+    _SECRET_COLS = {"token", "password_hash", "salt", "secret", "client_secret", "activation_key"}
 
     def _admin_tables() -> List[str]:
         rows = store.execute("SELECT name FROM sqlite_master WHERE type='table' AND name NOT LIKE 'sqlite_%' "
@@ -334,7 +337,11 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
 
     @app.get("/api/v1/projects")
     def list_projects(request: Request, user=Depends(auth)):
-        return page(store.list_projects(), request)
+        """All projects for superusers; otherwise the caller's own projects plus public ones."""
+        rows = store.list_projects()
+        if not user.get("is_superuser"):
+            rows = [p for p in rows if p["user"] == user.get("username") or p.get("is_public")]
+        return page(rows, request)
 
     @app.post("/api/v1/projects", status_code=201)
     async def create_project(request: Request, user=Depends(auth)):

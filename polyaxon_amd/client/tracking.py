@@ -142,14 +142,24 @@ class _HttpBackend:
 
 
 class MetricStream:
-    """Asynchronous device→store metric path: tensors are copied to pinned host memory on
-    a side stream; a flusher thread writes rows whose copy event has completed."""
+    """Asynchronous device -> store metric path.
 
-    def __init__(self, sink, xid: int, flush_every_s: float = 0.5):
+    Device tensors are gathered into one staging vector and copied device->host on a dedicated LOW-priority side
+    stream (``Stream.priority_range()[0]``) into a **preallocated pinned ring** (``ring_floats`` fp32 slots,
+    allocated once), with one event per ``log_metrics`` call; the training stream never waits.  A flusher thread
+    turns rows whose copy event has completed into store writes.  When the ring is full, the oldest pending rows
+    are flushed first (their events synchronised), so the ring never grows and nothing is dropped."""
+
+    def __init__(self, sink, xid: int, flush_every_s: float = 0.5, ring_floats: int = 4096):
         self.sink = sink
         self.xid = xid
         self.flush_every_s = flush_every_s
-        self._pending: List = []  # (event|None, {name: value|pinned tensor}, step, ts)
+        self.ring_floats = int(ring_floats)
+        self._ring = None          # pinned fp32 [ring_floats]
+        self._head = 0             # next free slot (monotonic; slot = head % ring_floats)
+        self._tail = 0             # oldest slot still referenced by a pending row
+        # (event|None, {name: float | (offset, numel)}, step, ts, end_offset)
+        self._pending: List = []
         self._lock = threading.Lock()
         self._stop = threading.Event()
         self._side = None
@@ -160,50 +170,85 @@ class MetricStream:
         import torch
 
         if self._side is None:
-            self._side = torch.cuda.Stream(device=t.device, priority=0)
+            low = torch.cuda.Stream.priority_range()[0]  # least priority: never delays the training kernels
+            self._side = torch.cuda.Stream(device=t.device, priority=low)
+            self._ring = torch.empty(self.ring_floats, dtype=torch.float32, pin_memory=True)
         return self._side
+
+    def _reserve(self, n: int) -> int:
+        """Offset of n contiguous ring slots (wrapping to the start when the tail end is too short)."""
+        if n > self.ring_floats:
+            raise ValueError(f"metric tensors of {n} elements exceed the {self.ring_floats}-float ring")
+        while True:
+            with self._lock:
+                off = self._head % self.ring_floats
+                skip = 0 if off + n <= self.ring_floats else self.ring_floats - off
+                if self._head + skip + n - self._tail <= self.ring_floats:
+                    self._head += skip
+                    start = self._head
+                    self._head += n
+                    return start
+            self.flush(force=True, oldest_only=True)  # ring full: drain the oldest rows first
 
     def put(self, values: Dict[str, Any], step: Optional[int]) -> None:
         ts = time.time()
         host: Dict[str, Any] = {}
         event = None
+        end = None
         tensors = {k: v for k, v in values.items() if hasattr(v, "is_cuda") and v.is_cuda}
         if tensors:
             import torch
 
             first = next(iter(tensors.values()))
             side = self._stream_for(first)
+            sizes = [v.numel() for v in tensors.values()]
+            start = self._reserve(sum(sizes))
+            off = start % self.ring_floats
             side.wait_stream(torch.cuda.current_stream(first.device))
             with torch.cuda.stream(side):
-                for k, v in tensors.items():
-                    buf = torch.empty(v.shape, dtype=torch.float32, pin_memory=True)
-                    buf.copy_(v.detach().float(), non_blocking=True)
+                flat = torch.cat([v.detach().reshape(-1).float() for v in tensors.values()])  # one gather kernel
+                self._ring[off: off + flat.numel()].copy_(flat, non_blocking=True)      # one D2H copy
+                for v in tensors.values():
                     v.record_stream(side)
-                    host[k] = buf
                 event = torch.cuda.Event()
                 event.record(side)
+            o = off
+            for (k, _), n in zip(tensors.items(), sizes):
+                host[k] = (o, n)
+                o += n
+            end = start + sum(sizes)
         for k, v in values.items():
             if k not in host:
                 host[k] = float(v.item()) if hasattr(v, "item") else float(v)
         with self._lock:
-            self._pending.append((event, host, step, ts))
+            self._pending.append((event, host, step, ts, end))
 
-    def _ready_rows(self, force: bool):
+    def _ready_rows(self, force: bool, oldest_only: bool = False):
         rows, keep = [], []
         with self._lock:
-            for ev, host, step, ts in self._pending:
-                if ev is not None and not force and not ev.query():
-                    keep.append((ev, host, step, ts))
+            for i, (ev, host, step, ts, end) in enumerate(self._pending):
+                if keep or (ev is not None and not force and not ev.query()) or (oldest_only and rows):
+                    keep.append((ev, host, step, ts, end))  # keep FIFO order: the ring is freed front to back
                     continue
                 if ev is not None:
                     ev.synchronize()
-                vals = {k: (float(v.reshape(-1)[0]) if hasattr(v, "reshape") else v) for k, v in host.items()}
+                vals = {}
+                for k, v in host.items():
+                    if isinstance(v, tuple):
+                        o, n = v
+                        vals[k] = float(self._ring[o])  # metrics are scalars: first element
+                    else:
+                        vals[k] = v
                 rows.append((vals, step, ts))
+                if end is not None:
+                    self._tail = end
             self._pending = keep
+            if not keep:
+                self._tail = self._head
         return rows
 
-    def flush(self, force: bool = True) -> None:
-        rows = self._ready_rows(force)
+    def flush(self, force: bool = True, oldest_only: bool = False) -> None:
+        rows = self._ready_rows(force, oldest_only)
         if rows:
             self.sink.log_metrics(self.xid, rows)
 

@@ -262,10 +262,20 @@ class EnvironmentSpec:
 
     @classmethod
     def from_dict(cls, d: Optional[Dict[str, Any]]):
-        d = d or {}
+        d = dict(d or {})
         fws = [f for f in FRAMEWORKS if d.get(f) is not None]
         if len(fws) > 1:
             raise MatrixValidationError(f"environment defines more than one framework: {fws}")
+        # the reference docs also place the per-replica sections next to the framework section
+        # (docs/templates/customization/customize_node_scheduling.md): fold them into it
+        replica_keys = [k for k in ("worker", "ps", "default_worker", "default_ps") if k in d]
+        if replica_keys:
+            if not fws:
+                raise MatrixValidationError(f"{replica_keys} need a distributed framework section")
+            fw = dict(d[fws[0]] or {})
+            for k in replica_keys:
+                fw.setdefault(k, d.pop(k))
+            d[fws[0]] = fw
         known = {"resources", "outputs", "persistence", "node_selector", "tolerations", "affinity", "secret_refs",
                  "configmap_refs", "env_vars", "max_restarts", "heartbeat_timeout", "profile", "executor", *FRAMEWORKS}
         unknown = set(d) - known

@@ -30,7 +30,6 @@ class Condition:
     value: Any
 
 
-_SCALAR = re.compile(r"^(>=|<=|>|<|=)?(.+)$")
 _NEG_OPS = {"=": "!=", ">": "<=", ">=": "<", "<": ">=", "<=": ">", "in": "not in", "range": "not range"}
 
 
@@ -67,15 +66,37 @@ def parse_datetime(s: str) -> float:
     raise QueryError(f"invalid datetime `{s}` (YYYY-MM-DD[ HH:MM[:SS]])")
 
 
+def parse_comparison(expr: str) -> Tuple[Optional[str], str]:
+    """Leading comparison operator (reference parse_comparison_operation, query/parser.py:25-41): ``<=``/``=<``,
+    ``>=``/``=>``, ``<``, ``>``; None when there is none."""
+    e = expr.strip()
+    if e[:2] in ("<=", "=<"):
+        return "<=", e[2:].strip()
+    if e[:2] in (">=", "=>"):
+        return ">=", e[2:].strip()
+    if e[:1] in ("<", ">"):
+        return e[:1], e[1:].strip()
+    if e[:1] == "=":
+        return "=", e[1:].strip()
+    return None, e
+
+
 def parse_scalar(expr: str, number=True) -> Tuple[bool, str, Any]:
+    """Scalar condition: ``[~][op]value``.  ``|`` and ``..`` are not allowed (reference query/parser.py:104-109)."""
+    if not expr.strip():
+        raise QueryError("empty scalar condition")
+    if number:
+        if "|" in expr:
+            raise QueryError(f"`|` is not allowed for scalar operations: `{expr}`")
+        if ".." in expr:
+            raise QueryError(f"`..` is not allowed for scalar operations: `{expr}`")
     neg = expr.startswith("~")
     if neg:
         expr = expr[1:].strip()
-    m = _SCALAR.match(expr)
-    if m is None:
+    op, raw = parse_comparison(expr)
+    op = op or "="
+    if not raw:
         raise QueryError("empty scalar condition")
-    op = m.group(1) or "="
-    raw = m.group(2).strip()
     val = _parse_number(raw) if number else raw
     return neg, op, val
 
@@ -91,17 +112,22 @@ def parse_value(expr: str) -> Tuple[bool, str, Any]:
 
 
 def parse_datetime_op(expr: str) -> Tuple[bool, str, Any]:
+    """Datetime condition (reference parse_datetime_operation): a comparison or an ``a .. b`` range; ``|`` is not
+    allowed and a range takes exactly two bounds."""
+    if "|" in expr:
+        raise QueryError(f"`|` is not allowed for datetime operations: `{expr}`")
     neg = expr.startswith("~")
     if neg:
         expr = expr[1:].strip()
     if ".." in expr:
-        a, b = [p.strip() for p in expr.split("..", 1)]
-        return neg, "range", (parse_datetime(a), parse_datetime(b))
-    m = _SCALAR.match(expr)
-    if m is None:
+        parts = [p.strip() for p in expr.split("..") if p.strip()]
+        if len(parts) != 2:
+            raise QueryError(f"a datetime range needs exactly 2 bounds: `{expr}`")
+        return neg, "range", (parse_datetime(parts[0]), parse_datetime(parts[1]))
+    op, raw = parse_comparison(expr)
+    if not raw:
         raise QueryError("empty datetime condition")
-    op = m.group(1) or "="
-    return neg, op, parse_datetime(m.group(2))
+    return neg, op or "=", parse_datetime(raw)
 
 
 class BaseQuery:

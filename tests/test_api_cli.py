@@ -236,3 +236,29 @@ def test_admin_table_browser(api):
     assert client.delete(f"/api/v1/admin/tables/projects/{proj['id']}").status_code == 404
     tok = client.post("/api/v1/users", json={"username": "bob"}).json()["token"]
     assert client.get("/api/v1/admin/tables", headers={"Authorization": f"token {tok}"}).status_code == 403
+
+
+def test_project_listing_privacy_and_ephemeral_scope(api):
+    """Advisor round 1: private projects are not listed to other users, ephemeral per-trial tokens cannot use
+    non-experiment routes, and the admin browser redacts password hashes."""
+    client, flow = api
+    assert client.post("/api/v1/projects", json={"name": "secret", "is_public": False}).status_code == 201
+    assert client.post("/api/v1/projects", json={"name": "open"}).status_code == 201
+    tok = client.post("/api/v1/users", json={"username": "carol"}).json()["token"]
+    carol = {"Authorization": f"token {tok}"}
+    names = [p["name"] for p in client.get("/api/v1/projects", headers=carol).json()["results"]]
+    assert "open" in names and "secret" not in names
+    assert {"open", "secret"} <= {p["name"] for p in client.get("/api/v1/projects").json()["results"]}
+    # an ephemeral token for one experiment
+    content = {"version": 1, "kind": "experiment", "run": {"cmd": "true"}}
+    xid = client.post("/api/v1/root/open/experiments", json={"content": content}).json()["id"]
+    eph = client.post(f"/api/v1/root/open/experiments/{xid}/ephemeraltoken").json()["token"]
+    e = {"Authorization": f"token {eph}"}
+    assert client.get(f"/api/v1/root/open/experiments/{xid}", headers=e).status_code == 200
+    assert client.get("/api/v1/projects", headers=e).status_code == 403
+    assert client.get("/api/v1/root/open/experiments", headers=e).status_code == 403
+    # password hashes never leave through the admin browser
+
+    flow.store.execute("INSERT OR REPLACE INTO user_credentials (username, password_hash) VALUES ('carol', 'pbkdf2$x')")
+    rows = client.get("/api/v1/admin/tables/user_credentials").json()["results"]
+    assert rows and all(r["password_hash"] == "***" for r in rows)

@@ -129,3 +129,27 @@ def test_group_and_job_queries():
     assert j.where("status:~failed")[0] and j.order_by("created_at")
     with pytest.raises(QueryError):
         g.where("metric.loss:1")
+
+
+def test_reference_operator_aliases_and_rejections():
+    """query/parser.py:25-41 accepts ``=<`` / ``=>`` as ``<=`` / ``>=``; :104-109 rejects ``|`` and ``..`` in
+    scalar conditions; datetime conditions reject ``|`` and ranges with more than two bounds."""
+    from polyaxon_amd.store.query import ExperimentQuery, QueryError, parse_datetime_op, parse_scalar
+
+    assert parse_scalar("=<0.5") == (False, "<=", 0.5)
+    assert parse_scalar("=>3") == (False, ">=", 3)
+    assert parse_scalar("~=<2") == (True, "<=", 2)
+    assert parse_scalar("<-0.12") == (False, "<", -0.12)
+    for bad in ("1|2", "1..2", "~0.1|0.2", "", "abc"):
+        with pytest.raises(QueryError):
+            parse_scalar(bad)
+    assert parse_datetime_op("=>2018-01-01")[1] == ">="
+    with pytest.raises(QueryError):
+        parse_datetime_op("2018-01-01|2018-02-01")
+    with pytest.raises(QueryError):
+        parse_datetime_op("2018-01-01 .. 2018-02-01 .. 2018-03-01")
+    q = ExperimentQuery()
+    w, p = q.where("metric.loss:=<0.5, created_at:=>2018-01-01")
+    assert len(w) == 2
+    with pytest.raises(QueryError):
+        q.where("metric.loss:0.1|0.2")
