@@ -1,0 +1,88 @@
+"""Multi-GPU readiness proven on one MI355X: the framework RCCL communicator (csrc/rccl_comm.cpp) at nranks = 1
+and FlatDDP on the nccl (RCCL) backend at world 1, in a child process (RCCL/process-group state stays out of the
+pytest process)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(code: str, timeout: int = 180) -> dict:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+               PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, "-c", textwrap.dedent(code)], capture_output=True, text=True,
+                         timeout=timeout, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-4000:]
+    return json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def test_rccl_comm_single_rank_collectives():
+    res = _run("""
+        import json, torch
+        from polyaxon_amd.parallel.rccl import RcclComm
+        from polyaxon_amd.ops import _native
+        torch.cuda.set_device(0)
+        comm = RcclComm(RcclComm.new_unique_id(), 1, 0, 0)
+        x = torch.arange(1024, dtype=torch.float32, device="cuda")
+        comm.all_reduce(x)
+        g = comm.all_gather(torch.full((8,), 3.0, device="cuda"))
+        rs = comm.reduce_scatter(torch.ones(16, device="cuda"))
+        b = comm.broadcast(torch.full((4,), 7.0, dtype=torch.bfloat16, device="cuda"))
+        mx = comm.all_reduce(torch.tensor([5.0], device="cuda"), op="max")
+        torch.cuda.synchronize()
+        alg, bus = comm.bus_bandwidth(64 << 20, iters=5)
+        comm.close()
+        print(json.dumps({"sum_ok": bool(torch.equal(x, torch.arange(1024, dtype=torch.float32, device="cuda"))),
+                          "gather": g.shape[0], "gather_ok": bool((g == 3).all()), "rs": rs.numel(),
+                          "rs_ok": bool((rs == 1).all()), "bcast_ok": bool((b.float() == 7).all()),
+                          "max": float(mx[0]), "algbw": alg, "busbw": bus,
+                          "loaded": "plx_rccl" in _native._loaded}))
+    """)
+    assert res["sum_ok"] and res["gather"] == 1 and res["gather_ok"] and res["rs"] == 16 and res["rs_ok"]
+    assert res["bcast_ok"] and res["max"] == 5.0 and res["loaded"]
+    assert res["algbw"] > 0
+
+
+def test_flat_ddp_on_rccl_backend_world1():
+    res = _run("""
+        import json, torch
+        import torch.distributed as dist
+        from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+        from polyaxon_amd.ops.flat import FlatParams
+        from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
+        import os
+        os.environ["WORLD_SIZE"] = "1"
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        info = init_from_env("nccl")
+        torch.manual_seed(0)
+        m = Transformer(tiny_llama()).cuda()
+        flat = FlatParams(m, info["device"], channels_last=False)
+        ddp = FlatDDP(flat, bucket_mb=0.01)
+        ddp.broadcast_params()
+        tok = torch.randint(0, 256, (4, 16), device="cuda")
+        lm_loss(m(tok), tok).backward()
+        ddp.finish()
+        torch.cuda.synchronize()
+        g = flat.grads.clone()
+        # the same step without DDP
+        torch.manual_seed(0)
+        m2 = Transformer(tiny_llama()).cuda()
+        f2 = FlatParams(m2, info["device"], channels_last=False)
+        lm_loss(m2(tok), tok).backward()
+        print(json.dumps({"backend": dist.get_backend(), "buckets": len(ddp.buckets),
+                          "err": float((g - f2.grads).abs().max()), "norm": float(g.norm())}))
+        dist.destroy_process_group()
+    """)
+    assert res["backend"] == "nccl" and res["buckets"] > 1
+    assert res["norm"] > 0 and res["err"] < 1e-5

@@ -60,16 +60,53 @@ def test_flat_ddp_gloo_world2(overlap):
     assert abs(res[0][2] - res[1][2]) < 1e-6
 
 
-def test_ddp_matches_single_process_average():
-    """Averaged DDP gradient == gradient of the mean loss over both ranks' batches (computed in one process)."""
-    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+def _avg_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
 
+    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
+
+    init_from_env("gloo")
+    torch.manual_seed(0)
+    model = Transformer(tiny_llama())
+    flat = FlatParams(model, "cpu", channels_last=False)
+    ddp = FlatDDP(flat, bucket_mb=0.01)
+    ddp.broadcast_params()
+    tokens = torch.randint(0, 256, (4, 16), generator=torch.Generator().manual_seed(100 + rank))
+    lm_loss(model(tokens), tokens).backward()
+    ddp.finish()
+    q.put((rank, flat.grads.clone()))
+    dist.destroy_process_group()
+
+
+def test_ddp_matches_single_process_average():
+    """FlatDDP over gloo (world 2, each rank its own batch) yields on every rank exactly the gradient of the MEAN
+    of the two ranks' losses computed in one process -- the DP correctness contract."""
+    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_avg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
     torch.manual_seed(0)
     m = Transformer(tiny_llama())
+    flat = FlatParams(m, "cpu", channels_last=False)
     toks = [torch.randint(0, 256, (4, 16), generator=torch.Generator().manual_seed(100 + r)) for r in range(2)]
-    loss = sum(lm_loss(m(t), t) for t in toks) / 2
-    loss.backward()
-    assert all(p.grad is not None for p in m.parameters())
+    (sum(lm_loss(m(t), t) for t in toks) / 2).backward()
+    ref = flat.grads.clone()
+    assert float(ref.norm()) > 0
+    for r in (0, 1):
+        torch.testing.assert_close(got[r], ref, rtol=1e-4, atol=1e-6)
 
 
 def _lp_worker(rank, world, port, q):
