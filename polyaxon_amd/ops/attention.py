@@ -8,7 +8,8 @@ so no transpose copy follows attention.  Backward recomputes the probabilities f
 128-key block x one query head (fp32 per-head partials summed over the GQA group by a reduce kernel;
 no atomics).
 
-CPU tensors (unit tests) use the fp32 PyTorch definition; on a GPU the HIP kernels are the only path.
+CPU tensors, fp32 and other head dims use the plain fp32 math definition (``_reference``); bf16 with head_dim
+64 / 128 on a GPU -- every training config -- always runs the HIP kernels.
 """
 from __future__ import annotations
 
@@ -17,7 +18,6 @@ import math
 from typing import Optional
 
 import torch
-import torch.nn.functional as F
 
 from polyaxon_amd.ops import _native
 
@@ -74,10 +74,17 @@ def _args(q, k, v, causal: bool, scale: float) -> _AttnArgs:
 
 
 def _reference(q, k, v, causal, scale):
+    """Plain fp32 math (matmul + softmax): the CPU path and the path for shapes / dtypes the HIP kernel does not
+    take (fp32 reference models, head_dim other than 64 / 128).  No SDPA, so no library attention kernel."""
     rep = q.shape[1] // k.shape[1]
     kk = k.repeat_interleave(rep, 1) if rep > 1 else k
     vv = v.repeat_interleave(rep, 1) if rep > 1 else v
-    return F.scaled_dot_product_attention(q, kk, vv, is_causal=causal, scale=scale).transpose(1, 2)
+    s = torch.matmul(q.float(), kk.float().transpose(-1, -2)) * scale
+    if causal:
+        S, Sk = q.shape[2], k.shape[2]
+        s = s.masked_fill(torch.ones(S, Sk, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
+    o = torch.matmul(s.softmax(-1), vv.float()).to(q.dtype)
+    return o.transpose(1, 2)
 
 
 class _FlashAttention(torch.autograd.Function):
@@ -129,8 +136,6 @@ def flash_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, causal: b
     if q.shape[1] % k.shape[1]:
         raise ValueError("query heads must be a multiple of key/value heads")
     scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else float(scale)
-    if not q.is_cuda:
+    if not q.is_cuda or q.dtype != torch.bfloat16 or q.shape[-1] not in (64, 128):
         return _reference(q, k, v, causal, scale)
-    if q.dtype != torch.bfloat16 or q.shape[-1] not in (64, 128):
-        raise ValueError("the HIP flash attention takes bf16 with head_dim 64 or 128")
     return _FlashAttention.apply(q, k, v, causal, scale)
