@@ -29,7 +29,7 @@ LIBRARIES: Dict[str, dict] = {
     "plx_polytune": {"sources": ["polytune_kernels.hip"], "kind": "hip", "link": []},
     "plx_bn": {"sources": ["bn_kernels.hip"], "kind": "hip", "link": []},
     "plx_procmon": {"sources": ["procmon.cpp"], "kind": "cpp", "link": ["-lpthread"]},
-    "plx_gp": {"sources": ["gp_kernels.hip"], "kind": "hip", "link": []},
+    "plx_gp": {"sources": ["gp_kernels.hip", "gp_chol.hip"], "kind": "hip", "link": []},
     "plx_rms": {"sources": ["rmsnorm.hip"], "kind": "hip", "link": []},
     "plx_conv": {"sources": ["conv_gemm.hip"], "kind": "hip", "link": []},
     "plx_pool": {"sources": ["pool_kernels.hip"], "kind": "hip", "link": []},
@@ -175,11 +175,17 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_pm_count": [_P],
     },
     "plx_gp": {
-        "plx_gp_kmat": [_P, _P, _I, _I, _I, _P, _I, _I, _F, _F, _F, _I, _F, _P],
+        "plx_gp_kmat": [_P, _P, _I, _I, _I, _P, _I, _I, _F, _F, _F, _I, _F, _P, _P, _D, _I, _P],
         "plx_gp_chol": [_P, _I, _I, _P, _P],
-        "plx_gp_kmat_batch_f64": [_P, _I, _I, _P, _I, _P, _I, _D, _D, _D, _P],
+        "plx_gp_kmat_batch_f64": [_P, _I, _I, _P, _I, _P, _I, _L, _I, _D, _D, _D, _P, _P, _D, _I, _P],
+        "plx_gp_matern_table": [_D, _D, _D, _I, _P, _P, _P],
+        "plx_gp_chol_aug_f64": [_P, _I, _I, _I, _L, _I, _P, _P],
+        "plx_gp_lml_f64": [_P, _I, _I, _L, _I, _P, _P, _P],
+        "plx_gp_acq_rows": [_P, _I, _I, _P, _F, _I, _F, _F, _F, _P, _P, _P, _P],
         "plx_gp_predict_acq": [_P, _I, _P, _I, _I, _P, _I, _P, _I, _F, _F, _F, _F, _I, _F, _F, _F, _P, _P, _P, _P,
-                               _P, _P],
+                               _P, _P, _P, _D, _I, _P],
+        "plx_gp_ascent": [_P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _I, _F, _F, _F, _F, _I, _F, _F, _F, _I, _P, _P, _D, _I,
+                          _P],
     },
     "plx_conv": {
         "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],

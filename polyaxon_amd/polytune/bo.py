@@ -230,11 +230,18 @@ def acquisition_np(mean, std, acq: str, y_max: float, kappa: float, eps: float) 
 class HipGP:
     """GP posterior + acquisition on the MI355X kernels. Training data and factors stay on the device.
 
-    Gram matrices are always built by our kernels; fp64 factorisations above ``DEVICE_FACTOR_MAX`` rows run
-    through LAPACK on the host (a one-off D2H of the Gram): torch's device Cholesky faulted the GPU at n = 1000
-    on this ROCm build (scripts/diag_bo1000.py), while n <= 128 goes through our LDS Cholesky or torch."""
+    Every factorisation is ours: the blocked fp64 Cholesky of csrc/gp_chol.hip, batched over length scales, with
+    right-hand sides appended as extra rows (y -> z = L^-1 y for the LML; the identity -> L^-T for the posterior),
+    so there is no host LAPACK and no rocSOLVER call at any n (torch's device Cholesky faulted the GPU at n = 1000
+    on this ROCm build).  The posterior for m candidates is one MFMA cross-kernel launch, one GEMM with L^-T
+    (V = K* L^-T, rows v_c = L^-1 k_c) and one fused mean/variance/acquisition epilogue; n <= 64 keeps the
+    single fused predict+acquisition kernel."""
 
-    DEVICE_FACTOR_MAX = 128
+    FUSED_MAX = 64
+    TABLE_NODES = 16384
+    TABLE_SMAX = 50.0  # tabulate s = sqrt(2 nu) r up to 50: k < 1e-20 beyond
+
+    _tables: Dict[Tuple[str, float], Tuple[Any, Any, float]] = {}
 
     def __init__(self, device=None):
         import torch
@@ -245,6 +252,25 @@ class HipGP:
 
         self.lib = _native.lib("plx_gp")
         self._native = _native
+
+    def table(self, kind: str, nu: float):
+        """(t64 ptr, t32 ptr, rmax, nodes) of the Matern-nu lookup table (built once per device and nu by
+        plx_gp_matern_table); null table for the closed-form kernels."""
+        if kind != "matern_nu":
+            return None, None, 0.0, 0
+        key = (str(self.device), float(nu))
+        if key not in HipGP._tables:
+            t = self.torch
+            n = self.TABLE_NODES
+            rmax = self.TABLE_SMAX / math.sqrt(2.0 * nu)
+            t64 = t.empty(2 * n, dtype=t.float64, device=self.device)
+            t32 = t.empty(2 * n, dtype=t.float32, device=self.device)
+            rc = self.lib.plx_gp_matern_table(float(nu), float(matern_c(nu)), rmax, n, t64.data_ptr(), t32.data_ptr(),
+                                              self._stream())
+            self._native.check(rc, "plx_gp_matern_table")
+            HipGP._tables[key] = (t64, t32, rmax)
+        t64, t32, rmax = HipGP._tables[key]
+        return t64.data_ptr(), t32.data_ptr(), rmax, self.TABLE_NODES
 
     def _stream(self):
         return self.torch.cuda.current_stream(self.device).cuda_stream
@@ -257,19 +283,47 @@ class HipGP:
         rc = self.lib.plx_gp_kmat(A.data_ptr(), B.data_ptr(), A.shape[0], B.shape[0], A.shape[1], K.data_ptr(),
                                   K.shape[1], KIND_IDS[kind], float(ls), float(nu),
                                   float(matern_c(nu)) if kind == "matern_nu" else 0.0, int(diag != 0.0), float(diag),
-                                  self._stream())
+                                  *self.table(kind, nu), self._stream())
         self._native.check(rc, "plx_gp_kmat")
         return K
 
+    def gram_f64(self, X, kind: str, nu: float, inv_ls2, rows: int, diag: float):
+        """fp64 Gram matrices for every 1/ls^2 in ``inv_ls2`` (device fp64 [nb]) into rows [0, n) of a zeroed
+        [nb, rows, n] buffer; rows [n, rows) are left for appended right-hand sides."""
+        t = self.torch
+        Xd = t.as_tensor(np.ascontiguousarray(X, dtype=np.float64), device=self.device)
+        n, d = Xd.shape
+        nb = int(inv_ls2.shape[0])
+        A = t.zeros((nb, rows, n), dtype=t.float64, device=self.device)
+        rc = self.lib.plx_gp_kmat_batch_f64(Xd.data_ptr(), n, d, inv_ls2.data_ptr(), nb, A.data_ptr(), n, rows * n,
+                                            KIND_IDS[kind], float(nu),
+                                            float(matern_c(nu)) if kind == "matern_nu" else 0.0, float(diag),
+                                            *self.table(kind, nu), self._stream())
+        self._native.check(rc, "plx_gp_kmat_batch_f64")
+        return A
+
+    def chol_aug(self, A, n: int):
+        """In-place blocked fp64 Cholesky of A [nb, rows, n] (plx_gp_chol_aug_f64). Returns the device int32
+        status per entry (0 = SPD, else the 1-based column of the first non-positive pivot)."""
+        t = self.torch
+        nb, rows = int(A.shape[0]), int(A.shape[1])
+        assert A.dtype == t.float64 and A.is_contiguous() and A.shape[2] == n and rows >= n
+        status = t.zeros(nb, dtype=t.int32, device=self.device)
+        rc = self.lib.plx_gp_chol_aug_f64(A.data_ptr(), n, rows, n, rows * n, nb, status.data_ptr(), self._stream())
+        self._native.check(rc, "plx_gp_chol_aug_f64")
+        return status
+
     def cholesky(self, K):
+        """Lower Cholesky factor of one SPD matrix (fp32 in/out): the single-workgroup LDS kernel up to n = 128,
+        the blocked fp64 kernel above."""
         t = self.torch
         n = K.shape[0]
         if n > 128:
-            try:
-                L = np.linalg.cholesky(K.double().cpu().numpy())
-            except np.linalg.LinAlgError as e:
-                raise np.linalg.LinAlgError(str(e))
-            return t.as_tensor(L, dtype=t.float32, device=self.device)
+            A = K.to(t.float64).contiguous()[None].clone()
+            st = int(self.chol_aug(A, n)[0].item())
+            if st != 0:
+                raise np.linalg.LinAlgError(f"not positive definite at column {st}")
+            return A[0].tril().to(t.float32)
         status = t.zeros(1, dtype=t.int32, device=self.device)
         out = K.clone()
         rc = self.lib.plx_gp_chol(out.data_ptr(), n, n, status.data_ptr(), self._stream())
@@ -279,57 +333,29 @@ class HipGP:
         return out
 
     def lml_batch(self, X, y, kind: str, nu: float, log_ls, alpha: float = 1e-10):
-        """Log marginal likelihood at every length scale exp(log_ls): ONE fp64 Gram launch for the whole batch
-        (plx_gp_kmat_batch_f64), fp64 Cholesky per scale, one batched solve."""
+        """Log marginal likelihood at every length scale exp(log_ls) with sklearn's semantics (fp64, alpha on the
+        diagonal, -inf when not positive definite): one batched Gram launch, one batched blocked Cholesky with y
+        appended (z = L^-1 y), one reduction launch; a single D2H of nb values."""
         t = self.torch
-        Xd = t.as_tensor(np.ascontiguousarray(X, dtype=np.float64), device=self.device)
-        yd = t.as_tensor(y, dtype=t.float64, device=self.device)
-        n, d = Xd.shape
+        n = len(X)
         nb = len(log_ls)
         inv = t.tensor([math.exp(-2.0 * float(l)) for l in log_ls], dtype=t.float64, device=self.device)
-        Ks = t.empty((nb, n, n), dtype=t.float64, device=self.device)
-        rc = self.lib.plx_gp_kmat_batch_f64(Xd.data_ptr(), n, d, inv.data_ptr(), nb, Ks.data_ptr(), KIND_IDS[kind],
-                                            float(nu), float(matern_c(nu)) if kind == "matern_nu" else 0.0,
-                                            float(alpha), self._stream())
-        self._native.check(rc, "plx_gp_kmat_batch_f64")
-        if n > self.DEVICE_FACTOR_MAX:
-            return self._lml_host(Ks.cpu().numpy(), np.asarray(y, dtype=np.float64))
-        # one factorisation per scale: a batched cholesky_ex on ROCm does not keep the other batch entries
-        # valid once one of them is not positive definite (measured: wrong LMLs beside a failing entry)
-        Ls, oks = [], []
-        for b in range(nb):
-            Lb, ib = t.linalg.cholesky_ex(Ks[b])
-            Ls.append(Lb)
-            oks.append(ib == 0)
-        L, ok = t.stack(Ls), t.stack(oks)
-        L = t.where(ok[:, None, None], L, t.eye(n, dtype=L.dtype, device=self.device).expand_as(L))
-        a = t.cholesky_solve(yd[None, :, None].expand(nb, n, 1).contiguous(), L)[..., 0]
-        lml = -0.5 * (a * yd[None]).sum(1) - t.log(t.diagonal(L, dim1=1, dim2=2)).sum(1) - 0.5 * n * math.log(2 * math.pi)
-        lml = t.where(ok & t.isfinite(lml), lml, t.full_like(lml, -math.inf))
-        return lml.cpu().numpy()
-
-    @staticmethod
-    def _lml_host(Ks: np.ndarray, y: np.ndarray) -> np.ndarray:
-        """fp64 LAPACK factorisations of device-built Gram matrices (sklearn semantics: not PD -> -inf)."""
-        out = np.full(Ks.shape[0], -np.inf)
-        n = Ks.shape[1]
-        for b in range(Ks.shape[0]):
-            try:
-                L = np.linalg.cholesky(Ks[b])
-            except np.linalg.LinAlgError:
-                continue
-            from scipy.linalg import cho_solve
-
-            a = cho_solve((L, True), y)
-            v = -0.5 * float(y @ a) - float(np.log(np.diag(L)).sum()) - 0.5 * n * math.log(2 * math.pi)
-            out[b] = v if math.isfinite(v) else -np.inf
-        return out
+        A = self.gram_f64(X, kind, nu, inv, n + 1, alpha)
+        A[:, n, :] = t.as_tensor(np.asarray(y, dtype=np.float64), device=self.device)
+        status = self.chol_aug(A, n)
+        out = t.empty(nb, dtype=t.float64, device=self.device)
+        rc = self.lib.plx_gp_lml_f64(A.data_ptr(), n, n, (n + 1) * n, nb, status.data_ptr(), out.data_ptr(),
+                                     self._stream())
+        self._native.check(rc, "plx_gp_lml_f64")
+        return out.cpu().numpy()
 
     def fit_length_scale(self, X, y, kind: str, nu: float, length_scale: float, alpha: float = 1e-10,
-                         bounds=(1e-5, 1e5), coarse: int = 24, rounds: int = 3) -> float:
+                         bounds=(1e-5, 1e5), coarse: int = 24, rounds: int = 2, zoom: int = 17) -> float:
         """Maximise the LML over log length scale on the device: a coarse batched grid over the bounds (plus the
         configured initial value, as sklearn always tries it), then batched zoom rounds around the best point.
-        Replaces the host 1-D search, whose O(n^3) factorisations dominate a suggestion at n ~ 1000."""
+        Replaces sklearn's L-BFGS-B on the LML, whose O(n^3) host factorisations dominate a suggestion at n ~ 1000.
+        Each round is one batched factorisation (32 panel steps at n = 1000 whatever the batch), so the search uses
+        few wide rounds: 25 points, then 2 zooms of 17 (final spacing 1/64 in log length scale)."""
         lo, hi = math.log(bounds[0]), math.log(bounds[1])
         grid = list(np.linspace(lo, hi, coarse)) + [math.log(length_scale)]
         vals = self.lml_batch(X, y, kind, nu, grid, alpha)
@@ -337,93 +363,97 @@ class HipGP:
         x_best, f_best = grid[best], vals[best]
         step = (hi - lo) / (coarse - 1)
         for _ in range(rounds):
-            g = list(np.linspace(max(lo, x_best - step), min(hi, x_best + step), 9))
+            g = list(np.linspace(max(lo, x_best - step), min(hi, x_best + step), zoom))
             v = self.lml_batch(X, y, kind, nu, g, alpha)
             i = int(np.argmax(v))
             if v[i] > f_best:
                 x_best, f_best = g[i], v[i]
-            step /= 4.0
+            step = 2.0 * step / (zoom - 1)
         return math.exp(x_best) if math.isfinite(f_best) else float(length_scale)
 
-    def fit(self, gp: GPState):
-        """Device factors for a fitted GP (length scale from the LML search): (X, L, alpha, L^-1 or None).
+    def fit(self, gp: GPState, alpha: float = 1e-10):
+        """Device factors of a fitted GP: (X fp32, L fp32, alpha fp32, L^-T fp32, z fp32).
 
-        n <= DEVICE_FACTOR_MAX: our LDS Cholesky + device triangular solves.  Larger n: the Gram comes from our
-        kernel, the fp64 factorisation, alpha and the explicit L^-1 from LAPACK; the posterior variance then
-        needs only a GEMM (v = L^-1 k*^T) on the device instead of a triangular solve."""
+        One blocked fp64 Cholesky of [K; y^T; I] (2n + 1 rows): row n comes back as z = L^-1 y and rows n+1.. as
+        L^-T, so alpha = L^-T z and the posterior needs only a GEMM.  A matrix that is not positive definite is
+        retried with growing diagonal jitter (one status readback per attempt)."""
         t = self.torch
         n = len(gp.X)
-        K = self.kmat(gp.X, gp.X, gp.kind, gp.ls, gp.nu, diag=1e-10)
-        Xd = t.as_tensor(gp.X, dtype=t.float32, device=self.device).contiguous()
-        if n > self.DEVICE_FACTOR_MAX:
-            from scipy.linalg import cho_solve, solve_triangular
-
-            Kh = K.double().cpu().numpy()
-            jitter = 0.0
-            for _ in range(8):
-                try:
-                    Lh = np.linalg.cholesky(Kh + jitter * np.eye(n) if jitter else Kh)
-                    break
-                except np.linalg.LinAlgError:
-                    jitter = max(jitter * 10, 1e-8)
-            else:
-                raise np.linalg.LinAlgError("GP Gram matrix not positive definite")
-            ah = cho_solve((Lh, True), np.asarray(gp.y, dtype=np.float64))
-            Linv = solve_triangular(Lh, np.eye(n), lower=True)
-            f32 = dict(dtype=t.float32, device=self.device)
-            return Xd, t.as_tensor(Lh, **f32).contiguous(), t.as_tensor(ah, **f32).contiguous(), \
-                t.as_tensor(Linv, **f32).contiguous()
+        inv = t.tensor([1.0 / (gp.ls * gp.ls)], dtype=t.float64, device=self.device)
+        yd = t.as_tensor(np.asarray(gp.y, dtype=np.float64), device=self.device)
+        eye = t.eye(n, dtype=t.float64, device=self.device)
         jitter = 0.0
-        for _ in range(6):
-            try:
-                L = self.cholesky(K if jitter == 0 else K + jitter * t.eye(K.shape[0], device=self.device))
+        for _ in range(8):
+            A = self.gram_f64(gp.X, gp.kind, gp.nu, inv, 2 * n + 1, alpha + jitter)
+            A[0, n] = yd
+            A[0, n + 1:] = eye
+            if int(self.chol_aug(A, n)[0].item()) == 0:
                 break
-            except np.linalg.LinAlgError:
-                jitter = max(jitter * 10, 1e-8)
-        y = t.as_tensor(gp.y, dtype=t.float32, device=self.device)
-        alpha = t.cholesky_solve(y[:, None], L)[:, 0]
-        return Xd, L.contiguous(), alpha.contiguous(), None
+            jitter = max(jitter * 10, 1e-8)
+        else:
+            raise np.linalg.LinAlgError("GP Gram matrix not positive definite")
+        A = A[0]
+        z = A[n]
+        LinvT = A[n + 1:]
+        a = LinvT @ z
+        f32 = dict(dtype=t.float32)
+        Xd = t.as_tensor(gp.X, dtype=t.float32, device=self.device).contiguous()
+        return (Xd, A[:n].tril().to(**f32).contiguous(), a.to(**f32).contiguous(), LinvT.to(**f32).contiguous(),
+                z.to(**f32).contiguous())
+
+    def acq_dev(self, gp: GPState, dev_state, Xc, acq: str, y_max: float, kappa: float, eps: float,
+                mean=None, std=None):
+        """Acquisition of every candidate row of Xc (device fp32 [m, d]) as a device tensor; no host sync."""
+        t = self.torch
+        Xd, L, alpha, LinvT, z = dev_state
+        m, n, d = Xc.shape[0], Xd.shape[0], Xd.shape[1]
+        acq_id = {"ucb": 0, "ei": 1, "poi": 2}[acq]
+        out = t.empty(m, dtype=t.float32, device=self.device)
+        mp = mean.data_ptr() if mean is not None else None
+        sp = std.data_ptr() if std is not None else None
+        if n <= self.FUSED_MAX and d <= 16:
+            rc = self.lib.plx_gp_predict_acq(
+                Xc.data_ptr(), m, Xd.data_ptr(), n, d, L.data_ptr(), n, alpha.data_ptr(), KIND_IDS[gp.kind],
+                float(gp.ls), float(gp.nu), float(matern_c(gp.nu)) if gp.kind == "matern_nu" else 0.0, 1.0, acq_id,
+                float(kappa), float(eps), float(y_max), out.data_ptr(), mp, sp, None, None, *self.table(gp.kind, gp.nu),
+                self._stream())
+            self._native.check(rc, "plx_gp_predict_acq")
+            return out
+        Ks = self.kmat(Xc, Xd, gp.kind, gp.ls, gp.nu)  # MFMA cross-kernel, fused Matern epilogue
+        V = Ks @ LinvT  # row c = (L^-1 k_c)^T
+        rc = self.lib.plx_gp_acq_rows(V.data_ptr(), m, n, z.data_ptr(), 1.0, acq_id, float(kappa), float(eps),
+                                      float(y_max), out.data_ptr(), mp, sp, self._stream())
+        self._native.check(rc, "plx_gp_acq_rows")
+        return out
+
+    def fused(self, dev_state) -> bool:
+        return dev_state[0].shape[0] <= self.FUSED_MAX and dev_state[0].shape[1] <= 16
+
+    def ascent(self, gp: GPState, dev_state, xs, lo, hi, acq: str, y_max: float, kappa: float, eps: float,
+               steps: int):
+        """In-place multi-start ascent of the seeds xs (device fp32 [k, d]) in ONE launch (plx_gp_ascent, fused
+        posterior, n <= 64); returns the device fp32 [k] acquisition values at the final points."""
+        t = self.torch
+        Xd, L, alpha, _, _ = dev_state
+        k, d = xs.shape
+        fx = t.empty(k, dtype=t.float32, device=self.device)
+        rc = self.lib.plx_gp_ascent(xs.data_ptr(), fx.data_ptr(), k, lo.data_ptr(), hi.data_ptr(), Xd.data_ptr(),
+                                    Xd.shape[0], d, L.data_ptr(), alpha.data_ptr(), KIND_IDS[gp.kind], float(gp.ls),
+                                    float(gp.nu), float(matern_c(gp.nu)) if gp.kind == "matern_nu" else 0.0, 1.0,
+                                    {"ucb": 0, "ei": 1, "poi": 2}[acq], float(kappa), float(eps), float(y_max),
+                                    int(steps), *self.table(gp.kind, gp.nu), self._stream())
+        self._native.check(rc, "plx_gp_ascent")
+        return fx
 
     def predict_acq(self, gp: GPState, dev_state, Xc, acq: str, y_max: float, kappa: float, eps: float,
                     want_mean_std: bool = False):
         t = self.torch
-        Xd, L, alpha, Linv = dev_state
         Xc = t.as_tensor(Xc, dtype=t.float32, device=self.device).contiguous()
-        m, n, d = Xc.shape[0], Xd.shape[0], Xd.shape[1]
-        acq_id = {"ucb": 0, "ei": 1, "poi": 2}[acq]
-        out = t.empty(m, dtype=t.float32, device=self.device)
+        m = Xc.shape[0]
         mean = t.empty(m, dtype=t.float32, device=self.device) if want_mean_std else None
         std = t.empty(m, dtype=t.float32, device=self.device) if want_mean_std else None
-        nblk = (m + 255) // 256
-        bb = t.empty(nblk, dtype=t.float32, device=self.device)
-        bi = t.empty(nblk, dtype=t.int32, device=self.device)
-        if n <= 64 and d <= 16:
-            rc = self.lib.plx_gp_predict_acq(
-                Xc.data_ptr(), m, Xd.data_ptr(), n, d, L.data_ptr(), n, alpha.data_ptr(), KIND_IDS[gp.kind],
-                float(gp.ls), float(gp.nu), float(matern_c(gp.nu)) if gp.kind == "matern_nu" else 0.0, 1.0, acq_id,
-                float(kappa), float(eps), float(y_max), out.data_ptr(), mean.data_ptr() if mean is not None else None,
-                std.data_ptr() if std is not None else None, bb.data_ptr(), bi.data_ptr(), self._stream())
-            self._native.check(rc, "plx_gp_predict_acq")
-            best = int(bi[int(t.argmax(bb))].item())
-        else:  # large n: MFMA cross-kernel + TRSM, acquisition in torch
-            Ks = self.kmat(Xc, Xd, gp.kind, gp.ls, gp.nu)
-            mu = Ks @ alpha
-            v = Linv @ Ks.T if Linv is not None else t.linalg.solve_triangular(L, Ks.T, upper=False)
-            sd = (1.0 - (v * v).sum(0)).clamp_min(0).sqrt()
-            out = self._acq_torch(mu, sd, acq, y_max, kappa, eps)
-            best = int(t.argmax(out).item())
-            mean, std = mu, sd
-        return out, best, mean, std
-
-    def _acq_torch(self, mu, sd, acq, y_max, kappa, eps):
-        t = self.torch
-        if acq == "ucb":
-            return mu + kappa * sd
-        z = t.where(sd > 0, (mu - y_max - eps) / sd.clamp_min(1e-30), t.zeros_like(sd))
-        cdf = 0.5 * t.erfc(-z / math.sqrt(2))
-        if acq == "poi":
-            return cdf
-        return (mu - y_max - eps) * cdf + sd * t.exp(-0.5 * z * z) / math.sqrt(2 * math.pi)
+        out = self.acq_dev(gp, dev_state, Xc, acq, y_max, kappa, eps, mean, std)
+        return out, int(t.argmax(out).item()), mean, std
 
 
 # ================================================================================ utility function / optimizer
@@ -505,28 +535,31 @@ class UtilityFunction:
                 if max_acq is None or val >= max_acq:
                     x_max, max_acq = res.x, val
             return np.clip(x_max, bounds[:, 0], bounds[:, 1])
-        # batched device search: one kernel launch per round over all candidates
+        if self.backend == "hip":
+            return self._max_compute_device(y_max, bounds, n_warmup, n_iter)
+        # batched search (numpy backend with a large warm-up): one evaluation per round over all candidates
         d = bounds.shape[0]
         lo, hi = bounds[:, 0], bounds[:, 1]
         width = np.maximum(hi - lo, 1e-12)
         cand = rng.uniform(lo, hi, size=(max(n_warmup, 1), d))
         ys = self.compute(cand, y_max)
-        best_i = int(np.argmax(ys))
-        x_max, max_acq = cand[best_i], ys[best_i]
-        top = cand[np.argsort(-ys)[:max(1, min(64, len(cand)))]]
+        order = np.argsort(-ys)[:max(1, min(64, len(cand)))]
+        top, top_v = cand[order], ys[order]
+        x_max, max_acq = top[0], top_v[0]
         scale = 0.1
         for _ in range(max(n_iter, 1)):
             pert = top[rng.randint(0, len(top), size=4096)] + rng.normal(0, 1, size=(4096, d)) * width * scale
             pert = np.clip(pert, lo, hi)
             yp = self.compute(pert, y_max)
-            order = np.argsort(-yp)
-            if yp[order[0]] >= max_acq:
-                x_max, max_acq = pert[order[0]], yp[order[0]]
-            top = np.concatenate([top, pert[order[:64]]])[: 128]
+            allx, allv = np.concatenate([top, pert]), np.concatenate([top_v, yp])
+            keep = np.argsort(-allv)[:len(top)]
+            top, top_v = allx[keep], allv[keep]
+            if top_v[0] >= max_acq:
+                x_max, max_acq = top[0], top_v[0]
             scale *= 0.7
         # batched multi-start projected gradient ascent (the reference's L-BFGS-B restarts, all seeds at once):
-        # central differences for every seed and coordinate are ONE acquisition launch per step
-        seeds = np.concatenate([x_max[None], top[:15]])
+        # central differences for every seed and coordinate are ONE acquisition evaluation per step
+        seeds = np.concatenate([x_max[None], top[1:16]])
         xs, fx = self._ascend(seeds, y_max, lo, hi, width)
         i = int(np.argmax(fx))
         if fx[i] >= max_acq:
@@ -551,6 +584,66 @@ class UtilityFunction:
             fx = np.where(better, fc, fx)
             step = np.where(better[:, None], step * 1.2, step * 0.5)
         return xs, fx
+
+    def _max_compute_device(self, y_max: float, bounds: np.ndarray, n_warmup: int, n_iter: int,
+                            ascent_steps: int = 25) -> np.ndarray:
+        """The same search as the batched numpy path, held on the device end to end: random warm-up, refinement
+        rounds around the running top-64, then multi-start finite-difference ascent.  Candidates, acquisition
+        values, top-k and the incumbent never leave HBM; the only host readback is the final argmax point."""
+        import torch as t
+
+        hip, gp, dev = self._hip, self._gp, self._dev
+        device = hip.device
+        acq, kappa, eps = self.acquisition_function, self.kappa, self.eps
+        g = t.Generator(device=device)
+        g.manual_seed(int(self.random_generator.randint(0, 2 ** 31 - 1)))
+        d = bounds.shape[0]
+        f32 = dict(dtype=t.float32, device=device)
+        lo, hi = t.tensor(bounds[:, 0], **f32), t.tensor(bounds[:, 1], **f32)
+        width = (hi - lo).clamp_min(1e-12)
+
+        def f(x):
+            return hip.acq_dev(gp, dev, x.contiguous(), acq, y_max, kappa, eps)
+
+        cand = lo + width * t.rand((max(n_warmup, 1), d), generator=g, **f32)
+        ys = f(cand)
+        top_v, ti = t.topk(ys, min(64, ys.shape[0]))
+        top = cand[ti]
+        x_max, max_acq = top[0], top_v[0]
+        scale = 0.1
+        for _ in range(max(n_iter, 1)):
+            idx = t.randint(0, top.shape[0], (4096,), generator=g, device=device)
+            pert = t.minimum(t.maximum(top[idx] + t.randn((4096, d), generator=g, **f32) * width * scale, lo), hi)
+            yp = f(pert)
+            allv = t.cat([top_v, yp])
+            top_v, keep = t.topk(allv, top.shape[0])
+            top = t.cat([top, pert])[keep]
+            x_max = t.where(top_v[0] >= max_acq, top[0], x_max)
+            max_acq = t.maximum(max_acq, top_v[0])
+            scale *= 0.7
+        xs = t.cat([x_max[None], top[1:16]]).contiguous()
+        k = xs.shape[0]
+        if hip.fused(dev):  # the whole ascent in one launch
+            fx = hip.ascent(gp, dev, xs, lo, hi, acq, y_max, kappa, eps, ascent_steps)
+        else:
+            fx = f(xs)
+            h = 1e-4 * width
+            step = (0.05 * width).expand(k, d).clone()
+            eye = t.eye(d, **f32)
+            for _ in range(ascent_steps):
+                probe = t.cat([xs[:, None, :] + eye[None] * h, xs[:, None, :] - eye[None] * h], dim=1).reshape(-1, d)
+                fp = f(t.minimum(t.maximum(probe, lo), hi)).reshape(k, 2 * d)
+                grad = (fp[:, :d] - fp[:, d:]) / (2 * h)
+                gn = (grad / width).norm(dim=1, keepdim=True).clamp_min(1e-30)
+                c = t.minimum(t.maximum(xs + step * grad / gn, lo), hi)
+                fc = f(c)
+                better = fc > fx
+                xs = t.where(better[:, None], c, xs)
+                fx = t.where(better, fc, fx)
+                step = t.where(better[:, None], step * 1.2, step * 0.5)
+        i = t.argmax(fx)
+        x_max = t.where(fx[i] >= max_acq, xs[i], x_max)
+        return np.clip(x_max.double().cpu().numpy(), bounds[:, 0], bounds[:, 1])
 
 
 class BOOptimizer:
