@@ -735,6 +735,15 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
         return Response(repo.archive(), media_type="application/gzip")
 
     # ------------------------------------------------------------------ pipelines
+    @app.get("/api/v1/{username}/{project}/pipelines")
+    def list_pipelines(username: str, project: str, request: Request, user=Depends(auth)):
+        p = project_or_404(username, project)
+        rows = store._rows(store.execute(
+            "SELECT p.*, (SELECT COUNT(*) FROM pipeline_runs r WHERE r.pipeline_id = p.id) AS num_runs, "
+            "(SELECT r.status FROM pipeline_runs r WHERE r.pipeline_id = p.id ORDER BY r.id DESC LIMIT 1) "
+            "AS last_run_status FROM pipelines p WHERE p.project_id = ? ORDER BY p.id DESC", (p["id"],)))
+        return page(rows, request)
+
     @app.get("/api/v1/{username}/{project}/pipelines/{pid}/runs/{rid}")
     def pipeline_run(username: str, project: str, pid: int, rid: int, user=Depends(auth)):
         r = store.get("pipeline_runs", rid)

@@ -262,3 +262,64 @@ def test_project_listing_privacy_and_ephemeral_scope(api):
     flow.store.execute("INSERT OR REPLACE INTO user_credentials (username, password_hash) VALUES ('carol', 'pbkdf2$x')")
     rows = client.get("/api/v1/admin/tables/user_credentials").json()["results"]
     assert rows and all(r["password_hash"] == "***" for r in rows)
+
+
+def test_dashboard_views_and_their_api_contract(api):
+    """The dashboard's hash views (project tabs, experiment / group / compare / job / pipeline detail) and the
+    fields each reads: one column per declaration and metric, status history, metric points, group hptuning and
+    iterations, replica rows, the pipelines list."""
+    client, flow = api
+    page = client.get("/ui").text
+    for marker in ("#/p/", "/compare/", "Status history", "Hyperparameter vs metric", "Learning curves",
+                   "Side by side", "Iterations", "Replicas", "/pipelines", "esc("):
+        assert marker in page, marker
+    import shutil
+    import subprocess
+
+    node = shutil.which("node")
+    if node:  # the page's script must at least parse
+        js = page.split("<script>", 1)[1].split("</script>", 1)[0]
+        r = subprocess.run([node, "--check", "-"], input=js, capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+    content = {"version": 1, "kind": "group",
+               "hptuning": {"concurrency": 2, "matrix": {"lr": {"values": [0.1, 0.2, 0.3]}},
+                            "grid_search": {"n_experiments": 3}},
+               "run": {"cmd": "echo {{ lr }}"}}
+    gid = client.post("/api/v1/root/dash/groups", json={"content": content}).json()["id"]
+    assert flow.wait("group", gid, timeout=30) == "succeeded"
+    xs = client.get(f"/api/v1/root/dash/groups/{gid}/experiments").json()["results"]
+    assert len(xs) == 3 and all(set(x["declarations"]) == {"lr"} for x in xs)
+    for k, x in enumerate(xs):
+        client.post(f"/api/v1/root/dash/experiments/{x['id']}/metrics",
+                    json=[{"values": {"loss": 1.0 / (k + 1 + s)}, "step": s} for s in range(3)])
+    x0 = xs[0]["id"]
+    x = client.get(f"/api/v1/root/dash/experiments/{x0}").json()
+    assert {"status", "declarations", "last_metric", "started_at", "finished_at", "group_id"} <= set(x)
+    pts = client.get(f"/api/v1/root/dash/experiments/{x0}/metrics", params={"limit": 20000}).json()["results"]
+    assert [p["step"] for p in pts] == [0, 1, 2] and all("loss" in p["values"] for p in pts)
+    sts = client.get(f"/api/v1/root/dash/experiments/{x0}/statuses").json()["results"]
+    assert {"status", "message", "created_at"} <= set(sts[0]) and sts[-1]["status"] == "succeeded"
+    jobs = client.get(f"/api/v1/root/dash/experiments/{x0}/jobs").json()["results"]
+    assert jobs and {"role", "idx", "status"} <= set(jobs[0])
+    g = client.get(f"/api/v1/root/dash/groups/{gid}").json()
+    assert g["search_algorithm"] and g["num_experiments"] == 3 and "hptuning" in g
+    assert client.get(f"/api/v1/root/dash/groups/{gid}/statuses").json()["results"][-1]["status"] == "succeeded"
+    assert "results" in client.get(f"/api/v1/root/dash/groups/{gid}/iterations").json()
+    for tab in ("experiments", "groups", "jobs", "builds", "pipelines"):
+        r = client.get(f"/api/v1/root/dash/{tab}")
+        assert r.status_code == 200 and "results" in r.json(), tab
+    pid = client.post("/api/v1/root/dash/pipelines", json={"content": {
+        "version": 1, "kind": "pipeline", "ops": [{"name": "a", "template": {"version": 1, "kind": "job",
+                                                                            "run": {"cmd": "true"}}}]}}).json()["id"]
+    import time as _t
+    end = _t.time() + 30
+    while _t.time() < end:
+        pl = client.get("/api/v1/root/dash/pipelines").json()["results"]
+        if pl and pl[0]["last_run_status"] in ("finished", "succeeded"):
+            break
+        _t.sleep(0.1)
+    assert pl[0]["id"] == pid and pl[0]["num_runs"] == 1 and pl[0]["last_run_status"] in ("finished", "succeeded")
+    d = client.get(f"/api/v1/root/dash/pipelines/{pid}").json()
+    run = client.get(f"/api/v1/root/dash/pipelines/{pid}/runs/{d['runs'][0]['id']}").json()
+    assert run["operations"][0]["name"] == "a"
+    assert "results" in client.get("/api/v1/activitylogs", params={"limit": 30}).json()
