@@ -11,8 +11,9 @@
 // sub-tile computed with v_mfma_f32_16x16x32_bf16; tiles are staged global -> LDS with 16-byte
 // global_load_lds (LDS image lane-linear, bank swizzle applied on the per-lane SOURCE address and on the
 // read, rule 21), double-buffered over BK = 64; blockIdx is remapped so blocks sharing an operand panel
-// run on one XCD (T1, bijective form).  Rows past the end of M read a zero page instead of being masked,
-// so partial tiles need no branches around the DMA.
+// run on one XCD (T1, bijective form).  The NT GEMM stages through buffer-resource LDS-DMA: rows past the end
+// of M and the taps of a convolution that fall outside the image get an out-of-range offset and read zeros, so
+// partial tiles and padding need no branches around the DMA; the TN GEMM reads a zero page instead.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -40,7 +41,38 @@ struct ConvGeom {
     int C, S, ntaps;
     int Hc, Wc, OS, oph, opw;  // output-row scatter (OS == 0: row m is output row m)
     signed char offh[9], offw[9], btap[9];
+    // per-tap byte offsets for the NT GEMM's staging (filled by finish_geom): A row shift (offh*W + offw)*C*2
+    // and B column start btap*C*2 -- dword arrays so a uniform tap index reads them with scalar loads
+    int tap_a[9], tap_b[9];
+    // x / Wr and q / Hr as __umulhi(x, m): m = floor(2^32 / d) + 1 is exact while x * d < 2^32, which holds for
+    // pixel indices (< 2^24) and row-grid sides (<= 255); m = 0 marks d == 1
+    uint32_t mWr, mHr;
+    // the taps factored into <= 3 distinct row offsets hv x <= 3 column offsets wv; pat[i * 3 + j] = bit set of
+    // the taps at (hv[i], wv[j]): a row's in-image tap mask is 6 compares and 9 selects (NT GEMM staging)
+    int nh, nw, hv[3], wv[3];
+    uint32_t pat[9];
 };
+
+inline uint32_t div_magic(int d) { return d <= 1 ? 0u : (uint32_t)((1ull << 32) / (unsigned)d + 1); }
+
+inline ConvGeom finish_geom(ConvGeom g) {
+    g.nh = g.nw = 0;
+    for (int i = 0; i < 9; ++i) g.pat[i] = 0;
+    for (int t = 0; t < 9; ++t) {
+        g.tap_a[t] = t < g.ntaps ? (g.offh[t] * g.W + g.offw[t]) * g.C * 2 : 0;
+        g.tap_b[t] = t < g.ntaps ? g.btap[t] * g.C * 2 : 0;
+        if (t >= g.ntaps) continue;
+        int i = 0, j = 0;
+        while (i < g.nh && g.hv[i] != g.offh[t]) ++i;
+        if (i == g.nh) g.hv[g.nh++] = g.offh[t];
+        while (j < g.nw && g.wv[j] != g.offw[t]) ++j;
+        if (j == g.nw) g.wv[g.nw++] = g.offw[t];
+        g.pat[i * 3 + j] |= 1u << t;
+    }
+    g.mWr = div_magic(g.Wr);
+    g.mHr = div_magic(g.Hr);
+    return g;
+}
 
 // BatchNorm-backward channel reduction fused into a data-gradient GEMM's epilogue.  The GEMM's output C is
 // dy of a BatchNorm(+ReLU) whose input x (same [rows][ldc] layout as C) and 1-bit ReLU mask the forward kept;
@@ -63,6 +95,14 @@ __device__ __forceinline__ void row_coords(int m, int Hr, int Wr, int& n, int& r
     r = q - n * Hr;
 }
 
+// row_coords with the host-computed magic divisors (ConvGeom::mWr / mHr): 2 multiply-highs instead of 2 divisions
+__device__ __forceinline__ void row_coords(int m, const ConvGeom& g, int& n, int& r, int& c) {
+    const int q = g.mWr ? (int)__umulhi((uint32_t)m, g.mWr) : m;
+    c = m - q * g.Wr;
+    n = g.mHr ? (int)__umulhi((uint32_t)q, g.mHr) : q;
+    r = q - n * g.Hr;
+}
+
 __device__ __forceinline__ size_t out_row(const ConvGeom& g, int m) {
     if (g.OS == 0) return (size_t)m;
     int n, r, c;
@@ -80,6 +120,19 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 __device__ __forceinline__ void glds16(const void* g, void* l) {
     __builtin_amdgcn_global_load_lds((gbl_void*)g, (lds_void*)l, 16, 0, 0);
+}
+
+// LDS-DMA through a buffer resource: base and range live in SGPRs, each lane supplies a 32-bit byte offset, and an
+// offset at or past the range (OOB) returns zeros -- the zero padding of a convolution costs one select, no
+// zero page and no 64-bit address math.  Operands here are < 2 GiB, so the range is 2^31 bytes.
+constexpr uint32_t OOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)OOB, 0x00020000);
+}
+
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t off, void* l) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)l, 16, off, 0, 0, 0);
 }
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
@@ -105,59 +158,72 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS-DMA destinations (M0) stay scalar
     const int ntn = N / BN, ntm = (M + BM - 1) / BM;
     const int id = xcd_remap(blockIdx.x, ntm * ntn);
     const int tn = id % ntn, tm = id / ntn;
     const int m0 = tm * BM, n0 = tn * BN;
     const int wm = wave / WGN, wn = wave % WGN;
 
-    // conv mode: image base and (r, c) of the A rows this thread stages, fixed over the whole k loop
-    int row_n[BM / 32], row_h[BM / 32], row_w[BM / 32];
-    if constexpr (CONV) {
+    // Staging addresses, fixed over the whole k loop: each A row this thread stages gets its element offset
+    // (with the lane's swizzled 16-B chunk folded in) and, in conv mode, a bit per tap saying whether that tap's
+    // source pixel is inside the image (else the zero page is read: the zero padding).  A stage then costs one
+    // bit test, one add and a select per row -- the per-stage bounds checks and 64-bit address math were ~20
+    // VALU per row and, beside 32 MFMAs per wave and stage, set the loop's pace.
+    int a_off[BM / 32];                                     // byte offsets
+    uint32_t a_ok[BM / 32];
 #pragma unroll
-        for (int i = 0; i < BM / 32; ++i) {
-            const int gm = m0 + (i * 4 + wave) * 8 + (lane >> 3);
+    for (int i = 0; i < BM / 32; ++i) {
+        const int row = (i * 4 + wave) * 8 + (lane >> 3);
+        const int lc = (lane & 7) ^ nt_swz(row);
+        const int gm = m0 + row;
+        if constexpr (CONV) {
             int n, r, c;
-            row_coords(gm, geo.Hr, geo.Wr, n, r, c);
-            row_n[i] = n * geo.H * geo.W;
-            row_h[i] = r * geo.S;
-            row_w[i] = c * geo.S;
+            row_coords(gm, geo, n, r, c);
+            const int ih0 = r * geo.S, iw0 = c * geo.S;
+            a_off[i] = (((n * geo.H + ih0) * geo.W + iw0) * lda + lc * 8) * 2;
+            uint32_t ok = 0;
+#pragma unroll
+            for (int hi = 0; hi < 3; ++hi) {
+                const bool vh = hi < geo.nh && (unsigned)(ih0 + geo.hv[hi]) < (unsigned)geo.H;
+#pragma unroll
+                for (int wj = 0; wj < 3; ++wj) {
+                    const bool vw = wj < geo.nw && (unsigned)(iw0 + geo.wv[wj]) < (unsigned)geo.W;
+                    ok |= (vh && vw) ? geo.pat[hi * 3 + wj] : 0u;
+                }
+            }
+            a_ok[i] = gm < M ? ok : 0u;
+        } else {
+            a_off[i] = (gm * lda + lc * 8) * 2;
+            a_ok[i] = gm < M ? 1u : 0u;
         }
     }
+    int b_off[BN / 32];
+#pragma unroll
+    for (int i = 0; i < BN / 32; ++i) {
+        const int row = (i * 4 + wave) * 8 + (lane >> 3);
+        b_off[i] = ((n0 + row) * ldb + ((lane & 7) ^ nt_swz(row)) * 8) * 2;
+    }
+    const __amdgpu_buffer_rsrc_t ra = buf_rsrc(A), rb = buf_rsrc(B);
 
-    // staging: each wave instruction moves 1024 B = 8 rows x 8 chunks; lane -> (row, physical chunk)
-    auto stage = [&](int buf, int k0) {
+    // staging: each wave instruction moves 1024 B = 8 rows x 8 chunks.  (t, c0): tap and channel offset of
+    // reduction index k0 = t * C + c0 (conv mode; t = 0, c0 = k0 otherwise)
+    auto stage = [&](int buf, int k0, int t, int c0) {
         char* base = smem + buf * STAGE;
-        int dh = 0, dw = 0, c0 = k0, bk0 = k0;
-        if constexpr (CONV) {
-            const int t = k0 / geo.C;
-            c0 = k0 - t * geo.C;
-            dh = geo.offh[t];
-            dw = geo.offw[t];
-            bk0 = geo.btap[t] * geo.C + c0;
+        int a_add = k0 * 2, bk0 = k0 * 2, bit = 0;
+        if constexpr (CONV) {                               // lda == C in conv mode
+            a_add = geo.tap_a[t] + c0 * 2;
+            bk0 = geo.tap_b[t] + c0 * 2;
+            bit = t;
         }
 #pragma unroll
         for (int i = 0; i < BM / 32; ++i) {                 // A: BM rows / 8 rows per instr / 4 waves
-            const int row = (i * 4 + wave) * 8 + (lane >> 3);
-            const int lc = (lane & 7) ^ nt_swz(row);
-            const int gm = m0 + row;
-            const __bf16* src;
-            if constexpr (CONV) {
-                const int ih = row_h[i] + dh, iw = row_w[i] + dw;
-                const bool ok = gm < M && (unsigned)ih < (unsigned)geo.H && (unsigned)iw < (unsigned)geo.W;
-                src = ok ? A + ((size_t)row_n[i] + ih * geo.W + iw) * lda + c0 + lc * 8 : zero;
-            } else {
-                src = gm < M ? A + (size_t)gm * lda + k0 + lc * 8 : zero;
-            }
-            glds16(src, base + (i * 4 + wave) * 1024);
+            const uint32_t off = (a_ok[i] >> bit) & 1u ? (uint32_t)(a_off[i] + a_add) : OOB;
+            blds16(ra, off, base + (i * 4 + wave) * 1024);
         }
 #pragma unroll
-        for (int i = 0; i < BN / 32; ++i) {
-            const int row = (i * 4 + wave) * 8 + (lane >> 3);
-            const int lc = (lane & 7) ^ nt_swz(row);
-            glds16(B + (size_t)(n0 + row) * ldb + bk0 + lc * 8, base + A_BYTES + (i * 4 + wave) * 1024);
-        }
+        for (int i = 0; i < BN / 32; ++i) blds16(rb, (uint32_t)(b_off[i] + bk0), base + A_BYTES + (i * 4 + wave) * 1024);
     };
 
     f32x4 acc[RN][RM];
@@ -167,13 +233,20 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         for (int b = 0; b < RM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int nk = K / BK;
-    stage(0, 0);
+    const int cdim = CONV ? geo.C : K;                      // channels per tap
+    stage(0, 0, 0, 0);
+    int st = 0, sc = BK;                                    // (tap, channel offset) of the next stage
+    if (sc == cdim) { sc = 0; ++st; }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const int fr = lane & 15, fq = lane >> 4;
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+        if (kt + 1 < nk) {
+            stage(cur ^ 1, (kt + 1) * BK, st, sc);
+            sc += BK;
+            if (sc == cdim) { sc = 0; ++st; }
+        }
         const char* As = smem + cur * STAGE;
         const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -215,6 +288,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     const int cc = tid % CHUNKS, r0 = tid / CHUNKS;
     const int ch0 = n0 + cc * 8;                            // this thread's 8 channels
     const bool bnr_on = bnr.part != nullptr;
+    const bool stats_on = stats != nullptr;
     size_t orow[ITERS];
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
@@ -229,6 +303,9 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         for (int it = 0; it < ITERS; ++it) dpre[it] = *(const uint4*)(D + orow[it] * ldd + ch0);
     }
     float sa[8], sb[8], mu[8], is[8];
+    float s1[8], s2[8];                                     // channel stats of this thread's rows (stats_on)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
     if (bnr_on) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) xpre[it] = *(const uint4*)(bnr.x + orow[it] * ldc + ch0);
@@ -265,6 +342,18 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         const int r = r0 + it * RSTEP;
         if (r >= rows) break;
         uint4 v = *(const uint4*)(smem + r * CROW + cc * 16);
+        if (stats_on) {
+            // sums / sums of squares of the bf16-rounded product (before any D), from the 8 channels in hand
+            const uint32_t* pv = (const uint32_t*)&v;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float lo = __uint_as_float(pv[j] << 16), hi = __uint_as_float(pv[j] & 0xffff0000u);
+                s1[2 * j] += lo;
+                s1[2 * j + 1] += hi;
+                s2[2 * j] = fmaf(lo, lo, s2[2 * j]);
+                s2[2 * j + 1] = fmaf(hi, hi, s2[2 * j + 1]);
+            }
+        }
         if (D != nullptr) {
             // C = A.B^T + D (a second gradient into the same tensor, e.g. the residual branch's): added in fp32
             // and rounded once, instead of a separate bf16 add pass over both tensors.  D is indexed like C, so
@@ -323,28 +412,33 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         }
         __syncthreads();                                    // red aliases the stats scratch below
     }
-    if (stats != nullptr) {
-        // per-channel partial sum / sum of squares of the bf16-rounded outputs over this block's rows:
-        // stats[0][tm][n] and stats[1][tm][n] (the BatchNorm that consumes this conv skips its stats pass)
-        constexpr int TPC = NTHREADS / BN;                  // threads per channel
-        const int c = tid % BN, part = tid / BN;
-        float s1 = 0.f, s2 = 0.f;
-        for (int r = part; r < rows; r += TPC) {
-            const float v = (float)*(const __bf16*)(smem + r * CROW + c * 2);
-            s1 += v;
-            s2 = fmaf(v, v, s2);
+    if (stats_on) {
+        // per-channel partial sum / sum of squares over this block's rows -> stats[0][tm][n], stats[1][tm][n]
+        // (the BatchNorm that consumes this conv skips its stats pass).  The threads sharing a chunk column
+        // (tid, tid + CHUNKS, ...) reduce through LDS past the staged tile, as the BatchNorm-backward partials do.
+        float* red = (float*)(smem + BM * CROW);            // [NTHREADS][16]
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            red[tid * 16 + k] = s1[k];
+            red[tid * 16 + 8 + k] = s2[k];
         }
-        float* red = (float*)(smem + BM * CROW);            // [2][NTHREADS]
-        red[tid] = s1;
-        red[NTHREADS + tid] = s2;
         __syncthreads();
-        if (part == 0) {
-            for (int j = 1; j < TPC; ++j) {
-                s1 += red[j * BN + c];
-                s2 += red[NTHREADS + j * BN + c];
+        if (tid < CHUNKS) {
+            for (int j = 1; j < NTHREADS / CHUNKS; ++j) {
+                const float* o = red + (j * CHUNKS + tid) * 16;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    s1[k] += o[k];
+                    s2[k] += o[8 + k];
+                }
             }
-            stats[(size_t)tm * N + n0 + c] = s1;
-            stats[(size_t)(ntm + tm) * N + n0 + c] = s2;
+            float* p1 = stats + (size_t)tm * N + ch0;
+            float* p2 = stats + (size_t)(ntm + tm) * N + ch0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                p1[k] = s1[k];
+                p2[k] = s2[k];
+            }
         }
     }
 }
@@ -372,11 +466,11 @@ __device__ __forceinline__ s16x4 tr_read(const char* img, int row, int col /* el
 }
 
 template <int ROWB, bool GATHER = false>
-__device__ __forceinline__ void stage_rows(char* img, const __bf16* __restrict__ G, int ld, int r0, int rend,
-                                           int c0, const __bf16* __restrict__ zero, int wave, int lane,
-                                           const ConvGeom* geo = nullptr, int dh = 0, int dw = 0) {
-    // BK rows x ROWB bytes, lane-linear image; 1024 B per wave instruction.  GATHER: row gr is the pixel
-    // shifted by (dh, dw) (zero page outside the image), for the weight gradient of a 3x3 convolution.
+__device__ __forceinline__ void stage_rows(char* img, __amdgpu_buffer_rsrc_t rsrc, int ld, int r0, int rend, int c0,
+                                           int wave, int lane, const ConvGeom* geo = nullptr, int dh = 0, int dw = 0) {
+    // BK rows x ROWB bytes, lane-linear image; 1024 B per wave instruction, through buffer-resource LDS-DMA (rows
+    // past rend and gathered pixels outside the image get an out-of-range offset: zeros).  GATHER: row gr is the
+    // pixel shifted by (dh, dw), for the weight gradient of a 3x3 convolution.
     constexpr int INSTR = BK * ROWB / 1024;
 #pragma unroll
     for (int i = 0; i < INSTR / 4; ++i) {
@@ -384,17 +478,17 @@ __device__ __forceinline__ void stage_rows(char* img, const __bf16* __restrict__
         const int row = off / ROWB, pc = (off % ROWB) >> 4;
         const int lc = pc ^ tr_swz<ROWB>(row);
         const int gr = r0 + row;
-        const __bf16* src;
+        uint32_t boff;
         if constexpr (GATHER) {
             int n, r, c;
-            row_coords(gr, geo->Hr, geo->Wr, n, r, c);
+            row_coords(gr, *geo, n, r, c);
             const int ih = r * geo->S + dh, iw = c * geo->S + dw;
             const bool ok = gr < rend && (unsigned)ih < (unsigned)geo->H && (unsigned)iw < (unsigned)geo->W;
-            src = ok ? G + (((size_t)n * geo->H + ih) * geo->W + iw) * ld + c0 + lc * 8 : zero;
+            boff = ok ? (uint32_t)(((((n * geo->H + ih) * geo->W + iw) * ld) + c0 + lc * 8) * 2) : OOB;
         } else {
-            src = gr < rend ? G + (size_t)gr * ld + c0 + lc * 8 : zero;
+            boff = gr < rend ? (uint32_t)((gr * ld + c0 + lc * 8) * 2) : OOB;
         }
-        glds16(src, img + (i * 4 + wave) * 1024);
+        blds16(rsrc, boff, img + (i * 4 + wave) * 1024);
     }
 }
 
@@ -408,7 +502,8 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
     constexpr int A_BYTES = BK * ROWA, STAGE = BK * (ROWA + ROWB_);
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: LDS-DMA destinations (M0) stay scalar
     const int nt1 = N1 / BN1, nt2 = N2 / BN2, ntiles = nt1 * nt2;
     const int nslices = (M + kchunk - 1) / kchunk;
     const int id = xcd_remap(blockIdx.x, ntiles * nslices);
@@ -433,10 +528,11 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
         dh = geo.offh[t];
         dw = geo.offw[t];
     }
+    const __amdgpu_buffer_rsrc_t ra = buf_rsrc(A), rb = buf_rsrc(B);
     auto stage = [&](int buf, int k0) {
         char* base = smem + buf * STAGE;
-        stage_rows<ROWA>(base, A, lda, k0, kend, n10, zero, wave, lane);
-        stage_rows<ROWB_, CONV>(base + A_BYTES, B, ldb, k0, kend, bc0, zero, wave, lane, &geo, dh, dw);
+        stage_rows<ROWA>(base, ra, lda, k0, kend, n10, wave, lane);
+        stage_rows<ROWB_, CONV>(base + A_BYTES, rb, ldb, k0, kend, bc0, wave, lane, &geo, dh, dw);
     };
     if (nk > 0) {
         stage(0, kbeg);
@@ -726,7 +822,7 @@ inline ConvGeom fwd_geom(int H, int W, int C, int K, int S) {
         g.offw[t] = (signed char)(t % K - K / 2);
         g.btap[t] = (signed char)t;
     }
-    return g;
+    return finish_geom(g);
 }
 
 template <int BM_, int BN_, int WGM_, int WGN_>
@@ -755,7 +851,7 @@ int for_each_dgrad_gemm(int Nb, int H, int W, int Cin, int Cout, int K, int S, F
             g.offh[t] = (signed char)(p - t / K);
             g.offw[t] = (signed char)(p - t % K);
         }
-        return f(g, Nb * H * W);
+        return f(finish_geom(g), Nb * H * W);
     }
     // stride 2: input pixel (ih, iw) = (2a + ph, 2b + pw) receives dy at ho = (ih + p - kh) / 2 for the taps kh
     // with (ih + p - kh) even; one GEMM per parity class, rows scattered back into dx.
@@ -778,7 +874,7 @@ int for_each_dgrad_gemm(int Nb, int H, int W, int Cin, int Cout, int K, int S, F
             }
             g.ntaps = nt;
             if (nt == 0 || g.Hr <= 0 || g.Wr <= 0) continue;
-            const int rc = f(g, Nb * g.Hr * g.Wr);
+            const int rc = f(finish_geom(g), Nb * g.Hr * g.Wr);
             if (rc) return rc;
         }
     return 0;
