@@ -158,9 +158,13 @@ class MetricStream:
         self._ring = None          # pinned fp32 [ring_floats]
         self._head = 0             # next free slot (monotonic; slot = head % ring_floats)
         self._tail = 0             # oldest slot still referenced by a pending row
+        # end of the newest row registered in _pending: slots past it may be reserved by a put() still enqueueing
+        # its copy, so an empty queue frees the ring only up to here (not up to _head)
+        self._committed = 0
         # (event|None, {name: float | (offset, numel)}, step, ts, end_offset)
         self._pending: List = []
         self._lock = threading.Lock()
+        self._flush_lock = threading.Lock()  # taking rows and writing them is one step: the sink sees FIFO order
         self._stop = threading.Event()
         self._side = None
         self._thread = threading.Thread(target=self._run, name="plx-metrics", daemon=True)
@@ -222,6 +226,8 @@ class MetricStream:
                 host[k] = float(v.item()) if hasattr(v, "item") else float(v)
         with self._lock:
             self._pending.append((event, host, step, ts, end))
+            if end is not None:
+                self._committed = max(self._committed, end)
 
     def _ready_rows(self, force: bool, oldest_only: bool = False):
         rows, keep = [], []
@@ -244,13 +250,14 @@ class MetricStream:
                     self._tail = end
             self._pending = keep
             if not keep:
-                self._tail = self._head
+                self._tail = max(self._tail, self._committed)
         return rows
 
     def flush(self, force: bool = True, oldest_only: bool = False) -> None:
-        rows = self._ready_rows(force, oldest_only)
-        if rows:
-            self.sink.log_metrics(self.xid, rows)
+        with self._flush_lock:
+            rows = self._ready_rows(force, oldest_only)
+            if rows:
+                self.sink.log_metrics(self.xid, rows)
 
     def _run(self) -> None:
         while not self._stop.wait(self.flush_every_s):

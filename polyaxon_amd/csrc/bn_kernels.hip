@@ -16,7 +16,8 @@
 //   plx_bn_fwd_apply     y = act(x*scale + bias [+ res])
 //   plx_bn_bwd_reduce    partial sums of dz and dz*xhat   (dz = dy * [y > 0] when act)
 //   plx_bn_bwd_finalize  dgamma, dbeta and the dx coefficients  dx = A*dz + B*x + D
-//   plx_bn_bwd_dx        dx (and d_residual = dz) in one pass
+//   plx_bn_bwd_dx        dx (and d_residual = dz) in one pass, optionally with the reduction partials of the
+//                        BatchNorm that produced the residual (ResBn: a downsampling branch's BN skips its reduce)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -315,21 +316,36 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   coef[2 * C + c] = -k1 * k2 + k1 * k3 * is * mean[c];  // D
 }
 
+// The BatchNorm that produced this one's residual input (a ResNet downsampling branch), when d_residual is that
+// BatchNorm's complete gradient: the dx pass also reduces its per-block partials  sum dz2  and
+// sum dz2 * (x2 - mean2) * invstd2  (dz2 = d_residual, masked by its own ReLU if it had one) into
+// part[2][gridDim.x][C], so that BatchNorm's backward skips its reduce pass (plx_bn_backward_from_partials).
+struct ResBn {
+  const bf16x8* x;
+  const uint8_t* mask;   // nullptr: no ReLU
+  const float* mean;
+  const float* invstd;
+  float* part;           // nullptr: disabled
+};
+
 __global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restrict__ x, const uint8_t* __restrict__ mask,
                                                            const bf16x8* __restrict__ dy, bf16x8* __restrict__ dx,
                                                            bf16x8* __restrict__ dres, const float* __restrict__ coef,
-                                                           int64_t n_vec, int G, int relu) {
+                                                           int64_t n_vec, int G, int relu, ResBn rb) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_vec) return;
-  const int cg = (int)(i % G);
+  const int cg = (int)(i % G);  // fixed over the grid stride (grid * 256 % G == 0)
   const int C = G * 8;
-  float A[8], B[8], D[8];
+  const bool rp = rb.part != nullptr;
+  float A[8], B[8], D[8], mu2[8], is2[8], ra[8], rc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     A[k] = coef[cg * 8 + k];
     B[k] = coef[C + cg * 8 + k];
     D[k] = coef[2 * C + cg * 8 + k];
+    ra[k] = rc[k] = 0.f;
+    mu2[k] = rp ? rb.mean[cg * 8 + k] : 0.f;
+    is2[k] = rp ? rb.invstd[cg * 8 + k] : 0.f;
   }
   for (; i < n_vec; i += stride) {
     float xv[8], g[8];
@@ -341,10 +357,47 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restr
       for (int k = 0; k < 8; ++k) g[k] = (mb >> k) & 1u ? g[k] : 0.f;
     }
     if (dres != nullptr) store8(dres + i, g);
+    if (rp) {
+      float x2[8];
+      load8(rb.x + i, x2);
+      const uint32_t m2 = rb.mask != nullptr ? rb.mask[i] : 0xffu;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float g2 = (m2 >> k) & 1u ? g[k] : 0.f;
+        ra[k] += g2;
+        rc[k] = fmaf(g2, (x2[k] - mu2[k]) * is2[k], rc[k]);
+      }
+    }
     float o[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = fmaf(A[k], g[k], fmaf(B[k], xv[k], D[k]));
     store8(dx + i, o);
+  }
+  if (!rp) return;
+  // threads tid, tid + G, ... of this block share channel group cg: sum them through LDS (G <= 256)
+  __shared__ float red[kBlock * 16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[threadIdx.x * 16 + k] = ra[k];
+    red[threadIdx.x * 16 + 8 + k] = rc[k];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < G) {
+    for (int j = 1; j < kBlock / G; ++j) {
+      const float* o = red + (j * G + threadIdx.x) * 16;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        ra[k] += o[k];
+        rc[k] += o[8 + k];
+      }
+    }
+    float* pa = rb.part + (int64_t)blockIdx.x * C + cg * 8;
+    float* pc = rb.part + ((int64_t)gridDim.x + blockIdx.x) * C + cg * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      pa[k] = ra[k];
+      pc[k] = rc[k];
+    }
   }
 }
 
@@ -453,12 +506,21 @@ PLX_API int plx_bn_apply(const void* x, const void* res, void* y, int64_t M, int
 }
 
 // mask: the ReLU bit mask written by the forward (required when relu); accumulate: dgamma/dbeta += (else =)
+// Row blocks of the dx pass = the nblk of the residual-BatchNorm partials it writes (ResBn, plx_bn_backward*).
+PLX_API int plx_bn_dx_blocks(int64_t M, int C) {
+  Plan p;
+  if (!plan_for(M, C, &p)) return -1;
+  return apply_grid(M * p.G, p.G);
+}
+
 PLX_API int plx_bn_backward(const void* x, const uint8_t* mask, const void* dy, void* dx, void* dres, int64_t M, int C,
                             const float* gamma, const float* save_mean, const float* save_invstd, float* dgamma,
                             float* dbeta, float* coef /* [3C] */, float* partials /* plx_bn_workspace floats */, int relu,
-                            int accumulate, hipStream_t stream) {
+                            int accumulate, const ResBn* resbn /* nullable, needs dres */, hipStream_t stream) {
   Plan p;
   if (!plan_for(M, C, &p) || M < 1 || (relu && mask == nullptr)) return 1;
+  if (resbn != nullptr && (dres == nullptr || resbn->part == nullptr)) return 1;
+  const ResBn rb = resbn != nullptr ? *resbn : ResBn{};
   float* pa = partials;
   float* pb = partials + (int64_t)p.nblk * C;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(p.nblk, p.gy), dim3(kBlock), 0, stream, (const bf16x8*)x,
@@ -471,7 +533,7 @@ PLX_API int plx_bn_backward(const void* x, const uint8_t* mask, const void* dy, 
                      gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
   const int64_t n_vec = M * p.G;
   hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     mask, (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, p.G, relu);
+                     mask, (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, p.G, relu, rb);
   return (int)hipGetLastError();
 }
 
@@ -482,9 +544,11 @@ PLX_API int plx_bn_backward_from_partials(const void* x, const uint8_t* mask, co
                                           int64_t M, int C, const float* gamma, const float* save_mean,
                                           const float* save_invstd, float* dgamma, float* dbeta, float* coef,
                                           const float* partials, int nblk, float* l2, int relu, int accumulate,
-                                          hipStream_t stream) {
+                                          const ResBn* resbn, hipStream_t stream) {
   Plan p;
   if (!plan_for(M, C, &p) || M < 1 || nblk < 1 || (relu && mask == nullptr)) return 1;
+  if (resbn != nullptr && (dres == nullptr || resbn->part == nullptr)) return 1;
+  const ResBn rb = resbn != nullptr ? *resbn : ResBn{};
   const int S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
   hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, S, 2), dim3(256), 0, stream, partials, nblk, C, l2,
                      S);
@@ -492,6 +556,6 @@ PLX_API int plx_bn_backward_from_partials(const void* x, const uint8_t* mask, co
                      M, gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
   const int64_t n_vec = M * p.G;
   hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     mask, (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, p.G, relu);
+                     mask, (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, p.G, relu, rb);
   return (int)hipGetLastError();
 }

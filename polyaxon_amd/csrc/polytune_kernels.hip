@@ -16,6 +16,10 @@
 //                       invalid / NaN entries sort last, ties keep the lower index first (stable, like
 //                       Python's sorted()).
 //   plx_early_stop_any  one wave64 per rule, ballot-OR over experiments, flag per rule.
+//   plx_philox_sample   random-search suggestions (reference search_managers/utils.py:41-64):
+//                       one thread per (suggestion, parameter) draws from a counter-based Philox4x32-10 stream,
+//                       so suggestion r of a seeded search is the same whatever n or the device; the numpy twin
+//                       in polytune/sampler.py reproduces it bit for bit on the host.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -100,6 +104,72 @@ __global__ void early_stop_any_kernel(const float* __restrict__ metrics, int E, 
   if (threadIdx.x == 0) flags[r] = sh;
 }
 
+// ---------------------------------------------------------------- Philox sampler
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// 53-bit uniform in [0, 1) from two words
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+  return (double)(((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// One hyper-parameter: kind 0 uniform(a, b), 1 normal(a, b) (log: exp of the draw; q > 0: round(x / q) * q),
+// 2 discrete index in [0, count), 3 categorical with probabilities (index into the cumulative table at cdf).
+struct ParamDesc {
+  int kind, log, count, cdf;
+  double a, b, q;
+};
+
+__global__ __launch_bounds__(256) void philox_sample_kernel(const ParamDesc* __restrict__ desc,
+                                                            const double* __restrict__ cdf, int P, int64_t n,
+                                                            int64_t row0, uint32_t k0, uint32_t k1,
+                                                            double* __restrict__ out) {
+  // no FMA contraction: the host twin (numpy) rounds every multiply and add separately, so the affine maps
+  // here must too for the two streams to agree bit for bit
+#pragma clang fp contract(off)
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * P) return;
+  const int64_t r = e / P;
+  const int p = (int)(e - r * P);
+  const int64_t row = row0 + r;
+  const U4 w = philox10(U4{(uint32_t)row, (uint32_t)(row >> 32), (uint32_t)p, 0x5a3e1e5u}, k0, k1);
+  const ParamDesc d = desc[p];
+  const double u = u53(w.x, w.y);
+  double v;
+  if (d.kind == 0) {
+    v = d.a + (d.b - d.a) * u;
+  } else if (d.kind == 1) {
+    const double u1 = 1.0 - u;  // (0, 1]
+    const double u2 = u53(w.z, w.w);
+    v = d.a + d.b * sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+  } else if (d.kind == 2) {
+    const int i = (int)(u * d.count);
+    v = (double)(i < d.count ? i : d.count - 1);
+  } else {
+    int i = 0;
+    while (i < d.count - 1 && cdf[d.cdf + i] <= u) ++i;
+    v = (double)i;
+  }
+  if (d.kind <= 1) {
+    if (d.log) v = exp(v);
+    if (d.q > 0.0) v = rint(v / d.q) * d.q;
+  }
+  out[e] = v;
+}
+
 }  // namespace
 
 PLX_API int plx_topk_brackets(const float* metrics, const int* counts, int n_brackets, int C, int ld, int maximize,
@@ -119,3 +189,17 @@ PLX_API int plx_early_stop_any(const float* metrics, int E, int M, const int* ru
                      rule_max, flags);
   return (int)hipGetLastError();
 }
+
+// out[n][P] (fp64, device) = rows row0 .. row0 + n - 1 of the seeded suggestion stream; desc: ParamDesc[P] and
+// cdf: the concatenated cumulative probability tables, both device memory.
+PLX_API int plx_philox_sample(const void* desc, const double* cdf, int P, long long n, long long row0,
+                              unsigned long long seed, double* out, hipStream_t stream) {
+  if (P <= 0 || n <= 0 || row0 < 0) return 1;
+  const int64_t total = (int64_t)n * P;
+  hipLaunchKernelGGL(philox_sample_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
+                     (const ParamDesc*)desc, cdf, P, (int64_t)n, (int64_t)row0, (uint32_t)seed, (uint32_t)(seed >> 32),
+                     out);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_philox_desc_size() { return (int)sizeof(ParamDesc); }

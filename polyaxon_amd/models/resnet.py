@@ -45,11 +45,12 @@ class Bottleneck(nn.Module):
             out = self.bn1(self.conv1(x, grad_box=box, bn_link=True))
             out = self.bn2(self.conv2(out, bn_link=True))
             return self.bn3(self.conv3(out, bn_link=True), x, residual_grad_box=box)
-        # downsampling block: conv1's data gradient is deferred into the downsample conv's dgrad epilogue
+        # downsampling block: conv1's data gradient is deferred into the downsample conv's dgrad epilogue, and the
+        # downsample BatchNorm's output feeds only bn3, so bn3's dx pass reduces that BatchNorm's backward partials
         identity = self.downsample(x, grad_box=box)
         out = self.bn1(self.conv1(x, grad_sink=box))
         out = self.bn2(self.conv2(out, bn_link=True))
-        return self.bn3(self.conv3(out, bn_link=True), identity)
+        return self.bn3(self.conv3(out, bn_link=True), identity, residual_link=True)
 
 
 class Downsample(nn.Module):

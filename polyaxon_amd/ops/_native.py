@@ -161,9 +161,9 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_bn_l2_workspace": [_I, _I],
         "plx_bn_forward_from_partials": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P, _P,
                                          _I, _P],
-        "plx_bn_backward": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P],
-        "plx_bn_backward_from_partials": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I,
-                                          _P],
+        "plx_bn_backward": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P],
+        "plx_bn_dx_blocks": [_L, _I],
+        "plx_bn_backward_from_partials": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I, _P, _P],
     },
     "plx_procmon": {
         "plx_pm_create": [],
@@ -235,6 +235,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
     },
     "plx_polytune": {
         "plx_topk_brackets": [_P, _P, _I, _I, _I, _I, _P, _P],
+        "plx_philox_sample": [_P, _P, _I, _L, _L, ctypes.c_uint64, _P, _P],
+        "plx_philox_desc_size": [],
         "plx_early_stop_any": [_P, _I, _I, _P, _P, _P, _I, _P, _P],
     },
 }
@@ -249,6 +251,12 @@ def _declare(name: str, handle: ctypes.CDLL) -> None:
         f = getattr(handle, fn)
         f.argtypes = argtypes
         f.restype = RESTYPES.get(fn, _I)
+
+
+class ResBnArgs(ctypes.Structure):
+    """Host image of ``ResBn`` (csrc/bn_kernels.hip): the residual BatchNorm whose reduction partials the dx pass
+    of the BatchNorm consuming its output also produces."""
+    _fields_ = [("x", _P), ("mask", _P), ("mean", _P), ("invstd", _P), ("part", _P)]
 
 
 class BnBwdArgs(ctypes.Structure):

@@ -7,6 +7,8 @@ With ReLU the forward also writes a 1-bit-per-element mask (1/16 of ``y``); the 
 """
 from __future__ import annotations
 
+import ctypes
+
 from typing import Optional
 
 import torch
@@ -35,7 +37,7 @@ def supported(x: torch.Tensor) -> bool:
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, ext=None, box=None,
-                link=None):
+                link=None, rlink=None):
         lib = _native.lib("plx_bn")
         x = _cl(x)
         n, c, h, w = x.shape
@@ -82,6 +84,10 @@ class _BNAct(torch.autograd.Function):
         ctx.link = link
         if link is not None:
             link.x, link.mask, link.mean, link.invstd = x, mask, stats[:c], stats[c:2 * c]
+        # rlink: the residual came from a fused BatchNorm whose output nothing else consumes (a downsampling branch):
+        # d_residual is that BatchNorm's whole gradient, so the dx pass below reduces its backward partials too
+        ctx.rlink = rlink if (rlink is not None and residual is not None and rlink.x is not None
+                              and rlink.x.shape == x.shape and ctx.box is None) else None
         return y
 
     @staticmethod
@@ -104,13 +110,22 @@ class _BNAct(torch.autograd.Function):
             dg_ptr, db_ptr, acc = dgb.data_ptr(), dgb[c:].data_ptr(), 0
         coef = torch.empty(3 * c, **f32)
         part, nblk = ctx.link.take() if ctx.link is not None else (None, 0)
+        rb = None
+        if ctx.rlink is not None and dres is not None:
+            rl = ctx.rlink
+            nblk2 = int(lib.plx_bn_dx_blocks(m, c))
+            rl.part = torch.empty(2 * nblk2 * c, **f32)
+            rl.nblk = nblk2
+            rb = _native.ResBnArgs(rl.x.data_ptr(), rl.mask.data_ptr() if rl.mask is not None else None,
+                                   rl.mean.data_ptr(), rl.invstd.data_ptr(), rl.part.data_ptr())
+        rbp = ctypes.addressof(rb) if rb is not None else None
         if part is not None:  # the consumer's dgrad epilogue already reduced dz and dz*xhat per block
             l2 = torch.empty(int(lib.plx_bn_l2_workspace(nblk, c)), **f32)
             rc = lib.plx_bn_backward_from_partials(
                 x.data_ptr(), mask.data_ptr() if mask is not None else None, dy.data_ptr(), dx.data_ptr(),
                 dres.data_ptr() if dres is not None else None, m, c, weight.data_ptr(), stats.data_ptr(),
                 stats[c:].data_ptr(), dg_ptr, db_ptr, coef.data_ptr(), part.data_ptr(), nblk, l2.data_ptr(),
-                int(ctx.relu), acc, _stream())
+                int(ctx.relu), acc, rbp, _stream())
             _native.check(rc, "plx_bn_backward_from_partials")
         else:
             partials = torch.empty(ctx.ws, **f32)
@@ -118,27 +133,31 @@ class _BNAct(torch.autograd.Function):
                 x.data_ptr(), mask.data_ptr() if mask is not None else None, dy.data_ptr(), dx.data_ptr(),
                 dres.data_ptr() if dres is not None else None, m, c, weight.data_ptr(), stats.data_ptr(),
                 stats[c:].data_ptr(), dg_ptr, db_ptr, coef.data_ptr(), partials.data_ptr(), int(ctx.relu), acc,
-                _stream())
+                rbp, _stream())
             _native.check(rc, "plx_bn_backward")
         if ctx.box is not None:  # the residual's gradient rides into conv1's dgrad epilogue (ops.conv1x1)
             ctx.box.put(dres)
             dres = None
         dgamma = dgb[:c] if dgb is not None else None
         dbeta = dgb[c:] if dgb is not None else None
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None
 
 
 def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
            running_var: Optional[torch.Tensor], training: bool, momentum: float, eps: float,
-           residual: Optional[torch.Tensor], act: bool, ext_stats=None, residual_grad_box=None) -> torch.Tensor:
+           residual: Optional[torch.Tensor], act: bool, ext_stats=None, residual_grad_box=None,
+           residual_link: bool = False) -> torch.Tensor:
     """``ext_stats`` = (fp32 [2][nblk][C] channel sums / sums of squares of ``x``, nblk) from the op that
-    produced ``x`` (the 1x1-conv GEMM epilogue); training mode then skips the stats pass."""
+    produced ``x`` (the 1x1-conv GEMM epilogue); training mode then skips the stats pass.  ``residual_link``:
+    ``residual`` is the output of a fused BatchNorm that nothing else consumes; its backward partials are then
+    reduced by this op's dx pass."""
     if residual is not None and residual.dtype != x.dtype:
         residual = residual.to(x.dtype)
     if training:
         link = BnLink()
+        rlink = getattr(residual, "_plx_bn_link", None) if (residual_link and residual is not None) else None
         y = _BNAct.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, act, ext_stats,
-                         residual_grad_box, link)
+                         residual_grad_box, link, rlink)
         y._plx_bn_link = link
         return y
     # inference: fold running stats into scale/bias, one apply pass

@@ -49,7 +49,8 @@ class BatchNormAct(nn.Module):
             self.running_mean.zero_()
             self.running_var.fill_(1.0)
 
-    def forward(self, x: torch.Tensor, identity: Optional[torch.Tensor] = None, residual_grad_box=None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, identity: Optional[torch.Tensor] = None, residual_grad_box=None,
+                residual_link: bool = False) -> torch.Tensor:
         if self.residual and identity is None:
             raise ValueError("BatchNormAct(residual=True) needs the identity tensor")
         if self.fused and x.is_cuda:
@@ -58,7 +59,7 @@ class BatchNormAct(nn.Module):
                 ext = getattr(x, "_plx_channel_stats", None)  # set by ops.conv1x1 on its output
                 return bn_fused.bn_act(x, self.weight, self.bias, self.running_mean, self.running_var,
                                        self.training, self.momentum, self.eps, identity, self.act, ext,
-                                       residual_grad_box)
+                                       residual_grad_box, residual_link)
         if x.is_cuda and torch.is_autocast_enabled("cuda"):
             # keep BN math in the activation dtype like the fused kernel (fp32 stats inside)
             pass

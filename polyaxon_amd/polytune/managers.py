@@ -53,6 +53,10 @@ class RandomSearchManager(BaseSearchAlgorithmManager):
 
     def get_suggestions(self, iteration_config=None):
         cfg = self.hptuning_config
+        if cfg.random_search.sampler == "device":
+            from polyaxon_amd.polytune.sampler import philox_random_suggestions
+
+            return philox_random_suggestions(cfg.matrix, cfg.random_search.n_experiments, seed=cfg.seed)
         return get_random_suggestions(cfg.matrix, cfg.random_search.n_experiments, seed=cfg.seed)
 
 

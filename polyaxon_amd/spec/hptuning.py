@@ -107,15 +107,24 @@ class GridSearchConfig:
 @dataclass
 class RandomSearchConfig:
     n_experiments: int
+    # "numpy": the reference's sequential RandomState stream (default, parity); "device": the counter-based
+    # Philox stream of polytune/sampler.py (one kernel launch for any n, same suggestions on any device)
+    sampler: str = "numpy"
 
     @classmethod
     def from_dict(cls, d):
         if not d or not d.get("n_experiments"):
             raise MatrixValidationError("random_search requires `n_experiments`")
-        return cls(n_experiments=int(d["n_experiments"]))
+        sampler = str(d.get("sampler", "numpy"))
+        if sampler not in ("numpy", "device"):
+            raise MatrixValidationError("random_search.sampler must be `numpy` or `device`")
+        return cls(n_experiments=int(d["n_experiments"]), sampler=sampler)
 
     def to_dict(self):
-        return {"n_experiments": self.n_experiments}
+        out = {"n_experiments": self.n_experiments}
+        if self.sampler != "numpy":
+            out["sampler"] = self.sampler
+        return out
 
 
 @dataclass

@@ -168,13 +168,13 @@ def main() -> None:
             bwd = lambda: bn.plx_bn_backward_from_partials(  # noqa
                 x.data_ptr(), mp, dy.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else None, m, c,
                 weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), dg.data_ptr(), db.data_ptr(), coef.data_ptr(),
-                part.data_ptr(), nblk, l2.data_ptr(), int(relu), 1, st)
+                part.data_ptr(), nblk, l2.data_ptr(), int(relu), 1, None, st)
         else:
             pw = torch.empty(int(bn.plx_bn_workspace(m, c)), **f32)
             bwd = lambda: bn.plx_bn_backward(  # noqa
                 x.data_ptr(), mp, dy.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else None, m, c,
                 weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), dg.data_ptr(), db.data_ptr(), coef.data_ptr(),
-                pw.data_ptr(), int(relu), 1, st)
+                pw.data_ptr(), int(relu), 1, None, st)
         nbytes = 2.0 * m * c * (3 + (1 if res else 0)) + (m * c / 8 if relu else 0)
         emit(name, "bn_bwd" + ("" if partials_bwd else "+reduce"), count, timeit(bwd), nbytes, 0.0)
 

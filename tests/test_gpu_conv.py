@@ -283,7 +283,8 @@ def test_direct_flat_grads_match_autograd(cuda):
 
 def test_downsample_mailbox_matches_autograd_sum(cuda):
     """Downsampling block: conv1's dgrad deferred into the (strided) downsample conv's dgrad epilogue equals
-    autograd summing the two branch gradients."""
+    autograd summing the two branch gradients, and the downsample BatchNorm's backward fed by the partials that
+    bn3's dx pass reduces (ResBn) gives the same gamma / beta / conv-weight gradients as its own reduce pass."""
     from polyaxon_amd.models.resnet import Bottleneck, Downsample
 
     for stride, cin in ((2, 256), (1, 64)):
@@ -302,6 +303,9 @@ def test_downsample_mailbox_matches_autograd_sum(cuda):
                 out = blk.bn3(blk.conv3(o), identity)
             torch.manual_seed(9)
             out.backward(torch.randn_like(out.float()).to(torch.bfloat16))
-            outs.append(xa.grad.float())
+            outs.append([xa.grad.float(), ds.bn.weight.grad.float().clone(), ds.bn.bias.grad.float().clone(),
+                         ds.conv.weight.grad.float().clone()])
             blk.zero_grad(set_to_none=True)
-        torch.testing.assert_close(outs[0], outs[1], rtol=2e-2, atol=2e-2 * float(outs[1].abs().max()))
+        for got, ref in zip(outs[0], outs[1]):
+            torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
+        assert float(outs[0][1].abs().sum()) > 0 and float(outs[0][2].abs().sum()) > 0
