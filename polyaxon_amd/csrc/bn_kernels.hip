@@ -328,15 +328,19 @@ struct ResBn {
   float* part;           // nullptr: disabled
 };
 
+// RP: also reduce the residual BatchNorm's partials (ResBn).  A separate instantiation: its extra state
+// (90 VGPRs) would cut the plain pass from 8 to 5 waves per SIMD, and this memory-bound pass needs them.
+template <bool RP>
 __global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restrict__ x, const uint8_t* __restrict__ mask,
                                                            const bf16x8* __restrict__ dy, bf16x8* __restrict__ dx,
                                                            bf16x8* __restrict__ dres, const float* __restrict__ coef,
                                                            int64_t n_vec, int G, int relu, ResBn rb) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (!RP && i >= n_vec) return;
   const int cg = (int)(i % G);  // fixed over the grid stride (grid * 256 % G == 0)
   const int C = G * 8;
-  const bool rp = rb.part != nullptr;
+  constexpr bool rp = RP;
   float A[8], B[8], D[8], mu2[8], is2[8], ra[8], rc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -357,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restr
       for (int k = 0; k < 8; ++k) g[k] = (mb >> k) & 1u ? g[k] : 0.f;
     }
     if (dres != nullptr) store8(dres + i, g);
-    if (rp) {
+    if constexpr (rp) {
       float x2[8];
       load8(rb.x + i, x2);
       const uint32_t m2 = rb.mask != nullptr ? rb.mask[i] : 0xffu;
@@ -373,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restr
     for (int k = 0; k < 8; ++k) o[k] = fmaf(A[k], g[k], fmaf(B[k], xv[k], D[k]));
     store8(dx + i, o);
   }
-  if (!rp) return;
+  if constexpr (rp) {
   // threads tid, tid + G, ... of this block share channel group cg: sum them through LDS (G <= 256)
   __shared__ float red[kBlock * 16];
 #pragma unroll
@@ -398,6 +402,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restr
       pa[k] = ra[k];
       pc[k] = rc[k];
     }
+  }
   }
 }
 
@@ -434,6 +439,17 @@ inline int apply_grid(int64_t n_vec, int G) {
   const int64_t mult = G > kBlock ? G / kBlock : 1;
   g = (g + mult - 1) / mult * mult;
   return (int)g;
+}
+
+inline void launch_dx(hipStream_t stream, int64_t n_vec, int G, const void* x, const uint8_t* mask, const void* dy,
+                      void* dx, void* dres, const float* coef, int relu, const ResBn& rb) {
+  const dim3 grid(apply_grid(n_vec, G));
+  if (rb.part != nullptr)
+    hipLaunchKernelGGL(bn_bwd_dx_kernel<true>, grid, dim3(kBlock), 0, stream, (const bf16x8*)x, mask,
+                       (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, G, relu, rb);
+  else
+    hipLaunchKernelGGL(bn_bwd_dx_kernel<false>, grid, dim3(kBlock), 0, stream, (const bf16x8*)x, mask,
+                       (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, G, relu, rb);
 }
 
 }  // namespace
@@ -532,8 +548,7 @@ PLX_API int plx_bn_backward(const void* x, const uint8_t* mask, const void* dy, 
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)p.S * C, p.S, C, M,
                      gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
   const int64_t n_vec = M * p.G;
-  hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     mask, (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, p.G, relu, rb);
+  launch_dx(stream, n_vec, p.G, x, mask, dy, dx, dres, coef, relu, rb);
   return (int)hipGetLastError();
 }
 
@@ -555,7 +570,6 @@ PLX_API int plx_bn_backward_from_partials(const void* x, const uint8_t* mask, co
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S, C,
                      M, gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
   const int64_t n_vec = M * p.G;
-  hipLaunchKernelGGL(bn_bwd_dx_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     mask, (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, p.G, relu, rb);
+  launch_dx(stream, n_vec, p.G, x, mask, dy, dx, dres, coef, relu, rb);
   return (int)hipGetLastError();
 }

@@ -384,63 +384,34 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
             }
         }
     }
-    if (bnr_on) {
-        // threads tid, tid + CHUNKS, ... share a chunk column: sum them through LDS past the staged tile
-        float* red = (float*)(smem + BM * CROW);            // [NTHREADS][16]
+    // Per-channel partials of this block's rows: the RSTEP threads sharing a chunk column each hold 16 values
+    // (8 channels x 2 sums).  They go through LDS past the staged tile (rows of 17 floats: conflict-free both
+    // ways) and every thread then sums ONE (chunk column, value) pair over the RSTEP rows -- 16 loads per thread
+    // instead of 16 threads each walking 15 x 16 dependent loads while the rest of the block waits.
+    auto reduce_store = [&](const float* va, const float* vb, float* dst_a, float* dst_b) {
+        float* red = (float*)(smem + BM * CROW);            // [NTHREADS][17]
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            red[tid * 16 + k] = sa[k];
-            red[tid * 16 + 8 + k] = sb[k];
+            red[tid * 17 + k] = va[k];
+            red[tid * 17 + 8 + k] = vb[k];
         }
         __syncthreads();
-        if (tid < CHUNKS) {
-            for (int j = 1; j < NTHREADS / CHUNKS; ++j) {
-                const float* o = red + (j * CHUNKS + tid) * 16;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    sa[k] += o[k];
-                    sb[k] += o[8 + k];
-                }
-            }
-            float* pa = bnr.part + (size_t)(bnr.blk_off + tm) * ldc + ch0;
-            float* pb = bnr.part + (size_t)(bnr.part_ld + bnr.blk_off + tm) * ldc + ch0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                pa[k] = sa[k];
-                pb[k] = sb[k];
-            }
+        if (tid < CHUNKS * 16) {
+            const int c = tid % CHUNKS, v = tid / CHUNKS;
+            float sum = 0.f;
+#pragma unroll 4
+            for (int j = 0; j < RSTEP; ++j) sum += red[(j * CHUNKS + c) * 17 + v];
+            if (v < 8) dst_a[c * 8 + v] = sum;
+            else dst_b[c * 8 + v - 8] = sum;
         }
-        __syncthreads();                                    // red aliases the stats scratch below
-    }
-    if (stats_on) {
-        // per-channel partial sum / sum of squares over this block's rows -> stats[0][tm][n], stats[1][tm][n]
-        // (the BatchNorm that consumes this conv skips its stats pass).  The threads sharing a chunk column
-        // (tid, tid + CHUNKS, ...) reduce through LDS past the staged tile, as the BatchNorm-backward partials do.
-        float* red = (float*)(smem + BM * CROW);            // [NTHREADS][16]
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            red[tid * 16 + k] = s1[k];
-            red[tid * 16 + 8 + k] = s2[k];
-        }
-        __syncthreads();
-        if (tid < CHUNKS) {
-            for (int j = 1; j < NTHREADS / CHUNKS; ++j) {
-                const float* o = red + (j * CHUNKS + tid) * 16;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    s1[k] += o[k];
-                    s2[k] += o[8 + k];
-                }
-            }
-            float* p1 = stats + (size_t)tm * N + ch0;
-            float* p2 = stats + (size_t)(ntm + tm) * N + ch0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                p1[k] = s1[k];
-                p2[k] = s2[k];
-            }
-        }
-    }
+        __syncthreads();                                    // red is reused by the next reduction
+    };
+    if (bnr_on)
+        reduce_store(sa, sb, bnr.part + (size_t)(bnr.blk_off + tm) * ldc + n0,
+                     bnr.part + (size_t)(bnr.part_ld + bnr.blk_off + tm) * ldc + n0);
+    // per-channel partial sum / sum of squares -> stats[0][tm][n], stats[1][tm][n] (the BatchNorm that consumes
+    // this conv skips its stats pass)
+    if (stats_on) reduce_store(s1, s2, stats + (size_t)tm * N + n0, stats + (size_t)(ntm + tm) * N + n0);
 }
 
 // ------------------------------------------------------------------------------------------- TN GEMM
@@ -652,7 +623,7 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
               const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}, const void* D = nullptr,
               int ldd = 0, BnBwd bnr = {}) {
     constexpr int LDS = 2 * (BM + BN) * BK * 2;
-    static_assert(BM * (BN * 2 + 16) + NTHREADS * 16 * 4 <= LDS, "epilogue staging must fit the k-loop LDS");
+    static_assert(BM * (BN * 2 + 16) + NTHREADS * 17 * 4 <= LDS, "epilogue staging must fit the k-loop LDS");
     auto k = gemm_nt_kernel<BM, BN, WGM, WGN, CONV>;
     static int attr = set_lds(k, LDS);
     if (attr) return attr;
