@@ -78,7 +78,7 @@ def _avg_worker(rank, world, port, q):
     tokens = torch.randint(0, 256, (4, 16), generator=torch.Generator().manual_seed(100 + rank))
     lm_loss(model(tokens), tokens).backward()
     ddp.finish()
-    q.put((rank, flat.grads.clone()))
+    q.put((rank, flat.grads.numpy().copy()))  # by value: a shared-memory tensor dies with its exiting producer
     dist.destroy_process_group()
 
 
@@ -106,7 +106,7 @@ def test_ddp_matches_single_process_average():
     ref = flat.grads.clone()
     assert float(ref.norm()) > 0
     for r in (0, 1):
-        torch.testing.assert_close(got[r], ref, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(torch.from_numpy(got[r]), ref, rtol=1e-4, atol=1e-6)
 
 
 def _lp_worker(rank, world, port, q):
