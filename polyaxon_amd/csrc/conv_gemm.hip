@@ -148,8 +148,8 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 // 16 rows of a fragment read on 16 distinct bank slots.
 __device__ __forceinline__ int nt_swz(int row) { return (row >> 1) & 7; }
 
-template <int BM, int BN, int WGM, int WGN, bool CONV>
-__global__ void __launch_bounds__(NTHREADS, 2)
+template <int BM, int BN, int WGM, int WGN, bool CONV, int MINB = 2>
+__global__ void __launch_bounds__(NTHREADS, MINB)
 gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
                int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
                float* __restrict__ stats, ConvGeom geo, const __bf16* __restrict__ D, int ldd, BnBwd bnr) {
@@ -289,18 +289,18 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     const int ch0 = n0 + cc * 8;                            // this thread's 8 channels
     const bool bnr_on = bnr.part != nullptr;
     const bool stats_on = stats != nullptr;
-    size_t orow[ITERS];
+    int orow[ITERS];                                        // output pixel rows (< 2^31)
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
         const int gm = min(m0 + r0 + it * RSTEP, M - 1);
-        if constexpr (CONV) orow[it] = out_row(geo, gm);
-        else orow[it] = (size_t)gm;
+        if constexpr (CONV) orow[it] = (int)out_row(geo, gm);
+        else orow[it] = gm;
     }
     uint4 dpre[ITERS], xpre[ITERS];
     uint32_t mpre[ITERS];
     if (D != nullptr) {
 #pragma unroll
-        for (int it = 0; it < ITERS; ++it) dpre[it] = *(const uint4*)(D + orow[it] * ldd + ch0);
+        for (int it = 0; it < ITERS; ++it) dpre[it] = *(const uint4*)(D + (size_t)orow[it] * ldd + ch0);
     }
     float sa[8], sb[8], mu[8], is[8];
     float s1[8], s2[8];                                     // channel stats of this thread's rows (stats_on)
@@ -308,10 +308,10 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
     if (bnr_on) {
 #pragma unroll
-        for (int it = 0; it < ITERS; ++it) xpre[it] = *(const uint4*)(bnr.x + orow[it] * ldc + ch0);
+        for (int it = 0; it < ITERS; ++it) xpre[it] = *(const uint4*)(bnr.x + (size_t)orow[it] * ldc + ch0);
         if (bnr.mask != nullptr) {
 #pragma unroll
-            for (int it = 0; it < ITERS; ++it) mpre[it] = bnr.mask[(orow[it] * ldc + ch0) >> 3];
+            for (int it = 0; it < ITERS; ++it) mpre[it] = bnr.mask[((size_t)orow[it] * ldc + ch0) >> 3];
         } else {
 #pragma unroll
             for (int it = 0; it < ITERS; ++it) mpre[it] = 0xffu;
@@ -367,7 +367,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                 pv[j] = pack_bf16x2(lo, hi);
             }
         }
-        *(uint4*)(C + orow[it] * ldc + ch0) = v;
+        *(uint4*)(C + (size_t)orow[it] * ldc + ch0) = v;
         if (bnr_on) {
             const uint32_t mb = mpre[it];
             const uint32_t* pv = (const uint32_t*)&v;
@@ -618,13 +618,18 @@ int set_lds(KernelT k, int bytes) {
                                                                                                                  : -2;
 }
 
-template <int BM, int BN, int WGM, int WGN, bool CONV = false>
+// NBUF = 1: a single K stage (K == BK, the skinny 1x1 GEMMs): LDS = max(stage, epilogue) and 3 blocks per CU
+template <int BM, int BN, int WGM, int WGN, bool CONV = false, int NBUF = 2>
 int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
               const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}, const void* D = nullptr,
               int ldd = 0, BnBwd bnr = {}) {
-    constexpr int LDS = 2 * (BM + BN) * BK * 2;
-    static_assert(BM * (BN * 2 + 16) + NTHREADS * 17 * 4 <= LDS, "epilogue staging must fit the k-loop LDS");
-    auto k = gemm_nt_kernel<BM, BN, WGM, WGN, CONV>;
+    constexpr int EPI = BM * (BN * 2 + 16) + NTHREADS * 17 * 4;
+    constexpr int KLOOP = NBUF * (BM + BN) * BK * 2;
+    constexpr int LDS = KLOOP > EPI ? KLOOP : EPI;
+    static_assert(NBUF == 2 || NBUF == 1, "one or two K stages");
+    static_assert(NBUF == 1 || EPI <= KLOOP, "epilogue staging must fit the k-loop LDS");
+    if (NBUF == 1 && K != BK) return -1;
+    auto k = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, NBUF == 1 ? 3 : 2>;
     static int attr = set_lds(k, LDS);
     if (attr) return attr;
     const int nwg = ((M + BM - 1) / BM) * (N / BN);
@@ -632,6 +637,8 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
                        K, lda, ldb, ldc, (const __bf16*)zero, stats, geo, (const __bf16*)D, ldd, bnr);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+bool g_nt_single_stage = true;
 
 // m-slicing of the weight-gradient GEMM
 struct TnPlan { int kchunk, slices, groups, per_group, blocks; };
@@ -702,10 +709,15 @@ int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int 
     if (bnr != nullptr && (ldc != N || bnr->part == nullptr)) return -1;
     const BnBwd b = bnr != nullptr ? *bnr : BnBwd{};
     hipStream_t s = (hipStream_t)stream;
+    const bool one = K == BK && g_nt_single_stage;
     if (N % 128 == 0)
-        return launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b);
+        return one ? launch_nt<128, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b)
+                   : launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b);
     return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b);
 }
+
+// A/B knob: single-stage (3 blocks per CU) instantiation for K == 64
+void plx_set_nt_single_stage(int on) { g_nt_single_stage = on != 0; }
 
 // weight-gradient slicing knobs; workspace sizes follow them, so set before sizing / launching
 void plx_set_tn_plan(int blocks_per_cu, int slab_mb) {

@@ -192,6 +192,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gemm_nt_rows_per_block": [_I],
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
         "plx_set_tn_plan": [_I, _I],
+        "plx_set_nt_single_stage": [_I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
         "plx_weight_prepk": [_P, _L, _L, _L, _L, _P, _P, _I, _I, _I, _P],

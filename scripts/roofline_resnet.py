@@ -30,6 +30,7 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--md", default="")
     ap.add_argument("--only", default="", help="comma-separated substrings: time only matching layers")
+    ap.add_argument("--nt-single-stage", type=int, default=1, help="A/B knob: 3-blocks/CU NT GEMM for K == 64")
     a = ap.parse_args()
     import torch
 
@@ -40,6 +41,7 @@ def main() -> None:
     conv = _native.lib("plx_conv")
     bn = _native.lib("plx_bn")
     cus = _num_cus(dev)
+    conv.plx_set_nt_single_stage(a.nt_single_stage)
     zero = _zero_page(dev).data_ptr()
     st = torch.cuda.current_stream().cuda_stream
     bf = dict(dtype=torch.bfloat16, device=dev)
