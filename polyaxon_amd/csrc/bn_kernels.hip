@@ -195,16 +195,21 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const bf16x8* __restrict__ x, const bf16x8* __restrict__ res,
                                                           bf16x8* __restrict__ y, const float* __restrict__ scale,
                                                           const float* __restrict__ bias, int64_t n_vec, int G,
-                                                          int relu, uint8_t* __restrict__ mask) {
+                                                          int relu, uint8_t* __restrict__ mask,
+                                                          const float* __restrict__ rsb) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // multiple of G (G | 256 or G % 256 == 0 handled by host)
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_vec) return;
   const int cg = (int)(i % G);
-  float a[8], b[8];
+  float a[8], b[8], ra[8], rb[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     a[k] = scale[cg * 8 + k];
     b[k] = bias[cg * 8 + k];
+    // rsb: the residual is the raw input of a BatchNorm (no activation) whose apply pass is deferred to here:
+    // res' = res * rsb[c] + rsb[C + c]  (a ResNet downsampling branch feeds only this add)
+    ra[k] = rsb != nullptr ? rsb[cg * 8 + k] : 1.f;
+    rb[k] = rsb != nullptr ? rsb[G * 8 + cg * 8 + k] : 0.f;
   }
   for (; i < n_vec; i += stride) {
     float v[8];
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const bf16x8* __restri
       float r[8];
       load8(res + i, r);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] += r[k];
+      for (int k = 0; k < 8; ++k) v[k] += fmaf(r[k], ra[k], rb[k]);
     }
     if (relu) {
 #pragma unroll
@@ -465,7 +470,8 @@ PLX_API int plx_bn_forward(const void* x, const void* res, void* y, int64_t M, i
                            const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                            float* save_mean, float* save_invstd, float* scale_bias /* [2C] */,
                            float* partials /* plx_bn_workspace floats */, uint8_t* mask /* M*C/8 bytes or null */,
-                           int relu, hipStream_t stream) {
+                           int relu, const float* res_sb /* nullable [2C], see bn_apply_kernel */,
+                           hipStream_t stream) {
   Plan p;
   if (!plan_for(M, C, &p) || M < 1) return 1;
   float* psum = partials;
@@ -479,8 +485,10 @@ PLX_API int plx_bn_forward(const void* x, const void* res, void* y, int64_t M, i
                      (const uint16_t*)x, C, M, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
                      save_invstd, scale_bias, scale_bias + C);
   const int64_t n_vec = M * p.G;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu, relu ? mask : nullptr);
+  if (y != nullptr)  // y == nullptr: statistics and scale/bias only (the apply is deferred to the consumer)
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
+                       (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu,
+                       relu ? mask : nullptr, res_sb);
   return (int)hipGetLastError();
 }
 
@@ -496,7 +504,8 @@ PLX_API int plx_bn_forward_from_partials(const void* x, const void* res, void* y
                                          const float* gamma, const float* beta, float eps, float momentum,
                                          float* running_mean, float* running_var, float* save_mean,
                                          float* save_invstd, float* scale_bias, const float* partials, int nblk,
-                                         float* l2, uint8_t* mask, int relu, hipStream_t stream) {
+                                         float* l2, uint8_t* mask, int relu, const float* res_sb,
+                                         hipStream_t stream) {
   Plan p;
   if (!plan_for(M, C, &p) || M < 1 || nblk < 1) return 1;
   const int S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
@@ -506,8 +515,10 @@ PLX_API int plx_bn_forward_from_partials(const void* x, const void* res, void* y
                      (const uint16_t*)nullptr, C, M, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
                      save_invstd, scale_bias, scale_bias + C);
   const int64_t n_vec = M * p.G;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu, relu ? mask : nullptr);
+  if (y != nullptr)
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
+                       (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu,
+                       relu ? mask : nullptr, res_sb);
   return (int)hipGetLastError();
 }
 
@@ -517,7 +528,7 @@ PLX_API int plx_bn_apply(const void* x, const void* res, void* y, int64_t M, int
   if (!plan_for(M, C, &p)) return 1;
   const int64_t n_vec = M * p.G;
   hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu, nullptr);
+                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu, nullptr, nullptr);
   return (int)hipGetLastError();
 }
 

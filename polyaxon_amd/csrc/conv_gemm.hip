@@ -152,7 +152,8 @@ template <int BM, int BN, int WGM, int WGN, bool CONV, int MINB = 2>
 __global__ void __launch_bounds__(NTHREADS, MINB)
 gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
                int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
-               float* __restrict__ stats, ConvGeom geo, const __bf16* __restrict__ D, int ldd, BnBwd bnr) {
+               float* __restrict__ stats, ConvGeom geo, const __bf16* __restrict__ D, int ldd, BnBwd bnr,
+               const uint8_t* __restrict__ dmask) {
     constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
     constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -297,10 +298,17 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         else orow[it] = gm;
     }
     uint4 dpre[ITERS], xpre[ITERS];
-    uint32_t mpre[ITERS];
+    uint32_t mpre[ITERS], dmpre[ITERS];
     if (D != nullptr) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) dpre[it] = *(const uint4*)(D + (size_t)orow[it] * ldd + ch0);
+        // dmask: D is a ReLU's incoming gradient and this bit mask (1 bit per element, ldd == N) its forward
+        // mask -- the residual gradient dz = D * mask is formed here instead of being written out by the ReLU's
+        // backward and read back
+        if (dmask != nullptr) {
+#pragma unroll
+            for (int it = 0; it < ITERS; ++it) dmpre[it] = dmask[((size_t)orow[it] * ldd + ch0) >> 3];
+        }
     }
     float sa[8], sb[8], mu[8], is[8];
     float s1[8], s2[8];                                     // channel stats of this thread's rows (stats_on)
@@ -360,10 +368,13 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
             // D == C (in place) is allowed.
             uint32_t* pv = (uint32_t*)&v;
             const uint32_t* pd = (const uint32_t*)&dpre[it];
+            const uint32_t db = dmask != nullptr ? dmpre[it] : 0xffu;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const float lo = __uint_as_float(pv[j] << 16) + __uint_as_float(pd[j] << 16);
-                const float hi = __uint_as_float(pv[j] & 0xffff0000u) + __uint_as_float(pd[j] & 0xffff0000u);
+                const float d0 = (db >> (2 * j)) & 1u ? __uint_as_float(pd[j] << 16) : 0.f;
+                const float d1 = (db >> (2 * j + 1)) & 1u ? __uint_as_float(pd[j] & 0xffff0000u) : 0.f;
+                const float lo = __uint_as_float(pv[j] << 16) + d0;
+                const float hi = __uint_as_float(pv[j] & 0xffff0000u) + d1;
                 pv[j] = pack_bf16x2(lo, hi);
             }
         }
@@ -622,7 +633,7 @@ int set_lds(KernelT k, int bytes) {
 template <int BM, int BN, int WGM, int WGN, bool CONV = false, int NBUF = 2>
 int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
               const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}, const void* D = nullptr,
-              int ldd = 0, BnBwd bnr = {}) {
+              int ldd = 0, BnBwd bnr = {}, const uint8_t* dmask = nullptr) {
     constexpr int EPI = BM * (BN * 2 + 16) + NTHREADS * 17 * 4;
     constexpr int KLOOP = NBUF * (BM + BN) * BK * 2;
     constexpr int LDS = KLOOP > EPI ? KLOOP : EPI;
@@ -634,7 +645,7 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
     if (attr) return attr;
     const int nwg = ((M + BM - 1) / BM) * (N / BN);
     hipLaunchKernelGGL(k, dim3(nwg), dim3(NTHREADS), LDS, s, (const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N,
-                       K, lda, ldb, ldc, (const __bf16*)zero, stats, geo, (const __bf16*)D, ldd, bnr);
+                       K, lda, ldb, ldc, (const __bf16*)zero, stats, geo, (const __bf16*)D, ldd, bnr, dmask);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -703,17 +714,21 @@ int plx_gemm_nt_rows_per_block(int N) { return N % 128 == 0 ? 128 : 256; }
 // stats (nullable): fp32 [2][ceil(M / rows_per_block)][N] per-block channel sums / sums of squares of C
 // D (nullable, bf16 [M][N], ldd): added to the product (C = A.B^T + D); not reflected in stats
 // bnr (nullable host struct): fused BatchNorm-backward partials of C (see BnBwd; needs ldc == N)
+// dmask (nullable, needs D and ldd == N): D is added where its bit is set (D * ReLU mask, 1 bit per element)
 int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                const void* zero, float* stats, const void* D, int ldd, const BnBwd* bnr, void* stream) {
+                const void* zero, float* stats, const void* D, int ldd, const uint8_t* dmask, const BnBwd* bnr,
+                void* stream) {
     if (M <= 0 || N % 64 || K % BK || lda % 8 || ldb % 8 || ldc % 8 || (D != nullptr && ldd % 8)) return -1;
+    if (dmask != nullptr && (D == nullptr || ldd != N)) return -1;
     if (bnr != nullptr && (ldc != N || bnr->part == nullptr)) return -1;
     const BnBwd b = bnr != nullptr ? *bnr : BnBwd{};
     hipStream_t s = (hipStream_t)stream;
     const bool one = K == BK && g_nt_single_stage;
     if (N % 128 == 0)
-        return one ? launch_nt<128, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b)
-                   : launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b);
-    return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b);
+        return one ? launch_nt<128, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b,
+                                                         dmask)
+                   : launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
+    return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
 }
 
 // A/B knob: single-stage (3 blocks per CU) instantiation for K == 64

@@ -8,6 +8,7 @@ map onto MFMA, bf16 autocast compute, fp32 master weights living in one flat buf
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Type
 
 import torch
@@ -53,6 +54,9 @@ class Bottleneck(nn.Module):
         return self.bn3(self.conv3(out, bn_link=True), identity, residual_link=True)
 
 
+_DEFER_DOWN_BN = os.environ.get("PLX_DEFER_DOWN_BN", "1") != "0"  # A/B knob (scripts/ab_check.sh)
+
+
 class Downsample(nn.Module):
     def __init__(self, in_ch: int, out_ch: int, stride: int, fused: bool = True, native_conv: bool = True):
         super().__init__()
@@ -61,7 +65,8 @@ class Downsample(nn.Module):
         self.bn = BatchNormAct(out_ch, act=False, fused=fused)
 
     def forward(self, x: torch.Tensor, grad_box: Optional[GradMailbox] = None) -> torch.Tensor:
-        return self.bn(self.conv(x, grad_box=grad_box))
+        # the output feeds only bn3's residual add, which applies this BatchNorm's scale/bias itself
+        return self.bn(self.conv(x, grad_box=grad_box), defer_apply=_DEFER_DOWN_BN)
 
 
 class ResNet(nn.Module):

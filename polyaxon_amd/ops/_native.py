@@ -130,6 +130,8 @@ def lib(name: str) -> ctypes.CDLL:
             build(name, force=os.environ.get("PLX_NATIVE_REBUILD") == "1")
         handle = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
         _declare(name, handle)
+        if name == "plx_conv" and os.environ.get("PLX_NT_SINGLE_STAGE") == "0":  # A/B knob
+            handle.plx_set_nt_single_stage(0)
         _loaded[name] = handle
         return handle
 
@@ -156,11 +158,11 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
     },
     "plx_bn": {
         "plx_bn_workspace": [_L, _I],
-        "plx_bn_forward": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _P],
+        "plx_bn_forward": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
         "plx_bn_apply": [_P, _P, _P, _L, _I, _P, _I, _P],
         "plx_bn_l2_workspace": [_I, _I],
         "plx_bn_forward_from_partials": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P, _P,
-                                         _I, _P],
+                                         _I, _P, _P],
         "plx_bn_backward": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P],
         "plx_bn_dx_blocks": [_L, _I],
         "plx_bn_backward_from_partials": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I, _P, _P],
@@ -188,7 +190,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
                           _P],
     },
     "plx_conv": {
-        "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P],
+        "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P],
         "plx_gemm_nt_rows_per_block": [_I],
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
         "plx_set_tn_plan": [_I, _I],

@@ -8,6 +8,7 @@ With ReLU the forward also writes a 1-bit-per-element mask (1/16 of ``y``); the 
 from __future__ import annotations
 
 import ctypes
+import os
 
 from typing import Optional
 
@@ -16,6 +17,9 @@ import torch
 from polyaxon_amd.ops import _native
 from polyaxon_amd.ops.conv1x1 import BnLink
 from polyaxon_amd.ops.flat import direct_grad
+
+
+_MASKED_RESGRAD = os.environ.get("PLX_MASKED_RESGRAD", "1") != "0"  # A/B knob (scripts/ab_check.sh)
 
 
 def _stream() -> int:
@@ -37,7 +41,7 @@ def supported(x: torch.Tensor) -> bool:
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, ext=None, box=None,
-                link=None, rlink=None):
+                link=None, rlink=None, defer=False):
         lib = _native.lib("plx_bn")
         x = _cl(x)
         n, c, h, w = x.shape
@@ -46,9 +50,19 @@ class _BNAct(torch.autograd.Function):
         if ws < 0:
             raise RuntimeError("unsupported channel count for fused BN")
         f32 = dict(dtype=torch.float32, device=x.device)
-        y = torch.empty_like(x, memory_format=torch.channels_last)
+        # defer: no apply pass -- the output aliases x and its only consumer (the residual add of a fused
+        # BatchNorm) applies scale/bias on the fly (link.affine); the backward is unchanged
+        defer = bool(defer) and not relu and residual is None and link is not None
+        y = None if defer else torch.empty_like(x, memory_format=torch.channels_last)
+        yp = y.data_ptr() if y is not None else None
         stats = torch.empty(4 * c, **f32)  # mean | invstd | scale | bias
+        res_sb = None
+        if residual is not None:
+            rl = getattr(residual, "_plx_bn_link", None)
+            if rl is not None and rl.affine is not None and getattr(residual, "_plx_deferred", False):
+                res_sb = rl.affine
         res = _cl(residual) if residual is not None else None
+        rsp = res_sb.data_ptr() if res_sb is not None else None
         rm = running_mean.data_ptr() if running_mean is not None else None
         rv = running_var.data_ptr() if running_var is not None else None
         mask = torch.empty(m * c // 8, dtype=torch.uint8, device=x.device) if relu else None
@@ -58,17 +72,17 @@ class _BNAct(torch.autograd.Function):
             part, nblk = ext
             l2 = torch.empty(int(lib.plx_bn_l2_workspace(nblk, c)), **f32)
             rc = lib.plx_bn_forward_from_partials(
-                x.data_ptr(), res.data_ptr() if res is not None else None, y.data_ptr(), m, c, weight.data_ptr(),
+                x.data_ptr(), res.data_ptr() if res is not None else None, yp, m, c, weight.data_ptr(),
                 bias.data_ptr(), float(eps), float(momentum), rm, rv, stats.data_ptr(), stats[c:].data_ptr(),
-                stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(), mp, int(relu), _stream())
+                stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(), mp, int(relu), rsp, _stream())
             _native.check(rc, "plx_bn_forward_from_partials")
         else:
             partials = torch.empty(ws, **f32)
             rc = lib.plx_bn_forward(
-                x.data_ptr(), res.data_ptr() if res is not None else None, y.data_ptr(), m, c,
+                x.data_ptr(), res.data_ptr() if res is not None else None, yp, m, c,
                 weight.data_ptr(), bias.data_ptr(), float(eps), float(momentum), rm, rv,
                 stats.data_ptr(), stats[c:].data_ptr(), stats[2 * c:].data_ptr(), partials.data_ptr(), mp, int(relu),
-                _stream())
+                rsp, _stream())
             _native.check(rc, "plx_bn_forward")
         ctx.save_for_backward(x, mask, weight, stats)
         ctx.relu = relu
@@ -84,10 +98,14 @@ class _BNAct(torch.autograd.Function):
         ctx.link = link
         if link is not None:
             link.x, link.mask, link.mean, link.invstd = x, mask, stats[:c], stats[c:2 * c]
+            if defer:
+                link.affine = stats[2 * c:]
         # rlink: the residual came from a fused BatchNorm whose output nothing else consumes (a downsampling branch):
         # d_residual is that BatchNorm's whole gradient, so the dx pass below reduces its backward partials too
         ctx.rlink = rlink if (rlink is not None and residual is not None and rlink.x is not None
                               and rlink.x.shape == x.shape and ctx.box is None) else None
+        if defer:
+            return x.view_as(x)  # the raw input; bn_act marks it _plx_deferred
         return y
 
     @staticmethod
@@ -101,7 +119,11 @@ class _BNAct(torch.autograd.Function):
             dy = dy.to(torch.bfloat16)
         f32 = dict(dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        # identity block: the residual's gradient dz = dy * mask is not written here; dy and the mask ride into
+        # conv1's dgrad epilogue (GradMailbox.put_masked), which adds them
+        masked_box = _MASKED_RESGRAD and ctx.box is not None and ctx.relu and mask is not None
+        dres = (torch.empty_like(x, memory_format=torch.channels_last)
+                if ctx.has_res and not masked_box else None)
         if ctx.direct is not None:
             dg_ptr, db_ptr, acc = ctx.direct[0].data_ptr(), ctx.direct[1].data_ptr(), 1
             dgb = None
@@ -136,30 +158,62 @@ class _BNAct(torch.autograd.Function):
                 rbp, _stream())
             _native.check(rc, "plx_bn_backward")
         if ctx.box is not None:  # the residual's gradient rides into conv1's dgrad epilogue (ops.conv1x1)
-            ctx.box.put(dres)
+            if masked_box:
+                ctx.box.put_masked(dy, mask)
+            else:
+                ctx.box.put(dres)
             dres = None
         dgamma = dgb[:c] if dgb is not None else None
         dbeta = dgb[c:] if dgb is not None else None
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None
+
+
+class _Materialize(torch.autograd.Function):
+    """A deferred BatchNorm output (the raw input plus its pending scale/bias) made real for a consumer that does
+    not apply the affine itself; the gradient passes through unchanged (it is the BatchNorm output's gradient)."""
+
+    @staticmethod
+    def forward(ctx, t, sb):
+        c = t.shape[1]
+        return (t.float() * sb[:c].view(1, c, 1, 1) + sb[c:].view(1, c, 1, 1)).to(t.dtype).contiguous(
+            memory_format=torch.channels_last)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+def materialize(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """The real value of a possibly deferred BatchNorm output (:func:`bn_act` with ``defer_apply``)."""
+    if t is None or not getattr(t, "_plx_deferred", False):
+        return t
+    return _Materialize.apply(t, t._plx_bn_link.affine)
 
 
 def bn_act(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, running_mean: Optional[torch.Tensor],
            running_var: Optional[torch.Tensor], training: bool, momentum: float, eps: float,
            residual: Optional[torch.Tensor], act: bool, ext_stats=None, residual_grad_box=None,
-           residual_link: bool = False) -> torch.Tensor:
+           residual_link: bool = False, defer_apply: bool = False) -> torch.Tensor:
     """``ext_stats`` = (fp32 [2][nblk][C] channel sums / sums of squares of ``x``, nblk) from the op that
     produced ``x`` (the 1x1-conv GEMM epilogue); training mode then skips the stats pass.  ``residual_link``:
     ``residual`` is the output of a fused BatchNorm that nothing else consumes; its backward partials are then
-    reduced by this op's dx pass."""
+    reduced by this op's dx pass.  ``defer_apply`` (training, no activation, no residual): skip the apply pass
+    and return ``x`` itself marked ``_plx_deferred``; the fused BatchNorm that takes it as its residual applies
+    the scale/bias while adding (a ResNet downsampling branch: ~0.3 ms of a bs-256 step), any other consumer
+    must call :func:`materialize` first."""
     if residual is not None and residual.dtype != x.dtype:
         residual = residual.to(x.dtype)
     if training:
         link = BnLink()
         rlink = getattr(residual, "_plx_bn_link", None) if (residual_link and residual is not None) else None
+        defer = bool(defer_apply) and not act and residual is None
         y = _BNAct.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, act, ext_stats,
-                         residual_grad_box, link, rlink)
+                         residual_grad_box, link, rlink, defer)
         y._plx_bn_link = link
+        if defer:
+            y._plx_deferred = True
         return y
+    residual = materialize(residual)
     # inference: fold running stats into scale/bias, one apply pass
     lib = _native.lib("plx_bn")
     x = _cl(x)

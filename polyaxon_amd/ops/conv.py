@@ -23,7 +23,8 @@ import torch.nn.functional as F
 import ctypes
 
 from polyaxon_amd.ops import _native, side_stream
-from polyaxon_amd.ops.conv1x1 import GradMailbox, _bf16_context, _num_cus, _stream, _zero_page, bn_link_of, nt_stats_rows
+from polyaxon_amd.ops.conv1x1 import (GradMailbox, _bf16_context, _num_cus, _stream, _zero_page, bn_link_of, nt_stats_rows,
+                                      unpack_relu_mask)
 from polyaxon_amd.ops.flat import direct_grad
 
 
@@ -78,7 +79,9 @@ class _ConvK(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         zero = _zero_page(x.device).data_ptr()
         dx = dw = None
-        extra = ctx.box.take() if ctx.box is not None else None
+        extra, extra_mask = ctx.box.take() if ctx.box is not None else (None, None)
+        if extra is not None and extra_mask is not None:
+            extra = unpack_relu_mask(extra, extra_mask)
         if ctx.needs_input_grad[0]:
             add = None
             if extra is not None:

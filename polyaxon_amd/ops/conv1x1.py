@@ -53,11 +53,12 @@ def nt_stats_rows(n: int) -> int:
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, stats: torch.Tensor = None,
-            add: torch.Tensor = None, bnr: "_native.BnBwdArgs" = None) -> torch.Tensor:
+            add: torch.Tensor = None, bnr: "_native.BnBwdArgs" = None, add_mask: torch.Tensor = None) -> torch.Tensor:
     """out[M][N] = a[M][K] · b[N][K]ᵀ, bf16 (rows may be strided, K contiguous).  ``stats`` (fp32
     [2][ceil(M / nt_stats_rows(N))][N]) receives per-block channel sums and sums of squares of ``out``;
-    ``add`` (bf16 [M][N]) is summed into the product in the epilogue; ``bnr`` (from :meth:`BnLink.request`)
-    makes the epilogue emit the BatchNorm-backward partials of ``out``."""
+    ``add`` (bf16 [M][N]) is summed into the product in the epilogue, only where ``add_mask`` (a ReLU's 1-bit
+    forward mask, uint8 [M*N/8]) is set when given; ``bnr`` (from :meth:`BnLink.request`) makes the epilogue
+    emit the BatchNorm-backward partials of ``out``."""
     m, k = a.shape
     n = b.shape[0]
     if out is None:
@@ -69,11 +70,14 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, stats: t
         assert stats.dtype == torch.float32 and stats.is_contiguous() and stats.numel() >= 2 * nblk * n
     if add is not None:
         assert add.shape == (m, n) and add.stride(1) == 1 and add.dtype == torch.bfloat16 and add.data_ptr() % 16 == 0
+    if add_mask is not None:
+        assert add is not None and add.stride(0) == n and add_mask.dtype == torch.uint8 and add_mask.numel() == m * n // 8
     rc = _native.lib("plx_conv").plx_gemm_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0),
                                              b.stride(0), out.stride(0), _zero_page(a.device).data_ptr(),
                                              stats.data_ptr() if stats is not None else None,
                                              add.data_ptr() if add is not None else None,
                                              add.stride(0) if add is not None else 0,
+                                             add_mask.data_ptr() if add_mask is not None else None,
                                              ctypes.addressof(bnr) if bnr is not None else None, _stream())
     _native.check(rc, "plx_gemm_nt")
     return out
@@ -124,21 +128,46 @@ class GradMailbox:
     autograd sequence number first) runs the producer's backward before the consumer's; ``take`` fails loudly
     if that ever does not hold instead of silently dropping a gradient."""
 
-    __slots__ = ("armed", "grad", "expect")
+    __slots__ = ("armed", "grad", "mask", "expect")
 
     def __init__(self):
         self.armed = False
         self.grad = None
+        self.mask = None
         self.expect = False
 
     def put(self, g: torch.Tensor) -> None:
-        self.grad = g if self.grad is None else self.grad + g
+        if self.grad is not None:
+            g = self._dense() + g
+        self.grad, self.mask = g, None
+
+    def put_masked(self, g: torch.Tensor, mask: torch.Tensor) -> None:
+        """The gradient is ``g`` where the 1-bit ReLU ``mask`` (uint8, bit k of byte i = element 8i+k of the NHWC
+        rows) is set, else 0: bn3's backward hands over its incoming gradient and forward mask instead of writing
+        d_residual, and the consumer's dgrad epilogue applies the mask (``gemm_nt(add_mask=...)``)."""
+        if self.grad is not None:
+            self.put(unpack_relu_mask(g, mask))
+            return
+        self.grad, self.mask = g, mask
+
+    def _dense(self) -> torch.Tensor:
+        return self.grad if self.mask is None else unpack_relu_mask(self.grad, self.mask)
 
     def take(self):
-        g, self.grad = self.grad, None
+        """(gradient, mask or None)."""
+        g, m = self.grad, self.mask
+        self.grad = self.mask = None
         if g is None and self.expect:
             raise RuntimeError("GradMailbox: the deferred gradient did not arrive before its consumer's backward")
-        return g
+        return g, m
+
+
+def unpack_relu_mask(g: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+    """g * mask with the 1-bit mask expanded (channels_last NHWC element order)."""
+    bits = (mask.view(-1, 1) >> torch.arange(8, device=mask.device, dtype=torch.uint8)) & 1
+    n, c, h, w = g.shape
+    keep = bits.view(n, h, w, c).permute(0, 3, 1, 2).to(g.dtype)
+    return (g * keep).contiguous(memory_format=torch.channels_last)
 
 
 class BnLink:
@@ -149,10 +178,11 @@ class BnLink:
     (``bn_link=True``) ``request``s a partials buffer and its dgrad GEMM epilogue writes the per-block
     Σdz and Σdz·x̂ (csrc/conv_gemm.hip ``BnBwd``); the BatchNorm backward then skips its reduce pass."""
 
-    __slots__ = ("x", "mask", "mean", "invstd", "part", "nblk", "_args")
+    __slots__ = ("x", "mask", "mean", "invstd", "part", "nblk", "_args", "affine")
 
     def __init__(self, x=None, mask=None, mean=None, invstd=None):
         self.x, self.mask, self.mean, self.invstd = x, mask, mean, invstd
+        self.affine = None  # deferred apply: fp32 [scale | bias] the consumer applies to the raw x
         self.part = None
         self.nblk = 0
         self._args = None
@@ -208,17 +238,21 @@ class _Conv1x1(torch.autograd.Function):
         n, cin, h, w = x.shape
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         dx = dw = None
-        extra = ctx.box.take() if ctx.box is not None else None
+        extra, extra_mask = ctx.box.take() if ctx.box is not None else (None, None)
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            if extra is not None:
+            if extra is not None and (extra.dtype != torch.bfloat16
+                                      or not extra.is_contiguous(memory_format=torch.channels_last)):
+                if extra_mask is not None:
+                    extra, extra_mask = unpack_relu_mask(extra, extra_mask), None
                 extra = extra.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
             bnr = None
             # the link is only served when dx (+ the box's gradient) is the whole gradient of x: with a box, the
             # producer must actually have deferred into it; a sink means dx is only part of it
             if ctx.link is not None and ctx.sink is None and (ctx.box is None or extra is not None):
                 bnr = ctx.link.request(-(-(n * h * w) // nt_stats_rows(cin)))
-            gemm_nt(_rows(dy), wt, _rows(dx), add=_rows(extra) if extra is not None else None, bnr=bnr)
+            gemm_nt(_rows(dy), wt, _rows(dx), add=_rows(extra) if extra is not None else None, bnr=bnr,
+                    add_mask=extra_mask)
             if ctx.sink is not None:  # the downsample conv's dgrad adds this gradient in its epilogue
                 ctx.sink.put(dx)
                 dx = None

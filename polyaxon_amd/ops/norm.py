@@ -50,7 +50,9 @@ class BatchNormAct(nn.Module):
             self.running_var.fill_(1.0)
 
     def forward(self, x: torch.Tensor, identity: Optional[torch.Tensor] = None, residual_grad_box=None,
-                residual_link: bool = False) -> torch.Tensor:
+                residual_link: bool = False, defer_apply: bool = False) -> torch.Tensor:
+        """``defer_apply``: the caller guarantees the output feeds only the residual add of another
+        BatchNormAct (see ``ops.bn_fused.bn_act``)."""
         if self.residual and identity is None:
             raise ValueError("BatchNormAct(residual=True) needs the identity tensor")
         if self.fused and x.is_cuda:
@@ -59,10 +61,10 @@ class BatchNormAct(nn.Module):
                 ext = getattr(x, "_plx_channel_stats", None)  # set by ops.conv1x1 on its output
                 return bn_fused.bn_act(x, self.weight, self.bias, self.running_mean, self.running_var,
                                        self.training, self.momentum, self.eps, identity, self.act, ext,
-                                       residual_grad_box, residual_link)
-        if x.is_cuda and torch.is_autocast_enabled("cuda"):
-            # keep BN math in the activation dtype like the fused kernel (fp32 stats inside)
-            pass
+                                       residual_grad_box, residual_link, defer_apply)
+        if identity is not None and identity.is_cuda:
+            from polyaxon_amd.ops.bn_fused import materialize
+            identity = materialize(identity)
         return bn_act_reference(x, self.weight, self.bias, self.running_mean, self.running_var,
                                 self.training, self.momentum, self.eps, identity, self.act)
 

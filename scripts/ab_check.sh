@@ -5,8 +5,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp PYTHONPATH=.
 mkdir -p gpurun_out/ab
-STEPS=${STEPS:-13}
-WARM=${WARM:-2}
+STEPS=${STEPS:-2}
+WARM=${WARM:-1}
 timeout -k 10 300 python -c "from polyaxon_amd.ops import _native; _native.build_all()" > gpurun_out/ab/build.log 2>&1 || { echo build failed; tail gpurun_out/ab/build.log; exit 1; }
 if [ -n "${TESTS:-}" ]; then
   timeout -k 10 600 python -m pytest $TESTS -x -q > gpurun_out/ab/tests.log 2>&1; rc=$?
@@ -23,7 +23,8 @@ for round in 1 2; do
   i=0
   for v in "${VS[@]}"; do
     i=$((i+1))
-    timeout -k 10 600 python bench.py --steps $STEPS --warmup $WARM $v > gpurun_out/ab/b_${round}_${i}.json 2> gpurun_out/ab/b_${round}_${i}.err; rc=$?
+    # a variant is bench flags and/or leading NAME=VALUE environment settings (A/B knobs)
+    timeout -k 10 600 env $v python bench.py --steps $STEPS --warmup $WARM > gpurun_out/ab/b_${round}_${i}.json 2> gpurun_out/ab/b_${round}_${i}.err; rc=$?
     if [ $rc -ne 0 ]; then echo "bench [$v] failed rc=$rc"; tail -5 gpurun_out/ab/b_${round}_${i}.err; exit $rc; fi
     python - "$v" gpurun_out/ab/b_${round}_${i}.json <<'PY'
 import json, sys

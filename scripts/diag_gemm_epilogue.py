@@ -54,7 +54,7 @@ def main() -> None:
         def run(stats_on=False, add=False, bn=False):
             return lambda: conv.plx_gemm_nt(a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, k, k, n, zero,
                                             stats.data_ptr() if stats_on else None, d.data_ptr() if add else None,
-                                            n if add else 0, ctypes.addressof(bnr) if bn else None, st)
+                                            n if add else 0, None, ctypes.addressof(bnr) if bn else None, st)
         plain = timeit(run())
         rec = {"M": m, "N": n, "K": k, "plain_us": plain, "stats_us": timeit(run(stats_on=True)),
                "add_us": timeit(run(add=True)), "bnr_us": timeit(run(bn=True)),

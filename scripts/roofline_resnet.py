@@ -101,7 +101,7 @@ def main() -> None:
         wt = rnd((cin, k * k * cout))
         if gemm:
             fwd = lambda: conv.plx_gemm_nt(x.data_ptr(), wb.data_ptr(), y.data_ptr(), m_out, cout, cin, cin, cin,  # noqa
-                                           cout, zero, stats.data_ptr(), None, 0, None, st)
+                                           cout, zero, stats.data_ptr(), None, 0, None, None, st)
         else:
             fwd = lambda: conv.plx_conv_fwd(x.data_ptr(), wb.data_ptr(), y.data_ptr(), nb, h, w, cin, cout, k, s,  # noqa
                                             zero, stats.data_ptr(), st)
@@ -109,8 +109,12 @@ def main() -> None:
         # data gradient
         extra = 0.0
         add = rnd((m_in, cin)) if "add" in dgrad_mode else None
+        amask = None
         if add is not None:
             extra += 2.0 * m_in * cin
+            if gemm and "bnr" in dgrad_mode:  # identity block: bn3's incoming gradient + its ReLU mask (no dres)
+                amask = torch.randint(0, 255, (m_in * cin // 8,), dtype=torch.uint8, device=dev)
+                extra += m_in * cin / 8
         bnr = None
         if "bnr" in dgrad_mode:
             bx, mask, mean, invstd = bn_args(m_in, cin)
@@ -123,7 +127,8 @@ def main() -> None:
         if gemm:
             dg = lambda: conv.plx_gemm_nt(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), m_in, cin, cout, cout, cout,  # noqa
                                           cin, zero, None, add.data_ptr() if add is not None else None,
-                                          cin if add is not None else 0, bp, st)
+                                          cin if add is not None else 0,
+                                          amask.data_ptr() if amask is not None else None, bp, st)
         else:
             target = add if (add is not None and k == 1 and s == 2) else dx  # strided 1x1: in place on the deferred grad
             dg = lambda: conv.plx_conv_dgrad(dy.data_ptr(), wt.data_ptr(), target.data_ptr(), nb, h, w, cin, cout,  # noqa
@@ -158,7 +163,7 @@ def main() -> None:
             x.data_ptr(), r.data_ptr() if r is not None else None, y.data_ptr(), m, c, weight.data_ptr(),
             bias.data_ptr(), 1e-5, 0.1, rm.data_ptr(), rv.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(),
             stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(),
-            mo.data_ptr() if mo is not None else None, int(relu), st)
+            mo.data_ptr() if mo is not None else None, int(relu), None, st)
         nbytes = 2.0 * m * c * (2 + (1 if res else 0)) + (m * c / 8 if relu else 0)
         emit(name, "bn_fwd", count, timeit(fwd), nbytes, 0.0)
         dy = rnd((m, c))

@@ -92,6 +92,22 @@ def test_conv1x1_in_autocast_graph(cuda):
     assert conv.weight.grad is not None and torch.isfinite(conv.weight.grad).all()
 
 
+@pytest.mark.parametrize("m,n,k", [(1000, 128, 64), (777, 64, 128), (4096, 256, 256), (2048, 256, 64)])
+def test_gemm_nt_masked_add(cuda, m, n, k):
+    """Epilogue D add under a 1-bit ReLU mask (bn3's incoming gradient in an identity block's conv1 dgrad) vs the
+    fp32 product plus D * mask; single-stage (K == 64) and pipelined instantiations."""
+    from polyaxon_amd.ops.conv1x1 import gemm_nt
+
+    torch.manual_seed(5)
+    a, b, d = _bf(m, k, dev=cuda), _bf(n, k, dev=cuda), _bf(m, n, dev=cuda)
+    keep = torch.rand(m, n, device=cuda) > 0.5
+    bits = keep.view(-1, 8).to(torch.uint8) * (2 ** torch.arange(8, device=cuda, dtype=torch.uint8))
+    mask = bits.sum(1).to(torch.uint8)
+    out = gemm_nt(a, b, add=d, add_mask=mask)
+    ref = a.float() @ b.float().t() + d.float() * keep
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2 * k ** 0.5)
+
+
 @pytest.mark.parametrize("m,n,k", [(1000, 128, 64), (777, 64, 128), (4096, 256, 64)])
 def test_gemm_nt_channel_stats(cuda, m, n, k):
     from polyaxon_amd.ops.conv1x1 import gemm_nt, nt_stats_rows
