@@ -164,6 +164,137 @@ __device__ __forceinline__ bool fin_sum2(const float* __restrict__ pa, const flo
   return true;
 }
 
+struct FwdFin {
+  const uint16_t* x_row0;  // shift of the stats pass (nullptr: producer-fused, unshifted sums)
+  int C;
+  int64_t M;
+  const float* gamma;
+  const float* beta;
+  float eps, momentum;
+  float* running_mean;
+  float* running_var;
+  float* save_mean;
+  float* save_invstd;
+  float* scale;
+  float* bias;
+};
+
+struct BwdFin {
+  int C;
+  int64_t M;
+  const float* gamma;
+  const float* mean;
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
+  float* coef;
+  int accumulate;
+};
+
+__device__ __forceinline__ void fwd_finalize(const float* psum, const float* psq, int nblk, const FwdFin& f) {
+  double S, Q;  // level-2 partials per channel, summed in fp64
+  if (!fin_sum2(psum, psq, nblk, f.C, S, Q)) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const double m = S / (double)f.M;
+  double var = Q / (double)f.M - m * m;
+  if (var < 0.0) var = 0.0;
+  const float mean = (f.x_row0 != nullptr ? bf2f(f.x_row0[c]) : 0.f) + (float)m;
+  const float invstd = rsqrtf((float)var + f.eps);
+  const float g = f.gamma[c];
+  f.save_mean[c] = mean;
+  f.save_invstd[c] = invstd;
+  f.scale[c] = g * invstd;
+  f.bias[c] = f.beta[c] - mean * g * invstd;
+  if (f.running_mean != nullptr) {
+    const float unbiased = f.M > 1 ? (float)(var * (double)f.M / (double)(f.M - 1)) : (float)var;
+    f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * mean;
+    f.running_var[c] = (1.f - f.momentum) * f.running_var[c] + f.momentum * unbiased;
+  }
+}
+
+__device__ __forceinline__ void bwd_finalize(const float* pdz, const float* pdzx, int nblk, const BwdFin& f) {
+  double A, B;
+  if (!fin_sum2(pdz, pdzx, nblk, f.C, A, B)) return;
+  const int C = f.C;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float db = (float)A, dg = (float)B;
+  // accumulate: dgamma / dbeta are the parameters' own (flat) gradient slots, summed into like autograd would
+  f.dbeta[c] = f.accumulate ? f.dbeta[c] + db : db;
+  f.dgamma[c] = f.accumulate ? f.dgamma[c] + dg : dg;
+  const float is = f.invstd[c], k1 = f.gamma[c] * is;
+  const float k2 = db / (float)f.M, k3 = dg / (float)f.M;
+  // dx = k1 * (dz - k2 - xhat*k3),  xhat = (x - mean) * is   =>  dx = A*dz + B*x + D
+  f.coef[c] = k1;                                    // A
+  f.coef[C + c] = -k1 * k3 * is;                     // B
+  f.coef[2 * C + c] = -k1 * k2 + k1 * k3 * is * f.mean[c];  // D
+}
+
+// Level-1 -> level-2 reduce and the finalize in ONE launch: grid (ceil(C/64), S), every block reduces its 64 partial
+// rows of both sums for 64 channels (same order as bn_partial_reduce_kernel), publishes them, and takes a ticket on
+// its channel group's counter; the block drawing S-1 runs the finalize over the S level-2 rows.  The hand-off is
+// the split-K last-arriver recipe (cdna_hip_programming.md §5, in-launch split-K reduction): plain stores, every
+// wave drained, agent-scope release by one lane before a relaxed agent-scope ticket add, agent-scope acquire by the
+// last arriver before the workgroup reads.  Counters start at zero (allocated zeroed) and the last arriver resets
+// its own; launches that share a counter array are stream-ordered.  Saves a launch boundary and the separate
+// finalize pass's own ramp per BatchNorm direction (106 per ResNet-50 step).
+__device__ __forceinline__ bool reduce_l2_last(const float* __restrict__ part, int nblk, int C, float* l2, int S,
+                                               unsigned* cnt) {
+  __shared__ float sh[2][256];
+  __shared__ int s_last;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane = threadIdx.x >> 6;
+  const int s = blockIdx.y;
+  const int b0 = s * kRowsPerSplit;
+  int b1 = b0 + kRowsPerSplit;
+  if (b1 > nblk) b1 = nblk;
+  float a0 = 0.f, a1 = 0.f;
+  if (c < C) {
+    const float* p0 = part;
+    const float* p1 = part + (int64_t)nblk * C;
+#pragma unroll 4
+    for (int b = b0 + lane; b < b1; b += 4) {
+      a0 += p0[(int64_t)b * C + c];
+      a1 += p1[(int64_t)b * C + c];
+    }
+  }
+  sh[0][threadIdx.x] = a0;
+  sh[1][threadIdx.x] = a1;
+  __syncthreads();
+  if (lane == 0 && c < C) {
+    const int t = threadIdx.x;
+    l2[(int64_t)s * C + c] = sh[0][t] + sh[0][t + 64] + sh[0][t + 128] + sh[0][t + 192];
+    l2[((int64_t)S + s) * C + c] = sh[1][t] + sh[1][t + 64] + sh[1][t + 128] + sh[1][t + 192];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (unsigned)(S - 1);
+    if (last) {
+      __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+__global__ __launch_bounds__(256) void bn_fwd_reduce_finalize_kernel(const float* __restrict__ part, int nblk,
+                                                                     float* l2, int S, unsigned* cnt, FwdFin f) {
+  if (!reduce_l2_last(part, nblk, f.C, l2, S, cnt)) return;
+  fwd_finalize(l2, l2 + (int64_t)S * f.C, S, f);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_finalize_kernel(const float* __restrict__ part, int nblk,
+                                                                     float* l2, int S, unsigned* cnt, BwdFin f) {
+  if (!reduce_l2_last(part, nblk, f.C, l2, S, cnt)) return;
+  bwd_finalize(l2, l2 + (int64_t)S * f.C, S, f);
+}
+
 __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq, int nblk,
                                        const uint16_t* __restrict__ x_row0, int C, int64_t M,
                                        const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
@@ -457,6 +588,35 @@ inline void launch_dx(hipStream_t stream, int64_t n_vec, int G, const void* x, c
                        (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, G, relu, rb);
 }
 
+// level-1 partials [2][nblk][C] -> finalize: one fused launch with a counter array (>= ceil(C/64) zeroed words),
+// else the reduce and finalize kernels back to back
+inline void reduce_finalize_fwd(hipStream_t stream, const float* part, int nblk, float* l2, unsigned* cnt,
+                                const FwdFin& f) {
+  const int C = f.C, S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
+  if (cnt != nullptr) {
+    hipLaunchKernelGGL(bn_fwd_reduce_finalize_kernel, dim3((C + 63) / 64, S), dim3(256), 0, stream, part, nblk, l2, S,
+                       cnt, f);
+    return;
+  }
+  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, S, 2), dim3(256), 0, stream, part, nblk, C, l2, S);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S,
+                     f.x_row0, C, f.M, f.gamma, f.beta, f.eps, f.momentum, f.running_mean, f.running_var, f.save_mean,
+                     f.save_invstd, f.scale, f.bias);
+}
+
+inline void reduce_finalize_bwd(hipStream_t stream, const float* part, int nblk, float* l2, unsigned* cnt,
+                                const BwdFin& f) {
+  const int C = f.C, S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
+  if (cnt != nullptr) {
+    hipLaunchKernelGGL(bn_bwd_reduce_finalize_kernel, dim3((C + 63) / 64, S), dim3(256), 0, stream, part, nblk, l2, S,
+                       cnt, f);
+    return;
+  }
+  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, S, 2), dim3(256), 0, stream, part, nblk, C, l2, S);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S, C,
+                     f.M, f.gamma, f.mean, f.invstd, f.dgamma, f.dbeta, f.coef, f.accumulate);
+}
+
 }  // namespace
 
 // fp32 workspace the host must pass as `partials`: level-1 [2][nblk][C] + level-2 [2][S][C].
@@ -471,6 +631,8 @@ PLX_API int plx_bn_forward(const void* x, const void* res, void* y, int64_t M, i
                            float* save_mean, float* save_invstd, float* scale_bias /* [2C] */,
                            float* partials /* plx_bn_workspace floats */, uint8_t* mask /* M*C/8 bytes or null */,
                            int relu, const float* res_sb /* nullable [2C], see bn_apply_kernel */,
+                           unsigned* counters /* nullable: >= ceil(C/64) zeroed words, one launch for
+                                                 reduce + finalize */,
                            hipStream_t stream) {
   Plan p;
   if (!plan_for(M, C, &p) || M < 1) return 1;
@@ -479,11 +641,9 @@ PLX_API int plx_bn_forward(const void* x, const void* res, void* y, int64_t M, i
   hipLaunchKernelGGL(bn_stats_kernel, dim3(p.nblk, p.gy), dim3(kBlock), 0, stream, (const bf16x8*)x, M, p.G, p.Gb,
                      p.rows_per_block, psum, psq);
   float* l2 = partials + 2 * (int64_t)p.nblk * C;
-  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, p.S, 2), dim3(256), 0, stream, partials, p.nblk, C,
-                     l2, p.S);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)p.S * C, p.S,
-                     (const uint16_t*)x, C, M, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
-                     save_invstd, scale_bias, scale_bias + C);
+  reduce_finalize_fwd(stream, partials, p.nblk, l2, counters,
+                      FwdFin{(const uint16_t*)x, C, M, gamma, beta, eps, momentum, running_mean, running_var,
+                             save_mean, save_invstd, scale_bias, scale_bias + C});
   const int64_t n_vec = M * p.G;
   if (y != nullptr)  // y == nullptr: statistics and scale/bias only (the apply is deferred to the consumer)
     hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
@@ -505,15 +665,12 @@ PLX_API int plx_bn_forward_from_partials(const void* x, const void* res, void* y
                                          float* running_mean, float* running_var, float* save_mean,
                                          float* save_invstd, float* scale_bias, const float* partials, int nblk,
                                          float* l2, uint8_t* mask, int relu, const float* res_sb,
-                                         hipStream_t stream) {
+                                         unsigned* counters, hipStream_t stream) {
   Plan p;
   if (!plan_for(M, C, &p) || M < 1 || nblk < 1) return 1;
-  const int S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
-  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, S, 2), dim3(256), 0, stream, partials, nblk, C, l2,
-                     S);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S,
-                     (const uint16_t*)nullptr, C, M, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
-                     save_invstd, scale_bias, scale_bias + C);
+  reduce_finalize_fwd(stream, partials, nblk, l2, counters,
+                      FwdFin{nullptr, C, M, gamma, beta, eps, momentum, running_mean, running_var, save_mean,
+                             save_invstd, scale_bias, scale_bias + C});
   const int64_t n_vec = M * p.G;
   if (y != nullptr)
     hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
@@ -543,7 +700,8 @@ PLX_API int plx_bn_dx_blocks(int64_t M, int C) {
 PLX_API int plx_bn_backward(const void* x, const uint8_t* mask, const void* dy, void* dx, void* dres, int64_t M, int C,
                             const float* gamma, const float* save_mean, const float* save_invstd, float* dgamma,
                             float* dbeta, float* coef /* [3C] */, float* partials /* plx_bn_workspace floats */, int relu,
-                            int accumulate, const ResBn* resbn /* nullable, needs dres */, hipStream_t stream) {
+                            int accumulate, const ResBn* resbn /* nullable, needs dres */, unsigned* counters,
+                            hipStream_t stream) {
   Plan p;
   if (!plan_for(M, C, &p) || M < 1 || (relu && mask == nullptr)) return 1;
   if (resbn != nullptr && (dres == nullptr || resbn->part == nullptr)) return 1;
@@ -554,10 +712,8 @@ PLX_API int plx_bn_backward(const void* x, const uint8_t* mask, const void* dy, 
                      mask, (const bf16x8*)dy, M, p.G, p.Gb, p.rows_per_block, save_mean, save_invstd,
                      relu, pa, pb);
   float* l2 = partials + 2 * (int64_t)p.nblk * C;
-  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, p.S, 2), dim3(256), 0, stream, partials, p.nblk, C,
-                     l2, p.S);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)p.S * C, p.S, C, M,
-                     gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
+  reduce_finalize_bwd(stream, partials, p.nblk, l2, counters,
+                      BwdFin{C, M, gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate});
   const int64_t n_vec = M * p.G;
   launch_dx(stream, n_vec, p.G, x, mask, dy, dx, dres, coef, relu, rb);
   return (int)hipGetLastError();
@@ -570,16 +726,13 @@ PLX_API int plx_bn_backward_from_partials(const void* x, const uint8_t* mask, co
                                           int64_t M, int C, const float* gamma, const float* save_mean,
                                           const float* save_invstd, float* dgamma, float* dbeta, float* coef,
                                           const float* partials, int nblk, float* l2, int relu, int accumulate,
-                                          const ResBn* resbn, hipStream_t stream) {
+                                          const ResBn* resbn, unsigned* counters, hipStream_t stream) {
   Plan p;
   if (!plan_for(M, C, &p) || M < 1 || nblk < 1 || (relu && mask == nullptr)) return 1;
   if (resbn != nullptr && (dres == nullptr || resbn->part == nullptr)) return 1;
   const ResBn rb = resbn != nullptr ? *resbn : ResBn{};
-  const int S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
-  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, S, 2), dim3(256), 0, stream, partials, nblk, C, l2,
-                     S);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S, C,
-                     M, gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate);
+  reduce_finalize_bwd(stream, partials, nblk, l2, counters,
+                      BwdFin{C, M, gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate});
   const int64_t n_vec = M * p.G;
   launch_dx(stream, n_vec, p.G, x, mask, dy, dx, dres, coef, relu, rb);
   return (int)hipGetLastError();

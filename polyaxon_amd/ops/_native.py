@@ -158,14 +158,15 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
     },
     "plx_bn": {
         "plx_bn_workspace": [_L, _I],
-        "plx_bn_forward": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
+        "plx_bn_forward": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P],
         "plx_bn_apply": [_P, _P, _P, _L, _I, _P, _I, _P],
         "plx_bn_l2_workspace": [_I, _I],
         "plx_bn_forward_from_partials": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P, _P,
-                                         _I, _P, _P],
-        "plx_bn_backward": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P],
+                                         _I, _P, _P, _P],
+        "plx_bn_backward": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P],
         "plx_bn_dx_blocks": [_L, _I],
-        "plx_bn_backward_from_partials": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I, _P, _P],
+        "plx_bn_backward_from_partials": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I, _P,
+                                          _P, _P],
     },
     "plx_procmon": {
         "plx_pm_create": [],

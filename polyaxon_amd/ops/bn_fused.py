@@ -26,6 +26,22 @@ def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+_COUNTERS = {}
+_FUSED_FINALIZE = os.environ.get("PLX_BN_FUSED_FINALIZE", "1") != "0"  # A/B knob
+
+
+def _counters(dev: torch.device):
+    """Zeroed ticket counters of the one-launch reduce + finalize (csrc/bn_kernels.hip ``reduce_l2_last``), one
+    array per (device, stream): launches sharing it are stream-ordered and each leaves it zeroed again."""
+    if not _FUSED_FINALIZE:
+        return None
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    t = _COUNTERS.get(key)
+    if t is None:
+        t = _COUNTERS[key] = torch.zeros(64, dtype=torch.int32, device=dev)  # >= ceil(2048 / 64) groups
+    return t.data_ptr()
+
+
 def _cl(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
 
@@ -74,7 +90,8 @@ class _BNAct(torch.autograd.Function):
             rc = lib.plx_bn_forward_from_partials(
                 x.data_ptr(), res.data_ptr() if res is not None else None, yp, m, c, weight.data_ptr(),
                 bias.data_ptr(), float(eps), float(momentum), rm, rv, stats.data_ptr(), stats[c:].data_ptr(),
-                stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(), mp, int(relu), rsp, _stream())
+                stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(), mp, int(relu), rsp,
+                _counters(x.device), _stream())
             _native.check(rc, "plx_bn_forward_from_partials")
         else:
             partials = torch.empty(ws, **f32)
@@ -82,7 +99,7 @@ class _BNAct(torch.autograd.Function):
                 x.data_ptr(), res.data_ptr() if res is not None else None, yp, m, c,
                 weight.data_ptr(), bias.data_ptr(), float(eps), float(momentum), rm, rv,
                 stats.data_ptr(), stats[c:].data_ptr(), stats[2 * c:].data_ptr(), partials.data_ptr(), mp, int(relu),
-                rsp, _stream())
+                rsp, _counters(x.device), _stream())
             _native.check(rc, "plx_bn_forward")
         ctx.save_for_backward(x, mask, weight, stats)
         ctx.relu = relu
@@ -147,7 +164,7 @@ class _BNAct(torch.autograd.Function):
                 x.data_ptr(), mask.data_ptr() if mask is not None else None, dy.data_ptr(), dx.data_ptr(),
                 dres.data_ptr() if dres is not None else None, m, c, weight.data_ptr(), stats.data_ptr(),
                 stats[c:].data_ptr(), dg_ptr, db_ptr, coef.data_ptr(), part.data_ptr(), nblk, l2.data_ptr(),
-                int(ctx.relu), acc, rbp, _stream())
+                int(ctx.relu), acc, rbp, _counters(x.device), _stream())
             _native.check(rc, "plx_bn_backward_from_partials")
         else:
             partials = torch.empty(ctx.ws, **f32)
@@ -155,7 +172,7 @@ class _BNAct(torch.autograd.Function):
                 x.data_ptr(), mask.data_ptr() if mask is not None else None, dy.data_ptr(), dx.data_ptr(),
                 dres.data_ptr() if dres is not None else None, m, c, weight.data_ptr(), stats.data_ptr(),
                 stats[c:].data_ptr(), dg_ptr, db_ptr, coef.data_ptr(), partials.data_ptr(), int(ctx.relu), acc,
-                rbp, _stream())
+                rbp, _counters(x.device), _stream())
             _native.check(rc, "plx_bn_backward")
         if ctx.box is not None:  # the residual's gradient rides into conv1's dgrad epilogue (ops.conv1x1)
             if masked_box:

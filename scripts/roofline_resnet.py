@@ -44,6 +44,7 @@ def main() -> None:
     conv.plx_set_nt_single_stage(a.nt_single_stage)
     zero = _zero_page(dev).data_ptr()
     st = torch.cuda.current_stream().cuda_stream
+    cnt = torch.zeros(64, dtype=torch.int32, device=dev)  # BatchNorm reduce + finalize tickets
     bf = dict(dtype=torch.bfloat16, device=dev)
     f32 = dict(dtype=torch.float32, device=dev)
     rows = []
@@ -163,7 +164,7 @@ def main() -> None:
             x.data_ptr(), r.data_ptr() if r is not None else None, y.data_ptr(), m, c, weight.data_ptr(),
             bias.data_ptr(), 1e-5, 0.1, rm.data_ptr(), rv.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(),
             stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(),
-            mo.data_ptr() if mo is not None else None, int(relu), None, st)
+            mo.data_ptr() if mo is not None else None, int(relu), None, cnt.data_ptr(), st)
         nbytes = 2.0 * m * c * (2 + (1 if res else 0)) + (m * c / 8 if relu else 0)
         emit(name, "bn_fwd", count, timeit(fwd), nbytes, 0.0)
         dy = rnd((m, c))
@@ -175,13 +176,13 @@ def main() -> None:
             bwd = lambda: bn.plx_bn_backward_from_partials(  # noqa
                 x.data_ptr(), mp, dy.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else None, m, c,
                 weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), dg.data_ptr(), db.data_ptr(), coef.data_ptr(),
-                part.data_ptr(), nblk, l2.data_ptr(), int(relu), 1, None, st)
+                part.data_ptr(), nblk, l2.data_ptr(), int(relu), 1, None, cnt.data_ptr(), st)
         else:
             pw = torch.empty(int(bn.plx_bn_workspace(m, c)), **f32)
             bwd = lambda: bn.plx_bn_backward(  # noqa
                 x.data_ptr(), mp, dy.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else None, m, c,
                 weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), dg.data_ptr(), db.data_ptr(), coef.data_ptr(),
-                pw.data_ptr(), int(relu), 1, None, st)
+                pw.data_ptr(), int(relu), 1, None, cnt.data_ptr(), st)
         nbytes = 2.0 * m * c * (3 + (1 if res else 0)) + (m * c / 8 if relu else 0)
         emit(name, "bn_bwd" + ("" if partials_bwd else "+reduce"), count, timeit(bwd), nbytes, 0.0)
 

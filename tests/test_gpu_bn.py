@@ -87,3 +87,53 @@ def test_resnet_fused_matches_unfused_loss(cuda):
     cos = {k: float(F.cosine_similarity(res[k][1], res["fp32"][1], dim=0)) for k in ("fused", "unfused")}
     assert cos["fused"] > 0.9, cos
     assert cos["fused"] >= cos["unfused"] - 0.01, cos
+
+
+def test_reduce_finalize_one_launch_matches_two(cuda):
+    """The one-launch reduce + finalize (ticket counters, last-arriver finalize) gives bit-identical statistics and
+    backward coefficients to the two-launch path, over many row splits (S = 16) and repeated calls (the counters
+    return to zero)."""
+    from polyaxon_amd.ops import _native
+
+    lib = _native.lib("plx_bn")
+    torch.manual_seed(7)
+    m, c, nblk = 128 * 1000, 256, 1000
+    f32 = dict(dtype=torch.float32, device=cuda)
+    x = torch.randn(m, c, device=cuda).to(torch.bfloat16)
+    part = torch.rand(2 * nblk * c, **f32) * 4.0
+    l2 = torch.empty(int(lib.plx_bn_l2_workspace(nblk, c)), **f32)
+    cnt = torch.zeros(64, dtype=torch.int32, device=cuda)
+    w, b = torch.rand(c, **f32) + 0.5, torch.randn(c, **f32)
+    st = torch.cuda.current_stream().cuda_stream
+
+    def fwd(counters):
+        stats, rm, rv = torch.empty(4 * c, **f32), torch.zeros(c, **f32), torch.ones(c, **f32)
+        rc = lib.plx_bn_forward_from_partials(x.data_ptr(), None, None, m, c, w.data_ptr(), b.data_ptr(), 1e-5, 0.1,
+                                              rm.data_ptr(), rv.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(),
+                                              stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(), None, 0,
+                                              None, counters, st)
+        assert rc == 0
+        return torch.cat([stats, rm, rv])
+
+    mean, inv = torch.randn(c, **f32), torch.rand(c, **f32) + 0.5
+
+    def bwd(counters):
+        dg, db, coef = torch.zeros(c, **f32), torch.zeros(c, **f32), torch.empty(3 * c, **f32)
+        dx = torch.empty_like(x)
+        rc = lib.plx_bn_backward_from_partials(x.data_ptr(), None, x.data_ptr(), dx.data_ptr(), None, m, c,
+                                               w.data_ptr(), mean.data_ptr(), inv.data_ptr(), dg.data_ptr(),
+                                               db.data_ptr(), coef.data_ptr(), part.data_ptr(), nblk, l2.data_ptr(),
+                                               0, 1, None, counters, st)
+        assert rc == 0
+        return torch.cat([dg, db, coef])
+
+    ref_f, ref_b = fwd(None), bwd(None)
+    for _ in range(3):
+        assert torch.equal(fwd(cnt.data_ptr()), ref_f)
+        assert torch.equal(bwd(cnt.data_ptr()), ref_b)
+    torch.cuda.synchronize()
+    assert int(cnt.abs().sum()) == 0
+    # and against the fp64 host sums
+    p = part.view(2, nblk, c).double().sum(1)
+    mean = p[0] / m
+    torch.testing.assert_close(ref_f[:c].double(), mean, rtol=1e-5, atol=1e-6)
