@@ -793,6 +793,49 @@ __global__ void weight_prepk_kernel(const float* __restrict__ w, long s_co, long
         wd[((long)ci * taps + tap) * cout + co] = v;          // [ci][tap][co]
     }
 }
+
+// One launch for every convolution weight of a model (plx_weight_prep_all): segment s reads the fp32 weight
+// [cout][taps][cin] at base + src (the flat buffer's channels_last order) and writes bf16 Wf (same order) at
+// wf + dst_f and bf16 Wd [cin][taps][cout] at wd + dst_d.  Block b handles one 32 x 32 (cout x cin) tile of one
+// tap of the segment whose tile0 <= b < next tile0; the transpose goes through LDS so both stores coalesce.
+struct WSeg {
+    long src, dst_f, dst_d;
+    int cout, cin, taps, tile0;
+};
+
+__global__ void __launch_bounds__(256) weight_prep_all_kernel(const float* __restrict__ base, __bf16* __restrict__ wf,
+                                                              __bf16* __restrict__ wd, const WSeg* __restrict__ segs,
+                                                              int nseg) {
+    __shared__ float tile[32][33];
+    int lo = 0, hi = nseg - 1;                              // last segment with tile0 <= blockIdx.x (uniform)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (segs[mid].tile0 <= (int)blockIdx.x) lo = mid;
+        else hi = mid - 1;
+    }
+    const WSeg s = segs[lo];
+    int t = blockIdx.x - s.tile0;
+    const int nci = (s.cin + 31) >> 5, nco = (s.cout + 31) >> 5;
+    const int ci0 = (t % nci) * 32;
+    t /= nci;
+    const int co0 = (t % nco) * 32, tap = t / nco;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int j = ty; j < 32; j += 8) {
+        const int co = co0 + j, ci = ci0 + tx;
+        float v = 0.f;
+        if (co < s.cout && ci < s.cin) {
+            const long e = ((long)co * s.taps + tap) * s.cin + ci;
+            v = base[s.src + e];
+            wf[s.dst_f + e] = (__bf16)v;
+        }
+        tile[j][tx] = v;
+    }
+    __syncthreads();
+    for (int j = ty; j < 32; j += 8) {
+        const int ci = ci0 + j, co = co0 + tx;
+        if (co < s.cout && ci < s.cin) wd[s.dst_d + ((long)ci * s.taps + tap) * s.cout + co] = (__bf16)tile[tx][j];
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -939,6 +982,17 @@ int plx_weight_prepk(const float* w, long s_co, long s_ci, long s_kh, long s_kw,
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(weight_prepk_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, w, s_co, s_ci, s_kh, s_kw,
                        (__bf16*)wf, (__bf16*)wd, cout, cin, K);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// segs: device array of nseg WSeg records (40 bytes each: int64 src, dst_f, dst_d; int32 cout, cin, taps, tile0),
+// sorted by tile0, tile0[0] == 0; total_tiles = sum over segments of taps * ceil(cout/32) * ceil(cin/32)
+int plx_weight_prep_all(const float* base, void* wf, void* wd, const void* segs, int nseg, int total_tiles,
+                        void* stream) {
+    static_assert(sizeof(WSeg) == 40, "WSeg layout is shared with ops/wcache.py");
+    if (nseg <= 0 || total_tiles <= 0) return -1;
+    hipLaunchKernelGGL(weight_prep_all_kernel, dim3(total_tiles), dim3(256), 0, (hipStream_t)stream, base,
+                       (__bf16*)wf, (__bf16*)wd, (const WSeg*)segs, nseg);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

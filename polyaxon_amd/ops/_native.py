@@ -199,6 +199,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
         "plx_weight_prepk": [_P, _L, _L, _L, _L, _P, _P, _I, _I, _I, _P],
+        "plx_weight_prep_all": [_P, _P, _P, _P, _I, _I, _P],
         "plx_conv_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
         "plx_conv_dgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
         "plx_conv_dgrad_blocks": [_I, _I, _I, _I, _I, _I, _I],

@@ -22,7 +22,7 @@ import torch.nn.functional as F
 
 import ctypes
 
-from polyaxon_amd.ops import _native, side_stream
+from polyaxon_amd.ops import _native, side_stream, wcache
 from polyaxon_amd.ops.conv1x1 import (GradMailbox, _bf16_context, _num_cus, _stream, _zero_page, bn_link_of, nt_stats_rows,
                                       unpack_relu_mask)
 from polyaxon_amd.ops.flat import direct_grad
@@ -54,7 +54,7 @@ class _ConvK(torch.autograd.Function):
         n, cin, h, w = x.shape
         cout, k = weight.shape[0], weight.shape[2]
         ho, wo = _out(h, k, stride), _out(w, k, stride)
-        wf, wd = weight_prep_k(weight)
+        wf, wd = wcache.lookup(weight) or weight_prep_k(weight)
         y = torch.empty((n, cout, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         rc = lib.plx_conv_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), n, h, w, cin, cout, k, stride,
                               _zero_page(x.device).data_ptr(), stats.data_ptr() if stats is not None else None,

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from polyaxon_amd.ops import _native, side_stream
+from polyaxon_amd.ops import _native, side_stream, wcache
 from polyaxon_amd.ops.flat import direct_grad
 
 _ZERO: Dict[int, torch.Tensor] = {}
@@ -224,7 +224,7 @@ class _Conv1x1(torch.autograd.Function):
         ctx.wgrad = direct_grad(weight)
         n, cin, h, w = x.shape
         cout = weight.shape[0]
-        wb, wt = weight_prep(weight)
+        wb, wt = wcache.lookup(weight) or weight_prep(weight)
         y = torch.empty((n, cout, h, w), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         gemm_nt(_rows(x), wb, _rows(y), stats)
         ctx.save_for_backward(x, wt)

@@ -21,6 +21,7 @@ The same class runs on CPU (no graph, reference kernels) for the unit tests.
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass
 from typing import Callable, Dict, Optional, Tuple
@@ -32,6 +33,7 @@ import torch.nn.functional as F
 from polyaxon_amd.ops import _native, side_stream
 from polyaxon_amd.ops.flat import FlatParams
 from polyaxon_amd.ops.optim import FusedAdamW, FusedSGD
+from polyaxon_amd.ops.wcache import ConvWeightCache
 
 
 def _stream_ptr(dev: torch.device) -> int:
@@ -85,6 +87,11 @@ class ResidentTrialExecutor:
         self.graph_rejected = False
         self.graph_check_error: Optional[float] = None
         self.snapshots: Dict[object, TrialState] = {}
+        # bf16 operands of every native conv from one launch per step (ops/wcache.py); PLX_WCACHE=0: per layer
+        self.wcache = None
+        if self.is_cuda and os.environ.get("PLX_WCACHE", "1") != "0":
+            cache = ConvWeightCache(model, self.flat.params)
+            self.wcache = cache if len(cache) else None
         self.model.train()
 
     # ------------------------------------------------------------------ buffers (BN running stats)
@@ -109,14 +116,20 @@ class ResidentTrialExecutor:
     def _train_step(self) -> None:
         if self.data is not None:
             self.data.next()
-        if self.amp_dtype is not None:
-            with torch.autocast("cuda", dtype=self.amp_dtype):
+        if self.wcache is not None:
+            self.wcache.activate()
+        try:
+            if self.amp_dtype is not None:
+                with torch.autocast("cuda", dtype=self.amp_dtype):
+                    out = self.model(self.x)
+                    loss = self.loss_fn(out, self.y)
+            else:
                 out = self.model(self.x)
                 loss = self.loss_fn(out, self.y)
-        else:
-            out = self.model(self.x)
-            loss = self.loss_fn(out, self.y)
-        loss.backward()
+            loss.backward()
+        finally:
+            if self.wcache is not None:
+                self.wcache.deactivate()
         side_stream.join(self.device)  # weight-gradient GEMMs overlapped on the side stream (ops/side_stream.py)
         self.opt.step_()
         self._record(loss.detach())

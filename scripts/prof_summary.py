@@ -68,6 +68,43 @@ def main():
     out.append("|---|---|---|")
     for cls, d in per_class.most_common():
         out.append(f"| {cls} | {d / n_steps / 1e6:.3f} | {100 * d / total:.1f}% |")
+    # GPU idle time: the union of kernel intervals over all streams vs the window, and per stream the gaps between
+    # consecutive kernels (launch / drain boundaries inside the replayed graph)
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in win)
+    union, cur_s, cur_e, prev = 0, iv[0][0], iv[0][1], iv[0][2]
+    idle = []                                               # (gap ns, kernel before, kernel after)
+    for s, e, name in iv[1:]:
+        if s > cur_e:
+            union += cur_e - cur_s
+            idle.append((s - cur_e, prev, name))
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+        if e >= cur_e:
+            prev = name
+    union += cur_e - cur_s
+    idle.sort(reverse=True)
+    big = [g for g in idle if g[0] > 20_000]
+    skey = "Stream_Id" if "Stream_Id" in win[0] else ("Queue_Id" if "Queue_Id" in win[0] else None)
+    out.append("")
+    out.append(f"GPU busy (union over streams) {union / n_steps / 1e6:.3f} ms/step, idle "
+               f"{(t1 - t0 - union) / n_steps / 1e6:.3f} ms/step ({len(idle)} gaps; {len(big)} over 20 us hold "
+               f"{sum(g[0] for g in big) / n_steps / 1e6:.3f} ms/step)")
+    for g, before, after in idle[:8]:
+        out.append(f"- idle {g / 1e3:.1f} us after `{before[:60]}` before `{after[:60]}`")
+    if skey is not None:
+        streams = collections.defaultdict(list)
+        for r in win:
+            streams[r[skey]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        out.append("")
+        out.append(f"| {skey} | launches/step | busy ms/step | gaps ms/step | median gap us |")
+        out.append("|---|---|---|---|---|")
+        for sid, ks in sorted(streams.items(), key=lambda kv: -len(kv[1])):
+            ks.sort()
+            gaps = sorted(max(0, ks[i + 1][0] - ks[i][1]) for i in range(len(ks) - 1))
+            med = gaps[len(gaps) // 2] / 1e3 if gaps else 0.0
+            out.append(f"| {sid} | {len(ks) / n_steps:.0f} | {sum(e - s for s, e in ks) / n_steps / 1e6:.3f} | "
+                       f"{sum(gaps) / n_steps / 1e6:.3f} | {med:.1f} |")
     out.append("")
     out.append("| kernel | calls/step | us/call | ms/step | share |")
     out.append("|---|---|---|---|---|")

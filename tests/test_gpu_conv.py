@@ -325,3 +325,46 @@ def test_downsample_mailbox_matches_autograd_sum(cuda):
         for got, ref in zip(outs[0], outs[1]):
             torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
         assert float(outs[0][1].abs().sum()) > 0 and float(outs[0][2].abs().sum()) > 0
+
+
+def test_weight_cache_matches_per_layer_prep(cuda):
+    """ops.wcache: one plx_weight_prep_all launch gives every native conv the same bf16 Wf / Wd operands as the
+    per-layer preps (bit-exact), and a step run from the cache gives the same flat gradients."""
+    from polyaxon_amd.models.resnet import ResNet
+    from polyaxon_amd.ops.conv import ConvKxK, weight_prep_k
+    from polyaxon_amd.ops.conv1x1 import Conv1x1, weight_prep
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.ops.wcache import ConvWeightCache
+
+    torch.manual_seed(0)
+    m = ResNet([2, 1, 1, 1], num_classes=10, width=64, zero_init_residual=False).to(memory_format=torch.channels_last)
+    flat = FlatParams(m, cuda)
+    flat.enable_direct_grads(True)
+    cache = ConvWeightCache(m, flat.params)
+    convs = [mod for mod in m.modules() if isinstance(mod, (Conv1x1, ConvKxK))]
+    n_native = sum(1 for mod in convs if mod.weight.shape[1] % 64 == 0)
+    assert len(cache) == n_native > 10
+    cache.refresh()
+    for mod in convs:
+        got = cache.views.get(mod.weight.data_ptr())
+        if got is None:
+            continue
+        k = mod.weight.shape[2]
+        ref = weight_prep(mod.weight) if k == 1 and mod.stride == (1, 1) else weight_prep_k(mod.weight)
+        assert torch.equal(got[0].reshape(-1), ref[0].reshape(-1))
+        assert torch.equal(got[1].reshape(-1), ref[1].reshape(-1))
+    x = torch.randn(4, 3, 64, 64, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (4,), device=cuda)
+    grads = []
+    for use in (False, True):
+        flat.grads.zero_()
+        if use:
+            cache.activate()
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x).float(), y)
+            loss.backward()
+        finally:
+            cache.deactivate()
+        grads.append(flat.grads.clone())
+    torch.testing.assert_close(grads[1], grads[0], rtol=1e-3, atol=1e-3 * float(grads[0].abs().max()))
