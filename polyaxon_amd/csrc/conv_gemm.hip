@@ -148,7 +148,11 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 // 16 rows of a fragment read on 16 distinct bank slots.
 __device__ __forceinline__ int nt_swz(int row) { return (row >> 1) & 7; }
 
-template <int BM, int BN, int WGM, int WGN, bool CONV, int MINB = 2>
+// NBUF = 2: double-buffered K stages (2 blocks per CU); NBUF = 1: one stage buffer (stage, wait, compute, barrier)
+// and 4 blocks per CU, whose interleaving hides the staging instead (MINB = blocks per CU the registers allow)
+// BWD: the data-gradient epilogue (D add, ReLU-masked D, BatchNorm-backward partials); !BWD: the forward one (channel
+// stats).  Compile-time so each kernel only holds the epilogue registers it uses.
+template <int BM, int BN, int WGM, int WGN, bool CONV, int MINB = 2, int NBUF = 2, bool BWD = false>
 __global__ void __launch_bounds__(NTHREADS, MINB)
 gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
                int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
@@ -242,8 +246,15 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     __syncthreads();
     const int fr = lane & 15, fq = lane >> 4;
     for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) {
+        const int cur = NBUF == 2 ? kt & 1 : 0;
+        if (NBUF == 1 && kt > 0) {                          // restage the single buffer (the loop's tail barrier
+            stage(0, kt * BK, st, sc);                      // retired its readers)
+            sc += BK;
+            if (sc == cdim) { sc = 0; ++st; }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        if (NBUF == 2 && kt + 1 < nk) {
             stage(cur ^ 1, (kt + 1) * BK, st, sc);
             sc += BK;
             if (sc == cdim) { sc = 0; ++st; }
@@ -271,7 +282,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                 for (int rm = 0; rm < RM; ++rm)
                     acc[rn][rm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rn], fb[rm], acc[rn][rm], 0, 0, 0);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (NBUF == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
     // Epilogue through LDS (the k-loop's last barrier freed it): D[n][m] has column m = fr and rows
@@ -288,8 +299,9 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     const int rows = min(BM, M - m0);
     const int cc = tid % CHUNKS, r0 = tid / CHUNKS;
     const int ch0 = n0 + cc * 8;                            // this thread's 8 channels
-    const bool bnr_on = bnr.part != nullptr;
-    const bool stats_on = stats != nullptr;
+    const bool bnr_on = BWD && bnr.part != nullptr;
+    const bool stats_on = !BWD && stats != nullptr;
+    const bool d_on = BWD && D != nullptr;
     int orow[ITERS];                                        // output pixel rows (< 2^31)
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
@@ -299,7 +311,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     }
     uint4 dpre[ITERS], xpre[ITERS];
     uint32_t mpre[ITERS], dmpre[ITERS];
-    if (D != nullptr) {
+    if (d_on) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) dpre[it] = *(const uint4*)(D + (size_t)orow[it] * ldd + ch0);
         // dmask: D is a ReLU's incoming gradient and this bit mask (1 bit per element, ldd == N) its forward
@@ -362,7 +374,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                 s2[2 * j + 1] = fmaf(hi, hi, s2[2 * j + 1]);
             }
         }
-        if (D != nullptr) {
+        if (d_on) {
             // C = A.B^T + D (a second gradient into the same tensor, e.g. the residual branch's): added in fp32
             // and rounded once, instead of a separate bf16 add pass over both tensors.  D is indexed like C, so
             // D == C (in place) is allowed.
@@ -396,11 +408,12 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         }
     }
     // Per-channel partials of this block's rows: the RSTEP threads sharing a chunk column each hold 16 values
-    // (8 channels x 2 sums).  They go through LDS past the staged tile (rows of 17 floats: conflict-free both
+    // (8 channels x 2 sums).  They go through LDS over the staged tile (rows of 17 floats: conflict-free both
     // ways) and every thread then sums ONE (chunk column, value) pair over the RSTEP rows -- 16 loads per thread
     // instead of 16 threads each walking 15 x 16 dependent loads while the rest of the block waits.
     auto reduce_store = [&](const float* va, const float* vb, float* dst_a, float* dst_b) {
-        float* red = (float*)(smem + BM * CROW);            // [NTHREADS][17]
+        float* red = (float*)smem;                          // [NTHREADS][17], over the staged tile: its reads
+        __syncthreads();                                    // (the store loop) must be done
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             red[tid * 17 + k] = va[k];
@@ -629,27 +642,51 @@ int set_lds(KernelT k, int bytes) {
                                                                                                                  : -2;
 }
 
-// NBUF = 1: a single K stage (K == BK, the skinny 1x1 GEMMs): LDS = max(stage, epilogue) and 3 blocks per CU
+// NBUF = 1: one K-stage buffer, LDS = max(stage, epilogue staging), 3-4 blocks per CU (the skinny GEMMs)
 template <int BM, int BN, int WGM, int WGN, bool CONV = false, int NBUF = 2>
 int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
               const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}, const void* D = nullptr,
               int ldd = 0, BnBwd bnr = {}, const uint8_t* dmask = nullptr) {
-    constexpr int EPI = BM * (BN * 2 + 16) + NTHREADS * 17 * 4;
+    constexpr int TILE = BM * (BN * 2 + 16), RED = NTHREADS * 17 * 4;
+    constexpr int EPI = TILE > RED ? TILE : RED;            // the reduction reuses the tile's LDS
     constexpr int KLOOP = NBUF * (BM + BN) * BK * 2;
     constexpr int LDS = KLOOP > EPI ? KLOOP : EPI;
     static_assert(NBUF == 2 || NBUF == 1, "one or two K stages");
     static_assert(NBUF == 1 || EPI <= KLOOP, "epilogue staging must fit the k-loop LDS");
-    if (NBUF == 1 && K != BK) return -1;
-    auto k = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, NBUF == 1 ? 3 : 2>;
-    static int attr = set_lds(k, LDS);
+    constexpr int PER_CU = (160 * 1024) / LDS;
+    // blocks per CU the registers are asked to allow: the forward epilogue fits 4 without spilling, the
+    // data-gradient one (prefetched D / x / masks) needs ~178 VGPRs (3 blocks spill 35)
+    constexpr int CAP_F = CONV && BN == 64 ? 3 : 4;        // the 256x64 conv staging spills 7 VGPRs at 4
+    constexpr int MIN_F = NBUF == 1 ? (PER_CU < CAP_F ? PER_CU : CAP_F) : 2, MIN_B = 2;
+    auto kf = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_F, NBUF, false>;
+    auto kb = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_B, NBUF, true>;
+    static int attr = set_lds(kf, LDS) | set_lds(kb, LDS);
     if (attr) return attr;
+    const bool bwd = D != nullptr || bnr.part != nullptr;
+    if (bwd && stats != nullptr) return -1;
+    auto k = bwd ? kb : kf;
     const int nwg = ((M + BM - 1) / BM) * (N / BN);
     hipLaunchKernelGGL(k, dim3(nwg), dim3(NTHREADS), LDS, s, (const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N,
                        K, lda, ldb, ldc, (const __bf16*)zero, stats, geo, (const __bf16*)D, ldd, bnr, dmask);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-bool g_nt_single_stage = true;
+// Single-buffer NT GEMM (NBUF = 1) or double-buffered.  The single-buffer forward-epilogue kernels run 4 blocks
+// per CU, which hides staging better than double buffering at 2 -- when the grid has the blocks to fill them
+// (>= 3 per CU: measured on the ResNet-50 shapes, scripts/ab_modes.sh); the data-gradient epilogue needs 2x the
+// registers, so there the single buffer only pays when K == BK (nothing to double-buffer).  Modes (A/B knob):
+// 0 never, 1 K == BK only (plain GEMMs), 2 every plain GEMM, 3 every GEMM, 4 (default) the rule above.
+int g_nt_single_stage = 4;
+
+inline bool nt_single(bool bwd, bool conv, int K, int nwg) {
+    switch (g_nt_single_stage) {
+        case 0: return false;
+        case 1: return !conv && K == BK;
+        case 2: return !conv;
+        case 3: return true;
+        default: return (!bwd && nwg >= 768) || (!conv && K == BK);
+    }
+}
 
 // m-slicing of the weight-gradient GEMM
 struct TnPlan { int kchunk, slices, groups, per_group, blocks; };
@@ -723,16 +760,20 @@ int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int 
     if (bnr != nullptr && (ldc != N || bnr->part == nullptr)) return -1;
     const BnBwd b = bnr != nullptr ? *bnr : BnBwd{};
     hipStream_t s = (hipStream_t)stream;
-    const bool one = K == BK && g_nt_single_stage;
-    if (N % 128 == 0)
+    const bool bwd = D != nullptr || bnr != nullptr;
+    if (N % 128 == 0) {
+        const bool one = nt_single(bwd, false, K, ((M + 127) / 128) * (N / 128));
         return one ? launch_nt<128, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b,
                                                          dmask)
                    : launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
-    return launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
+    }
+    const bool one = nt_single(bwd, false, K, ((M + 255) / 256) * (N / 64));
+    return one ? launch_nt<256, 64, 4, 1, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask)
+               : launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
 }
 
-// A/B knob: single-stage (3 blocks per CU) instantiation for K == 64
-void plx_set_nt_single_stage(int on) { g_nt_single_stage = on != 0; }
+// A/B knob: single-buffer NT GEMM mode (see nt_single)
+void plx_set_nt_single_stage(int mode) { g_nt_single_stage = mode; }
 
 // weight-gradient slicing knobs; workspace sizes follow them, so set before sizing / launching
 void plx_set_tn_plan(int blocks_per_cu, int slab_mb) {
@@ -866,10 +907,10 @@ inline ConvGeom fwd_geom(int H, int W, int C, int K, int S) {
     return finish_geom(g);
 }
 
-template <int BM_, int BN_, int WGM_, int WGN_>
+template <int BM_, int BN_, int WGM_, int WGN_, int NBUF_>
 int nt_conv(const void* A, const void* B, void* C, int M, int N, const ConvGeom& g, int ldb, int ldc,
             const void* zero, float* stats, hipStream_t s, const void* D, const BnBwd& bnr) {
-    return launch_nt<BM_, BN_, WGM_, WGN_, true>(A, B, C, M, N, g.ntaps * g.C, g.C, ldb, ldc, zero, stats, s, g, D,
+    return launch_nt<BM_, BN_, WGM_, WGN_, true, NBUF_>(A, B, C, M, N, g.ntaps * g.C, g.C, ldb, ldc, zero, stats, s, g, D,
                                                  D != nullptr ? ldc : 0, bnr);
 }
 
@@ -877,8 +918,15 @@ inline int nt_rows_per_block(int N) { return N % 128 == 0 ? 128 : 256; }
 
 int nt_conv_any(const void* A, const void* B, void* C, int M, int N, const ConvGeom& g, int ldb, int ldc,
                 const void* zero, float* stats, hipStream_t s, const void* D = nullptr, const BnBwd& bnr = {}) {
-    if (N % 128 == 0) return nt_conv<128, 128, 2, 2>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
-    return nt_conv<256, 64, 4, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
+    const bool bwd = D != nullptr || bnr.part != nullptr;
+    const int K = g.ntaps * g.C;
+    if (N % 128 == 0)
+        return nt_single(bwd, true, K, ((M + 127) / 128) * (N / 128))
+                   ? nt_conv<128, 128, 2, 2, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr)
+                   : nt_conv<128, 128, 2, 2, 2>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
+    return nt_single(bwd, true, K, ((M + 255) / 256) * (N / 64))
+               ? nt_conv<256, 64, 4, 1, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr)
+               : nt_conv<256, 64, 4, 1, 2>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
 }
 
 // the GEMMs of a data gradient: (row grid geometry, ntaps) per launch; S == 2 gives one per parity class

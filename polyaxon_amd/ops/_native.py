@@ -130,8 +130,8 @@ def lib(name: str) -> ctypes.CDLL:
             build(name, force=os.environ.get("PLX_NATIVE_REBUILD") == "1")
         handle = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
         _declare(name, handle)
-        if name == "plx_conv" and os.environ.get("PLX_NT_SINGLE_STAGE") == "0":  # A/B knob
-            handle.plx_set_nt_single_stage(0)
+        if name == "plx_conv" and os.environ.get("PLX_NT_SINGLE_STAGE"):  # A/B knob (csrc/conv_gemm.hip)
+            handle.plx_set_nt_single_stage(int(os.environ["PLX_NT_SINGLE_STAGE"]))
         _loaded[name] = handle
         return handle
 
