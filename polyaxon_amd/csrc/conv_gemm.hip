@@ -309,6 +309,25 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         if constexpr (CONV) orow[it] = (int)out_row(geo, gm);
         else orow[it] = gm;
     }
+    auto tile_to_lds = [&]() {
+#pragma unroll
+        for (int rm = 0; rm < RM; ++rm) {
+            const int ml = wm * WTM + rm * 16 + fr;
+#pragma unroll
+            for (int rn = 0; rn < RN; ++rn) {
+                const int nl = wn * WTN + rn * 16 + fq * 4;
+                const f32x4 v = acc[rn][rm];
+                uint2 packed;
+                packed.x = pack_bf16x2(v[0], v[1]);
+                packed.y = pack_bf16x2(v[2], v[3]);
+                *(uint2*)(smem + ml * CROW + nl * 2) = packed;
+            }
+        }
+    };
+    // LATE: the single-buffer data-gradient kernel parks the accumulators in LDS BEFORE it issues the epilogue
+    // loads, so they do not hold 64 VGPRs through the loads' latency (other resident blocks hide it instead)
+    constexpr bool LATE = BWD && NBUF == 1;
+    if constexpr (LATE) tile_to_lds();
     uint4 dpre[ITERS], xpre[ITERS];
     uint32_t mpre[ITERS], dmpre[ITERS];
     if (d_on) {
@@ -343,19 +362,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
             is[k] = bnr.invstd[ch0 + k];
         }
     }
-#pragma unroll
-    for (int rm = 0; rm < RM; ++rm) {
-        const int ml = wm * WTM + rm * 16 + fr;
-#pragma unroll
-        for (int rn = 0; rn < RN; ++rn) {
-            const int nl = wn * WTN + rn * 16 + fq * 4;
-            const f32x4 v = acc[rn][rm];
-            uint2 packed;
-            packed.x = pack_bf16x2(v[0], v[1]);
-            packed.y = pack_bf16x2(v[2], v[3]);
-            *(uint2*)(smem + ml * CROW + nl * 2) = packed;
-        }
-    }
+    if constexpr (!LATE) tile_to_lds();
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
@@ -654,10 +661,11 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
     static_assert(NBUF == 2 || NBUF == 1, "one or two K stages");
     static_assert(NBUF == 1 || EPI <= KLOOP, "epilogue staging must fit the k-loop LDS");
     constexpr int PER_CU = (160 * 1024) / LDS;
-    // blocks per CU the registers are asked to allow: the forward epilogue fits 4 without spilling, the
-    // data-gradient one (prefetched D / x / masks) needs ~178 VGPRs (3 blocks spill 35)
-    constexpr int CAP_F = CONV && BN == 64 ? 3 : 4;        // the 256x64 conv staging spills 7 VGPRs at 4
-    constexpr int MIN_F = NBUF == 1 ? (PER_CU < CAP_F ? PER_CU : CAP_F) : 2, MIN_B = 2;
+    // blocks per CU the registers are asked to allow (128 VGPRs at 4): the double-buffered data-gradient kernel
+    // keeps its accumulators live through the epilogue prefetch (~178 VGPRs), the single-buffer one parks them in
+    // LDS first (LATE in gemm_nt_kernel)
+    constexpr int CAP = CONV && BN == 64 ? 3 : 4;          // the 256x64 conv staging spills 7-8 VGPRs at 4
+    constexpr int MIN_F = NBUF == 1 ? (PER_CU < CAP ? PER_CU : CAP) : 2, MIN_B = MIN_F;
     auto kf = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_F, NBUF, false>;
     auto kb = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_B, NBUF, true>;
     static int attr = set_lds(kf, LDS) | set_lds(kb, LDS);
@@ -671,12 +679,12 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-// Single-buffer NT GEMM (NBUF = 1) or double-buffered.  The single-buffer forward-epilogue kernels run 4 blocks
-// per CU, which hides staging better than double buffering at 2 -- when the grid has the blocks to fill them
-// (>= 3 per CU: measured on the ResNet-50 shapes, scripts/ab_modes.sh); the data-gradient epilogue needs 2x the
-// registers, so there the single buffer only pays when K == BK (nothing to double-buffer).  Modes (A/B knob):
-// 0 never, 1 K == BK only (plain GEMMs), 2 every plain GEMM, 3 every GEMM, 4 (default) the rule above.
-int g_nt_single_stage = 4;
+// Single-buffer NT GEMM (NBUF = 1) or double-buffered.  The single-buffer kernels run 4 blocks per CU (3 for the
+// 256x64 conv tile), which hides the staging better than double buffering at 2 blocks -- when the grid has the
+// blocks to fill them (>= 3 per CU), or when K == BK leaves nothing to double-buffer.  Measured on the ResNet-50
+// shapes (scripts/ab_modes.sh, profiles/r2_nt_single_buffer_ab.md).  Modes (A/B knob): 0 never, 1 K == BK only
+// (plain GEMMs), 2 every plain GEMM, 3 every GEMM, 4 forward-epilogue GEMMs by the rule, 5 (default) the rule.
+int g_nt_single_stage = 5;
 
 inline bool nt_single(bool bwd, bool conv, int K, int nwg) {
     switch (g_nt_single_stage) {
@@ -684,6 +692,7 @@ inline bool nt_single(bool bwd, bool conv, int K, int nwg) {
         case 1: return !conv && K == BK;
         case 2: return !conv;
         case 3: return true;
+        case 5: return nwg >= 768 || (!conv && K == BK);
         default: return (!bwd && nwg >= 768) || (!conv && K == BK);
     }
 }
