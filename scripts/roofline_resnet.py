@@ -30,7 +30,10 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--md", default="")
     ap.add_argument("--only", default="", help="comma-separated substrings: time only matching layers")
-    ap.add_argument("--nt-single-stage", type=int, default=1, help="A/B knob: 3-blocks/CU NT GEMM for K == 64")
+    ap.add_argument("--bn-apply-only", type=int, default=0, help="also time the apply pass alone")
+    ap.add_argument("--bn-counters", type=int, default=1, help="A/B knob: 1 = fused BN reduce+finalize (ticket "
+                    "counters), 0 = the two-launch path")
+    ap.add_argument("--nt-single-stage", type=int, default=5, help="A/B knob: NT GEMM single-buffer mode (conv_gemm.hip nt_single)")
     a = ap.parse_args()
     import torch
 
@@ -45,6 +48,7 @@ def main() -> None:
     zero = _zero_page(dev).data_ptr()
     st = torch.cuda.current_stream().cuda_stream
     cnt = torch.zeros(64, dtype=torch.int32, device=dev)  # BatchNorm reduce + finalize tickets
+    cptr = cnt.data_ptr() if a.bn_counters else None
     bf = dict(dtype=torch.bfloat16, device=dev)
     f32 = dict(dtype=torch.float32, device=dev)
     rows = []
@@ -164,9 +168,13 @@ def main() -> None:
             x.data_ptr(), r.data_ptr() if r is not None else None, y.data_ptr(), m, c, weight.data_ptr(),
             bias.data_ptr(), 1e-5, 0.1, rm.data_ptr(), rv.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(),
             stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(),
-            mo.data_ptr() if mo is not None else None, int(relu), None, cnt.data_ptr(), st)
+            mo.data_ptr() if mo is not None else None, int(relu), None, cptr, st)
         nbytes = 2.0 * m * c * (2 + (1 if res else 0)) + (m * c / 8 if relu else 0)
         emit(name, "bn_fwd", count, timeit(fwd), nbytes, 0.0)
+        if a.bn_apply_only:
+            app = lambda: bn.plx_bn_apply(x.data_ptr(), r.data_ptr() if r is not None else None, y.data_ptr(), m, c,  # noqa
+                                          stats[2 * c:].data_ptr(), int(relu), st)
+            emit(name, "bn_apply", count, timeit(app), nbytes, 0.0)
         dy = rnd((m, c))
         dx = torch.empty(m, c, **bf)
         dres = torch.empty(m, c, **bf) if res else None
@@ -176,13 +184,13 @@ def main() -> None:
             bwd = lambda: bn.plx_bn_backward_from_partials(  # noqa
                 x.data_ptr(), mp, dy.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else None, m, c,
                 weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), dg.data_ptr(), db.data_ptr(), coef.data_ptr(),
-                part.data_ptr(), nblk, l2.data_ptr(), int(relu), 1, None, cnt.data_ptr(), st)
+                part.data_ptr(), nblk, l2.data_ptr(), int(relu), 1, None, cptr, st)
         else:
             pw = torch.empty(int(bn.plx_bn_workspace(m, c)), **f32)
             bwd = lambda: bn.plx_bn_backward(  # noqa
                 x.data_ptr(), mp, dy.data_ptr(), dx.data_ptr(), dres.data_ptr() if dres is not None else None, m, c,
                 weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), dg.data_ptr(), db.data_ptr(), coef.data_ptr(),
-                pw.data_ptr(), int(relu), 1, None, cnt.data_ptr(), st)
+                pw.data_ptr(), int(relu), 1, None, cptr, st)
         nbytes = 2.0 * m * c * (3 + (1 if res else 0)) + (m * c / 8 if relu else 0)
         emit(name, "bn_bwd" + ("" if partials_bwd else "+reduce"), count, timeit(bwd), nbytes, 0.0)
 
