@@ -323,11 +323,15 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
 }
 
 // ------------------------------------------------------------------------------- forward apply
+// RES / RELU are compile-time: with a runtime residual test hipcc waited for x's load before issuing the residual's
+// (one extra HBM round trip per trip), and a per-element `rsb ? rsb[c] : 1` in the prologue became eight
+// load-then-wait branches (cdna_hip_programming.md §5 item 4(c)) -- ~20 us of latency per block that dominated the
+// 14x14 / 7x7 layers (35 us for a 53 MB apply, profiles/r2_resnet50_roofline.md).
+template <bool RES, bool RELU>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const bf16x8* __restrict__ x, const bf16x8* __restrict__ res,
                                                           bf16x8* __restrict__ y, const float* __restrict__ scale,
                                                           const float* __restrict__ bias, int64_t n_vec, int G,
-                                                          int relu, uint8_t* __restrict__ mask,
-                                                          const float* __restrict__ rsb) {
+                                                          uint8_t* __restrict__ mask, const float* __restrict__ rsb) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // multiple of G (G | 256 or G % 256 == 0 handled by host)
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_vec) return;
@@ -337,28 +341,35 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const bf16x8* __restri
   for (int k = 0; k < 8; ++k) {
     a[k] = scale[cg * 8 + k];
     b[k] = bias[cg * 8 + k];
-    // rsb: the residual is the raw input of a BatchNorm (no activation) whose apply pass is deferred to here:
-    // res' = res * rsb[c] + rsb[C + c]  (a ResNet downsampling branch feeds only this add)
-    ra[k] = rsb != nullptr ? rsb[cg * 8 + k] : 1.f;
-    rb[k] = rsb != nullptr ? rsb[G * 8 + cg * 8 + k] : 0.f;
+    ra[k] = 1.f;
+    rb[k] = 0.f;
+  }
+  // rsb: the residual is the raw input of a BatchNorm (no activation) whose apply pass is deferred to here:
+  // res' = res * rsb[c] + rsb[C + c]  (a ResNet downsampling branch feeds only this add)
+  if (RES && rsb != nullptr) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ra[k] = rsb[cg * 8 + k];
+      rb[k] = rsb[G * 8 + cg * 8 + k];
+    }
   }
   for (; i < n_vec; i += stride) {
+    const bf16x8 xv = x[i];
+    bf16x8 rv;
+    if constexpr (RES) rv = res[i];
     float v[8];
-    load8(x + i, v);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], a[k], b[k]);
-    if (res != nullptr) {
-      float r[8];
-      load8(res + i, r);
+    for (int k = 0; k < 8; ++k) v[k] = fmaf(bf2f(xv.v[k]), a[k], b[k]);
+    if constexpr (RES) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] += fmaf(r[k], ra[k], rb[k]);
+      for (int k = 0; k < 8; ++k) v[k] += fmaf(bf2f(rv.v[k]), ra[k], rb[k]);
     }
-    if (relu) {
+    if constexpr (RELU) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
     }
     store8(y + i, v);
-    if (mask != nullptr) {
+    if (RELU && mask != nullptr) {
       // ReLU mask, 1 bit per element (bit k of byte i = channel 8*cg+k of vector i): the backward reads this
       // 1/16-size tensor instead of y (a positive float stays positive after bf16 rounding, so bit == y > 0).
       uint32_t bits = 0;
@@ -370,6 +381,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const bf16x8* __restri
 }
 
 // ------------------------------------------------------------------------------- backward reduce
+template <bool RELU>  // compile-time, so the mask load issues with the x / dy loads (see bn_apply_kernel)
 __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const bf16x8* __restrict__ x, const uint8_t* __restrict__ mask,
                                                                const bf16x8* __restrict__ dy, int64_t M, int G, int Gb,
                                                                int64_t rows_per_block, const float* __restrict__ mean,
@@ -395,10 +407,11 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const bf16x8* __r
   for (int64_t r = r0 + rlane; r < r1; r += R) {
     const int64_t off = r * G + cg;
     float xv[8], g[8];
+    uint32_t mb = 0xffu;
+    if constexpr (RELU) mb = mask[off];
     load8(x + off, xv);
     load8(dy + off, g);
-    if (relu) {
-      const uint32_t mb = mask[off];
+    if constexpr (RELU) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) g[k] = (mb >> k) & 1u ? g[k] : 0.f;
     }
@@ -466,7 +479,8 @@ struct ResBn {
 
 // RP: also reduce the residual BatchNorm's partials (ResBn).  A separate instantiation: its extra state
 // (90 VGPRs) would cut the plain pass from 8 to 5 waves per SIMD, and this memory-bound pass needs them.
-template <bool RP>
+// RMASK (RP only): the residual BatchNorm had a ReLU (rb.mask set) -- compile-time, no per-trip pointer test
+template <bool RP, bool RELU, bool RMASK = false>
 __global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restrict__ x, const uint8_t* __restrict__ mask,
                                                            const bf16x8* __restrict__ dy, bf16x8* __restrict__ dx,
                                                            bf16x8* __restrict__ dres, const float* __restrict__ coef,
@@ -489,10 +503,11 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restr
   }
   for (; i < n_vec; i += stride) {
     float xv[8], g[8];
+    uint32_t mb = 0xffu;
+    if constexpr (RELU) mb = mask[i];  // issued with the x / dy loads (RELU is compile-time)
     load8(x + i, xv);
     load8(dy + i, g);
-    if (relu) {
-      const uint32_t mb = mask[i];
+    if constexpr (RELU) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) g[k] = (mb >> k) & 1u ? g[k] : 0.f;
     }
@@ -500,7 +515,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_dx_kernel(const bf16x8* __restr
     if constexpr (rp) {
       float x2[8];
       load8(rb.x + i, x2);
-      const uint32_t m2 = rb.mask != nullptr ? rb.mask[i] : 0xffu;
+      const uint32_t m2 = RMASK ? rb.mask[i] : 0xffu;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float g2 = (m2 >> k) & 1u ? g[k] : 0.f;
@@ -580,12 +595,19 @@ inline int apply_grid(int64_t n_vec, int G) {
 inline void launch_dx(hipStream_t stream, int64_t n_vec, int G, const void* x, const uint8_t* mask, const void* dy,
                       void* dx, void* dres, const float* coef, int relu, const ResBn& rb) {
   const dim3 grid(apply_grid(n_vec, G));
-  if (rb.part != nullptr)
-    hipLaunchKernelGGL(bn_bwd_dx_kernel<true>, grid, dim3(kBlock), 0, stream, (const bf16x8*)x, mask,
-                       (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, G, relu, rb);
-  else
-    hipLaunchKernelGGL(bn_bwd_dx_kernel<false>, grid, dim3(kBlock), 0, stream, (const bf16x8*)x, mask,
-                       (const bf16x8*)dy, (bf16x8*)dx, (bf16x8*)dres, coef, n_vec, G, relu, rb);
+  auto k = rb.part == nullptr ? (relu ? bn_bwd_dx_kernel<false, true> : bn_bwd_dx_kernel<false, false>)
+           : rb.mask != nullptr ? (relu ? bn_bwd_dx_kernel<true, true, true> : bn_bwd_dx_kernel<true, false, true>)
+                                : (relu ? bn_bwd_dx_kernel<true, true> : bn_bwd_dx_kernel<true, false>);
+  hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, stream, (const bf16x8*)x, mask, (const bf16x8*)dy, (bf16x8*)dx,
+                     (bf16x8*)dres, coef, n_vec, G, relu, rb);
+}
+
+inline void launch_apply(hipStream_t stream, int64_t n_vec, int G, const void* x, const void* res, void* y,
+                         const float* scale, const float* bias, int relu, uint8_t* mask, const float* rsb) {
+  auto k = res != nullptr ? (relu ? bn_apply_kernel<true, true> : bn_apply_kernel<true, false>)
+                          : (relu ? bn_apply_kernel<false, true> : bn_apply_kernel<false, false>);
+  hipLaunchKernelGGL(k, dim3(apply_grid(n_vec, G)), dim3(kBlock), 0, stream, (const bf16x8*)x, (const bf16x8*)res,
+                     (bf16x8*)y, scale, bias, n_vec, G, mask, rsb);
 }
 
 // level-1 partials [2][nblk][C] -> finalize: one fused launch with a counter array (>= ceil(C/64) zeroed words),
@@ -617,6 +639,215 @@ inline void reduce_finalize_bwd(hipStream_t stream, const float* part, int nblk,
                      f.M, f.gamma, f.mean, f.invstd, f.dgamma, f.dbeta, f.coef, f.accumulate);
 }
 
+// ------------------------------------------------------------------------------- ResNet stem: BN + ReLU + max-pool
+// The stem's BatchNorm(+ReLU) output only feeds the 3x3/s2/p1 max-pool.  Forward: p = maxpool(bf16(relu(x*scale +
+// bias))) in one pass over x with the window position (0..8) of each max (first max in (kh, kw) order, the rule of
+// csrc/pool_kernels.hip), so the BatchNorm output (4x the pooled size) and its ReLU mask are never written or re-read.
+// Backward: every input pixel gathers dy from the <= 2x2 windows whose argmax it is (maxpool_bwd_kernel's gather, the
+// sum rounded to bf16 as that kernel stores it), masks it by the recomputed ReLU test (x*scale + bias > 0, the apply
+// pass's test bit for bit) and either reduces the BatchNorm partials (pass 1) or writes dx = A*dz + B*x + D (pass 2):
+// 2 passes over x instead of pool-bwd write + BN reduce + BN dx (3 reads and 2 writes of the 112x112 tensor).
+struct alignas(8) u8x8 {
+  uint8_t v[8];
+};
+
+__global__ __launch_bounds__(256) void stem_apply_pool_kernel(const bf16x8* __restrict__ x,
+                                                              const float* __restrict__ sb, bf16x8* __restrict__ y,
+                                                              u8x8* __restrict__ idx, int N, int H, int W, int G,
+                                                              int OH, int OW) {
+  const unsigned j = blockIdx.x * 256u + threadIdx.x;
+  if (j >= (unsigned)(OW * G)) return;
+  const unsigned g = j % (unsigned)G, ow = j / (unsigned)G;
+  const int C = G * 8;
+  float a[8], b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    a[k] = sb[g * 8 + k];
+    b[k] = sb[C + g * 8 + k];
+  }
+  for (int row = blockIdx.y; row < N * OH; row += gridDim.y) {
+    const int n = row / OH, oh = row - n * OH;
+    float best[8];
+    uint8_t arg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      best[k] = -INFINITY;
+      arg[k] = 255;
+    }
+    // all 9 window loads first, from clamped (always valid) addresses; out-of-image taps are skipped in the max
+    // (a branch around each load made hipcc wait for every load before issuing the next)
+    uint4 q[9];
+    bool ok[9];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = oh * 2 - 1 + kh;
+      const int ihc = ih < 0 ? 0 : (ih >= H ? H - 1 : ih);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = (int)ow * 2 - 1 + kw;
+        const int iwc = iw < 0 ? 0 : (iw >= W ? W - 1 : iw);
+        ok[kh * 3 + kw] = ih >= 0 && ih < H && iw >= 0 && iw < W;
+        q[kh * 3 + kw] = *(const uint4*)(x + ((size_t)(n * H + ihc) * W + iwc) * G + g);
+      }
+    }
+#pragma unroll
+    for (int t9 = 0; t9 < 9; ++t9) {
+      const uint32_t qw[4] = {q[t9].x, q[t9].y, q[t9].z, q[t9].w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float xk = __uint_as_float((k & 1) ? (qw[k >> 1] & 0xffff0000u) : (qw[k >> 1] << 16));
+        const float f = bf2f(f2bf(fmaxf(fmaf(xk, a[k], b[k]), 0.f)));  // the apply pass's bf16 value
+        if (ok[t9] && (f > best[k] || arg[k] == 255)) {
+          best[k] = f;
+          arg[k] = (uint8_t)t9;
+        }
+      }
+    }
+    bf16x8 o;
+    u8x8 m;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o.v[k] = f2bf(best[k]);
+      m.v[k] = arg[k];
+    }
+    const size_t t = (size_t)row * OW * G + j;
+    y[t] = o;
+    idx[t] = m;
+  }
+}
+
+// input row / column i of a 3x3/s2/p1 pool is covered by output o = (i + 1 - k) / 2 for the taps k of matching parity
+__device__ __forceinline__ int stem_cover(int i, int O, int* o, int* k) {
+  int n = 0;
+  if (i & 1) {
+    if ((i + 1) >> 1 < O) { o[n] = (i + 1) >> 1; k[n++] = 0; }
+    o[n] = (i - 1) >> 1; k[n++] = 2;
+  } else if ((i >> 1) < O) {
+    o[n] = i >> 1; k[n++] = 1;
+  }
+  return n;
+}
+
+// One thread = 8 channels of a 2x2 quad of input pixels (2a + di, 2b + dj): row 2a is covered only by output row a
+// (tap kh = 1), row 2a + 1 by rows a (kh = 2) and a + 1 (kh = 0), likewise for columns, so the quad's gradient comes
+// from the 4 windows (a + p, b + q) -- one window load per input pixel instead of every pixel gathering all 4 windows
+// (a first per-pixel version ran 1.6x the unfused pool-bwd + BN-bwd time).  Grid (ceil(QW*G / 256), rows_y) over quad
+// rows (n, a); block (bx, by) walks quad rows by, by + rows_y, ...  DX = false: per-block partials
+// part[2][gridDim.x * gridDim.y][C] of sum dz and sum dz * xhat; DX = true: dx from coef = [A | B | D].
+template <bool DX>
+__global__ __launch_bounds__(256) void stem_pool_bn_bwd_kernel(const bf16x8* __restrict__ dy, const u8x8* __restrict__ idx,
+                                                               const bf16x8* __restrict__ x, const float* __restrict__ sb,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd,
+                                                               const float* __restrict__ coef, bf16x8* __restrict__ dx,
+                                                               float* __restrict__ part, int N, int H, int W, int G,
+                                                               int OH, int OW) {
+  const int QH = (H + 1) / 2, QW = (W + 1) / 2;
+  const unsigned j0 = blockIdx.x * 256u + threadIdx.x;
+  const bool active = j0 < (unsigned)(QW * G);
+  const unsigned j = active ? j0 : 0u;
+  const unsigned g = j % (unsigned)G;                     // == threadIdx.x % G (256 % G == 0)
+  const int qb = (int)(j / (unsigned)G);
+  const int C = G * 8;
+  float a[8], b[8], c1[8], c2[8], c3[8], s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    a[k] = sb[g * 8 + k];
+    b[k] = sb[C + g * 8 + k];
+    if constexpr (DX) {
+      c1[k] = coef[g * 8 + k];
+      c2[k] = coef[C + g * 8 + k];
+      c3[k] = coef[2 * C + g * 8 + k];
+    } else {
+      c1[k] = mean[g * 8 + k];
+      c2[k] = invstd[g * 8 + k];
+      c3[k] = 0.f;
+    }
+    s1[k] = s2[k] = 0.f;
+  }
+  for (int row = blockIdx.y; active && row < N * QH; row += gridDim.y) {
+    const int n = row / QH, qa = row - n * QH;
+    // windows (qa + p, qb + q) and the quad's pixels: whole-vector loads from clamped addresses, all issued before
+    // any use; validity is applied per element
+    uint2 am[4];
+    uint4 d[4], xq[4];
+    bool wv[4], pv[4];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int w4 = p * 2 + q, oh = qa + p, ow = qb + q;
+        wv[w4] = oh < OH && ow < OW;
+        const size_t off = ((size_t)(n * OH + (oh < OH ? oh : OH - 1)) * OW + (ow < OW ? ow : OW - 1)) * G + g;
+        am[w4] = *(const uint2*)(idx + off);
+        d[w4] = *(const uint4*)(dy + off);
+        const int ih = 2 * qa + p, iw = 2 * qb + q;         // quad pixel (di, dj) = (p, q)
+        pv[w4] = ih < H && iw < W;
+        xq[w4] = *(const uint4*)(x + ((size_t)(n * H + (ih < H ? ih : H - 1)) * W + (iw < W ? iw : W - 1)) * G + g);
+      }
+#pragma unroll
+    for (int di = 0; di < 2; ++di)
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj) {
+        const int e = di * 2 + dj;
+        const uint32_t xw[4] = {xq[e].x, xq[e].y, xq[e].z, xq[e].w};
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float acc = 0.f;
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int kh = di + 1 - 2 * p, kw = dj + 1 - 2 * q;   // this pixel's tap in window (p, q)
+              if (kh < 0 || kw < 0) continue;                      // compile-time
+              const int w4 = p * 2 + q;
+              const uint32_t ab = (k < 4 ? am[w4].x : am[w4].y) >> (8 * (k & 3)) & 0xffu;
+              const uint32_t dw = (k >> 1) == 0 ? d[w4].x : (k >> 1) == 1 ? d[w4].y : (k >> 1) == 2 ? d[w4].z : d[w4].w;
+              const float dv = __uint_as_float((k & 1) ? (dw & 0xffff0000u) : (dw << 16));
+              acc += (wv[w4] && ab == (uint32_t)(kh * 3 + kw)) ? dv : 0.f;
+            }
+          const float xf = __uint_as_float((k & 1) ? (xw[k >> 1] & 0xffff0000u) : (xw[k >> 1] << 16));
+          const float dz = (pv[e] && fmaf(xf, a[k], b[k]) > 0.f) ? bf2f(f2bf(acc)) : 0.f;
+          if constexpr (DX) {
+            o[k] = fmaf(c1[k], dz, fmaf(c2[k], xf, c3[k]));
+          } else {
+            s1[k] += dz;
+            s2[k] = fmaf(dz, (xf - c1[k]) * c2[k], s2[k]);
+          }
+        }
+        if constexpr (DX) {
+          if (pv[e]) store8(dx + ((size_t)(n * H + 2 * qa + di) * W + 2 * qb + dj) * G + g, o);
+        }
+      }
+  }
+  if constexpr (!DX) {
+    // the 256 / G threads of this block that share channel group g: fixed-order sum through LDS
+    __shared__ float red[256 * 17];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[threadIdx.x * 17 + k] = s1[k];
+      red[threadIdx.x * 17 + 8 + k] = s2[k];
+    }
+    __syncthreads();
+    const int nb = gridDim.x * gridDim.y, blk = blockIdx.y * gridDim.x + blockIdx.x;
+    for (int e = threadIdx.x; e < G * 16; e += 256) {     // e = (value v, group gg)
+      const int gg = e % G, v = e / G;
+      float sum = 0.f;
+      for (int r = gg; r < 256; r += G) sum += red[r * 17 + v];
+      const int c = gg * 8 + (v & 7);
+      part[((int64_t)(v < 8 ? 0 : nb) + blk) * C + c] = sum;
+    }
+  }
+}
+
+// over quad rows: pass 1 (partials) a few per block (rows_y <= 4096 keeps the level-1 partials ~8 MB at the stem's
+// shape), pass 2 (dx) one per block
+inline dim3 stem_bwd_grid(int N, int H, int W, int G, bool dx) {
+  const int rows = N * ((H + 1) / 2), cap = dx ? 65535 : 4096;
+  return dim3((((W + 1) / 2) * G + 255) / 256, rows < cap ? rows : cap);
+}
+
 }  // namespace
 
 // fp32 workspace the host must pass as `partials`: level-1 [2][nblk][C] + level-2 [2][S][C].
@@ -646,9 +877,7 @@ PLX_API int plx_bn_forward(const void* x, const void* res, void* y, int64_t M, i
                              save_mean, save_invstd, scale_bias, scale_bias + C});
   const int64_t n_vec = M * p.G;
   if (y != nullptr)  // y == nullptr: statistics and scale/bias only (the apply is deferred to the consumer)
-    hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                       (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu,
-                       relu ? mask : nullptr, res_sb);
+    launch_apply(stream, n_vec, p.G, x, res, y, scale_bias, scale_bias + C, relu, relu ? mask : nullptr, res_sb);
   return (int)hipGetLastError();
 }
 
@@ -673,9 +902,7 @@ PLX_API int plx_bn_forward_from_partials(const void* x, const void* res, void* y
                              save_invstd, scale_bias, scale_bias + C});
   const int64_t n_vec = M * p.G;
   if (y != nullptr)
-    hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                       (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu,
-                       relu ? mask : nullptr, res_sb);
+    launch_apply(stream, n_vec, p.G, x, res, y, scale_bias, scale_bias + C, relu, relu ? mask : nullptr, res_sb);
   return (int)hipGetLastError();
 }
 
@@ -684,8 +911,7 @@ PLX_API int plx_bn_apply(const void* x, const void* res, void* y, int64_t M, int
   Plan p;
   if (!plan_for(M, C, &p)) return 1;
   const int64_t n_vec = M * p.G;
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(apply_grid(n_vec, p.G)), dim3(kBlock), 0, stream, (const bf16x8*)x,
-                     (const bf16x8*)res, (bf16x8*)y, scale_bias, scale_bias + C, n_vec, p.G, relu, nullptr, nullptr);
+  launch_apply(stream, n_vec, p.G, x, res, y, scale_bias, scale_bias + C, relu, nullptr, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -708,7 +934,7 @@ PLX_API int plx_bn_backward(const void* x, const uint8_t* mask, const void* dy, 
   const ResBn rb = resbn != nullptr ? *resbn : ResBn{};
   float* pa = partials;
   float* pb = partials + (int64_t)p.nblk * C;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(p.nblk, p.gy), dim3(kBlock), 0, stream, (const bf16x8*)x,
+  hipLaunchKernelGGL(relu ? bn_bwd_reduce_kernel<true> : bn_bwd_reduce_kernel<false>, dim3(p.nblk, p.gy), dim3(kBlock), 0, stream, (const bf16x8*)x,
                      mask, (const bf16x8*)dy, M, p.G, p.Gb, p.rows_per_block, save_mean, save_invstd,
                      relu, pa, pb);
   float* l2 = partials + 2 * (int64_t)p.nblk * C;
@@ -735,5 +961,53 @@ PLX_API int plx_bn_backward_from_partials(const void* x, const uint8_t* mask, co
                       BwdFin{C, M, gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate});
   const int64_t n_vec = M * p.G;
   launch_dx(stream, n_vec, p.G, x, mask, dy, dx, dres, coef, relu, rb);
+  return (int)hipGetLastError();
+}
+
+// ---- ResNet stem BatchNorm + ReLU + 3x3/s2/p1 max-pool (see stem_apply_pool_kernel)
+// Forward: statistics (workspace `partials`: plx_bn_workspace(N*H*W, C) floats) -> mean / invstd / scale|bias ->
+// y [N][OH][OW][C] bf16 and idx [N*OH*OW*C] window positions.
+PLX_API int plx_stem_bn_pool_forward(const void* x, void* y, void* idx, int N, int H, int W, int C, const float* gamma,
+                                     const float* beta, float eps, float momentum, float* running_mean,
+                                     float* running_var, float* save_mean, float* save_invstd, float* scale_bias,
+                                     float* partials, unsigned* counters, hipStream_t stream) {
+  const int G = C / 8;
+  if (N <= 0 || H <= 0 || W <= 0 || C % 8 || G > 256 || 256 % G) return 1;
+  const int rc = plx_bn_forward(x, nullptr, nullptr, (int64_t)N * H * W, C, gamma, beta, eps, momentum, running_mean,
+                                running_var, save_mean, save_invstd, scale_bias, partials, nullptr, 1, nullptr,
+                                counters, stream);
+  if (rc) return rc;
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const int rows = N * OH;
+  hipLaunchKernelGGL(stem_apply_pool_kernel, dim3((OW * G + 255) / 256, rows < 65535 ? rows : 65535), dim3(256), 0,
+                     stream, (const bf16x8*)x, scale_bias, (bf16x8*)y, (u8x8*)idx, N, H, W, G, OH, OW);
+  return (int)hipGetLastError();
+}
+
+// floats of workspace plx_stem_bn_pool_backward needs: level-1 [2][nblk][C] + level-2 [2][S][C]
+PLX_API int64_t plx_stem_bn_pool_bwd_workspace(int N, int H, int W, int C) {
+  const dim3 g = stem_bwd_grid(N, H, W, C / 8, false);
+  const int64_t nblk = (int64_t)g.x * g.y;
+  return 2 * (nblk + (nblk + kRowsPerSplit - 1) / kRowsPerSplit) * C;
+}
+
+// dy: gradient of the pooled output; dx: gradient of the BatchNorm input x.  dgamma / dbeta (+)= with accumulate.
+PLX_API int plx_stem_bn_pool_backward(const void* dy, const void* idx, const void* x, void* dx, int N, int H, int W,
+                                      int C, const float* gamma, const float* save_mean, const float* save_invstd,
+                                      const float* scale_bias, float* dgamma, float* dbeta, float* coef,
+                                      float* workspace, int accumulate, unsigned* counters, hipStream_t stream) {
+  const int G = C / 8;
+  if (N <= 0 || H <= 0 || W <= 0 || C % 8 || G > 256 || 256 % G) return 1;
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const dim3 grid = stem_bwd_grid(N, H, W, G, false), grid_dx = stem_bwd_grid(N, H, W, G, true);
+  const int nblk = grid.x * grid.y;
+  hipLaunchKernelGGL(stem_pool_bn_bwd_kernel<false>, grid, dim3(256), 0, stream, (const bf16x8*)dy, (const u8x8*)idx,
+                     (const bf16x8*)x, scale_bias, save_mean, save_invstd, (const float*)nullptr, (bf16x8*)nullptr,
+                     workspace, N, H, W, G, OH, OW);
+  reduce_finalize_bwd(stream, workspace, nblk, workspace + 2 * (int64_t)nblk * C, counters,
+                      BwdFin{C, (int64_t)N * H * W, gamma, save_mean, save_invstd, dgamma, dbeta, coef, accumulate});
+  hipLaunchKernelGGL(stem_pool_bn_bwd_kernel<true>, grid_dx, dim3(256), 0, stream, (const bf16x8*)dy, (const u8x8*)idx,
+                     (const bf16x8*)x, scale_bias, save_mean, save_invstd, coef, (bf16x8*)dx, (float*)nullptr, N, H,
+                     W, G, OH, OW);
   return (int)hipGetLastError();
 }

@@ -18,6 +18,7 @@ from polyaxon_amd.ops.conv1x1 import Conv1x1, GradMailbox
 from polyaxon_amd.ops.conv import Conv3x3, ConvKxK
 from polyaxon_amd.ops.norm import BatchNormAct
 from polyaxon_amd.ops.pool import MaxPool3s2
+from polyaxon_amd.ops.stem import stem_bn_relu_pool
 
 
 class Bottleneck(nn.Module):
@@ -55,6 +56,7 @@ class Bottleneck(nn.Module):
 
 
 _DEFER_DOWN_BN = os.environ.get("PLX_DEFER_DOWN_BN", "1") != "0"  # A/B knob (scripts/ab_check.sh)
+_STEM_FUSED = os.environ.get("PLX_STEM_FUSED", "1") != "0"  # A/B knob: stem BN + ReLU + max-pool in one op
 
 
 class Downsample(nn.Module):
@@ -127,7 +129,9 @@ class ResNet(nn.Module):
                 mod.reset_running_stats()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.pool(self.stem_bn(self.stem(x)))
+        x = self.stem(x)
+        # BN + ReLU + max-pool fused (ops/stem.py): the 112x112 BatchNorm output is never materialised
+        x = stem_bn_relu_pool(x, self.stem_bn, self.pool) if _STEM_FUSED else self.pool(self.stem_bn(x))
         x = self.stages(x)
         x = torch.flatten(x.mean((2, 3)), 1) if x.is_contiguous() else x.mean((2, 3))
         return self.fc(x)

@@ -167,6 +167,9 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_bn_dx_blocks": [_L, _I],
         "plx_bn_backward_from_partials": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I, _P,
                                           _P, _P],
+        "plx_stem_bn_pool_forward": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P],
+        "plx_stem_bn_pool_bwd_workspace": [_I, _I, _I, _I],
+        "plx_stem_bn_pool_backward": [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     },
     "plx_procmon": {
         "plx_pm_create": [],
@@ -247,7 +250,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

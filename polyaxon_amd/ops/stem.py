@@ -1,0 +1,87 @@
+"""ResNet stem BatchNorm + ReLU + 3x3/s2/p1 max-pool as one op (csrc/bn_kernels.hip ``plx_stem_bn_pool_*``).
+
+Unfused, the stem's 112x112x64 activation is the largest tensor of the step and it makes six HBM round trips
+around the BatchNorm and the pool: stats read, apply read + write (+ ReLU mask), pool read, then in the backward
+pool-bwd write, BN reduce read (dy, x, mask) and BN dx read (dy, x, mask) + write — ≈1.2 ms of a bs-256 step
+(``profiles/r2_*``).  Fused:
+
+* forward: statistics pass (as before) → one pass that applies scale/bias + ReLU while max-pooling, writing only the
+  pooled tensor and a 1-byte window position per element;
+* backward: two passes over x that gather the pooled gradient through the window positions, recompute the ReLU
+  test, and reduce the BatchNorm partials (pass 1) / write dx (pass 2).
+
+Same numerics as the unfused ops (the apply pass's bf16 value is what is pooled, ties keep the first maximum, the
+gathered gradient is rounded to bf16 as the pool backward stores it); the GPU test compares the two paths.
+"""
+from __future__ import annotations
+
+import torch
+
+from polyaxon_amd.ops import _native
+from polyaxon_amd.ops.bn_fused import _cl, _counters, _stream
+from polyaxon_amd.ops.flat import direct_grad
+
+
+class _StemBNReLUPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
+        lib = _native.lib("plx_bn")
+        x = _cl(x)
+        n, c, h, w = x.shape
+        oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+        f32 = dict(dtype=torch.float32, device=x.device)
+        stats = torch.empty(4 * c, **f32)  # mean | invstd | scale | bias
+        ws = torch.empty(int(lib.plx_bn_workspace(n * h * w, c)), **f32)
+        y = torch.empty((n, c, oh, ow), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        idx = torch.empty(n * oh * ow * c, dtype=torch.uint8, device=x.device)
+        rc = lib.plx_stem_bn_pool_forward(
+            x.data_ptr(), y.data_ptr(), idx.data_ptr(), n, h, w, c, weight.data_ptr(), bias.data_ptr(), float(eps),
+            float(momentum), running_mean.data_ptr(), running_var.data_ptr(), stats.data_ptr(),
+            stats[c:].data_ptr(), stats[2 * c:].data_ptr(), ws.data_ptr(), _counters(x.device), _stream())
+        _native.check(rc, "plx_stem_bn_pool_forward")
+        ctx.save_for_backward(x, idx, weight, stats)
+        gw, gb = direct_grad(weight), direct_grad(bias)
+        ctx.direct = (gw, gb) if (gw is not None and gb is not None) else None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _native.lib("plx_bn")
+        x, idx, weight, stats = ctx.saved_tensors
+        n, c, h, w = x.shape
+        dy = _cl(dy)
+        if dy.dtype != torch.bfloat16:
+            dy = dy.to(torch.bfloat16)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        if ctx.direct is not None:
+            dg_ptr, db_ptr, acc, dgb = ctx.direct[0].data_ptr(), ctx.direct[1].data_ptr(), 1, None
+        else:
+            dgb = torch.empty(2 * c, **f32)
+            dg_ptr, db_ptr, acc = dgb.data_ptr(), dgb[c:].data_ptr(), 0
+        coef = torch.empty(3 * c, **f32)
+        ws = torch.empty(int(lib.plx_stem_bn_pool_bwd_workspace(n, h, w, c)), **f32)
+        rc = lib.plx_stem_bn_pool_backward(
+            dy.data_ptr(), idx.data_ptr(), x.data_ptr(), dx.data_ptr(), n, h, w, c, weight.data_ptr(),
+            stats.data_ptr(), stats[c:].data_ptr(), stats[2 * c:].data_ptr(), dg_ptr, db_ptr, coef.data_ptr(),
+            ws.data_ptr(), acc, _counters(x.device), _stream())
+        _native.check(rc, "plx_stem_bn_pool_backward")
+        dgamma = dgb[:c] if dgb is not None else None
+        dbeta = dgb[c:] if dgb is not None else None
+        return dx, dgamma, dbeta, None, None, None, None
+
+
+def supported(x: torch.Tensor, bn, pool) -> bool:
+    """Training-mode fused path: CUDA bf16 NHWC input, a fused ReLU BatchNorm with running stats, a native pool."""
+    c = x.shape[1] if x.dim() == 4 else 0
+    g = c // 8
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and c % 8 == 0 and 0 < g <= 256
+            and 256 % g == 0 and bn.training and bn.fused and bn.act and not bn.residual
+            and bn.running_mean is not None and getattr(pool, "native", False) and x.numel() > 0)
+
+
+def stem_bn_relu_pool(x: torch.Tensor, bn, pool) -> torch.Tensor:
+    """``pool(bn(x))`` for a ``BatchNormAct(act=True)`` and a ``MaxPool3s2``, fused when :func:`supported`."""
+    if supported(x, bn, pool):
+        return _StemBNReLUPool.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum, bn.eps)
+    return pool(bn(x))

@@ -54,16 +54,31 @@ def main() -> None:
     rows = []
 
     def timeit(fn):
-        for _ in range(3):
-            fn()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
+        """GPU time per call: ``a.reps`` calls captured in one hipGraph, replayed back to back (as in the training
+        step), so host launch latency never shows up in a small kernel's number; median of 5 replays."""
+        nonlocal st
+        base = st
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            st = s.cuda_stream
+            for _ in range(2):
+                fn()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(a.reps):
+                    fn()
+        st = base
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
         for e0, e1 in ev:
             e0.record()
-            fn()
+            g.replay()
             e1.record()
         torch.cuda.synchronize()
         ts = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
-        return ts[len(ts) // 2] * 1e3  # us
+        return ts[len(ts) // 2] * 1e3 / a.reps  # us
 
     def emit(layer, kind, count, us, nbytes, flops):
         roof = max(nbytes / HBM, flops / MFMA) * 1e6
@@ -194,7 +209,55 @@ def main() -> None:
         nbytes = 2.0 * m * c * (3 + (1 if res else 0)) + (m * c / 8 if relu else 0)
         emit(name, "bn_bwd" + ("" if partials_bwd else "+reduce"), count, timeit(bwd), nbytes, 0.0)
 
+    def stem_pool(name):
+        """stem BN + ReLU + max-pool: fused (ops/stem.py) vs BN (stats, apply + mask) followed by the pool."""
+        if not wanted(name):
+            return
+        n, c, h, w = a.bs, 64, 112, 112
+        m = n * h * w
+        pool = _native.lib("plx_pool")
+        x, mask, mean, invstd = bn_args(m, c)
+        weight, bias = torch.ones(c, **f32), torch.zeros(c, **f32)
+        rm, rv = torch.zeros(c, **f32), torch.ones(c, **f32)
+        stats = torch.empty(4 * c, **f32)
+        ws = torch.empty(int(bn.plx_bn_workspace(m, c)), **f32)
+        y = torch.empty(m, c, **bf)
+        p = torch.empty(n * 56 * 56, c, **bf)
+        idx = torch.empty(n * 56 * 56 * c, dtype=torch.uint8, device=dev)
+        ff = lambda: bn.plx_stem_bn_pool_forward(  # noqa
+            x.data_ptr(), p.data_ptr(), idx.data_ptr(), n, h, w, c, weight.data_ptr(), bias.data_ptr(), 1e-5, 0.1,
+            rm.data_ptr(), rv.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(), stats[2 * c:].data_ptr(),
+            ws.data_ptr(), cptr, st)
+
+        def fu():
+            bn.plx_bn_forward(x.data_ptr(), None, y.data_ptr(), m, c, weight.data_ptr(), bias.data_ptr(), 1e-5, 0.1,
+                              rm.data_ptr(), rv.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(),
+                              stats[2 * c:].data_ptr(), ws.data_ptr(), mask.data_ptr(), 1, None, cptr, st)
+            pool.plx_maxpool3s2_forward(y.data_ptr(), p.data_ptr(), idx.data_ptr(), n, h, w, c, st)
+        nbytes = 2.0 * m * c * 2 + 3.0 * n * 56 * 56 * c
+        emit(name + " fused", "fwd", 1, timeit(ff), nbytes, 0.0)
+        emit(name + " unfused", "fwd", 1, timeit(fu), nbytes, 0.0)
+        dp = rnd((n * 56 * 56, c))
+        dx = torch.empty(m, c, **bf)
+        dy1 = torch.empty(m, c, **bf)
+        dg, db, coef = torch.zeros(c, **f32), torch.zeros(c, **f32), torch.empty(3 * c, **f32)
+        wsb = torch.empty(int(bn.plx_stem_bn_pool_bwd_workspace(n, h, w, c)), **f32)
+        bf_ = lambda: bn.plx_stem_bn_pool_backward(  # noqa
+            dp.data_ptr(), idx.data_ptr(), x.data_ptr(), dx.data_ptr(), n, h, w, c, weight.data_ptr(),
+            mean.data_ptr(), invstd.data_ptr(), stats[2 * c:].data_ptr(), dg.data_ptr(), db.data_ptr(),
+            coef.data_ptr(), wsb.data_ptr(), 1, cptr, st)
+
+        def bu():
+            pool.plx_maxpool3s2_backward(dp.data_ptr(), idx.data_ptr(), dy1.data_ptr(), n, h, w, c, st)
+            bn.plx_bn_backward(x.data_ptr(), mask.data_ptr(), dy1.data_ptr(), dx.data_ptr(), None, m, c,
+                               weight.data_ptr(), mean.data_ptr(), invstd.data_ptr(), dg.data_ptr(), db.data_ptr(),
+                               coef.data_ptr(), ws.data_ptr(), 1, 1, None, cptr, st)
+        nbytes = 2.0 * m * c * 2 + 3.0 * n * 56 * 56 * c
+        emit(name + " fused", "bwd", 1, timeit(bf_), nbytes, 0.0)
+        emit(name + " unfused", "bwd", 1, timeit(bu), nbytes, 0.0)
+
     nb = a.bs
+    stem_pool("stem_pool 64@112")
     bn_layer("stem_bn 64@112", 1, nb * 112 * 112, 64, True, False, False)
     cfg = [(3, 64, 56, 1), (4, 128, 56, 2), (6, 256, 28, 2), (3, 512, 14, 2)]
     in_ch = 64

@@ -137,3 +137,52 @@ def test_reduce_finalize_one_launch_matches_two(cuda):
     p = part.view(2, nblk, c).double().sum(1)
     mean = p[0] / m
     torch.testing.assert_close(ref_f[:c].double(), mean, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 64, 15, 17), (2, 128, 9, 8), (2, 8, 6, 5)])
+def test_stem_bn_relu_pool_matches_unfused(cuda, shape):
+    """ops.stem: BN + ReLU + max-pool in one forward pass and two backward passes (csrc/bn_kernels.hip) gives the
+    unfused ops' pooled output (bit-exact: same bf16 values pooled, same ties), the same running stats and the same
+    dx / dgamma / dbeta, and both match an fp32 PyTorch reference of the composition."""
+    from polyaxon_amd.ops.norm import BatchNormAct
+    from polyaxon_amd.ops.pool import MaxPool3s2
+    from polyaxon_amd.ops.stem import stem_bn_relu_pool, supported
+
+    torch.manual_seed(0)
+    n, c, h, w = shape
+    x = (torch.randn(shape, device=cuda) * 2 + 0.3).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    g = torch.randn(n, c, oh, ow, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for fused in (True, False):
+        bn = BatchNormAct(c, act=True).to(cuda)
+        with torch.no_grad():
+            bn.weight.copy_(torch.linspace(0.5, 1.5, c))
+            bn.bias.copy_(torch.linspace(-0.2, 0.2, c))
+        pool = MaxPool3s2()
+        xa = x.clone().requires_grad_()
+        if fused:
+            assert supported(xa, bn, pool)
+            y = stem_bn_relu_pool(xa, bn, pool)
+        else:
+            y = pool(bn(xa))
+        y.backward(g)
+        outs.append((y.detach().float(), xa.grad.float(), bn.weight.grad.clone(), bn.bias.grad.clone(),
+                     bn.running_mean.clone(), bn.running_var.clone(), g))
+    (yf, dxf, dgf, dbf, rmf, rvf, gf), (yu, dxu, dgu, dbu, rmu, rvu, _) = outs
+    assert torch.equal(yf, yu)
+    torch.testing.assert_close(rmf, rmu)
+    torch.testing.assert_close(rvf, rvu)
+    scale = float(dxu.abs().max())
+    torch.testing.assert_close(dxf, dxu, rtol=2e-2, atol=2e-2 * scale)
+    torch.testing.assert_close(dgf, dgu, rtol=1e-3, atol=1e-3 * float(dgu.abs().max()))
+    torch.testing.assert_close(dbf, dbu, rtol=1e-3, atol=1e-3 * float(dbu.abs().max()))
+    # fp32 reference of the composition
+    xr = x.float().clone().requires_grad_()
+    wr = torch.linspace(0.5, 1.5, c, device=cuda).requires_grad_()
+    br = torch.linspace(-0.2, 0.2, c, device=cuda).requires_grad_()
+    yr = F.max_pool2d(F.relu(F.batch_norm(xr, None, None, wr, br, True, 0.1, 1e-5)), 3, 2, 1)
+    yr.backward(gf.float())
+    torch.testing.assert_close(yf, yr, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(dgf, wr.grad, rtol=5e-2, atol=5e-2 * float(wr.grad.abs().max()))
+    torch.testing.assert_close(dbf, br.grad, rtol=5e-2, atol=5e-2 * float(br.grad.abs().max()))
