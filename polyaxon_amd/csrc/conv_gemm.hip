@@ -706,8 +706,11 @@ inline void tn_tile(int N1, int N2, int& bn1, int& bn2) {
 }
 
 // slicing knobs (plx_set_tn_plan): target resident blocks per CU, cap on the fp32 slab bytes
-int g_tn_blocks_per_cu = 3;   // swept 1..12 x 8..256 MB on MI355X (scripts/diag_wgrad_plan.py): 3 / 32 MB best
-long g_tn_slab_bytes = 32l << 20;
+// Swept in isolation (scripts/diag_wgrad_plan.py) 3 / 32 MB was best; in the training step the weight gradients run on
+// the side stream beside the data-gradient chain, and there 1 / 16 MB (fewer slices: less slab traffic competing with
+// the main stream) gave +0.8-1.3 % step throughput (interleaved bench runs, PLX_TN_PLAN)
+int g_tn_blocks_per_cu = 1;
+long g_tn_slab_bytes = 16l << 20;
 
 inline TnPlan tn_plan(int M, int N1, int N2, int num_cus) {
     int bn1, bn2;

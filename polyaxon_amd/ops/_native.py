@@ -132,6 +132,9 @@ def lib(name: str) -> ctypes.CDLL:
         _declare(name, handle)
         if name == "plx_conv" and os.environ.get("PLX_NT_SINGLE_STAGE"):  # A/B knob (csrc/conv_gemm.hip)
             handle.plx_set_nt_single_stage(int(os.environ["PLX_NT_SINGLE_STAGE"]))
+        if name == "plx_conv" and os.environ.get("PLX_TN_PLAN"):  # A/B knob: "blocks_per_cu,slab_mb"
+            bpc, mb = (int(v) for v in os.environ["PLX_TN_PLAN"].split(","))
+            handle.plx_set_tn_plan(bpc, mb)
         _loaded[name] = handle
         return handle
 
