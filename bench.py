@@ -54,6 +54,7 @@ def _args(argv=None):
     ap.add_argument("--target", type=float, default=1.0, help="loss target for wall-clock-to-target")
     ap.add_argument("--signal", type=float, default=0.5, help="class-pattern amplitude of the synthetic data")
     ap.add_argument("--max-active", type=int, default=8, help="brackets one executor interleaves")
+    ap.add_argument("--graph", type=int, default=0, help="replay each training step as a captured hipGraph")
     ap.add_argument("--cpu", action="store_true", help="CPU rehearsal (gloo, small ResNet, tiny images)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -238,7 +239,8 @@ def main() -> int:
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         program = "resnet50"
-        params = {"batch": args.batch, "image": args.image, "unit_steps": args.unit_steps, "signal": args.signal}
+        params = {"batch": args.batch, "image": args.image, "unit_steps": args.unit_steps, "signal": args.signal,
+                  "graph": bool(args.graph)}
     if world > 1:
         if dev.type == "cuda":
             dist.init_process_group("nccl", device_id=dev)

@@ -22,6 +22,41 @@ def _stream_ptr(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+class _PinnedRing:
+    """Preallocated pinned staging slots for the per-trial hyper-parameter H2D copies.  ``tensor.pin_memory()``
+    per call went through the caching host allocator, which allocates fresh pinned memory (a synchronising
+    hipHostMalloc) while earlier copies are still queued -- with the host running trials ahead of the GPU that
+    stalled it, and the GPU then idled at every trial start waiting for the host's next launches.  A slot is
+    reused only after the event recorded behind its copy has completed (it nearly always has: 64 trials later)."""
+
+    def __init__(self, slots: int = 64, width: int = 8):
+        self.buf = torch.zeros(slots, width, dtype=torch.float32).pin_memory()
+        self.events = [None] * slots
+        self.i = 0
+
+    def copy_to(self, dst: torch.Tensor, values) -> None:
+        i = self.i
+        self.i = (i + 1) % len(self.events)
+        ev = self.events[i]
+        if ev is not None:
+            ev.synchronize()
+        self.buf[i, : len(values)] = torch.tensor(values, dtype=torch.float32)
+        dst.copy_(self.buf[i, : dst.numel()], non_blocking=True)
+        ev = self.events[i] or torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dst.device))
+        self.events[i] = ev
+
+
+def _set_hp(opt, values) -> None:
+    if not opt.hp.is_cuda:
+        opt.hp.copy_(torch.tensor(values, dtype=torch.float32))
+        return
+    ring = getattr(opt, "_ring", None)
+    if ring is None:
+        ring = opt._ring = _PinnedRing(width=opt.hp.numel())
+    ring.copy_to(opt.hp, values)
+
+
 class FusedSGD:
     """SGD with momentum / nesterov / dampening and weight decay on the decay segment only."""
 
@@ -45,8 +80,7 @@ class FusedSGD:
                 raise KeyError(f"unknown SGD hyper-parameter {k!r}")
             vals[k] = float(v)
         self._hp_host = vals
-        host = torch.tensor([vals[k] for k in self.HP] + [0.0] * (8 - len(self.HP)), dtype=torch.float32)
-        self.hp.copy_(host.pin_memory() if self.hp.is_cuda else host, non_blocking=self.hp.is_cuda)
+        _set_hp(self, [vals[k] for k in self.HP] + [0.0] * (8 - len(self.HP)))
 
     def reset_state(self) -> None:
         if self.flat.params.is_cuda:
@@ -106,8 +140,7 @@ class FusedAdamW:
                 raise KeyError(f"unknown AdamW hyper-parameter {k!r}")
             vals[k] = float(v)
         self._hp_host = vals
-        host = torch.tensor([vals[k] for k in self.HP] + [0.0] * (8 - len(self.HP)), dtype=torch.float32)
-        self.hp.copy_(host.pin_memory() if self.hp.is_cuda else host, non_blocking=self.hp.is_cuda)
+        _set_hp(self, [vals[k] for k in self.HP] + [0.0] * (8 - len(self.HP)))
 
     def reset_state(self) -> None:
         self.exp_avg.zero_()

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--marker", default="sgd_flat_kernel")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--markdown", action="store_true")
+    ap.add_argument("--context", type=int, default=1, help="list the kernels around the last step's largest gap")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -92,6 +93,29 @@ def main():
                f"{sum(g[0] for g in big) / n_steps / 1e6:.3f} ms/step)")
     for g, before, after in idle[:8]:
         out.append(f"- idle {g / 1e3:.1f} us after `{before[:60]}` before `{after[:60]}`")
+    # kernel sequence around the largest idle gap inside one step (offsets from the step's first kernel)
+    if a.context and big:
+        step_rows = rows[marks[-2] + 1: marks[-1] + 1]
+        t_s = int(step_rows[0]["Start_Timestamp"])
+        ks = sorted(step_rows, key=lambda r: int(r["Start_Timestamp"]))
+        worst, wi = 0, None
+        for i in range(1, len(ks)):
+            g = int(ks[i]["Start_Timestamp"]) - max(int(k["End_Timestamp"]) for k in ks[:i])
+            if g > worst:
+                worst, wi = g, i
+        out.append("")
+        run_end = 0
+        for i, k in enumerate(ks):
+            if i and int(k["Start_Timestamp"]) - run_end > 20_000:
+                p_ = ks[i - 1]
+                out.append(f"- step gap {(int(k['Start_Timestamp']) - run_end) / 1e3:.1f} us at +"
+                           f"{(run_end - t_s) / 1e3:.1f}: `{p_['Kernel_Name'][:50]}` (stream {p_.get(skey, '?')}) -> "
+                           f"`{k['Kernel_Name'][:50]}` (stream {k.get(skey, '?')})")
+            run_end = max(run_end, int(k["End_Timestamp"]))
+        out.append(f"last step: largest idle {worst / 1e3:.1f} us before kernel #{wi}; neighbourhood:")
+        for k in ks[max(0, (wi or 0) - 6): (wi or 0) + 4]:
+            out.append(f"- +{(int(k['Start_Timestamp']) - t_s) / 1e3:9.1f} .. +{(int(k['End_Timestamp']) - t_s) / 1e3:9.1f} us"
+                       f"  stream {k.get(skey, '?') if skey else '?'}  `{k['Kernel_Name'][:70]}`")
     if skey is not None:
         streams = collections.defaultdict(list)
         for r in win:
