@@ -145,18 +145,25 @@ __device__ __forceinline__ bool fin_sum2(const float* __restrict__ pa, const flo
   __shared__ double sh[2][kFinSplit][64];
   const int lc = threadIdx.x & 63, sp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lc;
-  double a0 = 0.0, b0 = 0.0, a1 = 0.0, b1 = 0.0;
+  double a0 = 0.0, b0 = 0.0;
   if (c < C) {
+    // 8 rows (16 loads) in flight per batch: this runs in the last-arriving block, on the critical path of every
+    // BatchNorm, and two rows per trip left it a chain of ~12 dependent L2 round trips at S ~ 100
     int b = sp;
-    for (; b + kFinSplit < nblk; b += 2 * kFinSplit) {
-      const float x0 = pa[(int64_t)b * C + c], y0 = pb[(int64_t)b * C + c];
-      const float x1 = pa[(int64_t)(b + kFinSplit) * C + c], y1 = pb[(int64_t)(b + kFinSplit) * C + c];
-      a0 += x0; b0 += y0; a1 += x1; b1 += y1;
+    for (; b + 7 * kFinSplit < nblk; b += 8 * kFinSplit) {
+      float x[8], y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        x[u] = pa[(int64_t)(b + u * kFinSplit) * C + c];
+        y[u] = pb[(int64_t)(b + u * kFinSplit) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { a0 += x[u]; b0 += y[u]; }
     }
-    if (b < nblk) { a0 += pa[(int64_t)b * C + c]; b0 += pb[(int64_t)b * C + c]; }
+    for (; b < nblk; b += kFinSplit) { a0 += pa[(int64_t)b * C + c]; b0 += pb[(int64_t)b * C + c]; }
   }
-  sh[0][sp][lc] = a0 + a1;
-  sh[1][sp][lc] = b0 + b1;
+  sh[0][sp][lc] = a0;
+  sh[1][sp][lc] = b0;
   __syncthreads();
   if (sp != 0 || c >= C) return false;
   A = ((sh[0][0][lc] + sh[0][1][lc]) + sh[0][2][lc]) + sh[0][3][lc];
@@ -251,8 +258,18 @@ __device__ __forceinline__ bool reduce_l2_last(const float* __restrict__ part, i
   if (c < C) {
     const float* p0 = part;
     const float* p1 = part + (int64_t)nblk * C;
-#pragma unroll 4
-    for (int b = b0 + lane; b < b1; b += 4) {
+    int b = b0 + lane;
+    for (; b + 28 < b1; b += 32) {                          // 8 rows (16 loads) in flight per batch
+      float x[8], y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        x[u] = p0[(int64_t)(b + 4 * u) * C + c];
+        y[u] = p1[(int64_t)(b + 4 * u) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { a0 += x[u]; a1 += y[u]; }
+    }
+    for (; b < b1; b += 4) {
       a0 += p0[(int64_t)b * C + c];
       a1 += p1[(int64_t)b * C + c];
     }
