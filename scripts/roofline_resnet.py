@@ -1,6 +1,6 @@
 """Per-kernel roofline of the ResNet-50 training step (bs 256, 224^2, bf16 NHWC) on MI355X.
 
-Every native pass of every layer shape is timed in isolation (HIP events, median of 10) with the exact
+Every native pass of every layer shape is timed in isolation (10 calls captured in one hipGraph, median of 5 replays, per call) with the exact
 arguments the model uses (dgrad epilogues with the fused BatchNorm-backward partials / residual add, wgrad into
 the fp32 flat slot, BatchNorm from the GEMM-epilogue partials).  Bytes are the compulsory HBM traffic from the
 shapes (each operand read once, each output written once; a 3x3 gather counts its source image once) and FLOPs
