@@ -293,8 +293,8 @@ def main() -> None:
         lines = [
             f"# ResNet-50 training step roofline (bs {nb}, 224^2, bf16 NHWC, MI355X) -- per-kernel, shapes from the model",
             "",
-            "`scripts/roofline_resnet.py`: each native pass of each layer shape timed in isolation (HIP events, median "
-            f"of {a.reps}) with the model's arguments.  Bytes = compulsory HBM traffic from the shapes; roofline = "
+            "`scripts/roofline_resnet.py`: each native pass of each layer shape timed in isolation "
+            f"({a.reps} calls captured in one hipGraph, median of 5 replays, per call) with the model's arguments.  Bytes = compulsory HBM traffic from the shapes; roofline = "
             "max(bytes / 8 TB/s, FLOPs / 2.5 PFLOP/s).  `count` = occurrences of the shape per step.",
             "",
             "## Per class (sum over the network)",
