@@ -984,15 +984,23 @@ PLX_API int plx_bn_backward_from_partials(const void* x, const uint8_t* mask, co
 // ---- ResNet stem BatchNorm + ReLU + 3x3/s2/p1 max-pool (see stem_apply_pool_kernel)
 // Forward: statistics (workspace `partials`: plx_bn_workspace(N*H*W, C) floats) -> mean / invstd / scale|bias ->
 // y [N][OH][OW][C] bf16 and idx [N*OH*OW*C] window positions.
+// ext_part / ext_nblk (nullable / 0): level-1 channel-stat partials [2][ext_nblk][C] from the producing convolution's
+// epilogue (plx_stem_conv_fwd); `partials` then only needs the level-2 rows (plx_bn_l2_workspace(ext_nblk, C))
 PLX_API int plx_stem_bn_pool_forward(const void* x, void* y, void* idx, int N, int H, int W, int C, const float* gamma,
                                      const float* beta, float eps, float momentum, float* running_mean,
                                      float* running_var, float* save_mean, float* save_invstd, float* scale_bias,
-                                     float* partials, unsigned* counters, hipStream_t stream) {
+                                     float* partials, const float* ext_part, int ext_nblk, unsigned* counters,
+                                     hipStream_t stream) {
   const int G = C / 8;
   if (N <= 0 || H <= 0 || W <= 0 || C % 8 || G > 256 || 256 % G) return 1;
-  const int rc = plx_bn_forward(x, nullptr, nullptr, (int64_t)N * H * W, C, gamma, beta, eps, momentum, running_mean,
-                                running_var, save_mean, save_invstd, scale_bias, partials, nullptr, 1, nullptr,
-                                counters, stream);
+  const int rc = ext_part != nullptr
+                     ? plx_bn_forward_from_partials(x, nullptr, nullptr, (int64_t)N * H * W, C, gamma, beta, eps,
+                                                    momentum, running_mean, running_var, save_mean, save_invstd,
+                                                    scale_bias, ext_part, ext_nblk, partials, nullptr, 1, nullptr,
+                                                    counters, stream)
+                     : plx_bn_forward(x, nullptr, nullptr, (int64_t)N * H * W, C, gamma, beta, eps, momentum,
+                                      running_mean, running_var, save_mean, save_invstd, scale_bias, partials, nullptr,
+                                      1, nullptr, counters, stream);
   if (rc) return rc;
   const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
   const int rows = N * OH;

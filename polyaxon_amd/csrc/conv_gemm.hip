@@ -152,12 +152,14 @@ __device__ __forceinline__ int nt_swz(int row) { return (row >> 1) & 7; }
 // and 4 blocks per CU, whose interleaving hides the staging instead (MINB = blocks per CU the registers allow)
 // BWD: the data-gradient epilogue (D add, ReLU-masked D, BatchNorm-backward partials); !BWD: the forward one (channel
 // stats).  Compile-time so each kernel only holds the epilogue registers it uses.
-template <int BM, int BN, int WGM, int WGN, bool CONV, int MINB = 2, int NBUF = 2, bool BWD = false>
+// MODE: 0 dense rows, 1 implicit-GEMM convolution (ConvGeom gather), 2 the ResNet stem (see plx_stem_conv_fwd)
+template <int BM, int BN, int WGM, int WGN, int MODE, int MINB = 2, int NBUF = 2, bool BWD = false>
 __global__ void __launch_bounds__(NTHREADS, MINB)
 gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
                int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
                float* __restrict__ stats, ConvGeom geo, const __bf16* __restrict__ D, int ldd, BnBwd bnr,
                const uint8_t* __restrict__ dmask) {
+    constexpr bool CONV = MODE == 1, STEM = MODE == 2;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
     constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -199,6 +201,21 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                 }
             }
             a_ok[i] = gm < M ? ok : 0u;
+        } else if constexpr (STEM) {
+            // row = output pixel (n, r, c); A row chunk t (16 B) = super-pixel (2r - 3 + t / 4, c - 2 + t % 4) of the
+            // packed input (2 pixels x 4 channels); stage s stages chunk t = 8 s + lc, bit s says it is in the image
+            int n, r, c;
+            row_coords(gm, geo, n, r, c);
+            const int ih0 = 2 * r - 3, sc0 = c - 2;
+            a_off[i] = ((n * geo.H + ih0) * geo.W + sc0) * 16;
+            uint32_t ok = 0;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const int t = st * 8 + lc;
+                ok |= (t < 28 && (unsigned)(ih0 + (t >> 2)) < (unsigned)geo.H && (unsigned)(sc0 + (t & 3)) < (unsigned)geo.W)
+                          ? 1u << st : 0u;
+            }
+            a_ok[i] = gm < M ? ok : 0u;
         } else {
             a_off[i] = (gm * lda + lc * 8) * 2;
             a_ok[i] = gm < M ? 1u : 0u;
@@ -222,8 +239,13 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
             bk0 = geo.tap_b[t] + c0 * 2;
             bit = t;
         }
+        if constexpr (STEM) bit = k0 / BK;
 #pragma unroll
         for (int i = 0; i < BM / 32; ++i) {                 // A: BM rows / 8 rows per instr / 4 waves
+            if constexpr (STEM) {                           // this lane's chunk = tap t of the 7 x 4 super-pixel window
+                const int t = bit * 8 + ((lane & 7) ^ nt_swz((i * 4 + wave) * 8 + (lane >> 3)));
+                a_add = ((t >> 2) * geo.W + (t & 3)) * 16;
+            }
             const uint32_t off = (a_ok[i] >> bit) & 1u ? (uint32_t)(a_off[i] + a_add) : OOB;
             blds16(ra, off, base + (i * 4 + wave) * 1024);
         }
@@ -650,7 +672,7 @@ int set_lds(KernelT k, int bytes) {
 }
 
 // NBUF = 1: one K-stage buffer, LDS = max(stage, epilogue staging), 3-4 blocks per CU (the skinny GEMMs)
-template <int BM, int BN, int WGM, int WGN, bool CONV = false, int NBUF = 2>
+template <int BM, int BN, int WGM, int WGN, int CONV = 0, int NBUF = 2>
 int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
               const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}, const void* D = nullptr,
               int ldd = 0, BnBwd bnr = {}, const uint8_t* dmask = nullptr) {
@@ -664,7 +686,7 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
     // blocks per CU the registers are asked to allow (128 VGPRs at 4): the double-buffered data-gradient kernel
     // keeps its accumulators live through the epilogue prefetch (~178 VGPRs), the single-buffer one parks them in
     // LDS first (LATE in gemm_nt_kernel)
-    constexpr int CAP = CONV && BN == 64 ? 3 : 4;          // the 256x64 conv staging spills 7-8 VGPRs at 4
+    constexpr int CAP = CONV != 0 && BN == 64 ? 3 : 4;     // the 256x64 conv staging spills 7-8 VGPRs at 4
     constexpr int MIN_F = NBUF == 1 ? (PER_CU < CAP ? PER_CU : CAP) : 2, MIN_B = MIN_F;
     auto kf = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_F, NBUF, false>;
     auto kb = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_B, NBUF, true>;
@@ -1056,11 +1078,78 @@ int plx_weight_prep_all(const float* base, void* wf, void* wd, const void* segs,
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// ---- ResNet stem: 7x7 / stride 2 / pad 3 convolution, 3 -> 64 channels, as an MFMA GEMM with K = 256.
+// The input is packed once per step into "super-pixels" of 2 horizontally adjacent pixels x 4 channels (3 + a zero)
+// = 16 B, so one LDS-DMA chunk is one super-pixel and a 7 x 4 window of them (7 rows x 8 columns, the first column a
+// zero-weight tap) covers an output pixel's 7 x 7 receptive field: 28 chunks = 224 reduction values, padded to 256.
+// The epilogue writes the BatchNorm channel stats (as the other convolutions do), so the stem BatchNorm needs no
+// statistics pass over the 112 x 112 x 64 output.
+__global__ void stem_pack_input_kernel(const uint32_t* __restrict__ x, uint4* __restrict__ xp, long n_sp) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n_sp; i += (long)gridDim.x * blockDim.x) {
+        const uint32_t d0 = x[3 * i], d1 = x[3 * i + 1], d2 = x[3 * i + 2];  // 2 pixels x 3 bf16, 4-byte aligned
+        xp[i] = make_uint4(d0, d1 & 0xffffu, (d1 >> 16) | (d2 << 16), d2 >> 16);
+    }
+}
+
+// wp[co][t * 8 + px * 4 + ch] = w[co][ch][t / 4][2 (t % 4) - 1 + px]   (0 outside the 7x7x3 kernel and for t >= 28)
+__global__ void stem_pack_weight_kernel(const float* __restrict__ w, long s_co, long s_ci, long s_kh, long s_kw,
+                                        __bf16* __restrict__ wp, int cout) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= cout * 256) return;
+    const int co = e >> 8, k = e & 255, t = k >> 3, px = (k >> 2) & 1, ch = k & 3;
+    const int kh = t >> 2, kw = 2 * (t & 3) - 1 + px;
+    const bool ok = t < 28 && ch < 3 && kw >= 0 && kw < 7;
+    wp[e] = (__bf16)(ok ? w[co * s_co + ch * s_ci + kh * s_kh + kw * s_kw] : 0.f);
+}
+
 int plx_weight_prep(const float* w, void* wb, void* wt, int cout, int cin, void* stream) {
     dim3 grid((cin + 31) / 32, (cout + 31) / 32);
     hipLaunchKernelGGL(weight_prep_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, (__bf16*)wb, (__bf16*)wt, cout,
                        cin);
     return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// x: NHWC bf16 [N][H][W][3] (H, W even) -> xp [N][H][W/2][8] bf16 super-pixels
+int plx_stem_pack_input(const void* x, void* xp, int N, int H, int W, void* stream) {
+    if (N <= 0 || H <= 0 || W <= 0 || (W & 1)) return -1;
+    const long n_sp = (long)N * H * (W / 2);
+    long blocks = (n_sp + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(stem_pack_input_kernel, dim3((int)blocks), dim3(256), 0, (hipStream_t)stream, (const uint32_t*)x,
+                       (uint4*)xp, n_sp);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// fp32 weight [cout][3][7][7] (any strides) -> bf16 wp [cout][256]
+int plx_stem_pack_weight(const float* w, long s_co, long s_ci, long s_kh, long s_kw, void* wp, int cout, void* stream) {
+    hipLaunchKernelGGL(stem_pack_weight_kernel, dim3((cout * 256 + 255) / 256), dim3(256), 0, (hipStream_t)stream, w,
+                       s_co, s_ci, s_kh, s_kw, (__bf16*)wp, cout);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// rows of plx_stem_conv_fwd's channel-stat partials: stats is fp32 [2][ceil(M / 256)][64], M = N * Ho * Wo
+int plx_stem_conv_rows_per_block() { return 256; }
+
+// y[N*Ho*Wo][64] (NHWC bf16) = conv7x7/s2/p3(x) from the packed input xp (plx_stem_pack_input) and weights wp
+// (plx_stem_pack_weight); stats (nullable) as plx_gemm_nt's
+int plx_stem_conv_fwd(const void* xp, const void* wp, void* y, int N, int H, int W, const void* zero, float* stats,
+                      void* stream) {
+    if (N <= 0 || H <= 0 || W <= 0 || (W & 1)) return -1;
+    ConvGeom g{};
+    g.H = H;
+    g.W = W / 2;                                    // super-pixel columns
+    g.Hr = (H - 1) / 2 + 1;                         // (H + 2*3 - 7) / 2 + 1
+    g.Wr = (W - 1) / 2 + 1;
+    g.mWr = div_magic(g.Wr);
+    g.mHr = div_magic(g.Hr);
+    const int M = N * g.Hr * g.Wr;
+    return nt_single(false, true, 256, (M + 255) / 256)
+               ? launch_nt<256, 64, 4, 1, 2, 1>(xp, wp, y, M, 64, 256, 8, 256, 64, zero, stats, (hipStream_t)stream, g)
+               : launch_nt<256, 64, 4, 1, 2, 2>(xp, wp, y, M, 64, 256, 8, 256, 64, zero, stats, (hipStream_t)stream, g);
 }
 
 }  // extern "C"

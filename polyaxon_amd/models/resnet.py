@@ -18,7 +18,7 @@ from polyaxon_amd.ops.conv1x1 import Conv1x1, GradMailbox
 from polyaxon_amd.ops.conv import Conv3x3, ConvKxK
 from polyaxon_amd.ops.norm import BatchNormAct
 from polyaxon_amd.ops.pool import MaxPool3s2
-from polyaxon_amd.ops.stem import stem_bn_relu_pool
+from polyaxon_amd.ops.stem import StemConv, stem_bn_relu_pool
 
 
 class Bottleneck(nn.Module):
@@ -57,6 +57,7 @@ class Bottleneck(nn.Module):
 
 _DEFER_DOWN_BN = os.environ.get("PLX_DEFER_DOWN_BN", "1") != "0"  # A/B knob (scripts/ab_check.sh)
 _STEM_FUSED = os.environ.get("PLX_STEM_FUSED", "1") != "0"  # A/B knob: stem BN + ReLU + max-pool in one op
+_STEM_CONV = os.environ.get("PLX_STEM_CONV", "1") != "0"  # A/B knob: native stem convolution
 
 
 class Downsample(nn.Module):
@@ -75,7 +76,9 @@ class ResNet(nn.Module):
     def __init__(self, layers: List[int], num_classes: int = 1000, width: int = 64,
                  zero_init_residual: bool = True, fused: bool = True, native_conv: bool = True):
         super().__init__()
-        self.stem = nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False)
+        # 3 -> 64: the MFMA stem GEMM with BN-stats epilogue (ops/stem.py); other widths: the library convolution
+        self.stem = (StemConv(3, width, native=native_conv and _STEM_CONV) if width == 64
+                     else nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False))
         self.stem_bn = BatchNormAct(width, act=True, fused=fused)
         self.pool = MaxPool3s2(native=native_conv)
         stages = []

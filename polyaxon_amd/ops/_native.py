@@ -170,7 +170,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_bn_dx_blocks": [_L, _I],
         "plx_bn_backward_from_partials": [_P, _P, _P, _P, _P, _L, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I, _P,
                                           _P, _P],
-        "plx_stem_bn_pool_forward": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _P],
+        "plx_stem_bn_pool_forward": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _P,
+                                     _P],
         "plx_stem_bn_pool_bwd_workspace": [_I, _I, _I, _I],
         "plx_stem_bn_pool_backward": [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     },
@@ -206,6 +207,10 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
         "plx_weight_prepk": [_P, _L, _L, _L, _L, _P, _P, _I, _I, _I, _P],
         "plx_weight_prep_all": [_P, _P, _P, _P, _I, _I, _P],
+        "plx_stem_pack_input": [_P, _P, _I, _I, _I, _P],
+        "plx_stem_pack_weight": [_P, _L, _L, _L, _L, _P, _I, _P],
+        "plx_stem_conv_rows_per_block": [],
+        "plx_stem_conv_fwd": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
         "plx_conv_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
         "plx_conv_dgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
         "plx_conv_dgrad_blocks": [_I, _I, _I, _I, _I, _I, _I],

@@ -6,8 +6,8 @@ weight gradient is only needed by the optimizer at the end of the step.  The dir
 stream with an event, runs the launch on the device's side stream, and pins the operand tensors to that stream
 (``record_stream``) so the caching allocator does not recycle them early.  :func:`join`, queued as an autograd
 end-of-backward callback (and called again by the executor before the optimizer), makes the main stream wait
-for every side launch.  Inside hipGraph capture, or with
-``PLX_WGRAD_STREAM=0``, launches run inline.
+for every side launch.  Inside hipGraph capture the fork and join are captured as graph edges (with
+``PLX_WGRAD_CAPTURE_FORK=0`` capture runs them inline); ``PLX_WGRAD_STREAM=0`` runs every launch inline.
 """
 from __future__ import annotations
 
@@ -24,6 +24,15 @@ def enabled() -> bool:
     return os.environ.get("PLX_WGRAD_STREAM", "1") != "0"
 
 
+# Inside hipGraph capture the fork / join is captured too (event edges between the two captured streams), so a
+# replayed step keeps the overlap; PLX_WGRAD_CAPTURE_FORK=0 runs the launches inline during capture instead.
+_CAPTURE_FORK = os.environ.get("PLX_WGRAD_CAPTURE_FORK", "1") != "0"
+
+
+def capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 def _stream_for(dev: torch.device) -> "torch.cuda.Stream":
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     s = _side.get(idx)
@@ -34,7 +43,7 @@ def _stream_for(dev: torch.device) -> "torch.cuda.Stream":
 
 
 def run(fn: Callable[[], None], tensors: Iterable[torch.Tensor], dev: torch.device) -> None:
-    if not enabled() or dev.type != "cuda" or torch.cuda.is_current_stream_capturing():
+    if not enabled() or dev.type != "cuda" or (capturing() and not _CAPTURE_FORK):
         fn()
         return
     main = torch.cuda.current_stream(dev)
@@ -42,8 +51,9 @@ def run(fn: Callable[[], None], tensors: Iterable[torch.Tensor], dev: torch.devi
     side.wait_stream(main)  # operands (dy, x) and the gradient slot are ready in main-stream order
     with torch.cuda.stream(side):
         fn()
-    for t in tensors:
-        t.record_stream(side)
+    if not capturing():  # a captured graph owns its memory pool: nothing is recycled under it
+        for t in tensors:
+            t.record_stream(side)
     idx = side.device.index
     if not _pending.get(idx):
         _pending[idx] = True

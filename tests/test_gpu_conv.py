@@ -368,3 +368,31 @@ def test_weight_cache_matches_per_layer_prep(cuda):
             cache.deactivate()
         grads.append(flat.grads.clone())
     torch.testing.assert_close(grads[1], grads[0], rtol=1e-3, atol=1e-3 * float(grads[0].abs().max()))
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 224, 224), (3, 3, 30, 46), (1, 3, 17, 8)])
+def test_stem_conv_matches_conv2d(cuda, shape):
+    """ops.stem.StemConv: the packed-super-pixel MFMA stem (csrc/conv_gemm.hip plx_stem_conv_fwd) vs fp32 F.conv2d,
+    its epilogue channel stats vs the output's own sums, and the weight gradient vs fp32 autograd."""
+    from polyaxon_amd.ops.stem import StemConv, stem_conv_supported
+
+    torch.manual_seed(0)
+    conv = StemConv().to(cuda)
+    x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert stem_conv_supported(x, conv)
+    xa = x.clone()
+    y = conv(xa)
+    ref = F.conv2d(x.float(), conv.weight.float(), None, 2, 3)
+    assert y.shape == ref.shape
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=3e-2)
+    stats, nblk = y._plx_channel_stats
+    st = stats.view(2, nblk, 64).sum(1)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, 64)
+    torch.testing.assert_close(st[0], yf.sum(0), rtol=1e-3, atol=1e-2 * yf.abs().sum(0).max().item() ** 0.5)
+    torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
+    g = torch.randn_like(ref)
+    y.backward(g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+    torch.cuda.synchronize()
+    w = conv.weight.detach().clone().requires_grad_()
+    F.conv2d(x.float(), w, None, 2, 3).backward(g)
+    torch.testing.assert_close(conv.weight.grad, w.grad, rtol=3e-2, atol=3e-2 * float(w.grad.abs().max()))
