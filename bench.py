@@ -340,6 +340,7 @@ def main() -> int:
             "best_loss": round(res["best"], 4) if res["best"] is not None else None,
             "store_fsm_history_ok": res["fsm_ok"],
             "path": "polyflow scheduler + SQLite store + resident executors (same path as plx run)",
+            "hip_graph": bool(worker._ready_info.get("hip_graph")),
         }
         if args.verbose:
             print(json.dumps(res["pool"]), file=sys.stderr)

@@ -173,6 +173,7 @@ class ResidentWorker:
         return {"ev": "ready", "program": self.program_name, "device": str(ex.device), "pid": os.getpid(),
                 "build_s": round(time.time() - t0, 3), "snapshot_bytes": ex.snapshot_bytes(),
                 "metric": self.program.metric, "unit_steps": self.program.unit_steps, "info": self.program.info,
+                "hip_graph": ex.graph is not None, "graph_check_error": ex.graph_check_error,
                 "device_name": torch.cuda.get_device_name(ex.device) if ex.is_cuda else "cpu"}
 
     def _reset_clock(self) -> None:
