@@ -178,10 +178,15 @@ class ResidentTrialExecutor:
         key = "__graph_check__"
         self.snapshot(key)
         p0 = self.flat.params.detach().clone()
+        # a device data stream (ops/synth.py) advances its counter every step: both runs must see the same batch
+        counter = getattr(self.data, "counter", None)
+        c0 = counter.clone() if counter is not None else None
         self.graph, g = None, self.graph
         self.run(1)  # eager
         d_eager = self.flat.params.detach() - p0
         self.restore(key)
+        if counter is not None:
+            counter.copy_(c0)
         self.graph = g
         self.run(1)  # replay
         d_graph = self.flat.params.detach() - p0
