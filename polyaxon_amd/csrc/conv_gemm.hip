@@ -489,7 +489,9 @@ __device__ __forceinline__ s16x4 tr_read(const char* img, int row, int col /* el
         (__attribute__((address_space(3))) s16x4*)(img + row * ROWB + pc * 16 + half * 8));
 }
 
-template <int ROWB, bool GATHER = false>
+// GATHER: 0 dense rows, 1 the pixel shifted by (dh, dw) (3x3 weight gradient), 2 the stem's packed super-pixel
+// window: chunk k / 8 of row (n, r, c) is super-pixel (2r - 3 + t / 4, c - 2 + t % 4), t = k / 8 (plx_stem_conv_fwd)
+template <int ROWB, int GATHER = 0>
 __device__ __forceinline__ void stage_rows(char* img, __amdgpu_buffer_rsrc_t rsrc, int ld, int r0, int rend, int c0,
                                            int wave, int lane, const ConvGeom* geo = nullptr, int dh = 0, int dw = 0) {
     // BK rows x ROWB bytes, lane-linear image; 1024 B per wave instruction, through buffer-resource LDS-DMA (rows
@@ -503,7 +505,13 @@ __device__ __forceinline__ void stage_rows(char* img, __amdgpu_buffer_rsrc_t rsr
         const int lc = pc ^ tr_swz<ROWB>(row);
         const int gr = r0 + row;
         uint32_t boff;
-        if constexpr (GATHER) {
+        if constexpr (GATHER == 2) {
+            int n, r, c;
+            row_coords(gr, *geo, n, r, c);
+            const int t = (c0 >> 3) + lc, ih = 2 * r - 3 + (t >> 2), sc = c - 2 + (t & 3);
+            const bool ok = gr < rend && t < 28 && (unsigned)ih < (unsigned)geo->H && (unsigned)sc < (unsigned)geo->W;
+            boff = ok ? (uint32_t)(((n * geo->H + ih) * geo->W + sc) * 16) : OOB;
+        } else if constexpr (GATHER == 1) {
             int n, r, c;
             row_coords(gr, *geo, n, r, c);
             const int ih = r * geo->S + dh, iw = c * geo->S + dw;
@@ -516,7 +524,8 @@ __device__ __forceinline__ void stage_rows(char* img, __amdgpu_buffer_rsrc_t rsr
     }
 }
 
-template <int BN1, int BN2, int WG1, int WG2, bool CONV>
+// CONV: 0 dense, 1 3x3 gather (tap per N2 tile), 2 the stem's super-pixel window (plx_stem_conv_wgrad)
+template <int BN1, int BN2, int WG1, int WG2, int CONV>
 __global__ void __launch_bounds__(NTHREADS, 2)
 gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float* __restrict__ W,
                int M, int N1, int N2, int lda, int ldb, int kchunk, const __bf16* __restrict__ zero,
@@ -546,7 +555,7 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
     const int nk = (kend - kbeg + BK - 1) / BK;
     // conv mode: N2 = 9*C and a BN2 tile lies inside one tap (C % BN2 == 0, host-checked)
     int bc0 = n20, dh = 0, dw = 0;
-    if constexpr (CONV) {
+    if constexpr (CONV == 1) {
         const int t = n20 / geo.C;
         bc0 = n20 - t * geo.C;
         dh = geo.offh[t];
@@ -734,14 +743,15 @@ inline void tn_tile(int N1, int N2, int& bn1, int& bn2) {
 int g_tn_blocks_per_cu = 1;
 long g_tn_slab_bytes = 16l << 20;
 
-inline TnPlan tn_plan(int M, int N1, int N2, int num_cus) {
+// bpc > 0 overrides the blocks-per-CU target (the stem's weight gradient runs alone at the end of the backward)
+inline TnPlan tn_plan(int M, int N1, int N2, int num_cus, int bpc = 0) {
     int bn1, bn2;
     tn_tile(N1, N2, bn1, bn2);
     const int ntiles = (N1 / bn1) * (N2 / bn2);
     const long plane = (long)N1 * N2;
     // ~4 blocks per CU (one 4-wave block per CU leaves each SIMD a single wave: latency-bound), >= 4
     // k-stages per block, slabs <= 32 MB (they are re-read by the reducer, mostly from the infinity cache)
-    int slices = (g_tn_blocks_per_cu * (num_cus > 0 ? num_cus : 256)) / ntiles;
+    int slices = ((bpc > 0 ? bpc : g_tn_blocks_per_cu) * (num_cus > 0 ? num_cus : 256)) / ntiles;
     const int by_depth = M / (4 * BK);
     const int by_bytes = (int)(g_tn_slab_bytes / (plane * 4));
     if (slices > by_depth) slices = by_depth;
@@ -762,7 +772,7 @@ inline TnPlan tn_plan(int M, int N1, int N2, int num_cus) {
     return {kchunk, slices, groups, per_group, blocks};
 }
 
-template <int BN1, int BN2, int WG1, int WG2, bool CONV = false>
+template <int BN1, int BN2, int WG1, int WG2, int CONV = 0>
 int launch_tn(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
               const void* zero, hipStream_t s, ConvGeom geo = {}) {
     constexpr int LDS = 2 * BK * (BN1 + BN2) * 2;
@@ -825,10 +835,10 @@ long plx_gemm_tn_workspace(int M, int N1, int N2, int num_cus) {
 }  // extern "C"
 
 namespace {
-template <bool CONV>
+template <int CONV>
 int run_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int N2, int lda, int ldb, int ldc,
-           const void* zero, int num_cus, int accumulate, hipStream_t s, ConvGeom geo) {
-    const TnPlan plan = tn_plan(M, N1, N2, num_cus);
+           const void* zero, int num_cus, int accumulate, hipStream_t s, ConvGeom geo, int bpc = 0) {
+    const TnPlan plan = tn_plan(M, N1, N2, num_cus, bpc);
     int rc;
     if (N1 % 128 == 0 && N2 % 128 == 0)
         rc = launch_tn<128, 128, 2, 2, CONV>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
@@ -1102,6 +1112,18 @@ __global__ void stem_pack_weight_kernel(const float* __restrict__ w, long s_co, 
     wp[e] = (__bf16)(ok ? w[co * s_co + ch * s_ci + kh * s_kh + kw * s_kw] : 0.f);
 }
 
+// dw[co][ci][kh][kw] (+)= packed[co][(kh * 4 + j) * 8 + px * 4 + ci] with kw = 2j - 1 + px
+__global__ void stem_unpack_wgrad_kernel(const float* __restrict__ packed, float* __restrict__ dw, long s_co, long s_ci,
+                                         long s_kh, long s_kw, int accumulate) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= 64 * 147) return;
+    const int co = e / 147, r = e % 147, ci = r / 49, kh = (r % 49) / 7, kw = r % 7;
+    const int j = (kw + 1) >> 1, px = (kw + 1) & 1;
+    const float v = packed[co * 256 + (kh * 4 + j) * 8 + px * 4 + ci];
+    float* d = dw + co * s_co + ci * s_ci + kh * s_kh + kw * s_kw;
+    *d = accumulate ? *d + v : v;
+}
+
 int plx_weight_prep(const float* w, void* wb, void* wt, int cout, int cin, void* stream) {
     dim3 grid((cin + 31) / 32, (cout + 31) / 32);
     hipLaunchKernelGGL(weight_prep_kernel, grid, dim3(256), 0, (hipStream_t)stream, w, (__bf16*)wb, (__bf16*)wt, cout,
@@ -1128,6 +1150,39 @@ int plx_stem_pack_input(const void* x, void* xp, int N, int H, int W, void* stre
 int plx_stem_pack_weight(const float* w, long s_co, long s_ci, long s_kh, long s_kw, void* wp, int cout, void* stream) {
     hipLaunchKernelGGL(stem_pack_weight_kernel, dim3((cout * 256 + 255) / 256), dim3(256), 0, (hipStream_t)stream, w,
                        s_co, s_ci, s_kh, s_kw, (__bf16*)wp, cout);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+constexpr int kStemWgradBpc = 4;  // blocks per CU for the stem's weight gradient (alone on the GPU at the end)
+
+// floats of workspace plx_stem_conv_wgrad needs: the slab reduction's (as plx_gemm_tn_workspace) + dW packed [64][256]
+long plx_stem_conv_wgrad_workspace(int N, int H, int W, int num_cus) {
+    const int M = N * ((H - 1) / 2 + 1) * ((W - 1) / 2 + 1);
+    const TnPlan p = tn_plan(M, 64, 256, num_cus, kStemWgradBpc);
+    return (long)(p.slices + (p.groups > 1 ? p.groups : 0)) * 64 * 256 + 64 * 256;
+}
+
+// dw (fp32 [64][3][7][7], strides s_*; (+)= with accumulate) = the stem's weight gradient from dy (NHWC bf16
+// [N][Ho][Wo][64]) and the packed input xp: a TN GEMM over the output pixels gathering the super-pixel window
+// (stage_rows GATHER 2), then unpacked from the [64][28 x 8] chunk layout
+int plx_stem_conv_wgrad(const void* dy, const void* xp, float* dw, long s_co, long s_ci, long s_kh, long s_kw,
+                        float* ws, int N, int H, int W, const void* zero, int num_cus, int accumulate, void* stream) {
+    if (N <= 0 || H <= 0 || W <= 0 || (W & 1)) return -1;
+    ConvGeom g{};
+    g.H = H;
+    g.W = W / 2;
+    g.Hr = (H - 1) / 2 + 1;
+    g.Wr = (W - 1) / 2 + 1;
+    g.mWr = div_magic(g.Wr);
+    g.mHr = div_magic(g.Hr);
+    const int M = N * g.Hr * g.Wr;
+    const TnPlan p = tn_plan(M, 64, 256, num_cus, kStemWgradBpc);
+    float* packed = ws + (long)(p.slices + (p.groups > 1 ? p.groups : 0)) * 64 * 256;
+    hipStream_t s = (hipStream_t)stream;
+    const int rc = run_tn<2>(dy, xp, packed, ws, M, 64, 256, 64, 8, 256, zero, num_cus, 0, s, g, kStemWgradBpc);
+    if (rc) return rc;
+    hipLaunchKernelGGL(stem_unpack_wgrad_kernel, dim3((64 * 147 + 255) / 256), dim3(256), 0, s, packed, dw, s_co, s_ci,
+                       s_kh, s_kw, accumulate);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

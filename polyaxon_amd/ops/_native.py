@@ -211,6 +211,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_stem_pack_weight": [_P, _L, _L, _L, _L, _P, _I, _P],
         "plx_stem_conv_rows_per_block": [],
         "plx_stem_conv_fwd": [_P, _P, _P, _I, _I, _I, _P, _P, _P],
+        "plx_stem_conv_wgrad_workspace": [_I, _I, _I, _I],
+        "plx_stem_conv_wgrad": [_P, _P, _P, _L, _L, _L, _L, _P, _I, _I, _I, _P, _I, _I, _P],
         "plx_conv_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
         "plx_conv_dgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
         "plx_conv_dgrad_blocks": [_I, _I, _I, _I, _I, _I, _I],
@@ -258,7 +260,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

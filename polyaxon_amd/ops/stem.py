@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import torch
 
-from polyaxon_amd.ops import _native, side_stream
+from polyaxon_amd.ops import _native
 from polyaxon_amd.ops.bn_fused import _cl, _counters, _stream
 from polyaxon_amd.ops.flat import direct_grad
 
@@ -99,7 +99,7 @@ def stem_bn_relu_pool(x: torch.Tensor, bn, pool) -> torch.Tensor:
 class _StemConv(torch.autograd.Function):
     """7x7/s2/p3 3->64 convolution as an MFMA GEMM (csrc/conv_gemm.hip ``plx_stem_conv_fwd``): the input is packed
     into 16-byte super-pixels (2 pixels x 4 channels) and the epilogue emits the BatchNorm channel stats.  The weight
-    gradient (3.9 GFLOP of the step's 6 TFLOP) stays with the library (MIOpen's weight-gradient convolution)."""
+    gradient is the same window as a TN GEMM (``plx_stem_conv_wgrad``)."""
 
     @staticmethod
     def forward(ctx, x, weight, stats):
@@ -124,25 +124,32 @@ class _StemConv(torch.autograd.Function):
                                     _zero_page(x.device).data_ptr(),
                                     stats.data_ptr() if stats is not None else None, st)
         _native.check(rc, "plx_stem_conv_fwd")
-        ctx.save_for_backward(x, weight)
+        ctx.save_for_backward(xp, weight)
+        ctx.shape = (n, h, w)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
+        """Weight gradient only (the input is data): the same super-pixel window as a TN GEMM over the output pixels
+        (``plx_stem_conv_wgrad``), accumulated straight into the flat gradient slot when there is one.  It is the
+        step's last backward op, so it runs on the main stream (nothing is left to overlap it with)."""
+        xp, weight = ctx.saved_tensors
         if not ctx.needs_input_grad[1]:
             return None, None, None
+        conv = _native.lib("plx_conv")
+        n, h, w = ctx.shape
         dy = _cl(dy.to(torch.bfloat16))
-        wb = weight.to(torch.bfloat16)
-
-        def wgrad():
-            return torch.ops.aten.convolution_backward(dy, x, wb, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
-                                                       [False, True, False])[1]
+        from polyaxon_amd.ops.conv1x1 import _num_cus, _zero_page
+        cus = _num_cus(dy.device)
+        ws = torch.empty(int(conv.plx_stem_conv_wgrad_workspace(n, h, w, cus)), dtype=torch.float32, device=dy.device)
         slot = direct_grad(weight)
-        if slot is not None:  # into the flat gradient slot, overlapped on the side stream (the last op of backward)
-            side_stream.run(lambda: slot.add_(wgrad()), (dy, x, wb), x.device)
-            return None, None, None
-        return None, wgrad().to(weight.dtype), None
+        out = slot if slot is not None else torch.empty_like(weight, dtype=torch.float32)
+        st_ = out.stride()
+        rc = conv.plx_stem_conv_wgrad(dy.data_ptr(), xp.data_ptr(), out.data_ptr(), st_[0], st_[1], st_[2], st_[3],
+                                      ws.data_ptr(), n, h, w, _zero_page(dy.device).data_ptr(), cus,
+                                      int(slot is not None), _stream())
+        _native.check(rc, "plx_stem_conv_wgrad")
+        return None, (None if slot is not None else out.to(weight.dtype)), None
 
 
 def stem_conv_supported(x: torch.Tensor, conv) -> bool:

@@ -59,6 +59,15 @@ def main():
         "stem_gemm": timeit(lambda: lib.plx_stem_conv_fwd(xp.data_ptr(), wp.data_ptr(), y.data_ptr(), n, 224, 224, z,
                                                           stats.data_ptr(), st())),
     }
+    dy = torch.randn(n, 64, 112, 112, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    from polyaxon_amd.ops.conv1x1 import _num_cus
+    cus = _num_cus(dev)
+    ws = torch.empty(int(lib.plx_stem_conv_wgrad_workspace(n, 224, 224, cus)), dtype=torch.float32, device=dev)
+    gw = torch.zeros(64, 3, 7, 7, device=dev)
+    res["miopen_wgrad"] = timeit(lambda: torch.ops.aten.convolution_backward(
+        dy, x, wb, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False]))
+    res["stem_wgrad"] = timeit(lambda: lib.plx_stem_conv_wgrad(dy.data_ptr(), xp.data_ptr(), gw.data_ptr(), *gw.stride(),
+                                                               ws.data_ptr(), n, 224, 224, z, cus, 1, st()))
     for k, v in res.items():
         print(json.dumps({"pass": k, "us": round(v, 1)}))
 

@@ -112,6 +112,15 @@ def main():
                            f"{(run_end - t_s) / 1e3:.1f}: `{p_['Kernel_Name'][:50]}` (stream {p_.get(skey, '?')}) -> "
                            f"`{k['Kernel_Name'][:50]}` (stream {k.get(skey, '?')})")
             run_end = max(run_end, int(k["End_Timestamp"]))
+        ends = collections.defaultdict(int)
+        for k in ks:
+            ends[k.get(skey, "?")] = max(ends[k.get(skey, "?")], int(k["End_Timestamp"]) - t_s)
+        out.append("last step: last kernel end per stream " + ", ".join(f"stream {sid}: +{e / 1e3:.1f} us"
+                                                                 for sid, e in sorted(ends.items())))
+        out.append("last step: final kernels:")
+        for k in sorted(ks, key=lambda r: int(r["End_Timestamp"]))[-10:]:
+            out.append(f"- +{(int(k['Start_Timestamp']) - t_s) / 1e3:9.1f} .. +{(int(k['End_Timestamp']) - t_s) / 1e3:9.1f} us"
+                       f"  stream {k.get(skey, '?')}  `{k['Kernel_Name'][:70]}`")
         out.append(f"last step: largest idle {worst / 1e3:.1f} us before kernel #{wi}; neighbourhood:")
         for k in ks[max(0, (wi or 0) - 6): (wi or 0) + 4]:
             out.append(f"- +{(int(k['Start_Timestamp']) - t_s) / 1e3:9.1f} .. +{(int(k['End_Timestamp']) - t_s) / 1e3:9.1f} us"
