@@ -119,6 +119,19 @@ def available(name: str) -> bool:
     return lib_path(name).exists()
 
 
+_SIZES: Dict[tuple, int] = {}
+
+
+def size(libname: str, fn: str, *args: int) -> int:
+    """Memoised integer query (workspace sizes, block counts): pure functions of their int arguments (and of
+    knobs fixed at load time), called from every op's host path -- the ctypes round trip is not free there."""
+    key = (fn,) + args
+    v = _SIZES.get(key)
+    if v is None:
+        v = _SIZES[key] = int(getattr(lib(libname), fn)(*args))
+    return v
+
+
 def lib(name: str) -> ctypes.CDLL:
     """Load (building on first use if a compiler is present) the named native library."""
     with _lock:

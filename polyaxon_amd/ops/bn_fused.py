@@ -62,7 +62,7 @@ class _BNAct(torch.autograd.Function):
         x = _cl(x)
         n, c, h, w = x.shape
         m = n * h * w
-        ws = lib.plx_bn_workspace(m, c)
+        ws = _native.size("plx_bn", "plx_bn_workspace", m, c)
         if ws < 0:
             raise RuntimeError("unsupported channel count for fused BN")
         f32 = dict(dtype=torch.float32, device=x.device)
@@ -86,7 +86,7 @@ class _BNAct(torch.autograd.Function):
         if ext is not None:
             # channel sums came from the producing conv's GEMM epilogue: no stats pass over x
             part, nblk = ext
-            l2 = torch.empty(int(lib.plx_bn_l2_workspace(nblk, c)), **f32)
+            l2 = torch.empty(_native.size("plx_bn", "plx_bn_l2_workspace", nblk, c), **f32)
             rc = lib.plx_bn_forward_from_partials(
                 x.data_ptr(), res.data_ptr() if res is not None else None, yp, m, c, weight.data_ptr(),
                 bias.data_ptr(), float(eps), float(momentum), rm, rv, stats.data_ptr(), stats[c:].data_ptr(),
@@ -152,14 +152,14 @@ class _BNAct(torch.autograd.Function):
         rb = None
         if ctx.rlink is not None and dres is not None:
             rl = ctx.rlink
-            nblk2 = int(lib.plx_bn_dx_blocks(m, c))
+            nblk2 = _native.size("plx_bn", "plx_bn_dx_blocks", m, c)
             rl.part = torch.empty(2 * nblk2 * c, **f32)
             rl.nblk = nblk2
             rb = _native.ResBnArgs(rl.x.data_ptr(), rl.mask.data_ptr() if rl.mask is not None else None,
                                    rl.mean.data_ptr(), rl.invstd.data_ptr(), rl.part.data_ptr())
         rbp = ctypes.addressof(rb) if rb is not None else None
         if part is not None:  # the consumer's dgrad epilogue already reduced dz and dz*xhat per block
-            l2 = torch.empty(int(lib.plx_bn_l2_workspace(nblk, c)), **f32)
+            l2 = torch.empty(_native.size("plx_bn", "plx_bn_l2_workspace", nblk, c), **f32)
             rc = lib.plx_bn_backward_from_partials(
                 x.data_ptr(), mask.data_ptr() if mask is not None else None, dy.data_ptr(), dx.data_ptr(),
                 dres.data_ptr() if dres is not None else None, m, c, weight.data_ptr(), stats.data_ptr(),

@@ -95,7 +95,7 @@ class _ConvK(torch.autograd.Function):
                 dx = (torch.zeros_like if (s == 2 and k == 1) else torch.empty_like)(x, memory_format=torch.channels_last)
             bnr = None
             if ctx.link is not None and (ctx.box is None or extra is not None):
-                nblk = int(lib.plx_conv_dgrad_blocks(n, h, w, cin, cout, k, s))
+                nblk = _native.size("plx_conv", "plx_conv_dgrad_blocks", n, h, w, cin, cout, k, s)
                 bnr = ctx.link.request(nblk)
             rc = lib.plx_conv_dgrad(dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), n, h, w, cin, cout, k, s, zero,
                                     add.data_ptr() if add is not None else None,
@@ -107,7 +107,7 @@ class _ConvK(torch.autograd.Function):
             g = ctx.wgrad if direct else torch.empty(cout, k, k, cin, dtype=torch.float32, device=x.device)
 
             def wgrad():
-                ws = torch.empty(int(lib.plx_conv_wgrad_workspace(n, h, w, cin, cout, k, s, cus)),
+                ws = torch.empty(_native.size("plx_conv", "plx_conv_wgrad_workspace", n, h, w, cin, cout, k, s, cus),
                                  dtype=torch.float32, device=x.device)
                 rc = lib.plx_conv_wgrad(dy.data_ptr(), x.data_ptr(), g.data_ptr(), ws.data_ptr(), n, h, w, cin, cout,
                                         k, s, zero, cus, int(direct), _stream())

@@ -49,7 +49,7 @@ def _stream() -> int:
 
 def nt_stats_rows(n: int) -> int:
     """Rows per block of plx_gemm_nt for an N-wide output (the granularity of its BN-stats partials)."""
-    return int(_native.lib("plx_conv").plx_gemm_nt_rows_per_block(n))
+    return _native.size("plx_conv", "plx_gemm_nt_rows_per_block", n)
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, stats: torch.Tensor = None,
@@ -94,7 +94,8 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor = None, accumula
     assert a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0 and out.data_ptr() % 16 == 0
     lib = _native.lib("plx_conv")
     cus = _num_cus(a.device)
-    ws = torch.empty(int(lib.plx_gemm_tn_workspace(m, n1, n2, cus)), dtype=torch.float32, device=a.device)
+    ws = torch.empty(_native.size("plx_conv", "plx_gemm_tn_workspace", m, n1, n2, cus), dtype=torch.float32,
+                     device=a.device)
     rc = lib.plx_gemm_tn(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws.data_ptr(), m, n1, n2, a.stride(0),
                          b.stride(0), out.stride(0), _zero_page(a.device).data_ptr(), cus, int(accumulate),
                          _stream())

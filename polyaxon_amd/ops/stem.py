@@ -33,10 +33,10 @@ class _StemBNReLUPool(torch.autograd.Function):
         stats = torch.empty(4 * c, **f32)  # mean | invstd | scale | bias
         if ext is not None:  # channel sums from the stem convolution's epilogue (StemConv): no statistics pass
             part, nblk = ext
-            ws = torch.empty(int(lib.plx_bn_l2_workspace(nblk, c)), **f32)
+            ws = torch.empty(_native.size("plx_bn", "plx_bn_l2_workspace", nblk, c), **f32)
         else:
             part, nblk = None, 0
-            ws = torch.empty(int(lib.plx_bn_workspace(n * h * w, c)), **f32)
+            ws = torch.empty(_native.size("plx_bn", "plx_bn_workspace", n * h * w, c), **f32)
         y = torch.empty((n, c, oh, ow), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         idx = torch.empty(n * oh * ow * c, dtype=torch.uint8, device=x.device)
         rc = lib.plx_stem_bn_pool_forward(
