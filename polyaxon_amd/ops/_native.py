@@ -122,6 +122,15 @@ def available(name: str) -> bool:
 _SIZES: Dict[tuple, int] = {}
 
 
+def current_stream() -> int:
+    """Raw handle of the current HIP stream of the current device: two C calls, against ~8 us for
+    ``torch.cuda.current_stream().cuda_stream`` (a Python Stream object and device-index resolution per call) --
+    every op's launch path asks for it, ~160 times per ResNet-50 step."""
+    import torch
+
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
+
+
 def size(libname: str, fn: str, *args: int) -> int:
     """Memoised integer query (workspace sizes, block counts): pure functions of their int arguments (and of
     knobs fixed at load time), called from every op's host path -- the ctypes round trip is not free there."""

@@ -23,7 +23,7 @@ _MASKED_RESGRAD = os.environ.get("PLX_MASKED_RESGRAD", "1") != "0"  # A/B knob (
 
 
 def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    return _native.current_stream()
 
 
 _COUNTERS = {}

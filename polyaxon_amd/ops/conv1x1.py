@@ -44,7 +44,7 @@ def _num_cus(dev: torch.device) -> int:
 
 
 def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    return _native.current_stream()
 
 
 def nt_stats_rows(n: int) -> int:

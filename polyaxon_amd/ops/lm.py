@@ -16,7 +16,7 @@ from polyaxon_amd.ops import _native
 
 
 def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    return _native.current_stream()
 
 
 def _native_ok(x: torch.Tensor) -> bool:

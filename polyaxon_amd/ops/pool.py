@@ -13,7 +13,7 @@ from polyaxon_amd.ops import _native
 
 
 def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    return _native.current_stream()
 
 
 class _MaxPool3s2(torch.autograd.Function):

@@ -13,7 +13,7 @@ def rms_norm_reference(x: torch.Tensor, weight: torch.Tensor, eps: float) -> tor
 
 
 def _stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
+    return _native.current_stream()
 
 
 class _RMSNorm(torch.autograd.Function):

@@ -20,8 +20,11 @@ _side: Dict[int, "torch.cuda.Stream"] = {}
 _pending: Dict[int, bool] = {}
 
 
+_ENABLED = os.environ.get("PLX_WGRAD_STREAM", "1") != "0"
+
+
 def enabled() -> bool:
-    return os.environ.get("PLX_WGRAD_STREAM", "1") != "0"
+    return _ENABLED
 
 
 # Inside hipGraph capture the fork / join is captured too (event edges between the two captured streams), so a
@@ -30,7 +33,7 @@ _CAPTURE_FORK = os.environ.get("PLX_WGRAD_CAPTURE_FORK", "1") != "0"
 
 
 def capturing() -> bool:
-    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    return torch.cuda.is_current_stream_capturing()
 
 
 def _stream_for(dev: torch.device) -> "torch.cuda.Stream":
