@@ -738,9 +738,10 @@ inline void tn_tile(int N1, int N2, int& bn1, int& bn2) {
 
 // slicing knobs (plx_set_tn_plan): target resident blocks per CU, cap on the fp32 slab bytes
 // Swept in isolation (scripts/diag_wgrad_plan.py) 3 / 32 MB was best; in the training step the weight gradients run on
-// the side stream beside the data-gradient chain, and there 1 / 16 MB (fewer slices: less slab traffic competing with
-// the main stream) gave +0.8-1.3 % step throughput (interleaved bench runs, PLX_TN_PLAN)
-int g_tn_blocks_per_cu = 1;
+// the side stream beside the data-gradient chain, and there fewer slices (less slab traffic competing with the main
+// stream) win, except for the 56x56 layers whose gradients finish the backward: 0 = by size (tn_plan), 16 MB.  Same-box
+// bench, 2 interleaved rounds (PLX_TN_PLAN): 3/32 11.61k, 11.70k; 1/16 11.71k, 11.75k; by size 11.85k, 11.87k trials/h
+int g_tn_blocks_per_cu = 0;
 long g_tn_slab_bytes = 16l << 20;
 
 // bpc > 0 overrides the blocks-per-CU target (the stem's weight gradient runs alone at the end of the backward)
@@ -751,7 +752,10 @@ inline TnPlan tn_plan(int M, int N1, int N2, int num_cus, int bpc = 0) {
     const long plane = (long)N1 * N2;
     // ~4 blocks per CU (one 4-wave block per CU leaves each SIMD a single wave: latency-bound), >= 4
     // k-stages per block, slabs <= 32 MB (they are re-read by the reducer, mostly from the infinity cache)
-    int slices = ((bpc > 0 ? bpc : g_tn_blocks_per_cu) * (num_cus > 0 ? num_cus : 256)) / ntiles;
+    // g_tn_blocks_per_cu == 0: by size -- the 56x56 layers (M >= 400k rows) are the last weight gradients of the
+    // backward, with little main-stream work left to hide them behind, so they get 3 blocks per CU; the rest 1
+    const int bpc_eff = bpc > 0 ? bpc : (g_tn_blocks_per_cu > 0 ? g_tn_blocks_per_cu : (M >= 400000 ? 3 : 1));
+    int slices = (bpc_eff * (num_cus > 0 ? num_cus : 256)) / ntiles;
     const int by_depth = M / (4 * BK);
     const int by_bytes = (int)(g_tn_slab_bytes / (plane * 4));
     if (slices > by_depth) slices = by_depth;
@@ -821,7 +825,7 @@ void plx_set_nt_single_stage(int mode) { g_nt_single_stage = mode; }
 
 // weight-gradient slicing knobs; workspace sizes follow them, so set before sizing / launching
 void plx_set_tn_plan(int blocks_per_cu, int slab_mb) {
-    if (blocks_per_cu > 0) g_tn_blocks_per_cu = blocks_per_cu;
+    if (blocks_per_cu >= 0) g_tn_blocks_per_cu = blocks_per_cu;  // 0: by problem size (tn_plan)
     if (slab_mb > 0) g_tn_slab_bytes = (long)slab_mb << 20;
 }
 
