@@ -742,6 +742,7 @@ inline void tn_tile(int N1, int N2, int& bn1, int& bn2) {
 // stream) win, except for the 56x56 layers whose gradients finish the backward: 0 = by size (tn_plan), 16 MB.  Same-box
 // bench, 2 interleaved rounds (PLX_TN_PLAN): 3/32 11.61k, 11.70k; 1/16 11.71k, 11.75k; by size 11.85k, 11.87k trials/h
 int g_tn_blocks_per_cu = 0;
+int g_tn_bpc_big = 3, g_tn_bpc_mid = 1;  // by-size plan: 56x56 layers, 28x28 layers (plx_set_tn_sizes)
 long g_tn_slab_bytes = 16l << 20;
 
 // bpc > 0 overrides the blocks-per-CU target (the stem's weight gradient runs alone at the end of the backward)
@@ -754,7 +755,9 @@ inline TnPlan tn_plan(int M, int N1, int N2, int num_cus, int bpc = 0) {
     // k-stages per block, slabs <= 32 MB (they are re-read by the reducer, mostly from the infinity cache)
     // g_tn_blocks_per_cu == 0: by size -- the 56x56 layers (M >= 400k rows) are the last weight gradients of the
     // backward, with little main-stream work left to hide them behind, so they get 3 blocks per CU; the rest 1
-    const int bpc_eff = bpc > 0 ? bpc : (g_tn_blocks_per_cu > 0 ? g_tn_blocks_per_cu : (M >= 400000 ? 3 : 1));
+    const int bpc_eff = bpc > 0 ? bpc
+                                : (g_tn_blocks_per_cu > 0 ? g_tn_blocks_per_cu
+                                                          : (M >= 400000 ? g_tn_bpc_big : M >= 150000 ? g_tn_bpc_mid : 1));
     int slices = (bpc_eff * (num_cus > 0 ? num_cus : 256)) / ntiles;
     const int by_depth = M / (4 * BK);
     const int by_bytes = (int)(g_tn_slab_bytes / (plane * 4));
@@ -827,6 +830,12 @@ void plx_set_nt_single_stage(int mode) { g_nt_single_stage = mode; }
 void plx_set_tn_plan(int blocks_per_cu, int slab_mb) {
     if (blocks_per_cu >= 0) g_tn_blocks_per_cu = blocks_per_cu;  // 0: by problem size (tn_plan)
     if (slab_mb > 0) g_tn_slab_bytes = (long)slab_mb << 20;
+}
+
+// A/B knob: blocks per CU of the by-size plan for the 56x56 (big) and 28x28 (mid) weight gradients
+void plx_set_tn_sizes(int big, int mid) {
+    if (big > 0) g_tn_bpc_big = big;
+    if (mid > 0) g_tn_bpc_mid = mid;
 }
 
 // floats of slab workspace plx_gemm_tn needs for this problem

@@ -157,6 +157,9 @@ def lib(name: str) -> ctypes.CDLL:
         if name == "plx_conv" and os.environ.get("PLX_TN_PLAN"):  # A/B knob: "blocks_per_cu,slab_mb"
             bpc, mb = (int(v) for v in os.environ["PLX_TN_PLAN"].split(","))
             handle.plx_set_tn_plan(bpc, mb)
+        if name == "plx_conv" and os.environ.get("PLX_TN_SIZES"):  # A/B knob: "big,mid" blocks per CU
+            big, mid = (int(v) for v in os.environ["PLX_TN_SIZES"].split(","))
+            handle.plx_set_tn_sizes(big, mid)
         _loaded[name] = handle
         return handle
 
@@ -224,6 +227,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gemm_nt_rows_per_block": [_I],
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
         "plx_set_tn_plan": [_I, _I],
+        "plx_set_tn_sizes": [_I, _I],
         "plx_set_nt_single_stage": [_I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
@@ -282,7 +286,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 
