@@ -297,7 +297,8 @@ def test_github_sso_flow(make_api):
     q = parse_qs(loc.query)
     assert loc.netloc == "gh.test" and q["client_id"] == ["cid"] and q["scope"] == ["user:email"]
     state = q["state"][0]
-    bad = c.get("/oauth/github/complete", params={"code": "good", "state": state[:-1] + "0"})
+    tampered = state[:-1] + ("1" if state[-1] == "0" else "0")  # always a different last character
+    bad = c.get("/oauth/github/complete", params={"code": "good", "state": tampered})
     assert bad.status_code == 400
     r = c.get("/oauth/github/complete", params={"code": "good", "state": state})
     assert r.status_code == 200, r.text
