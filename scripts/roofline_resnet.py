@@ -227,7 +227,7 @@ def main() -> None:
         ff = lambda: bn.plx_stem_bn_pool_forward(  # noqa
             x.data_ptr(), p.data_ptr(), idx.data_ptr(), n, h, w, c, weight.data_ptr(), bias.data_ptr(), 1e-5, 0.1,
             rm.data_ptr(), rv.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(), stats[2 * c:].data_ptr(),
-            ws.data_ptr(), cptr, st)
+            ws.data_ptr(), None, 0, cptr, st)
 
         def fu():
             bn.plx_bn_forward(x.data_ptr(), None, y.data_ptr(), m, c, weight.data_ptr(), bias.data_ptr(), 1e-5, 0.1,
