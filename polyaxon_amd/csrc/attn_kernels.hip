@@ -128,9 +128,8 @@ __device__ __forceinline__ f32x16 zero16() {
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __device__ __forceinline__ uint2 pack4(float a, float b, float c, float d) {
-  auto bits = [](float f) -> uint32_t {
-    uint32_t u = __float_as_uint(f);
-    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+  auto bits = [](float f) -> uint32_t {  // hardware RNE conversion (v_cvt_pk_bf16_f32)
+    return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)f);
   };
   return make_uint2(bits(a) | (bits(b) << 16), bits(c) | (bits(d) << 16));
 }

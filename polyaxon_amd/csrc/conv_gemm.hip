@@ -135,11 +135,9 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, uint32_t off, v
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)l, 16, off, 0, 0, 0);
 }
 
+// round to nearest even with the hardware conversion (v_cvt_pk_bf16_f32: one instruction per pair, NaN-preserving)
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-    uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
-    ua += 0x7fffu + ((ua >> 16) & 1u);   // round to nearest even
-    ub += 0x7fffu + ((ub >> 16) & 1u);
-    return (ua >> 16) | (ub & 0xffff0000u);
+    return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
 }
 
 // ------------------------------------------------------------------------------------------- NT GEMM

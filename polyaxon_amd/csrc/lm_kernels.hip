@@ -30,11 +30,8 @@ struct alignas(16) bf16x8 {
 };
 
 __device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+__device__ __forceinline__ uint16_t f2bf(float f) {  // hardware RNE conversion, NaN stays NaN
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
 }
 
 inline int grid_for(int64_t items) {

@@ -103,10 +103,8 @@ typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float bf16_to_f(unsigned short h) { return __uint_as_float((uint32_t)h << 16); }
 
-__device__ __forceinline__ unsigned short f_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  u += 0x7fffu + ((u >> 16) & 1u);  // round to nearest even (finite inputs)
-  return (unsigned short)(u >> 16);
+__device__ __forceinline__ unsigned short f_to_bf16(float f) {  // hardware RNE conversion (v_cvt_pk_bf16_f32)
+  return __builtin_bit_cast(unsigned short, (__bf16)f);
 }
 
 __global__ __launch_bounds__(kBlock) void adamw_mixed_kernel(float4* __restrict__ p, u16x4* __restrict__ g,
