@@ -738,7 +738,8 @@ inline void tn_tile(int N1, int N2, int& bn1, int& bn2) {
 // Swept in isolation (scripts/diag_wgrad_plan.py) 3 / 32 MB was best; in the training step the weight gradients run on
 // the side stream beside the data-gradient chain, and there fewer slices (less slab traffic competing with the main
 // stream) win, except for the 56x56 layers whose gradients finish the backward: 0 = by size (tn_plan), 16 MB.  Same-box
-// bench, 2 interleaved rounds (PLX_TN_PLAN): 3/32 11.61k, 11.70k; 1/16 11.71k, 11.75k; by size 11.85k, 11.87k trials/h
+// bench, 2 interleaved rounds (PLX_TN_PLAN): 3/32 11.61k, 11.70k; 1/16 11.71k, 11.75k; by size 11.85k, 11.87k trials/h.
+// Slab cap under the by-size plan: 8 MB 10.62k / 10.60k (too few slices), 16 MB 11.92k / 11.93k, 32 MB 11.91k / 11.91k
 int g_tn_blocks_per_cu = 0;
 int g_tn_bpc_big = 3, g_tn_bpc_mid = 1;  // by-size plan: 56x56 layers, 28x28 layers (plx_set_tn_sizes)
 long g_tn_slab_bytes = 16l << 20;
