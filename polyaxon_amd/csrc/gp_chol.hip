@@ -20,6 +20,10 @@
 //   gp_chol_update_kernel  trailing update A[i][j] -= sum_k P[i][k] P[j][k] over the lower-trailing square and
 //                          every appended row: 64x64 output tiles, 256 threads x 4x4 fp64 accumulators, both
 //                          panel slices staged in LDS (row stride 33 doubles: conflict-free column reads).
+// Every panel workgroup reads the diagonal block A11 from a per-matrix scratch copy (D[b], PB x PB), never from
+// A itself: workgroup 0 overwrites A11 with L11 inside the same launch, and workgroups are not ordered, so a
+// workgroup reading A11 from A could see L11 and solve its rows against the wrong block.  The copy is made by
+// gp_chol_diag_copy_kernel for the first panel and by the update tile that produces the next A11 afterwards.
 //   gp_lml_kernel          per batch entry: -0.5 |z|^2 - sum log L_jj - n/2 log 2 pi, -inf when not SPD
 //                          (sklearn semantics: a failed factorisation scores -inf, no jitter retry).
 #include <hip/hip_runtime.h>
@@ -49,7 +53,8 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // Every lane scales its own a_k and applies a_j -= l_k l_jk (j > k).  So the factorisation of L11 and the
 // solve of the rows below (x = a L11^-T) are the same 32-step register loop.
 __global__ __launch_bounds__(PT) void gp_chol_panel_kernel(double* __restrict__ A, int n, int rows, int ld,
-                                                           int64_t bstride, int c, int* __restrict__ status) {
+                                                           int64_t bstride, int c, int* __restrict__ status,
+                                                           const double* __restrict__ D) {
   double* M = A + (int64_t)blockIdx.y * bstride;
   const int w = min(PB, n - c);
   const int tid = threadIdx.x;
@@ -57,7 +62,9 @@ __global__ __launch_bounds__(PT) void gp_chol_panel_kernel(double* __restrict__ 
   const int r = diag ? c + tid : c + w + blockIdx.x * (PT - PB) + (tid - PB);
   const bool live = diag ? tid < w : r < rows;
   double a[PB];
-  const double* src = M + (int64_t)(live ? r : c) * ld + c;
+  // diagonal-block rows come from the scratch copy (row stride PB), the rows below from A (each owned by this lane)
+  const double* src = diag ? D + (int64_t)blockIdx.y * PB * PB + (live ? tid : 0) * PB
+                           : M + (int64_t)(live ? r : c) * ld + c;
 #pragma unroll
   for (int j = 0; j < PB; ++j) a[j] = (live && j < w && (!diag || j <= tid)) ? src[j] : (diag && j == tid ? 1.0 : 0.0);
   int bad = 0;
@@ -90,7 +97,7 @@ __global__ __launch_bounds__(PT) void gp_chol_panel_kernel(double* __restrict__ 
 }
 
 __global__ __launch_bounds__(256) void gp_chol_update_kernel(double* __restrict__ A, int n, int rows, int ld,
-                                                             int64_t bstride, int c, int w) {
+                                                             int64_t bstride, int c, int w, double* __restrict__ D) {
   const int c0 = c + w;
   const int i0 = c0 + blockIdx.y * UT, j0 = c0 + blockIdx.x * UT;
   if (i0 < n && j0 > i0 + UT - 1) return;  // tile strictly above the diagonal of the square part
@@ -126,8 +133,24 @@ __global__ __launch_bounds__(256) void gp_chol_update_kernel(double* __restrict_
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int j = j0 + tx + 16 * s;
-      if (j < n && (i >= n || j <= i)) M[(int64_t)i * ld + j] -= acc[q][s];
+      if (j < n && (i >= n || j <= i)) {
+        const double v = M[(int64_t)i * ld + j] - acc[q][s];
+        M[(int64_t)i * ld + j] = v;
+        // the next panel's diagonal block (rows / columns [c0, c0 + PB)): its scratch copy for the panel kernel
+        if (i < n && i < c0 + PB && j < c0 + PB) D[(int64_t)blockIdx.z * PB * PB + (i - c0) * PB + (j - c0)] = v;
+      }
     }
+  }
+}
+
+// First panel's diagonal block -> scratch (lower triangle incl. the diagonal; the rest is never read)
+__global__ __launch_bounds__(256) void gp_chol_diag_copy_kernel(const double* __restrict__ A, int n, int ld,
+                                                                int64_t bstride, double* __restrict__ D) {
+  const double* M = A + (int64_t)blockIdx.x * bstride;
+  const int w = min(PB, n);
+  for (int e = threadIdx.x; e < PB * PB; e += 256) {
+    const int i = e / PB, j = e % PB;
+    if (i < w && j <= i) D[(int64_t)blockIdx.x * PB * PB + e] = M[(int64_t)i * ld + j];
   }
 }
 
@@ -202,24 +225,28 @@ __global__ __launch_bounds__(256) void gp_acq_rows_kernel(const float* __restric
 }  // namespace
 
 // In-place blocked Cholesky of nb matrices (see the layout above). status: int[nb], zeroed by the caller;
-// status[b] = 1-based column of the first non-positive pivot.
+// status[b] = 1-based column of the first non-positive pivot.  scratch: device fp64 [nb][PB][PB] (contents ignored).
 PLX_API int plx_gp_chol_aug_f64(double* A, int n, int rows, int ld, long long bstride, int nb, int* status,
-                                hipStream_t stream) {
-  if (n <= 0 || rows < n || ld < n || nb <= 0) return 1;
+                                double* scratch, hipStream_t stream) {
+  if (n <= 0 || rows < n || ld < n || nb <= 0 || scratch == nullptr) return 1;
+  hipLaunchKernelGGL(gp_chol_diag_copy_kernel, dim3(nb), dim3(256), 0, stream, A, n, ld, (int64_t)bstride, scratch);
   for (int c = 0; c < n; c += PB) {
     const int w = n - c < PB ? n - c : PB;
     const int below = rows - c - w;
     const int gx = below > 0 ? (below + PT - PB - 1) / (PT - PB) : 1;
     hipLaunchKernelGGL(gp_chol_panel_kernel, dim3(gx, nb), dim3(PT), 0, stream, A, n, rows, ld, (int64_t)bstride,
-                       c, status);
+                       c, status, (const double*)scratch);
     const int c0 = c + w;
     if (c0 < n) {
       dim3 grid((n - c0 + UT - 1) / UT, (rows - c0 + UT - 1) / UT, nb);
-      hipLaunchKernelGGL(gp_chol_update_kernel, grid, dim3(256), 0, stream, A, n, rows, ld, (int64_t)bstride, c, w);
+      hipLaunchKernelGGL(gp_chol_update_kernel, grid, dim3(256), 0, stream, A, n, rows, ld, (int64_t)bstride, c, w,
+                         scratch);
     }
   }
   return (int)hipGetLastError();
 }
+
+PLX_API int plx_gp_chol_scratch_doubles() { return PB * PB; }
 
 // LML per batch entry of a factor produced by plx_gp_chol_aug_f64 with y appended as row n.
 PLX_API int plx_gp_lml_f64(const double* A, int n, int ld, long long bstride, int nb, const int* status, double* out,

@@ -23,6 +23,8 @@ import glob
 import logging
 import os
 import re
+import time
+import threading
 from typing import Any, Callable, Dict, List, Optional
 
 from polyaxon_amd.obs.telemetry import _run_json
@@ -139,32 +141,62 @@ class GpuHealthProbe:
     """Callable returning the indices of unhealthy devices (Polyflow ``health_check``).
 
     A device is unhealthy when its uncorrectable RAS error count rose since the first probe, or when it vanished
-    from the KFD topology.  ``events`` receives (kind, level, message, data) the first time a device turns bad."""
+    from the KFD topology.  ``events`` receives (kind, level, message, data) the first time a device turns bad.
+
+    Devices are identified by a stable key (KFD ``unique_id``, else the DRM render minor, else the KFD node id)
+    mapped to the HIP index they had at the first probe, so a device that drops out is reported under its own
+    index, not under the highest ones.  The sysfs RAS counters are the source; ``amd-smi metric --ecc`` is used
+    only when the driver exposes no RAS files at all (decided once, at the first probe), never merely because
+    every count is zero.  With ``background=True`` (the scheduler's default) a call never blocks: it returns the
+    devices known bad so far, starts a probe on a worker thread when the last one is older than ``interval_s``,
+    and delivers the events that probe produced on the calling (scheduler) thread."""
 
     def __init__(self, sysfs: str = "/sys", use_smi: bool = True,
-                 events: Optional[Callable[[str, str, str, Dict[str, Any]], None]] = None):
+                 events: Optional[Callable[[str, str, str, Dict[str, Any]], None]] = None,
+                 background: bool = False, interval_s: float = 5.0):
         self.sysfs = sysfs
         self.use_smi = use_smi
         self.events = events
+        self.background = background
+        self.interval_s = interval_s
         self.baseline: Dict[int, int] = {}
+        self.keys: Optional[Dict[str, int]] = None  # stable device key -> HIP index at the first probe
         self.known: Optional[int] = None
         self.bad: set = set()
+        self._smi_source: Optional[bool] = None     # True: no RAS files anywhere, counts come from amd-smi
+        self._lock = threading.Lock()
+        self._pending: List[tuple] = []
+        self._thread: Optional[threading.Thread] = None
+        self._last = 0.0
 
-    def _render_minors(self) -> List[str]:
-        return [g["drm_render_minor"] for g in kfd_gpus(self.sysfs)]
+    @staticmethod
+    def _key(g: Dict[str, Any]) -> str:
+        for k in ("serial", "drm_render_minor"):
+            v = str(g.get(k) or "").strip()
+            if v and v != "0":
+                return f"{k}:{v}"
+        return f"kfd:{g.get('kfd_node')}"
 
-    def uncorrectable(self) -> Dict[int, int]:
-        """Per device index: total uncorrectable errors over every RAS block the driver reports."""
+    def _devices(self) -> List[Dict[str, Any]]:
+        return kfd_gpus(self.sysfs)
+
+    def uncorrectable(self, devices: Optional[List[Dict[str, Any]]] = None) -> Dict[int, int]:
+        """Per current device index: total uncorrectable errors over every RAS block the driver reports."""
+        devices = self._devices() if devices is None else devices
         out: Dict[int, int] = {}
-        for idx, minor in enumerate(self._render_minors()):
-            dev = os.path.join(self.sysfs, "class", "drm", f"renderD{minor}", "device", "ras")
+        have_ras = False
+        for idx, g in enumerate(devices):
+            dev = os.path.join(self.sysfs, "class", "drm", f"renderD{g['drm_render_minor']}", "device", "ras")
             total = 0
             for f in glob.glob(os.path.join(dev, "*_err_count")):
+                have_ras = True
                 m = re.search(r"ue:\s*(\d+)", _read(f) or "")
                 if m:
                     total += int(m.group(1))
             out[idx] = total
-        if self.use_smi and not any(out.values()):
+        if self._smi_source is None:
+            self._smi_source = bool(self.use_smi and devices and not have_ras)
+        if self._smi_source:
             data = _run_json(["amd-smi", "metric", "--ecc", "--json"], timeout=10.0)
             if isinstance(data, list):
                 for i, g in enumerate(data):
@@ -177,27 +209,63 @@ class GpuHealthProbe:
                         pass
         return out
 
+    def probe(self) -> List[int]:
+        """One synchronous probe: updates the bad set and queues an event per newly bad device."""
+        devices = self._devices()
+        counts = self.uncorrectable(devices)
+        keys = {self._key(g): i for i, g in enumerate(devices)}
+        with self._lock:
+            if self.keys is None:
+                self.keys = dict(keys)
+                self.known = len(devices)
+                self.baseline = {i: counts.get(i, 0) for i in range(len(devices))}
+            bad = set()
+            # counts are per CURRENT index; map them back to the index each device had at the first probe
+            for key, cur in keys.items():
+                orig = self.keys.get(key)
+                if orig is None:
+                    continue  # a device that was not there at the start is not ours to place
+                if counts.get(cur, 0) > self.baseline.get(orig, counts.get(cur, 0)):
+                    bad.add(orig)
+            vanished = {orig for key, orig in self.keys.items() if key not in keys}
+            bad |= vanished
+            new = bad - self.bad
+            self.bad |= bad
+            by_orig = {self.keys[k]: counts.get(c) for k, c in keys.items() if k in self.keys}
+            for idx in sorted(new):
+                msg = (f"device {idx} left the KFD topology" if idx in vanished else
+                       f"device {idx} unhealthy: uncorrectable RAS errors {by_orig.get(idx, 'n/a')} "
+                       f"(baseline {self.baseline.get(idx, 'n/a')})")
+                log.error(msg)
+                self._pending.append(("gpu_unhealthy", "error", msg, {"device": idx}))
+            return sorted(self.bad)
+
+    def _flush(self) -> None:
+        with self._lock:
+            pending, self._pending = self._pending, []
+        if self.events is not None:
+            for ev in pending:
+                self.events(*ev)
+
+    def _worker(self) -> None:
+        try:
+            self.probe()
+        except Exception:
+            log.exception("GPU health probe failed")
+
     def __call__(self) -> List[int]:
-        counts = self.uncorrectable()
-        n = len(counts)
-        if self.known is None:
-            self.known = n
-            self.baseline = dict(counts)
-        bad = set()
-        for idx, v in counts.items():
-            if v > self.baseline.get(idx, v):
-                bad.add(idx)
-        if n < (self.known or 0):  # a device dropped out of the topology (reset / fallen off the bus)
-            bad.update(range(n, self.known))
-        new = bad - self.bad
-        self.bad |= bad
-        for idx in sorted(new):
-            msg = f"device {idx} unhealthy: uncorrectable RAS errors {counts.get(idx, 'n/a')} " \
-                  f"(baseline {self.baseline.get(idx, 'n/a')})" if idx in counts else f"device {idx} left the KFD topology"
-            log.error(msg)
-            if self.events is not None:
-                self.events("gpu_unhealthy", "error", msg, {"device": idx})
-        return sorted(self.bad)
+        if not self.background:
+            out = self.probe()
+            self._flush()
+            return out
+        now = time.monotonic()
+        if (self._thread is None or not self._thread.is_alive()) and now - self._last >= self.interval_s:
+            self._last = now
+            self._thread = threading.Thread(target=self._worker, name="plx-gpu-health", daemon=True)
+            self._thread.start()
+        self._flush()
+        with self._lock:
+            return sorted(self.bad)
 
 
 def gpu_fault_in_log(path: str, tail_bytes: int = 65536) -> Optional[str]:

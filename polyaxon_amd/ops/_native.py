@@ -214,7 +214,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gp_chol": [_P, _I, _I, _P, _P],
         "plx_gp_kmat_batch_f64": [_P, _I, _I, _P, _I, _P, _I, _L, _I, _D, _D, _D, _P, _P, _D, _I, _P],
         "plx_gp_matern_table": [_D, _D, _D, _I, _P, _P, _P],
-        "plx_gp_chol_aug_f64": [_P, _I, _I, _I, _L, _I, _P, _P],
+        "plx_gp_chol_aug_f64": [_P, _I, _I, _I, _L, _I, _P, _P, _P],
+        "plx_gp_chol_scratch_doubles": [],
         "plx_gp_lml_f64": [_P, _I, _I, _L, _I, _P, _P, _P],
         "plx_gp_acq_rows": [_P, _I, _I, _P, _F, _I, _F, _F, _F, _P, _P, _P, _P],
         "plx_gp_predict_acq": [_P, _I, _P, _I, _I, _P, _I, _P, _I, _F, _F, _F, _F, _I, _F, _F, _F, _P, _P, _P, _P,

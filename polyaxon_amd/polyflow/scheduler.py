@@ -193,7 +193,8 @@ class Polyflow:
         if health_check is None and allocator is None and probe_on:
             from polyaxon_amd.obs.nodes import GpuHealthProbe
 
-            health_check = GpuHealthProbe(events=self.cluster_event)
+            health_check = GpuHealthProbe(events=self.cluster_event, background=True,
+                                          interval_s=max(1.0, reconcile_s))
         self.health_check = health_check
         self._unhealthy: set = set()
         self._pool = None  # resident executors (polyflow/pool.py), created on first use

@@ -309,7 +309,10 @@ class HipGP:
         nb, rows = int(A.shape[0]), int(A.shape[1])
         assert A.dtype == t.float64 and A.is_contiguous() and A.shape[2] == n and rows >= n
         status = t.zeros(nb, dtype=t.int32, device=self.device)
-        rc = self.lib.plx_gp_chol_aug_f64(A.data_ptr(), n, rows, n, rows * n, nb, status.data_ptr(), self._stream())
+        # per-matrix copy of the current diagonal block (the panel launch overwrites A11 in place, see gp_chol.hip)
+        scratch = t.empty(nb * int(self.lib.plx_gp_chol_scratch_doubles()), dtype=t.float64, device=self.device)
+        rc = self.lib.plx_gp_chol_aug_f64(A.data_ptr(), n, rows, n, rows * n, nb, status.data_ptr(),
+                                          scratch.data_ptr(), self._stream())
         self._native.check(rc, "plx_gp_chol_aug_f64")
         return status
 

@@ -253,13 +253,23 @@ class BaseSpecification:
 class ExperimentSpecification(BaseSpecification):
     KIND = Kinds.EXPERIMENT
 
+    def __init__(self, data: Dict[str, Any], render_templates: bool = True, group_trial: bool = False):
+        # group_trial: the spec of one trial of a group (GroupSpecification.get_experiment_spec).  Only such a spec
+        # may name a resident executor without a `run`: the group's resident driver trains it; the scheduler has no
+        # resident path for a standalone experiment, so one would only fail later, at spawn ("nothing to run").
+        self._group_trial = group_trial
+        super().__init__(data, render_templates=render_templates)
+
     def _parse(self, d):
         super()._parse(d)
         if d.get("hptuning") is not None:
             raise PolyaxonfileError("an experiment cannot define `hptuning`; use kind: group")
         ex = self.environment.executor
+        if ex is not None and ex.resident and not getattr(self, "_group_trial", False):
+            raise PolyaxonfileError("`environment.executor: resident` runs the trials of a group (kind: group); "
+                                    "a standalone experiment uses executor: process with a `run` section")
         if self.run is None and d.get("model") is None and not (ex is not None and ex.resident):
-            raise PolyaxonfileError("an experiment requires a `run` section (or `environment.executor: resident`)")
+            raise PolyaxonfileError("an experiment requires a `run` section")
 
 
 class JobSpecification(BaseSpecification):
@@ -352,7 +362,7 @@ class GroupSpecification(BaseSpecification):
         return data
 
     def get_experiment_spec(self, matrix_declaration: Dict[str, Any]) -> ExperimentSpecification:
-        return ExperimentSpecification(self.experiment_data(matrix_declaration))
+        return ExperimentSpecification(self.experiment_data(matrix_declaration), group_trial=True)
 
 
 def _first_value(m):

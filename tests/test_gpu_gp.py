@@ -137,6 +137,38 @@ def test_blocked_cholesky_with_appended_rows(cuda, n):
         np.testing.assert_allclose(out[b, n:], Z, rtol=1e-7, atol=1e-7 * max(1.0, np.abs(Z).max()))
 
 
+def test_blocked_cholesky_large_grid_matches_lapack(cuda):
+    """Many matrices with many appended rows: the panel launch's grid (rows / 32 x nb workgroups) is far larger than
+    one residency wave, so workgroups of one panel run at very different times.  Every one must solve against the
+    same A11 (the scratch copy), not against the L11 that workgroup 0 writes into A during that launch."""
+    import torch
+    from scipy.linalg import solve_triangular
+
+    from polyaxon_amd.polytune.bo import HipGP, kernel_np
+
+    rng = np.random.RandomState(11)
+    n, extra, nb = 320, 1700, 24
+    A = np.zeros((nb, n + extra, n))
+    refs = []
+    for b in range(nb):
+        X = rng.uniform(-2, 2, size=(n, 5))
+        K = kernel_np(X, X, "rbf", 0.5 + 0.1 * b, 2.5) + 1e-4 * np.eye(n)
+        R = rng.randn(extra, n)
+        A[b, :n], A[b, n:] = np.tril(K), R
+        L = np.linalg.cholesky(K)
+        refs.append((L, solve_triangular(L, R.T, lower=True).T))
+    Ad = torch.tensor(A, device=cuda)
+    gp = HipGP(cuda)
+    for _ in range(3):  # repeated launches over fresh copies: a race would show on some of them
+        Ad.copy_(torch.tensor(A, device=cuda))
+        status = gp.chol_aug(Ad, n).cpu().numpy()
+        out = Ad.cpu().numpy()
+        assert (status == 0).all()
+        for b, (L, Z) in enumerate(refs):
+            np.testing.assert_allclose(np.tril(out[b, :n]), L, rtol=1e-8, atol=1e-8)
+            np.testing.assert_allclose(out[b, n:], Z, rtol=1e-6, atol=1e-6 * max(1.0, np.abs(Z).max()))
+
+
 def test_blocked_cholesky_flags_indefinite_entry_only(cuda):
     import torch
 

@@ -69,6 +69,72 @@ def test_health_probe_flags_new_uncorrectable_errors_and_lost_devices(tmp_path):
     assert probe() == [1, 2] and len(events) == 2
 
 
+def test_health_probe_names_the_device_that_vanished_not_the_last_index(tmp_path):
+    """Device 0 (of 3) falls off the bus: the probe must report index 0, not the highest index (2), although the
+    remaining devices now enumerate as 0 and 1; a later RAS rise on the old device 2 (now enumerated 1) is still
+    reported as 2."""
+    import shutil
+
+    sysfs = _fake_sysfs(tmp_path / "sys", n_gpus=3)
+    probe = GpuHealthProbe(str(sysfs), use_smi=False)
+    assert probe() == []
+    shutil.rmtree(sysfs / "class" / "kfd" / "kfd" / "topology" / "nodes" / "1")
+    assert probe() == [0]
+    (sysfs / "class" / "drm" / "renderD130" / "device" / "ras" / "umc_err_count").write_text("ue: 1\nce: 3\n")
+    assert probe() == [0, 2]
+
+
+def test_health_probe_uses_amd_smi_only_without_ras_files(tmp_path, monkeypatch):
+    """Zero RAS counts on a healthy node must not trigger an amd-smi call per probe (it blocked the scheduler
+    thread up to 10 s every reconcile); amd-smi is the source only when the driver exposes no RAS files."""
+    import polyaxon_amd.obs.nodes as nodes
+
+    calls = []
+    monkeypatch.setattr(nodes, "_run_json", lambda cmd, timeout=0: calls.append(cmd) or [])
+    sysfs = _fake_sysfs(tmp_path / "sys", n_gpus=2)
+    probe = GpuHealthProbe(str(sysfs), use_smi=True)
+    for _ in range(3):
+        assert probe() == []
+    assert calls == []
+    import shutil
+
+    bare = _fake_sysfs(tmp_path / "bare", n_gpus=2)
+    shutil.rmtree(bare / "class" / "drm")
+    probe2 = GpuHealthProbe(str(bare), use_smi=True)
+    probe2()
+    probe2()
+    assert len(calls) == 2 and calls[0][:3] == ["amd-smi", "metric", "--ecc"]
+
+
+def test_health_probe_background_mode_never_blocks_the_caller(tmp_path, monkeypatch):
+    """Scheduler mode: the call returns at once; the probe runs on a worker thread and its events are delivered
+    on the next call (the scheduler thread), not from the worker."""
+    import threading
+
+    sysfs = _fake_sysfs(tmp_path / "sys", n_gpus=2)
+    events = []
+    probe = GpuHealthProbe(str(sysfs), use_smi=False, background=True, interval_s=0.0,
+                           events=lambda *a: events.append((threading.current_thread().name, a)))
+    gate = threading.Event()
+    real = probe.uncorrectable
+
+    def slow(devices=None):
+        gate.wait(5)
+        return real(devices)
+
+    monkeypatch.setattr(probe, "uncorrectable", slow)
+    t0 = time.time()
+    assert probe() == []
+    assert time.time() - t0 < 0.5
+    gate.set()
+    probe._thread.join(5)
+    (sysfs / "class" / "drm" / "renderD129" / "device" / "ras" / "umc_err_count").write_text("ue: 4\nce: 3\n")
+    probe()
+    probe._thread.join(5)
+    assert probe() == [1]
+    assert len(events) == 1 and events[0][0] == threading.current_thread().name
+
+
 def test_scheduler_marks_unhealthy_devices_and_records_events(tmp_path):
     sysfs = _fake_sysfs(tmp_path / "sys", n_gpus=2)
     store = Store(str(tmp_path / "plx" / "polyaxon.sqlite"))

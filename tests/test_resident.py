@@ -282,6 +282,12 @@ def test_resident_spec_validation():
     bad["environment"]["resources"] = {"gpu": 1.5}
     with pytest.raises(PolyaxonfileError):
         specification_for(bad)
+    # a standalone experiment cannot name a resident executor (only a group's trials are trained by one)
+    xp = {"version": 1, "kind": "experiment", "environment": _group()["environment"]}
+    with pytest.raises(PolyaxonfileError):
+        specification_for(xp)
+    # ... while the group's own trial specs (no run section) still parse
+    assert specification_for(_group()).get_experiment_spec({"lr": 0.01, "momentum": 0.9, "units": 1}).run is None
 
 
 def test_resident_rejects_non_hyperband(tmp_path, cpu_pool_env):
