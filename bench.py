@@ -5,20 +5,26 @@ BASELINE.json config 3 ("Hyperband/ASHA sweep of ResNet-50 on synthetic ImageNet
 64 brackets"), measured through the real control plane:
 
 * one rank per GPU (``torchrun``, or ``--gpus N`` spawns the N ranks itself before anything touches a GPU);
-  every rank builds a **resident trial executor** (polyflow/resident.py) for the ResNet-50 program and
-  attaches it to the **polyflow scheduler** that rank 0 runs (SQLite store, FSMs, group drivers);
-* the timed work is ``--steps K`` complete Hyperband sweeps **per GPU**: rank 0 submits ``K × N`` Polyaxonfile
-  groups (``hyperband: max_iter 9, eta 3, resume: true``; 3 brackets and 23 trials each, reference-exact
-  bracket arithmetic) with ``environment.executor: resident``; the scheduler spreads their ``3·K·N`` brackets
-  over the N executors (``--steps 3`` at 8 GPUs = 72 brackets, ``--steps 20`` = 480), every executor interleaves
-  its brackets and decides each round's promotions with one HIP top-k launch, and every trial is an experiment
-  row with its status history, metric and RESUME lineage.  The timed region starts after a barrier (after
-  ``--warmup W`` untimed sweeps per GPU through the same path) and ends when every group has SUCCEEDED and
-  every rank passed the final barrier: only whole sweeps are timed, never a prefix;
-* one Hyperband resource unit = ``--unit-steps`` full training steps (bf16 forward + backward + fused SGD) at
-  ``--batch`` 224×224 images; the data is a fresh, learnable synthetic batch generated on the device every step
-  (ops/synth.py), so ``wall_clock_to_target_s`` (first trial whose committed loss is below ``--target``,
-  measured from the start of the timed region) reflects real learning, not memorisation.
+  every rank builds a **resident trial executor** (polyflow/resident.py) for the ResNet-50 program, pinned to the
+  CPUs local to its GPU, and attaches it to the **polyflow scheduler**;
+* the scheduler (SQLite store, FSMs, group drivers) runs in a process of its own that never touches a GPU -- the
+  ``--gpus N`` launcher itself, or a control process rank 0 starts before its own GPU initialisation under
+  torchrun -- so no rank shares its interpreter (and GIL) with the scheduler's store writes and event handling;
+* the timed work is ``--steps K`` complete sweeps **per GPU**: ``K × N`` Polyaxonfile groups with
+  ``environment.executor: resident``.  ``--search hyperband`` (default; ``max_iter 9, eta 3, resume: true``:
+  3 brackets and 23 trials each, reference-exact bracket arithmetic) spreads its ``3·K·N`` brackets over the N
+  executors, each executor interleaves its brackets and decides each round's promotions with one HIP top-k launch;
+  ``--search asha`` runs each sweep as one asynchronous successive-halving search (min 1, max 9, eta 3 resource
+  units, ``--asha-n`` configs; no rung barrier).  Every trial is an experiment row with its status history, metric
+  and RESUME lineage.  The timed region starts after a barrier (after ``--warmup W`` untimed sweeps per GPU through
+  the same path) and ends when every group has SUCCEEDED and every rank passed the final barrier: only whole sweeps
+  are timed, never a prefix;
+* one resource unit = ``--unit-steps`` full training steps (bf16 forward + backward + fused SGD) at ``--batch``
+  224×224 images; the data is a fresh, learnable synthetic batch generated on the device every step
+  (ops/synth.py).  A trial's metric is its mean loss over its last 4 steps, each measured on a batch the weights
+  had never seen (the forward of a fresh batch precedes its update), so it is a held-out estimate;
+  ``wall_clock_to_target_s`` = time from the start of the timed region to the first trial whose metric is below
+  ``--target`` (set near the synthetic task's floor at this budget, so reaching it separates search strategies).
 
 ``value`` = trials completed in the timed region (all GPUs) / elapsed (max over ranks) × 3600.
 Data: synthetic ImageNet-shape tensors generated on the device, random-init weights (no datasets available).
@@ -46,92 +52,99 @@ MAX_ITER, ETA = 9, 3
 def _args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3, help="timed Hyperband sweeps per GPU (3 brackets, 23 trials each)")
+    ap.add_argument("--steps", type=int, default=3, help="timed sweeps per GPU (hyperband: 3 brackets, 23 trials)")
     ap.add_argument("--warmup", type=int, default=1, help="untimed sweeps per GPU through the same path")
+    ap.add_argument("--search", choices=("hyperband", "asha"), default="hyperband")
+    ap.add_argument("--asha-n", type=int, default=37,
+                    help="configs per ASHA sweep (37 at min 1 / max 9 / eta 3 ~ the 87 units of a Hyperband sweep)")
     ap.add_argument("--batch", type=int, default=256, help="per-trial batch (one trial per GPU at a time)")
     ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--unit-steps", type=int, default=4, help="training steps per Hyperband resource unit")
+    ap.add_argument("--unit-steps", type=int, default=4, help="training steps per resource unit")
     ap.add_argument("--target", type=float, default=1.0, help="loss target for wall-clock-to-target")
     ap.add_argument("--signal", type=float, default=0.5, help="class-pattern amplitude of the synthetic data")
+    ap.add_argument("--active-classes", type=int, default=100, help="classes the synthetic task draws from")
     ap.add_argument("--max-active", type=int, default=8, help="brackets one executor interleaves")
     ap.add_argument("--graph", type=int, default=0,
                     help="replay each training step as a captured (and verified) hipGraph; measured 8 %% slower than eager "
                          "launches for this step on ROCm 7.2 (10.5k vs 11.4k trials/h, same box)")
     ap.add_argument("--cpu", action="store_true", help="CPU rehearsal (gloo, small ResNet, tiny images)")
+    ap.add_argument("--control-only", action="store_true", help=argparse.SUPPRESS)  # internal: the scheduler process
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 
 
-def group_spec(seed: int, program: str, params: dict, concurrency: int, max_active: int) -> dict:
-    return {
-        "version": 1, "kind": "group", "project": "bench_resnet50_hyperband",
-        "hptuning": {
-            "seed": seed, "concurrency": concurrency,
-            "hyperband": {"max_iter": MAX_ITER, "eta": ETA, "resource": {"name": "units", "type": "int"},
-                          "metric": {"name": "loss", "optimization": "minimize"}, "resume": True},
-            "matrix": {"lr": {"loguniform": [math.log(0.02), math.log(1.0)]},
-                       "momentum": {"uniform": [0.8, 0.95]},
-                       "weight_decay": {"loguniform": [math.log(1e-5), math.log(1e-3)]}},
-        },
-        "environment": {"resources": {"gpu": 1},
-                        "executor": {"kind": "resident", "program": program, "params": params,
-                                     "max_active_brackets": max_active}},
-    }
+def program_params(args):
+    if args.cpu:
+        return "resnet_tiny", {"batch": min(args.batch, 8), "image": min(args.image, 32),
+                               "unit_steps": min(args.unit_steps, 1), "grid": 4, "signal": args.signal,
+                               "active_classes": min(args.active_classes, 10), "data_seed": 1234}
+    return "resnet50", {"batch": args.batch, "image": args.image, "unit_steps": args.unit_steps, "signal": args.signal,
+                        "active_classes": args.active_classes, "graph": bool(args.graph), "data_seed": 1234}
 
 
-# ----------------------------------------------------------------------------- launcher (no GPU calls here)
-def _free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def group_spec(seed: int, program: str, params: dict, concurrency: int, max_active: int, search: str = "hyperband",
+               asha_n: int = 37) -> dict:
+    matrix = {"lr": {"loguniform": [math.log(0.02), math.log(1.0)]},
+              "momentum": {"uniform": [0.8, 0.95]},
+              "weight_decay": {"loguniform": [math.log(1e-5), math.log(1e-3)]}}
+    metric = {"name": "loss", "optimization": "minimize"}
+    resource = {"name": "units", "type": "int"}
+    if search == "asha":
+        hp = {"seed": seed, "concurrency": concurrency, "matrix": matrix,
+              "asha": {"min_resource": 1, "max_resource": MAX_ITER, "eta": ETA, "n_experiments": asha_n,
+                       "resource": resource, "metric": metric, "resume": True}}
+    else:
+        hp = {"seed": seed, "concurrency": concurrency, "matrix": matrix,
+              "hyperband": {"max_iter": MAX_ITER, "eta": ETA, "resource": resource, "metric": metric, "resume": True}}
+    return {"version": 1, "kind": "group", "project": "bench_resnet50_" + search, "hptuning": hp,
+            "environment": {"resources": {"gpu": 1},
+                            "executor": {"kind": "resident", "program": program, "params": params,
+                                         "max_active_brackets": max_active}}}
 
 
-def spawn_ranks(n: int, argv) -> int:
-    """``--gpus N`` without torchrun: start N rank processes (one per GPU) and wait for them.  The parent never
-    initialises the GPU runtime, so starting children is safe."""
-    env = dict(os.environ)
-    env.update({"WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port()),
-                "LOCAL_WORLD_SIZE": str(n)})
-    procs = []
-    for r in range(n):
-        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=e))
-    rc = 0
-    for p in procs:
-        rc = max(rc, p.wait())
-    return rc
+# ----------------------------------------------------------------------------- control (no GPU calls here)
+class ControlServer:
+    """The polyflow scheduler of the benchmark, in a process that never touches a GPU.  Accepts ``world`` executor
+    channels (hello ``{"rank": r}``) and rank 0's bench channel (hello ``{"bench": 1}``), runs the warm-up sweeps,
+    pauses the executors, waits for rank 0's ``go``, runs the timed sweeps, pauses again and sends the summary."""
 
-
-# ----------------------------------------------------------------------------- rank 0: scheduler + control
-class Control(threading.Thread):
-    def __init__(self, args, world: int, listener: socket.socket, program: str, params: dict, log):
-        super().__init__(name="bench-control", daemon=True)
+    def __init__(self, args, world: int, log=None):
         from polyaxon_amd.polyflow.devices import Device, DeviceAllocator
         from polyaxon_amd.polyflow.scheduler import Polyflow
 
-        self.args, self.world, self.listener = args, world, listener
-        self.program, self.params, self.log = program, params, log
+        self.args, self.world = args, world
+        self.program, self.params = program_params(args)
+        self.log = log or (lambda m: print(f"[control +{time.perf_counter() - T0:.1f}s] {m}", file=sys.stderr,
+                                           flush=True))
+        self.listener = socket.socket()
+        self.listener.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self.listener.bind(("127.0.0.1", 0))
+        self.listener.listen(world + 2)
+        self.port = self.listener.getsockname()[1]
         self.root = tempfile.mkdtemp(prefix="plx_bench_")
         self.flow = Polyflow(self.root, allocator=DeviceAllocator([Device(i) for i in range(world)]),
                              reconcile_s=0, clean_on_start=False).start()
-        self.t0_set = threading.Event()
-        self.t0_wall = 0.0
-        self.result = None
-        self.error = None
+        self.bench = None
 
-    def _attach_all(self) -> None:
+    def _accept(self) -> None:
         from polyaxon_amd.polyflow.resident import Channel
 
-        for _ in range(self.world):
+        execs = 0
+        self.listener.settimeout(900)
+        while execs < self.world or self.bench is None:
             sock, _ = self.listener.accept()
             sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             chan = Channel(sock)
-            hello = chan.recv(timeout=600)
+            hello = chan.recv(timeout=900)
+            if hello is None:
+                raise TimeoutError("a benchmark peer connected but sent no hello")
+            if hello.get("bench"):
+                self.bench = chan
+                continue
             self.flow.attach_resident(chan, int(hello["rank"]), self.program, self.params,
                                       max_active=self.args.max_active)
-        end = time.time() + 600
+            execs += 1
+        end = time.time() + 900
         while time.time() < end:
             snap = self.flow.call(lambda: self.flow.resident_pool().snapshot())
             if sum(1 for w in snap if w["ready"]) == self.world:
@@ -142,10 +155,11 @@ class Control(threading.Thread):
     def _sweeps(self, n: int, seed0: int):
         gids = []
         for i in range(n):
-            spec = group_spec(seed0 + i, self.program, self.params, self.world, self.args.max_active)
+            spec = group_spec(seed0 + i, self.program, self.params, self.world, self.args.max_active,
+                              self.args.search, self.args.asha_n)
             gids.append(self.flow.submit(spec)["id"])
         for g in gids:
-            st = self.flow.wait("group", g, timeout=3600, poll_s=0.05)
+            st = self.flow.wait("group", g, timeout=7200, poll_s=0.05)
             if st != "succeeded":
                 raise RuntimeError(f"group {g} ended {st}")
         return gids
@@ -160,29 +174,43 @@ class Control(threading.Thread):
                 done.set()
 
         self.flow.call(lambda: self.flow.resident_pool().pause_all(tag, on_paused))
-        if not done.wait(600):
+        if not done.wait(900):
             raise TimeoutError(f"executors did not pause ({tag})")
 
-    def run(self) -> None:
+    def serve(self) -> int:
+        rc = 0
         try:
-            self._attach_all()
+            self._accept()
             self.log(f"{self.world} resident executors ready; warm-up: {self.args.warmup} sweep(s)/GPU")
             if self.args.warmup:
                 self._sweeps(self.args.warmup * self.world, 10_000)
+            base = self.flow.call(lambda: self.flow.resident_pool().snapshot())
             self._pause("warm")
-            self.t0_set.wait()
+            go = self.bench.recv(timeout=900)
+            if go is None or go.get("op") != "go":
+                raise RuntimeError(f"expected go from rank 0, got {go!r}")
+            t0_wall = float(go["t0"])
             gids = self._sweeps(self.args.steps * self.world, 1)
             self._pause("timed")
-            self.result = self._summarise(gids)
-        except BaseException as e:  # surfaced by the main thread
-            self.error = e
-            self.t0_set.set()
+            self.bench.send({"ev": "result", "result": self._summarise(gids, t0_wall, base)})
+        except BaseException as e:  # rank 0 raises it; every executor is released so no rank hangs
+            rc = 1
             try:
                 self.flow.call(lambda: self.flow.resident_pool().pause_all("abort"))
             except Exception:
                 pass
+            if self.bench is not None:
+                try:
+                    self.bench.send({"ev": "error", "message": repr(e)})
+                except OSError:
+                    pass
+            self.log(f"control failed: {e!r}")
+        finally:
+            self.flow.shutdown(stop_running=False, timeout=10)
+            self.listener.close()
+        return rc
 
-    def _summarise(self, gids) -> dict:
+    def _summarise(self, gids, t0_wall: float, base) -> dict:
         st = self.flow.store
         q = ",".join("?" * len(gids))
         xs = st.list_experiments(ids=[r["id"] for r in st.execute(
@@ -192,9 +220,10 @@ class Control(threading.Thread):
         steps = sum(int(r["step"] or 0) for r in st.execute(
             f"SELECT m.step FROM experiment_metrics m JOIN experiments e ON e.id = m.experiment_id "
             f"WHERE e.group_id IN ({q})", gids).fetchall())
+        target = self.args.target
         hit = [x["finished_at"] for x in xs
-               if (x.get("last_metric") or {}).get("loss") is not None and x["last_metric"]["loss"] <= self.args.target]
-        ttt = (min(hit) - self.t0_wall) if hit else None
+               if (x.get("last_metric") or {}).get("loss") is not None and x["last_metric"]["loss"] <= target]
+        ttt = (min(hit) - t0_wall) if hit else None
         best = min((x["last_metric"]["loss"] for x in xs if (x.get("last_metric") or {}).get("loss") is not None),
                    default=None)
         # the status history every trial must show (reference ExperimentLifeCycle)
@@ -203,24 +232,101 @@ class Control(threading.Thread):
         fsm_ok = all([s["status"] for s in st.experiment_statuses(x["id"])] == want
                      for x in sample if x["status"] == "succeeded")
         resumed = sum(1 for x in xs if x["cloning_strategy"] == "resume")
-        brackets = sum(1 for it in st.execute(
+        units = sum(1 for it in st.execute(
             f"SELECT data FROM experiment_group_iterations WHERE group_id IN ({q})", gids).fetchall()
             if json.loads(it["data"]).get("bracket_iteration") == 0)
         pool = self.flow.call(lambda: self.flow.resident_pool().snapshot())
+        b = {w["wid"]: w for w in base}
+        execs = []
+        for w in pool:
+            w0 = b.get(w["wid"], {})
+            execs.append({"wid": w["wid"], "devices": w["devices"], "pid": w["pid"],
+                          "load_units": round(w["assigned_units"] - w0.get("assigned_units", 0.0), 3),
+                          "units_of_work": w["assigned"] - w0.get("assigned", 0)})
         return {"trials": trials, "succeeded": ok, "train_steps": steps, "ttt": ttt, "best": best,
-                "fsm_ok": fsm_ok, "resumed": resumed, "brackets": brackets, "groups": len(gids), "pool": pool}
+                "fsm_ok": fsm_ok, "resumed": resumed, "brackets": units, "groups": len(gids), "executors": execs,
+                "control_pid": os.getpid()}
+
+
+def control_main(args) -> int:
+    """``--control-only``: the scheduler process rank 0 starts under torchrun (or a single-GPU run)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    srv = ControlServer(args, world)
+    print(f"PLX_BENCH_CONTROL 127.0.0.1:{srv.port}", flush=True)
+    return srv.serve()
+
+
+def _spawn_control(argv):
+    """Start the control process (no GPU), return (Popen, "host:port")."""
+    p = subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv, "--control-only"],
+                         stdout=subprocess.PIPE, text=True)
+    line = p.stdout.readline()
+    if not line.startswith("PLX_BENCH_CONTROL "):
+        p.kill()
+        raise RuntimeError(f"control process did not start: {line!r}")
+    return p, line.split()[1]
+
+
+# ----------------------------------------------------------------------------- launcher (no GPU calls here)
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int, args, argv) -> int:
+    """``--gpus N`` without torchrun: host the scheduler here (this process never initialises the GPU runtime) and
+    start N rank processes, one per GPU."""
+    srv = ControlServer(args, n)
+    ctl = threading.Thread(target=srv.serve, name="bench-control", daemon=True)
+    ctl.start()
+    env = dict(os.environ)
+    env.update({"WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port()),
+                "LOCAL_WORLD_SIZE": str(n), "PLX_BENCH_CONTROL": f"127.0.0.1:{srv.port}"})
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=e))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    ctl.join(timeout=60)
+    return rc
+
+
+def _pin_cpus(local_rank: int) -> list:
+    """Bind this rank to the CPUs local to its GPU (NUMA node of the PCIe root) before torch starts its threads."""
+    from polyaxon_amd.polyflow.devices import device_cpus
+
+    cpus = device_cpus(local_rank)
+    if cpus:
+        try:
+            os.sched_setaffinity(0, cpus)
+        except OSError:
+            return []
+    return cpus or []
 
 
 def main() -> int:
     args = _args()
+    if args.control_only:
+        return control_main(args)
+    argv = sys.argv[1:]
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        return spawn_ranks(args.gpus, sys.argv[1:])
+        return spawn_ranks(args.gpus, args, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
+    pinned = [] if args.cpu else _pin_cpus(local)
+    ctl_addr = os.environ.get("PLX_BENCH_CONTROL")
+    ctl_proc = None
+    if ctl_addr is None and rank == 0:  # torchrun / single GPU: the scheduler gets a process of its own
+        ctl_proc, ctl_addr = _spawn_control(argv)
 
     import torch
     import torch.distributed as dist
@@ -231,23 +337,30 @@ def main() -> int:
         if rank == 0:
             print(f"[bench +{time.perf_counter() - T0:.1f}s] {msg}", file=sys.stderr, flush=True)
 
+    program, params = program_params(args)
     if args.cpu:
         dev = torch.device("cpu")
         torch.set_num_threads(max(1, (os.cpu_count() or 2) // (2 * world)))  # ranks must not oversubscribe the CPU
-        program = "resnet_tiny"
-        params = {"batch": min(args.batch, 8), "image": min(args.image, 32), "unit_steps": min(args.unit_steps, 1),
-                  "grid": 4, "signal": args.signal}
     else:
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-        program = "resnet50"
-        params = {"batch": args.batch, "image": args.image, "unit_steps": args.unit_steps, "signal": args.signal,
-                  "graph": bool(args.graph)}
     if world > 1:
         if dev.type == "cuda":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        addr = [ctl_addr]
+        dist.broadcast_object_list(addr, src=0)
+        ctl_addr = addr[0]
+    host, _, port = ctl_addr.rpartition(":")
+
+    # framework-owned collectives (csrc/rccl_comm.cpp) for the timing reduction on the GPU path
+    comm = None
+    if dev.type == "cuda":
+        from polyaxon_amd.parallel.rccl import RcclComm
+
+        comm = (RcclComm.from_torch_distributed() if world > 1
+                else RcclComm(RcclComm.new_unique_id(), 1, 0, local))
 
     def barrier():
         if dev.type == "cuda":
@@ -257,53 +370,54 @@ def main() -> int:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
-    # rank 0 listens for the executors (its own included) before anybody connects
-    listener = None
-    port = [0]
-    if rank == 0:
-        listener = socket.socket()
-        listener.bind(("127.0.0.1", 0))
-        listener.listen(world)
-        port[0] = listener.getsockname()[1]
-    if world > 1:
-        dist.broadcast_object_list(port, src=0)
-
-    params["data_seed"] = 1234  # one task (class patterns) for every trial; the samples are fresh every step
     worker = ResidentWorker(program, params, device=dev, max_active=args.max_active)
-    log(f"building {program} executors (batch {params['batch']}, image {params['image']})")
+    log(f"building {program} executors (batch {params['batch']}, image {params['image']}, search {args.search})")
     worker._ready_info = worker.build()
     log(f"executor ready in {worker._ready_info['build_s']} s")
-    control = None
-    if rank == 0:
-        control = Control(args, world, listener, program, params, log)
-        control.start()
-    chan = Channel.connect("127.0.0.1", port[0])
+    chan = Channel.connect(host, int(port), timeout=300)
     chan.send({"rank": local if world > 1 else 0})
+    bench = None
+    if rank == 0:
+        bench = Channel.connect(host, int(port), timeout=300)
+        bench.send({"bench": 1})
 
     r = worker.serve(chan)                      # warm-up sweeps, until paused
     if r != "pause:warm":
-        raise RuntimeError(f"executor stopped during warm-up: {r} ({control.error if control else ''})")
+        raise RuntimeError(f"executor stopped during warm-up: {r}")
+    s0 = dict(worker.stats)
     barrier()
     t0 = time.perf_counter()
-    if control is not None:
-        control.t0_wall = time.time()
-        control.t0_set.set()
+    if bench is not None:
+        bench.send({"op": "go", "t0": time.time()})
         log("timed region")
     r = worker.serve(chan)                      # timed sweeps, until paused
     barrier()
     elapsed = time.perf_counter() - t0
     if r != "pause:timed":
-        raise RuntimeError(f"executor stopped during the timed region: {r} ({control.error if control else ''})")
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dev.type == "cuda" else "cpu")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t[0])
+        raise RuntimeError(f"executor stopped during the timed region: {r}")
+    mine = [elapsed, worker.stats["trials"] - s0["trials"], worker.stats["train_steps"] - s0["train_steps"],
+            float(os.getpid())]
+    if comm is not None:
+        t = torch.tensor(mine, dtype=torch.float64, device=dev)
+        per_rank = comm.all_gather(t).cpu().tolist()
+        torch.cuda.synchronize(dev)
+    elif world > 1:
+        g = [torch.zeros(4, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(g, torch.tensor(mine, dtype=torch.float64))
+        per_rank = [x.tolist() for x in g]
+    else:
+        per_rank = [mine]
+    elapsed_max = max(p[0] for p in per_rank)
+    rc = 0
     if rank == 0:
-        control.join(timeout=600)
-        if control.error is not None:
-            raise control.error
-        res = control.result
+        msg = bench.recv(timeout=900)
+        if msg is None or msg.get("ev") != "result":
+            raise RuntimeError(f"control process failed: {msg}")
+        res = msg["result"]
         value = res["trials"] / elapsed_max * 3600.0
+        search = (f"hyperband max_iter={MAX_ITER} eta={ETA} resume=true, 3 brackets / 23 trials per sweep"
+                  if args.search == "hyperband" else
+                  f"asha min_resource=1 max_resource={MAX_ITER} eta={ETA} resume=true, {args.asha_n} configs per sweep")
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -325,11 +439,13 @@ def main() -> int:
                 "seq_len": None,
                 "image_size": params["image"],
                 "parallelism": f"trial-parallel x{world} (resident executor per GPU, brackets balanced by polyflow)",
-                "search": f"hyperband max_iter={MAX_ITER} eta={ETA} resume=true, 3 brackets / 23 trials per sweep",
+                "search": search,
                 "unit_steps": params["unit_steps"],
-                "step": "one complete Hyperband sweep per GPU",
+                "step": "one complete sweep per GPU",
                 "sweeps": res["groups"],
                 "brackets": res["brackets"],
+                "signal": args.signal,
+                "active_classes": params["active_classes"],
             },
             "trials": res["trials"],
             "trials_succeeded": res["succeeded"],
@@ -339,17 +455,28 @@ def main() -> int:
             "target_loss": args.target,
             "best_loss": round(res["best"], 4) if res["best"] is not None else None,
             "store_fsm_history_ok": res["fsm_ok"],
-            "path": "polyflow scheduler + SQLite store + resident executors (same path as plx run)",
+            "path": "polyflow scheduler (own process) + SQLite store + resident executors (same path as plx run)",
             "hip_graph": bool(worker._ready_info.get("hip_graph")),
+            "per_rank": [{"rank": i, "pid": int(p[3]), "elapsed_s": round(p[0], 3), "trials": int(p[1]),
+                          "train_steps": int(p[2])} for i, p in enumerate(per_rank)],
+            "executors": res["executors"],
+            "control_pid": res["control_pid"],
+            "cpus_pinned": len(pinned),
         }
-        if args.verbose:
-            print(json.dumps(res["pool"]), file=sys.stderr)
         print(json.dumps(out), flush=True)
-        control.flow.shutdown(stop_running=False, timeout=10)
     chan.close()
+    if bench is not None:
+        bench.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
-    return 0
+    if ctl_proc is not None:
+        try:
+            rc = max(rc, ctl_proc.wait(timeout=60))
+        except subprocess.TimeoutExpired:
+            ctl_proc.kill()
+    return rc
 
 
 if __name__ == "__main__":

@@ -36,7 +36,7 @@ SUBJECTS = {
     "experiment_group": ["created", "updated", "deleted", "viewed", "stopped", "resumed", "bookmarked",
                          "unbookmarked", "new_status", "experiments_viewed", "statuses_viewed", "metrics_viewed",
                          "iteration", "random", "grid", "hyperband", "bo", "asha", "done", "succeeded", "failed",
-                         "deleted_triggered", "stopped_triggered"],
+                         "deleted_triggered", "stopped_triggered", "unit_redispatched"],
     "experiment_job": ["viewed", "resources_viewed", "logs_viewed", "statuses_viewed", "new_status", "failed",
                        "succeeded", "done"],
     "job": ["created", "updated", "started", "started_triggered", "deleted", "deleted_triggered", "viewed",

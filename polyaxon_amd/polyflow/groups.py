@@ -111,10 +111,11 @@ class GroupDriver:
         if self.done or self.queue or self.active or self.has_more_work():
             return
         self.done = True
-        status = "stopped" if self.stopped else "succeeded"
-        if self.store.get_group(self.gid)["status"] != "stopped":
-            self.store.set_group_status(self.gid, status)
-        self.flow.auditor.record(f"experiment_group.{'done' if status == 'stopped' else 'succeeded'}",
+        failed = getattr(self, "failed_message", None)
+        status = "failed" if failed else ("stopped" if self.stopped else "succeeded")
+        if self.store.get_group(self.gid)["status"] not in ("stopped", "failed"):
+            self.store.set_group_status(self.gid, status, failed)
+        self.flow.auditor.record(f"experiment_group.{ {'stopped': 'done', 'failed': 'failed'}.get(status, status)}",
                                  "experiment_group", self.gid)
 
     def _should_stop_early(self) -> bool:
@@ -308,24 +309,26 @@ class AshaDriver(GroupDriver):
         self._fill()
 
 
-class ResidentHyperbandDriver(GroupDriver):
-    """Hyperband on resident executors (``environment.executor: resident``; polyflow/resident.py, pool.py).
+class ResidentDriver(GroupDriver):
+    """Base of the drivers that run a group on resident executors (``environment.executor: resident``;
+    polyflow/resident.py, pool.py).  The group's work is cut into independent *units* -- Hyperband brackets or
+    ASHA shards -- that the pool spreads over the group's executors (at most ``concurrency`` of them, balanced by
+    training units).  This driver mirrors what the executors report into the store, so every trial is an
+    experiment row with its FSM history, metrics and ``last_metric``; promotions are RESUME (or RESTART) clones of
+    the previous rung's experiment with the resource declaration patched (iteration_managers/hyperband.py:79-113);
+    every rung decision is an iteration row.
 
-    The reference runs the brackets one after another with a synchronous rung barrier and a 30 s poll
-    (polyaxon/hpsearch/tasks/hyperband.py:7-83), every trial a pod.  Here all ``s_max + 1`` brackets are created
-    up front (same suggestions as the reference: ``get_suggestions`` per iteration, same seed) and handed to the
-    group's executors -- at most ``concurrency`` of them, balanced by training units -- which run them
-    concurrently; each executor decides its rungs on the device.  This driver mirrors what the executors report
-    into the store, so every trial is an experiment row with its FSM history, metrics and ``last_metric``;
-    promotions are RESUME (or RESTART) clones of the previous rung's experiment with the resource declaration
-    patched (iteration_managers/hyperband.py:79-113); every finished rung is an iteration row.
-    """
+    Faults: a unit whose executor is lost (process died, fatal error) is re-dispatched to a live or newly spawned
+    executor with its progress (the last completed rung and its promotions, or an ASHA shard's recorded results),
+    up to ``environment.max_restarts`` times (1 when unset) -- a cluster event records each re-dispatch; past the
+    budget the unit fails and the group ends ``failed``.  A group none of whose executors can be placed fails
+    immediately when the request can never fit, or after ``scheduler.resident_placement_timeout_s`` (300 s)."""
+
+    OP = "bracket"
 
     def begin(self) -> None:
-        from polyaxon_amd.polyflow.programs import bracket_units, program_key
+        from polyaxon_amd.polyflow.programs import program_key
 
-        self.m: HyperbandSearchManager = self.manager
-        self.hb = self.hp.hyperband
         self.ex = self.spec.environment.executor
         self.program_key = program_key(self.ex.program, self.ex.params)
         res = self.spec.environment.resources
@@ -337,33 +340,75 @@ class ResidentHyperbandDriver(GroupDriver):
         self.brackets: Dict[str, Dict[str, Any]] = {}
         self.pending_keys: List[str] = []
         self.used_workers: set = set()
-        self._xspec_cache: Dict[str, Any] = {}
-        rname = self.hb.resource.name
-        for it in range(self.m.s_max + 1):
-            sugg = self.m.get_suggestions(HyperbandIterationConfig(iteration=it))
-            key = f"{self.gid}.{it}"
-            configs = [{"cid": i, "params": {k: v for k, v in s.items() if k != rname}} for i, s in enumerate(sugg)]
-            self.brackets[key] = {"iteration": it, "configs": configs, "status": None, "wid": None, "xids": {},
-                                  "root": {}, "open": set(),
-                                  "units": bracket_units(self.hb.max_iter, self.hb.eta, it, self.hb.resume)}
-            self.pending_keys.append(key)
+        self.failed_message: Optional[str] = None
+        mr = int(getattr(self.spec.environment, "max_restarts", 0) or 0)
+        self.max_retries = mr if mr > 0 else 1
+        self._waiting_since: Optional[float] = None
+        self._dispatch_armed = False
+        timeout = self.flow.settings.get("scheduler.resident_placement_timeout_s") if self.flow.settings else None
+        self.placement_timeout = float(timeout or 300.0)
+        self.make_units()
         self._dispatch()
 
+    def make_units(self) -> None:
+        raise NotImplementedError
+
+    def _new_unit(self, key: str, iteration: int, configs: List[Dict[str, Any]], units: float) -> None:
+        self.brackets[key] = {"iteration": iteration, "configs": configs, "status": None, "wid": None, "xids": {},
+                              "root": {}, "open": set(), "units": units, "retries": 0, "last_rung": None,
+                              "promoted": None, "history": []}
+        self.pending_keys.append(key)
+
+    def unit_message(self, key: str, br: Dict[str, Any]) -> Dict[str, Any]:
+        early = [{"metric": r.metric, "value": r.value, "optimization": r.optimization}
+                 for r in self.hp.early_stopping]
+        return {"op": self.OP, "key": key, "hptuning": self.hp.to_dict(), "iteration": br["iteration"],
+                "configs": br["configs"], "seed": int(self.hp.seed or 0) + 7919 * self.gid, "early_stopping": early}
+
     # ------------------------------------------------------------------ placement
+    def _fail_group(self, message: str) -> None:
+        log.error("group %s: %s", self.gid, message)
+        self.failed_message = message
+        for key in list(self.pending_keys):
+            self.brackets[key]["status"] = "failed"
+        self.pending_keys.clear()
+        self.flow.store.add_cluster_event("resident_executor", "error", f"group {self.gid}: {message}")
+        self.stop(pending_only=False, message=message)
+
+    def _arm_dispatch(self) -> None:
+        if not self._dispatch_armed:
+            self._dispatch_armed = True
+            self.flow.after(0.5, self._retry_dispatch)
+
+    def _retry_dispatch(self) -> None:
+        self._dispatch_armed = False
+        self._dispatch()
+
     def _dispatch(self) -> None:
         if self.stopped or self.done or not self.pending_keys:
             return
         pool = self.flow.resident_pool()
-        pool.ensure(self.program_key, self.ex.program, self.ex.params, want=self.concurrency, gpu=self.gpu,
-                    hbm_gb=self.hbm, max_active=self.ex.max_active_brackets)
-        early = [{"metric": r.metric, "value": r.value, "optimization": r.optimization}
-                 for r in self.hp.early_stopping]
+        live = pool.ensure(self.program_key, self.ex.program, self.ex.params, want=self.concurrency, gpu=self.gpu,
+                           hbm_gb=self.hbm, max_active=self.ex.max_active_brackets)
+        if not live:
+            why = pool.placement_error
+            if why is not None:  # the request can never be placed on this node
+                self._fail_group(f"no resident executor can be placed: {why}")
+                return
+            now = time.time()
+            self._waiting_since = self._waiting_since or now
+            if now - self._waiting_since > self.placement_timeout:
+                self._fail_group(f"no resident executor could be placed within {self.placement_timeout:.0f} s")
+                return
+            self._arm_dispatch()
+            return
+        self._waiting_since = None
+        alive = {w.wid for w in pool.workers_for(self.program_key)}
+        self.used_workers &= alive  # dead executors never count against the group's concurrency
         while self.pending_keys:
             key = self.pending_keys[0]
             br = self.brackets[key]
-            msg = {"op": "bracket", "key": key, "hptuning": self.hp.to_dict(), "iteration": br["iteration"],
-                   "configs": br["configs"], "seed": int(self.hp.seed or 0) + 7919 * self.gid,
-                   "early_stopping": early}
+            msg = self.unit_message(key, br)
             allowed = sorted(self.used_workers) if len(self.used_workers) >= self.concurrency else None
             w = pool.assign(self, msg, br["units"], allowed=allowed, key=self.program_key)
             if w is None:
@@ -372,7 +417,7 @@ class ResidentHyperbandDriver(GroupDriver):
             br["wid"] = w.wid
             self.pending_keys.pop(0)
         if self.pending_keys:  # every device is busy: try again shortly (an executor or device will free up)
-            self.flow.after(0.5, self._dispatch)
+            self._arm_dispatch()
 
     def has_more_work(self) -> bool:
         return any(b["status"] is None for b in self.brackets.values())
@@ -396,15 +441,31 @@ class ResidentHyperbandDriver(GroupDriver):
             self._dispatch()
             self._check_finished()
         elif ev == "error":
-            log.warning("group %s bracket %s: %s", self.gid, msg.get("key"), msg.get("message"))
+            log.warning("group %s unit %s: %s", self.gid, msg.get("key"), msg.get("message"))
 
     def on_bracket_lost(self, h, key: str, reason: str) -> None:
         br = self.brackets.get(key)
+        self.used_workers.discard(h.wid)
         if br is None or br["status"] is not None:
             return
         self._close_open(br, "failed", f"resident executor {h.wid} lost: {reason}")
+        br["wid"] = None
+        if not self.stopped and br["retries"] < self.max_retries:
+            br["retries"] += 1
+            self.flow.store.add_cluster_event(
+                "resident_executor", "warning",
+                f"group {self.gid}: {self.OP} {key} re-dispatched after executor {h.wid} was lost ({reason}); "
+                f"retry {br['retries']} of {self.max_retries}", {"key": key, "from_rung": self._resume_rung(br)})
+            self.flow.auditor.record("experiment_group.unit_redispatched", "experiment_group", self.gid, key=key)
+            self.pending_keys.append(key)
+            self._dispatch()
+            return
         br["status"] = "failed"
+        self.failed_message = f"{self.OP} {key} lost with executor {h.wid} ({reason}) after {br['retries']} retries"
         self._check_finished()
+
+    def _resume_rung(self, br) -> int:
+        return 0 if br["last_rung"] is None else br["last_rung"] + 1
 
     def _close_open(self, br, status: str, message: str) -> None:
         for xid in list(br["open"]):
@@ -419,10 +480,17 @@ class ResidentHyperbandDriver(GroupDriver):
     def _experiment_data(self, params: Dict[str, Any]) -> Dict[str, Any]:
         return self.spec.experiment_data(params)
 
+    @property
+    def resume_enabled(self) -> bool:
+        raise NotImplementedError
+
     def _trial_start(self, h, br, msg) -> None:
         rung, cid, params = int(msg["rung"]), int(msg["cid"]), msg["params"]
         prev = br["xids"].get((rung - 1, cid)) if rung > 0 else None
-        strategy = ("resume" if self.hb.resume else "restart") if prev is not None else None
+        # RESUME only when the executor really continued from the previous rung's snapshot; a re-dispatched unit
+        # re-trains its promoted configs from scratch (RESTART of the previous rung's experiment)
+        resumed = bool(msg.get("resumed", self.resume_enabled))
+        strategy = ("resume" if resumed else "restart") if prev is not None else None
         xid = self.store.create_experiment(
             self.project["id"], self._experiment_data(params), group_id=self.gid, user=self.user,
             declarations=params, original_experiment_id=prev, cloning_strategy=strategy,
@@ -447,11 +515,13 @@ class ResidentHyperbandDriver(GroupDriver):
         self.active.add(xid)
 
     def _trial_end(self, br, msg) -> None:
-        xid = br["xids"].get((int(msg["rung"]), int(msg["cid"])))
+        rung, cid = int(msg["rung"]), int(msg["cid"])
+        xid = br["xids"].get((rung, cid))
         if xid is None:
             return
         v = msg.get("metric")
-        name = self.hb.metric.name
+        br["history"].append([rung, cid, v])
+        name = self.metric_name
         if v is not None:
             self.store.add_metrics(xid, {name: v}, step=int(msg.get("steps", 0)), created_at=msg.get("t_end"))
             status, message = "succeeded", None
@@ -466,9 +536,21 @@ class ResidentHyperbandDriver(GroupDriver):
         self.active.discard(xid)
         self.finished[xid] = status
         self.flow.auditor.record(f"experiment.{status}", "experiment", xid, status=status)
-        if self.hp.early_stopping and not self.stopped and self._should_stop_early():
+        if v is not None and self.hp.early_stopping and not self.stopped and self._crosses_rule(v):
             self.flow.auditor.record("experiment_group.stopped", "experiment_group", self.gid, reason="early_stopping")
             self.stop(pending_only=not self.stop_running_on_early_stop, message="Early stopping")
+
+    def _crosses_rule(self, v: float) -> bool:
+        """Incremental early stopping on the program metric: the reference re-reads every experiment of the group
+        per check (db/models/experiment_groups.py:211-221); a new result can only trip a rule by itself, so only it
+        is tested (rules on other metrics never see a resident trial's value).  The executors run the same rule
+        set over their device metric tensors (``early_stop_any``) and stop their own units."""
+        for r in self.hp.early_stopping:
+            if r.metric != self.metric_name:
+                continue
+            if (v >= float(r.value)) if Optimization.maximize(r.optimization) else (v <= float(r.value)):
+                return True
+        return False
 
     def _rung_done(self, br, msg) -> None:
         rung = int(msg["rung"])
@@ -476,9 +558,11 @@ class ResidentHyperbandDriver(GroupDriver):
         metrics = [[br["xids"][(rung, int(c))], float(v)] for c, v in msg.get("metrics") or []
                    if (rung, int(c)) in br["xids"]]
         promoted = [br["xids"][(rung, int(c))] for c in msg.get("promoted") or [] if (rung, int(c)) in br["xids"]]
+        br["last_rung"] = rung
+        br["promoted"] = [int(c) for c in msg.get("promoted") or []]
         self.store.create_iteration(self.gid, {"iteration": br["iteration"], "bracket_iteration": rung,
                                                "experiment_ids": ids, "experiments_metrics": metrics,
-                                               "promoted": promoted, "executor": br["wid"]})
+                                               "promoted": promoted, "executor": br["wid"], "unit": self.OP})
         if msg.get("early_stop") and not self.stopped:
             self.flow.auditor.record("experiment_group.stopped", "experiment_group", self.gid, reason="early_stopping")
             self.stop(pending_only=not self.stop_running_on_early_stop, message="Early stopping")
@@ -490,23 +574,104 @@ class ResidentHyperbandDriver(GroupDriver):
             self.brackets[key]["status"] = "stopped"
         self.pending_keys.clear()
         for key, br in self.brackets.items():
-            if br["status"] is None and br["wid"] is not None:
-                if not pool.send(br["wid"], {"op": "stop_bracket", "key": key}):
+            if br["status"] is None:
+                if br["wid"] is None or not pool.send(br["wid"], {"op": "stop_bracket", "key": key}):
                     self._close_open(br, "stopped", message)
                     br["status"] = "stopped"
         if self.store.get_group(self.gid)["status"] not in ("stopped", "succeeded", "failed"):
-            self.store.set_group_status(self.gid, "stopped", message)
+            self.store.set_group_status(self.gid, "failed" if self.failed_message else "stopped", message)
         self._check_finished()
+
+
+class ResidentHyperbandDriver(ResidentDriver):
+    """Hyperband on resident executors.  The reference runs the brackets one after another with a synchronous rung
+    barrier and a 30 s poll (polyaxon/hpsearch/tasks/hyperband.py:7-83), every trial a pod.  Here all ``s_max + 1``
+    brackets are created up front (same suggestions as the reference: ``get_suggestions`` per iteration, same seed)
+    and run concurrently on the executors; each executor decides its rungs on the device."""
+
+    OP = "bracket"
+
+    def make_units(self) -> None:
+        from polyaxon_amd.polyflow.programs import bracket_units
+
+        self.m: HyperbandSearchManager = self.manager
+        self.hb = self.hp.hyperband
+        rname = self.hb.resource.name
+        for it in range(self.m.s_max + 1):
+            sugg = self.m.get_suggestions(HyperbandIterationConfig(iteration=it))
+            configs = [{"cid": i, "params": {k: v for k, v in s.items() if k != rname}} for i, s in enumerate(sugg)]
+            self._new_unit(f"{self.gid}.{it}", it, configs,
+                           bracket_units(self.hb.max_iter, self.hb.eta, it, self.hb.resume))
+
+    @property
+    def metric_name(self) -> str:
+        return self.hb.metric.name
+
+    @property
+    def resume_enabled(self) -> bool:
+        return bool(self.hb.resume)
+
+    def unit_message(self, key, br):
+        msg = super().unit_message(key, br)
+        if br["last_rung"] is not None:  # re-dispatch: continue after the last completed rung
+            msg["start_rung"] = br["last_rung"] + 1
+            msg["active"] = list(br["promoted"] or [])
+        return msg
+
+
+class ResidentAshaDriver(ResidentDriver):
+    """ASHA on resident executors (BASELINE config 3's other half; the reference has only the synchronous barrier,
+    polyaxon/hpsearch/tasks/hyperband.py:48-83).  The group's ``n_experiments`` configs (same random suggestions as
+    process-mode ASHA) are cut into ``executor.shards`` independent shards (default 1); each shard runs on one
+    executor as an asynchronous successive-halving search: every round it starts the best unpromoted config in the
+    top 1/eta of the highest rung that has one -- ranked by the round's device top-k over the shard's
+    [rungs × configs] metric table -- or a new config at rung 0, and promotions RESUME from HBM snapshots."""
+
+    OP = "asha"
+
+    def make_units(self) -> None:
+        from polyaxon_amd.polyflow.programs import asha_units
+
+        a = self.hp.asha
+        rname = a.resource.name
+        sugg = list(self.manager.get_suggestions())
+        n = int(self.ex.shards or 1)
+        n = max(1, min(n, len(sugg)))
+        for s in range(n):
+            part = [(i, p) for i, p in enumerate(sugg) if i % n == s]
+            configs = [{"cid": j, "params": {k: v for k, v in p.items() if k != rname}} for j, (_i, p) in enumerate(part)]
+            self._new_unit(f"{self.gid}.a{s}", s, configs,
+                           asha_units(len(configs), a.min_resource, a.max_resource, a.eta, a.resume))
+
+    @property
+    def metric_name(self) -> str:
+        return self.hp.asha.metric.name
+
+    @property
+    def resume_enabled(self) -> bool:
+        return bool(self.hp.asha.resume)
+
+    def unit_message(self, key, br):
+        msg = super().unit_message(key, br)
+        if br["history"]:  # re-dispatch: the results recorded before the executor was lost
+            msg["history"] = [list(h) for h in br["history"]]
+        return msg
+
+    def _resume_rung(self, br) -> int:
+        return max((h[0] for h in br["history"]), default=0)
 
 
 def make_group_driver(flow, gid: int, spec: GroupSpecification, project: Dict, user: str, cwd: str) -> GroupDriver:
     algo = spec.search_algorithm
     ex = spec.environment.executor if spec.environment is not None else None
     if ex is not None and ex.resident:
+        if algo == SearchAlgorithms.ASHA:
+            return ResidentAshaDriver(flow, gid, spec, project, user, cwd)
         if algo != SearchAlgorithms.HYPERBAND:
             from polyaxon_amd.spec.specification import PolyaxonfileError
 
-            raise PolyaxonfileError(f"resident executors run hyperband groups; {algo} groups use executor: process")
+            raise PolyaxonfileError(f"resident executors run hyperband and asha groups; {algo} groups use "
+                                    "executor: process")
         return ResidentHyperbandDriver(flow, gid, spec, project, user, cwd)
     cls = {SearchAlgorithms.GRID: GridRandomDriver, SearchAlgorithms.RANDOM: GridRandomDriver,
            SearchAlgorithms.HYPERBAND: HyperbandDriver, SearchAlgorithms.BO: BODriver,

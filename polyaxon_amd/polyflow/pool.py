@@ -46,6 +46,8 @@ class WorkerHandle:
     units: Dict[str, float] = field(default_factory=dict)    # bracket key -> outstanding units
     idle_since: float = field(default_factory=time.time)
     closing: bool = False
+    assigned_units: float = 0.0                              # cumulative training units / units of work assigned
+    assigned_count: int = 0
     waiters: Dict[str, Callable[[Dict[str, Any]], None]] = field(default_factory=dict)
 
     @property
@@ -64,6 +66,9 @@ class ResidentPool:
         self.workers: Dict[int, WorkerHandle] = {}
         self._next = 1
         self._reaper_armed = False
+        # why the last spawn could NEVER succeed on this node (allocator ValueError: no such device, a fraction or
+        # HBM request larger than a device); None when it merely found every device busy
+        self.placement_error: Optional[str] = None
 
     # ------------------------------------------------------------------ queries
     def workers_for(self, key: str) -> List[WorkerHandle]:
@@ -72,6 +77,7 @@ class ResidentPool:
     def snapshot(self) -> List[Dict[str, Any]]:
         return [{"wid": w.wid, "program": w.program, "devices": w.devices, "external": w.external, "ready": w.ready,
                  "alive": w.alive, "brackets": sorted(w.brackets), "load_units": w.load,
+                 "assigned_units": w.assigned_units, "assigned": w.assigned_count,
                  "pid": w.proc.pid if w.proc else w.info.get("pid")} for w in self.workers.values()]
 
     # ------------------------------------------------------------------ creation
@@ -79,6 +85,7 @@ class ResidentPool:
                hbm_gb: float = 0.0, max_active: int = 8) -> List[WorkerHandle]:
         """Make sure up to ``want`` workers run ``program`` (spawning on free devices); returns the live ones."""
         have = self.workers_for(key)
+        self.placement_error = None
         while len(have) < want:
             h = self._spawn(key, program, params, gpu, hbm_gb, max_active)
             if h is None:
@@ -93,8 +100,14 @@ class ResidentPool:
             a = self.flow.alloc.allocate(owner, gpu, hbm_gb)
         except ValueError as e:
             log.warning("resident executor allocation rejected: %s", e)
+            self.placement_error = str(e)
             return None
         if a is None:
+            devs = self.flow.alloc.devices
+            if not devs:
+                self.placement_error = "no devices on this node"
+            elif not any(d.healthy and d.memory_gb >= hbm_gb for d in devs):
+                self.placement_error = f"no healthy device with {hbm_gb} GB of HBM"
             return None
         self._next += 1
         parent, child = socket.socketpair()
@@ -161,6 +174,8 @@ class ResidentPool:
         w = min(cands, key=lambda h: (h.load, h.wid))
         w.brackets[msg["key"]] = driver
         w.units[msg["key"]] = units
+        w.assigned_units += units
+        w.assigned_count += 1
         try:
             w.chan.send(msg)
         except OSError:

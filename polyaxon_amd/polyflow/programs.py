@@ -131,3 +131,15 @@ def bracket_units(max_iter: float, eta: float, iteration: int, resume: bool) -> 
         n = 0 if i == s + 1 else int(n0 * (eta ** -i) / eta)
         i += 1
     return total
+
+
+def asha_units(n_configs: int, min_r: float, max_r: float, eta: float, resume: bool) -> float:
+    """Expected training resource (in units) of an ASHA shard over ``n_configs`` configs: rung k holds about
+    n / eta^k configs, each training r_k (or r_k - r_{k-1} when resumed) -- the load the pool balances."""
+    n_rungs = int(math.floor(math.log(max_r / min_r) / math.log(eta) + 1e-9)) + 1
+    total, prev = 0.0, 0.0
+    for k in range(n_rungs):
+        rk = min(min_r * eta ** k, max_r)
+        total += (n_configs / eta ** k) * ((rk - prev) if (resume and k) else rk)
+        prev = rk
+    return total

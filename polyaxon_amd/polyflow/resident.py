@@ -18,6 +18,14 @@ warm, so polyflow keeps **one resident executor per GPU**:
 * promotions with ``resume: true`` restore the config's HBM snapshot (the reference RESUME clone,
   db/models/experiments.py:225-316) instead of a checkpoint file round trip -- 288 GB of HBM holds hundreds of
   ResNet-50 trial states;
+* ASHA groups (``hptuning.asha``) come as *shards*: an independent asynchronous successive-halving search over a
+  set of configs, no rung barrier.  Every round a shard runs ONE job -- the best not-yet-promoted config in the
+  top 1/eta of the highest rung that has one (RESUME from its HBM snapshot), else a new config at rung 0 -- and the
+  round's single top-k launch (over the shard's ``[rungs × configs]`` device metric table, beside the Hyperband
+  brackets' rows) gives the next round its rung rankings;
+* a bracket or shard whose executor died can be re-sent with its progress (``start_rung``/``active`` for a
+  bracket, ``history`` for a shard): the new executor continues from the last completed decision, re-training
+  promoted configs from scratch (their snapshots died with the old process);
 * every trial is still a Polyaxon experiment: the worker streams ``trial_start``/``trial_end``/``rung_done``
   events, and the scheduler thread (polyflow/groups.py ``ResidentHyperbandDriver``) writes the experiment rows,
   RESUME clones, FSM status history, metrics/``last_metric`` and iteration rows, while the GPU keeps running.
@@ -25,7 +33,7 @@ warm, so polyflow keeps **one resident executor per GPU**:
 Protocol (length-prefixed JSON over a stream socket; ``Channel``):
 
   scheduler -> worker  {"op": "init", "program", "params", "max_active"} | {"op": "bracket", ...} |
-                       {"op": "stop_bracket", "key"} | {"op": "pause", "tag"} | {"op": "shutdown"}
+                       {"op": "asha", ...} | {"op": "stop_bracket", "key"} | {"op": "pause", "tag"} | {"op": "shutdown"}
   worker -> scheduler  {"ev": "ready", ...} | {"ev": "trial_start", ...} | {"ev": "trial_end", ...} |
                        {"ev": "rung_done", ...} | {"ev": "bracket_done", ...} | {"ev": "paused", "tag"} |
                        {"ev": "error", ...}
@@ -137,8 +145,51 @@ class _Bracket:
     early_stopped: bool = False
 
 
+@dataclass
+class _AshaShard:
+    """One asynchronous successive-halving search (Li et al. 2018, "Massively parallel hyperparameter tuning") over
+    ``configs``: rungs k = 0..K-1 with resource min_r * eta^k (capped at max_r); a config enters rung k+1 once it is
+    in the top floor(n_k / eta) of rung k's n_k results -- decided from the device top-k order of the rung table."""
+    key: str
+    configs: Dict[int, Dict[str, Any]]
+    pending: List[int]                # configs not started yet (in suggestion order)
+    n_rungs: int
+    eta: float
+    min_r: float
+    max_r: float
+    resource_name: str
+    resource: Any
+    maximize: bool
+    resume: bool
+    seed: int
+    rules: List[Tuple[int, float, bool]] = field(default_factory=list)
+    row0: int = -1                    # first row of this shard in the worker's ASHA metric table
+    results: List[Dict[int, float]] = field(default_factory=list)      # rung -> {cid: metric} (host mirror)
+    promoted: List[set] = field(default_factory=list)                  # rung -> cids promoted out of it
+    snap_rung: Dict[int, int] = field(default_factory=dict)            # cid -> rung of its HBM snapshot
+    order: List[List[int]] = field(default_factory=list)               # rung -> cids best first (last top-k)
+    stopped: bool = False
+    early_stopped: bool = False
+
+    def r(self, rung: int):
+        return self.resource.cast_value(min(self.min_r * self.eta ** rung, self.max_r))
+
+    def next_job(self) -> Optional[Tuple[int, int]]:
+        """(cid, rung) to run next, or None when the search has nothing runnable (it is then finished: jobs of a
+        round all complete before the next decision)."""
+        for rung in range(self.n_rungs - 2, -1, -1):
+            k = int(len(self.results[rung]) / self.eta)
+            for cid in self.order[rung][:k]:
+                if cid not in self.promoted[rung]:
+                    self.promoted[rung].add(cid)
+                    return cid, rung + 1
+        if self.pending:
+            return self.pending.pop(0), 0
+        return None
+
+
 class ResidentWorker:
-    """The GPU side.  Owns one TrialProgram; runs the brackets it is handed, in rounds."""
+    """The GPU side.  Owns one TrialProgram; runs the brackets (and ASHA shards) it is handed, in rounds."""
 
     def __init__(self, program: str, params: Optional[Dict[str, Any]] = None, device=None, max_active: int = 8):
         self.program_name = program
@@ -148,9 +199,13 @@ class ResidentWorker:
         self.program = None
         self.queue: List[_Bracket] = []
         self.active: List[_Bracket] = []
+        self.asha_queue: List[_AshaShard] = []
+        self.asha_active: List[_AshaShard] = []
+        self.asha_metrics = None          # BracketMetrics: rung rows of every active shard
         self.pause_tag: Optional[str] = None
         self.metrics = None
-        self.stats = {"trials": 0, "train_steps": 0, "rounds": 0, "topk_launches": 0, "early_stop_launches": 0}
+        self.stats = {"trials": 0, "train_steps": 0, "rounds": 0, "topk_launches": 0, "early_stop_launches": 0,
+                      "asha_jobs": 0}
         self._base_ev = None
         self._base_wall = 0.0
         self._shutdown: Optional[str] = None
@@ -206,12 +261,15 @@ class ResidentWorker:
         op = msg.get("op")
         if op == "bracket":
             self.queue.append(self._make_bracket(msg))
+        elif op == "asha":
+            self.asha_queue.append(self._make_shard(msg))
         elif op == "stop_bracket":
-            for br in list(self.queue):
-                if br.key == msg["key"]:
-                    self.queue.remove(br)
-                    chan.send({"ev": "bracket_done", "key": br.key, "status": "stopped"})
-            for br in self.active:
+            for q in (self.queue, self.asha_queue):
+                for br in list(q):
+                    if br.key == msg["key"]:
+                        q.remove(br)
+                        chan.send({"ev": "bracket_done", "key": br.key, "status": "stopped"})
+            for br in self.active + self.asha_active:
                 if br.key == msg["key"]:
                     br.stopped = True
         elif op == "pause":
@@ -249,15 +307,51 @@ class ResidentWorker:
                       resource_name=hb.resource.name, resource=hb.resource,
                       maximize=Optimization.maximize(hb.metric.optimization), resume=hb.resume,
                       seed=int(msg.get("seed", 0)), rules=rules)
-        br.active = sorted(configs)
+        # a re-dispatched bracket starts at the rung after its last completed one, with that rung's promotions;
+        # no snapshot exists here, so those configs re-train from scratch with the full resource of the rung
+        br.rung = int(msg.get("start_rung", 0))
+        br.active = [int(c) for c in msg["active"]] if msg.get("active") is not None else sorted(configs)
         return br
+
+    def _make_shard(self, msg: Dict[str, Any]) -> _AshaShard:
+        from polyaxon_amd.spec.hptuning import HPTuningConfig, Optimization
+
+        hp = HPTuningConfig.from_dict(msg["hptuning"])
+        a = hp.asha
+        if a.metric.name != self.program.metric:
+            raise ValueError(f"asha metric {a.metric.name!r} is not what program {self.program_name} "
+                             f"reports ({self.program.metric!r})")
+        rules = [(0, float(r["value"]), Optimization.maximize(r["optimization"]))
+                 for r in msg.get("early_stopping") or [] if r["metric"] == self.program.metric]
+        configs = {int(c["cid"]): dict(c["params"]) for c in msg["configs"]}
+        n_rungs = int(math.floor(math.log(a.max_resource / a.min_resource) / math.log(a.eta) + 1e-9)) + 1
+        sh = _AshaShard(key=msg["key"], configs=configs, pending=sorted(configs), n_rungs=n_rungs, eta=float(a.eta),
+                        min_r=float(a.min_resource), max_r=float(a.max_resource), resource_name=a.resource.name,
+                        resource=a.resource, maximize=Optimization.maximize(a.metric.optimization), resume=a.resume,
+                        seed=int(msg.get("seed", 0)), rules=rules)
+        sh.results = [dict() for _ in range(n_rungs)]
+        sh.promoted = [set() for _ in range(n_rungs)]
+        sh.order = [[] for _ in range(n_rungs)]
+        # re-dispatch: the results the scheduler recorded before the old executor died ([rung, cid, metric])
+        for rung, cid, v in msg.get("history") or []:
+            rung, cid = int(rung), int(cid)
+            if cid in sh.pending:
+                sh.pending.remove(cid)
+            if v is not None and not (isinstance(v, float) and math.isnan(v)):
+                sh.results[rung][cid] = float(v)
+            if rung > 0:
+                sh.promoted[rung - 1].add(cid)
+        for rung in range(n_rungs):
+            sh.order[rung] = sorted(sh.results[rung], key=lambda c: (-sh.results[rung][c] if sh.maximize
+                                                                     else sh.results[rung][c], c))
+        return sh
 
     # ------------------------------------------------------------------ serve loop
     def serve(self, chan: Channel) -> str:
         """Process messages and run rounds until paused (returns ``pause:<tag>``), shut down or disconnected."""
         self._ready_info = getattr(self, "_ready_info", None) or {"ev": "ready", "program": self.program_name}
         while True:
-            busy = bool(self.active or self.queue)
+            busy = bool(self.active or self.queue or self.asha_active or self.asha_queue)
             try:
                 msg = chan.recv(timeout=0 if busy else (None if self.pause_tag is None else 0))
             except ChannelClosed:
@@ -274,7 +368,7 @@ class ResidentWorker:
                 if r is not None:
                     return r
                 continue
-            if self.active or self.queue:
+            if self.active or self.queue or self.asha_active or self.asha_queue:
                 self._shutdown = None
                 self.run_round(chan)
                 if self._shutdown is not None:
@@ -307,21 +401,61 @@ class ResidentWorker:
                 self._shutdown = r
 
     # ------------------------------------------------------------------ one round
+    def _asha_rows(self, sh: _AshaShard) -> None:
+        """Give an admitted shard ``n_rungs`` contiguous rows of the ASHA metric table (grown, values kept)."""
+        from polyaxon_amd.polytune.kernels import BracketMetrics
+
+        dev = self.program.executor.device
+        width = max(len(sh.configs), 1)
+        used = sorted((o.row0, o.row0 + o.n_rungs) for o in self.asha_active if o is not sh and o.row0 >= 0)
+        row0, prev = 0, 0
+        for lo, hi in used:
+            if lo - prev >= sh.n_rungs:
+                break
+            prev = hi
+        row0 = prev
+        need_rows, cur = row0 + sh.n_rungs, self.asha_metrics
+        if cur is None or cur.values.shape[0] < need_rows or cur.values.shape[1] < width:
+            rows = max(need_rows, cur.values.shape[0] if cur is not None else 0, 4 * sh.n_rungs)
+            cols = max(width, cur.values.shape[1] if cur is not None else 0)
+            grown = BracketMetrics(rows, cols, dev)
+            if cur is not None:
+                r, c = cur.values.shape
+                grown.values[:r, :c].copy_(cur.values)
+                grown.counts[:r].copy_(cur.counts)
+                grown._host_counts[:r] = cur._host_counts
+            self.asha_metrics = grown
+        sh.row0 = row0
+        for rung in range(sh.n_rungs):
+            self.asha_metrics.reset_bracket(row0 + rung, len(sh.configs))
+        # a re-dispatched shard brings its recorded results back onto the device table
+        cols = sorted(sh.configs)
+        for rung in range(sh.n_rungs):
+            for cid, v in sh.results[rung].items():
+                self.asha_metrics.values[row0 + rung, cols.index(cid)] = v
+
     def run_round(self, chan: Channel) -> None:
         import torch
 
         from polyaxon_amd.polytune.kernels import BracketMetrics, early_stop_any
 
-        while len(self.active) < self.max_active and self.queue:
-            self.active.append(self.queue.pop(0))
+        while len(self.active) + len(self.asha_active) < self.max_active and (self.queue or self.asha_queue):
+            if self.queue:
+                self.active.append(self.queue.pop(0))
+            if self.asha_queue and len(self.active) + len(self.asha_active) < self.max_active:
+                sh = self.asha_queue.pop(0)
+                self.asha_active.append(sh)
+                self._asha_rows(sh)
         brs = list(self.active)
+        shards = list(self.asha_active)
         ex = self.program.executor
-        width = max(len(br.active) for br in brs)
-        if self.metrics.values.shape[1] < width or self.metrics.values.shape[0] < len(brs):
-            self.metrics = BracketMetrics(max(self.max_active, len(brs)), max(width, self.metrics.values.shape[1]),
-                                          ex.device)
-        for row, br in enumerate(brs):
-            self.metrics.reset_bracket(row, len(br.active))
+        if brs:
+            width = max(len(br.active) for br in brs)
+            if self.metrics.values.shape[1] < width or self.metrics.values.shape[0] < len(brs):
+                self.metrics = BracketMetrics(max(self.max_active, len(brs)), max(width, self.metrics.values.shape[1]),
+                                              ex.device)
+            for row, br in enumerate(brs):
+                self.metrics.reset_bracket(row, len(br.active))
         records = []
         for row, br in enumerate(brs):
             m = br.manager
@@ -333,10 +467,11 @@ class ResidentWorker:
                     break
                 params = dict(br.configs[cid])
                 params[br.resource_name] = r
+                resumed = br.resume and br.rung > 0 and cid in br.prev_r
                 chan.send({"ev": "trial_start", "key": br.key, "rung": br.rung, "cid": cid, "params": params,
-                           "t": time.time()})
+                           "resumed": resumed, "t": time.time()})
                 t_start = self._event()
-                if br.resume and br.rung > 0 and cid in br.prev_r:
+                if resumed:
                     ex.restore((br.key, cid))
                     steps = int(round((r - br.prev_r[cid]) * self.program.unit_steps))
                 else:
@@ -348,31 +483,90 @@ class ResidentWorker:
                 if br.resume and more:
                     ex.snapshot((br.key, cid))
                 records.append((row, br, slot, cid, steps, t_start, self._event()))
+        # ---- ASHA shards: one job each, decided from the previous round's device rankings
+        asha_records = []
+        finished = []
+        for sh in shards:
+            self._poll_control(chan)
+            job = None if (sh.stopped or sh.early_stopped) else sh.next_job()
+            if job is None:
+                finished.append(sh)
+                continue
+            cid, rung = job
+            col = sorted(sh.configs).index(cid)
+            r = sh.r(rung)
+            params = dict(sh.configs[cid])
+            params[sh.resource_name] = r
+            resumed = sh.resume and rung > 0 and sh.snap_rung.get(cid) == rung - 1
+            chan.send({"ev": "trial_start", "key": sh.key, "rung": rung, "cid": cid, "params": params,
+                       "resumed": resumed, "t": time.time()})
+            t_start = self._event()
+            if resumed:
+                ex.restore((sh.key, cid))
+                steps = int(round((r - sh.r(rung - 1)) * self.program.unit_steps))
+            else:
+                ex.reset(seed=(sh.seed * 1000003 + cid) & 0x7FFFFFFF)
+                steps = int(round(r * self.program.unit_steps))
+            ex.set_hparams(**{k: v for k, v in params.items() if k in self.program.hp_keys})
+            ex.run(steps)
+            ex.commit(self.asha_metrics.values[sh.row0 + rung], col, self.program.window)
+            if rung < sh.n_rungs - 1:
+                ex.snapshot((sh.key, cid))
+                sh.snap_rung[cid] = rung
+            self.stats["asha_jobs"] += 1
+            asha_records.append((sh, rung, cid, col, steps, t_start, self._event()))
         # ---- the round's decision: one top-k launch per optimisation direction over every active bracket
         n = len(brs)
-        vals_dev = self.metrics.values[:n]
         orders = {}
-        for mx in sorted({br.maximize for br in brs}):
-            orders[mx] = self.metrics.order(mx, rows=n)
-            self.stats["topk_launches"] += 1
+        if n:
+            vals_dev = self.metrics.values[:n]
+            for mx in sorted({br.maximize for br in brs}):
+                orders[mx] = self.metrics.order(mx, rows=n)
+                self.stats["topk_launches"] += 1
+        # ... and one per direction over every ASHA rung row (the shards' rankings for the next round)
+        a_orders = {}
+        live = [sh for sh in shards if sh not in finished]
+        a_rows = max((sh.row0 + sh.n_rungs for sh in live), default=0)
+        if live:
+            for mx in sorted({sh.maximize for sh in live}):
+                a_orders[mx] = self.asha_metrics.order(mx, rows=a_rows)
+                self.stats["topk_launches"] += 1
         early = {}
         by_rules: Dict[Tuple, List[int]] = {}
         for row, br in enumerate(brs):
             if br.rules:
                 by_rules.setdefault(tuple(br.rules), []).append(row)
         for rules, rows in by_rules.items():
-            idx = torch.tensor(rows, device=vals_dev.device)
-            flags = early_stop_any(vals_dev.index_select(0, idx).reshape(-1, 1), list(rules))
+            idx = torch.tensor(rows, device=self.metrics.values.device)
+            flags = early_stop_any(self.metrics.values[:n].index_select(0, idx).reshape(-1, 1), list(rules))
             self.stats["early_stop_launches"] += 1
             for row in rows:
                 early[row] = any(flags)
-        vals = vals_dev.detach().cpu().tolist()          # the round's one D2H read (synchronises)
+        a_early = {}
+        for sh in live:
+            if sh.rules:
+                flags = early_stop_any(self.asha_metrics.values[sh.row0: sh.row0 + sh.n_rungs].reshape(-1, 1),
+                                       list(sh.rules))
+                self.stats["early_stop_launches"] += 1
+                a_early[sh.key] = any(flags)
+        # the round's D2H reads (the first one synchronises)
+        vals = self.metrics.values[:n].detach().cpu().tolist() if n else []
         orders_h = {mx: o[:n].cpu().tolist() for mx, o in orders.items()}
+        a_vals = self.asha_metrics.values[:a_rows].detach().cpu().tolist() if live else []
+        a_orders_h = {mx: o[:a_rows].cpu().tolist() for mx, o in a_orders.items()}
         for row, br, slot, cid, steps, t0, t1 in records:
             v = vals[row][slot]
             self.stats["trials"] += 1
             self.stats["train_steps"] += steps
             chan.send({"ev": "trial_end", "key": br.key, "rung": br.rung, "cid": cid, "steps": steps,
+                       "metric": None if math.isnan(v) else v, "t_start": self._wall(t0), "t_end": self._wall(t1)})
+        for sh, rung, cid, col, steps, t0, t1 in asha_records:
+            v = a_vals[sh.row0 + rung][col]
+            self.stats["trials"] += 1
+            self.stats["train_steps"] += steps
+            if not math.isnan(v):
+                sh.results[rung][cid] = v
+            chan.send({"ev": "trial_end", "key": sh.key, "rung": rung, "cid": cid, "steps": steps,
                        "metric": None if math.isnan(v) else v, "t_start": self._wall(t0), "t_end": self._wall(t1)})
         self.stats["rounds"] += 1
         for row, br in enumerate(brs):
@@ -399,6 +593,35 @@ class ResidentWorker:
                 self.active.remove(br)
                 status = "stopped" if (br.stopped or br.early_stopped) else "succeeded"
                 chan.send({"ev": "bracket_done", "key": br.key, "status": status})
+        # ASHA: refresh every live shard's rung rankings from the device order (NaN results sort last and are not
+        # in ``results``, so they never enter a top set)
+        for sh in live:
+            cols = sorted(sh.configs)
+            order = a_orders_h[sh.maximize]
+            for rung in range(sh.n_rungs):
+                sh.order[rung] = [cols[i] for i in order[sh.row0 + rung]
+                                  if 0 <= i < len(cols) and cols[i] in sh.results[rung]]
+            if a_early.get(sh.key):
+                sh.early_stopped = True
+        for sh in finished:
+            self._finish_shard(sh, chan)
+
+    def _finish_shard(self, sh: _AshaShard, chan: Channel) -> None:
+        """Rung summaries (one ``rung_done`` per rung: its results and the configs promoted out of it), snapshots
+        released, rows freed, ``bracket_done``."""
+        for rung in range(sh.n_rungs):
+            if not sh.results[rung] and rung > 0:
+                continue
+            chan.send({"ev": "rung_done", "key": sh.key, "rung": rung,
+                       "metrics": [[cid, v] for cid, v in sorted(sh.results[rung].items())],
+                       "promoted": sorted(sh.promoted[rung]) if rung < sh.n_rungs - 1 else [],
+                       "early_stop": sh.early_stopped})
+        for cid in list(sh.snap_rung):
+            self.program.executor.drop((sh.key, cid))
+        self.asha_active.remove(sh)
+        sh.row0 = -1
+        status = "stopped" if (sh.stopped or sh.early_stopped) else "succeeded"
+        chan.send({"ev": "bracket_done", "key": sh.key, "status": status})
 
 
 def serve_forever(worker: ResidentWorker, chan: Channel) -> str:

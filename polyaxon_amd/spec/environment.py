@@ -199,13 +199,15 @@ class ExecutorSpec:
       process per GPU holds the model, its flat weights, the captured step and the HBM snapshots, and receives
       trials over a socket.  ``program`` names the trial program (polyflow/programs.py registry or
       ``module:callable``), ``params`` are its build arguments (batch, image size, ``unit_steps`` = training steps
-      per Hyperband resource unit ...), ``max_active_brackets`` bounds how many brackets one executor
-      interleaves (each keeps its promotion snapshots in HBM).
+      per Hyperband resource unit ...), ``max_active_brackets`` bounds how many brackets (or ASHA shards) one
+      executor interleaves (each keeps its promotion snapshots in HBM), ``shards`` cuts an ASHA group into that many
+      independent asynchronous searches, one per executor (default 1).
     """
     kind: str = "process"
     program: Optional[str] = None
     params: Dict[str, Any] = field(default_factory=dict)
     max_active_brackets: int = 8
+    shards: int = 1
 
     @classmethod
     def from_dict(cls, d):
@@ -213,7 +215,7 @@ class ExecutorSpec:
             return None
         if isinstance(d, str):
             d = {"kind": d}
-        unknown = set(d) - {"kind", "program", "params", "max_active_brackets"}
+        unknown = set(d) - {"kind", "program", "params", "max_active_brackets", "shards"}
         if unknown:
             raise MatrixValidationError(f"unknown executor keys {sorted(unknown)}")
         kind = d.get("kind", "process")
@@ -224,7 +226,11 @@ class ExecutorSpec:
         n = int(d.get("max_active_brackets", 8))
         if n < 1:
             raise MatrixValidationError("executor.max_active_brackets must be >= 1")
-        return cls(kind=kind, program=d.get("program"), params=dict(d.get("params") or {}), max_active_brackets=n)
+        shards = int(d.get("shards", 1))
+        if shards < 1:
+            raise MatrixValidationError("executor.shards must be >= 1")
+        return cls(kind=kind, program=d.get("program"), params=dict(d.get("params") or {}), max_active_brackets=n,
+                   shards=shards)
 
     def to_dict(self):
         out: Dict[str, Any] = {"kind": self.kind}
@@ -234,6 +240,8 @@ class ExecutorSpec:
             out["params"] = dict(self.params)
         if self.max_active_brackets != 8:
             out["max_active_brackets"] = self.max_active_brackets
+        if self.shards != 1:
+            out["shards"] = self.shards
         return out
 
     @property

@@ -238,29 +238,153 @@ def test_polyflow_resident_group_end_to_end(tmp_path, cpu_pool_env):
     assert flow.alloc.allocations == {}
 
 
-def test_resident_executor_crash_fails_trials_and_frees_device(tmp_path, cpu_pool_env):
+def _kill_when_running(flow, gid, n_ready=1, timeout=120, exclude=()):
+    end = time.time() + timeout
+    while time.time() < end:
+        snap = [p for p in flow.call(lambda: flow.resident_pool().snapshot()) if p["alive"] and p["pid"] not in exclude]
+        running = flow.store.list_experiments(group_id=gid)
+        if len(snap) >= n_ready and snap[0]["ready"] and any(x["status"] == "running" for x in running):
+            os.kill(snap[0]["pid"], 9)
+            return snap[0]["pid"]
+        time.sleep(0.05)
+    raise AssertionError("no running resident trial to interrupt")
+
+
+def test_resident_executor_crash_redispatches_brackets(tmp_path, cpu_pool_env):
+    """A lost executor's unfinished brackets go to a replacement executor (spawned on the freed device) and continue
+    after their last completed rung; the trials that were running fail, the group still completes every bracket."""
     from polyaxon_amd.polyflow.scheduler import Polyflow
 
     params = dict(TINY, unit_steps=3)
     with Polyflow(str(tmp_path), reconcile_s=0) as flow:
         r = flow.submit(_group(concurrency=1, params=params))
-        end = time.time() + 120
-        pid = None
-        while time.time() < end and pid is None:
-            snap = flow.call(lambda: flow.resident_pool().snapshot())
-            running = flow.store.list_experiments(group_id=r["id"])
-            if snap and snap[0]["ready"] and any(x["status"] == "running" for x in running):
-                pid = snap[0]["pid"]
-            time.sleep(0.05)
-        assert pid is not None
-        os.kill(pid, 9)
-        assert flow.wait("group", r["id"], timeout=120) == "succeeded"  # the group ends; trials are failed
+        pid = _kill_when_running(flow, r["id"])
+        assert flow.wait("group", r["id"], timeout=300) == "succeeded"
         xs = flow.store.list_experiments(group_id=r["id"])
         assert any(x["status"] == "failed" for x in xs)
         assert all(x["status"] in ("succeeded", "failed") for x in xs)
         ev = flow.store.cluster_events()
         assert any(e["kind"] == "resident_executor" and "gone" in e["message"] for e in ev)
-        assert not any(o.startswith("resident:") for o in flow.alloc.allocations)
+        assert any(e["kind"] == "resident_executor" and "re-dispatched" in e["message"] for e in ev)
+        # every bracket reached its last rung: 3 + 2 + 2 rung decisions (more if a rung was redone)
+        its = flow.store.iterations(r["id"])
+        last = {}
+        for it in its:
+            d = it["data"]
+            last[d["iteration"]] = max(last.get(d["iteration"], -1), d["bracket_iteration"])
+        assert last == {0: 2, 1: 1, 2: 1}
+        # the dead executor's device was released; the replacement holds one
+        snap = flow.call(lambda: flow.resident_pool().snapshot())
+        assert any(p["alive"] and p["pid"] != pid for p in snap)
+        assert not any(p["alive"] and p["pid"] == pid for p in snap)
+        owners = [o for o in flow.alloc.allocations if o.startswith("resident:")]
+        assert owners and "resident:1" not in owners
+
+
+def test_resident_group_fails_when_no_executor_can_be_placed(tmp_path, cpu_pool_env):
+    from polyaxon_amd.polyflow.scheduler import Polyflow
+
+    g = _group()
+    g["environment"]["resources"] = {"gpu": 1, "hbm": 100000}
+    with Polyflow(str(tmp_path), reconcile_s=0) as flow:
+        r = flow.submit(g)
+        assert flow.wait("group", r["id"], timeout=30) == "failed"
+        assert "placed" in (flow.store.group_statuses(r["id"])[-1].get("message") or "")
+
+
+def _asha_group(n=14, seed=5, concurrency=1, shards=1, params=None, min_r=1, max_r=9, eta=3):
+    return {"version": 1, "kind": "group", "project": "rt",
+            "hptuning": {"seed": seed, "concurrency": concurrency,
+                         "asha": {"min_resource": min_r, "max_resource": max_r, "eta": eta, "n_experiments": n,
+                                  "resource": {"name": "units", "type": "int"},
+                                  "metric": {"name": "loss", "optimization": "minimize"}, "resume": True},
+                         "matrix": {"lr": {"loguniform": [-4, -1]}, "momentum": {"uniform": [0.8, 0.95]}}},
+            "environment": {"resources": {"gpu": 1},
+                            "executor": {"kind": "resident", "program": "resnet_tiny", "params": params or TINY,
+                                         "shards": shards}}}
+
+
+def test_worker_runs_asha_shard_asynchronously():
+    """One ASHA shard on a worker: every round runs one job; a config enters rung k+1 only from the top
+    floor(n_k / eta) of rung k's results at decision time; promoted jobs resume (train only the extra resource)."""
+    from polyaxon_amd.spec.hptuning import HPTuningConfig
+
+    g = _asha_group(n=10)
+    hp = HPTuningConfig.from_dict(g["hptuning"])
+    w, sched, t = _worker_thread()
+    from polyaxon_amd.polytune.managers import AshaSearchManager
+
+    sugg = AshaSearchManager(hp).get_suggestions()
+    sched.send({"op": "asha", "key": "a0", "hptuning": g["hptuning"], "iteration": 0, "seed": 3,
+                "configs": [{"cid": i, "params": {k: v for k, v in p.items() if k != "units"}}
+                            for i, p in enumerate(sugg)]})
+    evs = _collect(sched, 1)
+    starts = [e for e in evs if e["ev"] == "trial_start"]
+    ends = [e for e in evs if e["ev"] == "trial_end"]
+    assert len(starts) == len(ends) and w.stats["asha_jobs"] == len(ends)
+    assert sum(1 for e in ends if e["rung"] == 0) == 10
+    # replay the decisions: at each promotion the config was in the top floor(n/eta) of its rung so far
+    seen = {0: {}, 1: {}, 2: {}}
+    for e in evs:
+        if e["ev"] == "trial_start" and e["rung"] > 0:
+            prev = seen[e["rung"] - 1]
+            k = int(len(prev) / 3)
+            top = sorted(prev, key=lambda c: (prev[c], c))[:k]
+            assert e["cid"] in top, (e, prev)
+            assert e["resumed"] is True
+            assert e["params"]["units"] == 3 ** e["rung"]
+        if e["ev"] == "trial_end" and e["metric"] is not None:
+            seen[e["rung"]][e["cid"]] = e["metric"]
+    for e in ends:
+        if e["rung"] > 0:
+            assert e["steps"] == (3 ** e["rung"] - 3 ** (e["rung"] - 1)) * TINY["unit_steps"]
+    assert any(e["rung"] == 2 for e in ends)  # promotions reached the top rung
+    rungs = [e for e in evs if e["ev"] == "rung_done"]
+    assert [r["rung"] for r in rungs] == [0, 1, 2]
+    assert [e["status"] for e in evs if e["ev"] == "bracket_done"] == ["succeeded"]
+    assert not any(k[0] == "a0" for k in w.program.executor.snapshots if isinstance(k, tuple))
+    sched.send({"op": "shutdown"})
+    t.join(10)
+
+
+def test_polyflow_resident_asha_group_end_to_end(tmp_path, cpu_pool_env):
+    from polyaxon_amd.polyflow.scheduler import Polyflow
+
+    with Polyflow(str(tmp_path), reconcile_s=0) as flow:
+        r = flow.submit(_asha_group(n=12, concurrency=2, shards=2))
+        assert flow.wait("group", r["id"], timeout=300) == "succeeded"
+        st = flow.store
+        xs = st.list_experiments(group_id=r["id"])
+        assert sum(1 for x in xs if x["declarations"]["units"] == 1) == 12
+        assert {x["status"] for x in xs} == {"succeeded"}
+        for x in xs:
+            assert [s["status"] for s in st.experiment_statuses(x["id"])] == [
+                "created", "scheduled", "starting", "running", "succeeded"]
+        resumed = [x for x in xs if x["cloning_strategy"] == "resume"]
+        assert resumed
+        for x in resumed:  # RESUME lineage: same config, one rung lower, same outputs
+            orig = st.get_experiment(x["original_experiment_id"])
+            assert x["declarations"]["units"] == 3 * orig["declarations"]["units"]
+            assert x["declarations"]["lr"] == orig["declarations"]["lr"]
+            assert x["outputs_path"] == orig["outputs_path"]
+        its = st.iterations(r["id"])
+        assert {it["data"]["unit"] for it in its} == {"asha"}
+        # two shards on two executors
+        assert {tuple(j["devices"]) for x in xs for j in st.experiment_jobs(x["id"])} == {(0,), (1,)}
+
+
+def test_resident_asha_shard_survives_executor_loss(tmp_path, cpu_pool_env):
+    from polyaxon_amd.polyflow.scheduler import Polyflow
+
+    with Polyflow(str(tmp_path), reconcile_s=0) as flow:
+        r = flow.submit(_asha_group(n=9, params=dict(TINY, unit_steps=3)))
+        _kill_when_running(flow, r["id"])
+        assert flow.wait("group", r["id"], timeout=300) == "succeeded"
+        xs = flow.store.list_experiments(group_id=r["id"])
+        done0 = {x["declarations"]["lr"] for x in xs if x["declarations"]["units"] == 1 and x["status"] == "succeeded"}
+        assert len(done0) == 9  # every config was evaluated at rung 0 despite the crash
+        ev = flow.store.cluster_events()
+        assert any("re-dispatched" in e["message"] for e in ev)
 
 
 def test_resident_spec_validation():
@@ -290,7 +414,7 @@ def test_resident_spec_validation():
     assert specification_for(_group()).get_experiment_spec({"lr": 0.01, "momentum": 0.9, "units": 1}).run is None
 
 
-def test_resident_rejects_non_hyperband(tmp_path, cpu_pool_env):
+def test_resident_rejects_grid_random_bo(tmp_path, cpu_pool_env):
     from polyaxon_amd.polyflow.scheduler import Polyflow
     from polyaxon_amd.spec.specification import PolyaxonfileError
 
@@ -319,3 +443,42 @@ def test_bench_cpu_two_ranks_complete_sweeps():
     assert res["trials"] == 46 and res["trials_succeeded"] == 46
     assert res["store_fsm_history_ok"] is True
     assert res["value"] > 0 and res["ms_per_step"] > 0
+
+
+def _bench(*extra, threads="1", timeout=900):
+    import json
+
+    env = dict(os.environ, OMP_NUM_THREADS=threads)
+    env.pop("WORLD_SIZE", None)
+    env.pop("PLX_BENCH_CONTROL", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", *extra], capture_output=True,
+                         text=True, timeout=timeout, env=env, cwd="/tmp")
+    assert out.returncode == 0, out.stderr[-3000:]
+    return json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def test_bench_cpu_four_ranks_scheduler_off_the_ranks():
+    """The scheduler runs in the launcher (no GPU, no rank): its PID is none of the ranks'; per-rank times, trials
+    and executor loads are reported, and the brackets are balanced to within one bracket of the mean load."""
+    from polyaxon_amd.polyflow.programs import bracket_units
+
+    res = _bench("--gpus", "4", "--steps", "2", "--warmup", "0")
+    assert res["n_gpus"] == 4 and res["trials"] == 8 * 23
+    ranks = res["per_rank"]
+    assert len(ranks) == 4 and res["control_pid"] not in {r["pid"] for r in ranks}
+    assert sum(r["trials"] for r in ranks) == res["trials"]
+    assert all(r["elapsed_s"] > 0 for r in ranks)
+    loads = [e["load_units"] for e in res["executors"]]
+    assert len(loads) == 4 and sum(loads) == pytest.approx(8 * 87)
+    biggest = max(bracket_units(9, 3, it, True) for it in range(3))
+    mean = sum(loads) / 4
+    assert all(abs(x - mean) <= biggest for x in loads), loads
+
+
+def test_bench_cpu_single_rank_control_process_and_asha():
+    """--gpus 1 (and torchrun's rank 0) start the scheduler as a process of its own; --search asha times whole
+    asynchronous successive-halving sweeps through the same resident path."""
+    res = _bench("--gpus", "1", "--steps", "1", "--warmup", "0", "--search", "asha", "--asha-n", "12", threads="2")
+    assert res["n_gpus"] == 1 and res["control_pid"] != res["per_rank"][0]["pid"]
+    assert res["config"]["search"].startswith("asha") and res["trials_succeeded"] == res["trials"]
+    assert res["trials"] > 12 and res["trials_resumed"] > 0  # promotions happened and resumed
