@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 import signal
 import threading
 import time
@@ -314,6 +315,13 @@ class Experiment:
         self._done = False
         self._last_beat = 0.0
         self._fault = _step_fault()
+        if "torch" in sys.modules:  # a GPU trial: enforce the replica's HBM reservation (client/budget.py)
+            from polyaxon_amd.client.budget import apply_hbm_budget
+
+            try:
+                apply_hbm_budget()
+            except Exception:  # no device visible / runtime not usable: nothing to cap
+                pass
 
     # ------------------------------------------------------------------ properties
     @property

@@ -53,8 +53,45 @@ def init_from_env(backend: Optional[str] = None, device: Optional[torch.device] 
     return {"rank": rank, "world": world, "local_rank": local, "device": device, "backend": backend}
 
 
+class MetricReducer:
+    """Cross-rank mean of a DP trial's scalar metrics (the loss the tracking client logs, the final result).
+
+    SURVEY.md §2.3 names the metric all-reduce as a framework-owned collective: on the GPU it runs on the C++ RCCL
+    communicator (csrc/rccl_comm.cpp, one ``ncclAllReduce(avg)`` of a few floats on the current HIP stream, no
+    ProcessGroup layer and no host sync); on the CPU (gloo tests) through torch.distributed.  World 1: identity."""
+
+    def __init__(self, device: torch.device, process_group=None, force_comm: bool = False):
+        """``force_comm``: build the RCCL communicator even at world 1 (a single-GPU test of the real path)."""
+        self.device = device
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.comm = None
+        if (self.world > 1 or force_comm) and device.type == "cuda" and dist.is_initialized():
+            from polyaxon_amd.parallel.rccl import RcclComm
+
+            self.comm = RcclComm.from_torch_distributed(process_group)
+
+    def mean(self, t: torch.Tensor) -> torch.Tensor:
+        """Mean over ranks of a small float tensor (returned new; the input is untouched)."""
+        out = t.detach().float().reshape(-1).clone()
+        if self.comm is not None:
+            return self.comm.all_reduce(out, op="avg")
+        if self.world == 1:
+            return out
+        dist.all_reduce(out, op=dist.ReduceOp.SUM, group=self.pg)
+        return out.div_(self.world)
+
+    def close(self) -> None:
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None
+
+
 class FlatDDP:
-    def __init__(self, flat: FlatParams, process_group=None, bucket_mb: float = 64.0, overlap: bool = True):
+    def __init__(self, flat: FlatParams, process_group=None, bucket_mb: float = 64.0, overlap: bool = True,
+                 force_collectives: bool = False):
+        """``force_collectives``: launch every bucket's all-reduce even at world 1 (hooks on), so a single-GPU
+        test executes the real RCCL path and can count the launches (``launched``)."""
         self.flat = flat
         if flat.lp_params is None:
             # the ResNet native ops write weight grads without telling anyone: bucket readiness then needs
@@ -62,7 +99,9 @@ class FlatDDP:
             flat.enable_direct_grads(False)
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
-        self.overlap = overlap and self.world > 1
+        self.force = bool(force_collectives) and dist.is_initialized()
+        self.overlap = overlap and (self.world > 1 or self.force)
+        self.launched = 0
         self.avg_supported = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
         bucket_elems = max(1, int(bucket_mb * 2 ** 20 / 4))
         segs = list(reversed(flat.segments))
@@ -112,6 +151,7 @@ class FlatDDP:
         return hook
 
     def _launch(self, b: int) -> None:
+        self.launched += 1
         lo, hi, _ = self.buckets[b]
         view = self.flat.grad_view(lo, hi)
         if self.avg_supported:
@@ -123,7 +163,7 @@ class FlatDDP:
 
     def finish(self) -> None:
         """Call after backward(): launches any bucket not fired by hooks, waits, averages."""
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return
         if not self.overlap:
             for b in range(len(self.buckets)):
@@ -140,7 +180,7 @@ class FlatDDP:
 
     def broadcast_params(self, src: int = 0) -> None:
         """Make every rank start from rank ``src``'s weights (one collective over the flat buffer)."""
-        if self.world > 1:
+        if self.world > 1 or self.force:
             dist.broadcast(self.flat.params, src=src, group=self.pg)
             self.flat.sync_lp()
 

@@ -74,7 +74,8 @@ def trial_env(*, base_env: Optional[Dict[str, str]] = None, experiment: Dict[str
               cluster: Dict[str, List[str]], devices: List[int], outputs_path: str, logs_path: str,
               declarations: Dict[str, Any], data_paths: Dict[str, str], refs_outputs: Dict[str, List[str]],
               log_level: Optional[str], store_path: Optional[str], api_host: Optional[str],
-              ephemeral_token: Optional[str], master_port: int, local_rank: int) -> Dict[str, str]:
+              ephemeral_token: Optional[str], master_port: int, local_rank: int, hbm_gb: float = 0.0,
+              gpu_share: float = 1.0) -> Dict[str, str]:
     env = dict(base_env if base_env is not None else os.environ)
     for k in list(env):
         if k.startswith("POLYAXON_") or k in ("MASTER_ADDR", "MASTER_PORT", "WORLD_SIZE", "RANK", "LOCAL_RANK",
@@ -122,4 +123,12 @@ def trial_env(*, base_env: Optional[Dict[str, str]] = None, experiment: Dict[str
         env.setdefault("PLX_COLLECTIVE_TIMEOUT_S", "600")
     if not devices:
         env["PLX_CPU_ONLY"] = "1"
+    # HBM budget of the replica (client/budget.py enforces it in the trial process): the reserved GB, else the
+    # device share of a fractional request, so packed trials cannot exhaust each other's memory
+    env.pop("PLX_HBM_GB", None)
+    env.pop("PLX_HBM_FRACTION", None)
+    if devices and hbm_gb > 0:
+        env["PLX_HBM_GB"] = f"{hbm_gb:g}"
+    elif devices and 0 < gpu_share < 1:
+        env["PLX_HBM_FRACTION"] = f"{gpu_share:g}"
     return env

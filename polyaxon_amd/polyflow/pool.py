@@ -115,6 +115,12 @@ class ResidentPool:
         env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in a.devices)
         env.pop("ROCR_VISIBLE_DEVICES", None)
         env["PYTHONUNBUFFERED"] = "1"
+        env.pop("PLX_HBM_GB", None)
+        env.pop("PLX_HBM_FRACTION", None)
+        if hbm_gb > 0:  # the executor's HBM budget (client/budget.py, applied in ResidentWorker.build)
+            env["PLX_HBM_GB"] = f"{hbm_gb:g}"
+        elif 0 < gpu < 1:
+            env["PLX_HBM_FRACTION"] = f"{gpu:g}"
         pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = pkg_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
         log_dir = os.path.join(self.flow.paths.root, "executors")

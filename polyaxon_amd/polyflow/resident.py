@@ -217,9 +217,13 @@ class ResidentWorker:
         from polyaxon_amd.polyflow.programs import build_program
         from polyaxon_amd.polytune.kernels import BracketMetrics
 
+        from polyaxon_amd.client.budget import apply_hbm_budget
+
         t0 = time.time()
         if self.device is None:
             self.device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        if torch.device(self.device).type == "cuda":
+            apply_hbm_budget(self.device)
         self.program = build_program(self.program_name, self.params, self.device)
         self.program.warm()
         ex = self.program.executor

@@ -778,7 +778,8 @@ class Polyflow:
                             declarations=spec.declarations, data_paths=data_paths, refs_outputs=refs,
                             log_level=(spec.logging or {}).get("level"), store_path=self.store_path,
                             api_host=self.api_host, ephemeral_token=uuid.uuid4().hex, master_port=master_port,
-                            local_rank=local_rank)
+                            local_rank=local_rank,
+                            hbm_gb=spec.resources.hbm_gb if spec.resources is not None else 0.0, gpu_share=g)
             env.update(run.extra_env)
             env["POLYAXON_RESTART_COUNT"] = str(run.attempt)
             if spec.kind == Kinds.BUILD:

@@ -57,7 +57,11 @@ def _parse(ap: argparse.ArgumentParser, argv):
 def _device(args):
     if args.cpu or not torch.cuda.is_available() or os.environ.get("PLX_CPU_ONLY") == "1":
         return torch.device("cpu")
-    return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) if torch.cuda.device_count() > 1 else 0)
+    from polyaxon_amd.client.budget import apply_hbm_budget
+
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) if torch.cuda.device_count() > 1 else 0)
+    apply_hbm_budget(dev)  # the replica's HBM reservation (PLX_HBM_GB / PLX_HBM_FRACTION from polyflow)
+    return dev
 
 
 def _tracker():
@@ -167,7 +171,7 @@ def train_lm(argv=None) -> float:
     from polyaxon_amd.models.transformer import Transformer, gpt2_125m, llama3_8b, lm_loss, tiny_llama
     from polyaxon_amd.ops.flat import FlatParams
     from polyaxon_amd.ops.optim import FusedAdamW
-    from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
+    from polyaxon_amd.parallel.ddp import FlatDDP, MetricReducer, init_from_env
 
     ap = _parser("lm")
     ap.add_argument("--model", default="gpt2_125m", choices=["gpt2_125m", "llama3_8b", "tiny"])
@@ -184,6 +188,10 @@ def train_lm(argv=None) -> float:
     backend = "gloo" if args.cpu or not torch.cuda.is_available() else "nccl"
     info = init_from_env(backend)
     dev = info["device"]
+    if dev.type == "cuda":
+        from polyaxon_amd.client.budget import apply_hbm_budget
+
+        apply_hbm_budget(dev)
     cfg = {"gpt2_125m": gpt2_125m, "llama3_8b": llama3_8b, "tiny": tiny_llama}[args.model](
         checkpoint=args.checkpoint_activations)
     seq = min(args.seq, cfg.max_seq_len)
@@ -197,6 +205,7 @@ def train_lm(argv=None) -> float:
     opt = FusedAdamW(flat, lr=args.lr, betas=(0.9, args.beta2), weight_decay=args.weight_decay, step_counter=step)
     ddp = FlatDDP(flat, bucket_mb=args.bucket_mb)
     ddp.broadcast_params()
+    metrics = MetricReducer(dev)  # cross-rank mean of the logged loss (RCCL communicator on the GPU)
     g = torch.Generator(device=dev).manual_seed(args.seed + 1000 * info["rank"])
 
     def batch():  # synthetic tokens drawn on the device: a fresh batch per step costs one tiny kernel
@@ -223,10 +232,12 @@ def train_lm(argv=None) -> float:
         ddp.finish()
         opt.step_()
         step += 1
-        if xp is not None and (it + 1) % args.log_every == 0:
-            xp.log_metrics(step=it + 1, loss=loss.detach())
-        if it == args.steps - 1:
-            loss_val = float(loss.detach())
+        if (it + 1) % args.log_every == 0 or it == args.steps - 1:
+            loss_mean = metrics.mean(loss)  # every rank joins the collective; rank 0 logs it
+            if xp is not None and (it + 1) % args.log_every == 0:
+                xp.log_metrics(step=it + 1, loss=loss_mean[0])
+            if it == args.steps - 1:
+                loss_val = float(loss_mean[0])
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     dt = time.time() - t0
@@ -237,6 +248,7 @@ def train_lm(argv=None) -> float:
     if info["rank"] == 0:
         print(json.dumps({"loss": loss_val, "tokens_per_s": round(tok_s, 1), "world": info["world"],
                           "params_m": round(sum(s.numel for s in flat.segments) / 1e6, 1)}))
+    metrics.close()
     if info["world"] > 1:
         import torch.distributed as dist
 

@@ -49,7 +49,7 @@ def test_mlp_grid_group_on_gpu(tmp_path):
                 "hptuning": {"concurrency": 4, "matrix": {"lr": {"values": [0.01, 0.05]},
                                                           "bs": {"values": [128, 256]}}},
                 "environment": {"resources": {"gpu": {"limits": 0.25}}},
-                "run": {"cmd": f"PYTHONPATH={ROOT} {sys.executable} -m polyaxon_amd.trainers mlp "
+                "run": {"cmd": f"PYTHONPATH={ROOT}${{PYTHONPATH:+:$PYTHONPATH}} {sys.executable} -m polyaxon_amd.trainers mlp "
                                "--lr={{ lr }} --bs={{ bs }} --steps=50"}}
         g = flow.submit(spec, cwd=ROOT)
         assert flow.wait("group", g["id"], timeout=600) == "succeeded"

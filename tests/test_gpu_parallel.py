@@ -19,8 +19,10 @@ def _run(code: str, timeout: int = 180) -> dict:
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    # prepend (never overwrite) PYTHONPATH: the driver's native-load hook rides on it and must see the child's .so
+    pp = os.environ.get("PYTHONPATH")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
-               PYTHONPATH=ROOT)
+               PYTHONPATH=ROOT + (os.pathsep + pp if pp else ""))
     out = subprocess.run([sys.executable, "-c", textwrap.dedent(code)], capture_output=True, text=True,
                          timeout=timeout, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-4000:]
@@ -55,12 +57,16 @@ def test_rccl_comm_single_rank_collectives():
 
 
 def test_flat_ddp_on_rccl_backend_world1():
+    """force_collectives: every bucket's RCCL all-reduce (AVG) really runs through the post-accumulate hooks at
+    world 1, and the averaged gradient equals the single-process one; the metric reducer's RCCL communicator
+    (csrc/rccl_comm.cpp) averages a loss in the same process."""
     res = _run("""
         import json, torch
         import torch.distributed as dist
         from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
         from polyaxon_amd.ops.flat import FlatParams
-        from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
+        from polyaxon_amd.ops import _native
+        from polyaxon_amd.parallel.ddp import FlatDDP, MetricReducer, init_from_env
         import os
         os.environ["WORLD_SIZE"] = "1"
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
@@ -68,11 +74,14 @@ def test_flat_ddp_on_rccl_backend_world1():
         torch.manual_seed(0)
         m = Transformer(tiny_llama()).cuda()
         flat = FlatParams(m, info["device"], channels_last=False)
-        ddp = FlatDDP(flat, bucket_mb=0.01)
+        ddp = FlatDDP(flat, bucket_mb=0.01, force_collectives=True)
         ddp.broadcast_params()
         tok = torch.randint(0, 256, (4, 16), device="cuda")
-        lm_loss(m(tok), tok).backward()
+        loss = lm_loss(m(tok), tok)
+        loss.backward()
         ddp.finish()
+        red = MetricReducer(info["device"], force_comm=True)
+        lm = red.mean(loss)
         torch.cuda.synchronize()
         g = flat.grads.clone()
         # the same step without DDP
@@ -80,9 +89,13 @@ def test_flat_ddp_on_rccl_backend_world1():
         m2 = Transformer(tiny_llama()).cuda()
         f2 = FlatParams(m2, info["device"], channels_last=False)
         lm_loss(m2(tok), tok).backward()
-        print(json.dumps({"backend": dist.get_backend(), "buckets": len(ddp.buckets),
-                          "err": float((g - f2.grads).abs().max()), "norm": float(g.norm())}))
+        print(json.dumps({"backend": dist.get_backend(), "buckets": len(ddp.buckets), "launched": ddp.launched,
+                          "err": float((g - f2.grads).abs().max()), "norm": float(g.norm()),
+                          "loss": float(loss), "loss_mean": float(lm[0]), "rccl": red.comm is not None,
+                          "loaded": "plx_rccl" in _native._loaded}))
+        red.close()
         dist.destroy_process_group()
     """)
-    assert res["backend"] == "nccl" and res["buckets"] > 1
+    assert res["backend"] == "nccl" and res["buckets"] > 1 and res["launched"] == res["buckets"]
     assert res["norm"] > 0 and res["err"] < 1e-5
+    assert res["rccl"] and res["loaded"] and abs(res["loss_mean"] - res["loss"]) < 1e-6

@@ -42,6 +42,52 @@ def _worker(rank, world, port, q, overlap):
     dist.destroy_process_group()
 
 
+def _reducer_worker(rank, world, port, q):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.parallel.ddp import FlatDDP, MetricReducer, init_from_env
+
+    init_from_env("gloo")
+    torch.manual_seed(0)
+    model = Transformer(tiny_llama())
+    flat = FlatParams(model, "cpu", channels_last=False)
+    ddp = FlatDDP(flat, bucket_mb=0.01, force_collectives=True)
+    red = MetricReducer(torch.device("cpu"))
+    torch.manual_seed(7 + rank)
+    tokens = torch.randint(0, 256, (2, 16))
+    loss = lm_loss(model(tokens), tokens)
+    loss.backward()
+    ddp.finish()
+    m = red.mean(loss)
+    q.put((rank, float(loss), float(m[0]), ddp.launched, len(ddp.buckets)))
+    dist.destroy_process_group()
+
+
+def test_metric_reducer_and_bucket_launches_gloo_world2():
+    """The DP trial's metric all-reduce (MetricReducer: the RCCL communicator on the GPU, torch.distributed here)
+    returns the cross-rank mean on every rank, and every gradient bucket's all-reduce is launched exactly once."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reducer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    mean = (res[0][1] + res[1][1]) / 2
+    assert res[0][1] != res[1][1]
+    assert all(abs(r[2] - mean) < 1e-5 for r in res)
+    assert all(r[3] == r[4] > 1 for r in res)
+
+
 @pytest.mark.parametrize("overlap", [True, False])
 def test_flat_ddp_gloo_world2(overlap):
     ctx = mp.get_context("spawn")

@@ -121,3 +121,40 @@ def test_multi_rank_trials_get_the_rccl_watchdog():
     assert e["TORCH_NCCL_ASYNC_ERROR_HANDLING"] == "1" and e["PLX_COLLECTIVE_TIMEOUT_S"] == "600"
     e = _env(framework="pytorch", cluster=c, base_env={"PLX_COLLECTIVE_TIMEOUT_S": "30"})
     assert e["PLX_COLLECTIVE_TIMEOUT_S"] == "30"  # operator override wins
+
+
+def test_trial_env_carries_the_hbm_budget():
+    """resources.hbm (GB) and fractional gpu shares reach the trial as PLX_HBM_GB / PLX_HBM_FRACTION, which
+    client/budget.py turns into a caching-allocator cap (set_per_process_memory_fraction)."""
+    from polyaxon_amd.client.budget import budget_fraction
+
+    e = _env(hbm_gb=72.0, gpu_share=0.25, base_env={"PLX_HBM_FRACTION": "0.9"})
+    assert e["PLX_HBM_GB"] == "72" and "PLX_HBM_FRACTION" not in e
+    e = _env(gpu_share=0.25)
+    assert e["PLX_HBM_FRACTION"] == "0.25" and "PLX_HBM_GB" not in e
+    e = _env()
+    assert "PLX_HBM_GB" not in e and "PLX_HBM_FRACTION" not in e
+    e = _env(devices=[], hbm_gb=10.0)  # CPU replica: nothing to cap
+    assert "PLX_HBM_GB" not in e
+    total = 288 * 2 ** 30
+    assert budget_fraction(total, {"PLX_HBM_GB": "72"}) == pytest.approx(0.25)
+    assert budget_fraction(total, {"PLX_HBM_FRACTION": "0.5"}) == 0.5
+    assert budget_fraction(total, {"PLX_HBM_GB": "1000"}) == 1.0
+    assert budget_fraction(total, {}) is None
+
+
+def test_scheduler_exports_the_budget_to_packed_trials(tmp_path):
+    """Two gpu: 0.5 trials with hbm: 100 share one device; each sees its own budget in its environment."""
+    from polyaxon_amd.polyflow.devices import Device, DeviceAllocator
+    from polyaxon_amd.polyflow.scheduler import Polyflow
+
+    with Polyflow(str(tmp_path), allocator=DeviceAllocator([Device(0)]), reconcile_s=0) as flow:
+        ids = [flow.submit({"version": 1, "kind": "experiment",
+                            "run": {"cmd": "echo BUDGET=$PLX_HBM_GB/$PLX_HBM_FRACTION/$HIP_VISIBLE_DEVICES"},
+                            "environment": {"resources": {"gpu": 0.5, "hbm": 100}}})["id"] for _ in range(2)]
+        for i in ids:
+            assert flow.wait("experiment", i, timeout=30) == "succeeded"
+        for i in ids:
+            x = flow.store.get_experiment(i)
+            logs = open(flow.paths.replica_log(x["logs_path"], "master", 0)).read()
+            assert "BUDGET=100//0" in logs
