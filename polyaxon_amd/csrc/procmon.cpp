@@ -152,13 +152,17 @@ PLX_API int plx_pm_wait(void* h, int timeout_ms, int* out_pid, int* out_status) 
     int st = 0;
     pid_t r = waitpid(pid, &st, WNOHANG);
     if (r == 0) continue;  // spurious
-    epoll_ctl(m->ep, EPOLL_CTL_DEL, ev.data.fd, nullptr);
-    close(ev.data.fd);
+    // Forget the pidfd BEFORE closing it: once closed, its number can be handed to the next pidfd_open on the
+    // spawning thread, and erasing fd_to_pid[fd] after that would drop the NEW child's entry -- its exit would
+    // then never be reaped (level-triggered epoll keeps reporting an fd this loop no longer knows).  Found as an
+    // intermittent timeout of tests/native/procmon_stress.cpp under TSan (slow spawns widen the window).
     {
       std::lock_guard<std::mutex> lk(m->mu);
       m->fd_to_pid.erase(ev.data.fd);
       m->pid_to_fd.erase(pid);
     }
+    epoll_ctl(m->ep, EPOLL_CTL_DEL, ev.data.fd, nullptr);
+    close(ev.data.fd);
     *out_pid = (int)pid;
     if (r < 0)
       *out_status = -255;

@@ -60,7 +60,7 @@ class GroupDriver:
     def create_experiment(self, params: Dict[str, Any], enqueue: bool = False, original_id: Optional[int] = None,
                           strategy: Optional[str] = None) -> int:
         if original_id is not None:
-            return self.flow._clone(original_id, strategy, params, None, group_id=self.gid)
+            return self.flow._clone(original_id, strategy, params, None, group_id=self.gid, enqueue=enqueue)
         xspec = self.spec.get_experiment_spec(params)
         return self.flow._create_experiment(xspec, self.project, self.user, self.cwd, group_id=self.gid,
                                             enqueue=enqueue)
@@ -93,7 +93,7 @@ class GroupDriver:
         if self.stopped:  # teardown in progress (stop() itself finishes pending trials)
             self._check_finished()
             return
-        if self._should_stop_early():
+        if self._should_stop_early(xid):
             self.flow.auditor.record("experiment_group.stopped", "experiment_group", self.gid, reason="early_stopping")
             self.stop(pending_only=not self.stop_running_on_early_stop, message="Early stopping")
             return
@@ -118,13 +118,23 @@ class GroupDriver:
         self.flow.auditor.record(f"experiment_group.{ {'stopped': 'done', 'failed': 'failed'}.get(status, status)}",
                                  "experiment_group", self.gid)
 
-    def _should_stop_early(self) -> bool:
+    def _should_stop_early(self, xid: Optional[int] = None) -> bool:
         """Reference ExperimentGroup.should_stop_early (db/models/experiment_groups.py:211-221): any experiment whose
-        ``last_metric`` crosses any rule.  The group's metrics are pulled in one query into an [experiments x
-        metrics] matrix and every rule is evaluated in one ``early_stop_any`` call (HIP kernel for device tensors,
-        the same vectorised reduction on the host otherwise)."""
+        ``last_metric`` crosses any rule.  Incremental: the reference re-reads every experiment of the group per
+        check (O(n^2) over a group); a rule can only newly trip on the experiment that just finished, so only its
+        ``last_metric`` is read and tested (``xid``), the group-wide scan is the fallback for a check without one.
+        A whole-group scan evaluates every rule in one ``early_stop_any`` call (HIP kernel for device tensors, the
+        same vectorised reduction on the host otherwise)."""
         rules = self.hp.early_stopping
         if not rules:
+            return False
+        if xid is not None:
+            last = (self.store.get_experiment(xid) or {}).get("last_metric") or {}
+            for r in rules:
+                v = last.get(r.metric)
+                if isinstance(v, (int, float)) and not math.isnan(v):
+                    if (v >= float(r.value)) if Optimization.maximize(r.optimization) else (v <= float(r.value)):
+                        return True
             return False
         import numpy as np
         import torch
@@ -179,15 +189,22 @@ class GridRandomDriver(GroupDriver):
 
 
 class HyperbandDriver(GroupDriver):
-    """Synchronous rung barrier per bracket, exactly like the reference — but event-driven."""
+    """Hyperband in process mode: the reference's arithmetic and synchronous rung barrier *within* a bracket, but the
+    ``s_max + 1`` brackets are independent successive-halving runs, so they all start at once and share the group's
+    ``concurrency`` slots -- the reference runs them one after another (polyaxon/hpsearch/tasks/hyperband.py:7-83),
+    which leaves devices idle while a small bracket (e.g. 3 configs of ``max_iter: 9``) finishes.  Promotions go to
+    the front of the queue (deeper rungs first), so a bracket's later rungs do not wait behind the other brackets'
+    first rungs.  Every (bracket, rung) is an iteration row as in the reference."""
 
     def begin(self) -> None:
         self.m: HyperbandSearchManager = self.manager
-        self.it = self.m.next_iteration(None)
-        self.iteration_id: Optional[int] = None
-        self._launch_iteration(self.m.get_suggestions(self.it), None)
+        self.brk: Dict[int, Dict[str, Any]] = {}          # iteration (bracket index) -> {"it", "iid", "done"}
+        self.xp_bracket: Dict[int, int] = {}
+        for i in range(self.m.s_max + 1):
+            it = HyperbandIterationConfig(iteration=i, bracket_iteration=0)
+            self._launch(it, self.m.get_suggestions(it), None)
 
-    def _launch_iteration(self, params_list: List[Dict], originals: Optional[List[int]]) -> None:
+    def _launch(self, it: HyperbandIterationConfig, params_list: List[Dict], originals: Optional[List[int]]) -> None:
         ids = []
         strategy = "resume" if self.hp.hyperband.resume else "restart"
         for i, params in enumerate(params_list):
@@ -195,34 +212,46 @@ class HyperbandDriver(GroupDriver):
                 ids.append(self.create_experiment(params))
             else:
                 ids.append(self.create_experiment(params, original_id=originals[i], strategy=strategy))
-        self.it.experiment_ids = ids
-        self.iteration_id = self.store.create_iteration(self.gid, self.it.to_dict())
-        self.queue.extend(ids)
+        it.experiment_ids = ids
+        iid = self.store.create_iteration(self.gid, it.to_dict())
+        self.brk[it.iteration] = {"it": it, "iid": iid, "done": False}
+        for x in ids:
+            self.xp_bracket[x] = it.iteration
+        if originals is None:
+            self.queue.extend(ids)
+        else:
+            self.queue[:0] = ids
+
+    def has_more_work(self) -> bool:
+        return not self.stopped and any(not b["done"] for b in self.brk.values())
 
     def advance(self, xid: int, status: str) -> None:
-        if any(x not in self.finished for x in self.it.experiment_ids):
-            return  # rung barrier: wait for the whole iteration
-        metric = self.hp.hyperband.metric.name
-        self.it.experiments_metrics = [(x, v) for x, v in ((x, self.metric_of(x, metric))
-                                                           for x in self.it.experiment_ids) if v is not None]
-        self.store.update_iteration(self.iteration_id, self.it.to_dict())
-        if self.m.is_done(self.it):
+        b = self.brk.get(self.xp_bracket.get(xid, -1))
+        if b is None or b["done"]:
             return
-        nxt = self.m.next_iteration(self.it)
-        if nxt.iteration == self.it.iteration:  # reduce: promote the top-k
-            keep_ids = self.m.reduce(self.it)
-            r = self.hp.hyperband.resource.cast_value(
-                self.m.get_n_resources_for_iteration(nxt.iteration, nxt.bracket_iteration))
-            params = []
-            for x in keep_ids:
-                decl = dict(self.store.get_experiment(x)["declarations"])
-                decl[self.hp.hyperband.resource.name] = r
-                params.append(decl)
-            self.it = nxt
-            self._launch_iteration(params, keep_ids)
-        else:
-            self.it = nxt
-            self._launch_iteration(self.m.get_suggestions(self.it), None)
+        it = b["it"]
+        if any(x not in self.finished for x in it.experiment_ids):
+            return  # rung barrier of this bracket only
+        metric = self.hp.hyperband.metric.name
+        it.experiments_metrics = [(x, v) for x, v in ((x, self.metric_of(x, metric))
+                                                      for x in it.experiment_ids) if v is not None]
+        self.store.update_iteration(b["iid"], it.to_dict())
+        if not self.m.should_reduce_configs(it.iteration, it.bracket_iteration):
+            b["done"] = True  # this bracket's last rung
+            return
+        keep_ids = self.m.reduce(it)
+        nxt = HyperbandIterationConfig(iteration=it.iteration, bracket_iteration=it.bracket_iteration + 1)
+        r = self.hp.hyperband.resource.cast_value(
+            self.m.get_n_resources_for_iteration(nxt.iteration, nxt.bracket_iteration))
+        params = []
+        for x in keep_ids:
+            decl = dict(self.store.get_experiment(x)["declarations"])
+            decl[self.hp.hyperband.resource.name] = r
+            params.append(decl)
+        if not params:
+            b["done"] = True
+            return
+        self._launch(nxt, params, keep_ids)
 
 
 class BODriver(GroupDriver):

@@ -1129,7 +1129,9 @@ class Polyflow:
             raise ValueError(f"unknown cloning strategy {strategy}")
         return self.call(self._clone, xid, strategy, declarations, content)
 
-    def _clone(self, xid: int, strategy: str, declarations, content, group_id=None) -> int:
+    def _clone(self, xid: int, strategy: str, declarations, content, group_id=None, enqueue: bool = True) -> int:
+        """``enqueue=False``: a group driver's promotion -- the driver starts it from its own queue (bounded by the
+        group's concurrency); enqueuing it here as well would place the same run twice."""
         orig = self.store.get_experiment(xid)
         if orig is None:
             raise KeyError(f"experiment {xid} not found")
@@ -1142,7 +1144,7 @@ class Polyflow:
         cwd = old.cwd if old else os.getcwd()
         new = self._create_experiment(spec, proj, orig["user"], cwd,
                                       group_id=orig["group_id"] if group_id is None else group_id,
-                                      original_id=xid, strategy=strategy)
+                                      original_id=xid, strategy=strategy, enqueue=enqueue)
         self.auditor.record(f"experiment.{ {'restart': 'restarted', 'resume': 'resumed', 'copy': 'copied'}[strategy]}",
                             "experiment", new, original=xid)
         return new

@@ -345,3 +345,41 @@ def test_pipeline_dag_triggers_and_retries(tmp_path):
         assert ops["cleanup"]["status"] == "succeeded"
     finally:
         flow.shutdown()
+
+
+def test_process_mode_hyperband_runs_brackets_concurrently(tmp_path):
+    """examples/resnet50_hyperband.yml (max_iter 9, eta 3, concurrency 8) in process mode with stub trials on 8
+    virtual devices: the three brackets share the slots, so while any trial waits in the group's queue all 8 devices
+    are busy (the reference runs the brackets one after another: bracket 0's 3-config rung 1 would idle 5 GPUs)."""
+    import yaml
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = yaml.safe_load(open(os.path.join(root, "examples", "resnet50_hyperband.yml")))
+    stub = TRIAL.replace("d.get('steps', 1)", "d['units']").replace("float(d.get('sleep', 0.05))", "0.4")
+    stub = stub.replace("(d['lr'] - 0.3) ** 2", "abs(d['lr'] - 0.3)")
+    spec["run"]["cmd"] = f"PYTHONPATH={root} {PY} -c \"{stub}\""
+    flow = _flow(tmp_path, n_gpus=8)
+    try:
+        g = flow.submit(spec)
+        gid = g["id"]
+        samples = []
+        end = time.time() + 120
+        while time.time() < end:
+            st = flow.store.group_status_counts(gid)
+            running = sum(st.get(k, 0) for k in ("scheduled", "starting", "running"))
+            queued = st.get("created", 0)
+            samples.append((running, queued))
+            if flow.store.get_group(gid)["status"] in ("succeeded", "failed", "stopped"):
+                break
+            time.sleep(0.02)
+        assert flow.store.get_group(gid)["status"] == "succeeded"
+        xs = flow.store.list_experiments(group_id=gid)
+        assert len(xs) == 9 + 5 + 3 + 3 + 1 + 1 + 1  # reference bracket arithmetic (incl. the s=0 reduction)
+        busy = [r for r, q in samples if q > 0]
+        assert busy and max(r for r, _ in samples) == 8
+        assert sum(1 for r in busy if r == 8) >= 0.8 * len(busy), samples
+        its = flow.store.iterations(gid)
+        assert sorted((i["data"]["iteration"], i["data"]["bracket_iteration"]) for i in its) == [
+            (0, 0), (0, 1), (0, 2), (1, 0), (1, 1), (2, 0), (2, 1)]
+    finally:
+        flow.shutdown()
