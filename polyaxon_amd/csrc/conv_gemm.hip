@@ -44,6 +44,8 @@ struct ConvGeom {
     // per-tap byte offsets for the NT GEMM's staging (filled by finish_geom): A row shift (offh*W + offw)*C*2
     // and B column start btap*C*2 -- dword arrays so a uniform tap index reads them with scalar loads
     int tap_a[9], tap_b[9];
+    // halo mode (stride-1 3x3 on the same grid): flattened pixel shift of tap t, offh[t] * W + offw[t]
+    int tap_shift[9];
     // x / Wr and q / Hr as __umulhi(x, m): m = floor(2^32 / d) + 1 is exact while x * d < 2^32, which holds for
     // pixel indices (< 2^24) and row-grid sides (<= 255); m = 0 marks d == 1
     uint32_t mWr, mHr;
@@ -61,6 +63,7 @@ inline ConvGeom finish_geom(ConvGeom g) {
     for (int t = 0; t < 9; ++t) {
         g.tap_a[t] = t < g.ntaps ? (g.offh[t] * g.W + g.offw[t]) * g.C * 2 : 0;
         g.tap_b[t] = t < g.ntaps ? g.btap[t] * g.C * 2 : 0;
+        g.tap_shift[t] = t < g.ntaps ? g.offh[t] * g.W + g.offw[t] : 0;
         if (t >= g.ntaps) continue;
         int i = 0, j = 0;
         while (i < g.nh && g.hv[i] != g.offh[t]) ++i;
@@ -150,14 +153,18 @@ __device__ __forceinline__ int nt_swz(int row) { return (row >> 1) & 7; }
 // and 4 blocks per CU, whose interleaving hides the staging instead (MINB = blocks per CU the registers allow)
 // BWD: the data-gradient epilogue (D add, ReLU-masked D, BatchNorm-backward partials); !BWD: the forward one (channel
 // stats).  Compile-time so each kernel only holds the epilogue registers it uses.
-// MODE: 0 dense rows, 1 implicit-GEMM convolution (ConvGeom gather), 2 the ResNet stem (see plx_stem_conv_fwd)
+// MODE: 0 dense rows, 1 implicit-GEMM convolution (ConvGeom gather), 2 the ResNet stem (see plx_stem_conv_fwd),
+// 3 halo convolution: a stride-1 3x3 convolution on the same row grid whose input rows are staged ONCE per 64-channel
+// chunk as a halo (the block's BM output pixels +- (W + 1) flattened pixels) and read by all 9 taps from LDS at a
+// per-tap row shift; only the weights are staged per tap.  Mode 1 re-stages the gathered A rows for every tap: 9x the
+// input bytes through the per-CU LDS-DMA path, which bounds those layers (~52 GB/s per CU, 34 % of MFMA peak).
 template <int BM, int BN, int WGM, int WGN, int MODE, int MINB = 2, int NBUF = 2, bool BWD = false>
 __global__ void __launch_bounds__(NTHREADS, MINB)
 gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
                int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
                float* __restrict__ stats, ConvGeom geo, const __bf16* __restrict__ D, int ldd, BnBwd bnr,
                const uint8_t* __restrict__ dmask) {
-    constexpr bool CONV = MODE == 1, STEM = MODE == 2;
+    constexpr bool CONV = MODE == 1 || MODE == 3, STEM = MODE == 2, HALO = MODE == 3;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
     constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -179,7 +186,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     int a_off[BM / 32];                                     // byte offsets
     uint32_t a_ok[BM / 32];
 #pragma unroll
-    for (int i = 0; i < BM / 32; ++i) {
+    for (int i = 0; i < (HALO ? 0 : BM / 32); ++i) {
         const int row = (i * 4 + wave) * 8 + (lane >> 3);
         const int lc = (lane & 7) ^ nt_swz(row);
         const int gm = m0 + row;
@@ -257,6 +264,90 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
 #pragma unroll
         for (int b = 0; b < RM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    const int fr = lane & 15, fq = lane >> 4;
+    if constexpr (HALO) {
+        // ---- halo mode: LDS = [HR halo rows x 128 B] then 2 weight stages [BN x 128 B]
+        const int W = geo.W, hoff = W + 1;
+        const int HR = (BM + 2 * W + 2 + 31) & ~31;
+        char* hal = smem;
+        char* bsm = smem + HR * 128;
+        const int m_lo = m0 - hoff;                         // flattened pixel of halo row 0 (may be < 0: zeros)
+        const int nck = geo.C / BK;
+        auto stage_halo = [&](int ck) {
+            for (int i = 0; i < HR / 32; ++i) {
+                const int row = (i * 4 + wave) * 8 + (lane >> 3);
+                const int p = m_lo + row;
+                const int lc = (lane & 7) ^ nt_swz(row);
+                const uint32_t off = (unsigned)p < (unsigned)M ? (uint32_t)((p * lda + ck * BK + lc * 8) * 2) : OOB;
+                blds16(ra, off, hal + (i * 4 + wave) * 1024);
+            }
+        };
+        auto stage_bt = [&](int buf, int ck, int t) {
+            const int bk0 = geo.tap_b[t] + ck * BK * 2;
+#pragma unroll
+            for (int i = 0; i < BN / 32; ++i) blds16(rb, (uint32_t)(b_off[i] + bk0), bsm + buf * B_BYTES + (i * 4 + wave) * 1024);
+        };
+        // tap validity of this lane's fragment rows (bit t: the tap's source pixel is inside the image): the halo
+        // holds the flattened neighbours, which cross image rows / images at the borders -- those taps read zero
+        uint32_t vb[RM];
+#pragma unroll
+        for (int rm = 0; rm < RM; ++rm) {
+            const int gm = m0 + wm * WTM + rm * 16 + fr;
+            int n, r, c;
+            row_coords(gm, geo, n, r, c);
+            uint32_t ok = 0;
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+                ok |= ((unsigned)(r + geo.offh[t]) < (unsigned)geo.H && (unsigned)(c + geo.offw[t]) < (unsigned)geo.W)
+                          ? 1u << t : 0u;
+            vb[rm] = gm < M ? ok : 0u;
+        }
+        stage_halo(0);
+        stage_bt(0, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const bf16x8 zero8 = {};
+        int ck = 0, t = 0;
+        const int nsteps = nck * 9;
+        for (int st = 0; st < nsteps; ++st) {
+            const int cur = st & 1;
+            if (st + 1 < nsteps) stage_bt(cur ^ 1, t == 8 ? ck + 1 : ck, t == 8 ? 0 : t + 1);
+            const int shift = hoff + geo.tap_shift[t];
+            const char* Bs = bsm + cur * B_BYTES;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                bf16x8 fa[RN], fb[RM];
+#pragma unroll
+                for (int rn = 0; rn < RN; ++rn) {
+                    const int row = wn * WTN + rn * 16 + fr;
+                    const int pc = (kk * 4 + fq) ^ nt_swz(row);
+                    fa[rn] = *(const bf16x8*)(Bs + row * 128 + pc * 16);
+                }
+#pragma unroll
+                for (int rm = 0; rm < RM; ++rm) {
+                    const int hrow = wm * WTM + rm * 16 + fr + shift;
+                    const int pc = (kk * 4 + fq) ^ nt_swz(hrow);
+                    const bf16x8 v = *(const bf16x8*)(hal + hrow * 128 + pc * 16);
+                    fb[rm] = (vb[rm] >> t) & 1u ? v : zero8;
+                }
+#pragma unroll
+                for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+                    for (int rm = 0; rm < RM; ++rm)
+                        acc[rn][rm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rn], fb[rm], acc[rn][rm], 0, 0, 0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (++t == 9) {
+                t = 0;
+                if (++ck < nck) {                           // next channel chunk: restage the halo (all reads done)
+                    stage_halo(ck);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                }
+            }
+        }
+    } else {
     const int nk = K / BK;
     const int cdim = CONV ? geo.C : K;                      // channels per tap
     stage(0, 0, 0, 0);
@@ -264,7 +355,6 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     if (sc == cdim) { sc = 0; ++st; }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const int fr = lane & 15, fq = lane >> 4;
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = NBUF == 2 ? kt & 1 : 0;
         if (NBUF == 1 && kt > 0) {                          // restage the single buffer (the loop's tail barrier
@@ -305,6 +395,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         if (NBUF == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
+    }  // !HALO
     // Epilogue through LDS (the k-loop's last barrier freed it): D[n][m] has column m = fr and rows
     // n = 4*fq + r in each lane, i.e. 4 consecutive channels of one pixel.  Stage the bf16 tile as [m][n] rows
     // padded by 16 B, then store whole output rows with 16 B per lane (a wave instruction writes contiguous
@@ -708,6 +799,41 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// Halo convolution (MODE 3): LDS = the halo image (rows rounded to 32) + two weight stages, or the epilogue tile if
+// larger; the halo depends on the image width, so the size is a launch argument (attribute set to the maximum).
+template <int BM, int BN, int WGM, int WGN, int MINB>
+int launch_halo(const void* A, const void* B, void* C, int M, int N, int lda, int ldb, int ldc, const void* zero,
+                float* stats, hipStream_t s, const ConvGeom& geo, const void* D, int ldd, BnBwd bnr) {
+    constexpr int TILE = BM * (BN * 2 + 16), RED = NTHREADS * 17 * 4;
+    constexpr int EPI = TILE > RED ? TILE : RED;
+    const int HR = (BM + 2 * geo.W + 2 + 31) & ~31;
+    int lds = HR * 128 + 2 * BN * BK * 2;
+    if (lds < EPI) lds = EPI;
+    if (lds > 160 * 1024) return -4;
+    auto kf = gemm_nt_kernel<BM, BN, WGM, WGN, 3, MINB, 2, false>;
+    auto kb = gemm_nt_kernel<BM, BN, WGM, WGN, 3, MINB, 2, true>;
+    static int attr = set_lds(kf, 160 * 1024) | set_lds(kb, 160 * 1024);
+    if (attr) return attr;
+    const bool bwd = D != nullptr || bnr.part != nullptr;
+    if (bwd && stats != nullptr) return -1;
+    auto k = bwd ? kb : kf;
+    const int nwg = ((M + BM - 1) / BM) * (N / BN);
+    hipLaunchKernelGGL(k, dim3(nwg), dim3(NTHREADS), lds, s, (const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N,
+                       9 * geo.C, lda, ldb, ldc, (const __bf16*)zero, stats, geo, (const __bf16*)D, ldd, bnr,
+                       (const uint8_t*)nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// stride-1 3x3 convolutions on the same grid run in halo mode (A/B knob plx_set_halo: 0 off, 1 on)
+int g_halo = 1;
+
+inline bool halo_ok(const ConvGeom& g) {
+    if (!g_halo || g.ntaps != 9 || g.S != 1 || g.OS != 0 || g.Hr != g.H || g.Wr != g.W || g.C % BK) return false;
+    for (int t = 0; t < 9; ++t)
+        if (g.offh[t] < -1 || g.offh[t] > 1 || g.offw[t] < -1 || g.offw[t] > 1) return false;
+    return true;
+}
+
 // Single-buffer NT GEMM (NBUF = 1) or double-buffered.  The single-buffer kernels run 4 blocks per CU (3 for the
 // 256x64 conv tile), which hides the staging better than double buffering at 2 blocks -- when the grid has the
 // blocks to fill them (>= 3 per CU), or when K == BK leaves nothing to double-buffer.  Measured on the ResNet-50
@@ -824,6 +950,9 @@ int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int 
 
 // A/B knob: single-buffer NT GEMM mode (see nt_single)
 void plx_set_nt_single_stage(int mode) { g_nt_single_stage = mode; }
+
+// A/B knob: halo mode for the stride-1 3x3 convolutions (1 on, 0 the per-tap gather)
+void plx_set_halo(int on) { g_halo = on ? 1 : 0; }
 
 // weight-gradient slicing knobs; workspace sizes follow them, so set before sizing / launching
 void plx_set_tn_plan(int blocks_per_cu, int slab_mb) {
@@ -976,6 +1105,12 @@ int nt_conv_any(const void* A, const void* B, void* C, int M, int N, const ConvG
                 const void* zero, float* stats, hipStream_t s, const void* D = nullptr, const BnBwd& bnr = {}) {
     const bool bwd = D != nullptr || bnr.part != nullptr;
     const int K = g.ntaps * g.C;
+    if (halo_ok(g)) {
+        const int ldd = D != nullptr ? ldc : 0;
+        if (N % 128 == 0)
+            return launch_halo<128, 128, 2, 2, 2>(A, B, C, M, N, g.C, ldb, ldc, zero, stats, s, g, D, ldd, bnr);
+        return launch_halo<256, 64, 4, 1, 2>(A, B, C, M, N, g.C, ldb, ldc, zero, stats, s, g, D, ldd, bnr);
+    }
     if (N % 128 == 0)
         return nt_single(bwd, true, K, ((M + 127) / 128) * (N / 128))
                    ? nt_conv<128, 128, 2, 2, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr)

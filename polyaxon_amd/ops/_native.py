@@ -154,6 +154,8 @@ def lib(name: str) -> ctypes.CDLL:
         _declare(name, handle)
         if name == "plx_conv" and os.environ.get("PLX_NT_SINGLE_STAGE"):  # A/B knob (csrc/conv_gemm.hip)
             handle.plx_set_nt_single_stage(int(os.environ["PLX_NT_SINGLE_STAGE"]))
+        if name == "plx_conv" and os.environ.get("PLX_HALO"):  # A/B knob: halo mode of the 3x3 convolutions
+            handle.plx_set_halo(int(os.environ["PLX_HALO"]))
         if name == "plx_conv" and os.environ.get("PLX_TN_PLAN"):  # A/B knob: "blocks_per_cu,slab_mb"
             bpc, mb = (int(v) for v in os.environ["PLX_TN_PLAN"].split(","))
             handle.plx_set_tn_plan(bpc, mb)
@@ -230,6 +232,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_set_tn_plan": [_I, _I],
         "plx_set_tn_sizes": [_I, _I],
         "plx_set_nt_single_stage": [_I],
+        "plx_set_halo": [_I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
         "plx_weight_prepk": [_P, _L, _L, _L, _L, _P, _P, _I, _I, _I, _P],

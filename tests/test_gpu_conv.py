@@ -396,3 +396,40 @@ def test_stem_conv_matches_conv2d(cuda, shape):
     w = conv.weight.detach().clone().requires_grad_()
     F.conv2d(x.float(), w, None, 2, 3).backward(g)
     torch.testing.assert_close(conv.weight.grad, w.grad, rtol=3e-2, atol=3e-2 * float(w.grad.abs().max()))
+
+
+@pytest.mark.parametrize("shape,cout", [((2, 64, 56, 56), 64), ((2, 128, 28, 28), 128), ((3, 256, 14, 14), 256),
+                                        ((5, 512, 7, 7), 512), ((1, 64, 3, 17), 128), ((3, 192, 9, 5), 64)])
+def test_conv3x3_halo_matches_gather_and_fp32(cuda, shape, cout):
+    """Halo mode (the input rows staged once per 64-channel chunk, read by all 9 taps at a row shift) against the
+    per-tap gather and an fp32 F.conv2d: forward and data gradient, ResNet-50 stage shapes plus ragged ones (partial
+    last tile, images narrower than a tile, several chunks)."""
+    from polyaxon_amd.ops import _native
+    from polyaxon_amd.ops.conv import ConvKxK
+
+    lib = _native.lib("plx_conv")
+    torch.manual_seed(11)
+    conv = ConvKxK(shape[1], cout, 3, 1).to(cuda)
+    conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
+    x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    out = {}
+    try:
+        for halo in (1, 0):
+            lib.plx_set_halo(halo)
+            xa = x.clone().requires_grad_()
+            y = conv(xa)
+            g = torch.ones_like(y) * 0.01 + torch.randn(y.shape, device=cuda, generator=torch.Generator(
+                device=cuda).manual_seed(3)).to(y.dtype)
+            y.backward(g)
+            out[halo] = (y.float(), xa.grad.float(), g)
+    finally:
+        lib.plx_set_halo(1)
+    xr = x.float().clone().requires_grad_()
+    yr = F.conv2d(xr, conv.weight.detach().to(torch.bfloat16).float(), padding=1)
+    yr.backward(out[1][2].float())
+    for halo in (1, 0):
+        torch.testing.assert_close(out[halo][0], yr, rtol=2e-2, atol=8e-2)
+        torch.testing.assert_close(out[halo][1], xr.grad, rtol=2e-2, atol=8e-2)
+    # same bf16 rounding points, different fp32 summation order: tight agreement between the two native paths
+    torch.testing.assert_close(out[1][0], out[0][0], rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-2, atol=2e-2)
