@@ -161,6 +161,20 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
     def me(user=Depends(auth)):
         return {k: v for k, v in user.items() if k != "token"}
 
+    # registered before the /api/v1/{username}/{project}/... routes: 'bookmarks/<user>/experiments' would match them
+    @app.get("/api/v1/bookmarks/{username}/experiments")
+    def user_bookmarks(username: str, user=Depends(auth)):
+        out = []
+        for b in store.bookmarks(username, "experiment"):
+            x = store.get_experiment(b["object_id"])
+            if x is not None:  # enough of the experiment to list and link it (the dashboard's bookmarks view)
+                proj = store.get("projects", x["project_id"]) or {}
+                b = dict(b, experiment={"id": x["id"], "status": x["status"], "project": proj.get("name"),
+                                        "user": proj.get("user") or x.get("user"), "declarations": x["declarations"],
+                                        "last_metric": x["last_metric"], "group_id": x["group_id"]})
+            out.append(b)
+        return {"results": out}
+
     def superuser(user=Depends(auth)):
         if not user.get("is_superuser"):
             raise HTTPException(403, "superuser only")
@@ -787,10 +801,6 @@ def create_app(flow, admin_token: Optional[str] = None, internal_token: Optional
     @app.get("/api/v1/notifications")
     def notifications(user=Depends(auth)):
         return {"results": store.notifications()}
-
-    @app.get("/api/v1/bookmarks/{username}/experiments")
-    def user_bookmarks(username: str, user=Depends(auth)):
-        return {"results": store.bookmarks(username, "experiment")}
 
     @app.get("/api/v1/searches/{username}/{project}/experiments")
     def searches(username: str, project: str, user=Depends(auth)):

@@ -323,3 +323,52 @@ def test_dashboard_views_and_their_api_contract(api):
     run = client.get(f"/api/v1/root/dash/pipelines/{pid}/runs/{d['runs'][0]['id']}").json()
     assert run["operations"][0]["name"] == "a"
     assert "results" in client.get("/api/v1/activitylogs", params={"limit": 30}).json()
+
+
+def test_dashboard_tables_filters_charts_contract(api):
+    """The reference client's tables / filters / autocomplete / chart builder (client/src/components/{tables,filters,
+    autocomplete,charts,metrics}): the page carries the query autocomplete, saved searches, server-side sort and
+    pagination, the column chooser, bookmarks, the chart builder with saved chart views and parallel coordinates,
+    and the API answers every call those make with the fields they read."""
+    client, flow = api
+    page = client.get("/ui").text
+    for marker in ("function autocomplete(", "QFIELDS", "savesearch", "pager", "colpick", "function parallel(",
+                   "chartviews", "smoothing", "log y", "#/bookmarks", "unbookmark", "offset="):
+        assert marker in page, marker
+    content = {"version": 1, "kind": "group",
+               "hptuning": {"concurrency": 3, "matrix": {"lr": {"values": [0.1, 0.2, 0.3]}},
+                            "grid_search": {"n_experiments": 3}}, "run": {"cmd": "echo {{ lr }}"}}
+    gid = client.post("/api/v1/root/tf/groups", json={"content": content}).json()["id"]
+    assert flow.wait("group", gid, timeout=30) == "succeeded"
+    xs = client.get("/api/v1/root/tf/experiments", params={"sort": "declarations.lr"}).json()["results"]
+    for k, x in enumerate(xs):
+        client.post(f"/api/v1/root/tf/experiments/{x['id']}/metrics", json=[{"values": {"loss": 3.0 - k}, "step": 1}])
+    # server-side sort on a metric + pagination (what the sort select and pager send)
+    r = client.get("/api/v1/root/tf/experiments", params={"sort": "-metric.loss", "limit": 2, "offset": 0}).json()
+    assert r["count"] == 3 and len(r["results"]) == 2
+    assert [x["last_metric"]["loss"] for x in r["results"]] == [3.0, 2.0]
+    r2 = client.get("/api/v1/root/tf/experiments", params={"sort": "-metric.loss", "limit": 2, "offset": 2}).json()
+    assert [x["last_metric"]["loss"] for x in r2["results"]] == [1.0]
+    # the autocomplete's field forms parse
+    for q in ("status:succeeded", "metric.loss:<2.5", "declarations.lr:0.2|0.3", "status:~failed, metric.loss:>=1", "created_at:2020-01-01..2100-01-01"):
+        assert client.get("/api/v1/root/tf/experiments", params={"query": q}).status_code == 200, q
+    # saved searches
+    assert client.post("/api/v1/searches/root/tf/experiments",
+                       json={"name": "good", "query": "metric.loss:<2.5", "sort": "metric.loss"}).status_code == 201
+    ss = client.get("/api/v1/searches/root/tf/experiments").json()["results"]
+    assert ss[0]["name"] == "good" and ss[0]["query"]["query"] == "metric.loss:<2.5"
+    # bookmarks, enriched with what the bookmarks view links to
+    x0 = xs[0]["id"]
+    assert client.post(f"/api/v1/root/tf/experiments/{x0}/bookmark").json()["bookmarked"]
+    me = client.get("/api/v1/users").json()["username"]
+    bm = client.get(f"/api/v1/bookmarks/{me}/experiments").json()["results"]
+    assert bm and bm[0]["object_id"] == x0 and bm[0]["experiment"]["project"] == "tf"
+    assert client.delete(f"/api/v1/root/tf/experiments/{x0}/unbookmark").json()["bookmarked"] is False
+    assert client.get(f"/api/v1/bookmarks/{me}/experiments").json()["results"] == []
+    # chart views (the chart builder's saved state)
+    view = {"name": "v", "charts": [{"metrics": ["loss"], "x": "time", "smoothing": 0.6, "logy": True}]}
+    assert client.post(f"/api/v1/root/tf/experiments/{x0}/chartviews", json=view).status_code == 201
+    cv = client.get(f"/api/v1/root/tf/experiments/{x0}/chartviews").json()["results"]
+    assert cv[0]["charts"][0]["smoothing"] == 0.6 and cv[0]["charts"][0]["logy"] is True
+    pts = client.get(f"/api/v1/root/tf/experiments/{x0}/metrics", params={"limit": 20000}).json()["results"]
+    assert "created_at" in pts[0]  # the wall-time x axis
