@@ -226,6 +226,15 @@ class ControlServer:
         ttt = (min(hit) - t0_wall) if hit else None
         best = min((x["last_metric"]["loss"] for x in xs if (x.get("last_metric") or {}).get("loss") is not None),
                    default=None)
+        # per sweep: its best metric and when that sweep first reached the target (the calibration of --target:
+        # a target near the task's floor is reached by a minority of sweeps, so the time to it spans several)
+        per_sweep = []
+        for g in gids:
+            gx = [x for x in xs if x["group_id"] == g and (x.get("last_metric") or {}).get("loss") is not None]
+            b = min((x["last_metric"]["loss"] for x in gx), default=None)
+            h = [x["finished_at"] for x in gx if x["last_metric"]["loss"] <= target]
+            per_sweep.append({"group": g, "best": round(b, 4) if b is not None else None,
+                              "hit_s": round(min(h) - t0_wall, 2) if h else None})
         # the status history every trial must show (reference ExperimentLifeCycle)
         want = ["created", "scheduled", "starting", "running", "succeeded"]
         sample = xs[:: max(1, len(xs) // 50)]
@@ -243,7 +252,7 @@ class ControlServer:
             execs.append({"wid": w["wid"], "devices": w["devices"], "pid": w["pid"],
                           "load_units": round(w["assigned_units"] - w0.get("assigned_units", 0.0), 3),
                           "units_of_work": w["assigned"] - w0.get("assigned", 0)})
-        return {"trials": trials, "succeeded": ok, "train_steps": steps, "ttt": ttt, "best": best,
+        return {"trials": trials, "succeeded": ok, "train_steps": steps, "ttt": ttt, "best": best, "per_sweep": per_sweep,
                 "fsm_ok": fsm_ok, "resumed": resumed, "brackets": units, "groups": len(gids), "executors": execs,
                 "control_pid": os.getpid()}
 
@@ -296,11 +305,31 @@ def spawn_ranks(n: int, args, argv) -> int:
     return rc
 
 
-def _pin_cpus(local_rank: int) -> list:
+def _physical_gpu(local_rank: int, world: int):
+    """KFD index of this rank's GPU, or None when it cannot be known before the GPU runtime starts.  The KFD topology
+    lists every GPU of the machine whatever this process may use: with HIP/ROCR_VISIBLE_DEVICES the rank's GPU is
+    that list's entry; without it the ranks own the node's GPUs in order only when they use all of them (the
+    driver's whole-node runs).  A 1-GPU lease on a shared machine is neither: pinning it to GPU 0's CPUs measured
+    20 % slower (remote NUMA node for the launch path), so it is left unpinned."""
+    from polyaxon_amd.obs.nodes import kfd_gpus
+
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+    if vis:
+        ids = [v for v in vis.split(",") if v.strip()]
+        return int(ids[local_rank]) if local_rank < len(ids) and ids[local_rank].strip().isdigit() else None
+    n = len(kfd_gpus())
+    return local_rank if n and n == world else None
+
+
+def _pin_cpus(local_rank: int, world: int) -> list:
     """Bind this rank to the CPUs local to its GPU (NUMA node of the PCIe root) before torch starts its threads."""
     from polyaxon_amd.polyflow.devices import device_cpus
 
-    cpus = device_cpus(local_rank)
+    mode = os.environ.get("PLX_BENCH_PIN", "1")  # A/B knob: 0 never, force = KFD index = local rank (round-3 default)
+    phys = local_rank if mode == "force" else _physical_gpu(local_rank, world)
+    if phys is None or mode == "0":
+        return []
+    cpus = device_cpus(phys)
     if cpus:
         try:
             os.sched_setaffinity(0, cpus)
@@ -322,7 +351,7 @@ def main() -> int:
     if world != args.gpus:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
-    pinned = [] if args.cpu else _pin_cpus(local)
+    pinned = [] if args.cpu else _pin_cpus(local, world)
     ctl_addr = os.environ.get("PLX_BENCH_CONTROL")
     ctl_proc = None
     if ctl_addr is None and rank == 0:  # torchrun / single GPU: the scheduler gets a process of its own
@@ -356,7 +385,7 @@ def main() -> int:
 
     # framework-owned collectives (csrc/rccl_comm.cpp) for the timing reduction on the GPU path
     comm = None
-    if dev.type == "cuda":
+    if dev.type == "cuda" and os.environ.get("PLX_BENCH_RCCL", "1") != "0":
         from polyaxon_amd.parallel.rccl import RcclComm
 
         comm = (RcclComm.from_torch_distributed() if world > 1
@@ -454,6 +483,8 @@ def main() -> int:
             "wall_clock_to_target_s": round(res["ttt"], 3) if res["ttt"] is not None else None,
             "target_loss": args.target,
             "best_loss": round(res["best"], 4) if res["best"] is not None else None,
+            "sweeps_reaching_target": sum(1 for p in res["per_sweep"] if p["hit_s"] is not None),
+            "sweep_best_loss": [p["best"] for p in res["per_sweep"]],
             "store_fsm_history_ok": res["fsm_ok"],
             "path": "polyflow scheduler (own process) + SQLite store + resident executors (same path as plx run)",
             "hip_graph": bool(worker._ready_info.get("hip_graph")),
