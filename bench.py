@@ -352,6 +352,12 @@ def main() -> int:
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
     pinned = [] if args.cpu else _pin_cpus(local, world)
+    # The result is ONE JSON line on stdout.  Native libraries print to fd 1 on their own (RCCL's version banner at
+    # communicator init), so fd 1 is pointed at stderr for the rest of the run and the JSON goes to a saved copy
+    # of the original stdout.
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ctl_addr = os.environ.get("PLX_BENCH_CONTROL")
     ctl_proc = None
     if ctl_addr is None and rank == 0:  # torchrun / single GPU: the scheduler gets a process of its own
@@ -494,7 +500,7 @@ def main() -> int:
             "control_pid": res["control_pid"],
             "cpus_pinned": len(pinned),
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result_out, flush=True)
     chan.close()
     if bench is not None:
         bench.close()

@@ -824,8 +824,10 @@ int launch_halo(const void* A, const void* B, void* C, int M, int N, int lda, in
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-// stride-1 3x3 convolutions on the same grid run in halo mode (A/B knob plx_set_halo: 0 off, 1 on)
-int g_halo = 1;
+// stride-1 3x3 convolutions on the same grid can run in halo mode (A/B knob plx_set_halo / PLX_HALO: 0 off, 1 on).
+// Off by default: measured 0.99-1.17x the gather mode's time on the ResNet-50 3x3 layers (the halo image costs
+// occupancy: 2 blocks/CU instead of 4), see profiles/r3_negative_results.md.
+int g_halo = 0;
 
 inline bool halo_ok(const ConvGeom& g) {
     if (!g_halo || g.ntaps != 9 || g.S != 1 || g.OS != 0 || g.Hr != g.H || g.Wr != g.W || g.C % BK) return false;

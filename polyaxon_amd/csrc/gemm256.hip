@@ -1,0 +1,461 @@
+// Large-tile bf16 GEMMs for the language-model linears on MI355X (gfx950).
+//
+//   C[M][N] = alpha * sum_k A(m, k) B(n, k)   (+ C when accumulating), C bf16 row-major (ldc)
+//
+// with each operand either K-MAJOR (X[r][k], k contiguous) or MN-MAJOR (X[k][r], r contiguous).  A transformer linear
+// y = x W^T (W stored [out][in], as nn.Linear) needs all three combinations (ops/gemm.py):
+//   forward  y[T][out]  = x[T][in] . W[out][in]^T    A K-major, B K-major   ("NT")
+//   dgrad    dx[T][in]  = dy[T][out] . W[out][in]    A K-major, B MN-major  ("NN")
+//   wgrad    dW[out][in] = dy[T][out]^T . x[T][in]   A MN-major, B MN-major ("TN"), K = tokens
+//
+// The kernel is the 256 x 256 x 64 tile of cdna_hip_programming.md §5 ("the 256^2 8-phase template"), written for
+// this repository:
+//   * 512 threads = 8 waves as 2 (M) x 4 (N); each wave owns a 128 x 64 block of C as 8 x 4 tiles of
+//     v_mfma_f32_16x16x32_bf16 (128 accumulator registers).  The MFMA A operand is B's rows (n), its B operand A's
+//     rows (m), so each lane's accumulator holds 4 consecutive n of one m: the epilogue stores 8 contiguous bytes.
+//   * LDS: 2 buffers x (A 256 x 64 + B 256 x 64) bf16 = 128 KiB, one block per CU.  A buffer is staged as four 16 KiB
+//     "quarters" by global_load_lds (buffer-resource LDS-DMA, 16 B per lane, lane-linear 1 KiB pieces, XOR swizzle
+//     applied to the per-lane SOURCE chunk and to the read: rule 21).  A-mi0 / A-mi1 hold rows 0-63 / 64-127 of each
+//     wave row's 128, B-ni0 / B-ni1 columns 0-31 / 32-63 of each wave column's 64.  A K-major quarter is 128 rows of
+//     128 B read with ds_read_b128; an MN-major quarter is 64 k-rows of 256 B read with ds_read_b64_tr_b16 (T10, the
+//     hardware transpose), two reads per fragment.
+//   * A K-tile runs as 4 phases, one C quadrant (4 x 2 MFMA tiles x K 64 = 16 MFMAs per wave) each, in the order
+//     (mi, ni) = (0,0) (0,1) (1,1) (1,0).  Phase p reads B-ni0, B-ni1, A-mi1, and in phase 3 the NEXT tile's A-mi0
+//     (B-ni0 stays in registers for phase 3), so every wave reads 8 / 4 / 4 / 8 KiB per phase instead of 12 / 4 / 8 / 0.
+//     Each phase: ds_read its fragments -> issue one quarter DMA -> counted vmcnt -> lgkmcnt(0) -> raw s_barrier ->
+//     16 MFMAs at s_setprio 1 -> raw s_barrier.
+//   * DMA ring: a slot is restaged one phase after its last read, for the tile two ahead, so six quarters (12 DMAs)
+//     stay in flight and vmcnt never drains in the loop (see `ring` below for the sequence numbering).  A quarter
+//     is rewritten only after the barrier that follows the lgkmcnt retiring its last read (WAR) and read only one
+//     phase after the wait that retired it (RAW).  Never __syncthreads() here: its fence would drain vmcnt.
+//   * Ping-pong (T5): the waves of row 1 run one barrier behind row 0, so on every SIMD one wave's MFMAs overlap
+//     the other wave's LDS reads (measured +5-10 % on the K-major shapes over the lock-step schedule).
+//   * blockIdx is remapped so consecutive tiles share an XCD (T1), and blockIdx.y splits K when the tile grid alone
+//     cannot fill the 256 CUs (weight gradients of narrow layers: out x in tiles, K = tokens): the splits write fp32
+//     slabs that gemm256_reduce sums (and adds to C).
+// Requirements (host-checked): M, N multiples of 256, K of 64, 16-B aligned rows, offsets below 2 GiB per tile origin.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PLX_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int BM = 256, BN = 256, BK = 64, NTH = 512;
+constexpr int QUARTER = 16384;             // 128 rows x 128 B (K-major) or 64 k-rows x 256 B (MN-major)
+constexpr int BUF = 4 * QUARTER;           // one K-tile: [A-mi0 | A-mi1 | B-ni0 | B-ni1]
+constexpr int LDS_BYTES = 2 * BUF;
+
+// K-major quarter rows (128 B): physical 16-B chunk = logical ^ kswz(row) (conflict-free ds_read_b128)
+__device__ __forceinline__ int kswz(int row) { return (row >> 1) & 7; }
+// MN-major quarter k-rows (256 B): physical chunk = logical ^ tswz(row): the 8 k-rows one 32-lane half of a
+// ds_read_b64_tr_b16 touches land on 8 disjoint 32-B bank windows
+__device__ __forceinline__ int tswz(int row) { return 2 * ((row & 3) | (((row >> 3) & 1) << 2)); }
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7ffffff0, 0x00020000);
+}
+
+__device__ __forceinline__ void glds(__amdgpu_buffer_rsrc_t r, uint32_t off, void* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)l, 16, off, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
+}
+
+// tile row/column of quarter position c (0..127) of quarter `sub`: A quarters split each wave row's 128 rows into
+// 64 + 64, B quarters each wave column's 64 columns into 32 + 32
+template <bool IS_A>
+__device__ __forceinline__ int tile_idx(int sub, int c) {
+  return IS_A ? (c >> 6) * 128 + sub * 64 + (c & 63) : (c >> 5) * 64 + sub * 32 + (c & 31);
+}
+
+// byte offset (relative to the operand's tile origin at the block's first k) that this lane's DMA of piece `piece`
+// of quarter `sub` fetches at K-tile 0; K-tile kt adds kt * (K-tile stride)
+template <bool IS_A, bool KMAJ>
+__device__ __forceinline__ uint32_t src_off(int sub, int piece, int lane, int ld) {
+  if (KMAJ) {
+    const int row = piece * 8 + (lane >> 3);
+    const int chunk = (lane & 7) ^ kswz(row);
+    return (uint32_t)((tile_idx<IS_A>(sub, row) * ld + chunk * 8) * 2);
+  } else {
+    const int kr = piece * 4 + (lane >> 4);
+    const int chunk = (lane & 15) ^ tswz(kr);
+    return (uint32_t)((kr * ld + tile_idx<IS_A>(sub, chunk * 8)) * 2);
+  }
+}
+
+// Fragment addresses.  An MFMA fragment holds row r = c0 + (lane & 15) of a quarter image (c0 = 16-aligned quarter
+// position), k = 32 s + 8 (lane >> 4) + j.  The per-lane byte offset is computed once; the rest of the address is a
+// compile-time constant, so every ds_read in the loop is "base VGPR + immediate" (computing the XOR-swizzled
+// address per read made the compiler hoist ~50 loop-invariant addresses into VGPRs and spill).
+//   K-major: kswz(c0 + fr) = kswz(fr), so the offset depends on (lane, s) only; tile t adds t * 16 rows * 128 B.
+//   MN-major: tswz(kr) is unchanged by kr + 32 s and kr + 4, so (lane, t) fixes the offset; step s adds 32 k-rows
+//   (8192 B) and the second half of the fragment 4 k-rows (1024 B).
+template <bool KMAJ>
+__device__ __forceinline__ int frag_off(int c0, int ts, int lane) {
+  const int fr = lane & 15, fq = lane >> 4;
+  if (KMAJ) {  // ts = s
+    return (c0 + fr) * 128 + (((ts * 4 + fq) ^ kswz(fr)) << 4);
+  } else {     // ts = t; T10: lane 4q+p of a 16-lane group addresses k-row q, columns c + 4p .. 4p+3
+    const int col = c0 + ts * 16 + 4 * (lane & 3);
+    const int kr = 8 * fq + (fr >> 2);
+    return kr * 256 + (((col >> 3) ^ tswz(kr)) << 4) + ((col >> 2) & 1) * 8;
+  }
+}
+
+__device__ __forceinline__ bf16x8 ld_frag_k(const char* p) { return *(const bf16x8*)p; }
+
+__device__ __forceinline__ bf16x8 ld_frag_t(const char* p) {
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p + 1024));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+struct FragA {
+  bf16x8 v[4][2];
+};
+struct FragB {
+  bf16x8 v[2][2];
+};
+
+template <int V>
+struct IC {
+  static constexpr int value = V;
+};
+
+struct Gemm256Args {
+  const __bf16* A;
+  const __bf16* B;
+  void* C;            // bf16 [M][ldc], or fp32 slabs [splits][M][N] when K is split
+  int M, N, K, lda, ldb, ldc;
+  int kt_per_split;   // K-tiles per blockIdx.y
+  float alpha;
+};
+
+// ACC: C += alpha * AB (bf16 read-modify-write); SLAB: write fp32 partials (split K)
+template <bool AK, bool BKM, bool ACC, bool SLAB>
+__global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int ntn = p.N / BN, ntm = p.M / BM;
+  const int id = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = id / ntn, tn = id % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kt0 = blockIdx.y * p.kt_per_split;
+  const int nk = min(p.kt_per_split, p.K / BK - kt0);
+  const size_t k0 = (size_t)kt0 * BK;
+
+  // buffer resources anchored at this block's tile origin (offsets stay 32-bit for any matrix size)
+  const __bf16* abase = AK ? p.A + (size_t)m0 * p.lda + k0 : p.A + k0 * p.lda + m0;
+  const __bf16* bbase = BKM ? p.B + (size_t)n0 * p.ldb + k0 : p.B + k0 * p.ldb + n0;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(abase), rb = rsrc(bbase);
+  const uint32_t astep = AK ? BK * 2 : (uint32_t)(BK * p.lda * 2);
+  const uint32_t bstep = BKM ? BK * 2 : (uint32_t)(BK * p.ldb * 2);
+
+  // per-lane source offsets of the two pieces (wave, wave + 8) of each quarter, in issue order:
+  // 0 = A-mi0, 1 = B-ni0, 2 = B-ni1, 3 = A-mi1
+  uint32_t src[4][2];
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) {
+    src[0][pc] = src_off<true, AK>(0, wave + 8 * pc, lane, p.lda);
+    src[1][pc] = src_off<false, BKM>(0, wave + 8 * pc, lane, p.ldb);
+    src[2][pc] = src_off<false, BKM>(1, wave + 8 * pc, lane, p.ldb);
+    src[3][pc] = src_off<true, AK>(1, wave + 8 * pc, lane, p.lda);
+  }
+  auto issue = [&](int buf, int kt, int q) {
+    // LDS placement: A-mi0 at 0, A-mi1 at QUARTER, B-ni0 at 2 QUARTER, B-ni1 at 3 QUARTER
+    const int qoff = q == 0 ? 0 : q == 3 ? QUARTER : q == 1 ? 2 * QUARTER : 3 * QUARTER;
+    char* dst = smem + buf * BUF + qoff;
+    const bool isa = q == 0 || q == 3;
+    const uint32_t koff = (uint32_t)kt * (isa ? astep : bstep);
+    const __amdgpu_buffer_rsrc_t r = isa ? ra : rb;
+    glds(r, src[q][0] + koff, dst + wave * 1024);
+    glds(r, src[q][1] + koff, dst + (wave + 8) * 1024);
+  };
+
+  f32x4 acc[4][8];  // [n tile: 4 x 16 = the wave's 64 columns][m tile: 8 x 16 = its 128 rows]
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane fragment offsets inside a quarter image (K-major: [s]; MN-major: [t])
+  int aoff[4], boff[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) aoff[i] = frag_off<AK>(wm * 64, AK ? (i & 1) : i, lane);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) boff[i] = frag_off<BKM>(wn * 32, i, lane);
+  // Fragments are returned by value and live only inside one K-tile (declaring them outside the loop made them
+  // loop-carried: phis over the issue / no-issue paths kept dead copies alive and the kernel spilled).
+  // img = smem + compile-time constant, so each read is base VGPR + immediate offset.
+  auto read_a = [&](const char* img) {  // MFMA B operand = A rows (m): [m tile of the quadrant][k step]
+    FragA f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        f.v[t][s] = AK ? ld_frag_k(img + aoff[s] + t * 2048) : ld_frag_t(img + aoff[t] + s * 8192);
+    return f;
+  };
+  auto read_b = [&](const char* img) {  // MFMA A operand = B rows (n): [n tile of the quadrant][k step]
+    FragB f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        f.v[t][s] = BKM ? ld_frag_k(img + boff[s] + t * 2048) : ld_frag_t(img + boff[t] + s * 8192);
+    return f;
+  };
+  // One phase's synchronisation + MFMAs.  This wave's ds_reads retire (lgkmcnt(0)) BEFORE the first barrier, so
+  // a slot read in phase p may be restaged by any wave from phase p + 1 on (WAR), and a DMA retired by the issuing
+  // waves' vmcnt before phase p's first barrier may be read from phase p + 1 on (RAW).
+  auto mfma_phase = [&](const FragA& fa, const FragB& fb, int mi, int ni) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          acc[ni * 2 + a][mi * 4 + b] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb.v[a][s], fa.v[b][s], acc[ni * 2 + a][mi * 4 + b], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  };
+  // DMA ring.  Quarters are numbered in issue order, seq = 4 u + o for K-tile u and o = 0 A-mi0, 1 B-ni0, 2 B-ni1,
+  // 3 A-mi1; there are S = 4 nk of them.  Tile t reads B-ni0 in phase 0, B-ni1 in phase 1, A-mi1 in phase 2 and
+  // the NEXT tile's A-mi0 in phase 3 (its own A-mi0 came in the previous tile's phase 3), 8 / 4 / 4 / 8 KiB-reads
+  // per wave.  Each slot of buffer t & 1 is free one phase after its last read, so global phase g = 4 t + p
+  // restages quarter o = p of tile t + 2, seq g + 8 (the prologue issues 0..7), and every phase retires up to
+  // seq g + 2, the quarter first read in phase g + 1: six quarters = 12 DMAs stay in flight in the steady state.
+  const int S = 4 * nk;
+  auto wait_vm = [&](int n) {  // n = DMAs allowed in flight (even), wave-uniform
+    if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (n >= 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // issue seq g + 8 (tile kt + 2, kind P, into this tile's buffer CB) and wait for seq g + 2
+  auto ring = [&](auto cb, auto ph, int kt) {
+    constexpr int CB = decltype(cb)::value, P = decltype(ph)::value;
+    const int g = 4 * kt + P;
+    if (g + 8 < S) {
+      issue(CB, kt + 2, P);
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else {
+      wait_vm(2 * ((S - 1) - (g + 2)));
+    }
+  };
+  auto tile = [&](auto cb, int kt, FragA& a0) {
+    constexpr int CB = decltype(cb)::value;
+    const char* qa1 = smem + CB * BUF + QUARTER;
+    const char* qb0 = smem + CB * BUF + 2 * QUARTER;
+    const char* qb1 = smem + CB * BUF + 3 * QUARTER;
+    const char* qa0_next = smem + (1 - CB) * BUF;
+    // phase 0: quadrant (0,0); reads B-ni0
+    const FragB b0 = read_b(qb0);
+    ring(cb, IC<0>{}, kt);
+    mfma_phase(a0, b0, 0, 0);
+    // phase 1: quadrant (0,1); reads B-ni1
+    const FragB b1 = read_b(qb1);
+    ring(cb, IC<1>{}, kt);
+    mfma_phase(a0, b1, 0, 1);
+    // phase 2: quadrant (1,1); reads A-mi1
+    const FragA a1 = read_a(qa1);
+    ring(cb, IC<2>{}, kt);
+    mfma_phase(a1, b1, 1, 1);
+    // phase 3: quadrant (1,0) from registers; reads the next tile's A-mi0
+    if (kt + 1 < nk) a0 = read_a(qa0_next);
+    ring(cb, IC<3>{}, kt);
+    mfma_phase(a1, b0, 1, 0);
+  };
+
+  // prologue: seq 0 .. min(7, S - 1) (tiles 0 and 1); retire seq 0, 1 and read tile 0's A-mi0
+#pragma unroll
+  for (int q = 0; q < 4; ++q) issue(0, 0, q);
+  if (nk > 1) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) issue(1, 1, q);
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  FragA a0 = read_a(smem);
+  // Ping-pong (T5): the waves of row wm = 1 (one per SIMD) run one barrier behind those of row 0, so on every SIMD
+  // one wave's MFMAs (priority 1) overlap the other wave's ds_reads and DMA issue.
+  if (wm == 1) __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < nk; kt += 2) {
+    tile(IC<0>{}, kt, a0);
+    if (kt + 1 < nk) tile(IC<1>{}, kt + 1, a0);
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // every wave executes the same number of barriers
+
+  // epilogue: acc[nt][mt] is a 16 x 16 tile D[n][m]: m = lane & 15, n = 4 (lane >> 4) + j, j = 0..3
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int m = m0 + wm * 128 + mt * 16 + fr;
+      const int n = n0 + wn * 64 + nt * 16 + 4 * fq;
+      f32x4 v = acc[nt][mt];
+      if (SLAB) {
+        float* dst = (float*)p.C + ((size_t)blockIdx.y * p.M + m) * p.N + n;
+        *(f32x4*)dst = v;
+      } else {
+        __bf16* dst = (__bf16*)p.C + (size_t)m * p.ldc + n;
+        if (ACC) {
+          const uint2 o = *(const uint2*)dst;
+          v[0] = p.alpha * v[0] + __uint_as_float(o.x << 16);
+          v[1] = p.alpha * v[1] + __uint_as_float(o.x & 0xffff0000u);
+          v[2] = p.alpha * v[2] + __uint_as_float(o.y << 16);
+          v[3] = p.alpha * v[3] + __uint_as_float(o.y & 0xffff0000u);
+        } else {
+          v *= p.alpha;
+        }
+        uint2 packed;
+        packed.x = pack_bf16x2(v[0], v[1]);
+        packed.y = pack_bf16x2(v[2], v[3]);
+        *(uint2*)dst = packed;
+      }
+    }
+}
+
+// C (bf16, ldc) = alpha * sum over splits of the fp32 slabs (+ C when accumulating); 8 elements per thread
+template <bool ACC>
+__global__ void __launch_bounds__(256) gemm256_reduce(const float* __restrict__ ws, __bf16* __restrict__ C, int M,
+                                                      int N, int ldc, int splits, float alpha) {
+  const size_t i8 = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i8 >= (size_t)M * N / 8) return;
+  const size_t e = i8 * 8;
+  const int m = (int)(e / N), n = (int)(e % N);
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  const size_t slab = (size_t)M * N;
+  for (int k = 0; k < splits; ++k) {
+    const f32x4* src = (const f32x4*)(ws + k * slab + e);
+    s0 += src[0];
+    s1 += src[1];
+  }
+  s0 *= alpha;
+  s1 *= alpha;
+  __bf16* dst = C + (size_t)m * ldc + n;
+  if (ACC) {
+    const uint4 o = *(const uint4*)dst;
+    s0[0] += __uint_as_float(o.x << 16);
+    s0[1] += __uint_as_float(o.x & 0xffff0000u);
+    s0[2] += __uint_as_float(o.y << 16);
+    s0[3] += __uint_as_float(o.y & 0xffff0000u);
+    s1[0] += __uint_as_float(o.z << 16);
+    s1[1] += __uint_as_float(o.z & 0xffff0000u);
+    s1[2] += __uint_as_float(o.w << 16);
+    s1[3] += __uint_as_float(o.w & 0xffff0000u);
+  }
+  uint4 packed;
+  packed.x = pack_bf16x2(s0[0], s0[1]);
+  packed.y = pack_bf16x2(s0[2], s0[3]);
+  packed.z = pack_bf16x2(s1[0], s1[1]);
+  packed.w = pack_bf16x2(s1[2], s1[3]);
+  *(uint4*)dst = packed;
+}
+
+template <bool AK, bool BKM, bool ACC, bool SLAB>
+int launch(const Gemm256Args& a, int splits, hipStream_t st) {
+  auto k = gemm256_kernel<AK, BKM, ACC, SLAB>;
+  static const int attr =
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess ? 0 : -4;
+  if (attr) return attr;
+  hipLaunchKernelGGL(k, dim3((a.M / BM) * (a.N / BN), splits), dim3(NTH), LDS_BYTES, st, a);
+  return 0;
+}
+
+template <bool AK, bool BKM>
+int dispatch(const Gemm256Args& a, int splits, int accumulate, hipStream_t st) {
+  if (splits > 1) return launch<AK, BKM, false, true>(a, splits, st);
+  return accumulate ? launch<AK, BKM, true, false>(a, 1, st) : launch<AK, BKM, false, false>(a, 1, st);
+}
+
+int g_split_target = 256;  // blocks the split-K planner aims for (one per CU: splitting a grid that already
+                           // fills the chip measured slower); plx_gemm256_set_split_target
+
+// K-tiles per split so that tiles x splits reaches ~g_split_target blocks while every split keeps >= 8 K-tiles
+int plan_kt_per_split(int M, int N, int K) {
+  const int tiles = (M / BM) * (N / BN), nk = K / BK;
+  int splits = 1;
+  while (tiles * splits * 2 <= g_split_target && nk / (splits * 2) >= 8) splits *= 2;
+  return (nk + splits - 1) / splits;
+}
+
+}  // namespace
+
+// Split-K plan: number of K splits (blockIdx.y) the kernel uses for this shape (1 = no workspace needed);
+// the fp32 workspace must hold splits * M * N floats
+PLX_API int plx_gemm256_splits(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return 0;
+  const int kps = plan_kt_per_split(M, N, K);
+  return (K / BK + kps - 1) / kps;
+}
+
+// A/B knob: blocks the split-K planner aims for (0 disables splitting)
+PLX_API void plx_gemm256_set_split_target(int blocks) { g_split_target = blocks; }
+
+// C[M][N] (bf16, ldc) = alpha * A . B (+ C when accumulate), layouts per a_kmajor / b_kmajor (see the file header).
+// ws: fp32 workspace of plx_gemm256_splits(M, N, K) * M * N floats when that is > 1 (may be null otherwise).
+// Returns 0, or < 0 on a shape / layout the kernel does not take (nothing launched).
+PLX_API int plx_gemm256(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb, int ldc,
+                        int a_kmajor, int b_kmajor, float alpha, int accumulate, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return -1;
+  if (lda % 8 || ldb % 8 || ldc % 8 || (uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return -1;
+  // largest relative byte offset a block's buffer resource sees
+  const long long aspan = a_kmajor ? (long long)BM * lda * 2 : (long long)K * lda * 2;
+  const long long bspan = b_kmajor ? (long long)BN * ldb * 2 : (long long)K * ldb * 2;
+  if (aspan >= 0x7ffffff0LL || bspan >= 0x7ffffff0LL) return -2;
+  const int kps = plan_kt_per_split(M, N, K);
+  const int splits = (K / BK + kps - 1) / kps;
+  if (splits > 1 && !ws) return -5;
+  Gemm256Args a{(const __bf16*)A, (const __bf16*)B, splits > 1 ? ws : C, M, N, K, lda, ldb, ldc, kps, alpha};
+  hipStream_t st = (hipStream_t)stream;
+  int rc;
+  if (a_kmajor && b_kmajor) rc = dispatch<true, true>(a, splits, accumulate, st);
+  else if (a_kmajor) rc = dispatch<true, false>(a, splits, accumulate, st);
+  else if (b_kmajor) rc = dispatch<false, true>(a, splits, accumulate, st);
+  else rc = dispatch<false, false>(a, splits, accumulate, st);
+  if (rc) return rc;
+  if (splits > 1) {
+    const size_t total8 = (size_t)M * N / 8;
+    const dim3 grid((unsigned)((total8 + 255) / 256));
+    if (accumulate)
+      hipLaunchKernelGGL(gemm256_reduce<true>, grid, dim3(256), 0, st, (const float*)ws, (__bf16*)C, M, N, ldc, splits,
+                         alpha);
+    else
+      hipLaunchKernelGGL(gemm256_reduce<false>, grid, dim3(256), 0, st, (const float*)ws, (__bf16*)C, M, N, ldc,
+                         splits, alpha);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// the kernel's tile edge: M and N must be multiples of it, K of 64
+PLX_API int plx_gemm256_tile() { return BM; }

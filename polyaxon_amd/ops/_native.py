@@ -34,6 +34,7 @@ LIBRARIES: Dict[str, dict] = {
     "plx_conv": {"sources": ["conv_gemm.hip"], "kind": "hip", "link": []},
     "plx_pool": {"sources": ["pool_kernels.hip"], "kind": "hip", "link": []},
     "plx_lm": {"sources": ["lm_kernels.hip"], "kind": "hip", "link": []},
+    "plx_gemm": {"sources": ["gemm256.hip"], "kind": "hip", "link": []},
     "plx_attn": {"sources": ["attn_kernels.hip"], "kind": "hip", "link": []},
     "plx_rccl": {"sources": ["rccl_comm.cpp"], "kind": "hip_host", "link": ["-lrccl"]},
 }
@@ -156,6 +157,8 @@ def lib(name: str) -> ctypes.CDLL:
             handle.plx_set_nt_single_stage(int(os.environ["PLX_NT_SINGLE_STAGE"]))
         if name == "plx_conv" and os.environ.get("PLX_HALO"):  # A/B knob: halo mode of the 3x3 convolutions
             handle.plx_set_halo(int(os.environ["PLX_HALO"]))
+        if name == "plx_gemm" and os.environ.get("PLX_GEMM_SPLIT_TARGET"):  # A/B knob: split-K planner target
+            handle.plx_gemm256_set_split_target(int(os.environ["PLX_GEMM_SPLIT_TARGET"]))
         if name == "plx_conv" and os.environ.get("PLX_TN_PLAN"):  # A/B knob: "blocks_per_cu,slab_mb"
             bpc, mb = (int(v) for v in os.environ["PLX_TN_PLAN"].split(","))
             handle.plx_set_tn_plan(bpc, mb)
@@ -255,6 +258,12 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_swiglu_fwd": [_P, _P, _L, _I, _P],
         "plx_swiglu_bwd": [_P, _P, _P, _L, _I, _P],
     },
+    "plx_gemm": {
+        "plx_gemm256": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
+        "plx_gemm256_splits": [_I, _I, _I],
+        "plx_gemm256_set_split_target": [_I],
+        "plx_gemm256_tile": [],
+    },
     "plx_attn": {
         "plx_attn_fwd": [_P, _I, _P],
         "plx_attn_bwd": [_P, _I, _P, _P],
@@ -290,7 +299,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_gemm256_set_split_target": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

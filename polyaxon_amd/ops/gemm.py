@@ -1,0 +1,102 @@
+"""bf16 GEMMs of the transformer linears on the hand-written 256x256 MFMA kernel (csrc/gemm256.hip).
+
+``linear(x, W, b)`` is y = x W^T + b with all three GEMMs of its training step on that kernel:
+
+* forward  y[T][out]   = x[T][in] . W[out][in]^T  (both operands K-major),
+* dgrad    dx[T][in]   = dy[T][out] . W[out][in]  (W read MN-major through the LDS transpose read),
+* wgrad    dW[out][in] = dy^T . x, K = tokens     (both MN-major; split-K over fp32 slabs when the out x in tile grid
+  alone cannot fill the 256 CUs).
+
+The weight gradient can be written straight into a flat gradient slot (``out=``, ``accumulate=``): the kernel's
+epilogue adds to the bf16 slot in place, so a weight used twice needs no separate gradient tensor.
+
+Shapes the kernel does not take (a dimension not a multiple of 256, or K of 64) go to ``torch`` (hipBLASLt) —
+:func:`supported` says which; on a GPU box a missing library raises instead of falling back (ops/_native.py).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from polyaxon_amd.ops import _native
+
+TILE = 256
+_ws: Dict[Tuple[str, int], torch.Tensor] = {}
+
+
+def enabled() -> bool:
+    """PLX_LM_GEMM=0 routes the LM linears back to hipBLASLt (A/B knob)."""
+    return os.environ.get("PLX_LM_GEMM", "1") != "0"
+
+
+def supported(M: int, N: int, K: int) -> bool:
+    return M > 0 and N > 0 and K > 0 and M % TILE == 0 and N % TILE == 0 and K % 64 == 0
+
+
+def _workspace(device: torch.device, floats: int) -> torch.Tensor:
+    key = (device.type, device.index or 0)
+    w = _ws.get(key)
+    if w is None or w.numel() < floats:
+        w = _ws[key] = torch.empty(max(floats, 1 << 20), dtype=torch.float32, device=device)
+    return w
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool,
+         out: Optional[torch.Tensor] = None, accumulate: bool = False, alpha: float = 1.0) -> torch.Tensor:
+    """out[M][N] (bf16, row-major, may be a strided view with unit column stride) = alpha * A . B (+ out).
+
+    ``a`` is A[M][K] when ``a_kmajor`` else A stored [K][M]; ``b`` is B[N][K] when ``b_kmajor`` else [K][N].
+    Both are contiguous bf16 (leading dimension = their row length)."""
+    if not supported(M, N, K):
+        raise ValueError(f"gemm256 needs M, N % 256 == 0 and K % 64 == 0 (got {M}x{N}x{K})")
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not (a.is_contiguous() and b.is_contiguous()):
+        raise ValueError("gemm256 takes contiguous bf16 operands")
+    if a.numel() != M * K or b.numel() != N * K:
+        raise ValueError(f"operand sizes {a.numel()}, {b.numel()} do not match {M}x{N}x{K}")
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs out")
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    if out.dtype != torch.bfloat16 or out.dim() != 2 or out.shape != (M, N) or out.stride(1) != 1:
+        raise ValueError("out must be a [M][N] bf16 matrix with unit column stride")
+    lib = _native.lib("plx_gemm")
+    splits = _native.size("plx_gemm", "plx_gemm256_splits", M, N, K)
+    ws = _workspace(a.device, splits * M * N).data_ptr() if splits > 1 else None
+    lda = K if a_kmajor else M
+    ldb = K if b_kmajor else N
+    rc = lib.plx_gemm256(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, M, N, K, lda, ldb, out.stride(0),
+                         int(a_kmajor), int(b_kmajor), float(alpha), int(accumulate), _native.current_stream())
+    if rc != 0:
+        raise RuntimeError(f"plx_gemm256 failed ({rc}) for {M}x{N}x{K} a_kmajor={a_kmajor} b_kmajor={b_kmajor}")
+    return out
+
+
+def linear_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and enabled()):
+        return False
+    T = x.numel() // x.shape[-1]
+    return supported(T, weight.shape[0], weight.shape[1]) and supported(T, weight.shape[1], weight.shape[0])
+
+
+def forward(x2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """y[T][out] = x[T][in] . W[out][in]^T"""
+    T, fin = x2.shape
+    return gemm(x2, weight, T, weight.shape[0], fin, True, True)
+
+
+def dgrad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """dx[T][in] = dy[T][out] . W[out][in]"""
+    T, fout = dy2.shape
+    return gemm(dy2, weight, T, weight.shape[1], fout, True, False)
+
+
+def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] = None,
+          accumulate: bool = False) -> torch.Tensor:
+    """dW[out][in] (+)= dy[T][out]^T . x[T][in]"""
+    T, fout = dy2.shape
+    fin = x2.shape[1]
+    if out is not None:
+        out = out.view(fout, fin)
+    return gemm(dy2, x2, fout, fin, T, False, False, out=out, accumulate=accumulate)

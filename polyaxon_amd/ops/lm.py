@@ -156,13 +156,59 @@ class _LinearDirect(torch.autograd.Function):
         return dx, None, db, None, None
 
 
+class _LinearMfma(torch.autograd.Function):
+    """y = x W^T (+ b) with forward, data-gradient and weight-gradient GEMMs on the hand-written 256x256 MFMA kernel
+    (ops/gemm.py, csrc/gemm256.hip).  ``slot``/``flat`` as in :class:`_LinearDirect`: when given, dW is written
+    (or, for a weight already written this step, accumulated by the kernel's epilogue) straight into the flat
+    gradient slot."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, slot, flat):
+        from polyaxon_amd.ops import gemm
+
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        ctx.save_for_backward(x2, weight)
+        ctx.slot, ctx.flat, ctx.has_bias, ctx.xshape = slot, flat, bias is not None, x.shape
+        y = gemm.forward(x2, weight)
+        if bias is not None:
+            y.add_(bias)
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        from polyaxon_amd.ops import gemm
+
+        x2, weight = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dx = gemm.dgrad(dy2, weight).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.slot is not None:
+            g = ctx.slot
+            gemm.wgrad(dy2, x2, out=g, accumulate=bool(ctx.flat.mark_written(g)))
+            cb = getattr(weight, "_plx_ready_cb", None)
+            if cb is not None:
+                cb(weight)
+        elif ctx.needs_input_grad[1]:
+            dw = gemm.wgrad(dy2, x2)
+        db = dy2.sum(0) if ctx.has_bias else None
+        return dx, dw, db, None, None
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """F.linear, or the direct-gradient form when ``weight`` is a flat parameter whose grad slot has the
-    compute dtype (FlatParams lp mode with direct grads enabled)."""
+    """F.linear on the MFMA GEMM kernel when the shapes fit it (ops/gemm.py: tokens, in and out multiples of 256,
+    bf16, PLX_LM_GEMM != 0), with the weight gradient written into the flat gradient slot when ``weight`` is a flat
+    parameter in lp mode with direct grads; hipBLASLt (F.linear / the direct-gradient form) otherwise."""
     slot = getattr(weight, "grad", None)
     flat = getattr(weight, "_plx_flat", None)
-    if (flat is not None and getattr(weight, "_plx_direct_grad", False) and slot is not None and weight.requires_grad
-            and torch.is_grad_enabled() and slot.dtype == weight.dtype and x.dtype == weight.dtype
-            and slot.is_contiguous()):
+    direct = (flat is not None and getattr(weight, "_plx_direct_grad", False) and slot is not None
+              and weight.requires_grad and torch.is_grad_enabled() and slot.dtype == weight.dtype
+              and x.dtype == weight.dtype and slot.is_contiguous())
+    from polyaxon_amd.ops import gemm
+
+    if weight.is_contiguous() and gemm.linear_supported(x, weight):
+        if direct:
+            return _LinearMfma.apply(x, weight, bias, slot, flat)
+        return _LinearMfma.apply(x, weight, bias, None, None)
+    if direct:
         return _LinearDirect.apply(x, weight, bias, slot, flat)
     return F.linear(x, weight, bias)

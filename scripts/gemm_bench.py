@@ -1,0 +1,77 @@
+"""Time the 256x256 MFMA GEMM (csrc/gemm256.hip) against torch (hipBLASLt) on the LM linears' shapes.
+
+    python scripts/gemm_bench.py [--models gpt2,llama] [--reps 20]
+
+One JSON line per (model, linear, pass): ms and TFLOP/s of both, and the max |diff| relative to the output scale.
+Passes: fwd (x . W^T), dgrad (dy . W), wgrad (dy^T . x, K = tokens).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from polyaxon_amd.ops import gemm  # noqa: E402
+
+# (model, tokens, [(linear, in, out)])
+MODELS = {
+    "gpt2": (16 * 1024, [("qkv", 768, 2304), ("proj", 768, 768), ("up", 768, 3072), ("down", 3072, 768)]),
+    "llama": (4096, [("qkv", 4096, 6144), ("proj", 4096, 4096), ("up", 4096, 28672), ("down", 14336, 4096)]),
+}
+
+
+def timed(fn, reps):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--models", default="gpt2,llama")
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    tot = {"native": 0.0, "torch": 0.0}
+    for model in args.models.split(","):
+        T, linears = MODELS[model]
+        for name, fin, fout in linears:
+            x = torch.randn(T, fin, device=dev).to(torch.bfloat16)
+            w = (torch.randn(fout, fin, device=dev) * 0.02).to(torch.bfloat16)
+            dy = torch.randn(T, fout, device=dev).to(torch.bfloat16)
+            cases = [
+                ("fwd", T, fout, fin, lambda: gemm.forward(x, w), lambda: x @ w.t()),
+                ("dgrad", T, fin, fout, lambda: gemm.dgrad(dy, w), lambda: dy @ w),
+                ("wgrad", fout, fin, T, lambda: gemm.wgrad(dy, x), lambda: dy.t() @ x),
+            ]
+            for pas, M, N, K, nat, ref in cases:
+                a, b = nat(), ref()
+                err = ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6)).item()
+                tn, tt = timed(nat, args.reps), timed(ref, args.reps)
+                tot["native"] += tn
+                tot["torch"] += tt
+                fl = 2.0 * M * N * K
+                print(json.dumps({"model": model, "linear": name, "pass": pas, "M": M, "N": N, "K": K,
+                                  "splits": gemm._native.size("plx_gemm", "plx_gemm256_splits", M, N, K),
+                                  "native_ms": round(tn, 4), "torch_ms": round(tt, 4),
+                                  "native_tflops": round(fl / tn / 1e9, 1), "torch_tflops": round(fl / tt / 1e9, 1),
+                                  "speedup": round(tt / tn, 3), "rel_err": round(err, 5)}), flush=True)
+            del x, w, dy
+    print(json.dumps({"total_native_ms": round(tot["native"], 3), "total_torch_ms": round(tot["torch"], 3)}))
+
+
+if __name__ == "__main__":
+    main()

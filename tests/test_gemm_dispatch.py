@@ -1,0 +1,50 @@
+"""Host-side contract of the LM GEMM path (ops/gemm.py, ops/lm.py): shape gating, fallbacks, argument checks.
+The kernel's numerics are in tests/test_gpu_gemm.py."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from polyaxon_amd.ops import gemm, lm
+
+
+def test_supported_shapes():
+    assert gemm.supported(4096, 6144, 4096)
+    assert gemm.supported(256, 256, 64)
+    assert not gemm.supported(4096, 50257, 768)  # GPT-2 vocab: not a multiple of 256
+    assert not gemm.supported(4096, 768, 96)     # K not a multiple of 64
+    assert not gemm.supported(0, 256, 64)
+
+
+def test_linear_supported_needs_cuda_bf16_and_tiles():
+    x = torch.zeros(2, 128, 768, dtype=torch.bfloat16)
+    w = torch.zeros(2304, 768, dtype=torch.bfloat16)
+    assert not gemm.linear_supported(x, w)  # CPU tensors never take the kernel
+
+
+def test_linear_on_cpu_is_f_linear():
+    torch.manual_seed(0)
+    x = torch.randn(3, 5, 16, requires_grad=True)
+    w = torch.randn(8, 16, requires_grad=True)
+    b = torch.randn(8, requires_grad=True)
+    y = lm.linear(x, w, b)
+    torch.testing.assert_close(y, F.linear(x, w, b))
+    y.sum().backward()
+    assert x.grad is not None and w.grad is not None and b.grad is not None
+
+
+def test_gemm_rejects_bad_shapes_before_launch():
+    a = torch.zeros(256, 64, dtype=torch.bfloat16)
+    b = torch.zeros(256, 64, dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        gemm.gemm(a, b, 256, 256, 96, True, True)
+    with pytest.raises(ValueError):
+        gemm.gemm(a.float(), b, 256, 256, 64, True, True)
+    with pytest.raises(ValueError):
+        gemm.gemm(a, b, 256, 256, 64, True, True, accumulate=True)
+
+
+def test_knob_disables_kernel(monkeypatch):
+    monkeypatch.setenv("PLX_LM_GEMM", "0")
+    assert not gemm.enabled()
+    monkeypatch.setenv("PLX_LM_GEMM", "1")
+    assert gemm.enabled()

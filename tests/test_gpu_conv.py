@@ -1,4 +1,6 @@
 """MFMA GEMM kernels for 1x1 convolutions (csrc/conv_gemm.hip) vs fp32 PyTorch references."""
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -423,7 +425,7 @@ def test_conv3x3_halo_matches_gather_and_fp32(cuda, shape, cout):
             y.backward(g)
             out[halo] = (y.float(), xa.grad.float(), g)
     finally:
-        lib.plx_set_halo(1)
+        lib.plx_set_halo(int(os.environ.get("PLX_HALO", "0")))
     xr = x.float().clone().requires_grad_()
     yr = F.conv2d(xr, conv.weight.detach().to(torch.bfloat16).float(), padding=1)
     yr.backward(out[1][2].float())

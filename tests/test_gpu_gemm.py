@@ -1,0 +1,151 @@
+"""The 256x256 MFMA GEMM of the LM linears (csrc/gemm256.hip via ops/gemm.py) vs fp32 PyTorch references."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    return torch.device("cuda", 0)
+
+
+def _rand(shape, device, seed):
+    g = torch.Generator(device=device).manual_seed(seed)
+    return torch.randn(shape, device=device, generator=g).to(torch.bfloat16)
+
+
+def _check(out, ref, K):
+    # bf16 output of a K-long fp32 accumulation of bf16 products: relative error ~2^-8 on the output
+    err = (out.float() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 1.5e-2 * scale + 1e-3, (err, scale, K)
+
+
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (768, 512, 1024)])
+def test_gemm256_layouts_match_fp32(cuda, a_kmajor, b_kmajor, M, N, K):
+    from polyaxon_amd.ops import gemm
+
+    a = _rand((M, K) if a_kmajor else (K, M), cuda, 1)
+    b = _rand((N, K) if b_kmajor else (K, N), cuda, 2)
+    out = gemm.gemm(a, b, M, N, K, a_kmajor, b_kmajor)
+    af = a.float() if a_kmajor else a.float().t()
+    bf = b.float() if b_kmajor else b.float().t()
+    torch.cuda.synchronize()
+    _check(out, af @ bf.t(), K)
+
+
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 8192), (512, 256, 4096), (256, 512, 2048 + 64)])
+def test_gemm256_split_k_and_accumulate(cuda, accumulate, M, N, K):
+    """Small tile grids with long K (the weight gradient) run split-K over fp32 slabs; accumulate adds into C."""
+    from polyaxon_amd.ops import _native, gemm
+
+    splits = _native.size("plx_gemm", "plx_gemm256_splits", M, N, K)
+    if K >= 4096:
+        assert splits > 1
+    a = _rand((K, M), cuda, 3)
+    b = _rand((K, N), cuda, 4)
+    c0 = _rand((M, N), cuda, 5)
+    out = c0.clone()
+    gemm.gemm(a, b, M, N, K, False, False, out=out, accumulate=accumulate, alpha=0.5)
+    ref = 0.5 * (a.float().t() @ b.float())
+    if accumulate:
+        ref = ref + c0.float()
+    torch.cuda.synchronize()
+    _check(out, ref, K)
+
+
+def test_gemm256_strided_output(cuda):
+    """out may be a column block of a wider matrix (ldc > N)."""
+    from polyaxon_amd.ops import gemm
+
+    M, N, K = 256, 256, 512
+    a, b = _rand((M, K), cuda, 6), _rand((N, K), cuda, 7)
+    wide = torch.zeros(M, 3 * N, dtype=torch.bfloat16, device=cuda)
+    gemm.gemm(a, b, M, N, K, True, True, out=wide[:, N:2 * N])
+    torch.cuda.synchronize()
+    _check(wide[:, N:2 * N], a.float() @ b.float().t(), K)
+    assert wide[:, :N].abs().max().item() == 0 and wide[:, 2 * N:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("bias", [False, True])
+def test_lm_linear_on_mfma_matches_fp32(cuda, bias):
+    """ops.lm.linear: forward, dx and dW (and db) of the MFMA path vs fp32 autograd."""
+    from polyaxon_amd.ops import _native, lm
+
+    B, S, fin, fout = 2, 256, 768, 1280
+    x = _rand((B, S, fin), cuda, 8).requires_grad_()
+    w = (_rand((fout, fin), cuda, 9).float() * 0.05).to(torch.bfloat16).requires_grad_()
+    b = (_rand((fout,), cuda, 10).float() * 0.1).to(torch.bfloat16).requires_grad_() if bias else None
+    y = lm.linear(x, w, b)
+    assert y.grad_fn is not None and "Mfma" in type(y.grad_fn).__name__
+    dy = _rand((B, S, fout), cuda, 11)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    br = b.detach().float().requires_grad_() if bias else None
+    yr = F.linear(xr, wr, br)
+    yr.backward(dy.float())
+    torch.cuda.synchronize()
+    _check(y, yr.detach(), fin)
+    _check(x.grad, xr.grad, fout)
+    _check(w.grad, wr.grad, B * S)
+    if bias:
+        torch.testing.assert_close(b.grad.float(), br.grad, rtol=2e-2, atol=2e-1)
+    assert _native.lib_path("plx_gemm").exists()
+
+
+def test_lm_linear_direct_grad_slot_accumulates(cuda):
+    """A flat-parameter weight used twice: the first wgrad writes the bf16 slot, the second accumulates in place."""
+    from polyaxon_amd.ops import lm
+
+    class _Flat:
+        def __init__(self):
+            self.written = set()
+
+        def mark_written(self, g):
+            k = g.data_ptr()
+            seen = k in self.written
+            self.written.add(k)
+            return seen
+
+    T, fin, fout = 512, 512, 768
+    w = (_rand((fout, fin), cuda, 12).float() * 0.05).to(torch.bfloat16).requires_grad_()
+    w.grad = torch.full_like(w, 7.0)  # stale content: the first write must overwrite it
+    w._plx_flat, w._plx_direct_grad = _Flat(), True
+    x1, x2 = _rand((T, fin), cuda, 13).requires_grad_(), _rand((T, fin), cuda, 14).requires_grad_()
+    y = lm.linear(x1, w) + lm.linear(x2, w)
+    dy = _rand((T, fout), cuda, 15)
+    slot = w.grad
+    y.backward(dy)
+    ref = dy.float().t() @ (x1.detach().float() + x2.detach().float())
+    torch.cuda.synchronize()
+    assert w.grad.data_ptr() == slot.data_ptr()
+    _check(w.grad, ref, 2 * T)
+
+
+def test_transformer_step_uses_mfma_linears(cuda):
+    """A GPT-2-shaped block in lp-bf16 takes the MFMA path for every projection (no hipBLASLt fallback)."""
+    from polyaxon_amd.models.transformer import Block, gpt2_125m
+
+    cfg = gpt2_125m(n_layers=1)
+    blk = Block(cfg).to(cuda).to(torch.bfloat16)
+    x = _rand((1, 256, cfg.d_model), cuda, 16).requires_grad_()
+    y = blk(x)
+    names = set()
+    stack = [y.grad_fn]
+    while stack:
+        fn = stack.pop()
+        if fn is None:
+            continue
+        names.add(type(fn).__name__)
+        stack.extend(f for f, _ in fn.next_functions)
+    assert any("Mfma" in n for n in names), names
+    assert not any(n.startswith("AddmmBackward") or n.startswith("MmBackward") for n in names), names
+    y.float().square().mean().backward()
+    assert torch.isfinite(x.grad.float()).all()
