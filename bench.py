@@ -380,22 +380,15 @@ def main() -> int:
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     if world > 1:
-        if dev.type == "cuda":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+        # The ranks' own control traffic (control address, barriers around the timed region) is a few bytes: it
+        # goes over gloo.  No RCCL communicator may exist while the sweeps run -- one created before the timed
+        # region measured 17 % fewer trials/h on one GPU (profiles/r3_negative_results.md) -- so the only RCCL
+        # collective, the per-rank gather, is made on a communicator created after the timed region.
+        dist.init_process_group("gloo")
         addr = [ctl_addr]
         dist.broadcast_object_list(addr, src=0)
         ctl_addr = addr[0]
     host, _, port = ctl_addr.rpartition(":")
-
-    # framework-owned collectives (csrc/rccl_comm.cpp) for the timing reduction on the GPU path
-    comm = None
-    if dev.type == "cuda" and os.environ.get("PLX_BENCH_RCCL", "1") != "0":
-        from polyaxon_amd.parallel.rccl import RcclComm
-
-        comm = (RcclComm.from_torch_distributed() if world > 1
-                else RcclComm(RcclComm.new_unique_id(), 1, 0, local))
 
     def barrier():
         if dev.type == "cuda":
@@ -431,13 +424,21 @@ def main() -> int:
     if r != "pause:timed":
         raise RuntimeError(f"executor stopped during the timed region: {r}")
     mine = [elapsed, worker.stats["trials"] - s0["trials"], worker.stats["train_steps"] - s0["train_steps"],
-            float(os.getpid())]
+            float(os.getpid())] + [worker.stats[k] - s0[k] for k in ("idle_s", "round_s", "sync_s")]
+    # framework-owned collective (csrc/rccl_comm.cpp) for the per-rank gather on the GPU path, on a communicator
+    # created only now (see the process-group note above).
+    comm = None
+    if dev.type == "cuda" and os.environ.get("PLX_BENCH_RCCL", "1") != "0":
+        from polyaxon_amd.parallel.rccl import RcclComm
+
+        comm = (RcclComm.from_torch_distributed() if world > 1
+                else RcclComm(RcclComm.new_unique_id(), 1, 0, local))
     if comm is not None:
         t = torch.tensor(mine, dtype=torch.float64, device=dev)
         per_rank = comm.all_gather(t).cpu().tolist()
         torch.cuda.synchronize(dev)
     elif world > 1:
-        g = [torch.zeros(4, dtype=torch.float64) for _ in range(world)]
+        g = [torch.zeros(len(mine), dtype=torch.float64) for _ in range(world)]
         dist.all_gather(g, torch.tensor(mine, dtype=torch.float64))
         per_rank = [x.tolist() for x in g]
     else:
@@ -495,7 +496,8 @@ def main() -> int:
             "path": "polyflow scheduler (own process) + SQLite store + resident executors (same path as plx run)",
             "hip_graph": bool(worker._ready_info.get("hip_graph")),
             "per_rank": [{"rank": i, "pid": int(p[3]), "elapsed_s": round(p[0], 3), "trials": int(p[1]),
-                          "train_steps": int(p[2])} for i, p in enumerate(per_rank)],
+                          "train_steps": int(p[2]), "idle_s": round(p[4], 3), "round_s": round(p[5], 3),
+                          "sync_s": round(p[6], 3)} for i, p in enumerate(per_rank)],
             "executors": res["executors"],
             "control_pid": res["control_pid"],
             "cpus_pinned": len(pinned),

@@ -12,6 +12,11 @@ epilogue adds to the bf16 slot in place, so a weight used twice needs no separat
 
 Shapes the kernel does not take (a dimension not a multiple of 256, or K of 64) go to ``torch`` (hipBLASLt) —
 :func:`supported` says which; on a GPU box a missing library raises instead of falling back (ops/_native.py).
+
+Dispatch (``PLX_LM_GEMM``): ``1`` always the MFMA kernel, ``0`` always hipBLASLt, ``auto`` (default) times both
+once per (M, N, K, layout) on first use and keeps the faster -- measured on MI355X the kernel wins the narrow
+weight gradients (split-K, 1.1-1.4x) and trails hipBLASLt by 10-25 % on the large forward / data-gradient shapes
+(profiles/r3_lm_gemm.md), so ``auto`` is what the trainers run.  :func:`decisions` lists what was chosen.
 """
 from __future__ import annotations
 
@@ -26,9 +31,67 @@ TILE = 256
 _ws: Dict[Tuple[str, int], torch.Tensor] = {}
 
 
+_choice: Dict[Tuple[int, int, int, bool, bool], Tuple[bool, float, float]] = {}
+
+
+def mode() -> str:
+    m = os.environ.get("PLX_LM_GEMM", "auto")
+    return m if m in ("0", "1", "auto") else "auto"
+
+
 def enabled() -> bool:
     """PLX_LM_GEMM=0 routes the LM linears back to hipBLASLt (A/B knob)."""
-    return os.environ.get("PLX_LM_GEMM", "1") != "0"
+    return mode() != "0"
+
+
+def decisions() -> Dict[str, Dict[str, object]]:
+    """Per shape measured by ``auto``: which GEMM runs and both times (ms)."""
+    return {f"{M}x{N}x{K}:{'K' if ak else 'M'}{'K' if bk else 'N'}": {"native": nat, "native_ms": tn, "torch_ms": tt}
+            for (M, N, K, ak, bk), (nat, tn, tt) in _choice.items()}
+
+
+def _torch_gemm(a, b, M, N, K, a_kmajor, b_kmajor, out=None, accumulate=False, alpha=1.0):
+    A = a.view(M, K) if a_kmajor else a.view(K, M).t()
+    Bt = b.view(N, K).t() if b_kmajor else b.view(K, N)
+    if out is None:
+        return torch.mm(A, Bt) if alpha == 1.0 else torch.mm(A, Bt).mul_(alpha)
+    if accumulate:
+        out.addmm_(A, Bt, alpha=alpha)
+    else:
+        torch.mm(A, Bt, out=out)
+        if alpha != 1.0:
+            out.mul_(alpha)
+    return out
+
+
+def _use_native(a, b, M, N, K, a_kmajor, b_kmajor) -> bool:
+    m = mode()
+    if m != "auto":
+        return m == "1"
+    key = (M, N, K, bool(a_kmajor), bool(b_kmajor))
+    hit = _choice.get(key)
+    if hit is None:
+        ts = []
+        for native in (True, False):
+            fn = (lambda: gemm(a, b, M, N, K, a_kmajor, b_kmajor)) if native else (
+                lambda: _torch_gemm(a, b, M, N, K, a_kmajor, b_kmajor))
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(3):
+                fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) / 3)
+        hit = _choice[key] = (ts[0] <= ts[1], round(ts[0], 4), round(ts[1], 4))
+    return hit[0]
+
+
+def matmul(a, b, M, N, K, a_kmajor, b_kmajor, out=None, accumulate=False) -> torch.Tensor:
+    """:func:`gemm` semantics on whichever of the MFMA kernel / hipBLASLt the dispatch mode picks."""
+    if _use_native(a, b, M, N, K, a_kmajor, b_kmajor):
+        return gemm(a, b, M, N, K, a_kmajor, b_kmajor, out=out, accumulate=accumulate)
+    return _torch_gemm(a, b, M, N, K, a_kmajor, b_kmajor, out=out, accumulate=accumulate)
 
 
 def supported(M: int, N: int, K: int) -> bool:
@@ -83,13 +146,13 @@ def linear_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
 def forward(x2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """y[T][out] = x[T][in] . W[out][in]^T"""
     T, fin = x2.shape
-    return gemm(x2, weight, T, weight.shape[0], fin, True, True)
+    return matmul(x2, weight, T, weight.shape[0], fin, True, True)
 
 
 def dgrad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """dx[T][in] = dy[T][out] . W[out][in]"""
     T, fout = dy2.shape
-    return gemm(dy2, weight, T, weight.shape[1], fout, True, False)
+    return matmul(dy2, weight, T, weight.shape[1], fout, True, False)
 
 
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -99,4 +162,4 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: Optional[torch.Tensor] = Non
     fin = x2.shape[1]
     if out is not None:
         out = out.view(fout, fin)
-    return gemm(dy2, x2, fout, fin, T, False, False, out=out, accumulate=accumulate)
+    return matmul(dy2, x2, fout, fin, T, False, False, out=out, accumulate=accumulate)

@@ -205,7 +205,10 @@ class ResidentWorker:
         self.pause_tag: Optional[str] = None
         self.metrics = None
         self.stats = {"trials": 0, "train_steps": 0, "rounds": 0, "topk_launches": 0, "early_stop_launches": 0,
-                      "asha_jobs": 0}
+                      "asha_jobs": 0,
+                      # wall seconds: blocked waiting for work, inside rounds, and in each round's synchronising
+                      # D2H read (host waiting for the GPU to finish the round's queued work)
+                      "idle_s": 0.0, "round_s": 0.0, "sync_s": 0.0}
         self._base_ev = None
         self._base_wall = 0.0
         self._shutdown: Optional[str] = None
@@ -357,7 +360,10 @@ class ResidentWorker:
         while True:
             busy = bool(self.active or self.queue or self.asha_active or self.asha_queue)
             try:
+                t_wait = time.perf_counter()
                 msg = chan.recv(timeout=0 if busy else (None if self.pause_tag is None else 0))
+                if not busy:
+                    self.stats["idle_s"] += time.perf_counter() - t_wait
             except ChannelClosed:
                 return "eof"
             if msg is not None:
@@ -374,7 +380,9 @@ class ResidentWorker:
                 continue
             if self.active or self.queue or self.asha_active or self.asha_queue:
                 self._shutdown = None
+                t_round = time.perf_counter()
                 self.run_round(chan)
+                self.stats["round_s"] += time.perf_counter() - t_round
                 if self._shutdown is not None:
                     return self._shutdown
             elif self.pause_tag is not None:
@@ -554,10 +562,12 @@ class ResidentWorker:
                 self.stats["early_stop_launches"] += 1
                 a_early[sh.key] = any(flags)
         # the round's D2H reads (the first one synchronises)
+        t_sync = time.perf_counter()
         vals = self.metrics.values[:n].detach().cpu().tolist() if n else []
         orders_h = {mx: o[:n].cpu().tolist() for mx, o in orders.items()}
         a_vals = self.asha_metrics.values[:a_rows].detach().cpu().tolist() if live else []
         a_orders_h = {mx: o[:a_rows].cpu().tolist() for mx, o in a_orders.items()}
+        self.stats["sync_s"] += time.perf_counter() - t_sync
         for row, br, slot, cid, steps, t0, t1 in records:
             v = vals[row][slot]
             self.stats["trials"] += 1

@@ -246,8 +246,13 @@ def train_lm(argv=None) -> float:
         xp.log_metrics(step=args.steps, loss=loss_val, tokens_per_s=tok_s)
         xp.close()
     if info["rank"] == 0:
+        from polyaxon_amd.ops import gemm as _gemm
+
+        dec = _gemm.decisions()
         print(json.dumps({"loss": loss_val, "tokens_per_s": round(tok_s, 1), "world": info["world"],
-                          "params_m": round(sum(s.numel for s in flat.segments) / 1e6, 1)}))
+                          "params_m": round(sum(s.numel for s in flat.segments) / 1e6, 1),
+                          "lm_gemm": {"mode": _gemm.mode(), "native_shapes": sum(1 for d in dec.values() if d["native"]),
+                                      "shapes": len(dec), "decisions": dec}}))
     metrics.close()
     if info["world"] > 1:
         import torch.distributed as dist

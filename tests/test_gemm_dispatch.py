@@ -43,8 +43,28 @@ def test_gemm_rejects_bad_shapes_before_launch():
         gemm.gemm(a, b, 256, 256, 64, True, True, accumulate=True)
 
 
-def test_knob_disables_kernel(monkeypatch):
+def test_knob_modes(monkeypatch):
     monkeypatch.setenv("PLX_LM_GEMM", "0")
-    assert not gemm.enabled()
+    assert not gemm.enabled() and gemm.mode() == "0"
     monkeypatch.setenv("PLX_LM_GEMM", "1")
-    assert gemm.enabled()
+    assert gemm.enabled() and gemm.mode() == "1"
+    monkeypatch.delenv("PLX_LM_GEMM")
+    assert gemm.mode() == "auto" and gemm.enabled()
+    monkeypatch.setenv("PLX_LM_GEMM", "bogus")
+    assert gemm.mode() == "auto"
+
+
+def test_torch_path_layouts_match_reference():
+    """The hipBLASLt side of the dispatch (here on CPU) computes the same layouts as the kernel contract."""
+    torch.manual_seed(0)
+    M, N, K = 8, 6, 4
+    a_k, b_k = torch.randn(M, K), torch.randn(N, K)
+    ref = a_k @ b_k.t()
+    for ak in (True, False):
+        for bk in (True, False):
+            a = a_k.contiguous() if ak else a_k.t().contiguous()
+            b = b_k.contiguous() if bk else b_k.t().contiguous()
+            torch.testing.assert_close(gemm._torch_gemm(a, b, M, N, K, ak, bk), ref)
+            out = torch.ones(M, N)
+            gemm._torch_gemm(a, b, M, N, K, ak, bk, out=out, accumulate=True)
+            torch.testing.assert_close(out, ref + 1)

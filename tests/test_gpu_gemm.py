@@ -74,9 +74,11 @@ def test_gemm256_strided_output(cuda):
 
 
 @pytest.mark.parametrize("bias", [False, True])
-def test_lm_linear_on_mfma_matches_fp32(cuda, bias):
+def test_lm_linear_on_mfma_matches_fp32(cuda, bias, monkeypatch):
     """ops.lm.linear: forward, dx and dW (and db) of the MFMA path vs fp32 autograd."""
     from polyaxon_amd.ops import _native, lm
+
+    monkeypatch.setenv("PLX_LM_GEMM", "1")
 
     B, S, fin, fout = 2, 256, 768, 1280
     x = _rand((B, S, fin), cuda, 8).requires_grad_()
@@ -100,9 +102,13 @@ def test_lm_linear_on_mfma_matches_fp32(cuda, bias):
     assert _native.lib_path("plx_gemm").exists()
 
 
-def test_lm_linear_direct_grad_slot_accumulates(cuda):
-    """A flat-parameter weight used twice: the first wgrad writes the bf16 slot, the second accumulates in place."""
+@pytest.mark.parametrize("mode", ["1", "0"])
+def test_lm_linear_direct_grad_slot_accumulates(cuda, mode, monkeypatch):
+    """A flat-parameter weight used twice: the first wgrad writes the bf16 slot, the second accumulates in place
+    (on the MFMA kernel's epilogue, and on the hipBLASLt addmm path)."""
     from polyaxon_amd.ops import lm
+
+    monkeypatch.setenv("PLX_LM_GEMM", mode)
 
     class _Flat:
         def __init__(self):
@@ -129,9 +135,11 @@ def test_lm_linear_direct_grad_slot_accumulates(cuda):
     _check(w.grad, ref, 2 * T)
 
 
-def test_transformer_step_uses_mfma_linears(cuda):
+def test_transformer_step_uses_mfma_linears(cuda, monkeypatch):
     """A GPT-2-shaped block in lp-bf16 takes the MFMA path for every projection (no hipBLASLt fallback)."""
     from polyaxon_amd.models.transformer import Block, gpt2_125m
+
+    monkeypatch.setenv("PLX_LM_GEMM", "1")
 
     cfg = gpt2_125m(n_layers=1)
     blk = Block(cfg).to(cuda).to(torch.bfloat16)
@@ -149,3 +157,20 @@ def test_transformer_step_uses_mfma_linears(cuda):
     assert not any(n.startswith("AddmmBackward") or n.startswith("MmBackward") for n in names), names
     y.float().square().mean().backward()
     assert torch.isfinite(x.grad.float()).all()
+
+
+def test_auto_dispatch_times_both_and_matches(cuda, monkeypatch):
+    """PLX_LM_GEMM=auto: the first call of a shape times the kernel and hipBLASLt, records the choice, and either
+    way the result matches fp32."""
+    from polyaxon_amd.ops import gemm
+
+    monkeypatch.setenv("PLX_LM_GEMM", "auto")
+    T, fin, fout = 1024, 768, 2304
+    x, w = _rand((T, fin), cuda, 17), _rand((fout, fin), cuda, 18)
+    y = gemm.forward(x, w)
+    dec = gemm.decisions()
+    assert f"{T}x{fout}x{fin}:KK" in dec
+    d = dec[f"{T}x{fout}x{fin}:KK"]
+    assert d["native_ms"] > 0 and d["torch_ms"] > 0
+    torch.cuda.synchronize()
+    _check(y, x.float() @ w.float().t(), fin)
