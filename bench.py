@@ -14,8 +14,9 @@ BASELINE.json config 3 ("Hyperband/ASHA sweep of ResNet-50 on synthetic ImageNet
   ``environment.executor: resident``.  ``--search hyperband`` (default; ``max_iter 9, eta 3, resume: true``:
   3 brackets and 23 trials each, reference-exact bracket arithmetic) spreads its ``3·K·N`` brackets over the N
   executors, each executor interleaves its brackets and decides each round's promotions with one HIP top-k launch;
-  ``--search asha`` runs each sweep as one asynchronous successive-halving search (min 1, max 9, eta 3 resource
-  units, ``--asha-n`` configs; no rung barrier).  Every trial is an experiment row with its status history, metric
+  ``--search asha`` runs each sweep as one asynchronous successive-halving search (min 1, max 27, eta 3 resource
+  units -- 27 is the largest budget the reference's Hyperband arithmetic gives one trial of a max_iter 9 sweep --
+  and ``--asha-n`` 29 configs, about the 87 units of a Hyperband sweep; no rung barrier).  Every trial is an experiment row with its status history, metric
   and RESUME lineage.  The timed region starts after a barrier (after ``--warmup W`` untimed sweeps per GPU through
   the same path) and ends when every group has SUCCEEDED and every rank passed the final barrier: only whole sweeps
   are timed, never a prefix;
@@ -47,6 +48,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 T0 = time.perf_counter()
 METRIC = "HPO trials/hour (whole node) + wall-clock-to-target, ResNet-50 Hyperband sweep"
 MAX_ITER, ETA = 9, 3
+# ASHA's largest rung: the reference's Hyperband (r_i = r * eta^i, polytune/managers.py) trains its last bracket's
+# survivor 27 units at max_iter 9, so ASHA gets the same top budget to be comparable
+ASHA_MAX = MAX_ITER * ETA
 
 
 def _args(argv=None):
@@ -55,12 +59,15 @@ def _args(argv=None):
     ap.add_argument("--steps", type=int, default=3, help="timed sweeps per GPU (hyperband: 3 brackets, 23 trials)")
     ap.add_argument("--warmup", type=int, default=1, help="untimed sweeps per GPU through the same path")
     ap.add_argument("--search", choices=("hyperband", "asha"), default="hyperband")
-    ap.add_argument("--asha-n", type=int, default=37,
-                    help="configs per ASHA sweep (37 at min 1 / max 9 / eta 3 ~ the 87 units of a Hyperband sweep)")
+    ap.add_argument("--asha-n", type=int, default=29,
+                    help="configs per ASHA sweep (29 at min 1 / max 27 / eta 3 with resume ~ the 87 units of a "
+                         "Hyperband sweep)")
     ap.add_argument("--batch", type=int, default=256, help="per-trial batch (one trial per GPU at a time)")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--unit-steps", type=int, default=4, help="training steps per resource unit")
-    ap.add_argument("--target", type=float, default=1.0, help="loss target for wall-clock-to-target")
+    ap.add_argument("--target", type=float, default=0.03,
+                    help="loss target for wall-clock-to-target: near the synthetic task's floor at a sweep's budget "
+                         "(Hyperband sweeps reach 0.015-0.1), so only some sweeps reach it")
     ap.add_argument("--signal", type=float, default=0.5, help="class-pattern amplitude of the synthetic data")
     ap.add_argument("--active-classes", type=int, default=100, help="classes the synthetic task draws from")
     ap.add_argument("--max-active", type=int, default=8, help="brackets one executor interleaves")
@@ -83,7 +90,7 @@ def program_params(args):
 
 
 def group_spec(seed: int, program: str, params: dict, concurrency: int, max_active: int, search: str = "hyperband",
-               asha_n: int = 37) -> dict:
+               asha_n: int = 29) -> dict:
     matrix = {"lr": {"loguniform": [math.log(0.02), math.log(1.0)]},
               "momentum": {"uniform": [0.8, 0.95]},
               "weight_decay": {"loguniform": [math.log(1e-5), math.log(1e-3)]}}
@@ -91,7 +98,7 @@ def group_spec(seed: int, program: str, params: dict, concurrency: int, max_acti
     resource = {"name": "units", "type": "int"}
     if search == "asha":
         hp = {"seed": seed, "concurrency": concurrency, "matrix": matrix,
-              "asha": {"min_resource": 1, "max_resource": MAX_ITER, "eta": ETA, "n_experiments": asha_n,
+              "asha": {"min_resource": 1, "max_resource": ASHA_MAX, "eta": ETA, "n_experiments": asha_n,
                        "resource": resource, "metric": metric, "resume": True}}
     else:
         hp = {"seed": seed, "concurrency": concurrency, "matrix": matrix,
@@ -235,6 +242,15 @@ class ControlServer:
             h = [x["finished_at"] for x in gx if x["last_metric"]["loss"] <= target]
             per_sweep.append({"group": g, "best": round(b, 4) if b is not None else None,
                               "hit_s": round(min(h) - t0_wall, 2) if h else None})
+        # per training budget (resource units): trials and their best / median metric -- what each rung bought
+        by_units: dict = {}
+        for x in xs:
+            u = (x.get("declarations") or {}).get("units")
+            v = (x.get("last_metric") or {}).get("loss")
+            if u is not None and v is not None:
+                by_units.setdefault(str(u), []).append(float(v))
+        per_units = {u: {"trials": len(v), "best": round(min(v), 4), "median": round(sorted(v)[len(v) // 2], 4)}
+                     for u, v in sorted(by_units.items(), key=lambda kv: float(kv[0]))}
         # the status history every trial must show (reference ExperimentLifeCycle)
         want = ["created", "scheduled", "starting", "running", "succeeded"]
         sample = xs[:: max(1, len(xs) // 50)]
@@ -253,6 +269,7 @@ class ControlServer:
                           "load_units": round(w["assigned_units"] - w0.get("assigned_units", 0.0), 3),
                           "units_of_work": w["assigned"] - w0.get("assigned", 0)})
         return {"trials": trials, "succeeded": ok, "train_steps": steps, "ttt": ttt, "best": best, "per_sweep": per_sweep,
+                "per_units": per_units,
                 "fsm_ok": fsm_ok, "resumed": resumed, "brackets": units, "groups": len(gids), "executors": execs,
                 "control_pid": os.getpid()}
 
@@ -453,7 +470,7 @@ def main() -> int:
         value = res["trials"] / elapsed_max * 3600.0
         search = (f"hyperband max_iter={MAX_ITER} eta={ETA} resume=true, 3 brackets / 23 trials per sweep"
                   if args.search == "hyperband" else
-                  f"asha min_resource=1 max_resource={MAX_ITER} eta={ETA} resume=true, {args.asha_n} configs per sweep")
+                  f"asha min_resource=1 max_resource={ASHA_MAX} eta={ETA} resume=true, {args.asha_n} configs per sweep")
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -492,6 +509,7 @@ def main() -> int:
             "best_loss": round(res["best"], 4) if res["best"] is not None else None,
             "sweeps_reaching_target": sum(1 for p in res["per_sweep"] if p["hit_s"] is not None),
             "sweep_best_loss": [p["best"] for p in res["per_sweep"]],
+            "loss_by_units": res["per_units"],
             "store_fsm_history_ok": res["fsm_ok"],
             "path": "polyflow scheduler (own process) + SQLite store + resident executors (same path as plx run)",
             "hip_graph": bool(worker._ready_info.get("hip_graph")),
