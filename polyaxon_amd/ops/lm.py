@@ -198,6 +198,9 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
     """F.linear on the MFMA GEMM kernel when the shapes fit it (ops/gemm.py: tokens, in and out multiples of 256,
     bf16, PLX_LM_GEMM != 0), with the weight gradient written into the flat gradient slot when ``weight`` is a flat
     parameter in lp mode with direct grads; hipBLASLt (F.linear / the direct-gradient form) otherwise."""
+    if (x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.bfloat16
+            and torch.is_autocast_enabled("cuda")):
+        x = x.to(torch.bfloat16)  # what autocast's F.linear does; here it keeps the LayerNorm outputs on the MFMA path
     slot = getattr(weight, "grad", None)
     flat = getattr(weight, "_plx_flat", None)
     direct = (flat is not None and getattr(weight, "_plx_direct_grad", False) and slot is not None

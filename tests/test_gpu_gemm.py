@@ -174,3 +174,20 @@ def test_auto_dispatch_times_both_and_matches(cuda, monkeypatch):
     assert d["native_ms"] > 0 and d["torch_ms"] > 0
     torch.cuda.synchronize()
     _check(y, x.float() @ w.float().t(), fin)
+
+
+def test_autocast_fp32_input_takes_mfma_path(cuda, monkeypatch):
+    """Under bf16 autocast a LayerNorm output arrives in fp32: lm.linear casts it like autocast's F.linear would and
+    keeps the projection on the MFMA kernel (GPT-2's qkv / up linears)."""
+    from polyaxon_amd.ops import lm
+
+    monkeypatch.setenv("PLX_LM_GEMM", "1")
+    x = torch.randn(256, 768, device=cuda, requires_grad=True)
+    w = (_rand((2304, 768), cuda, 19).float() * 0.05).to(torch.bfloat16).requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = lm.linear(x, w)
+    assert y.dtype == torch.bfloat16 and "Mfma" in type(y.grad_fn).__name__
+    y.float().sum().backward()
+    torch.cuda.synchronize()
+    _check(y, x.detach().to(torch.bfloat16).float() @ w.detach().float().t(), 768)
+    assert x.grad is not None and x.grad.dtype == torch.float32
