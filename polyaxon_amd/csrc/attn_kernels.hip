@@ -63,19 +63,19 @@ __device__ __forceinline__ int swz(int row) {
 // Stage R rows x D of a row-major tile (row stride ld elements, rows >= nvalid -> zero page) into a lane-linear
 // LDS image: wave instruction i writes bytes [1024 i, 1024 i + 1024) = rows of 2D bytes, physical 16-B chunk
 // p of row r holds logical chunk p ^ swz(r).
-template <int D, int R>
+template <int D, int R, int NW = 4>
 __device__ __forceinline__ void stage_tile(char* img, const __bf16* g, long long ld, int nvalid,
                                            const __bf16* zero, int wave, int lane) {
   constexpr int ROWB = 2 * D;
   constexpr int INSTR = R * ROWB / 1024;
-  static_assert(INSTR % 4 == 0, "tile must split evenly over the 4 waves");
+  static_assert(INSTR % NW == 0, "tile must split evenly over the waves");
 #pragma unroll
-  for (int i = 0; i < INSTR / 4; ++i) {
-    const int off = (i * 4 + wave) * 1024 + lane * 16;
+  for (int i = 0; i < INSTR / NW; ++i) {
+    const int off = (i * NW + wave) * 1024 + lane * 16;
     const int row = off / ROWB, pc = (off % ROWB) >> 4;
     const int lc = pc ^ swz<D>(row);
     const __bf16* src = row < nvalid ? g + (long long)row * ld + lc * 8 : zero;
-    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(img + (i * 4 + wave) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(img + (i * NW + wave) * 1024), 16, 0, 0);
   }
 }
 
@@ -152,30 +152,50 @@ struct QBlock {
   int b, hq, hk, q0;
 };
 
+// Query block of this workgroup (QB rows).  Heaviest-first over the WHOLE grid: block id i covers q-block index
+// nqb - 1 - i / (B*H) of head i % (B*H), so under the causal mask the longest key ranges of every head are
+// dispatched first and the short ones fill the tail (a per-head order still put heavy blocks of late heads last).
+template <int QB>
 __device__ __forceinline__ QBlock q_block(const AttnArgs& a) {
-  const int nqb = (a.S + 127) / 128;
+  const int nqb = (a.S + QB - 1) / QB;
+  const int bhn = a.B * a.H;
   const int bid = blockIdx.x;
   QBlock r;
-  r.q0 = (nqb - 1 - bid % nqb) * 128;  // heaviest (longest causal range) blocks first
-  const int bh = bid / nqb;
+  r.q0 = (nqb - 1 - bid / bhn) * QB;
+  const int bh = bid % bhn;
   r.b = bh / a.H;
   r.hq = bh % a.H;
   r.hk = r.hq / (a.H / a.Hkv);
   return r;
 }
 
+// raw v_exp_f32 (2^x): the libm exp2f adds a denormal range fix-up (compare, two selects, ldexp) per call; softmax
+// arguments are <= RESCALE_TH and anything below 2^-126 may flush to zero
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Deferred rescale (lazy max): the running max m of a query row only moves when a tile's max exceeds it by more than
+// RESCALE_TH (log2 units), so O and l are rescaled on a few tiles instead of every tile; probabilities stay
+// <= 2^RESCALE_TH (fp32 sums and bf16 P are exact enough there), and o / l always see the same reference max.
+constexpr float RESCALE_TH = 8.f;
+
 // ------------------------------------------------------------------------------------------------ forward
-template <int D>
-__global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
-  constexpr int TB = 64 * 2 * D, STAGE = 2 * TB, ND = D / 32, NS = D / 16;
+// NW waves x 32 queries per workgroup: one K/V tile in LDS feeds NW * 32 queries (8 waves halve the per-CU LDS-DMA
+// fill of the 4-wave form, which at the MFMA-bound rate needed ~77 GB/s per CU, above what LDS-DMA sustains).
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int QB = 32 * NW, TB = 64 * 2 * D, STAGE = 2 * TB, ND = D / 32, NS = D / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, ql = lane & 31;
-  const QBlock blk = q_block(a);
+  const QBlock blk = q_block<QB>(a);
   const int q0w = blk.q0 + 32 * wave, qi = q0w + ql;
   const __bf16* Q = a.q + blk.b * a.sq.b + blk.hq * a.sq.h;
   const __bf16* K = a.k + blk.b * a.sk.b + blk.hk * a.sk.h;
   const __bf16* V = a.v + blk.b * a.sv.b + blk.hk * a.sv.h;
 
+  const int kv_end = a.causal ? min(a.Skv, blk.q0 + QB) : a.Skv;
+  const int nt = (kv_end + 63) / 64;
+  stage_tile<D, 64, NW>(smem, K, a.sk.s, a.Skv, a.zero, wave, lane);
+  stage_tile<D, 64, NW>(smem + TB, V, a.sv.s, a.Skv, a.zero, wave, lane);
   bf16x8 qf[NS];
   {
     const __bf16* qr = Q + (long long)min(qi, a.S - 1) * a.sq.s + 8 * h;
@@ -186,19 +206,15 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) o[dt] = zero16();
   float m_run = NEG_INF, l_run = 0.f;
-
-  const int kv_end = a.causal ? min(a.Skv, blk.q0 + 128) : a.Skv;
-  const int nt = (kv_end + 63) / 64;
-  stage_tile<D, 64>(smem, K, a.sk.s, a.Skv, a.zero, wave, lane);
-  stage_tile<D, 64>(smem + TB, V, a.sv.s, a.Skv, a.zero, wave, lane);
+  const float c = a.c;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int j = 0; j < nt; ++j) {
     const int kv0 = j * 64;
     if (j + 1 < nt) {
       char* nb = smem + ((j + 1) & 1) * STAGE;
-      stage_tile<D, 64>(nb, K + (long long)(kv0 + 64) * a.sk.s, a.sk.s, a.Skv - kv0 - 64, a.zero, wave, lane);
-      stage_tile<D, 64>(nb + TB, V + (long long)(kv0 + 64) * a.sv.s, a.sv.s, a.Skv - kv0 - 64, a.zero, wave, lane);
+      stage_tile<D, 64, NW>(nb, K + (long long)(kv0 + 64) * a.sk.s, a.sk.s, a.Skv - kv0 - 64, a.zero, wave, lane);
+      stage_tile<D, 64, NW>(nb + TB, V + (long long)(kv0 + 64) * a.sv.s, a.sv.s, a.Skv - kv0 - 64, a.zero, wave, lane);
     }
     const char* Ks = smem + (j & 1) * STAGE;
     const char* Vs = Ks + TB;
@@ -209,40 +225,43 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
         st[0] = mfma(row_frag<D>(Ks, ql, 2 * s + h), qf[s], st[0]);
         st[1] = mfma(row_frag<D>(Ks, 32 + ql, 2 * s + h), qf[s], st[1]);
       }
-      const bool mask = (a.causal && kv0 + 63 > q0w) || kv0 + 64 > a.Skv;
+      if ((a.causal && kv0 + 63 > q0w) || kv0 + 64 > a.Skv) {  // diagonal / ragged tile: mask (raw scores)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kv0 + 32 * t + acc_row(r, h);
+            if ((a.causal && key > qi) || key >= a.Skv) st[t][r] = NEG_INF;
+          }
+      }
       float mx = NEG_INF;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float v = st[t][r] * a.c;
-          if (mask) {
-            const int key = kv0 + 32 * t + acc_row(r, h);
-            if ((a.causal && key > qi) || key >= a.Skv) v = NEG_INF;
-          }
-          st[t][r] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float m_new = fmaxf(m_run, mx);
-      const float msub = m_new == NEG_INF ? 0.f : m_new;
-      const float alpha = exp2f(m_run - msub);  // m_run = -inf -> 0
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[t][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32)) * c;  // c > 0: max of the scaled scores
+      const bool grow = mx > m_run + RESCALE_TH;
+      if (__builtin_amdgcn_ballot_w64(grow)) {   // wave-uniform branch; lanes that do not grow keep alpha = 1
+        const float m_new = grow ? mx : m_run;
+        const float alpha = m_run == NEG_INF ? 0.f : fast_exp2(m_run - m_new);
+        l_run *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        m_run = m_new;
+      }
+      const float msub = m_run == NEG_INF ? 0.f : m_run;  // a fully masked row so far: p = 2^-inf = 0
       float sum = 0.f;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = exp2f(st[t][r] - msub);
+          const float p = fast_exp2(fmaf(st[t][r], c, -msub));
           st[t][r] = p;
           sum += p;
         }
-      sum += __shfl_xor(sum, 32);
-      l_run = l_run * alpha + sum;
-      m_run = m_new;
-#pragma unroll
-      for (int dt = 0; dt < ND; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+      l_run += sum + __shfl_xor(sum, 32);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -291,7 +310,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int TB = 64 * 2 * D, STAGE = 2 * TB, ND = D / 32, NS = D / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, ql = lane & 31;
-  const QBlock blk = q_block(a);
+  const QBlock blk = q_block<128>(a);
   const int q0w = blk.q0 + 32 * wave, qi = q0w + ql, qc = min(qi, a.S - 1);
   const __bf16* K = a.k + blk.b * a.sk.b + blk.hk * a.sk.h;
   const __bf16* V = a.v + blk.b * a.sv.b + blk.hk * a.sv.h;
@@ -549,21 +568,27 @@ bool args_ok(const AttnArgs& a, int D) {
 
 }  // namespace
 
+// forward waves per workgroup (A/B knob plx_attn_set_fwd_waves: 4 or 8)
+int g_fwd_waves = 8;
+
+template <int D, int NW>
+int launch_fwd(const AttnArgs& a, hipStream_t stream) {
+  constexpr int LDS = 4 * 64 * 2 * D;  // 2 stages x {K, V} x 64 rows
+  static int once = prepare(attn_fwd_kernel<D, NW>, LDS);
+  if (once) return once;
+  const int grid = ((a.S + 32 * NW - 1) / (32 * NW)) * a.H * a.B;
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NW>), dim3(grid), dim3(64 * NW), LDS, stream, a);
+  return (int)hipGetLastError();
+}
+
+PLX_API void plx_attn_set_fwd_waves(int nw) { g_fwd_waves = nw == 4 ? 4 : 8; }
+
 PLX_API int plx_attn_fwd(const AttnArgs* args, int D, hipStream_t stream) {
   const AttnArgs& a = *args;
   if (!args_ok(a, D)) return 1;
   if (a.so.s % 4 || a.so.h % 4 || a.so.b % 4) return 1;
-  const int grid = ((a.S + 127) / 128) * a.H * a.B;
-  if (D == 128) {
-    static int once = prepare(attn_fwd_kernel<128>, 4 * 64 * 256);
-    if (once) return once;
-    hipLaunchKernelGGL(attn_fwd_kernel<128>, dim3(grid), dim3(NT), 4 * 64 * 256, stream, a);
-  } else {
-    static int once = prepare(attn_fwd_kernel<64>, 4 * 64 * 128);
-    if (once) return once;
-    hipLaunchKernelGGL(attn_fwd_kernel<64>, dim3(grid), dim3(NT), 4 * 64 * 128, stream, a);
-  }
-  return (int)hipGetLastError();
+  if (D == 128) return g_fwd_waves == 4 ? launch_fwd<128, 4>(a, stream) : launch_fwd<128, 8>(a, stream);
+  return g_fwd_waves == 4 ? launch_fwd<64, 4>(a, stream) : launch_fwd<64, 8>(a, stream);
 }
 
 PLX_API long long plx_attn_bwd_workspace(int B, int H, int Hkv, int Skv, int D) {

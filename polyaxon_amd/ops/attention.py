@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Optional
 
 import torch
@@ -87,11 +88,25 @@ def _reference(q, k, v, causal, scale):
     return o.transpose(1, 2)
 
 
+_KNOBS_SET = False
+
+
+def _lib():
+    """The attention library with its A/B knobs applied once (PLX_ATTN_FWD_WAVES: 8 (default) or 4 waves per
+    forward workgroup)."""
+    global _KNOBS_SET
+    lib = _native.lib("plx_attn")
+    if not _KNOBS_SET:
+        _check(lib.plx_attn_args_size())
+        lib.plx_attn_set_fwd_waves(int(os.environ.get("PLX_ATTN_FWD_WAVES", "8")))
+        _KNOBS_SET = True
+    return lib
+
+
 class _FlashAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal: bool, scale: float):
-        lib = _native.lib("plx_attn")
-        _check(lib.plx_attn_args_size())
+        lib = _lib()
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         B, H, S, D = q.shape
         out = torch.empty(B, S, H, D, dtype=q.dtype, device=q.device)
@@ -107,7 +122,7 @@ class _FlashAttention(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         q, k, v, out, lse2 = ctx.saved_tensors
-        lib = _native.lib("plx_attn")
+        lib = _lib()
         dout = dout.contiguous()
         B, H, S, D = q.shape
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)

@@ -94,3 +94,24 @@ def test_transformer_uses_hip_attention(cuda):
         losses.append(float(loss))
     assert losses[-1] < losses[0] * 0.7
     assert "plx_attn" in _native._loaded
+
+
+@pytest.mark.parametrize("waves", [4, 8])
+def test_flash_attention_forward_wave_counts(cuda, waves):
+    """Both forward workgroup shapes (4 waves / 128 queries, 8 waves / 256 queries) against fp32, causal and full,
+    with a sequence that leaves a ragged last query block and key tile."""
+    from polyaxon_amd.ops import attention
+
+    lib = attention._lib()
+    lib.plx_attn_set_fwd_waves(waves)
+    try:
+        torch.manual_seed(2)
+        for causal, D in ((True, 128), (False, 64), (True, 64)):
+            q = torch.randn(2, 4, 328, D, device=cuda).to(torch.bfloat16)
+            k = torch.randn(2, 2, 328, D, device=cuda).to(torch.bfloat16)
+            v = torch.randn(2, 2, 328, D, device=cuda).to(torch.bfloat16)
+            out = attention.flash_attention(q, k, v, causal=causal)
+            ref = _ref(q, k, v, causal, 1 / math.sqrt(D))
+            assert _rel(out, ref) < 1e-2, (waves, causal, D, _rel(out, ref))
+    finally:
+        lib.plx_attn_set_fwd_waves(8)
