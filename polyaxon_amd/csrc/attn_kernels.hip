@@ -305,15 +305,20 @@ __global__ __launch_bounds__(NT) void attn_bwd_delta_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------- backward: dQ
-template <int D>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
-  constexpr int TB = 64 * 2 * D, STAGE = 2 * TB, ND = D / 32, NS = D / 16;
+// NW waves x 32 queries per workgroup: the K / V tile in LDS serves NW * 32 query rows (see the forward)
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void attn_bwd_dq_kernel(AttnArgs a) {
+  constexpr int QB = 32 * NW, TB = 64 * 2 * D, STAGE = 2 * TB, ND = D / 32, NS = D / 16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, ql = lane & 31;
-  const QBlock blk = q_block<128>(a);
+  const QBlock blk = q_block<QB>(a);
   const int q0w = blk.q0 + 32 * wave, qi = q0w + ql, qc = min(qi, a.S - 1);
   const __bf16* K = a.k + blk.b * a.sk.b + blk.hk * a.sk.h;
   const __bf16* V = a.v + blk.b * a.sv.b + blk.hk * a.sv.h;
+  const int kv_end = a.causal ? min(a.Skv, blk.q0 + QB) : a.Skv;
+  const int nt = (kv_end + 63) / 64;
+  stage_tile<D, 64, NW>(smem, K, a.sk.s, a.Skv, a.zero, wave, lane);
+  stage_tile<D, 64, NW>(smem + TB, V, a.sv.s, a.Skv, a.zero, wave, lane);
   bf16x8 qf[NS], gf[NS];
   {
     const __bf16* qr = a.q + blk.b * a.sq.b + blk.hq * a.sq.h + (long long)qc * a.sq.s + 8 * h;
@@ -325,23 +330,18 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     }
   }
   const long long srow = ((long long)blk.b * a.H + blk.hq) * a.S + qc;
-  const float lse2 = a.lse2[srow], dlt = a.delta[srow];
+  const float lse2 = a.lse2[srow], dlt = a.delta[srow], c = a.c;
   f32x16 dq[ND];
 #pragma unroll
   for (int dt = 0; dt < ND; ++dt) dq[dt] = zero16();
-
-  const int kv_end = a.causal ? min(a.Skv, blk.q0 + 128) : a.Skv;
-  const int nt = (kv_end + 63) / 64;
-  stage_tile<D, 64>(smem, K, a.sk.s, a.Skv, a.zero, wave, lane);
-  stage_tile<D, 64>(smem + TB, V, a.sv.s, a.Skv, a.zero, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int j = 0; j < nt; ++j) {
     const int kv0 = j * 64;
     if (j + 1 < nt) {
       char* nb = smem + ((j + 1) & 1) * STAGE;
-      stage_tile<D, 64>(nb, K + (long long)(kv0 + 64) * a.sk.s, a.sk.s, a.Skv - kv0 - 64, a.zero, wave, lane);
-      stage_tile<D, 64>(nb + TB, V + (long long)(kv0 + 64) * a.sv.s, a.sv.s, a.Skv - kv0 - 64, a.zero, wave, lane);
+      stage_tile<D, 64, NW>(nb, K + (long long)(kv0 + 64) * a.sk.s, a.sk.s, a.Skv - kv0 - 64, a.zero, wave, lane);
+      stage_tile<D, 64, NW>(nb + TB, V + (long long)(kv0 + 64) * a.sv.s, a.sv.s, a.Skv - kv0 - 64, a.zero, wave, lane);
     }
     const char* Ks = smem + (j & 1) * STAGE;
     const char* Vs = Ks + TB;
@@ -359,7 +359,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = exp2f(st[t][r] * a.c - lse2);
+          float p = fast_exp2(fmaf(st[t][r], c, -lse2));
           if (mask) {
             const int key = kv0 + 32 * t + acc_row(r, h);
             if ((a.causal && key > qi) || key >= a.Skv || qi >= a.S) p = 0.f;
@@ -433,6 +433,14 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(AttnArgs a, float*
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int key = kw0 + kl;
+  // this wave's 32 keys are fixed for the whole sweep: their K / V row fragments live in registers (the one-wave-per-
+  // SIMD budget has the room), which takes 2 of the 4 ds_read_b128 streams out of every S / dP step
+  bf16x8 kf[NS], vf[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    kf[s] = row_frag<D>(Kimg, 32 * wave + kl, 2 * s + h);
+    vf[s] = row_frag<D>(Vimg, 32 * wave + kl, 2 * s + h);
+  }
   for (int it = 0; it < total; ++it) {
     if (it + 1 < total) stage_q((it + 1) & 1, it + 1);
     const char* Qs = qbase + (it & 1) * QSTAGE;
@@ -446,10 +454,8 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(AttnArgs a, float*
       f32x16 s_acc = zero16(), dp = zero16();
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        const bf16x8 kf = row_frag<D>(Kimg, 32 * wave + kl, 2 * s + h);
-        const bf16x8 vf = row_frag<D>(Vimg, 32 * wave + kl, 2 * s + h);
-        s_acc = mfma(row_frag<D>(Qs, 32 * sub + kl, 2 * s + h), kf, s_acc);  // S[q][key]
-        dp = mfma(row_frag<D>(Gs, 32 * sub + kl, 2 * s + h), vf, dp);         // dP[q][key]
+        s_acc = mfma(row_frag<D>(Qs, 32 * sub + kl, 2 * s + h), kf[s], s_acc);  // S[q][key]
+        dp = mfma(row_frag<D>(Gs, 32 * sub + kl, 2 * s + h), vf[s], dp);         // dP[q][key]
       }
       const bool mask = (a.causal && kw0 + 31 > q0) || q0 + 32 > a.S || kw0 + 32 > a.Skv;
 #pragma unroll
@@ -460,7 +466,7 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(AttnArgs a, float*
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * g + e;
-          float p = exp2f(s_acc[r] * a.c - lv[e]);
+          float p = fast_exp2(fmaf(s_acc[r], a.c, -lv[e]));
           if (mask) {
             const int q = q0 + 8 * g + 4 * h + e;
             if ((a.causal && key > q) || q >= a.S || key >= a.Skv) p = 0.f;
@@ -519,6 +525,148 @@ __global__ __launch_bounds__(NT, 1) void attn_bwd_dkdv_kernel(AttnArgs a, float*
         *(const uint4*)(dks + row * D + ch * 8);
     *(uint4*)(a.dv + b * a.sdv.b + hk * a.sdv.h + (long long)(k0 + row) * a.sdv.s + ch * 8) =
         *(const uint4*)(dvs + row * D + ch * 8);
+  }
+}
+
+// 8-wave form: one workgroup = 256 keys (32 per wave) x one query head, so every Q / dO tile staged into LDS feeds
+// 8 waves (half the LDS-DMA fill per FLOP of the 128-key form) at two waves per SIMD.  A wave's K / V row fragments
+// come straight from global memory into registers (they are fixed for the whole sweep), so LDS holds only the
+// double-buffered { Q tile [64][D] | dO tile [64][D] | lse2[64] | delta[64] } stages; the bf16 dK / dV rows (no GQA)
+// are staged through that region one tensor at a time.
+template <int D>
+__global__ __launch_bounds__(512, 1) void attn_bwd_dkdv8_kernel(AttnArgs a, float* __restrict__ ws) {
+  constexpr int NW = 8, KBLK = 32 * NW, QTB = 64 * 2 * D, QSTAGE = 2 * QTB + 512, ND = D / 32, NS = D / 16;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* Vimg = lds;                                    // [256][D] V rows of this key block
+  char* smem = lds + KBLK * 2 * D;                     // 2 Q / dO stages
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, kl = lane & 31;
+  const int nkb = (a.Skv + KBLK - 1) / KBLK;
+  const int bhn = a.B * a.H;
+  const int bid = blockIdx.x;
+  const int kb = bid / bhn, bh = bid % bhn;            // key block 0 (the longest causal query range) first
+  const int b = bh / a.H, hq = bh % a.H, G = a.H / a.Hkv, hk = hq / G;
+  const int k0 = kb * KBLK, kw0 = k0 + 32 * wave;
+  (void)nkb;
+  const __bf16* Qh = a.q + b * a.sq.b + hq * a.sq.h;
+  const __bf16* Gh = a.dout + b * a.sdo.b + hq * a.sdo.h;
+  const long long srow0 = ((long long)b * a.H + hq) * a.S;
+  const int qt0 = a.causal ? k0 / 64 : 0;
+  const int total = (a.S + 63) / 64 - qt0;
+  auto stage_q = [&](int buf, int it) {
+    const int q0 = (qt0 + it) * 64;
+    char* base = smem + buf * QSTAGE;
+    stage_tile<D, 64, NW>(base, Qh + (long long)q0 * a.sq.s, a.sq.s, a.S - q0, a.zero, wave, lane);
+    stage_tile<D, 64, NW>(base + QTB, Gh + (long long)q0 * a.sdo.s, a.sdo.s, a.S - q0, a.zero, wave, lane);
+    if (wave < 2) {  // lse2[64] | delta[64]: one 4-byte LDS-DMA per lane (rows past S: clamp, masked later)
+      const long long srow = srow0 + min(q0 + lane, a.S - 1);
+      const float* src = wave == 0 ? a.lse2 + srow : a.delta + srow;
+      __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)(base + 2 * QTB + 256 * wave), 4, 0, 0);
+    }
+  };
+  stage_tile<D, KBLK, NW>(Vimg, a.v + b * a.sv.b + hk * a.sv.h + (long long)k0 * a.sv.s, a.sv.s, a.Skv - k0, a.zero,
+                          wave, lane);
+  if (total > 0) stage_q(0, 0);
+  const int key = kw0 + kl;
+  bf16x8 kf[NS];
+  {
+    const int kr = min(key, a.Skv - 1);  // rows past Skv: any valid row, their scores are masked
+    const __bf16* kp = a.k + b * a.sk.b + hk * a.sk.h + (long long)kr * a.sk.s + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) kf[s] = *(const bf16x8*)(kp + 16 * s);
+  }
+  f32x16 dk[ND], dv[ND];
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt) {
+    dk[dt] = zero16();
+    dv[dt] = zero16();
+  }
+  const float c = a.c;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    if (it + 1 < total) stage_q((it + 1) & 1, it + 1);
+    const char* Qs = smem + (it & 1) * QSTAGE;
+    const char* Gs = Qs + QTB;
+    const float* st_lse = (const float*)(Qs + 2 * QTB);
+    const float* st_dlt = st_lse + 64;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int q0 = (qt0 + it) * 64 + 32 * sub;
+      if (a.causal && q0 + 31 < kw0) continue;  // wave-uniform: every query precedes this wave's keys
+      f32x16 s_acc = zero16(), dp = zero16();
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        s_acc = mfma(row_frag<D>(Qs, 32 * sub + kl, 2 * s + h), kf[s], s_acc);  // S[q][key]
+        dp = mfma(row_frag<D>(Gs, 32 * sub + kl, 2 * s + h), row_frag<D>(Vimg, 32 * wave + kl, 2 * s + h), dp);
+      }
+      const bool mask = (a.causal && kw0 + 31 > q0) || q0 + 32 > a.S || kw0 + 32 > a.Skv;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 l4 = *(const float4*)(st_lse + 32 * sub + 8 * g + 4 * h);
+        const float4 d4 = *(const float4*)(st_dlt + 32 * sub + 8 * g + 4 * h);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * g + e;
+          float p = fast_exp2(fmaf(s_acc[r], c, -lv[e]));
+          if (mask) {
+            const int q = q0 + 8 * g + 4 * h + e;
+            if ((a.causal && key > q) || q >= a.S || key >= a.Skv) p = 0.f;
+          }
+          s_acc[r] = p;
+          dp[r] = p * (dp[r] - dv4[e]);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pa = acc_frag(s_acc, s), da = acc_frag(dp, s);
+#pragma unroll
+        for (int dt = 0; dt < ND; ++dt) {
+          dv[dt] = mfma(pa, tr_frag<D>(Gs, 32 * sub + 16 * s, 32 * dt, lane), dv[dt]);
+          dk[dt] = mfma(da, tr_frag<D>(Qs, 32 * sub + 16 * s, 32 * dt, lane), dk[dt]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (G > 1) {
+    // fp32 partials of this query head: ws[{dk, dv}][b][hq][key][d]; rows = keys (registers), column = d (lane)
+    const long long plane = (long long)a.B * a.H * a.Skv * D;
+    float* wk = ws + (((long long)b * a.H + hq) * a.Skv) * D;
+    float* wv = wk + plane;
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kr = kw0 + acc_row(r, h);
+        if (kr < a.Skv) {
+          wk[(long long)kr * D + 32 * dt + kl] = dk[dt][r] * a.scale;
+          wv[(long long)kr * D + 32 * dt + kl] = dv[dt][r];
+        }
+      }
+    return;
+  }
+  // no GQA: stage [256][D] bf16 through the (now idle) Q/dO stage region, dK then dV, and write whole rows
+  __bf16* st = (__bf16*)smem;
+  constexpr int CH = D / 8;  // 16-B chunks per row
+#pragma unroll
+  for (int which = 0; which < 2; ++which) {
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = 32 * wave + acc_row(r, h), col = 32 * dt + kl;
+        st[row * D + col] = which == 0 ? (__bf16)(dk[dt][r] * a.scale) : (__bf16)dv[dt][r];
+      }
+    __syncthreads();
+    __bf16* dst = which == 0 ? a.dk + b * a.sdk.b + hk * a.sdk.h : a.dv + b * a.sdv.b + hk * a.sdv.h;
+    const long long ld = which == 0 ? a.sdk.s : a.sdv.s;
+    for (int i = threadIdx.x; i < KBLK * CH; i += 64 * NW) {
+      const int row = i / CH, ch = i % CH;
+      if (k0 + row < a.Skv) *(uint4*)(dst + (long long)(k0 + row) * ld + ch * 8) = *(const uint4*)(st + row * D + ch * 8);
+    }
+    __syncthreads();
   }
 }
 
@@ -582,6 +730,7 @@ int launch_fwd(const AttnArgs& a, hipStream_t stream) {
 }
 
 PLX_API void plx_attn_set_fwd_waves(int nw) { g_fwd_waves = nw == 4 ? 4 : 8; }
+PLX_API void plx_attn_set_dq_waves(int nw);
 
 PLX_API int plx_attn_fwd(const AttnArgs* args, int D, hipStream_t stream) {
   const AttnArgs& a = *args;
@@ -596,18 +745,29 @@ PLX_API long long plx_attn_bwd_workspace(int B, int H, int Hkv, int Skv, int D) 
   return H == Hkv ? 0 : 2LL * B * H * Skv * D * (long long)sizeof(float);
 }
 
+// dQ / dK-dV waves per workgroup (A/B knobs plx_attn_set_dq_waves / plx_attn_set_dkdv_waves: 4 or 8)
+int g_dq_waves = 8, g_dkdv_waves = 8;
+
 template <int D>
 int launch_bwd(const AttnArgs& a, float* ws, hipStream_t stream) {
   constexpr int QLDS = 4 * 64 * 2 * D, KLDS = 2 * 128 * 2 * D + 2 * (2 * 64 * 2 * D + 512);
-  static int once = prepare(attn_bwd_dq_kernel<D>, QLDS) | prepare(attn_bwd_dkdv_kernel<D>, KLDS);
+  constexpr int KLDS8 = 256 * 2 * D + 2 * (2 * 64 * 2 * D + 512);
+  static_assert(KLDS8 - 256 * 2 * D >= 256 * D * 2, "the dK / dV output staging must fit the stage region");
+  static int once = prepare(attn_bwd_dq_kernel<D, 4>, QLDS) | prepare(attn_bwd_dq_kernel<D, 8>, QLDS) |
+                    prepare(attn_bwd_dkdv_kernel<D>, KLDS) | prepare(attn_bwd_dkdv8_kernel<D>, KLDS8);
   if (once) return once;
   const long long rows = (long long)a.B * a.H * a.S;
-  const int qgrid = ((a.S + 127) / 128) * a.H * a.B;
+  const int qb = 32 * g_dq_waves;
+  const int qgrid = ((a.S + qb - 1) / qb) * a.H * a.B;
   const int kgrid = ((a.Skv + 127) / 128) * a.H * a.B;
   hipLaunchKernelGGL(attn_bwd_delta_kernel<D>, dim3((unsigned)((rows * (D / 8) + NT - 1) / NT)), dim3(NT), 0, stream,
                      a);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel<D>, dim3(qgrid), dim3(NT), QLDS, stream, a);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel<D>, dim3(kgrid), dim3(NT), KLDS, stream, a, ws);
+  if (g_dq_waves == 4) hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 4>), dim3(qgrid), dim3(256), QLDS, stream, a);
+  else hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 8>), dim3(qgrid), dim3(512), QLDS, stream, a);
+  if (g_dkdv_waves == 8)
+    hipLaunchKernelGGL(attn_bwd_dkdv8_kernel<D>, dim3(((a.Skv + 255) / 256) * a.H * a.B), dim3(512), KLDS8, stream, a,
+                       ws);
+  else hipLaunchKernelGGL(attn_bwd_dkdv_kernel<D>, dim3(kgrid), dim3(NT), KLDS, stream, a, ws);
   if (a.H != a.Hkv) {
     const long long n8 = (long long)a.B * a.Hkv * a.Skv * (D / 8);
     const int grid = (int)std::min<long long>((n8 + NT - 1) / NT, 2048);
@@ -615,6 +775,9 @@ int launch_bwd(const AttnArgs& a, float* ws, hipStream_t stream) {
   }
   return (int)hipGetLastError();
 }
+
+PLX_API void plx_attn_set_dq_waves(int nw) { g_dq_waves = nw == 4 ? 4 : 8; }
+PLX_API void plx_attn_set_dkdv_waves(int nw) { g_dkdv_waves = nw == 4 ? 4 : 8; }
 
 PLX_API int plx_attn_bwd(const AttnArgs* args, int D, float* ws, hipStream_t stream) {
   const AttnArgs& a = *args;

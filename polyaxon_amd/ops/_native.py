@@ -270,6 +270,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_attn_bwd_workspace": [_I, _I, _I, _I, _I],
         "plx_attn_args_size": [],
         "plx_attn_set_fwd_waves": [_I],
+        "plx_attn_set_dq_waves": [_I],
+        "plx_attn_set_dkdv_waves": [_I],
     },
     "plx_pool": {
         "plx_maxpool3s2_forward": [_P, _P, _P, _I, _I, _I, _I, _P],
@@ -300,7 +302,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_attn_set_fwd_waves": None, "plx_gemm256_set_split_target": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

@@ -92,13 +92,15 @@ _KNOBS_SET = False
 
 
 def _lib():
-    """The attention library with its A/B knobs applied once (PLX_ATTN_FWD_WAVES: 8 (default) or 4 waves per
-    forward workgroup)."""
+    """The attention library with its A/B knobs applied once (PLX_ATTN_FWD_WAVES / PLX_ATTN_DQ_WAVES /
+    PLX_ATTN_DKDV_WAVES: 8 (default) or 4 waves per forward / dQ / dK-dV workgroup)."""
     global _KNOBS_SET
     lib = _native.lib("plx_attn")
     if not _KNOBS_SET:
         _check(lib.plx_attn_args_size())
         lib.plx_attn_set_fwd_waves(int(os.environ.get("PLX_ATTN_FWD_WAVES", "8")))
+        lib.plx_attn_set_dq_waves(int(os.environ.get("PLX_ATTN_DQ_WAVES", "8")))
+        lib.plx_attn_set_dkdv_waves(int(os.environ.get("PLX_ATTN_DKDV_WAVES", "8")))
         _KNOBS_SET = True
     return lib
 

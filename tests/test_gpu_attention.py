@@ -115,3 +115,31 @@ def test_flash_attention_forward_wave_counts(cuda, waves):
             assert _rel(out, ref) < 1e-2, (waves, causal, D, _rel(out, ref))
     finally:
         lib.plx_attn_set_fwd_waves(8)
+
+
+@pytest.mark.parametrize("dq_waves,dkdv_waves", [(4, 4), (8, 8)])
+def test_flash_attention_backward_wave_counts(cuda, dq_waves, dkdv_waves):
+    """Both dQ and dK/dV workgroup shapes against the fp32 reference: GQA and plain heads, causal and full, a
+    sequence that leaves ragged key blocks (the 8-wave dK/dV block is 256 keys)."""
+    from polyaxon_amd.ops import attention
+
+    lib = attention._lib()
+    lib.plx_attn_set_dq_waves(dq_waves)
+    lib.plx_attn_set_dkdv_waves(dkdv_waves)
+    try:
+        torch.manual_seed(3)
+        for H, Hkv, causal, D in ((4, 2, True, 128), (4, 4, False, 64), (2, 2, True, 128)):
+            q = torch.randn(1, H, 328, D, device=cuda).to(torch.bfloat16).requires_grad_()
+            k = torch.randn(1, Hkv, 328, D, device=cuda).to(torch.bfloat16).requires_grad_()
+            v = torch.randn(1, Hkv, 328, D, device=cuda).to(torch.bfloat16).requires_grad_()
+            out = attention.flash_attention(q, k, v, causal=causal)
+            qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+            ref = _ref(qr, kr, vr, causal, 1 / math.sqrt(D))
+            g = torch.randn_like(ref)
+            out.backward(g.to(torch.bfloat16))
+            ref.backward(g)
+            for name, x, y in (("dq", q.grad, qr.grad), ("dk", k.grad, kr.grad), ("dv", v.grad, vr.grad)):
+                assert _rel(x, y) < 2e-2, (dq_waves, dkdv_waves, H, Hkv, causal, D, name, _rel(x, y))
+    finally:
+        lib.plx_attn_set_dq_waves(8)
+        lib.plx_attn_set_dkdv_waves(8)
