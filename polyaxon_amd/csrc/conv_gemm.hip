@@ -613,15 +613,30 @@ __device__ __forceinline__ void stage_rows(char* img, __amdgpu_buffer_rsrc_t rsr
     }
 }
 
+// vmcnt(n) with a run-time n in [0, 3 * step] in multiples of `step` (the counter is an instruction immediate)
+template <int STEP>
+__device__ __forceinline__ void wait_vm_stages(int stages) {
+    if (stages >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * STEP) : "memory");
+    else if (stages == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * STEP) : "memory");
+    else if (stages == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // CONV: 0 dense, 1 3x3 gather (tap per N2 tile), 2 the stem's super-pixel window (plx_stem_conv_wgrad)
-template <int BN1, int BN2, int WG1, int WG2, int CONV>
-__global__ void __launch_bounds__(NTHREADS, 2)
+// NST: K-stages in the LDS ring.  2 = double buffering (stage k+1 in flight while k computes, vmcnt(0) + barrier
+// per stage); 3-4 = a ring with NST-1 stages in flight behind a counted vmcnt.  A stage is 32 KB for a 128x128 tile
+// and takes longer to land by LDS-DMA (~1.5 us incl. latency) than its 32 MFMAs per wave take to run (~0.2 us),
+// so with one block per CU (the side-stream plan) the double-buffered loop mostly waited on its own fills.
+template <int BN1, int BN2, int WG1, int WG2, int CONV, int NST = 2>
+__global__ void __launch_bounds__(NTHREADS, NST == 2 ? 2 : 1)
 gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float* __restrict__ W,
                int M, int N1, int N2, int lda, int ldb, int kchunk, const __bf16* __restrict__ zero,
                ConvGeom geo) {
     constexpr int WT1 = BN1 / WG1, WT2 = BN2 / WG2, R1 = WT1 / 16, R2 = WT2 / 16;
     constexpr int ROWA = BN1 * 2, ROWB_ = BN2 * 2;
     constexpr int A_BYTES = BK * ROWA, STAGE = BK * (ROWA + ROWB_);
+    constexpr int PER_STAGE = (BK * ROWA / 1024 + BK * ROWB_ / 1024) / 4;  // LDS-DMA instructions per wave per stage
+    static_assert(NST >= 2 && NST <= 4, "2-4 stages");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -656,15 +671,30 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
         stage_rows<ROWA>(base, ra, lda, k0, kend, n10, wave, lane);
         stage_rows<ROWB_, CONV>(base + A_BYTES, rb, ldb, k0, kend, bc0, wave, lane, &geo, dh, dw);
     };
-    if (nk > 0) {
-        stage(0, kbeg);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
     const int gi = lane & 15, g = lane >> 4, q = gi >> 2, p = gi & 3;
+    if constexpr (NST == 2) {
+        if (nk > 0) {
+            stage(0, kbeg);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    } else {
+        for (int st = 0; st < NST - 1 && st < nk; ++st) stage(st, kbeg + st * BK);
+    }
     for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) stage(cur ^ 1, kbeg + (kt + 1) * BK);
+        int cur;
+        if constexpr (NST == 2) {
+            cur = kt & 1;
+            if (kt + 1 < nk) stage(cur ^ 1, kbeg + (kt + 1) * BK);
+        } else {
+            // stages kt+1 .. min(kt+NST-2, nk-1) may stay in flight; stage kt must have landed for every wave, and
+            // every wave is done with stage kt-1's buffer, which the fill of stage kt+NST-1 reuses
+            const int later = min(NST - 2, nk - 1 - kt);
+            wait_vm_stages<PER_STAGE>(later);
+            __syncthreads();
+            if (kt + NST - 1 < nk) stage((kt + NST - 1) % NST, kbeg + (kt + NST - 1) * BK);
+            cur = kt % NST;
+        }
         const char* As = smem + cur * STAGE;
         const char* Bs = As + A_BYTES;
 #pragma unroll
@@ -689,8 +719,10 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
                 for (int b = 0; b < R2; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if constexpr (NST == 2) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
     }
     // D[n1][n2]: lane holds column n2 = lane&15, rows n1 = 4*(lane>>4) + r
     float* slab = W + (size_t)slice * N1 * N2;
@@ -906,17 +938,34 @@ inline TnPlan tn_plan(int M, int N1, int N2, int num_cus, int bpc = 0) {
     return {kchunk, slices, groups, per_group, blocks};
 }
 
-template <int BN1, int BN2, int WG1, int WG2, int CONV = 0>
-int launch_tn(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
-              const void* zero, hipStream_t s, ConvGeom geo = {}) {
-    constexpr int LDS = 2 * BK * (BN1 + BN2) * 2;
-    auto k = gemm_tn_kernel<BN1, BN2, WG1, WG2, CONV>;
+// LDS ring depth of the weight-gradient GEMM (A/B knob plx_set_tn_stages: 2 = double buffering, 3 or 4).  Default 2:
+// in the training step the deeper rings measured slower (same box, 3-sweep bench: 2 stages 11.92k, 3 stages 11.60k,
+// 4 stages 11.36k trials/h) -- a 96-128 KB ring leaves no LDS on its CU for the data-gradient chain's blocks
+// (profiles/r3_negative_results.md)
+int g_tn_stages = 2;
+
+template <int BN1, int BN2, int WG1, int WG2, int CONV, int NST>
+int launch_tn_st(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
+                 const void* zero, hipStream_t s, const ConvGeom& geo) {
+    constexpr int LDS = NST * BK * (BN1 + BN2) * 2;
+    static_assert(LDS <= 160 * 1024, "LDS ring exceeds the CU's LDS");
+    auto k = gemm_tn_kernel<BN1, BN2, WG1, WG2, CONV, NST>;
     static int attr = set_lds(k, LDS);
     if (attr) return attr;
     const int ntiles = (N1 / BN1) * (N2 / BN2);
     hipLaunchKernelGGL(k, dim3(ntiles * plan.slices), dim3(NTHREADS), LDS, s, (const __bf16*)A, (const __bf16*)B, W,
                        M, N1, N2, lda, ldb, plan.kchunk, (const __bf16*)zero, geo);
     return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <int BN1, int BN2, int WG1, int WG2, int CONV = 0>
+int launch_tn(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
+              const void* zero, hipStream_t s, ConvGeom geo = {}) {
+    if (g_tn_stages >= 4)
+        return launch_tn_st<BN1, BN2, WG1, WG2, CONV, 4>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo);
+    if (g_tn_stages == 3)
+        return launch_tn_st<BN1, BN2, WG1, WG2, CONV, 3>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo);
+    return launch_tn_st<BN1, BN2, WG1, WG2, CONV, 2>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo);
 }
 
 }  // namespace
@@ -955,6 +1004,9 @@ void plx_set_nt_single_stage(int mode) { g_nt_single_stage = mode; }
 
 // A/B knob: halo mode for the stride-1 3x3 convolutions (1 on, 0 the per-tap gather)
 void plx_set_halo(int on) { g_halo = on ? 1 : 0; }
+
+// A/B knob: LDS ring depth of the weight-gradient GEMM (2, 3 or 4 stages)
+void plx_set_tn_stages(int n) { g_tn_stages = n < 2 ? 2 : (n > 4 ? 4 : n); }
 
 // weight-gradient slicing knobs; workspace sizes follow them, so set before sizing / launching
 void plx_set_tn_plan(int blocks_per_cu, int slab_mb) {
