@@ -71,7 +71,7 @@ def _args(argv=None):
     ap.add_argument("--signal", type=float, default=0.5, help="class-pattern amplitude of the synthetic data")
     ap.add_argument("--active-classes", type=int, default=100, help="classes the synthetic task draws from")
     ap.add_argument("--max-active", type=int, default=8, help="brackets one executor interleaves")
-    ap.add_argument("--graph", type=int, default=0,
+    ap.add_argument("--graph", type=int, default=int(os.environ.get("PLX_BENCH_GRAPH", "0")),
                     help="replay each training step as a captured (and verified) hipGraph; measured 8 %% slower than eager "
                          "launches for this step on ROCm 7.2 (10.5k vs 11.4k trials/h, same box)")
     ap.add_argument("--cpu", action="store_true", help="CPU rehearsal (gloo, small ResNet, tiny images)")
