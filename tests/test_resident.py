@@ -482,3 +482,28 @@ def test_bench_cpu_single_rank_control_process_and_asha():
     assert res["n_gpus"] == 1 and res["control_pid"] != res["per_rank"][0]["pid"]
     assert res["config"]["search"].startswith("asha") and res["trials_succeeded"] == res["trials"]
     assert res["trials"] > 12 and res["trials_resumed"] > 0  # promotions happened and resumed
+
+
+def test_bench_cpu_under_torchrun_like_the_driver():
+    """The driver's multi-GPU launch, rehearsed on CPU: ``python -m torch.distributed.run --nproc-per-node 2
+    --master-addr 127.0.0.1 bench.py --gpus 2``; rank 0 prints the one JSON line with the whole-job value."""
+    import json
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "PLX_BENCH_CONTROL"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                         capture_output=True, text=True, timeout=600, env=env, cwd="/tmp")
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 1 and res["warmup"] == 0
+    assert res["trials"] == 46 and res["trials_succeeded"] == 46 and res["store_fsm_history_ok"] is True
+    assert res["value"] > 0 and res["higher_is_better"] is True and res["scaling"] == "weak"
