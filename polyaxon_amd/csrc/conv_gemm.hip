@@ -548,12 +548,37 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         }
         __syncthreads();                                    // red is reused by the next reduction
     };
-    if (bnr_on)
-        reduce_store(sa, sb, bnr.part + (size_t)(bnr.blk_off + tm) * ldc + n0,
-                     bnr.part + (size_t)(bnr.part_ld + bnr.blk_off + tm) * ldc + n0);
-    // per-channel partial sum / sum of squares -> stats[0][tm][n], stats[1][tm][n] (the BatchNorm that consumes
+    // Partial rows are in units of SROWS pixel rows (plx_gemm_nt_rows_per_block(N): 128 for N % 128 == 0, else 256)
+    // whatever the tile height, so the host sizes them without knowing the tile; a taller block writes its partial
+    // into its first row and zeros into the others.
+    constexpr int SROWS = BN % 128 == 0 ? 128 : 256, SPB = BM / SROWS;
+    static_assert(SPB >= 1 && BM % SROWS == 0, "block height must be a multiple of the stats row height");
+    const int srow = m0 / SROWS, nsr = (M + SROWS - 1) / SROWS;
+    auto zero_rows = [&](float* base_a, float* base_b, int ld) {  // rows srow+1 .. srow+SPB-1 (those < nsr)
+        if constexpr (SPB > 1) {
+            for (int i = tid; i < (SPB - 1) * BN; i += NTHREADS) {
+                const int r = srow + 1 + i / BN, c = i % BN;
+                if (r < nsr) {
+                    base_a[(size_t)(r - srow) * ld + c] = 0.f;
+                    base_b[(size_t)(r - srow) * ld + c] = 0.f;
+                }
+            }
+        }
+    };
+    if (bnr_on) {
+        float* pa = bnr.part + (size_t)(bnr.blk_off + srow) * ldc + n0;
+        float* pb = bnr.part + (size_t)(bnr.part_ld + bnr.blk_off + srow) * ldc + n0;
+        reduce_store(sa, sb, pa, pb);
+        zero_rows(pa, pb, ldc);
+    }
+    // per-channel partial sum / sum of squares -> stats[0][srow][n], stats[1][srow][n] (the BatchNorm that consumes
     // this conv skips its stats pass)
-    if (stats_on) reduce_store(s1, s2, stats + (size_t)tm * N + n0, stats + (size_t)(ntm + tm) * N + n0);
+    if (stats_on) {
+        float* pa = stats + (size_t)srow * N + n0;
+        float* pb = stats + (size_t)(nsr + srow) * N + n0;
+        reduce_store(s1, s2, pa, pb);
+        zero_rows(pa, pb, N);
+    }
 }
 
 // ------------------------------------------------------------------------------------------- TN GEMM
@@ -875,6 +900,18 @@ inline bool halo_ok(const ConvGeom& g) {
 // (plain GEMMs), 2 every plain GEMM, 3 every GEMM, 4 forward-epilogue GEMMs by the rule, 5 (default) the rule.
 int g_nt_single_stage = 5;
 
+// Tall tiles (A/B knob plx_set_nt_tall): 256 pixel rows x 128 channels per block (4 waves of 128 x 64) instead of
+// 128 x 128 for N % 128 == 0 -- 85 instead of 64 FLOP per staged byte and a quarter fewer LDS fragment reads per MFMA,
+// for the compute-bound GEMMs (reduction depth K >= g_nt_tall_k: the 3x3 layers and the wide 1x1s; the HBM-bound
+// shallow ones lose the 4-blocks-per-CU latency hiding).  0 off, 1 forward GEMMs, 2 forward and data-gradient GEMMs;
+// only when the grid still fills the CUs.
+int g_nt_tall = 0, g_nt_tall_k = 1024;
+
+inline bool nt_tall(bool bwd, int M, int N, int K) {
+    if (g_nt_tall == 0 || N % 128 || K < g_nt_tall_k || (bwd && g_nt_tall < 2)) return false;
+    return ((M + 255) / 256) * (N / 128) >= 256;
+}
+
 inline bool nt_single(bool bwd, bool conv, int K, int nwg) {
     switch (g_nt_single_stage) {
         case 0: return false;
@@ -988,6 +1025,8 @@ int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int 
     const BnBwd b = bnr != nullptr ? *bnr : BnBwd{};
     hipStream_t s = (hipStream_t)stream;
     const bool bwd = D != nullptr || bnr != nullptr;
+    if (nt_tall(bwd, M, N, K))
+        return launch_nt<256, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
     if (N % 128 == 0) {
         const bool one = nt_single(bwd, false, K, ((M + 127) / 128) * (N / 128));
         return one ? launch_nt<128, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b,
@@ -1004,6 +1043,12 @@ void plx_set_nt_single_stage(int mode) { g_nt_single_stage = mode; }
 
 // A/B knob: halo mode for the stride-1 3x3 convolutions (1 on, 0 the per-tap gather)
 void plx_set_halo(int on) { g_halo = on ? 1 : 0; }
+
+// A/B knob: 256 x 128 NT tiles (0 off, 1 forward, 2 forward + data gradient), see nt_tall
+void plx_set_nt_tall(int mode, int min_k) {
+    g_nt_tall = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
+    if (min_k > 0) g_nt_tall_k = min_k;
+}
 
 // A/B knob: LDS ring depth of the weight-gradient GEMM (2, 3 or 4 stages)
 void plx_set_tn_stages(int n) { g_tn_stages = n < 2 ? 2 : (n > 4 ? 4 : n); }
@@ -1165,6 +1210,7 @@ int nt_conv_any(const void* A, const void* B, void* C, int M, int N, const ConvG
             return launch_halo<128, 128, 2, 2, 2>(A, B, C, M, N, g.C, ldb, ldc, zero, stats, s, g, D, ldd, bnr);
         return launch_halo<256, 64, 4, 1, 2>(A, B, C, M, N, g.C, ldb, ldc, zero, stats, s, g, D, ldd, bnr);
     }
+    if (nt_tall(bwd, M, N, K)) return nt_conv<256, 128, 2, 2, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
     if (N % 128 == 0)
         return nt_single(bwd, true, K, ((M + 127) / 128) * (N / 128))
                    ? nt_conv<128, 128, 2, 2, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr)

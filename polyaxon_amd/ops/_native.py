@@ -159,6 +159,8 @@ def lib(name: str) -> ctypes.CDLL:
             handle.plx_set_halo(int(os.environ["PLX_HALO"]))
         if name == "plx_conv" and os.environ.get("PLX_TN_STAGES"):  # A/B knob: weight-gradient LDS ring depth
             handle.plx_set_tn_stages(int(os.environ["PLX_TN_STAGES"]))
+        if name == "plx_conv" and os.environ.get("PLX_NT_TALL"):  # A/B knob: 256x128 NT tiles (0 / 1 fwd / 2 +dgrad)
+            handle.plx_set_nt_tall(int(os.environ["PLX_NT_TALL"]), int(os.environ.get("PLX_NT_TALL_K", "0")))
         if name == "plx_gemm" and os.environ.get("PLX_GEMM_SPLIT_TARGET"):  # A/B knob: split-K planner target
             handle.plx_gemm256_set_split_target(int(os.environ["PLX_GEMM_SPLIT_TARGET"]))
         if name == "plx_conv" and os.environ.get("PLX_TN_PLAN"):  # A/B knob: "blocks_per_cu,slab_mb"
@@ -239,6 +241,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_set_nt_single_stage": [_I],
         "plx_set_halo": [_I],
         "plx_set_tn_stages": [_I],
+        "plx_set_nt_tall": [_I, _I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
         "plx_weight_prepk": [_P, _L, _L, _L, _L, _P, _P, _I, _I, _I, _P],
@@ -305,7 +308,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_stages": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

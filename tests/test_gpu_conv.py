@@ -435,3 +435,39 @@ def test_conv3x3_halo_matches_gather_and_fp32(cuda, shape, cout):
     # same bf16 rounding points, different fp32 summation order: tight agreement between the two native paths
     torch.testing.assert_close(out[1][0], out[0][0], rtol=1e-2, atol=2e-2)
     torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-2, atol=2e-2)
+
+
+def test_tall_nt_tiles_match_default_tiles(cuda):
+    """256x128 NT tiles (plx_set_nt_tall 2: forward and data gradient) against the default 128x128 tiles and fp32: the
+    plain GEMM with channel stats (partial rows stay in 128-row units: the tall block zero-fills its second row), a
+    3x3 convolution forward, and a conv -> BN chain whose BN-backward partials come from the dgrad epilogue."""
+    from polyaxon_amd.ops import _native
+    from polyaxon_amd.ops.conv import ConvKxK
+    from polyaxon_amd.ops.conv1x1 import gemm_nt, nt_stats_rows
+
+    lib = _native.lib("plx_conv")
+    torch.manual_seed(11)
+    m, n, k = 256 * 600 + 77, 128, 192  # >= 512 tall blocks, ragged last block
+    a, b = _bf(m, k, dev=cuda), _bf(n, k, dev=cuda)
+    rows = nt_stats_rows(n)
+    nblk = -(-m // rows)
+    res = {}
+    try:
+        for tall in (0, 2):
+            lib.plx_set_nt_tall(tall, 64)
+            stats = torch.full((2 * nblk * n,), float("nan"), device=cuda)
+            out = gemm_nt(a, b, stats=stats)
+            st = stats.view(2, nblk, n).sum(1)
+            # 32 x 64 x 64 pixels = 512 tall blocks: the 3x3 forward and its data gradient both take the tall tile
+            res[tall] = (out.float(), st, _bn_chain_grads(cuda, lambda: ConvKxK(128, 128, 3, 1), (32, 128, 64, 64),
+                                                          link=True))
+    finally:
+        lib.plx_set_nt_tall(0, 1024)
+    ref = a.float() @ b.float().t()
+    torch.testing.assert_close(res[2][0], ref, rtol=2e-2, atol=2e-2 * k ** 0.5)
+    torch.testing.assert_close(res[2][0], res[0][0], rtol=0, atol=0)  # same MFMA order per output element
+    o = res[2][0]
+    torch.testing.assert_close(res[2][1][0], o.sum(0), rtol=1e-4, atol=1e-1)
+    torch.testing.assert_close(res[2][1][1], o.square().sum(0), rtol=1e-4, atol=1e0)
+    for x2, x0, name in zip(res[2][2], res[0][2], ("dx", "dgamma", "dbeta", "dw")):
+        torch.testing.assert_close(x2, x0, rtol=1e-2, atol=1e-2 * float(x0.abs().max()), msg=name)
