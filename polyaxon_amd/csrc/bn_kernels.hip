@@ -859,10 +859,12 @@ __global__ __launch_bounds__(256) void stem_pool_bn_bwd_kernel(const bf16x8* __r
   }
 }
 
-// over quad rows: pass 1 (partials) a few per block (rows_y <= 4096 keeps the level-1 partials ~8 MB at the stem's
-// shape), pass 2 (dx) one per block
+// over quad rows: pass 1 (partials) a few per block (rows_y <= g_stem_bwd_cap bounds the level-1 partials: 4096 rows
+// ~4 MB at the stem's shape), pass 2 (dx) one per block.  A/B knob plx_set_stem_bwd_cap.
+int g_stem_bwd_cap = 4096;
+
 inline dim3 stem_bwd_grid(int N, int H, int W, int G, bool dx) {
-  const int rows = N * ((H + 1) / 2), cap = dx ? 65535 : 4096;
+  const int rows = N * ((H + 1) / 2), cap = dx ? 65535 : g_stem_bwd_cap;
   return dim3((((W + 1) / 2) * G + 255) / 256, rows < cap ? rows : cap);
 }
 
@@ -1009,6 +1011,9 @@ PLX_API int plx_stem_bn_pool_forward(const void* x, void* y, void* idx, int N, i
                      stream, (const bf16x8*)x, scale_bias, (bf16x8*)y, (u8x8*)idx, N, H, W, G, OH, OW);
   return (int)hipGetLastError();
 }
+
+// A/B knob: quad rows of the stem backward's partials pass (1 .. 65535; set before sizing the workspace)
+PLX_API void plx_set_stem_bwd_cap(int cap) { g_stem_bwd_cap = cap < 1 ? 1 : (cap > 65535 ? 65535 : cap); }
 
 // floats of workspace plx_stem_bn_pool_backward needs: level-1 [2][nblk][C] + level-2 [2][S][C]
 PLX_API int64_t plx_stem_bn_pool_bwd_workspace(int N, int H, int W, int C) {

@@ -26,12 +26,18 @@ namespace {
 
 constexpr int kBlock = 256;
 
-inline int grid_for(int64_t n_vec) {
+inline int grid_for(int64_t n_vec, int cap = 2048) {
   int64_t g = (n_vec + kBlock - 1) / kBlock;
-  if (g > 2048) g = 2048;
+  if (g > cap) g = cap;
   if (g < 1) g = 1;
   return (int)g;
 }
+
+// Block cap of the AdamW launches (A/B knob plx_set_adamw_grid_cap, PLX_OPT_BWD_GRID for the update inside the
+// backward, parallel/ddp.py FlatDDP(optimizer=...)).  That update is HBM-bound like the backward's elementwise
+// kernels: with the full grid those ran 2-40x slower beside it; capped at 32 / 64 / 128 / 256 blocks the update
+// outlasted the backward (Llama-3 8B 13.4k / 16.1k / 17.5k / 17.8k vs 17.8k tokens/s without it, same box).
+int g_adamw_grid_cap = 2048;
 
 // ---------------------------------------------------------------- SGD
 // hp layout (fp32, device): [0] lr, [1] momentum, [2] weight_decay, [3] nesterov (0/1), [4] dampening
@@ -329,16 +335,18 @@ PLX_API int plx_adamw_flat(float* p, float* g, float* m, float* v, int64_t n, in
                            const int* step, hipStream_t stream) {
   if ((n & 3) || (n_decay & 3)) return 1;
   const int64_t nv = n >> 2;
-  hipLaunchKernelGGL(adamw_flat_kernel, dim3(grid_for(nv)), dim3(kBlock), 0, stream, (float4*)p, (float4*)g,
+  hipLaunchKernelGGL(adamw_flat_kernel, dim3(grid_for(nv, g_adamw_grid_cap)), dim3(kBlock), 0, stream, (float4*)p, (float4*)g,
                      (float4*)m, (float4*)v, nv, n_decay >> 2, hp, step);
   return (int)hipGetLastError();
 }
+
+PLX_API void plx_set_adamw_grid_cap(int blocks) { g_adamw_grid_cap = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks); }
 
 PLX_API int plx_adamw_mixed(float* p, void* g, float* m, float* v, void* plp, int64_t n, int decay_on,
                             const float* hp, const int* step, hipStream_t stream) {
   if (n & 3) return 1;
   const int64_t nv = n >> 2;
-  hipLaunchKernelGGL(adamw_mixed_kernel, dim3(grid_for(nv)), dim3(kBlock), 0, stream, (float4*)p, (u16x4*)g,
+  hipLaunchKernelGGL(adamw_mixed_kernel, dim3(grid_for(nv, g_adamw_grid_cap)), dim3(kBlock), 0, stream, (float4*)p, (u16x4*)g,
                      (float4*)m, (float4*)v, (u16x4*)plp, nv, decay_on, hp, step);
   return (int)hipGetLastError();
 }

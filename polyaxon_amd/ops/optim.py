@@ -146,9 +146,15 @@ class FusedAdamW:
         self.exp_avg.zero_()
         self.exp_avg_sq.zero_()
 
+    # set by FlatDDP(optimizer=...): the update runs per gradient bucket during the backward (step_range_), and
+    # step_() only closes the step's bookkeeping
+    in_backward = False
+
     def step_(self) -> None:
         f = self.flat
         f.grads_consumed()  # every kernel below zeroes the gradients it reads
+        if self.in_backward:
+            return  # every bucket was already updated (FlatDDP.finish joined the optimizer stream)
         if not f.params.is_cuda:
             self._step_reference()
             return
@@ -173,9 +179,39 @@ class FusedAdamW:
                 self.exp_avg_sq.data_ptr() + off, f.numel - nd, 0, self.hp.data_ptr(), self.step.data_ptr(), st),
                 "plx_adamw_flat")
 
-    @torch.no_grad()
-    def _step_reference(self) -> None:
+    def step_range_(self, lo: int, hi: int, stream: Optional[int] = None) -> None:
+        """AdamW over flat elements [lo, hi) on ``stream`` (a FlatDDP bucket: 4-aligned, and in lp mode entirely
+        inside the bf16 decay segment or entirely inside the fp32 tail).  The same per-element update as
+        :meth:`step_`; weight decay applies to the elements below ``n_decay``; the range's gradients are zeroed."""
         f = self.flat
+        if not f.params.is_cuda:
+            self._step_reference(lo, hi)
+            return
+        lib = _native.lib("plx_train")
+        st = stream if stream is not None else _stream_ptr(f.params)
+        nd, n = f.n_decay, hi - lo
+        p, m, v = f.params.data_ptr() + 4 * lo, self.exp_avg.data_ptr() + 4 * lo, self.exp_avg_sq.data_ptr() + 4 * lo
+        if f.lp_params is None:
+            rc = lib.plx_adamw_flat(p, f.grads.data_ptr() + 4 * lo, m, v, n, max(0, min(hi, nd) - lo),
+                                    self.hp.data_ptr(), self.step.data_ptr(), st)
+            _native.check(rc, "plx_adamw_flat")
+        elif hi <= nd:
+            rc = lib.plx_adamw_mixed(p, f.lp_grads.data_ptr() + 2 * lo, m, v, f.lp_params.data_ptr() + 2 * lo, n, 1,
+                                     self.hp.data_ptr(), self.step.data_ptr(), st)
+            _native.check(rc, "plx_adamw_mixed")
+        elif lo >= nd:
+            rc = lib.plx_adamw_flat(p, f.grads.data_ptr() + 4 * (lo - nd), m, v, n, 0, self.hp.data_ptr(),
+                                    self.step.data_ptr(), st)
+            _native.check(rc, "plx_adamw_flat")
+        else:
+            raise ValueError(f"range [{lo}, {hi}) straddles the bf16/fp32 boundary at {nd}")
+
+    @torch.no_grad()
+    def _step_reference(self, lo: int = 0, hi: Optional[int] = None) -> None:
+        f = self.flat
+        if lo != 0 or (hi is not None and hi != f.numel):
+            self._step_reference_range(lo, f.numel if hi is None else hi)
+            return
         lr, b1, b2, eps, wd = (float(self.hp[i]) for i in range(5))
         t = int(self.step.item()) + 1
         g = f.grads if f.lp_grads is None else torch.cat([f.lp_grads.float(), f.grads])
@@ -187,6 +223,28 @@ class FusedAdamW:
         f.params.addcdiv_(self.exp_avg, denom, value=-lr / bc1)
         f.zero_grads()
         f.sync_lp()
+
+    @torch.no_grad()
+    def _step_reference_range(self, lo: int, hi: int) -> None:
+        """The reference update restricted to [lo, hi) (CPU).  It runs inside the backward (FlatDDP optimizer mode),
+        so it writes through ``.data``: the parameters are views of the flat buffers and share their autograd version
+        counter, which an in-place op on any slice would bump under the tensors other layers saved for backward (the
+        native kernels write through pointers and never touch it)."""
+        f = self.flat
+        lr, b1, b2, eps, wd = (float(self.hp[i]) for i in range(5))
+        t = int(self.step.item()) + 1
+        g = f.grad_view(lo, hi).data
+        p, m, v = f.params.data[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi]
+        nd = max(0, min(hi, f.n_decay) - lo)
+        if nd:
+            p[:nd].mul_(1.0 - lr * wd)
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1, bc2 = 1 - b1 ** t, 1 - b2 ** t
+        p.addcdiv_(m, (v.sqrt() / bc2 ** 0.5).add_(eps), value=-lr / bc1)
+        g.zero_()
+        if f.lp_params is not None and hi <= f.n_decay:
+            f.lp_params.data[lo:hi].copy_(p)
 
     def state_buffers(self) -> Dict[str, torch.Tensor]:
         return {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}

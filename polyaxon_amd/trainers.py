@@ -203,7 +203,12 @@ def train_lm(argv=None) -> float:
         flat.enable_direct_grads(True)  # weight-gradient GEMMs write into the flat bf16 grads (ops/lm.py)
     step = torch.zeros(1, dtype=torch.int32, device=dev)
     opt = FusedAdamW(flat, lr=args.lr, betas=(0.9, args.beta2), weight_decay=args.weight_decay, step_counter=step)
-    ddp = FlatDDP(flat, bucket_mb=args.bucket_mb)
+    # PLX_OPT_IN_BACKWARD=1: the AdamW update of each gradient bucket runs inside the backward as the bucket completes
+    # (parallel/ddp.py).  Off by default: bitwise the same trajectory, but on one MI355X the HBM-bound update only
+    # moved time from itself to the backward's memory-bound kernels (Llama-3 8B 18.17k vs 18.03k tokens/s with a
+    # full-chip grid, slower with a capped one; profiles/r3_negative_results.md)
+    in_bwd = dev.type == "cuda" and os.environ.get("PLX_OPT_IN_BACKWARD", "0") == "1"
+    ddp = FlatDDP(flat, bucket_mb=args.bucket_mb, optimizer=opt if in_bwd else None)
     ddp.broadcast_params()
     metrics = MetricReducer(dev)  # cross-rank mean of the logged loss (RCCL communicator on the GPU)
     g = torch.Generator(device=dev).manual_seed(args.seed + 1000 * info["rank"])

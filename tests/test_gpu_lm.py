@@ -85,3 +85,43 @@ def test_lp_model_matches_fp32_model(cuda):
         a = g32[seg.offset: seg.offset + seg.numel]
         b = glp[seg.offset: seg.offset + seg.numel]
         assert float(b.norm()) > 0 and abs(float(a.norm()) - float(b.norm())) <= 0.1 * float(a.norm()) + 1e-4, seg.name
+
+
+@pytest.mark.parametrize("arch", ["llama", "gpt2"])
+def test_optimizer_in_backward_matches_monolithic_step_on_gpu(cuda, arch):
+    """FlatDDP(optimizer=...) on the GPU: per-bucket plx_adamw_mixed / plx_adamw_flat launches on the optimizer
+    stream during the backward (lp mode: bf16 weights, fp32 master) give bitwise the trajectory of one update pass
+    after the backward, and the main stream sees the updated bf16 weights in the next forward."""
+    from polyaxon_amd.models.transformer import Transformer, gpt2_125m, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.ops.optim import FusedAdamW
+    from polyaxon_amd.parallel.ddp import FlatDDP
+
+    res = {}
+    for in_bwd in (False, True):
+        torch.manual_seed(0)
+        cfg = (tiny_llama(d_model=256, n_heads=2, n_kv_heads=1, max_seq_len=128) if arch == "llama" else
+               gpt2_125m(vocab_size=256, n_layers=2, d_model=256, n_heads=2, d_ff=1024, max_seq_len=128))
+        with torch.device(cuda):
+            model = Transformer(cfg)  # gpt2: tied embeddings, learned positions, LayerNorm, GELU, biases
+        flat = FlatParams(model, cuda, channels_last=False, lp_dtype=torch.bfloat16)
+        flat.enable_direct_grads(True)
+        opt = FusedAdamW(flat, lr=3e-3, weight_decay=0.1)
+        ddp = FlatDDP(flat, bucket_mb=0.05, optimizer=opt if in_bwd else None)
+        gen = torch.Generator(device=cuda).manual_seed(9)
+        losses = []
+        for _ in range(4):
+            tok = torch.randint(0, 256, (2, 128), device=cuda, generator=gen)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = lm_loss(model(tok), tok)
+            loss.backward()
+            ddp.finish()
+            opt.step_()
+            opt.step += 1
+            losses.append(float(loss))
+        torch.cuda.synchronize()
+        res[in_bwd] = (losses, flat.params.clone(), flat.lp_params.clone(), ddp)
+    assert res[False][0] == res[True][0]
+    assert torch.equal(res[False][1], res[True][1]) and torch.equal(res[False][2], res[True][2])
+    d = res[True][3]
+    assert len(d.buckets) > 3 and d.stepped == 4 * len(d.buckets)

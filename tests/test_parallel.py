@@ -253,3 +253,95 @@ def test_direct_grad_linear_matches_autograd():
             torch.testing.assert_close(flat.lp_grads.float() * 2, grads[True][0], rtol=0.02, atol=2e-3)
     torch.testing.assert_close(grads[True][0], grads[False][0], rtol=0.02, atol=2e-3)
     torch.testing.assert_close(grads[True][1], grads[False][1], rtol=1e-3, atol=1e-5)
+
+
+def _train_steps(lp, in_backward, steps=3, bucket_mb=0.01):
+    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.ops.optim import FusedAdamW
+    from polyaxon_amd.parallel.ddp import FlatDDP
+
+    torch.manual_seed(0)
+    model = Transformer(tiny_llama())
+    flat = FlatParams(model, "cpu", channels_last=False, lp_dtype=lp)
+    opt = FusedAdamW(flat, lr=1e-2, weight_decay=0.1)
+    ddp = FlatDDP(flat, bucket_mb=bucket_mb, optimizer=opt if in_backward else None)
+    gen = torch.Generator().manual_seed(5)
+    losses = []
+    for _ in range(steps):
+        tokens = torch.randint(0, 256, (4, 16), generator=gen)
+        loss = lm_loss(model(tokens), tokens)
+        loss.backward()
+        ddp.finish()
+        opt.step_()
+        opt.step += 1
+        losses.append(float(loss))
+    return losses, flat, ddp
+
+
+@pytest.mark.parametrize("lp", [None, torch.bfloat16])
+def test_optimizer_in_backward_matches_monolithic_step(lp):
+    """FlatDDP(optimizer=...): AdamW runs per gradient bucket as each bucket completes in the backward; the
+    trajectory (losses, fp32 master, bf16 model copy, moments) is bitwise the monolithic step's, every bucket is
+    updated exactly once per step, and the gradients are left zeroed."""
+    la, fa, _ = _train_steps(lp, False)
+    lb, fb, ddp = _train_steps(lp, True)
+    assert la == lb
+    assert torch.equal(fa.params, fb.params)
+    if lp is not None:
+        assert torch.equal(fa.lp_params, fb.lp_params)
+        assert float(fb.lp_grads.abs().max()) == 0.0
+    assert float(fb.grads.abs().max()) == 0.0
+    assert len(ddp.buckets) > 3 and ddp.stepped == 3 * len(ddp.buckets)
+
+
+def _opt_in_bwd_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.ops.optim import FusedAdamW
+    from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
+
+    init_from_env("gloo")
+    out = {}
+    for in_bwd in (False, True):
+        torch.manual_seed(0)
+        model = Transformer(tiny_llama())
+        flat = FlatParams(model, "cpu", channels_last=False)
+        opt = FusedAdamW(flat, lr=1e-2, weight_decay=0.1)
+        ddp = FlatDDP(flat, bucket_mb=0.01, optimizer=opt if in_bwd else None)
+        ddp.broadcast_params()
+        gen = torch.Generator().manual_seed(100 + rank)  # different data per rank
+        for _ in range(2):
+            loss = lm_loss(model(torch.randint(0, 256, (4, 16), generator=gen)), torch.randint(0, 256, (4, 16),
+                                                                                                generator=gen))
+            loss.backward()
+            ddp.finish()
+            opt.step_()
+            opt.step += 1
+        p = flat.params.clone()
+        gathered = [torch.zeros_like(p) for _ in range(world)]
+        dist.all_gather(gathered, p)
+        out[in_bwd] = (p, all(torch.equal(gathered[0], x) for x in gathered))
+        ddp.remove_hooks()
+    q.put((rank, out[True][1], out[False][1], bool(torch.allclose(out[True][0], out[False][0], rtol=0, atol=1e-6))))
+    dist.destroy_process_group()
+
+
+def test_optimizer_in_backward_gloo_world2():
+    """DP world 2: each bucket's update waits for its all-reduce; the ranks stay identical and match the
+    all-reduce-then-step path."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_opt_in_bwd_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(r[1] and r[2] and r[3] for r in res), res
