@@ -605,13 +605,14 @@ __device__ __forceinline__ s16x4 tr_read(const char* img, int row, int col /* el
 
 // GATHER: 0 dense rows, 1 the pixel shifted by (dh, dw) (3x3 weight gradient), 2 the stem's packed super-pixel
 // window: chunk k / 8 of row (n, r, c) is super-pixel (2r - 3 + t / 4, c - 2 + t % 4), t = k / 8 (plx_stem_conv_fwd)
-template <int ROWB, int GATHER = 0>
+template <int ROWB, int GATHER = 0, int BKR = BK>
 __device__ __forceinline__ void stage_rows(char* img, __amdgpu_buffer_rsrc_t rsrc, int ld, int r0, int rend, int c0,
                                            int wave, int lane, const ConvGeom* geo = nullptr, int dh = 0, int dw = 0) {
-    // BK rows x ROWB bytes, lane-linear image; 1024 B per wave instruction, through buffer-resource LDS-DMA (rows
+    // BKR rows x ROWB bytes, lane-linear image; 1024 B per wave instruction, through buffer-resource LDS-DMA (rows
     // past rend and gathered pixels outside the image get an out-of-range offset: zeros).  GATHER: row gr is the
     // pixel shifted by (dh, dw), for the weight gradient of a 3x3 convolution.
-    constexpr int INSTR = BK * ROWB / 1024;
+    constexpr int INSTR = BKR * ROWB / 1024;
+    static_assert(INSTR % 4 == 0, "a stage splits evenly over the 4 waves");
 #pragma unroll
     for (int i = 0; i < INSTR / 4; ++i) {
         const int off = (i * 4 + wave) * 1024 + lane * 16;
@@ -652,15 +653,17 @@ __device__ __forceinline__ void wait_vm_stages(int stages) {
 // per stage); 3-4 = a ring with NST-1 stages in flight behind a counted vmcnt.  A stage is 32 KB for a 128x128 tile
 // and takes longer to land by LDS-DMA (~1.5 us incl. latency) than its 32 MFMAs per wave take to run (~0.2 us),
 // so with one block per CU (the side-stream plan) the double-buffered loop mostly waited on its own fills.
-template <int BN1, int BN2, int WG1, int WG2, int CONV, int NST = 2>
-__global__ void __launch_bounds__(NTHREADS, NST == 2 ? 2 : 1)
+// BKT: reduction rows per stage (64, or 32: half-size stages, so a 4-deep ring fits the double buffer's 64 KB)
+template <int BN1, int BN2, int WG1, int WG2, int CONV, int NST = 2, int BKT = BK>
+__global__ void __launch_bounds__(NTHREADS, NST * BKT <= 2 * BK ? 2 : 1)
 gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float* __restrict__ W,
                int M, int N1, int N2, int lda, int ldb, int kchunk, const __bf16* __restrict__ zero,
                ConvGeom geo) {
     constexpr int WT1 = BN1 / WG1, WT2 = BN2 / WG2, R1 = WT1 / 16, R2 = WT2 / 16;
     constexpr int ROWA = BN1 * 2, ROWB_ = BN2 * 2;
-    constexpr int A_BYTES = BK * ROWA, STAGE = BK * (ROWA + ROWB_);
-    constexpr int PER_STAGE = (BK * ROWA / 1024 + BK * ROWB_ / 1024) / 4;  // LDS-DMA instructions per wave per stage
+    constexpr int A_BYTES = BKT * ROWA, STAGE = BKT * (ROWA + ROWB_);
+    constexpr int PER_STAGE = (BKT * ROWA / 1024 + BKT * ROWB_ / 1024) / 4;  // LDS-DMA instructions per wave per stage
+    static_assert(BKT == 64 || BKT == 32, "32- or 64-row stages");
     static_assert(NST >= 2 && NST <= 4, "2-4 stages");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -681,7 +684,7 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
 #pragma unroll
         for (int b = 0; b < R2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int nk = (kend - kbeg + BK - 1) / BK;
+    const int nk = (kend - kbeg + BKT - 1) / BKT;
     // conv mode: N2 = 9*C and a BN2 tile lies inside one tap (C % BN2 == 0, host-checked)
     int bc0 = n20, dh = 0, dw = 0;
     if constexpr (CONV == 1) {
@@ -693,8 +696,8 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
     const __amdgpu_buffer_rsrc_t ra = buf_rsrc(A), rb = buf_rsrc(B);
     auto stage = [&](int buf, int k0) {
         char* base = smem + buf * STAGE;
-        stage_rows<ROWA>(base, ra, lda, k0, kend, n10, wave, lane);
-        stage_rows<ROWB_, CONV>(base + A_BYTES, rb, ldb, k0, kend, bc0, wave, lane, &geo, dh, dw);
+        stage_rows<ROWA, 0, BKT>(base, ra, lda, k0, kend, n10, wave, lane);
+        stage_rows<ROWB_, CONV, BKT>(base + A_BYTES, rb, ldb, k0, kend, bc0, wave, lane, &geo, dh, dw);
     };
     const int gi = lane & 15, g = lane >> 4, q = gi >> 2, p = gi & 3;
     if constexpr (NST == 2) {
@@ -704,26 +707,26 @@ gemm_tn_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float
             __syncthreads();
         }
     } else {
-        for (int st = 0; st < NST - 1 && st < nk; ++st) stage(st, kbeg + st * BK);
+        for (int st = 0; st < NST - 1 && st < nk; ++st) stage(st, kbeg + st * BKT);
     }
     for (int kt = 0; kt < nk; ++kt) {
         int cur;
         if constexpr (NST == 2) {
             cur = kt & 1;
-            if (kt + 1 < nk) stage(cur ^ 1, kbeg + (kt + 1) * BK);
+            if (kt + 1 < nk) stage(cur ^ 1, kbeg + (kt + 1) * BKT);
         } else {
             // stages kt+1 .. min(kt+NST-2, nk-1) may stay in flight; stage kt must have landed for every wave, and
             // every wave is done with stage kt-1's buffer, which the fill of stage kt+NST-1 reuses
             const int later = min(NST - 2, nk - 1 - kt);
             wait_vm_stages<PER_STAGE>(later);
             __syncthreads();
-            if (kt + NST - 1 < nk) stage((kt + NST - 1) % NST, kbeg + (kt + NST - 1) * BK);
+            if (kt + NST - 1 < nk) stage((kt + NST - 1) % NST, kbeg + (kt + NST - 1) * BKT);
             cur = kt % NST;
         }
         const char* As = smem + cur * STAGE;
         const char* Bs = As + A_BYTES;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
+        for (int kk = 0; kk < BKT / 32; ++kk) {
             const int kb = kk * 32 + 8 * g + q;             // this lane's address row for the first tr read
             bf16x8 fa[R1], fb[R2];
 #pragma unroll
@@ -975,18 +978,21 @@ inline TnPlan tn_plan(int M, int N1, int N2, int num_cus, int bpc = 0) {
     return {kchunk, slices, groups, per_group, blocks};
 }
 
+// Rows per stage of the weight-gradient GEMM (A/B knob plx_set_tn_stages' second argument: 64 or 32)
+int g_tn_bk = 64;
+
 // LDS ring depth of the weight-gradient GEMM (A/B knob plx_set_tn_stages: 2 = double buffering, 3 or 4).  Default 2:
 // in the training step the deeper rings measured slower (same box, 3-sweep bench: 2 stages 11.92k, 3 stages 11.60k,
 // 4 stages 11.36k trials/h) -- a 96-128 KB ring leaves no LDS on its CU for the data-gradient chain's blocks
 // (profiles/r3_negative_results.md)
 int g_tn_stages = 2;
 
-template <int BN1, int BN2, int WG1, int WG2, int CONV, int NST>
+template <int BN1, int BN2, int WG1, int WG2, int CONV, int NST, int BKT = BK>
 int launch_tn_st(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
                  const void* zero, hipStream_t s, const ConvGeom& geo) {
-    constexpr int LDS = NST * BK * (BN1 + BN2) * 2;
+    constexpr int LDS = NST * BKT * (BN1 + BN2) * 2;
     static_assert(LDS <= 160 * 1024, "LDS ring exceeds the CU's LDS");
-    auto k = gemm_tn_kernel<BN1, BN2, WG1, WG2, CONV, NST>;
+    auto k = gemm_tn_kernel<BN1, BN2, WG1, WG2, CONV, NST, BKT>;
     static int attr = set_lds(k, LDS);
     if (attr) return attr;
     const int ntiles = (N1 / BN1) * (N2 / BN2);
@@ -998,6 +1004,10 @@ int launch_tn_st(const void* A, const void* B, float* W, int M, int N1, int N2, 
 template <int BN1, int BN2, int WG1, int WG2, int CONV = 0>
 int launch_tn(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
               const void* zero, hipStream_t s, ConvGeom geo = {}) {
+    if (g_tn_bk == 32)  // half-size stages: a 3- or 4-deep ring in (at most) the double buffer's LDS
+        return g_tn_stages >= 4
+                   ? launch_tn_st<BN1, BN2, WG1, WG2, CONV, 4, 32>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo)
+                   : launch_tn_st<BN1, BN2, WG1, WG2, CONV, 3, 32>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo);
     if (g_tn_stages >= 4)
         return launch_tn_st<BN1, BN2, WG1, WG2, CONV, 4>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo);
     if (g_tn_stages == 3)
@@ -1051,7 +1061,10 @@ void plx_set_nt_tall(int mode, int min_k) {
 }
 
 // A/B knob: LDS ring depth of the weight-gradient GEMM (2, 3 or 4 stages)
-void plx_set_tn_stages(int n) { g_tn_stages = n < 2 ? 2 : (n > 4 ? 4 : n); }
+void plx_set_tn_stages(int n, int bk) {
+    g_tn_stages = n < 2 ? 2 : (n > 4 ? 4 : n);
+    if (bk == 32 || bk == 64) g_tn_bk = bk;
+}
 
 // weight-gradient slicing knobs; workspace sizes follow them, so set before sizing / launching
 void plx_set_tn_plan(int blocks_per_cu, int slab_mb) {

@@ -158,7 +158,8 @@ def lib(name: str) -> ctypes.CDLL:
         if name == "plx_conv" and os.environ.get("PLX_HALO"):  # A/B knob: halo mode of the 3x3 convolutions
             handle.plx_set_halo(int(os.environ["PLX_HALO"]))
         if name == "plx_conv" and os.environ.get("PLX_TN_STAGES"):  # A/B knob: weight-gradient LDS ring depth
-            handle.plx_set_tn_stages(int(os.environ["PLX_TN_STAGES"]))
+            st, _, bk = os.environ["PLX_TN_STAGES"].partition(",")  # "stages[,rows per stage]"
+            handle.plx_set_tn_stages(int(st), int(bk or 0))
         if name == "plx_bn" and os.environ.get("PLX_STEM_BWD_CAP"):  # A/B knob: stem backward partials-pass rows
             handle.plx_set_stem_bwd_cap(int(os.environ["PLX_STEM_BWD_CAP"]))
         if name == "plx_conv" and os.environ.get("PLX_NT_TALL"):  # A/B knob: 256x128 NT tiles (0 / 1 fwd / 2 +dgrad)
@@ -244,7 +245,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_set_tn_sizes": [_I, _I],
         "plx_set_nt_single_stage": [_I],
         "plx_set_halo": [_I],
-        "plx_set_tn_stages": [_I],
+        "plx_set_tn_stages": [_I, _I],
         "plx_set_nt_tall": [_I, _I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],

@@ -471,3 +471,30 @@ def test_tall_nt_tiles_match_default_tiles(cuda):
     torch.testing.assert_close(res[2][1][1], o.square().sum(0), rtol=1e-4, atol=1e0)
     for x2, x0, name in zip(res[2][2], res[0][2], ("dx", "dgamma", "dbeta", "dw")):
         torch.testing.assert_close(x2, x0, rtol=1e-2, atol=1e-2 * float(x0.abs().max()), msg=name)
+
+
+@pytest.mark.parametrize("stages,bk", [(2, 64), (3, 64), (4, 64), (3, 32), (4, 32)])
+def test_gemm_tn_stage_rings(cuda, stages, bk):
+    """Every weight-gradient LDS ring (plx_set_tn_stages: depth 2-4, 64- or 32-row stages) against fp32, dense and
+    the 3x3 gather (conv wgrad), with ragged reductions."""
+    from polyaxon_amd.ops import _native
+    from polyaxon_amd.ops.conv import ConvKxK
+    from polyaxon_amd.ops.conv1x1 import gemm_tn
+
+    lib = _native.lib("plx_conv")
+    lib.plx_set_tn_stages(stages, bk)
+    try:
+        torch.manual_seed(2)
+        for m, n1, n2 in ((5000, 128, 128), (777, 64, 256), (20000, 256, 64)):
+            a, b = _bf(m, n1, dev=cuda), _bf(m, n2, dev=cuda)
+            torch.testing.assert_close(gemm_tn(a, b), a.float().t() @ b.float(), rtol=1e-3, atol=1e-3 * m ** 0.5)
+        conv = ConvKxK(64, 128, 3, 1).to(cuda)
+        x = torch.randn(4, 64, 17, 13, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y = conv(x.requires_grad_())
+        g = torch.randn_like(y.float())
+        y.backward(g.to(torch.bfloat16))
+    finally:
+        lib.plx_set_tn_stages(2, 64)
+    w = conv.weight.detach().float().requires_grad_()
+    F.conv2d(x.detach().float(), w, None, 1, 1).backward(g)
+    torch.testing.assert_close(conv.weight.grad.float(), w.grad, rtol=2e-2, atol=2e-2 * float(w.grad.abs().max()))
