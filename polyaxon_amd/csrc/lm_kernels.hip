@@ -7,6 +7,11 @@
 //   plx_qkv_rope_bwd   dq, dk, dv -> dqkv[T][(H+2KV)*D] (inverse rotation + the transpose back)
 //   plx_swiglu_fwd     h[T][2F] (gate | up halves of the fused gate/up GEMM) -> a[T][F] = silu(g) * u
 //   plx_swiglu_bwd     da, h -> dh[T][2F]: dg = da*u*silu'(g), du = da*silu(g)
+//   plx_xent_fwd       next-token cross entropy from bf16 logits [B][S][V]: per row (b, s < S-1) the log-sum-exp
+//                      (online max / sum over 16-byte chunks, one workgroup per row) and loss = lse - x[target]
+//   plx_xent_bwd       dlogits[B][S][V] (bf16) = (softmax - onehot(target)) * dloss / rows, zero rows at s = S-1
+//                      -- replaces slice copy + fp32 cast + log_softmax + NLL and their backward chain (~5.5 ms of
+//                      a 37 ms GPT-2 125M step: vocab 50257 x 16k tokens through fp32 twice)
 //
 // Llama RoPE convention (rotate the two halves of each head): for j < D/2
 //   y[j] = x[j] c_j - x[j+D/2] s_j,  y[j+D/2] = x[j] s_j + x[j+D/2] c_j,  c_j = cos(pos * theta^(-2j/D)).
@@ -173,6 +178,116 @@ __global__ __launch_bounds__(kBlock) void swiglu_bwd_kernel(const bf16x8* __rest
   }
 }
 
+
+// ------------------------------------------------------------------------------------------- cross entropy
+// Rows of V bf16 at an element stride of V: with V odd a row starts anywhere inside a 16-byte chunk, so a row is
+// walked as the aligned chunks that cover it (head = misalignment in elements) and elements outside [0, V) are
+// masked; the backward stores whole chunks inside the row and single elements in the two edge chunks (a chunk
+// shared with the neighbouring row is never written as a whole).
+constexpr float kNegInf = -__builtin_huge_valf();
+
+__device__ __forceinline__ void lse_combine(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == kNegInf) return;
+  s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+  m = mn;
+}
+
+__global__ __launch_bounds__(kBlock) void xent_fwd_kernel(const uint16_t* __restrict__ logits,
+                                                          const int64_t* __restrict__ tokens, float* __restrict__ lse,
+                                                          float* __restrict__ loss, int S, int V) {
+  const int r = blockIdx.x;                      // loss row: (b, s), s < S - 1
+  const int b = r / (S - 1), s = r - b * (S - 1);
+  const int64_t lrow = (int64_t)b * S + s;
+  const uint16_t* row = logits + lrow * V;
+  const uintptr_t p0 = (uintptr_t)row;
+  const bf16x8* base = (const bf16x8*)(p0 & ~(uintptr_t)15);
+  const int head = (int)((p0 & 15) >> 1);
+  const int nch = (head + V + 7) >> 3;
+  float m = kNegInf, sum = 0.f;
+  for (int c = threadIdx.x; c < nch; c += kBlock) {
+    const bf16x8 v = base[c];
+    float x[8], cm = kNegInf;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = c * 8 + j - head;
+      x[j] = (e >= 0 && e < V) ? bf2f(v.v[j]) : kNegInf;
+      cm = fmaxf(cm, x[j]);
+    }
+    if (cm == kNegInf) continue;
+    float cs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cs += __expf(x[j] - cm);
+    lse_combine(m, sum, cm, cs);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) lse_combine(m, sum, __shfl_xor(m, off), __shfl_xor(sum, off));
+  __shared__ float sm[kBlock / 64], ss[kBlock / 64];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sm[wave] = m;
+    ss[wave] = sum;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kBlock / 64; ++w) lse_combine(m, sum, sm[w], ss[w]);
+    const float l = m + __logf(sum);
+    const int64_t t = tokens[lrow + 1];
+    lse[r] = l;
+    loss[r] = l - bf2f(row[t]);
+  }
+}
+
+// scale: device scalar dloss (the mean's incoming gradient); inv_rows = 1 / (B * (S - 1))
+__global__ __launch_bounds__(kBlock) void xent_bwd_kernel(const uint16_t* __restrict__ logits,
+                                                          const int64_t* __restrict__ tokens,
+                                                          const float* __restrict__ lse, const float* __restrict__ dloss,
+                                                          uint16_t* __restrict__ grad, int S, int V, float inv_rows) {
+  const int lrow = blockIdx.x;                   // every logits row (b, s), s < S
+  const int b = lrow / S, s = lrow - b * S;
+  uint16_t* grow = grad + (int64_t)lrow * V;
+  const uintptr_t q0 = (uintptr_t)grow;
+  bf16x8* gbase = (bf16x8*)(q0 & ~(uintptr_t)15);
+  const int head = (int)((q0 & 15) >> 1);       // logits and grad share the layout (same offsets)
+  const int nch = (head + V + 7) >> 3;
+  if (s == S - 1) {                              // the last position predicts nothing: zero gradient
+    for (int c = threadIdx.x; c < nch; c += kBlock) {
+      if (c * 8 - head >= 0 && c * 8 - head + 8 <= V) {
+        gbase[c] = bf16x8{};
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int e = c * 8 + j - head;
+          if (e >= 0 && e < V) grow[e] = 0;
+        }
+      }
+    }
+    return;
+  }
+  const int r = b * (S - 1) + s;
+  const float l = lse[r], g = dloss[0] * inv_rows;
+  const int64_t t = tokens[(int64_t)lrow + 1];
+  const bf16x8* base = (const bf16x8*)((uintptr_t)(logits + (int64_t)lrow * V) & ~(uintptr_t)15);
+  for (int c = threadIdx.x; c < nch; c += kBlock) {
+    const bf16x8 v = base[c];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = c * 8 + j - head;
+      const float p = __expf(bf2f(v.v[j]) - l);
+      o.v[j] = f2bf((p - (e == t ? 1.f : 0.f)) * g);
+    }
+    if (c * 8 - head >= 0 && c * 8 - head + 8 <= V) {
+      gbase[c] = o;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = c * 8 + j - head;
+        if (e >= 0 && e < V) grow[e] = o.v[j];
+      }
+    }
+  }
+}
 }  // namespace
 
 PLX_API int plx_qkv_rope_fwd(const void* qkv, const float* cosv, const float* sinv, void* q, void* k, void* v,
@@ -204,5 +319,23 @@ PLX_API int plx_swiglu_bwd(const void* da, const void* h, void* dh, int64_t T, i
   if (T <= 0 || F % 8) return 1;
   hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(grid_for(T * (F / 8))), dim3(kBlock), 0, stream, (const bf16x8*)da,
                      (const bf16x8*)h, (bf16x8*)dh, T, F / 8);
+  return (int)hipGetLastError();
+}
+
+// logits bf16 [B][S][V] contiguous, tokens int64 [B][S]; lse / loss fp32 [B * (S - 1)]
+PLX_API int plx_xent_fwd(const void* logits, const int64_t* tokens, float* lse, float* loss, int B, int S, int V,
+                         hipStream_t stream) {
+  if (B <= 0 || S < 2 || V <= 0) return 1;
+  hipLaunchKernelGGL(xent_fwd_kernel, dim3(B * (S - 1)), dim3(kBlock), 0, stream, (const uint16_t*)logits, tokens, lse,
+                     loss, S, V);
+  return (int)hipGetLastError();
+}
+
+// grad bf16 [B][S][V] (same layout as logits); dloss: device scalar gradient of the mean loss
+PLX_API int plx_xent_bwd(const void* logits, const int64_t* tokens, const float* lse, const float* dloss, void* grad,
+                         int B, int S, int V, hipStream_t stream) {
+  if (B <= 0 || S < 2 || V <= 0) return 1;
+  hipLaunchKernelGGL(xent_bwd_kernel, dim3(B * S), dim3(kBlock), 0, stream, (const uint16_t*)logits, tokens, lse,
+                     dloss, (uint16_t*)grad, S, V, 1.f / (float)(B * (S - 1)));
   return (int)hipGetLastError();
 }

@@ -221,5 +221,6 @@ class Transformer(nn.Module):
 
 
 def lm_loss(logits: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
-    """Next-token cross entropy (targets = tokens shifted left)."""
-    return F.cross_entropy(logits[:, :-1].reshape(-1, logits.shape[-1]).float(), tokens[:, 1:].reshape(-1))
+    """Next-token cross entropy (targets = tokens shifted left), mean over B * (S - 1) positions: the fused HIP kernels
+    on bf16 GPU logits (ops/lm.py next_token_xent), F.cross_entropy in fp32 otherwise."""
+    return lm_ops.next_token_xent(logits, tokens)

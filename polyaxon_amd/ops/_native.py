@@ -268,6 +268,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_qkv_rope_bwd": [_P, _P, _P, _P, _P, _P, _L, _I, _I, _I, _I, _I, _P],
         "plx_swiglu_fwd": [_P, _P, _L, _I, _P],
         "plx_swiglu_bwd": [_P, _P, _P, _L, _I, _P],
+        "plx_xent_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
+        "plx_xent_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
     },
     "plx_gemm": {
         "plx_gemm256": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],

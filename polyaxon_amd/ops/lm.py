@@ -125,6 +125,46 @@ def swiglu(h: torch.Tensor) -> torch.Tensor:
     return _SwiGLU.apply(h)
 
 
+# ---------------------------------------------------------------------------------------------- cross entropy
+class _NextTokenXent(torch.autograd.Function):
+    """mean over (b, s < S-1) of lse(logits[b, s]) - logits[b, s, tokens[b, s+1]] straight from the bf16 logits
+    (csrc/lm_kernels.hip plx_xent_fwd / plx_xent_bwd): no slice copy, no fp32 logits, no log-softmax tensor; the
+    backward writes bf16 (softmax - onehot) * dloss / rows into a logits-shaped gradient in one pass."""
+
+    @staticmethod
+    def forward(ctx, logits, tokens):
+        lib = _native.lib("plx_lm")
+        B, S, V = logits.shape
+        rows = B * (S - 1)
+        lse = torch.empty(rows, dtype=torch.float32, device=logits.device)
+        loss = torch.empty(rows, dtype=torch.float32, device=logits.device)
+        _native.check(lib.plx_xent_fwd(logits.data_ptr(), tokens.data_ptr(), lse.data_ptr(), loss.data_ptr(), B, S, V,
+                                       _stream()), "plx_xent_fwd")
+        ctx.save_for_backward(logits, tokens, lse)
+        return loss.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _native.lib("plx_lm")
+        logits, tokens, lse = ctx.saved_tensors
+        B, S, V = logits.shape
+        grad = torch.empty_like(logits)
+        g = g.detach().to(torch.float32).reshape(1).contiguous()
+        _native.check(lib.plx_xent_bwd(logits.data_ptr(), tokens.data_ptr(), lse.data_ptr(), g.data_ptr(),
+                                       grad.data_ptr(), B, S, V, _stream()), "plx_xent_bwd")
+        return grad, None
+
+
+def next_token_xent(logits: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
+    """Next-token cross entropy (targets = tokens shifted left), mean over B * (S - 1) positions: the fused HIP pair on
+    bf16 CUDA logits [B, S, V] (contiguous, 16-byte aligned) with int64 tokens [B, S]; the fp32 reference otherwise."""
+    if (logits.is_cuda and logits.dtype == torch.bfloat16 and logits.dim() == 3 and logits.is_contiguous()
+            and logits.data_ptr() % 16 == 0 and tokens.dtype == torch.int64 and tokens.is_contiguous()
+            and tokens.shape == logits.shape[:2] and logits.shape[1] >= 2):
+        return _NextTokenXent.apply(logits, tokens)
+    return F.cross_entropy(logits[:, :-1].reshape(-1, logits.shape[-1]).float(), tokens[:, 1:].reshape(-1))
+
+
 # ---------------------------------------------------------------------------------------------- direct-grad Linear
 class _LinearDirect(torch.autograd.Function):
     """y = x W^T (+ b).  Backward writes dW = dy^T x with the GEMM's output pointer on the parameter's flat

@@ -125,3 +125,24 @@ def test_optimizer_in_backward_matches_monolithic_step_on_gpu(cuda, arch):
     assert torch.equal(res[False][1], res[True][1]) and torch.equal(res[False][2], res[True][2])
     d = res[True][3]
     assert len(d.buckets) > 3 and d.stepped == 4 * len(d.buckets)
+
+
+@pytest.mark.parametrize("B,S,V", [(2, 5, 50257), (3, 17, 256), (1, 2, 1000), (4, 33, 130001)])
+def test_next_token_xent_matches_fp32(cuda, B, S, V):
+    """The fused cross entropy (csrc/lm_kernels.hip plx_xent_fwd / _bwd) on bf16 logits -- odd vocabularies whose rows
+    start mid-chunk included -- against F.cross_entropy of the same logits in fp32: loss and logits gradient (the
+    last position of every sequence gets a zero gradient), with a non-unit incoming gradient."""
+    from polyaxon_amd.ops.lm import next_token_xent
+
+    torch.manual_seed(0)
+    logits = (torch.randn(B, S, V, device=cuda) * 3).to(torch.bfloat16).requires_grad_()
+    tokens = torch.randint(0, V, (B, S), device=cuda)
+    loss = next_token_xent(logits, tokens)
+    (loss * 1.7).backward()
+    ref_in = logits.detach().float().requires_grad_()
+    ref = F.cross_entropy(ref_in[:, :-1].reshape(-1, V), tokens[:, 1:].reshape(-1))
+    (ref * 1.7).backward()
+    assert abs(float(loss) - float(ref)) < 1e-4 * max(1.0, abs(float(ref)))
+    g, gr = logits.grad.float(), ref_in.grad
+    assert float(g[:, -1].abs().max()) == 0.0
+    torch.testing.assert_close(g, gr, rtol=1e-2, atol=1e-2 * float(gr.abs().max()))
