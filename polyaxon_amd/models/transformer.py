@@ -25,6 +25,7 @@ import torch.nn.functional as F
 from torch.utils.checkpoint import checkpoint
 
 from polyaxon_amd.ops import lm as lm_ops
+from polyaxon_amd.ops import rmsnorm as _rms
 from polyaxon_amd.ops.attention import flash_attention
 
 
@@ -154,7 +155,7 @@ class Block(nn.Module):
     def __init__(self, cfg: TransformerConfig):
         super().__init__()
         Norm = (lambda d: RMSNorm(d, cfg.norm_eps)) if cfg.norm == "rmsnorm" else (
-            lambda d: nn.LayerNorm(d, eps=cfg.norm_eps))
+            lambda d: _rms.LayerNorm(d, eps=cfg.norm_eps))  # fused bf16 LayerNorm (csrc/rmsnorm.hip)
         self.n1, self.n2 = Norm(cfg.d_model), Norm(cfg.d_model)
         self.attn, self.mlp = Attention(cfg), MLP(cfg)
 
@@ -170,7 +171,7 @@ class Transformer(nn.Module):
         self.embed = nn.Embedding(cfg.vocab_size, cfg.d_model)
         self.pos = nn.Embedding(cfg.max_seq_len, cfg.d_model) if cfg.pos == "learned" else None
         self.blocks = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layers)])
-        self.norm = RMSNorm(cfg.d_model, cfg.norm_eps) if cfg.norm == "rmsnorm" else nn.LayerNorm(cfg.d_model)
+        self.norm = RMSNorm(cfg.d_model, cfg.norm_eps) if cfg.norm == "rmsnorm" else _rms.LayerNorm(cfg.d_model)
         self.head = None if cfg.tie_embeddings else nn.Linear(cfg.d_model, cfg.vocab_size, bias=False)
         self._rope = None
         self.reset_parameters()

@@ -294,6 +294,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_rms_forward": [_P, _P, _P, _P, _L, _I, _F, _P],
         "plx_rms_bwd_blocks": [_L],
         "plx_rms_backward": [_P, _P, _P, _P, _P, _P, _L, _I, _P],
+        "plx_ln_forward": [_P, _P, _P, _P, _P, _P, _L, _I, _F, _P],
+        "plx_ln_backward": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
     },
     "plx_rccl": {
         "plx_rccl_unique_id": [ctypes.c_char_p],

@@ -1,4 +1,4 @@
-"""GPU tests: RMSNorm HIP kernels vs fp32 reference, transformer/LM trainer, MLP grid group through polyflow."""
+"""GPU tests: RMSNorm / LayerNorm HIP kernels vs fp32 reference, transformer/LM trainer, MLP grid group through polyflow."""
 import json
 import os
 import subprocess
@@ -28,6 +28,30 @@ def test_rmsnorm_matches_fp32(cuda, rows, d):
     yr.backward(g.float())
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(w.grad, wr.grad, rtol=2e-2, atol=2e-2 * rows ** 0.5)
+
+
+@pytest.mark.parametrize("rows,d", [(1, 64), (37, 768), (5000, 768), (3, 8192)])
+def test_layernorm_matches_fp32(cuda, rows, d):
+    """Fused bf16 LayerNorm (csrc/rmsnorm.hip plx_ln_*) vs fp32 F.layer_norm: output, dx, dweight, dbias; an input
+    with a large offset exercises the two-pass (mean, then centred variance) statistics."""
+    from polyaxon_amd.ops.rmsnorm import layer_norm, layer_norm_reference
+
+    torch.manual_seed(0)
+    x = (torch.randn(rows, d, device=cuda) * 3 + 20).to(torch.bfloat16).requires_grad_()
+    w = (torch.rand(d, device=cuda) + 0.5).requires_grad_()
+    b = torch.randn(d, device=cuda).requires_grad_()
+    y = layer_norm(x, w, b, 1e-5)
+    assert y.dtype == torch.bfloat16
+    xr = x.detach().float().requires_grad_()
+    wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    yr = layer_norm_reference(xr, wr, br, 1e-5)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    g = torch.randn(rows, d, device=cuda).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=3e-2 * float(xr.grad.abs().max()))
+    torch.testing.assert_close(w.grad, wr.grad, rtol=2e-2, atol=2e-2 * rows ** 0.5)
+    torch.testing.assert_close(b.grad, br.grad, rtol=2e-2, atol=2e-2 * rows ** 0.5)
 
 
 def test_tiny_llama_trains_on_gpu(cuda):
