@@ -143,10 +143,16 @@ def linear_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
     return supported(T, weight.shape[0], weight.shape[1]) and supported(T, weight.shape[1], weight.shape[0])
 
 
-def forward(x2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    """y[T][out] = x[T][in] . W[out][in]^T"""
+def forward(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y[T][out] = x[T][in] . W[out][in]^T (+ bias): on hipBLASLt the bias rides in the GEMM epilogue (addmm) instead
+    of a separate read-modify-write pass over y"""
     T, fin = x2.shape
-    return matmul(x2, weight, T, weight.shape[0], fin, True, True)
+    N = weight.shape[0]
+    if bias is None:
+        return matmul(x2, weight, T, N, fin, True, True)
+    if _use_native(x2, weight, T, N, fin, True, True):
+        return gemm(x2, weight, T, N, fin, True, True).add_(bias)
+    return torch.addmm(bias.to(x2.dtype), x2, weight.t())
 
 
 def dgrad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:

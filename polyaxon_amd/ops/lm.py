@@ -209,9 +209,7 @@ class _LinearMfma(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         ctx.save_for_backward(x2, weight)
         ctx.slot, ctx.flat, ctx.has_bias, ctx.xshape = slot, flat, bias is not None, x.shape
-        y = gemm.forward(x2, weight)
-        if bias is not None:
-            y.add_(bias)
+        y = gemm.forward(x2, weight, bias)
         return y.view(*x.shape[:-1], weight.shape[0])
 
     @staticmethod
