@@ -111,26 +111,41 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const bf16x8* __restri
 // large nblk (stem) leaves the reduction on a handful of CUs.
 constexpr int kRowsPerSplit = 64;
 
-__global__ __launch_bounds__(256) void bn_partial_reduce_kernel(const float* __restrict__ part, int nblk, int C,
-                                                                float* __restrict__ out, int S) {
-  __shared__ float sh[256];
+// Per thread: the U = kRowsPerSplit / G rows lane, lane + G, ... of split s, all loads issued at once, summed in
+// row order; the G group sums are then combined in group order.  bn_partial_reduce_kernel<NT> and the one-launch
+// reduce_l2_last<NT> share this arithmetic, so both paths give bit-identical level-2 rows.
+template <int NT>
+__device__ __forceinline__ float l1_rows(const float* __restrict__ src, int b0, int b1, int C, int c, int lane) {
+  constexpr int G = NT / 64, U = kRowsPerSplit / G;
+  float x[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int b = b0 + lane + u * G;
+    x[u] = b < b1 ? src[(int64_t)b * C + c] : 0.f;
+  }
+  float a = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) a += x[u];
+  return a;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void bn_partial_reduce_kernel(const float* __restrict__ part, int nblk, int C,
+                                                               float* __restrict__ out, int S) {
+  constexpr int G = NT / 64;
+  __shared__ float sh[NT];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int lane = threadIdx.x >> 6;
   const int s = blockIdx.y, which = blockIdx.z;
-  const float* src = part + (int64_t)which * nblk * C;
   const int b0 = s * kRowsPerSplit;
-  int b1 = b0 + kRowsPerSplit;
-  if (b1 > nblk) b1 = nblk;
-  float acc = 0.f;
-  if (c < C) {
-#pragma unroll 4
-    for (int b = b0 + lane; b < b1; b += 4) acc += src[(int64_t)b * C + c];
-  }
-  sh[threadIdx.x] = acc;
+  const int b1 = b0 + kRowsPerSplit < nblk ? b0 + kRowsPerSplit : nblk;
+  sh[threadIdx.x] = c < C ? l1_rows<NT>(part + (int64_t)which * nblk * C, b0, b1, C, c, lane) : 0.f;
   __syncthreads();
   if (lane == 0 && c < C) {
-    const int t = threadIdx.x;
-    out[((int64_t)which * S + s) * C + c] = sh[t] + sh[t + 64] + sh[t + 128] + sh[t + 192];
+    float r = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) r += sh[threadIdx.x + 64 * g];
+    out[((int64_t)which * S + s) * C + c] = r;
   }
 }
 
@@ -138,35 +153,38 @@ __global__ __launch_bounds__(256) void bn_partial_reduce_kernel(const float* __r
 // sums every 4th of the S partial rows (independent loads, fp64 accumulation), then the 4 group sums are combined
 // through LDS in a fixed order (deterministic).  One thread per channel walking all S rows serially was 19 us per
 // backward BatchNorm on the 56x56 layers (S ~ 100 dependent-latency iterations on a single 256-thread block).
-constexpr int kFinSplit = 4;
+template <int NT = 256>
 __device__ __forceinline__ bool fin_sum2(const float* __restrict__ pa, const float* __restrict__ pb, int nblk, int C,
                                          double& A, double& B) {
-  __shared__ double sh[2][kFinSplit][64];
+  constexpr int G = NT / 64;  // split lane-groups
+  __shared__ double sh[2][G][64];
   const int lc = threadIdx.x & 63, sp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lc;
   double a0 = 0.0, b0 = 0.0;
   if (c < C) {
-    // 8 rows (16 loads) in flight per batch: this runs in the last-arriving block, on the critical path of every
-    // BatchNorm, and two rows per trip left it a chain of ~12 dependent L2 round trips at S ~ 100
-    int b = sp;
-    for (; b + 7 * kFinSplit < nblk; b += 8 * kFinSplit) {
+    // 8 rows (16 predicated loads) in flight per trip: this runs in the last-arriving block, on the critical path of
+    // every BatchNorm; with 16 groups (1024 threads) S <= 128 level-2 rows is ONE dependent L2 round trip
+    for (int b = sp; b < nblk; b += 8 * G) {
       float x[8], y[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        x[u] = pa[(int64_t)(b + u * kFinSplit) * C + c];
-        y[u] = pb[(int64_t)(b + u * kFinSplit) * C + c];
+        const int r = b + u * G;
+        x[u] = r < nblk ? pa[(int64_t)r * C + c] : 0.f;
+        y[u] = r < nblk ? pb[(int64_t)r * C + c] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) { a0 += x[u]; b0 += y[u]; }
     }
-    for (; b < nblk; b += kFinSplit) { a0 += pa[(int64_t)b * C + c]; b0 += pb[(int64_t)b * C + c]; }
   }
   sh[0][sp][lc] = a0;
   sh[1][sp][lc] = b0;
   __syncthreads();
   if (sp != 0 || c >= C) return false;
-  A = ((sh[0][0][lc] + sh[0][1][lc]) + sh[0][2][lc]) + sh[0][3][lc];
-  B = ((sh[1][0][lc] + sh[1][1][lc]) + sh[1][2][lc]) + sh[1][3][lc];
+  double sa = 0.0, sb = 0.0;
+#pragma unroll
+  for (int g = 0; g < G; ++g) { sa += sh[0][g][lc]; sb += sh[1][g][lc]; }  // fixed order: deterministic
+  A = sa;
+  B = sb;
   return true;
 }
 
@@ -197,9 +215,10 @@ struct BwdFin {
   int accumulate;
 };
 
+template <int NT>
 __device__ __forceinline__ void fwd_finalize(const float* psum, const float* psq, int nblk, const FwdFin& f) {
   double S, Q;  // level-2 partials per channel, summed in fp64
-  if (!fin_sum2(psum, psq, nblk, f.C, S, Q)) return;
+  if (!fin_sum2<NT>(psum, psq, nblk, f.C, S, Q)) return;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const double m = S / (double)f.M;
   double var = Q / (double)f.M - m * m;
@@ -218,9 +237,10 @@ __device__ __forceinline__ void fwd_finalize(const float* psum, const float* psq
   }
 }
 
+template <int NT>
 __device__ __forceinline__ void bwd_finalize(const float* pdz, const float* pdzx, int nblk, const BwdFin& f) {
   double A, B;
-  if (!fin_sum2(pdz, pdzx, nblk, f.C, A, B)) return;
+  if (!fin_sum2<NT>(pdz, pdzx, nblk, f.C, A, B)) return;
   const int C = f.C;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const float db = (float)A, dg = (float)B;
@@ -243,9 +263,11 @@ __device__ __forceinline__ void bwd_finalize(const float* pdz, const float* pdzx
 // last arriver before the workgroup reads.  Counters start at zero (allocated zeroed) and the last arriver resets
 // its own; launches that share a counter array are stream-ordered.  Saves a launch boundary and the separate
 // finalize pass's own ramp per BatchNorm direction (106 per ResNet-50 step).
+template <int NT>
 __device__ __forceinline__ bool reduce_l2_last(const float* __restrict__ part, int nblk, int C, float* l2, int S,
                                                unsigned* cnt) {
-  __shared__ float sh[2][256];
+  constexpr int G = NT / 64;
+  __shared__ float sh[2][NT];
   __shared__ int s_last;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int lane = threadIdx.x >> 6;
@@ -255,31 +277,19 @@ __device__ __forceinline__ bool reduce_l2_last(const float* __restrict__ part, i
   if (b1 > nblk) b1 = nblk;
   float a0 = 0.f, a1 = 0.f;
   if (c < C) {
-    const float* p0 = part;
-    const float* p1 = part + (int64_t)nblk * C;
-    int b = b0 + lane;
-    for (; b + 28 < b1; b += 32) {                          // 8 rows (16 loads) in flight per batch
-      float x[8], y[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        x[u] = p0[(int64_t)(b + 4 * u) * C + c];
-        y[u] = p1[(int64_t)(b + 4 * u) * C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) { a0 += x[u]; a1 += y[u]; }
-    }
-    for (; b < b1; b += 4) {
-      a0 += p0[(int64_t)b * C + c];
-      a1 += p1[(int64_t)b * C + c];
-    }
+    a0 = l1_rows<NT>(part, b0, b1, C, c, lane);
+    a1 = l1_rows<NT>(part + (int64_t)nblk * C, b0, b1, C, c, lane);
   }
   sh[0][threadIdx.x] = a0;
   sh[1][threadIdx.x] = a1;
   __syncthreads();
   if (lane == 0 && c < C) {
     const int t = threadIdx.x;
-    l2[(int64_t)s * C + c] = sh[0][t] + sh[0][t + 64] + sh[0][t + 128] + sh[0][t + 192];
-    l2[((int64_t)S + s) * C + c] = sh[1][t] + sh[1][t + 64] + sh[1][t + 128] + sh[1][t + 192];
+    float r0 = 0.f, r1 = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) { r0 += sh[0][t + 64 * g]; r1 += sh[1][t + 64 * g]; }
+    l2[(int64_t)s * C + c] = r0;
+    l2[((int64_t)S + s) * C + c] = r1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
   __syncthreads();
@@ -299,19 +309,26 @@ __device__ __forceinline__ bool reduce_l2_last(const float* __restrict__ part, i
   return s_last != 0;
 }
 
-__global__ __launch_bounds__(256) void bn_fwd_reduce_finalize_kernel(const float* __restrict__ part, int nblk,
-                                                                     float* l2, int S, unsigned* cnt, FwdFin f) {
-  if (!reduce_l2_last(part, nblk, f.C, l2, S, cnt)) return;
-  fwd_finalize(l2, l2 + (int64_t)S * f.C, S, f);
+// 1024 threads: 16 row groups make both the level-1 rows (4 per thread) and the S level-2 rows (<= 8 per thread
+// up to S = 128) a single L2 round trip each; with 256 threads they were 2 and up to 4 dependent trips
+constexpr int kFinNT = 1024;
+static int g_fin_nt = kFinNT;  // plx_set_bn_fin_threads(256) restores the 256-thread variant (A/B)
+template <int NT>
+__global__ __launch_bounds__(NT) void bn_fwd_reduce_finalize_kernel(const float* __restrict__ part, int nblk, float* l2,
+                                                                    int S, unsigned* cnt, FwdFin f) {
+  if (!reduce_l2_last<NT>(part, nblk, f.C, l2, S, cnt)) return;
+  fwd_finalize<NT>(l2, l2 + (int64_t)S * f.C, S, f);
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_reduce_finalize_kernel(const float* __restrict__ part, int nblk,
-                                                                     float* l2, int S, unsigned* cnt, BwdFin f) {
-  if (!reduce_l2_last(part, nblk, f.C, l2, S, cnt)) return;
-  bwd_finalize(l2, l2 + (int64_t)S * f.C, S, f);
+template <int NT>
+__global__ __launch_bounds__(NT) void bn_bwd_reduce_finalize_kernel(const float* __restrict__ part, int nblk, float* l2,
+                                                                    int S, unsigned* cnt, BwdFin f) {
+  if (!reduce_l2_last<NT>(part, nblk, f.C, l2, S, cnt)) return;
+  bwd_finalize<NT>(l2, l2 + (int64_t)S * f.C, S, f);
 }
 
-__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq, int nblk,
+template <int NT>
+__global__ __launch_bounds__(NT) void bn_fwd_finalize_kernel(const float* __restrict__ psum, const float* __restrict__ psq, int nblk,
                                        const uint16_t* __restrict__ x_row0, int C, int64_t M,
                                        const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
                                        float momentum, float* __restrict__ running_mean,
@@ -319,7 +336,7 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const float* __res
                                        float* __restrict__ save_invstd, float* __restrict__ scale,
                                        float* __restrict__ bias) {
   double S, Q;  // level-2 partials per channel, summed in fp64
-  if (!fin_sum2(psum, psq, nblk, C, S, Q)) return;
+  if (!fin_sum2<NT>(psum, psq, nblk, C, S, Q)) return;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const double m = S / (double)M;
   double var = Q / (double)M - m * m;
@@ -462,12 +479,13 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const bf16x8* __r
   }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ pdz, const float* __restrict__ pdzx, int nblk, int C,
+template <int NT>
+__global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(const float* __restrict__ pdz, const float* __restrict__ pdzx, int nblk, int C,
                                        int64_t M, const float* __restrict__ gamma, const float* __restrict__ mean,
                                        const float* __restrict__ invstd, float* __restrict__ dgamma,
                                        float* __restrict__ dbeta, float* __restrict__ coef, int accumulate) {
   double A, B;
-  if (!fin_sum2(pdz, pdzx, nblk, C, A, B)) return;
+  if (!fin_sum2<NT>(pdz, pdzx, nblk, C, A, B)) return;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const float db = (float)A, dg = (float)B;
   // accumulate: dgamma / dbeta are the parameters' own (flat) gradient slots, summed into like autograd would
@@ -632,12 +650,16 @@ inline void reduce_finalize_fwd(hipStream_t stream, const float* part, int nblk,
                                 const FwdFin& f) {
   const int C = f.C, S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
   if (cnt != nullptr) {
-    hipLaunchKernelGGL(bn_fwd_reduce_finalize_kernel, dim3((C + 63) / 64, S), dim3(256), 0, stream, part, nblk, l2, S,
+    auto k = g_fin_nt == 256 ? bn_fwd_reduce_finalize_kernel<256> : bn_fwd_reduce_finalize_kernel<kFinNT>;
+    hipLaunchKernelGGL(k, dim3((C + 63) / 64, S), dim3(g_fin_nt == 256 ? 256 : kFinNT), 0, stream, part, nblk, l2, S,
                        cnt, f);
     return;
   }
-  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, S, 2), dim3(256), 0, stream, part, nblk, C, l2, S);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S,
+  const int nt = g_fin_nt == 256 ? 256 : kFinNT;
+  hipLaunchKernelGGL(nt == 256 ? bn_partial_reduce_kernel<256> : bn_partial_reduce_kernel<kFinNT>,
+                     dim3((C + 63) / 64, S, 2), dim3(nt), 0, stream, part, nblk, C, l2, S);
+  hipLaunchKernelGGL(nt == 256 ? bn_fwd_finalize_kernel<256> : bn_fwd_finalize_kernel<kFinNT>, dim3((C + 63) / 64),
+                     dim3(nt), 0, stream, l2, l2 + (int64_t)S * C, S,
                      f.x_row0, C, f.M, f.gamma, f.beta, f.eps, f.momentum, f.running_mean, f.running_var, f.save_mean,
                      f.save_invstd, f.scale, f.bias);
 }
@@ -646,12 +668,16 @@ inline void reduce_finalize_bwd(hipStream_t stream, const float* part, int nblk,
                                 const BwdFin& f) {
   const int C = f.C, S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
   if (cnt != nullptr) {
-    hipLaunchKernelGGL(bn_bwd_reduce_finalize_kernel, dim3((C + 63) / 64, S), dim3(256), 0, stream, part, nblk, l2, S,
+    auto k = g_fin_nt == 256 ? bn_bwd_reduce_finalize_kernel<256> : bn_bwd_reduce_finalize_kernel<kFinNT>;
+    hipLaunchKernelGGL(k, dim3((C + 63) / 64, S), dim3(g_fin_nt == 256 ? 256 : kFinNT), 0, stream, part, nblk, l2, S,
                        cnt, f);
     return;
   }
-  hipLaunchKernelGGL(bn_partial_reduce_kernel, dim3((C + 63) / 64, S, 2), dim3(256), 0, stream, part, nblk, C, l2, S);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, l2, l2 + (int64_t)S * C, S, C,
+  const int nt = g_fin_nt == 256 ? 256 : kFinNT;
+  hipLaunchKernelGGL(nt == 256 ? bn_partial_reduce_kernel<256> : bn_partial_reduce_kernel<kFinNT>,
+                     dim3((C + 63) / 64, S, 2), dim3(nt), 0, stream, part, nblk, C, l2, S);
+  hipLaunchKernelGGL(nt == 256 ? bn_bwd_finalize_kernel<256> : bn_bwd_finalize_kernel<kFinNT>, dim3((C + 63) / 64),
+                     dim3(nt), 0, stream, l2, l2 + (int64_t)S * C, S, C,
                      f.M, f.gamma, f.mean, f.invstd, f.dgamma, f.dbeta, f.coef, f.accumulate);
 }
 
@@ -1014,6 +1040,7 @@ PLX_API int plx_stem_bn_pool_forward(const void* x, void* y, void* idx, int N, i
 
 // A/B knob: quad rows of the stem backward's partials pass (1 .. 65535; set before sizing the workspace)
 PLX_API void plx_set_stem_bwd_cap(int cap) { g_stem_bwd_cap = cap < 1 ? 1 : (cap > 65535 ? 65535 : cap); }
+PLX_API void plx_set_bn_fin_threads(int n) { g_fin_nt = n == 256 ? 256 : kFinNT; }
 
 // floats of workspace plx_stem_bn_pool_backward needs: level-1 [2][nblk][C] + level-2 [2][S][C]
 PLX_API int64_t plx_stem_bn_pool_bwd_workspace(int N, int H, int W, int C) {

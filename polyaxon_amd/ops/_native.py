@@ -162,6 +162,8 @@ def lib(name: str) -> ctypes.CDLL:
             handle.plx_set_tn_stages(int(st), int(bk or 0))
         if name == "plx_bn" and os.environ.get("PLX_STEM_BWD_CAP"):  # A/B knob: stem backward partials-pass rows
             handle.plx_set_stem_bwd_cap(int(os.environ["PLX_STEM_BWD_CAP"]))
+        if name == "plx_bn" and os.environ.get("PLX_BN_FIN_THREADS"):  # A/B knob: 256-thread BN finalize
+            handle.plx_set_bn_fin_threads(int(os.environ["PLX_BN_FIN_THREADS"]))
         if name == "plx_conv" and os.environ.get("PLX_NT_TALL"):  # A/B knob: 256x128 NT tiles (0 / 1 fwd / 2 +dgrad)
             handle.plx_set_nt_tall(int(os.environ["PLX_NT_TALL"]), int(os.environ.get("PLX_NT_TALL_K", "0")))
         if name == "plx_gemm" and os.environ.get("PLX_GEMM_SPLIT_TARGET"):  # A/B knob: split-K planner target
@@ -212,6 +214,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
                                      _P],
         "plx_stem_bn_pool_bwd_workspace": [_I, _I, _I, _I],
         "plx_set_stem_bwd_cap": [_I],
+        "plx_set_bn_fin_threads": [_I],
         "plx_stem_bn_pool_backward": [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     },
     "plx_procmon": {
@@ -270,6 +273,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_swiglu_bwd": [_P, _P, _P, _L, _I, _P],
         "plx_xent_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
         "plx_xent_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+        "plx_colsum_splits": [_L, _I],
+        "plx_colsum": [_P, _L, _I, _P, _P, _P, _I, _P],
     },
     "plx_gemm": {
         "plx_gemm256": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
@@ -317,7 +322,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_set_stem_bwd_cap": None, "plx_set_adamw_grid_cap": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_set_stem_bwd_cap": None, "plx_set_bn_fin_threads": None, "plx_set_adamw_grid_cap": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

@@ -7,6 +7,7 @@ kernel cannot take (odd head size, ...) raises instead of silently falling back.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -165,6 +166,30 @@ def next_token_xent(logits: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
     return F.cross_entropy(logits[:, :-1].reshape(-1, logits.shape[-1]).float(), tokens[:, 1:].reshape(-1))
 
 
+# ---------------------------------------------------------------------------------------------- bias gradient
+_COLSUM_CNT: dict = {}
+_COLSUM = os.environ.get("PLX_COLSUM", "1") != "0"  # A/B knob: 0 = torch's column reduction
+
+
+def bias_grad(dy2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """db = dy2.sum(0) for a bias of ``dtype``: the deterministic one-launch column sum (csrc/lm_kernels.hip
+    plx_colsum, fp32 accumulation) for a contiguous bf16 CUDA [T, N] with N % 8 == 0; torch's reduction otherwise."""
+    T, N = dy2.shape
+    if not (_COLSUM and _native_ok(dy2) and dy2.is_contiguous() and N % 8 == 0 and dy2.data_ptr() % 16 == 0 and T > 0
+            and dtype in (torch.float32, torch.bfloat16) and (N + 63) // 64 <= 4096):
+        return dy2.sum(0).to(dtype)
+    lib = _native.lib("plx_lm")
+    dev = dy2.device
+    cnt = _COLSUM_CNT.get(dev)
+    if cnt is None:
+        cnt = _COLSUM_CNT[dev] = torch.zeros(4096, dtype=torch.int32, device=dev)
+    part = torch.empty(lib.plx_colsum_splits(T, N), N, dtype=torch.float32, device=dev)
+    out = torch.empty(N, dtype=dtype, device=dev)
+    _native.check(lib.plx_colsum(dy2.data_ptr(), T, N, part.data_ptr(), cnt.data_ptr(), out.data_ptr(),
+                                 int(dtype == torch.float32), _stream()), "plx_colsum")
+    return out
+
+
 # ---------------------------------------------------------------------------------------------- direct-grad Linear
 class _LinearDirect(torch.autograd.Function):
     """y = x W^T (+ b).  Backward writes dW = dy^T x with the GEMM's output pointer on the parameter's flat
@@ -176,6 +201,7 @@ class _LinearDirect(torch.autograd.Function):
     def forward(ctx, x, weight, bias, slot, flat):
         ctx.save_for_backward(x, weight)
         ctx.slot, ctx.flat, ctx.has_bias = slot, flat, bias is not None
+        ctx.bias_dtype = bias.dtype if bias is not None else None
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -189,7 +215,7 @@ class _LinearDirect(torch.autograd.Function):
             torch.addmm(g, dy2.t(), x2, out=g)
         else:
             torch.mm(dy2.t(), x2, out=g)
-        db = dy2.sum(0) if ctx.has_bias else None
+        db = bias_grad(dy2, ctx.bias_dtype) if ctx.has_bias else None
         cb = getattr(weight, "_plx_ready_cb", None)
         if cb is not None:
             cb(weight)
@@ -209,6 +235,7 @@ class _LinearMfma(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         ctx.save_for_backward(x2, weight)
         ctx.slot, ctx.flat, ctx.has_bias, ctx.xshape = slot, flat, bias is not None, x.shape
+        ctx.bias_dtype = bias.dtype if bias is not None else None
         y = gemm.forward(x2, weight, bias)
         return y.view(*x.shape[:-1], weight.shape[0])
 
@@ -228,7 +255,7 @@ class _LinearMfma(torch.autograd.Function):
                 cb(weight)
         elif ctx.needs_input_grad[1]:
             dw = gemm.wgrad(dy2, x2)
-        db = dy2.sum(0) if ctx.has_bias else None
+        db = bias_grad(dy2, ctx.bias_dtype) if ctx.has_bias else None
         return dx, dw, db, None, None
 
 

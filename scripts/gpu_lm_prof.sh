@@ -12,5 +12,10 @@ db=$(find /tmp/plx_lmprof -name '*.db' | head -1)
 python scripts/kernel_totals.py "$db" --top 40 > gpurun_out/${TAG}_kernels.md
 python scripts/lm_step_streams.py "$db" --steps 2 > gpurun_out/${TAG}_streams.md || true
 cat gpurun_out/${TAG}_streams.md
+if [ -n "${NEIGHBORS:-}" ]; then  # comma-separated kernel-name patterns: who launches them
+  IFS=',' read -ra pats <<< "$NEIGHBORS"
+  for p in "${pats[@]}"; do python scripts/kernel_neighbors.py "$db" "$p" --n 2 --skip 40; done > gpurun_out/${TAG}_neighbors.txt
+  cat gpurun_out/${TAG}_neighbors.txt
+fi
 grep tokens_per_s gpurun_out/${TAG}.log | tail -1 | cut -c1-200
 head -25 gpurun_out/${TAG}_kernels.md

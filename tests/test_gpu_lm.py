@@ -146,3 +146,22 @@ def test_next_token_xent_matches_fp32(cuda, B, S, V):
     g, gr = logits.grad.float(), ref_in.grad
     assert float(g[:, -1].abs().max()) == 0.0
     torch.testing.assert_close(g, gr, rtol=1e-2, atol=1e-2 * float(gr.abs().max()))
+
+
+@pytest.mark.parametrize("T,N", [(16384, 768), (16384, 3072), (1000, 2304), (37, 264), (1, 8)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bias_grad_colsum_matches_fp32(cuda, T, N, dtype):
+    """plx_colsum (csrc/lm_kernels.hip, the Linear bias gradient) against an fp64 column sum of the same bf16 matrix:
+    tiles that end mid-tile (N % 64 != 0), a single row, both output dtypes, and bitwise-identical repeats (the
+    last-arriver reduction runs in a fixed order)."""
+    from polyaxon_amd.ops import lm as lm_ops
+
+    assert _native.available("plx_lm")
+    g = torch.Generator(device="cuda").manual_seed(T * 7 + N)
+    dy = torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16)
+    out = lm_ops.bias_grad(dy, dtype)
+    assert out.dtype == dtype and out.shape == (N,)
+    ref = dy.double().sum(0)
+    tol = 1e-4 * T ** 0.5 + (0.01 * ref.abs().max().item() if dtype == torch.bfloat16 else 0.0)
+    torch.testing.assert_close(out.double(), ref, rtol=1e-2 if dtype == torch.bfloat16 else 1e-5, atol=tol)
+    assert torch.equal(lm_ops.bias_grad(dy, dtype), out)
