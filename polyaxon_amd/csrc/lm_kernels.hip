@@ -16,6 +16,8 @@
 //                      (64-column tiles x row splits, fp32 partials, last-arriving split reduces them in a fixed
 //                      order: deterministic).  The generic column reduction it replaces ran ~26 us per GPT-2 bias at
 //                      16k tokens, several times the 25-100 MB read.
+//   plx_gelu_bwd_colsum GPT-2 MLP: dh = dA * gelu_tanh'(h) and the up-projection's bias gradient (column sums of
+//                      dh) in one pass -- replaces the activation-backward kernel plus a separate read of dh.
 //
 // Llama RoPE convention (rotate the two halves of each head): for j < D/2
 //   y[j] = x[j] c_j - x[j+D/2] s_j,  y[j+D/2] = x[j] s_j + x[j+D/2] c_j,  c_j = cos(pos * theta^(-2j/D)).
@@ -301,8 +303,20 @@ __global__ __launch_bounds__(kBlock) void xent_bwd_kernel(const uint16_t* __rest
 // stream-ordered.
 constexpr int kCsGroups = 32;
 
+// GELU (tanh approximation, GPT-2) derivative: d/dh [0.5 h (1 + tanh(u))], u = sqrt(2/pi) (h + 0.044715 h^3)
+__device__ __forceinline__ float gelu_tanh_grad(float h) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float t = tanhf(k0 * fmaf(k1 * h * h, h, h));
+  return fmaf(0.5f, 1.f + t, 0.5f * h * (1.f - t * t) * k0 * fmaf(3.f * k1, h * h, 1.f));
+}
+
+// GELU = true: x is dA (the gradient of gelu(h)) and the kernel also writes dh = dA * gelu'(h) (bf16, rounded
+// before it is summed, so the bias gradient is the column sum of exactly the dh the GEMMs read) -- the activation
+// backward and the up-projection's bias gradient in one pass over dA and h.
+template <bool GELU>
 __global__ __launch_bounds__(kBlock) void colsum_kernel(const bf16x8* __restrict__ x, int64_t T, int N, int rpb,
-                                                        float* part, unsigned* cnt, void* out, int out_f32) {
+                                                        float* part, unsigned* cnt, void* out, int mode,
+                                                        const bf16x8* __restrict__ h, bf16x8* __restrict__ dh) {
   const int N8 = N >> 3;
   const int cl = threadIdx.x & 7, rg = threadIdx.x >> 3;
   const int ch = blockIdx.x * 8 + cl;
@@ -314,11 +328,21 @@ __global__ __launch_bounds__(kBlock) void colsum_kernel(const bf16x8* __restrict
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
   if (ch < N8) {
     for (int64_t r = r0 + rg; r < r1; r += 4 * kCsGroups) {  // 4 row segments in flight per lane
-      bf16x8 v[4];
+      bf16x8 v[4], hv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t rr = r + u * kCsGroups;
         v[u] = rr < r1 ? x[rr * N8 + ch] : bf16x8{};
+        if (GELU) hv[u] = rr < r1 ? h[rr * N8 + ch] : bf16x8{};
+      }
+      if (GELU) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[u].v[j] = f2bf(bf2f(v[u].v[j]) * gelu_tanh_grad(bf2f(hv[u].v[j])));
+          const int64_t rr = r + u * kCsGroups;
+          if (rr < r1) dh[rr * N8 + ch] = v[u];
+        }
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
@@ -371,7 +395,9 @@ __global__ __launch_bounds__(kBlock) void colsum_kernel(const bf16x8* __restrict
   __syncthreads();
   if (g == 0 && col < N) {
     const float v = ((sf[0][lc] + sf[1][lc]) + sf[2][lc]) + sf[3][lc];
-    if (out_f32)
+    if (mode == 2)
+      ((float*)out)[col] += v;
+    else if (mode == 1)
       ((float*)out)[col] = v;
     else
       ((uint16_t*)out)[col] = f2bf(v);
@@ -441,15 +467,28 @@ PLX_API int plx_colsum_splits(int64_t T, int N) {
   return (int)((T + rpb - 1) / rpb);
 }
 
-// out[N] (fp32 if out_f32 else bf16) = column sums of x bf16 [T][N] (N % 8 == 0, 16-byte aligned rows);
+// out[N] = column sums (mode 0: bf16 store, 1: fp32 store, 2: fp32 accumulate into out) of x bf16 [T][N] (N % 8 == 0, 16-byte aligned rows);
 // part: fp32 [plx_colsum_splits(T, N)][N]; cnt: >= ceil(N/64) zeroed counters
-PLX_API int plx_colsum(const void* x, int64_t T, int N, float* part, unsigned* cnt, void* out, int out_f32,
+PLX_API int plx_colsum(const void* x, int64_t T, int N, float* part, unsigned* cnt, void* out, int mode,
                        hipStream_t stream) {
-  if (T <= 0 || N <= 0 || N % 8 || ((uintptr_t)x & 15)) return 1;
+  if (T <= 0 || N <= 0 || N % 8 || ((uintptr_t)x & 15) || mode < 0 || mode > 2) return 1;
   const int R0 = plx_colsum_splits(T, N);
   const int rpb = (int)((T + R0 - 1) / R0);
   const int R = (int)((T + rpb - 1) / rpb);
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64, R), dim3(kBlock), 0, stream, (const bf16x8*)x, T, N, rpb, part,
-                     cnt, out, out_f32);
+  hipLaunchKernelGGL(colsum_kernel<false>, dim3((N + 63) / 64, R), dim3(kBlock), 0, stream, (const bf16x8*)x, T, N, rpb,
+                     part, cnt, out, mode, nullptr, nullptr);
+  return (int)hipGetLastError();
+}
+
+// dh = dA * gelu_tanh'(h) (bf16 [T][N], written) and out = column sums of dh (modes as plx_colsum); same workspace
+PLX_API int plx_gelu_bwd_colsum(const void* da, const void* h, void* dh, int64_t T, int N, float* part, unsigned* cnt,
+                                void* out, int mode, hipStream_t stream) {
+  if (T <= 0 || N <= 0 || N % 8 || (((uintptr_t)da | (uintptr_t)h | (uintptr_t)dh) & 15) || mode < 0 || mode > 2)
+    return 1;
+  const int R0 = plx_colsum_splits(T, N);
+  const int rpb = (int)((T + R0 - 1) / R0);
+  const int R = (int)((T + rpb - 1) / rpb);
+  hipLaunchKernelGGL(colsum_kernel<true>, dim3((N + 63) / 64, R), dim3(kBlock), 0, stream, (const bf16x8*)da, T, N, rpb,
+                     part, cnt, out, mode, (const bf16x8*)h, (bf16x8*)dh);
   return (int)hipGetLastError();
 }

@@ -235,6 +235,212 @@ __global__ __launch_bounds__(kBlock) void ln_bwd_kernel(const bf16x8* __restrict
     }
   }
 }
+
+// Narrow rows (GPT-2: d = 768 -> 96 vectors) leave most of a 256-thread workgroup idle and pay two LDS barriers per
+// row: there one WAVE owns a row (VPL 16-byte vectors per lane, d <= 64 * 8 * VPL), statistics are wave shuffles
+// only, and the 4 waves of a workgroup walk independent rows.  Backward column partials stay in registers per wave
+// and are combined through LDS once per workgroup at the end.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int VPL>
+__global__ __launch_bounds__(kBlock) void ln_fwd_wave_kernel(const bf16x8* __restrict__ x, const float* __restrict__ w,
+                                                             const float* __restrict__ bias, bf16x8* __restrict__ y,
+                                                             float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                             int64_t rows, int dv, float eps) {
+  const int lane = threadIdx.x & 63;
+  const float inv_d = 1.f / (float)(dv * 8);
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t r = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); r < rows; r += nw) {
+    const bf16x8* xr = x + r * dv;
+    float xs[VPL][8];
+    float s1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int i = lane + j * 64;
+      const bf16x8 v = i < dv ? xr[i] : bf16x8{};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        xs[j][k] = bf2f(v.v[k]);
+        s1 += xs[j][k];
+      }
+    }
+    const float mean = wave_sum(s1) * inv_d;
+    float s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      if (lane + j * 64 < dv) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float c = xs[j][k] - mean;
+          s2 = fmaf(c, c, s2);
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(s2) * inv_d + eps);
+    if (lane == 0) {
+      mean_out[r] = mean;
+      rstd_out[r] = rstd;
+    }
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int i = lane + j * 64;
+      if (i < dv) {
+        bf16x8 o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o.v[k] = f2bf(fmaf((xs[j][k] - mean) * rstd, w[i * 8 + k], bias[i * 8 + k]));
+        y[r * dv + i] = o;
+      }
+    }
+  }
+}
+
+template <int VPL>
+__global__ __launch_bounds__(kBlock) void ln_bwd_wave_kernel(const bf16x8* __restrict__ x, const float* __restrict__ w,
+                                                             const bf16x8* __restrict__ dy,
+                                                             const float* __restrict__ mean_in,
+                                                             const float* __restrict__ rstd_in, bf16x8* __restrict__ dx,
+                                                             float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                             int64_t rows, int dv) {
+  __shared__ float shw[kBlock / 64][VPL * 64 * 8];
+  __shared__ float shb[kBlock / 64][VPL * 64 * 8];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float inv_d = 1.f / (float)(dv * 8);
+  float dwacc[VPL][8], dbacc[VPL][8];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dwacc[j][k] = dbacc[j][k] = 0.f;
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t r = (int64_t)blockIdx.x * (kBlock / 64) + wv; r < rows; r += nw) {
+    const float mean = mean_in[r], rstd = rstd_in[r];
+    float xh[VPL][8], gw[VPL][8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int i = lane + j * 64;
+      if (i < dv) {
+        const bf16x8 xv = x[r * dv + i], gv = dy[r * dv + i];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float g = bf2f(gv.v[k]);
+          xh[j][k] = (bf2f(xv.v[k]) - mean) * rstd;
+          gw[j][k] = g * w[i * 8 + k];
+          sg += gw[j][k];
+          sgx = fmaf(gw[j][k], xh[j][k], sgx);
+          dwacc[j][k] = fmaf(g, xh[j][k], dwacc[j][k]);
+          dbacc[j][k] += g;
+        }
+      }
+    }
+    const float mg = wave_sum(sg) * inv_d;
+    const float mgx = wave_sum(sgx) * inv_d;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+      const int i = lane + j * 64;
+      if (i < dv) {
+        bf16x8 o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o.v[k] = f2bf(rstd * (gw[j][k] - mg - xh[j][k] * mgx));
+        dx[r * dv + i] = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int i = lane + j * 64;
+    if (i < dv) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        shw[wv][i * 8 + k] = dwacc[j][k];
+        shb[wv][i * 8 + k] = dbacc[j][k];
+      }
+    }
+  }
+  __syncthreads();
+  const int d = dv * 8;
+  for (int c = threadIdx.x; c < d; c += kBlock) {  // the 4 waves' columns in wave order
+    dw_part[(int64_t)blockIdx.x * d + c] = ((shw[0][c] + shw[1][c]) + shw[2][c]) + shw[3][c];
+    db_part[(int64_t)blockIdx.x * d + c] = ((shb[0][c] + shb[1][c]) + shb[2][c]) + shb[3][c];
+  }
+}
+
+// ----------------------------------------------------------------------------- partial rows -> parameter gradient
+// The backward kernels leave fp32 [nb][d] partial rows of dw (and db); this sums up to two such matrices column-wise
+// into their outputs in ONE launch: grid (ceil(d/64), R row splits of 64, nz matrices), block = 64 columns x 4 row
+// groups (a wave reads 256 contiguous bytes per row), level-2 rows published with the split-K last-arriver hand-off
+// (drain, agent-scope release, relaxed ticket, acquire; the last arriver resets its counter) and summed by the last
+// split in split order: deterministic.  out = sum (store) or out += sum (accumulate: the parameter's flat gradient
+// slot, instead of autograd's separate `grad += g` pass).  Replaces a strided torch reduction (~19 us at nb = 1024,
+// d = 768) plus one accumulate kernel per parameter.
+constexpr int kPsRows = 64;
+
+__global__ __launch_bounds__(kBlock) void partial_colsum_kernel(const float* __restrict__ p0, const float* __restrict__ p1,
+                                                                int rows, int d, float* l2, unsigned* cnt, float* o0,
+                                                                float* o1, int acc0, int acc1) {
+  const int z = blockIdx.z;
+  const float* p = z ? p1 : p0;
+  const int lc = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lc;
+  const int R = gridDim.y, s = blockIdx.y;
+  const int r0 = s * kPsRows;
+  const int r1 = r0 + kPsRows < rows ? r0 + kPsRows : rows;
+  float a = 0.f;
+  if (c < d) {
+    float x[kPsRows / 4];
+#pragma unroll
+    for (int u = 0; u < kPsRows / 4; ++u) {
+      const int r = r0 + g + 4 * u;
+      x[u] = r < r1 ? p[(int64_t)r * d + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kPsRows / 4; ++u) a += x[u];
+  }
+  __shared__ float sh[4][64];
+  __shared__ int s_last;
+  sh[g][lc] = a;
+  __syncthreads();
+  float* l2z = l2 + (int64_t)z * R * d;
+  if (g == 0 && c < d) l2z[(int64_t)s * d + c] = ((sh[0][lc] + sh[1][lc]) + sh[2][lc]) + sh[3][lc];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* ctr = cnt + (int64_t)z * gridDim.x + blockIdx.x;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (unsigned)(R - 1);
+    if (last) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  float b = 0.f;
+  if (c < d) {
+    for (int r = g; r < R; r += 32) {  // 8 level-2 rows in flight per lane
+      float y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) y[u] = r + 4 * u < R ? l2z[(int64_t)(r + 4 * u) * d + c] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) b += y[u];
+    }
+  }
+  __syncthreads();
+  sh[g][lc] = b;
+  __syncthreads();
+  if (g == 0 && c < d) {
+    const float v = ((sh[0][lc] + sh[1][lc]) + sh[2][lc]) + sh[3][lc];
+    float* o = z ? o1 : o0;
+    o[c] = (z ? acc1 : acc0) ? o[c] + v : v;
+  }
+}
 }  // namespace
 
 PLX_API int plx_rms_forward(const void* x, const float* w, void* y, float* rstd, int64_t rows, int d, float eps,
@@ -258,20 +464,60 @@ PLX_API int plx_rms_backward(const void* x, const float* w, const void* dy, cons
 }
 
 // LayerNorm: mean / rstd fp32 [rows] saved for the backward
+static int g_ln_wave = 1;  // plx_set_ln_wave(0): the workgroup-per-row kernels for every width (A/B)
+PLX_API void plx_set_ln_wave(int on) { g_ln_wave = on != 0; }
+
+// wave-per-row path: 16-byte vectors per lane (1 or 2: d <= 1024), 0 = workgroup-per-row kernels
+static inline int ln_vpl(int d) { return !g_ln_wave ? 0 : d <= 512 ? 1 : d <= 1024 ? 2 : 0; }
+
 PLX_API int plx_ln_forward(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
                            int64_t rows, int d, float eps, hipStream_t stream) {
   if (d % 8 || d > kBlock * 8 * kMaxVecPerLane || rows <= 0) return 1;
+  const int vpl = ln_vpl(d);
+  if (vpl) {
+    int64_t g = (rows + 3) / 4;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(vpl == 1 ? ln_fwd_wave_kernel<1> : ln_fwd_wave_kernel<2>, dim3((int)g), dim3(kBlock), 0, stream,
+                       (const bf16x8*)x, w, b, (bf16x8*)y, mean, rstd, rows, d / 8, eps);
+    return (int)hipGetLastError();
+  }
   int64_t g = rows < 4096 ? rows : 4096;
   hipLaunchKernelGGL(ln_fwd_kernel, dim3((int)g), dim3(kBlock), 0, stream, (const bf16x8*)x, w, b, (bf16x8*)y, mean,
                      rstd, rows, d / 8, eps);
   return (int)hipGetLastError();
 }
 
-// dw / db partials [plx_rms_bwd_blocks(rows), d] each, summed by the host side
+// partial rows plx_ln_backward writes: [plx_ln_bwd_blocks(rows, d), d] for dw and for db
+PLX_API int plx_ln_bwd_blocks(int64_t rows, int d) {
+  if (ln_vpl(d)) {
+    const int64_t g = (rows + 3) / 4;
+    return (int)(g < 1024 ? g : 1024);
+  }
+  return plx_rms_bwd_blocks(rows);
+}
+
+// dw / db partials [plx_ln_bwd_blocks(rows, d), d] each, summed by plx_partial_colsum
 PLX_API int plx_ln_backward(const void* x, const float* w, const void* dy, const float* mean, const float* rstd,
                             void* dx, float* dw_part, float* db_part, int64_t rows, int d, hipStream_t stream) {
   if (d % 8 || d > kBlock * 8 * kMaxVecPerLane || rows <= 0) return 1;
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(plx_rms_bwd_blocks(rows)), dim3(kBlock), 0, stream, (const bf16x8*)x, w,
+  const int vpl = ln_vpl(d);
+  auto k = vpl == 1 ? ln_bwd_wave_kernel<1> : vpl == 2 ? ln_bwd_wave_kernel<2> : ln_bwd_kernel;
+  hipLaunchKernelGGL(k, dim3(plx_ln_bwd_blocks(rows, d)), dim3(kBlock), 0, stream, (const bf16x8*)x, w,
                      (const bf16x8*)dy, mean, rstd, (bf16x8*)dx, dw_part, db_part, rows, d / 8);
+  return (int)hipGetLastError();
+}
+
+// level-2 workspace floats for plx_partial_colsum: nz * ceil(rows / 64) * d
+PLX_API int64_t plx_partial_colsum_workspace(int rows, int d, int nz) {
+  return (int64_t)nz * ((rows + kPsRows - 1) / kPsRows) * d;
+}
+
+// o_z[c] (+)= sum_r p_z[r][c] for z < nz (1 or 2); cnt: >= nz * ceil(d/64) zeroed counters (stream-ordered reuse)
+PLX_API int plx_partial_colsum(const float* p0, const float* p1, int rows, int d, int nz, float* l2, unsigned* cnt,
+                               float* o0, float* o1, int acc0, int acc1, hipStream_t stream) {
+  if (rows <= 0 || d <= 0 || nz < 1 || nz > 2) return 1;
+  const int R = (rows + kPsRows - 1) / kPsRows;
+  hipLaunchKernelGGL(partial_colsum_kernel, dim3((d + 63) / 64, R, nz), dim3(kBlock), 0, stream, p0, p1, rows, d, l2,
+                     cnt, o0, o1, acc0, acc1);
   return (int)hipGetLastError();
 }

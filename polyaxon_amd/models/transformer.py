@@ -143,11 +143,10 @@ class MLP(nn.Module):
         self.down = nn.Linear(cfg.d_ff, cfg.d_model, bias=cfg.bias)
 
     def forward(self, x):
-        h = lm_ops.linear(x, self.up.weight, self.up.bias)
         if self.kind == "swiglu":
-            h = lm_ops.swiglu(h)
-        else:
-            h = F.gelu(h, approximate="tanh")
+            h = lm_ops.swiglu(lm_ops.linear(x, self.up.weight, self.up.bias))
+        else:  # GELU inside the op: its backward and the up-projection's bias gradient are one pass
+            h = lm_ops.linear(x, self.up.weight, self.up.bias, act="gelu_tanh")
         return lm_ops.linear(h, self.down.weight, self.down.bias)
 
 

@@ -123,6 +123,21 @@ def available(name: str) -> bool:
 _SIZES: Dict[tuple, int] = {}
 
 
+_COUNTERS: Dict[tuple, object] = {}
+
+
+def counters(device, key: str, n: int = 4096):
+    """A zeroed int32 counter array per (device, op) for the last-arriver kernels: each arriver that finishes a
+    reduction resets its own counter, so the array is reused by every stream-ordered launch of that op."""
+    import torch
+
+    k = (str(device), key)
+    c = _COUNTERS.get(k)
+    if c is None:
+        c = _COUNTERS[k] = torch.zeros(n, dtype=torch.int32, device=device)
+    return c
+
+
 def current_stream() -> int:
     """Raw handle of the current HIP stream of the current device: two C calls, against ~8 us for
     ``torch.cuda.current_stream().cuda_stream`` (a Python Stream object and device-index resolution per call) --
@@ -162,6 +177,8 @@ def lib(name: str) -> ctypes.CDLL:
             handle.plx_set_tn_stages(int(st), int(bk or 0))
         if name == "plx_bn" and os.environ.get("PLX_STEM_BWD_CAP"):  # A/B knob: stem backward partials-pass rows
             handle.plx_set_stem_bwd_cap(int(os.environ["PLX_STEM_BWD_CAP"]))
+        if name == "plx_rms" and os.environ.get("PLX_LN_WAVE"):  # A/B knob: wave-per-row LayerNorm (d <= 1024)
+            handle.plx_set_ln_wave(int(os.environ["PLX_LN_WAVE"]))
         if name == "plx_bn" and os.environ.get("PLX_BN_FIN_THREADS"):  # A/B knob: 256-thread BN finalize
             handle.plx_set_bn_fin_threads(int(os.environ["PLX_BN_FIN_THREADS"]))
         if name == "plx_conv" and os.environ.get("PLX_NT_TALL"):  # A/B knob: 256x128 NT tiles (0 / 1 fwd / 2 +dgrad)
@@ -275,6 +292,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_xent_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
         "plx_colsum_splits": [_L, _I],
         "plx_colsum": [_P, _L, _I, _P, _P, _P, _I, _P],
+        "plx_gelu_bwd_colsum": [_P, _P, _P, _L, _I, _P, _P, _P, _I, _P],
     },
     "plx_gemm": {
         "plx_gemm256": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
@@ -298,6 +316,10 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
     "plx_rms": {
         "plx_rms_forward": [_P, _P, _P, _P, _L, _I, _F, _P],
         "plx_rms_bwd_blocks": [_L],
+        "plx_ln_bwd_blocks": [_L, _I],
+        "plx_set_ln_wave": [_I],
+        "plx_partial_colsum_workspace": [_I, _I, _I],
+        "plx_partial_colsum": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _P],
         "plx_rms_backward": [_P, _P, _P, _P, _P, _P, _L, _I, _P],
         "plx_ln_forward": [_P, _P, _P, _P, _P, _P, _L, _I, _F, _P],
         "plx_ln_backward": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
@@ -322,7 +344,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_set_stem_bwd_cap": None, "plx_set_bn_fin_threads": None, "plx_set_adamw_grid_cap": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_partial_colsum_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_set_stem_bwd_cap": None, "plx_set_bn_fin_threads": None, "plx_set_ln_wave": None, "plx_set_adamw_grid_cap": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

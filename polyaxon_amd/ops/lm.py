@@ -167,102 +167,151 @@ def next_token_xent(logits: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------------------------------------- bias gradient
-_COLSUM_CNT: dict = {}
 _COLSUM = os.environ.get("PLX_COLSUM", "1") != "0"  # A/B knob: 0 = torch's column reduction
 
 
-def bias_grad(dy2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
-    """db = dy2.sum(0) for a bias of ``dtype``: the deterministic one-launch column sum (csrc/lm_kernels.hip
-    plx_colsum, fp32 accumulation) for a contiguous bf16 CUDA [T, N] with N % 8 == 0; torch's reduction otherwise."""
+def bias_grad(dy2: torch.Tensor, bias: torch.Tensor, gelu_h: Optional[torch.Tensor] = None):
+    """db = dy2.sum(0) for ``bias``.  With a direct fp32 flat-gradient slot (ops/flat.py) the sum is written -- or,
+    for a slot already written this step, accumulated -- there and None is returned (no autograd ``grad += g``
+    kernel; FlatDDP still sees the parameter through its post-accumulate hook); otherwise returned in the bias
+    dtype.  The sum
+    is the deterministic one-launch column reduction (csrc/lm_kernels.hip plx_colsum, fp32 accumulation) for a
+    contiguous bf16 CUDA [T, N] with N % 8 == 0, torch's reduction otherwise.
+
+    ``gelu_h``: dy2 is the gradient of gelu_tanh(gelu_h); returns (dh, db) with dh = dy2 * gelu_tanh'(gelu_h)
+    computed in the same pass as its column sums (plx_gelu_bwd_colsum)."""
+    from polyaxon_amd.ops.flat import direct_grad
+
     T, N = dy2.shape
-    if not (_COLSUM and _native_ok(dy2) and dy2.is_contiguous() and N % 8 == 0 and dy2.data_ptr() % 16 == 0 and T > 0
-            and dtype in (torch.float32, torch.bfloat16) and (N + 63) // 64 <= 4096):
-        return dy2.sum(0).to(dtype)
-    lib = _native.lib("plx_lm")
-    dev = dy2.device
-    cnt = _COLSUM_CNT.get(dev)
-    if cnt is None:
-        cnt = _COLSUM_CNT[dev] = torch.zeros(4096, dtype=torch.int32, device=dev)
-    part = torch.empty(lib.plx_colsum_splits(T, N), N, dtype=torch.float32, device=dev)
-    out = torch.empty(N, dtype=dtype, device=dev)
-    _native.check(lib.plx_colsum(dy2.data_ptr(), T, N, part.data_ptr(), cnt.data_ptr(), out.data_ptr(),
-                                 int(dtype == torch.float32), _stream()), "plx_colsum")
-    return out
+    slot = direct_grad(bias)
+    if slot is not None and not (slot.dtype == torch.float32 and slot.is_contiguous() and slot.numel() == N
+                                 and slot.device == dy2.device):
+        slot = None
+    acc = bool(bias._plx_flat.mark_written(slot)) if slot is not None else False
+    native = (_COLSUM and _native_ok(dy2) and dy2.is_contiguous() and N % 8 == 0 and dy2.data_ptr() % 16 == 0
+              and T > 0 and (N + 63) // 64 <= 4096 and (slot is not None or bias.dtype in (torch.float32, torch.bfloat16)))
+    if gelu_h is not None:
+        native = (native and gelu_h.dtype == torch.bfloat16 and gelu_h.is_contiguous() and gelu_h.shape == dy2.shape
+                  and gelu_h.data_ptr() % 16 == 0)
+    dh = None
+    if native:
+        lib = _native.lib("plx_lm")
+        dev = dy2.device
+        part = torch.empty(lib.plx_colsum_splits(T, N), N, dtype=torch.float32, device=dev)
+        out = slot if slot is not None else torch.empty(N, dtype=bias.dtype, device=dev)
+        mode = (2 if acc else 1) if out.dtype == torch.float32 else 0
+        cnt = _native.counters(dev, "plx_colsum")
+        if gelu_h is None:
+            _native.check(lib.plx_colsum(dy2.data_ptr(), T, N, part.data_ptr(), cnt.data_ptr(), out.data_ptr(), mode,
+                                         _stream()), "plx_colsum")
+        else:
+            dh = torch.empty_like(dy2)
+            _native.check(lib.plx_gelu_bwd_colsum(dy2.data_ptr(), gelu_h.data_ptr(), dh.data_ptr(), T, N,
+                                                  part.data_ptr(), cnt.data_ptr(), out.data_ptr(), mode, _stream()),
+                          "plx_gelu_bwd_colsum")
+    else:
+        if gelu_h is not None:
+            dy2 = dh = torch.ops.aten.gelu_backward(dy2, gelu_h, approximate="tanh")
+        if slot is not None:
+            with torch.no_grad():
+                s = dy2.sum(0, dtype=torch.float32)
+                slot.add_(s) if acc else slot.copy_(s)
+        else:
+            out = dy2.sum(0).to(bias.dtype)
+    db = out if slot is None else None
+    return db if gelu_h is None else (dh, db)
+
+
+def _act_backward(ctx, dy2: torch.Tensor, h2: Optional[torch.Tensor]):
+    """(dz, db) of a Linear (+ optional GELU) from the output gradient: with the activation fused, dz = dA * gelu'(h)
+    and the bias gradient come out of one pass; otherwise dz = dy and db is the plain column sum."""
+    if h2 is not None:
+        if ctx.has_bias:
+            return bias_grad(dy2, ctx.bias, gelu_h=h2)
+        return torch.ops.aten.gelu_backward(dy2, h2, approximate="tanh"), None
+    return dy2, (bias_grad(dy2, ctx.bias) if ctx.has_bias else None)
 
 
 # ---------------------------------------------------------------------------------------------- direct-grad Linear
 class _LinearDirect(torch.autograd.Function):
-    """y = x W^T (+ b).  Backward writes dW = dy^T x with the GEMM's output pointer on the parameter's flat
-    gradient slot (``p.grad``, bf16 in lp mode): no separate gradient tensor and no autograd ``grad += g``
-    read-modify-write.  The flat buffer is zeroed by the optimizer, so the first write of a step is a plain
-    GEMM (beta = 0) and any later one (a weight used twice) accumulates (beta = 1)."""
+    """y = x W^T (+ b), optionally followed by GELU (tanh; ``act``).  Backward writes dW = dz^T x with the GEMM's
+    output pointer on the parameter's flat gradient slot (``p.grad``, bf16 in lp mode): no separate gradient tensor
+    and no autograd ``grad += g`` read-modify-write.  The flat buffer is zeroed by the optimizer, so the first write
+    of a step is a plain GEMM (beta = 0) and any later one (a weight used twice) accumulates (beta = 1).  With the
+    activation fused, its backward and the bias gradient are one pass (``bias_grad(..., gelu_h=h)``)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, slot, flat):
-        ctx.save_for_backward(x, weight)
+    def forward(ctx, x, weight, bias, slot, flat, act=None):
         ctx.slot, ctx.flat, ctx.has_bias = slot, flat, bias is not None
-        ctx.bias_dtype = bias.dtype if bias is not None else None
-        return F.linear(x, weight, bias)
+        ctx.bias, ctx.act = bias, act
+        y = F.linear(x, weight, bias)
+        if act is None:
+            ctx.save_for_backward(x, weight)
+            return y
+        ctx.save_for_backward(x, weight, y)
+        return F.gelu(y, approximate="tanh")
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
-        dx = dy @ weight if ctx.needs_input_grad[0] else None
-        dy2 = dy.reshape(-1, dy.shape[-1])
+        x, weight, *h = ctx.saved_tensors
+        n = dy.shape[-1]
+        dy2, db = _act_backward(ctx, dy.reshape(-1, n).contiguous() if h else dy.reshape(-1, n),
+                                h[0].reshape(-1, n) if h else None)
+        dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1]) if ctx.needs_input_grad[0] else None
         x2 = x.reshape(-1, x.shape[-1]).to(dy2.dtype)
         g = ctx.slot
         if ctx.flat.mark_written(g):
             torch.addmm(g, dy2.t(), x2, out=g)
         else:
             torch.mm(dy2.t(), x2, out=g)
-        db = bias_grad(dy2, ctx.bias_dtype) if ctx.has_bias else None
-        cb = getattr(weight, "_plx_ready_cb", None)
-        if cb is not None:
-            cb(weight)
-        return dx, None, db, None, None
+        return dx, None, db, None, None, None
 
 
 class _LinearMfma(torch.autograd.Function):
-    """y = x W^T (+ b) with forward, data-gradient and weight-gradient GEMMs on the hand-written 256x256 MFMA kernel
-    (ops/gemm.py, csrc/gemm256.hip).  ``slot``/``flat`` as in :class:`_LinearDirect`: when given, dW is written
-    (or, for a weight already written this step, accumulated by the kernel's epilogue) straight into the flat
-    gradient slot."""
+    """y = x W^T (+ b) (then GELU with ``act``) with forward, data-gradient and weight-gradient GEMMs on the
+    hand-written 256x256 MFMA kernel (ops/gemm.py, csrc/gemm256.hip).  ``slot``/``flat`` as in
+    :class:`_LinearDirect`: when given, dW is written (or, for a weight already written this step, accumulated by
+    the kernel's epilogue) straight into the flat gradient slot."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, slot, flat):
+    def forward(ctx, x, weight, bias, slot, flat, act=None):
         from polyaxon_amd.ops import gemm
 
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
-        ctx.save_for_backward(x2, weight)
         ctx.slot, ctx.flat, ctx.has_bias, ctx.xshape = slot, flat, bias is not None, x.shape
-        ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.bias, ctx.act = bias, act
         y = gemm.forward(x2, weight, bias)
+        if act is None:
+            ctx.save_for_backward(x2, weight)
+        else:
+            ctx.save_for_backward(x2, weight, y)
+            y = F.gelu(y, approximate="tanh")
         return y.view(*x.shape[:-1], weight.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         from polyaxon_amd.ops import gemm
 
-        x2, weight = ctx.saved_tensors
-        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        x2, weight, *h = ctx.saved_tensors
+        dy2, db = _act_backward(ctx, dy.reshape(-1, dy.shape[-1]).contiguous(), h[0] if h else None)
         dx = gemm.dgrad(dy2, weight).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.slot is not None:
             g = ctx.slot
             gemm.wgrad(dy2, x2, out=g, accumulate=bool(ctx.flat.mark_written(g)))
-            cb = getattr(weight, "_plx_ready_cb", None)
-            if cb is not None:
-                cb(weight)
         elif ctx.needs_input_grad[1]:
             dw = gemm.wgrad(dy2, x2)
-        db = bias_grad(dy2, ctx.bias_dtype) if ctx.has_bias else None
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+           act: Optional[str] = None) -> torch.Tensor:
     """F.linear on the MFMA GEMM kernel when the shapes fit it (ops/gemm.py: tokens, in and out multiples of 256,
     bf16, PLX_LM_GEMM != 0), with the weight gradient written into the flat gradient slot when ``weight`` is a flat
-    parameter in lp mode with direct grads; hipBLASLt (F.linear / the direct-gradient form) otherwise."""
+    parameter in lp mode with direct grads; hipBLASLt (F.linear / the direct-gradient form) otherwise.
+    ``act="gelu_tanh"`` applies GPT-2's GELU inside the op, so its backward is fused with the bias gradient."""
+    if act not in (None, "gelu_tanh"):
+        raise ValueError(f"unknown activation {act!r}")
     if (x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.bfloat16
             and torch.is_autocast_enabled("cuda")):
         x = x.to(torch.bfloat16)  # what autocast's F.linear does; here it keeps the LayerNorm outputs on the MFMA path
@@ -275,8 +324,9 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
 
     if weight.is_contiguous() and gemm.linear_supported(x, weight):
         if direct:
-            return _LinearMfma.apply(x, weight, bias, slot, flat)
-        return _LinearMfma.apply(x, weight, bias, None, None)
+            return _LinearMfma.apply(x, weight, bias, slot, flat, act)
+        return _LinearMfma.apply(x, weight, bias, None, None, act)
     if direct:
-        return _LinearDirect.apply(x, weight, bias, slot, flat)
-    return F.linear(x, weight, bias)
+        return _LinearDirect.apply(x, weight, bias, slot, flat, act)
+    y = F.linear(x, weight, bias)
+    return y if act is None else F.gelu(y, approximate="tanh")

@@ -2,6 +2,8 @@
 statistics and parameters), PyTorch composition otherwise."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from polyaxon_amd.ops import _native
@@ -17,6 +19,42 @@ def _stream() -> int:
     return _native.current_stream()
 
 
+_NORM_DIRECT = os.environ.get("PLX_NORM_DIRECT", "1") != "0"  # A/B knob: 0 = return the sums to autograd
+
+
+def _param_grads(parts, params, d: int):
+    """Column sums of the backward kernel's fp32 [nb, d] partial matrices (one per parameter) in one launch
+    (csrc/rmsnorm.hip plx_partial_colsum).  A parameter with a direct fp32 flat-gradient slot (ops/flat.py) gets its
+    sum written -- or, for a slot already written this step, accumulated -- there and None is returned for it (no
+    autograd ``grad += g`` kernel; FlatDDP still sees the parameter through its post-accumulate hook); otherwise the sum is
+    returned in the parameter's dtype."""
+    from polyaxon_amd.ops.flat import direct_grad
+
+    lib = _native.lib("plx_rms")
+    dev = parts[0].device
+    nb = parts[0].shape[0]
+    outs, accs, ret = [], [], []
+    for p in params:
+        slot = direct_grad(p) if _NORM_DIRECT else None
+        if (slot is not None and slot.dtype == torch.float32 and slot.is_contiguous() and slot.numel() == d
+                and slot.device == dev):
+            accs.append(int(p._plx_flat.mark_written(slot)))
+            outs.append(slot)
+            ret.append(None)
+        else:
+            t = torch.empty(d, dtype=torch.float32, device=dev)
+            accs.append(0)
+            outs.append(t)
+            ret.append(t)
+    nz = len(parts)
+    l2 = torch.empty(int(lib.plx_partial_colsum_workspace(nb, d, nz)), dtype=torch.float32, device=dev)
+    cnt = _native.counters(dev, "plx_partial_colsum")
+    _native.check(lib.plx_partial_colsum(parts[0].data_ptr(), parts[-1].data_ptr(), nb, d, nz, l2.data_ptr(),
+                                         cnt.data_ptr(), outs[0].data_ptr(), outs[-1].data_ptr(), accs[0], accs[-1],
+                                         _stream()), "plx_partial_colsum")
+    return [r if r is None else r.to(p.dtype) for r, p in zip(ret, params)]
+
+
 class _RMSNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, eps):
@@ -30,7 +68,7 @@ class _RMSNorm(torch.autograd.Function):
         _native.check(lib.plx_rms_forward(x.data_ptr(), w.data_ptr(), y.data_ptr(), rstd.data_ptr(), rows, d,
                                           float(eps), _stream()), "plx_rms_forward")
         ctx.save_for_backward(x, w, rstd)
-        ctx.wdtype = weight.dtype
+        ctx.param = weight
         return y
 
     @staticmethod
@@ -45,7 +83,7 @@ class _RMSNorm(torch.autograd.Function):
         part = torch.empty((nb, d), dtype=torch.float32, device=x.device)
         _native.check(lib.plx_rms_backward(x.data_ptr(), w.data_ptr(), dy.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
                                            part.data_ptr(), rows, d, _stream()), "plx_rms_backward")
-        return dx, part.sum(0).to(ctx.wdtype), None
+        return dx, _param_grads([part], [ctx.param], d)[0], None
 
 
 def supported(x: torch.Tensor) -> bool:
@@ -79,7 +117,7 @@ class _LayerNorm(torch.autograd.Function):
         _native.check(lib.plx_ln_forward(x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), mean.data_ptr(),
                                          rstd.data_ptr(), rows, d, float(eps), _stream()), "plx_ln_forward")
         ctx.save_for_backward(x, w, mean, rstd)
-        ctx.dtypes = (weight.dtype, bias.dtype)
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
@@ -90,13 +128,13 @@ class _LayerNorm(torch.autograd.Function):
         d = x.shape[-1]
         rows = x.numel() // d
         dx = torch.empty_like(x)
-        nb = lib.plx_rms_bwd_blocks(rows)
+        nb = lib.plx_ln_bwd_blocks(rows, d)
         part = torch.empty((2, nb, d), dtype=torch.float32, device=x.device)
         _native.check(lib.plx_ln_backward(x.data_ptr(), w.data_ptr(), dy.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                                           dx.data_ptr(), part[0].data_ptr(), part[1].data_ptr(), rows, d, _stream()),
                       "plx_ln_backward")
-        dwb = part.sum(1)
-        return dx, dwb[0].to(ctx.dtypes[0]), dwb[1].to(ctx.dtypes[1]), None
+        dw, db = _param_grads([part[0], part[1]], list(ctx.params), d)
+        return dx, dw, db, None
 
 
 def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:

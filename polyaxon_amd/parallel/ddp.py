@@ -11,9 +11,10 @@ WORLD_SIZE and call NCCL themselves.  This module is what a polyflow DP trial us
   so communication overlaps the rest of the backward; ``finish()`` waits for the tail;
 * segments are bucketed in reverse registration order so the buckets fill in backward order;
 * lp mode (FlatParams ``lp_dtype=bf16``, the language models): the weight gradients are bf16, so the
-  all-reduce moves half the bytes; buckets never straddle the bf16 / fp32-tail boundary, and the direct
-  weight-gradient GEMMs (ops/lm.py) count their bucket down through ``_plx_ready_cb`` instead of autograd's
-  post-accumulate hook.  (Optimizer-state sharding / ZeRO-1 is not implemented: an 8B model's fp32 master +
+  all-reduce moves half the bytes; buckets never straddle the bf16 / fp32-tail boundary.  Direct-gradient
+  ops (ops/lm.py, ops/rmsnorm.py: GEMM-written weights, bias / norm sums written into the slots) return None and
+  are still counted by autograd's post-accumulate hook, which runs once per parameter per backward after every
+  Function feeding it; each segment counts its bucket down once per step.  (Optimizer-state sharding / ZeRO-1 is not implemented: an 8B model's fp32 master +
   moments are 96 GB, which one 288 GB MI355X holds unsharded.)
 * optimizer in the backward (``optimizer=``, a FusedAdamW): the moment a bucket's gradient is complete (and, with
   DP, its all-reduce is done) the AdamW update of that bucket runs on a side stream, overlapped with the rest of
@@ -112,8 +113,8 @@ class FlatDDP:
         self._side = torch.cuda.Stream(device=flat.device) if (optimizer is not None and flat.params.is_cuda) else None
         self.stepped = 0
         if flat.lp_params is None:
-            # the ResNet native ops write weight grads without telling anyone: bucket readiness then needs
-            # autograd's post-accumulate hooks.  lp-mode direct-gradient GEMMs (ops/lm.py) call _plx_ready_cb.
+            # fp32 (ResNet) mode keeps autograd's accumulation: its native ops' direct writes are not ordered
+            # against the all-reduce streams.  lp-mode direct writes are counted by the same post-accumulate hooks.
             flat.enable_direct_grads(False)
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
@@ -141,12 +142,14 @@ class FlatDDP:
         self._pending = [0] * len(self.buckets)
         self._handles: List = []
         self._hooks = []
+        self._ready: List[bool] = [False] * len(flat.segments)
         if self.overlap:
-            for seg in flat.segments:
+            # autograd runs a parameter's AccumulateGrad node -- and so this hook -- once per backward, after every
+            # Function that feeds it, including direct-gradient ops (ops/lm.py, ops/rmsnorm.py) that wrote the
+            # flat slot themselves and returned None: the hook is the readiness signal for both kinds
+            for i, seg in enumerate(flat.segments):
                 p = flat.parameter(seg.name)
-                hook = self._make_hook(self.seg_bucket[seg.name])
-                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
-                p._plx_ready_cb = hook
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(self.seg_bucket[seg.name], i)))
         self.reset()
 
     def _close(self, segs) -> None:
@@ -159,10 +162,14 @@ class FlatDDP:
 
     def reset(self) -> None:
         self._pending = [n for _, _, n in self.buckets]
+        self._ready = [False] * len(self.flat.segments)
         self._handles = []
 
-    def _make_hook(self, b: int):
+    def _make_hook(self, b: int, seg: int):
         def hook(_p):
+            if self._ready[seg]:  # a segment counts its bucket down once per step
+                return
+            self._ready[seg] = True
             self._pending[b] -= 1
             if self._pending[b] == 0:
                 self._launch(b)
@@ -230,5 +237,3 @@ class FlatDDP:
         for h in self._hooks:
             h.remove()
         self._hooks = []
-        for seg in self.flat.segments:
-            self.flat.parameter(seg.name).__dict__.pop("_plx_ready_cb", None)

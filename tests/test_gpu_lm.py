@@ -159,9 +159,71 @@ def test_bias_grad_colsum_matches_fp32(cuda, T, N, dtype):
     assert _native.available("plx_lm")
     g = torch.Generator(device="cuda").manual_seed(T * 7 + N)
     dy = torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16)
-    out = lm_ops.bias_grad(dy, dtype)
+    bias = torch.zeros(N, dtype=dtype, device="cuda")
+    out = lm_ops.bias_grad(dy, bias)
     assert out.dtype == dtype and out.shape == (N,)
     ref = dy.double().sum(0)
     tol = 1e-4 * T ** 0.5 + (0.01 * ref.abs().max().item() if dtype == torch.bfloat16 else 0.0)
     torch.testing.assert_close(out.double(), ref, rtol=1e-2 if dtype == torch.bfloat16 else 1e-5, atol=tol)
-    assert torch.equal(lm_ops.bias_grad(dy, dtype), out)
+    assert torch.equal(lm_ops.bias_grad(dy, bias), out)
+
+
+def test_direct_bias_and_norm_grads_into_flat_slots(cuda):
+    """lp-mode flat parameters with direct gradients: the Linear bias (plx_colsum) and LayerNorm weight / bias
+    (plx_partial_colsum) gradients land in their fp32 flat slots -- stored by the first backward, accumulated by the
+    second -- and match fp32 autograd of the same computation run twice."""
+    from polyaxon_amd.ops import lm as lm_ops
+    from polyaxon_amd.ops import rmsnorm as rms
+    from polyaxon_amd.ops.flat import FlatParams
+
+    torch.manual_seed(3)
+    d, n, T = 256, 512, 2048
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.norm = rms.LayerNorm(d)
+            self.fc = torch.nn.Linear(d, n)
+
+        def forward(self, x):
+            return lm_ops.linear(self.norm(x), self.fc.weight, self.fc.bias)
+
+    ref = M().cuda()
+    with torch.no_grad():
+        ref.norm.weight.uniform_(0.5, 1.5)
+        ref.norm.bias.normal_()
+        ref.fc.bias.normal_()
+    m = M().cuda()
+    m.load_state_dict(ref.state_dict())
+    flat = FlatParams(m, torch.device("cuda"), lp_dtype=torch.bfloat16)
+    flat.enable_direct_grads(True)
+    flat.zero_grads()
+    x = torch.randn(T, d, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(T, n, device="cuda").to(torch.bfloat16)
+    for _ in range(2):
+        m(x).backward(dy)
+    xr = x.float()
+    for _ in range(2):
+        y = torch.nn.functional.linear(torch.nn.functional.layer_norm(xr, (d,), ref.norm.weight, ref.norm.bias),
+                                       ref.fc.weight.bfloat16().float(), ref.fc.bias)
+        y.backward(dy.float())
+    for name, rp in (("fc.bias", ref.fc.bias), ("norm.weight", ref.norm.weight), ("norm.bias", ref.norm.bias)):
+        slot = flat.parameter(name).grad
+        assert slot.dtype == torch.float32
+        torch.testing.assert_close(slot, rp.grad, rtol=3e-2, atol=3e-2 * rp.grad.abs().max().item()), name
+
+
+@pytest.mark.parametrize("T,N", [(16384, 3072), (777, 264)])
+def test_gelu_backward_bias_fused_matches_fp32(cuda, T, N):
+    """plx_gelu_bwd_colsum (csrc/lm_kernels.hip): dh = dA * gelu_tanh'(h) against fp32 aten.gelu_backward of the same
+    bf16 inputs, and the bias gradient against the fp64 column sum of the dh it wrote."""
+    from polyaxon_amd.ops import lm as lm_ops
+
+    g = torch.Generator(device="cuda").manual_seed(T + N)
+    da = torch.randn(T, N, device="cuda", generator=g).to(torch.bfloat16)
+    h = (torch.randn(T, N, device="cuda", generator=g) * 3).to(torch.bfloat16)
+    bias = torch.zeros(N, device="cuda")
+    dh, db = lm_ops.bias_grad(da, bias, gelu_h=h)
+    ref = torch.ops.aten.gelu_backward(da.float(), h.float(), approximate="tanh")
+    torch.testing.assert_close(dh.float(), ref, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(db.double(), dh.double().sum(0), rtol=1e-5, atol=1e-4 * T ** 0.5)

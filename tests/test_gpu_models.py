@@ -30,7 +30,8 @@ def test_rmsnorm_matches_fp32(cuda, rows, d):
     torch.testing.assert_close(w.grad, wr.grad, rtol=2e-2, atol=2e-2 * rows ** 0.5)
 
 
-@pytest.mark.parametrize("rows,d", [(1, 64), (37, 768), (5000, 768), (3, 8192)])
+@pytest.mark.parametrize("rows,d", [(1, 64), (37, 768), (5000, 768), (6001, 1024), (70000, 512), (4099, 1032),
+                                    (3, 8192)])
 def test_layernorm_matches_fp32(cuda, rows, d):
     """Fused bf16 LayerNorm (csrc/rmsnorm.hip plx_ln_*) vs fp32 F.layer_norm: output, dx, dweight, dbias; an input
     with a large offset exercises the two-pass (mean, then centred variance) statistics."""

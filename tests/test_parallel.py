@@ -168,7 +168,7 @@ def _lp_worker(rank, world, port, q):
     torch.manual_seed(0)
     model = Transformer(tiny_llama())
     flat = FlatParams(model, "cpu", channels_last=False, lp_dtype=torch.bfloat16)
-    flat.enable_direct_grads(True)  # weight grads written by the GEMM; buckets counted down by _plx_ready_cb
+    flat.enable_direct_grads(True)  # weight grads written by the GEMM; buckets counted by post-accumulate hooks
     ddp = FlatDDP(flat, bucket_mb=0.01)
     torch.manual_seed(100 + rank)
     tokens = torch.randint(0, 256, (4, 16))
@@ -255,22 +255,26 @@ def test_direct_grad_linear_matches_autograd():
     torch.testing.assert_close(grads[True][1], grads[False][1], rtol=1e-3, atol=1e-5)
 
 
-def _train_steps(lp, in_backward, steps=3, bucket_mb=0.01):
-    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+def _train_steps(lp, in_backward, steps=3, bucket_mb=0.01, arch="llama", direct=False):
+    from polyaxon_amd.models.transformer import Transformer, gpt2_125m, lm_loss, tiny_llama
     from polyaxon_amd.ops.flat import FlatParams
     from polyaxon_amd.ops.optim import FusedAdamW
     from polyaxon_amd.parallel.ddp import FlatDDP
 
     torch.manual_seed(0)
-    model = Transformer(tiny_llama())
+    cfg = tiny_llama() if arch == "llama" else gpt2_125m(vocab_size=256, n_layers=2, d_model=64, n_heads=2,
+                                                            d_ff=256, max_seq_len=32)
+    model = Transformer(cfg)
     flat = FlatParams(model, "cpu", channels_last=False, lp_dtype=lp)
+    flat.enable_direct_grads(direct)
     opt = FusedAdamW(flat, lr=1e-2, weight_decay=0.1)
     ddp = FlatDDP(flat, bucket_mb=bucket_mb, optimizer=opt if in_backward else None)
     gen = torch.Generator().manual_seed(5)
     losses = []
     for _ in range(steps):
         tokens = torch.randint(0, 256, (4, 16), generator=gen)
-        loss = lm_loss(model(tokens), tokens)
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=lp is not None and arch != "llama"):
+            loss = lm_loss(model(tokens), tokens)
         loss.backward()
         ddp.finish()
         opt.step_()
@@ -293,6 +297,20 @@ def test_optimizer_in_backward_matches_monolithic_step(lp):
         assert float(fb.lp_grads.abs().max()) == 0.0
     assert float(fb.grads.abs().max()) == 0.0
     assert len(ddp.buckets) > 3 and ddp.stepped == 3 * len(ddp.buckets)
+
+
+@pytest.mark.parametrize("arch", ["llama", "gpt2"])
+def test_optimizer_in_backward_direct_grads_shared_buckets(arch):
+    """Direct gradients (GEMM-written weights, bias sums written into their flat slots) with several parameters per
+    bucket: each parameter counts its bucket down exactly once per backward -- autograd's post-accumulate hook also
+    fires for a parameter whose Function returned None -- so no bucket is updated before all of its gradients are
+    in, and the trajectory is bitwise the monolithic step's."""
+    la, fa, _ = _train_steps(torch.bfloat16, False, bucket_mb=0.25, arch=arch, direct=True)
+    lb, fb, ddp = _train_steps(torch.bfloat16, True, bucket_mb=0.25, arch=arch, direct=True)
+    assert any(n > 2 for _, _, n in ddp.buckets)
+    assert la == lb
+    assert torch.equal(fa.params, fb.params) and torch.equal(fa.lp_params, fb.lp_params)
+    assert ddp.stepped == 3 * len(ddp.buckets)
 
 
 def _opt_in_bwd_worker(rank, world, port, q):
