@@ -153,7 +153,9 @@ __global__ __launch_bounds__(NT) void bn_partial_reduce_kernel(const float* __re
 // sums every 4th of the S partial rows (independent loads, fp64 accumulation), then the 4 group sums are combined
 // through LDS in a fixed order (deterministic).  One thread per channel walking all S rows serially was 19 us per
 // backward BatchNorm on the 56x56 layers (S ~ 100 dependent-latency iterations on a single 256-thread block).
-template <int NT = 256>
+// ATOMIC: the rows were published inside this launch by other workgroups (agent-scope atomic stores): read them with
+// agent-scope atomic loads (coherent across the XCDs' L2s without an acquire fence / L2 invalidate)
+template <int NT = 256, bool ATOMIC = false>
 __device__ __forceinline__ bool fin_sum2(const float* __restrict__ pa, const float* __restrict__ pb, int nblk, int C,
                                          double& A, double& B) {
   constexpr int G = NT / 64;  // split lane-groups
@@ -169,8 +171,13 @@ __device__ __forceinline__ bool fin_sum2(const float* __restrict__ pa, const flo
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int r = b + u * G;
-        x[u] = r < nblk ? pa[(int64_t)r * C + c] : 0.f;
-        y[u] = r < nblk ? pb[(int64_t)r * C + c] : 0.f;
+        if (ATOMIC) {
+          x[u] = r < nblk ? __hip_atomic_load(pa + (int64_t)r * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+          y[u] = r < nblk ? __hip_atomic_load(pb + (int64_t)r * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+        } else {
+          x[u] = r < nblk ? pa[(int64_t)r * C + c] : 0.f;
+          y[u] = r < nblk ? pb[(int64_t)r * C + c] : 0.f;
+        }
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) { a0 += x[u]; b0 += y[u]; }
@@ -215,10 +222,10 @@ struct BwdFin {
   int accumulate;
 };
 
-template <int NT>
+template <int NT, bool ATOMIC = false>
 __device__ __forceinline__ void fwd_finalize(const float* psum, const float* psq, int nblk, const FwdFin& f) {
   double S, Q;  // level-2 partials per channel, summed in fp64
-  if (!fin_sum2<NT>(psum, psq, nblk, f.C, S, Q)) return;
+  if (!fin_sum2<NT, ATOMIC>(psum, psq, nblk, f.C, S, Q)) return;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const double m = S / (double)f.M;
   double var = Q / (double)f.M - m * m;
@@ -237,10 +244,10 @@ __device__ __forceinline__ void fwd_finalize(const float* psum, const float* psq
   }
 }
 
-template <int NT>
+template <int NT, bool ATOMIC = false>
 __device__ __forceinline__ void bwd_finalize(const float* pdz, const float* pdzx, int nblk, const BwdFin& f) {
   double A, B;
-  if (!fin_sum2<NT>(pdz, pdzx, nblk, f.C, A, B)) return;
+  if (!fin_sum2<NT, ATOMIC>(pdz, pdzx, nblk, f.C, A, B)) return;
   const int C = f.C;
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const float db = (float)A, dg = (float)B;
@@ -288,21 +295,17 @@ __device__ __forceinline__ bool reduce_l2_last(const float* __restrict__ part, i
     float r0 = 0.f, r1 = 0.f;
 #pragma unroll
     for (int g = 0; g < G; ++g) { r0 += sh[0][t + 64 * g]; r1 += sh[1][t + 64 * g]; }
-    l2[(int64_t)s * C + c] = r0;
-    l2[((int64_t)S + s) * C + c] = r1;
+    // agent-scope atomic stores: coherent across the XCDs' L2s, so no release fence (an L2 write-back per
+    // workgroup on gfx950) and, on the reading side, no acquire fence (an L2 invalidate): atomic loads instead
+    __hip_atomic_store(l2 + (int64_t)s * C + c, r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(l2 + ((int64_t)S + s) * C + c, r1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned old = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == (unsigned)(S - 1);
-    if (last) {
-      __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (last) __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = last;
   }
   __syncthreads();
@@ -317,14 +320,14 @@ template <int NT>
 __global__ __launch_bounds__(NT) void bn_fwd_reduce_finalize_kernel(const float* __restrict__ part, int nblk, float* l2,
                                                                     int S, unsigned* cnt, FwdFin f) {
   if (!reduce_l2_last<NT>(part, nblk, f.C, l2, S, cnt)) return;
-  fwd_finalize<NT>(l2, l2 + (int64_t)S * f.C, S, f);
+  fwd_finalize<NT, true>(l2, l2 + (int64_t)S * f.C, S, f);
 }
 
 template <int NT>
 __global__ __launch_bounds__(NT) void bn_bwd_reduce_finalize_kernel(const float* __restrict__ part, int nblk, float* l2,
                                                                     int S, unsigned* cnt, BwdFin f) {
   if (!reduce_l2_last<NT>(part, nblk, f.C, l2, S, cnt)) return;
-  bwd_finalize<NT>(l2, l2 + (int64_t)S * f.C, S, f);
+  bwd_finalize<NT, true>(l2, l2 + (int64_t)S * f.C, S, f);
 }
 
 template <int NT>

@@ -143,6 +143,7 @@ struct Gemm256Args {
   int M, N, K, lda, ldb, ldc;
   int kt_per_split;   // K-tiles per blockIdx.y
   float alpha;
+  const float* bias;  // fp32 [N] added after alpha in the bf16 epilogue (the Linear bias), or null
 };
 
 // ACC: C += alpha * AB (bf16 read-modify-write); SLAB: write fp32 partials (split K)
@@ -336,6 +337,7 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
           v[3] = p.alpha * v[3] + __uint_as_float(o.y & 0xffff0000u);
         } else {
           v *= p.alpha;
+          if (p.bias != nullptr) v += *(const f32x4*)(p.bias + n);  // uniform branch; 16-byte aligned (n % 4 == 0)
         }
         uint2 packed;
         packed.x = pack_bf16x2(v[0], v[1]);
@@ -348,7 +350,8 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
 // C (bf16, ldc) = alpha * sum over splits of the fp32 slabs (+ C when accumulating); 8 elements per thread
 template <bool ACC>
 __global__ void __launch_bounds__(256) gemm256_reduce(const float* __restrict__ ws, __bf16* __restrict__ C, int M,
-                                                      int N, int ldc, int splits, float alpha) {
+                                                      int N, int ldc, int splits, float alpha,
+                                                      const float* __restrict__ bias) {
   const size_t i8 = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i8 >= (size_t)M * N / 8) return;
   const size_t e = i8 * 8;
@@ -362,6 +365,10 @@ __global__ void __launch_bounds__(256) gemm256_reduce(const float* __restrict__ 
   }
   s0 *= alpha;
   s1 *= alpha;
+  if (bias != nullptr) {
+    s0 += *(const f32x4*)(bias + n);
+    s1 += *(const f32x4*)(bias + n + 4);
+  }
   __bf16* dst = C + (size_t)m * ldc + n;
   if (ACC) {
     const uint4 o = *(const uint4*)dst;
@@ -422,12 +429,15 @@ PLX_API int plx_gemm256_splits(int M, int N, int K) {
 // A/B knob: blocks the split-K planner aims for (0 disables splitting)
 PLX_API void plx_gemm256_set_split_target(int blocks) { g_split_target = blocks; }
 
-// C[M][N] (bf16, ldc) = alpha * A . B (+ C when accumulate), layouts per a_kmajor / b_kmajor (see the file header).
+// C[M][N] (bf16, ldc) = alpha * A . B (+ bias[n]) (+ C when accumulate), layouts per a_kmajor / b_kmajor (see the
+// file header).  bias: fp32 [N], 16-byte aligned, or null (not combined with accumulate).
 // ws: fp32 workspace of plx_gemm256_splits(M, N, K) * M * N floats when that is > 1 (may be null otherwise).
 // Returns 0, or < 0 on a shape / layout the kernel does not take (nothing launched).
-PLX_API int plx_gemm256(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb, int ldc,
-                        int a_kmajor, int b_kmajor, float alpha, int accumulate, void* stream) {
+PLX_API int plx_gemm256_bias(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb,
+                             int ldc, int a_kmajor, int b_kmajor, float alpha, int accumulate, const float* bias,
+                             void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return -1;
+  if (bias != nullptr && (accumulate || (uintptr_t)bias % 16)) return -1;
   if (lda % 8 || ldb % 8 || ldc % 8 || (uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return -1;
   // largest relative byte offset a block's buffer resource sees
   const long long aspan = a_kmajor ? (long long)BM * lda * 2 : (long long)K * lda * 2;
@@ -436,7 +446,7 @@ PLX_API int plx_gemm256(const void* A, const void* B, void* C, void* ws, int M, 
   const int kps = plan_kt_per_split(M, N, K);
   const int splits = (K / BK + kps - 1) / kps;
   if (splits > 1 && !ws) return -5;
-  Gemm256Args a{(const __bf16*)A, (const __bf16*)B, splits > 1 ? ws : C, M, N, K, lda, ldb, ldc, kps, alpha};
+  Gemm256Args a{(const __bf16*)A, (const __bf16*)B, splits > 1 ? ws : C, M, N, K, lda, ldb, ldc, kps, alpha, bias};
   hipStream_t st = (hipStream_t)stream;
   int rc;
   if (a_kmajor && b_kmajor) rc = dispatch<true, true>(a, splits, accumulate, st);
@@ -449,12 +459,17 @@ PLX_API int plx_gemm256(const void* A, const void* B, void* C, void* ws, int M, 
     const dim3 grid((unsigned)((total8 + 255) / 256));
     if (accumulate)
       hipLaunchKernelGGL(gemm256_reduce<true>, grid, dim3(256), 0, st, (const float*)ws, (__bf16*)C, M, N, ldc, splits,
-                         alpha);
+                         alpha, (const float*)nullptr);
     else
       hipLaunchKernelGGL(gemm256_reduce<false>, grid, dim3(256), 0, st, (const float*)ws, (__bf16*)C, M, N, ldc,
-                         splits, alpha);
+                         splits, alpha, bias);
   }
   return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+PLX_API int plx_gemm256(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb, int ldc,
+                        int a_kmajor, int b_kmajor, float alpha, int accumulate, void* stream) {
+  return plx_gemm256_bias(A, B, C, ws, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor, alpha, accumulate, nullptr, stream);
 }
 
 // the kernel's tile edge: M and N must be multiples of it, K of 64

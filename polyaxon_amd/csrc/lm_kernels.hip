@@ -211,19 +211,29 @@ __global__ __launch_bounds__(kBlock) void xent_fwd_kernel(const uint16_t* __rest
   const int head = (int)((p0 & 15) >> 1);
   const int nch = (head + V + 7) >> 3;
   float m = kNegInf, sum = 0.f;
-  for (int c = threadIdx.x; c < nch; c += kBlock) {
-    const bf16x8 v = base[c];
-    float x[8], cm = kNegInf;
+  // 4 chunks (64 bytes) per lane in flight per trip: one load per trip left the row walk latency-bound (~3.9 TB/s)
+  for (int c0 = threadIdx.x; c0 < nch; c0 += 4 * kBlock) {
+    bf16x8 v[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int e = c * 8 + j - head;
-      x[j] = (e >= 0 && e < V) ? bf2f(v.v[j]) : kNegInf;
-      cm = fmaxf(cm, x[j]);
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + u * kBlock;
+      v[u] = c < nch ? base[c] : bf16x8{};
     }
+    float x[4][8], cm = kNegInf;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = (c0 + u * kBlock) * 8 + j - head;
+        x[u][j] = (e >= 0 && e < V) ? bf2f(v[u].v[j]) : kNegInf;
+        cm = fmaxf(cm, x[u][j]);
+      }
     if (cm == kNegInf) continue;
     float cs = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) cs += __expf(x[j] - cm);
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs += __expf(x[u][j] - cm);
     lse_combine(m, sum, cm, cs);
   }
 #pragma unroll
@@ -274,22 +284,32 @@ __global__ __launch_bounds__(kBlock) void xent_bwd_kernel(const uint16_t* __rest
   const float l = lse[r], g = dloss[0] * inv_rows;
   const int64_t t = tokens[(int64_t)lrow + 1];
   const bf16x8* base = (const bf16x8*)((uintptr_t)(logits + (int64_t)lrow * V) & ~(uintptr_t)15);
-  for (int c = threadIdx.x; c < nch; c += kBlock) {
-    const bf16x8 v = base[c];
-    bf16x8 o;
+  for (int c0 = threadIdx.x; c0 < nch; c0 += 2 * kBlock) {  // 2 chunks per lane in flight per trip
+    bf16x8 v[2];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int e = c * 8 + j - head;
-      const float p = __expf(bf2f(v.v[j]) - l);
-      o.v[j] = f2bf((p - (e == t ? 1.f : 0.f)) * g);
+    for (int u = 0; u < 2; ++u) {
+      const int c = c0 + u * kBlock;
+      v[u] = c < nch ? base[c] : bf16x8{};
     }
-    if (c * 8 - head >= 0 && c * 8 - head + 8 <= V) {
-      gbase[c] = o;
-    } else {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = c0 + u * kBlock;
+      if (c >= nch) break;
+      bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int e = c * 8 + j - head;
-        if (e >= 0 && e < V) grow[e] = o.v[j];
+        const float p = __expf(bf2f(v[u].v[j]) - l);
+        o.v[j] = f2bf((p - (e == t ? 1.f : 0.f)) * g);
+      }
+      if (c * 8 - head >= 0 && c * 8 - head + 8 <= V) {
+        gbase[c] = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int e = c * 8 + j - head;
+          if (e >= 0 && e < V) grow[e] = o.v[j];
+        }
       }
     }
   }
@@ -297,9 +317,8 @@ __global__ __launch_bounds__(kBlock) void xent_bwd_kernel(const uint16_t* __rest
 
 // ------------------------------------------------------------------------------------------------- column sums
 // Block = 8 lanes x 8 columns (one 128-byte row segment per 8 lanes) x 32 row groups; grid (ceil(N/64), R) with R
-// row splits of rpb rows.  Each split writes its 64 fp32 column partials, drains, releases and takes a ticket on the
-// column tile's counter (the split-K last-arriver hand-off of bn_kernels.hip); the last one sums the R partial rows
-// in split order.  Counters start zeroed and the last arriver resets its own; launches sharing the counters are
+// row splits of rpb rows.  Each split writes its 64 fp32 column partials (agent-scope atomic stores), drains and
+// takes a ticket on the column tile's counter; the last one sums the R partial rows in split order.  Counters start zeroed and the last arriver resets its own; launches sharing the counters are
 // stream-ordered.
 constexpr int kCsGroups = 32;
 
@@ -361,20 +380,18 @@ __global__ __launch_bounds__(kBlock) void colsum_kernel(const bf16x8* __restrict
     float t = 0.f;
 #pragma unroll 8
     for (int g = 0; g < kCsGroups; ++g) t += sh[g][threadIdx.x];
-    if (col < N) part[(int64_t)s * N + col] = t;
+    if (col < N) __hip_atomic_store(part + (int64_t)s * N + col, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // Hand-off without agent-scope fences: on gfx950 a release fence is an L2 write-back (buffer_wbl2) and an acquire
+  // an L2 invalidate, per workgroup -- with ~1000 workgroups (and, in the GELU form, 100 MB of dirty dh in the L2s)
+  // that dominated the kernel.  The partials are agent-scope atomic stores instead (coherent across the XCDs'
+  // L2s), drained (vmcnt(0)) before the ticket, and the last arriver reads them with agent-scope atomic loads.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned old = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == (unsigned)(R - 1);
-    if (last) {
-      __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (last) __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = last;
   }
   __syncthreads();
@@ -386,7 +403,10 @@ __global__ __launch_bounds__(kBlock) void colsum_kernel(const bf16x8* __restrict
     for (int b = g; b < R; b += 32) {  // 8 partial rows in flight per lane
       float y[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) y[u] = b + 4 * u < R ? part[(int64_t)(b + 4 * u) * N + col] : 0.f;
+      for (int u = 0; u < 8; ++u)
+        y[u] = b + 4 * u < R ? __hip_atomic_load(part + (int64_t)(b + 4 * u) * N + col, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : 0.f;
 #pragma unroll
       for (int u = 0; u < 8; ++u) a += y[u];
     }

@@ -371,9 +371,9 @@ __global__ __launch_bounds__(kBlock) void ln_bwd_wave_kernel(const bf16x8* __res
 // ----------------------------------------------------------------------------- partial rows -> parameter gradient
 // The backward kernels leave fp32 [nb][d] partial rows of dw (and db); this sums up to two such matrices column-wise
 // into their outputs in ONE launch: grid (ceil(d/64), R row splits of 64, nz matrices), block = 64 columns x 4 row
-// groups (a wave reads 256 contiguous bytes per row), level-2 rows published with the split-K last-arriver hand-off
-// (drain, agent-scope release, relaxed ticket, acquire; the last arriver resets its counter) and summed by the last
-// split in split order: deterministic.  out = sum (store) or out += sum (accumulate: the parameter's flat gradient
+// groups (a wave reads 256 contiguous bytes per row), level-2 rows published as agent-scope atomic stores (coherent
+// across the XCDs' L2s; no release fence = no per-workgroup L2 write-back), drained before a relaxed ticket, read by
+// the last split (which resets its counter) with agent-scope atomic loads and summed in split order: deterministic.  out = sum (store) or out += sum (accumulate: the parameter's flat gradient
 // slot, instead of autograd's separate `grad += g` pass).  Replaces a strided torch reduction (~19 us at nb = 1024,
 // d = 768) plus one accumulate kernel per parameter.
 constexpr int kPsRows = 64;
@@ -404,20 +404,16 @@ __global__ __launch_bounds__(kBlock) void partial_colsum_kernel(const float* __r
   sh[g][lc] = a;
   __syncthreads();
   float* l2z = l2 + (int64_t)z * R * d;
-  if (g == 0 && c < d) l2z[(int64_t)s * d + c] = ((sh[0][lc] + sh[1][lc]) + sh[2][lc]) + sh[3][lc];
+  if (g == 0 && c < d)  // agent-scope atomic store: coherent across the XCDs' L2s without a release fence
+    __hip_atomic_store(l2z + (int64_t)s * d + c, ((sh[0][lc] + sh[1][lc]) + sh[2][lc]) + sh[3][lc], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   unsigned* ctr = cnt + (int64_t)z * gridDim.x + blockIdx.x;
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == (unsigned)(R - 1);
-    if (last) {
-      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = last;
   }
   __syncthreads();
@@ -427,7 +423,10 @@ __global__ __launch_bounds__(kBlock) void partial_colsum_kernel(const float* __r
     for (int r = g; r < R; r += 32) {  // 8 level-2 rows in flight per lane
       float y[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) y[u] = r + 4 * u < R ? l2z[(int64_t)(r + 4 * u) * d + c] : 0.f;
+      for (int u = 0; u < 8; ++u)
+        y[u] = r + 4 * u < R ? __hip_atomic_load(l2z + (int64_t)(r + 4 * u) * d + c, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : 0.f;
 #pragma unroll
       for (int u = 0; u < 8; ++u) b += y[u];
     }

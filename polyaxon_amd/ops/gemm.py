@@ -107,11 +107,13 @@ def _workspace(device: torch.device, floats: int) -> torch.Tensor:
 
 
 def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool,
-         out: Optional[torch.Tensor] = None, accumulate: bool = False, alpha: float = 1.0) -> torch.Tensor:
-    """out[M][N] (bf16, row-major, may be a strided view with unit column stride) = alpha * A . B (+ out).
+         out: Optional[torch.Tensor] = None, accumulate: bool = False, alpha: float = 1.0,
+         bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[M][N] (bf16, row-major, may be a strided view with unit column stride) = alpha * A . B (+ bias) (+ out).
 
     ``a`` is A[M][K] when ``a_kmajor`` else A stored [K][M]; ``b`` is B[N][K] when ``b_kmajor`` else [K][N].
-    Both are contiguous bf16 (leading dimension = their row length)."""
+    Both are contiguous bf16 (leading dimension = their row length).  ``bias``: [N], added in fp32 by the epilogue
+    (cast to a contiguous fp32 copy if it is not one); not with ``accumulate``."""
     if not supported(M, N, K):
         raise ValueError(f"gemm256 needs M, N % 256 == 0 and K % 64 == 0 (got {M}x{N}x{K})")
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not (a.is_contiguous() and b.is_contiguous()):
@@ -124,13 +126,20 @@ def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: boo
         out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
     if out.dtype != torch.bfloat16 or out.dim() != 2 or out.shape != (M, N) or out.stride(1) != 1:
         raise ValueError("out must be a [M][N] bf16 matrix with unit column stride")
+    if bias is not None:
+        if accumulate or bias.numel() != N:
+            raise ValueError("bias needs numel N and no accumulate")
+        bias = bias.to(torch.float32).contiguous()
+        if bias.data_ptr() % 16:
+            bias = bias.clone()
     lib = _native.lib("plx_gemm")
     splits = _native.size("plx_gemm", "plx_gemm256_splits", M, N, K)
     ws = _workspace(a.device, splits * M * N).data_ptr() if splits > 1 else None
     lda = K if a_kmajor else M
     ldb = K if b_kmajor else N
-    rc = lib.plx_gemm256(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, M, N, K, lda, ldb, out.stride(0),
-                         int(a_kmajor), int(b_kmajor), float(alpha), int(accumulate), _native.current_stream())
+    rc = lib.plx_gemm256_bias(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, M, N, K, lda, ldb, out.stride(0),
+                              int(a_kmajor), int(b_kmajor), float(alpha), int(accumulate),
+                              bias.data_ptr() if bias is not None else None, _native.current_stream())
     if rc != 0:
         raise RuntimeError(f"plx_gemm256 failed ({rc}) for {M}x{N}x{K} a_kmajor={a_kmajor} b_kmajor={b_kmajor}")
     return out
@@ -144,14 +153,14 @@ def linear_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
 
 
 def forward(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y[T][out] = x[T][in] . W[out][in]^T (+ bias): on hipBLASLt the bias rides in the GEMM epilogue (addmm) instead
-    of a separate read-modify-write pass over y"""
+    """y[T][out] = x[T][in] . W[out][in]^T (+ bias): the bias rides in the GEMM epilogue (gemm256's fp32 bias add, or
+    hipBLASLt's through addmm) instead of a separate read-modify-write pass over y"""
     T, fin = x2.shape
     N = weight.shape[0]
     if bias is None:
         return matmul(x2, weight, T, N, fin, True, True)
     if _use_native(x2, weight, T, N, fin, True, True):
-        return gemm(x2, weight, T, N, fin, True, True).add_(bias)
+        return gemm(x2, weight, T, N, fin, True, True, bias=bias)
     return torch.addmm(bias.to(x2.dtype), x2, weight.t())
 
 

@@ -60,6 +60,21 @@ def test_gemm256_split_k_and_accumulate(cuda, accumulate, M, N, K):
     _check(out, ref, K)
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (256, 256, 8192)])
+def test_gemm256_bias_epilogue(cuda, M, N, K):
+    """The fp32 bias added by the epilogue (plx_gemm256_bias): one-pass tiles and the split-K reduce, a bf16 bias
+    (cast to fp32 on the host side) included."""
+    from polyaxon_amd.ops import gemm
+
+    a = _rand((M, K), cuda, 6)
+    b = _rand((N, K), cuda, 7)
+    for bias in (torch.randn(N, device=cuda), torch.randn(N, device=cuda).to(torch.bfloat16)):
+        out = gemm.gemm(a, b, M, N, K, True, True, bias=bias)
+        ref = a.float() @ b.float().t() + bias.float()
+        torch.cuda.synchronize()
+        _check(out, ref, K)
+
+
 def test_gemm256_strided_output(cuda):
     """out may be a column block of a wider matrix (ldc > N)."""
     from polyaxon_amd.ops import gemm
