@@ -284,32 +284,22 @@ __global__ __launch_bounds__(kBlock) void xent_bwd_kernel(const uint16_t* __rest
   const float l = lse[r], g = dloss[0] * inv_rows;
   const int64_t t = tokens[(int64_t)lrow + 1];
   const bf16x8* base = (const bf16x8*)((uintptr_t)(logits + (int64_t)lrow * V) & ~(uintptr_t)15);
-  for (int c0 = threadIdx.x; c0 < nch; c0 += 2 * kBlock) {  // 2 chunks per lane in flight per trip
-    bf16x8 v[2];
+  for (int c = threadIdx.x; c < nch; c += kBlock) {
+    const bf16x8 v = base[c];
+    bf16x8 o;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int c = c0 + u * kBlock;
-      v[u] = c < nch ? base[c] : bf16x8{};
+    for (int j = 0; j < 8; ++j) {
+      const int e = c * 8 + j - head;
+      const float p = __expf(bf2f(v.v[j]) - l);
+      o.v[j] = f2bf((p - (e == t ? 1.f : 0.f)) * g);
     }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int c = c0 + u * kBlock;
-      if (c >= nch) break;
-      bf16x8 o;
+    if (c * 8 - head >= 0 && c * 8 - head + 8 <= V) {
+      gbase[c] = o;
+    } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int e = c * 8 + j - head;
-        const float p = __expf(bf2f(v[u].v[j]) - l);
-        o.v[j] = f2bf((p - (e == t ? 1.f : 0.f)) * g);
-      }
-      if (c * 8 - head >= 0 && c * 8 - head + 8 <= V) {
-        gbase[c] = o;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int e = c * 8 + j - head;
-          if (e >= 0 && e < V) grow[e] = o.v[j];
-        }
+        if (e >= 0 && e < V) grow[e] = o.v[j];
       }
     }
   }
@@ -325,7 +315,10 @@ constexpr int kCsGroups = 32;
 // GELU (tanh approximation, GPT-2) derivative: d/dh [0.5 h (1 + tanh(u))], u = sqrt(2/pi) (h + 0.044715 h^3)
 __device__ __forceinline__ float gelu_tanh_grad(float h) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float t = tanhf(k0 * fmaf(k1 * h * h, h, h));
+  // tanh(u) = 1 - 2 / (1 + e^{2u}) on v_exp_f32 and v_rcp_f32 (saturates to +-1 at the extremes): libm tanhf made
+  // this pass VALU-bound at ~3 TB/s
+  const float e = __expf(2.f * k0 * fmaf(k1 * h * h, h, h));
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
   return fmaf(0.5f, 1.f + t, 0.5f * h * (1.f - t * t) * k0 * fmaf(3.f * k1, h * h, 1.f));
 }
 

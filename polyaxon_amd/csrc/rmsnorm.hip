@@ -246,11 +246,15 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-template <int VPL>
+// ADD: the residual add feeding the norm is fused in: s = bf16(x + res) is written (the next residual) and
+// normalised -- one pass instead of an add kernel (3 row streams) followed by the norm (2).
+template <int VPL, bool ADD = false>
 __global__ __launch_bounds__(kBlock) void ln_fwd_wave_kernel(const bf16x8* __restrict__ x, const float* __restrict__ w,
                                                              const float* __restrict__ bias, bf16x8* __restrict__ y,
                                                              float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                             int64_t rows, int dv, float eps) {
+                                                             int64_t rows, int dv, float eps,
+                                                             const bf16x8* __restrict__ res = nullptr,
+                                                             bf16x8* __restrict__ s_out = nullptr) {
   const int lane = threadIdx.x & 63;
   const float inv_d = 1.f / (float)(dv * 8);
   const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
@@ -261,7 +265,13 @@ __global__ __launch_bounds__(kBlock) void ln_fwd_wave_kernel(const bf16x8* __res
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
       const int i = lane + j * 64;
-      const bf16x8 v = i < dv ? xr[i] : bf16x8{};
+      bf16x8 v = i < dv ? xr[i] : bf16x8{};
+      if (ADD && i < dv) {
+        const bf16x8 rv = res[r * dv + i];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v.v[k] = f2bf(bf2f(v.v[k]) + bf2f(rv.v[k]));
+        s_out[r * dv + i] = v;
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         xs[j][k] = bf2f(v.v[k]);
@@ -298,13 +308,16 @@ __global__ __launch_bounds__(kBlock) void ln_fwd_wave_kernel(const bf16x8* __res
   }
 }
 
-template <int VPL>
+// ADD: dx = LN backward + dres (the gradient arriving through the residual path), summed in fp32 and rounded once:
+// the backward of the fused add + norm (both of its inputs get this same gradient)
+template <int VPL, bool ADD = false>
 __global__ __launch_bounds__(kBlock) void ln_bwd_wave_kernel(const bf16x8* __restrict__ x, const float* __restrict__ w,
                                                              const bf16x8* __restrict__ dy,
                                                              const float* __restrict__ mean_in,
                                                              const float* __restrict__ rstd_in, bf16x8* __restrict__ dx,
                                                              float* __restrict__ dw_part, float* __restrict__ db_part,
-                                                             int64_t rows, int dv) {
+                                                             int64_t rows, int dv,
+                                                             const bf16x8* __restrict__ dres = nullptr) {
   __shared__ float shw[kBlock / 64][VPL * 64 * 8];
   __shared__ float shb[kBlock / 64][VPL * 64 * 8];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -343,8 +356,14 @@ __global__ __launch_bounds__(kBlock) void ln_bwd_wave_kernel(const bf16x8* __res
       const int i = lane + j * 64;
       if (i < dv) {
         bf16x8 o;
+        if (ADD) {
+          const bf16x8 dr = dres[r * dv + i];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o.v[k] = f2bf(rstd * (gw[j][k] - mg - xh[j][k] * mgx));
+          for (int k = 0; k < 8; ++k) o.v[k] = f2bf(fmaf(rstd, gw[j][k] - mg - xh[j][k] * mgx, bf2f(dr.v[k])));
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o.v[k] = f2bf(rstd * (gw[j][k] - mg - xh[j][k] * mgx));
+        }
         dx[r * dv + i] = o;
       }
     }
@@ -477,7 +496,8 @@ PLX_API int plx_ln_forward(const void* x, const float* w, const float* b, void* 
     int64_t g = (rows + 3) / 4;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(vpl == 1 ? ln_fwd_wave_kernel<1> : ln_fwd_wave_kernel<2>, dim3((int)g), dim3(kBlock), 0, stream,
-                       (const bf16x8*)x, w, b, (bf16x8*)y, mean, rstd, rows, d / 8, eps);
+                       (const bf16x8*)x, w, b, (bf16x8*)y, mean, rstd, rows, d / 8, eps, (const bf16x8*)nullptr,
+                       (bf16x8*)nullptr);
     return (int)hipGetLastError();
   }
   int64_t g = rows < 4096 ? rows : 4096;
@@ -500,8 +520,13 @@ PLX_API int plx_ln_backward(const void* x, const float* w, const void* dy, const
                             void* dx, float* dw_part, float* db_part, int64_t rows, int d, hipStream_t stream) {
   if (d % 8 || d > kBlock * 8 * kMaxVecPerLane || rows <= 0) return 1;
   const int vpl = ln_vpl(d);
-  auto k = vpl == 1 ? ln_bwd_wave_kernel<1> : vpl == 2 ? ln_bwd_wave_kernel<2> : ln_bwd_kernel;
-  hipLaunchKernelGGL(k, dim3(plx_ln_bwd_blocks(rows, d)), dim3(kBlock), 0, stream, (const bf16x8*)x, w,
+  if (vpl) {
+    hipLaunchKernelGGL(vpl == 1 ? ln_bwd_wave_kernel<1> : ln_bwd_wave_kernel<2>, dim3(plx_ln_bwd_blocks(rows, d)),
+                       dim3(kBlock), 0, stream, (const bf16x8*)x, w, (const bf16x8*)dy, mean, rstd, (bf16x8*)dx,
+                       dw_part, db_part, rows, d / 8, (const bf16x8*)nullptr);
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(plx_ln_bwd_blocks(rows, d)), dim3(kBlock), 0, stream, (const bf16x8*)x, w,
                      (const bf16x8*)dy, mean, rstd, (bf16x8*)dx, dw_part, db_part, rows, d / 8);
   return (int)hipGetLastError();
 }
@@ -518,5 +543,33 @@ PLX_API int plx_partial_colsum(const float* p0, const float* p1, int rows, int d
   const int R = (rows + kPsRows - 1) / kPsRows;
   hipLaunchKernelGGL(partial_colsum_kernel, dim3((d + 63) / 64, R, nz), dim3(kBlock), 0, stream, p0, p1, rows, d, l2,
                      cnt, o0, o1, acc0, acc1);
+  return (int)hipGetLastError();
+}
+
+// fused residual add + LayerNorm: s = bf16(x + res) (written), y = LN(s).  Wave path only (d <= 1024): returns 2
+// (nothing launched) otherwise, and the caller adds and normalises separately.
+PLX_API int plx_add_ln_forward(const void* x, const void* res, const float* w, const float* b, void* s, void* y,
+                               float* mean, float* rstd, int64_t rows, int d, float eps, hipStream_t stream) {
+  if (d % 8 || rows <= 0) return 1;
+  const int vpl = ln_vpl(d);
+  if (!vpl) return 2;
+  int64_t g = (rows + 3) / 4;
+  if (g > 8192) g = 8192;
+  auto k = vpl == 1 ? ln_fwd_wave_kernel<1, true> : ln_fwd_wave_kernel<2, true>;
+  hipLaunchKernelGGL(k, dim3((int)g), dim3(kBlock), 0, stream, (const bf16x8*)x, w, b, (bf16x8*)y, mean, rstd, rows, d / 8, eps, (const bf16x8*)res,
+                     (bf16x8*)s);
+  return (int)hipGetLastError();
+}
+
+// its backward: dx = LN backward(s, dy) + dres (the gradient of both x and res); partials as plx_ln_backward
+PLX_API int plx_add_ln_backward(const void* s, const float* w, const void* dy, const float* mean, const float* rstd,
+                                const void* dres, void* dx, float* dw_part, float* db_part, int64_t rows, int d,
+                                hipStream_t stream) {
+  if (d % 8 || rows <= 0) return 1;
+  const int vpl = ln_vpl(d);
+  if (!vpl) return 2;
+  auto k = vpl == 1 ? ln_bwd_wave_kernel<1, true> : ln_bwd_wave_kernel<2, true>;
+  hipLaunchKernelGGL(k, dim3(plx_ln_bwd_blocks(rows, d)), dim3(kBlock), 0, stream, (const bf16x8*)s, w, (const bf16x8*)dy,
+                     mean, rstd, (bf16x8*)dx, dw_part, db_part, rows, d / 8, (const bf16x8*)dres);
   return (int)hipGetLastError();
 }

@@ -206,15 +206,32 @@ class Transformer(nn.Module):
             if self._rope is None or self._rope[0].shape[0] < S or self._rope[0].device != tokens.device:
                 self._rope = rope_cache(max(S, 16), self.cfg.head_dim, self.cfg.rope_theta, tokens.device)
             rope = (self._rope[0][:S], self._rope[1][:S])  # fp32 tables; the attention casts as needed
-        for blk in self.blocks:
-            if self.cfg.checkpoint and self.training:
-                x = checkpoint(blk, x, rope, use_reentrant=False)
-            else:
-                x = blk(x, rope)
-        x = self.norm(x)
+        if self.cfg.norm != "rmsnorm" and not (self.cfg.checkpoint and self.training):
+            # GPT-2: every residual add is fused into the LayerNorm that reads its sum (ops/rmsnorm.py
+            # add_layer_norm) -- the same computation as Block.forward, one pass fewer over the residual per add
+            r = None
+            for blk in self.blocks:
+                x, h = self._add_norm(x, r, blk.n1)
+                r = blk.attn(h, rope)
+                x, h = self._add_norm(x, r, blk.n2)
+                r = blk.mlp(h)
+            x = self._add_norm(x, r, self.norm)[1]
+        else:
+            for blk in self.blocks:
+                if self.cfg.checkpoint and self.training:
+                    x = checkpoint(blk, x, rope, use_reentrant=False)
+                else:
+                    x = blk(x, rope)
+            x = self.norm(x)
         if self.head is None:  # tied: the embedding's gradient also arrives through autograd, keep F.linear
             return F.linear(x, self.embed.weight)
         return lm_ops.linear(x, self.head.weight)
+
+    @staticmethod
+    def _add_norm(x, r, norm):
+        if r is None:
+            return x, norm(x)
+        return _rms.add_layer_norm(x, r, norm.weight, norm.bias, norm.eps)
 
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())

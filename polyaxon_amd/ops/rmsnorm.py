@@ -147,6 +147,66 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: f
     return layer_norm_reference(x, weight, bias, eps)
 
 
+class _AddLayerNorm(torch.autograd.Function):
+    """(s, y) = (x + res, LayerNorm(x + res)) in one pass (csrc/rmsnorm.hip plx_add_ln_forward); backward: the norm's
+    dx plus the residual gradient ds in one pass, returned for both x and res."""
+
+    @staticmethod
+    def forward(ctx, x, res, weight, bias, eps):
+        ctx.set_materialize_grads(False)
+        lib = _native.lib("plx_rms")
+        d = x.shape[-1]
+        rows = x.numel() // d
+        s, y = torch.empty_like(x), torch.empty_like(x)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        w, b = weight.float().contiguous(), bias.float().contiguous()
+        _native.check(lib.plx_add_ln_forward(x.data_ptr(), res.data_ptr(), w.data_ptr(), b.data_ptr(), s.data_ptr(),
+                                             y.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, d, float(eps),
+                                             _stream()), "plx_add_ln_forward")
+        ctx.save_for_backward(s, w, mean, rstd)
+        ctx.params = (weight, bias)
+        return s, y
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        lib = _native.lib("plx_rms")
+        s, w, mean, rstd = ctx.saved_tensors
+        d = s.shape[-1]
+        rows = s.numel() // d
+        if dy is None:  # only the residual stream is used downstream
+            return ds, ds, None, None, None
+        dy = dy.contiguous().to(s.dtype)
+        dx = torch.empty_like(s)
+        nb = lib.plx_ln_bwd_blocks(rows, d)
+        part = torch.empty((2, nb, d), dtype=torch.float32, device=s.device)
+        if ds is None:
+            _native.check(lib.plx_ln_backward(s.data_ptr(), w.data_ptr(), dy.data_ptr(), mean.data_ptr(),
+                                              rstd.data_ptr(), dx.data_ptr(), part[0].data_ptr(), part[1].data_ptr(),
+                                              rows, d, _stream()), "plx_ln_backward")
+        else:
+            ds = ds.contiguous().to(s.dtype)
+            _native.check(lib.plx_add_ln_backward(s.data_ptr(), w.data_ptr(), dy.data_ptr(), mean.data_ptr(),
+                                                  rstd.data_ptr(), ds.data_ptr(), dx.data_ptr(), part[0].data_ptr(),
+                                                  part[1].data_ptr(), rows, d, _stream()), "plx_add_ln_backward")
+        dw, db = _param_grads([part[0], part[1]], list(ctx.params), d)
+        return dx, dx, dw, db, None
+
+
+def add_layer_norm(x: torch.Tensor, res: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor,
+                   eps: float = 1e-5):
+    """(s, y) = (x + res, LayerNorm(s)): the pre-norm transformer's residual add fused into the next norm for bf16 GPU
+    rows of d <= 1024 (one wave per row); the separate add and :func:`layer_norm` otherwise."""
+    if (supported(x) and res.dtype == x.dtype and res.shape == x.shape and x.shape[-1] <= 1024 and x.is_contiguous()
+            and res.is_contiguous() and _LN_WAVE):
+        return _AddLayerNorm.apply(x, res, weight, bias, eps)
+    s = x + res
+    return s, layer_norm(s, weight, bias, eps)
+
+
+_LN_WAVE = os.environ.get("PLX_LN_WAVE", "1") != "0" and os.environ.get("PLX_ADD_LN", "1") != "0"
+
+
 class LayerNorm(torch.nn.Module):
     """``nn.LayerNorm(d)`` (same parameter names, fp32 weight / bias) on the fused kernels for bf16 GPU inputs."""
 

@@ -14,15 +14,16 @@ WORLD_SIZE and call NCCL themselves.  This module is what a polyflow DP trial us
   all-reduce moves half the bytes; buckets never straddle the bf16 / fp32-tail boundary.  Direct-gradient
   ops (ops/lm.py, ops/rmsnorm.py: GEMM-written weights, bias / norm sums written into the slots) return None and
   are still counted by autograd's post-accumulate hook, which runs once per parameter per backward after every
-  Function feeding it; each segment counts its bucket down once per step.  (Optimizer-state sharding / ZeRO-1 is not implemented: an 8B model's fp32 master +
-  moments are 96 GB, which one 288 GB MI355X holds unsharded.)
+  Function feeding it; each segment counts its bucket down once per step.  (Optimizer-state sharding / ZeRO-1 is
+  not implemented: an 8B model's fp32 master + moments are 96 GB, which one 288 GB MI355X holds unsharded.)
 * optimizer in the backward (``optimizer=``, a FusedAdamW): the moment a bucket's gradient is complete (and, with
   DP, its all-reduce is done) the AdamW update of that bucket runs on a side stream, overlapped with the rest of
   the backward instead of one HBM-bound pass over every parameter after it (~41 ms of a 227 ms Llama-3 8B step on
   one MI355X; measured: the overlap mostly moves that time into the backward's memory-bound kernels, so the LM
-  trainer leaves it off by default, PLX_OPT_IN_BACKWARD=1).  Each parameter's backward uses are issued before its bucket counts down (ops/lm.py calls the ready
-  callback after the data-gradient GEMM), and ``finish()`` makes the main stream wait for the optimizer stream
-  before the next forward reads the updated bf16 weights.  Same per-element update as the monolithic step.
+  trainer leaves it off by default, PLX_OPT_IN_BACKWARD=1).  Each parameter's backward uses are issued before its
+  bucket counts down (its AccumulateGrad hook runs after every Function that reads the weight), and ``finish()``
+  makes the main stream wait for the optimizer stream before the next forward reads the updated bf16 weights.
+  Same per-element update as the monolithic step.
 Backend ``"nccl"`` is RCCL on ROCm; ``"gloo"`` works for CPU tests.
 """
 from __future__ import annotations

@@ -85,3 +85,31 @@ def test_mlp_grid_group_on_gpu(tmp_path):
         assert max(sum(1 for s, f in spans if s <= t < f) for t, _ in spans) >= 2  # really concurrent
     finally:
         flow.shutdown()
+
+
+@pytest.mark.parametrize("rows,d", [(37, 768), (4099, 1024), (300, 264)])
+def test_add_layernorm_matches_fp32(cuda, rows, d):
+    """Fused residual add + LayerNorm (plx_add_ln_forward / _backward) vs the bf16 add then fp32 F.layer_norm: both
+    outputs, the gradient of both inputs (norm backward + residual gradient), dweight, dbias."""
+    from polyaxon_amd.ops.rmsnorm import add_layer_norm, layer_norm_reference
+
+    torch.manual_seed(1)
+    x = (torch.randn(rows, d, device=cuda) * 2 + 5).to(torch.bfloat16).requires_grad_()
+    r = torch.randn(rows, d, device=cuda).to(torch.bfloat16).requires_grad_()
+    w = (torch.rand(d, device=cuda) + 0.5).requires_grad_()
+    b = torch.randn(d, device=cuda).requires_grad_()
+    s, y = add_layer_norm(x, r, w, b, 1e-5)
+    sr = (x.detach() + r.detach()).float().requires_grad_()  # the bf16 add, then fp32
+    wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    yr = layer_norm_reference(sr, wr, br, 1e-5)
+    assert torch.equal(s, (x + r).detach())
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    gs = torch.randn(rows, d, device=cuda).to(torch.bfloat16)
+    gy = torch.randn(rows, d, device=cuda).to(torch.bfloat16)
+    torch.autograd.backward([s, y], [gs, gy])  # both gradients at once: the fused dx = LN backward + ds kernel
+    yr.backward(gy.float())
+    ref_dx = sr.grad + gs.float()
+    torch.testing.assert_close(x.grad.float(), ref_dx, rtol=3e-2, atol=3e-2 * float(ref_dx.abs().max()))
+    torch.testing.assert_close(r.grad.float(), ref_dx, rtol=3e-2, atol=3e-2 * float(ref_dx.abs().max()))
+    torch.testing.assert_close(w.grad, wr.grad, rtol=2e-2, atol=2e-2 * rows ** 0.5)
+    torch.testing.assert_close(b.grad, br.grad, rtol=2e-2, atol=2e-2 * rows ** 0.5)
