@@ -113,3 +113,34 @@ def test_add_layernorm_matches_fp32(cuda, rows, d):
     torch.testing.assert_close(r.grad.float(), ref_dx, rtol=3e-2, atol=3e-2 * float(ref_dx.abs().max()))
     torch.testing.assert_close(w.grad, wr.grad, rtol=2e-2, atol=2e-2 * rows ** 0.5)
     torch.testing.assert_close(b.grad, br.grad, rtol=2e-2, atol=2e-2 * rows ** 0.5)
+
+
+def test_gpt2_fused_residual_norm_path_matches_block_path(cuda):
+    """Transformer.forward's GPT-2 path (every residual add fused into the next LayerNorm) against the plain
+    Block.forward loop on the same weights: logits and the loss gradient of every parameter."""
+    from polyaxon_amd.models.transformer import Transformer, gpt2_125m, lm_loss
+
+    torch.manual_seed(0)
+    cfg = gpt2_125m(vocab_size=512, n_layers=2, d_model=256, n_heads=4, d_ff=1024, max_seq_len=128)
+    with torch.device(cuda):
+        model = Transformer(cfg)
+    tok = torch.randint(0, 512, (2, 128), device=cuda)
+
+    def block_path(m):
+        x = m.embed(tok) + m.pos(torch.arange(tok.shape[1], device=cuda))[None]
+        for blk in m.blocks:
+            x = blk(x, None)
+        return torch.nn.functional.linear(m.norm(x), m.embed.weight)
+
+    out = {}
+    for name, fn in (("fused", model), ("blocks", block_path)):
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = model(tok) if name == "fused" else fn(model)
+            loss = lm_loss(logits, tok)
+        loss.backward()
+        out[name] = (logits.float(), {n: p.grad.float().clone() for n, p in model.named_parameters()})
+    torch.testing.assert_close(out["fused"][0], out["blocks"][0], rtol=3e-2, atol=3e-2)
+    for n, g in out["blocks"][1].items():
+        gf = out["fused"][1][n]
+        assert float((gf - g).norm()) <= 0.03 * float(g.norm()) + 1e-6, n
