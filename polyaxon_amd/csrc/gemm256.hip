@@ -144,7 +144,17 @@ struct Gemm256Args {
   int kt_per_split;   // K-tiles per blockIdx.y
   float alpha;
   const float* bias;  // fp32 [N] added after alpha in the bf16 epilogue (the Linear bias), or null
+  void* C2;           // bf16 [M][ldc]: gelu_tanh of the stored (bf16-rounded) C, or null (GPT-2's up-projection)
 };
+
+// GELU, tanh approximation, of the bf16-rounded value (what a separate activation pass reading C would compute);
+// tanh(u) = 1 - 2 / (1 + e^{2u}) on v_exp_f32 / v_rcp_f32
+__device__ __forceinline__ float gelu_tanh(float h) {
+  const float u = 0.7978845608028654f * fmaf(0.044715f * h * h, h, h);
+  return 0.5f * h * (2.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u)));
+}
+
+__device__ __forceinline__ float bf16_round(float f) { return (float)(__bf16)f; }
 
 // ACC: C += alpha * AB (bf16 read-modify-write); SLAB: write fp32 partials (split K)
 template <bool AK, bool BKM, bool ACC, bool SLAB>
@@ -343,6 +353,12 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
         packed.x = pack_bf16x2(v[0], v[1]);
         packed.y = pack_bf16x2(v[2], v[3]);
         *(uint2*)dst = packed;
+        if (!ACC && p.C2 != nullptr) {  // uniform branch
+          uint2 g;
+          g.x = pack_bf16x2(gelu_tanh(bf16_round(v[0])), gelu_tanh(bf16_round(v[1])));
+          g.y = pack_bf16x2(gelu_tanh(bf16_round(v[2])), gelu_tanh(bf16_round(v[3])));
+          *(uint2*)((__bf16*)p.C2 + (size_t)m * p.ldc + n) = g;
+        }
       }
     }
 }
@@ -351,7 +367,7 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
 template <bool ACC>
 __global__ void __launch_bounds__(256) gemm256_reduce(const float* __restrict__ ws, __bf16* __restrict__ C, int M,
                                                       int N, int ldc, int splits, float alpha,
-                                                      const float* __restrict__ bias) {
+                                                      const float* __restrict__ bias, __bf16* __restrict__ C2) {
   const size_t i8 = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i8 >= (size_t)M * N / 8) return;
   const size_t e = i8 * 8;
@@ -387,6 +403,14 @@ __global__ void __launch_bounds__(256) gemm256_reduce(const float* __restrict__ 
   packed.z = pack_bf16x2(s1[0], s1[1]);
   packed.w = pack_bf16x2(s1[2], s1[3]);
   *(uint4*)dst = packed;
+  if (!ACC && C2 != nullptr) {
+    uint4 g;
+    g.x = pack_bf16x2(gelu_tanh(bf16_round(s0[0])), gelu_tanh(bf16_round(s0[1])));
+    g.y = pack_bf16x2(gelu_tanh(bf16_round(s0[2])), gelu_tanh(bf16_round(s0[3])));
+    g.z = pack_bf16x2(gelu_tanh(bf16_round(s1[0])), gelu_tanh(bf16_round(s1[1])));
+    g.w = pack_bf16x2(gelu_tanh(bf16_round(s1[2])), gelu_tanh(bf16_round(s1[3])));
+    *(uint4*)(C2 + (size_t)m * ldc + n) = g;
+  }
 }
 
 template <bool AK, bool BKM, bool ACC, bool SLAB>
@@ -433,11 +457,13 @@ PLX_API void plx_gemm256_set_split_target(int blocks) { g_split_target = blocks;
 // file header).  bias: fp32 [N], 16-byte aligned, or null (not combined with accumulate).
 // ws: fp32 workspace of plx_gemm256_splits(M, N, K) * M * N floats when that is > 1 (may be null otherwise).
 // Returns 0, or < 0 on a shape / layout the kernel does not take (nothing launched).
-PLX_API int plx_gemm256_bias(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb,
-                             int ldc, int a_kmajor, int b_kmajor, float alpha, int accumulate, const float* bias,
-                             void* stream) {
+// gelu_out: bf16 [M][ldc] (same layout as C, 16-byte aligned) receiving gelu_tanh(C), or null (not with accumulate).
+PLX_API int plx_gemm256_ex(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb,
+                           int ldc, int a_kmajor, int b_kmajor, float alpha, int accumulate, const float* bias,
+                           void* gelu_out, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return -1;
   if (bias != nullptr && (accumulate || (uintptr_t)bias % 16)) return -1;
+  if (gelu_out != nullptr && (accumulate || (uintptr_t)gelu_out % 16)) return -1;
   if (lda % 8 || ldb % 8 || ldc % 8 || (uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return -1;
   // largest relative byte offset a block's buffer resource sees
   const long long aspan = a_kmajor ? (long long)BM * lda * 2 : (long long)K * lda * 2;
@@ -446,7 +472,8 @@ PLX_API int plx_gemm256_bias(const void* A, const void* B, void* C, void* ws, in
   const int kps = plan_kt_per_split(M, N, K);
   const int splits = (K / BK + kps - 1) / kps;
   if (splits > 1 && !ws) return -5;
-  Gemm256Args a{(const __bf16*)A, (const __bf16*)B, splits > 1 ? ws : C, M, N, K, lda, ldb, ldc, kps, alpha, bias};
+  Gemm256Args a{(const __bf16*)A, (const __bf16*)B, splits > 1 ? ws : C, M, N, K, lda, ldb, ldc, kps, alpha, bias,
+                splits > 1 ? nullptr : gelu_out};
   hipStream_t st = (hipStream_t)stream;
   int rc;
   if (a_kmajor && b_kmajor) rc = dispatch<true, true>(a, splits, accumulate, st);
@@ -459,17 +486,25 @@ PLX_API int plx_gemm256_bias(const void* A, const void* B, void* C, void* ws, in
     const dim3 grid((unsigned)((total8 + 255) / 256));
     if (accumulate)
       hipLaunchKernelGGL(gemm256_reduce<true>, grid, dim3(256), 0, st, (const float*)ws, (__bf16*)C, M, N, ldc, splits,
-                         alpha, (const float*)nullptr);
+                         alpha, (const float*)nullptr, (__bf16*)nullptr);
     else
       hipLaunchKernelGGL(gemm256_reduce<false>, grid, dim3(256), 0, st, (const float*)ws, (__bf16*)C, M, N, ldc,
-                         splits, alpha, bias);
+                         splits, alpha, bias, (__bf16*)gelu_out);
   }
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+PLX_API int plx_gemm256_bias(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb,
+                             int ldc, int a_kmajor, int b_kmajor, float alpha, int accumulate, const float* bias,
+                             void* stream) {
+  return plx_gemm256_ex(A, B, C, ws, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor, alpha, accumulate, bias, nullptr,
+                        stream);
+}
+
 PLX_API int plx_gemm256(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb, int ldc,
                         int a_kmajor, int b_kmajor, float alpha, int accumulate, void* stream) {
-  return plx_gemm256_bias(A, B, C, ws, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor, alpha, accumulate, nullptr, stream);
+  return plx_gemm256_ex(A, B, C, ws, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor, alpha, accumulate, nullptr, nullptr,
+                        stream);
 }
 
 // the kernel's tile edge: M and N must be multiples of it, K of 64

@@ -108,12 +108,13 @@ def _workspace(device: torch.device, floats: int) -> torch.Tensor:
 
 def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool,
          out: Optional[torch.Tensor] = None, accumulate: bool = False, alpha: float = 1.0,
-         bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+         bias: Optional[torch.Tensor] = None, gelu_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[M][N] (bf16, row-major, may be a strided view with unit column stride) = alpha * A . B (+ bias) (+ out).
 
     ``a`` is A[M][K] when ``a_kmajor`` else A stored [K][M]; ``b`` is B[N][K] when ``b_kmajor`` else [K][N].
     Both are contiguous bf16 (leading dimension = their row length).  ``bias``: [N], added in fp32 by the epilogue
-    (cast to a contiguous fp32 copy if it is not one); not with ``accumulate``."""
+    (cast to a contiguous fp32 copy if it is not one); not with ``accumulate``.  ``gelu_out``: a bf16 tensor shaped
+    like ``out`` that also receives gelu_tanh(out) from the same epilogue (GPT-2's up-projection + activation)."""
     if not supported(M, N, K):
         raise ValueError(f"gemm256 needs M, N % 256 == 0 and K % 64 == 0 (got {M}x{N}x{K})")
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not (a.is_contiguous() and b.is_contiguous()):
@@ -132,14 +133,18 @@ def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: boo
         bias = bias.to(torch.float32).contiguous()
         if bias.data_ptr() % 16:
             bias = bias.clone()
+    if gelu_out is not None and (accumulate or gelu_out.dtype != torch.bfloat16 or gelu_out.shape != out.shape
+                                 or gelu_out.stride() != out.stride() or gelu_out.data_ptr() % 16):
+        raise ValueError("gelu_out must be a bf16 tensor laid out like out (and no accumulate)")
     lib = _native.lib("plx_gemm")
     splits = _native.size("plx_gemm", "plx_gemm256_splits", M, N, K)
     ws = _workspace(a.device, splits * M * N).data_ptr() if splits > 1 else None
     lda = K if a_kmajor else M
     ldb = K if b_kmajor else N
-    rc = lib.plx_gemm256_bias(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, M, N, K, lda, ldb, out.stride(0),
-                              int(a_kmajor), int(b_kmajor), float(alpha), int(accumulate),
-                              bias.data_ptr() if bias is not None else None, _native.current_stream())
+    rc = lib.plx_gemm256_ex(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, M, N, K, lda, ldb, out.stride(0),
+                            int(a_kmajor), int(b_kmajor), float(alpha), int(accumulate),
+                            bias.data_ptr() if bias is not None else None,
+                            gelu_out.data_ptr() if gelu_out is not None else None, _native.current_stream())
     if rc != 0:
         raise RuntimeError(f"plx_gemm256 failed ({rc}) for {M}x{N}x{K} a_kmajor={a_kmajor} b_kmajor={b_kmajor}")
     return out
@@ -162,6 +167,23 @@ def forward(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]
     if _use_native(x2, weight, T, N, fin, True, True):
         return gemm(x2, weight, T, N, fin, True, True, bias=bias)
     return torch.addmm(bias.to(x2.dtype), x2, weight.t())
+
+
+_GELU_EPILOGUE = os.environ.get("PLX_GELU_EPILOGUE", "1") != "0"  # A/B knob: 0 = GEMM then a separate F.gelu
+
+
+def forward_gelu(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None):
+    """(h, gelu_tanh(h)) with h = x . W^T (+ bias): on the MFMA kernel the activation is a second store of the same
+    epilogue (no separate pass reading h back); on hipBLASLt addmm then F.gelu."""
+    T, fin = x2.shape
+    N = weight.shape[0]
+    if _GELU_EPILOGUE and _use_native(x2, weight, T, N, fin, True, True):
+        h = torch.empty(T, N, dtype=torch.bfloat16, device=x2.device)
+        a = torch.empty_like(h)
+        gemm(x2, weight, T, N, fin, True, True, out=h, bias=bias, gelu_out=a)
+        return h, a
+    h = forward(x2, weight, bias)
+    return h, torch.nn.functional.gelu(h, approximate="tanh")
 
 
 def dgrad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:

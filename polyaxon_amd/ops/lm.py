@@ -280,12 +280,12 @@ class _LinearMfma(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         ctx.slot, ctx.flat, ctx.has_bias, ctx.xshape = slot, flat, bias is not None, x.shape
         ctx.bias, ctx.act = bias, act
-        y = gemm.forward(x2, weight, bias)
         if act is None:
+            y = gemm.forward(x2, weight, bias)
             ctx.save_for_backward(x2, weight)
-        else:
-            ctx.save_for_backward(x2, weight, y)
-            y = F.gelu(y, approximate="tanh")
+        else:  # GELU as a second store of the GEMM epilogue (ops/gemm.py forward_gelu)
+            h, y = gemm.forward_gelu(x2, weight, bias)
+            ctx.save_for_backward(x2, weight, h)
         return y.view(*x.shape[:-1], weight.shape[0])
 
     @staticmethod

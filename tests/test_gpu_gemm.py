@@ -206,3 +206,22 @@ def test_autocast_fp32_input_takes_mfma_path(cuda, monkeypatch):
     torch.cuda.synchronize()
     _check(y, x.detach().to(torch.bfloat16).float() @ w.detach().float().t(), 768)
     assert x.grad is not None and x.grad.dtype == torch.float32
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 3072, 768), (256, 256, 8192)])
+def test_gemm256_gelu_epilogue(cuda, M, N, K):
+    """gelu_out (plx_gemm256_ex): the epilogue's second store is gelu_tanh of the bf16 output it stored, against
+    F.gelu(approximate='tanh') of that output -- one-pass tiles and the split-K reduce."""
+    import torch.nn.functional as F
+
+    from polyaxon_amd.ops import gemm
+
+    a = _rand((M, K), cuda, 8)
+    b = _rand((N, K), cuda, 9)
+    bias = torch.randn(N, device=cuda)
+    h = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    g = torch.empty_like(h)
+    gemm.gemm(a, b, M, N, K, True, True, out=h, bias=bias, gelu_out=g)
+    _check(h, a.float() @ b.float().t() + bias, K)
+    ref = F.gelu(h.float(), approximate="tanh")
+    torch.testing.assert_close(g.float(), ref, rtol=1e-2, atol=1e-2)
