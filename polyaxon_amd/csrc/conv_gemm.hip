@@ -164,7 +164,10 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
                float* __restrict__ stats, ConvGeom geo, const __bf16* __restrict__ D, int ldd, BnBwd bnr,
                const uint8_t* __restrict__ dmask) {
-    constexpr bool CONV = MODE == 1 || MODE == 3, STEM = MODE == 2, HALO = MODE == 3;
+    // MODE 4: dense rows whose A operand is a BatchNorm output not yet applied: every A fragment becomes
+    // relu(a * scale[k] + bias[k]) between the LDS read and the MFMA (scale / bias = bnr.mean / bnr.invstd in this
+    // forward-only mode).  Prototype of the BN-apply prologue fusion (plx_gemm_nt_prologue).
+    constexpr bool CONV = MODE == 1 || MODE == 3, STEM = MODE == 2, HALO = MODE == 3, PRO = MODE == 4;
     constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
     constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -385,6 +388,18 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                 const int row = wm * WTM + rm * 16 + fr;
                 const int pc = (kk * 4 + fq) ^ nt_swz(row);
                 fb[rm] = *(const bf16x8*)(As + row * 128 + pc * 16);
+            }
+            if constexpr (PRO) {
+                const int kb = kt * BK + (kk * 4 + fq) * 8;    // this lane's 8 channels
+                const f32x4 s0 = *(const f32x4*)(bnr.mean + kb), s1 = *(const f32x4*)(bnr.mean + kb + 4);
+                const f32x4 b0 = *(const f32x4*)(bnr.invstd + kb), b1 = *(const f32x4*)(bnr.invstd + kb + 4);
+#pragma unroll
+                for (int rm = 0; rm < RM; ++rm)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float sc = e < 4 ? s0[e & 3] : s1[e & 3], bi = e < 4 ? b0[e & 3] : b1[e & 3];
+                        fb[rm][e] = (__bf16)fmaxf(fmaf((float)fb[rm][e], sc, bi), 0.f);
+                    }
             }
 #pragma unroll
             for (int rn = 0; rn < RN; ++rn)
@@ -1046,6 +1061,28 @@ int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int 
     const bool one = nt_single(bwd, false, K, ((M + 255) / 256) * (N / 64));
     return one ? launch_nt<256, 64, 4, 1, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask)
                : launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
+}
+
+// Prototype of the BatchNorm-apply prologue (MODE 4): C = relu(A * scale + bias) . B^T, the per-channel affine of A
+// (scale / bias fp32 [K], 16-byte aligned) applied to the MFMA fragments instead of a separate apply pass writing
+// relu(bn(A)).  Forward only, same tile selection as plx_gemm_nt; stats (nullable) as there.  Used by
+// scripts/diag_bn_prologue.py to price the fusion on the ResNet-50 1x1 shapes.
+int plx_gemm_nt_prologue(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                         const void* zero, const float* scale, const float* bias, float* stats, void* stream) {
+    if (M <= 0 || N % 64 || K % BK || lda % 8 || ldb % 8 || ldc % 8 || !scale || !bias) return -1;
+    if ((uintptr_t)scale % 16 || (uintptr_t)bias % 16) return -1;
+    BnBwd b{};
+    b.mean = scale;
+    b.invstd = bias;
+    hipStream_t s = (hipStream_t)stream;
+    if (N % 128 == 0) {
+        const bool one = nt_single(false, false, K, ((M + 127) / 128) * (N / 128));
+        return one ? launch_nt<128, 128, 2, 2, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, nullptr, 0, b)
+                   : launch_nt<128, 128, 2, 2, 4, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, nullptr, 0, b);
+    }
+    const bool one = nt_single(false, false, K, ((M + 255) / 256) * (N / 64));
+    return one ? launch_nt<256, 64, 4, 1, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, nullptr, 0, b)
+               : launch_nt<256, 64, 4, 1, 4, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, nullptr, 0, b);
 }
 
 // A/B knob: single-buffer NT GEMM mode (see nt_single)

@@ -259,6 +259,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
     },
     "plx_conv": {
         "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P],
+        "plx_gemm_nt_prologue": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
         "plx_gemm_nt_rows_per_block": [_I],
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
         "plx_set_tn_plan": [_I, _I],
