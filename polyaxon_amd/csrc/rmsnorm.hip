@@ -42,15 +42,26 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
   return t;
 }
 
+// ADD: the residual add feeding the norm is fused in -- s = bf16(x + res) is written (the next residual) and
+// normalised; the second pass re-reads the s chunk this same thread wrote.
+template <bool ADD = false>
 __global__ __launch_bounds__(kBlock) void rms_fwd_kernel(const bf16x8* __restrict__ x, const float* __restrict__ w,
                                                          bf16x8* __restrict__ y, float* __restrict__ rstd_out,
-                                                         int64_t rows, int dv, float eps) {
+                                                         int64_t rows, int dv, float eps,
+                                                         const bf16x8* __restrict__ res = nullptr,
+                                                         bf16x8* __restrict__ s_out = nullptr) {
   __shared__ float sh[kBlock / 64];
   for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
-    const bf16x8* xr = x + r * dv;
+    const bf16x8* xr = ADD ? s_out + r * dv : x + r * dv;  // pass 2 reads the sum
     float ss = 0.f;
     for (int i = threadIdx.x; i < dv; i += kBlock) {
-      const bf16x8 v = xr[i];
+      bf16x8 v = x[r * dv + i];
+      if (ADD) {
+        const bf16x8 rv = res[r * dv + i];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v.v[k] = f2bf(bf2f(v.v[k]) + bf2f(rv.v[k]));
+        s_out[r * dv + i] = v;
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float f = bf2f(v.v[k]);
@@ -70,10 +81,13 @@ __global__ __launch_bounds__(kBlock) void rms_fwd_kernel(const bf16x8* __restric
   }
 }
 
+// ADD: dx = RMSNorm backward + dres (the residual path's gradient), fp32 sum rounded once
+template <bool ADD = false>
 __global__ __launch_bounds__(kBlock) void rms_bwd_kernel(const bf16x8* __restrict__ x, const float* __restrict__ w,
                                                          const bf16x8* __restrict__ dy, const float* __restrict__ rstd_in,
                                                          bf16x8* __restrict__ dx, float* __restrict__ dw_part,
-                                                         int64_t rows, int dv) {
+                                                         int64_t rows, int dv,
+                                                         const bf16x8* __restrict__ dres = nullptr) {
   __shared__ float sh[kBlock / 64];
   float dwacc[kMaxVecPerLane][8];
 #pragma unroll
@@ -102,11 +116,14 @@ __global__ __launch_bounds__(kBlock) void rms_bwd_kernel(const bf16x8* __restric
       const int i = threadIdx.x + j * kBlock;
       if (i < dv) {
         const bf16x8 xv = x[r * dv + i], gv = dy[r * dv + i];
+        bf16x8 dr = {};
+        if (ADD) dr = dres[r * dv + i];
         bf16x8 o;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float xh = bf2f(xv.v[k]) * rstd;
-          o.v[k] = f2bf(rstd * (bf2f(gv.v[k]) * w[i * 8 + k] - xh * mean_dot));
+          const float g = rstd * (bf2f(gv.v[k]) * w[i * 8 + k] - xh * mean_dot);
+          o.v[k] = f2bf(ADD ? g + bf2f(dr.v[k]) : g);
         }
         dx[r * dv + i] = o;
       }
@@ -465,8 +482,8 @@ PLX_API int plx_rms_forward(const void* x, const float* w, void* y, float* rstd,
                             hipStream_t stream) {
   if (d % 8 || d > kBlock * 8 * kMaxVecPerLane || rows <= 0) return 1;
   int64_t g = rows < 4096 ? rows : 4096;
-  hipLaunchKernelGGL(rms_fwd_kernel, dim3((int)g), dim3(kBlock), 0, stream, (const bf16x8*)x, w, (bf16x8*)y, rstd, rows,
-                     d / 8, eps);
+  hipLaunchKernelGGL(rms_fwd_kernel<false>, dim3((int)g), dim3(kBlock), 0, stream, (const bf16x8*)x, w, (bf16x8*)y, rstd,
+                     rows, d / 8, eps, (const bf16x8*)nullptr, (bf16x8*)nullptr);
   return (int)hipGetLastError();
 }
 
@@ -476,8 +493,8 @@ PLX_API int plx_rms_bwd_blocks(int64_t rows) { return (int)(rows < 1024 ? rows :
 PLX_API int plx_rms_backward(const void* x, const float* w, const void* dy, const float* rstd, void* dx,
                              float* dw_part, int64_t rows, int d, hipStream_t stream) {
   if (d % 8 || d > kBlock * 8 * kMaxVecPerLane || rows <= 0) return 1;
-  hipLaunchKernelGGL(rms_bwd_kernel, dim3(plx_rms_bwd_blocks(rows)), dim3(kBlock), 0, stream, (const bf16x8*)x, w,
-                     (const bf16x8*)dy, rstd, (bf16x8*)dx, dw_part, rows, d / 8);
+  hipLaunchKernelGGL(rms_bwd_kernel<false>, dim3(plx_rms_bwd_blocks(rows)), dim3(kBlock), 0, stream, (const bf16x8*)x, w,
+                     (const bf16x8*)dy, rstd, (bf16x8*)dx, dw_part, rows, d / 8, (const bf16x8*)nullptr);
   return (int)hipGetLastError();
 }
 
@@ -571,5 +588,24 @@ PLX_API int plx_add_ln_backward(const void* s, const float* w, const void* dy, c
   auto k = vpl == 1 ? ln_bwd_wave_kernel<1, true> : ln_bwd_wave_kernel<2, true>;
   hipLaunchKernelGGL(k, dim3(plx_ln_bwd_blocks(rows, d)), dim3(kBlock), 0, stream, (const bf16x8*)s, w, (const bf16x8*)dy,
                      mean, rstd, (bf16x8*)dx, dw_part, db_part, rows, d / 8, (const bf16x8*)dres);
+  return (int)hipGetLastError();
+}
+
+// fused residual add + RMSNorm (Llama): s = bf16(x + res) (written), y = RMSNorm(s); backward dx = RMSNorm backward
+// (s, dy) + dres for both inputs, dw partials as plx_rms_backward
+PLX_API int plx_add_rms_forward(const void* x, const void* res, const float* w, void* s, void* y, float* rstd,
+                                int64_t rows, int d, float eps, hipStream_t stream) {
+  if (d % 8 || d > kBlock * 8 * kMaxVecPerLane || rows <= 0) return 1;
+  int64_t g = rows < 4096 ? rows : 4096;
+  hipLaunchKernelGGL(rms_fwd_kernel<true>, dim3((int)g), dim3(kBlock), 0, stream, (const bf16x8*)x, w, (bf16x8*)y, rstd,
+                     rows, d / 8, eps, (const bf16x8*)res, (bf16x8*)s);
+  return (int)hipGetLastError();
+}
+
+PLX_API int plx_add_rms_backward(const void* s, const float* w, const void* dy, const float* rstd, const void* dres,
+                                 void* dx, float* dw_part, int64_t rows, int d, hipStream_t stream) {
+  if (d % 8 || d > kBlock * 8 * kMaxVecPerLane || rows <= 0) return 1;
+  hipLaunchKernelGGL(rms_bwd_kernel<true>, dim3(plx_rms_bwd_blocks(rows)), dim3(kBlock), 0, stream, (const bf16x8*)s, w,
+                     (const bf16x8*)dy, rstd, (bf16x8*)dx, dw_part, rows, d / 8, (const bf16x8*)dres);
   return (int)hipGetLastError();
 }

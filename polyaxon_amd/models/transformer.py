@@ -206,9 +206,9 @@ class Transformer(nn.Module):
             if self._rope is None or self._rope[0].shape[0] < S or self._rope[0].device != tokens.device:
                 self._rope = rope_cache(max(S, 16), self.cfg.head_dim, self.cfg.rope_theta, tokens.device)
             rope = (self._rope[0][:S], self._rope[1][:S])  # fp32 tables; the attention casts as needed
-        if self.cfg.norm != "rmsnorm" and not (self.cfg.checkpoint and self.training):
-            # GPT-2: every residual add is fused into the LayerNorm that reads its sum (ops/rmsnorm.py
-            # add_layer_norm) -- the same computation as Block.forward, one pass fewer over the residual per add
+        if not (self.cfg.checkpoint and self.training):
+            # every residual add is fused into the norm that reads its sum (ops/rmsnorm.py add_layer_norm /
+            # add_rms_norm) -- the same computation as Block.forward, one pass fewer over the residual per add
             r = None
             for blk in self.blocks:
                 x, h = self._add_norm(x, r, blk.n1)
@@ -231,6 +231,8 @@ class Transformer(nn.Module):
     def _add_norm(x, r, norm):
         if r is None:
             return x, norm(x)
+        if isinstance(norm, RMSNorm):
+            return _rms.add_rms_norm(x, r, norm.weight, norm.eps)
         return _rms.add_layer_norm(x, r, norm.weight, norm.bias, norm.eps)
 
     def num_params(self) -> int:

@@ -321,6 +321,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_rms_bwd_blocks": [_L],
         "plx_ln_bwd_blocks": [_L, _I],
         "plx_add_ln_forward": [_P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _F, _P],
+        "plx_add_rms_forward": [_P, _P, _P, _P, _P, _P, _L, _I, _F, _P],
+        "plx_add_rms_backward": [_P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
         "plx_add_ln_backward": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
         "plx_set_ln_wave": [_I],
         "plx_partial_colsum_workspace": [_I, _I, _I],

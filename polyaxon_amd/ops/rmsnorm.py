@@ -86,6 +86,57 @@ class _RMSNorm(torch.autograd.Function):
         return dx, _param_grads([part], [ctx.param], d)[0], None
 
 
+class _AddRMSNorm(torch.autograd.Function):
+    """(s, y) = (x + res, RMSNorm(x + res)) in one pass (csrc/rmsnorm.hip plx_add_rms_forward); backward: the norm's
+    dx plus the residual gradient ds in one pass, returned for both x and res."""
+
+    @staticmethod
+    def forward(ctx, x, res, weight, eps):
+        ctx.set_materialize_grads(False)
+        lib = _native.lib("plx_rms")
+        d = x.shape[-1]
+        rows = x.numel() // d
+        s, y = torch.empty_like(x), torch.empty_like(x)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        w = weight.float().contiguous()
+        _native.check(lib.plx_add_rms_forward(x.data_ptr(), res.data_ptr(), w.data_ptr(), s.data_ptr(), y.data_ptr(),
+                                              rstd.data_ptr(), rows, d, float(eps), _stream()), "plx_add_rms_forward")
+        ctx.save_for_backward(s, w, rstd)
+        ctx.param = weight
+        return s, y
+
+    @staticmethod
+    def backward(ctx, ds, dy):
+        lib = _native.lib("plx_rms")
+        s, w, rstd = ctx.saved_tensors
+        if dy is None:
+            return ds, ds, None, None
+        d = s.shape[-1]
+        rows = s.numel() // d
+        dy = dy.contiguous().to(s.dtype)
+        dx = torch.empty_like(s)
+        part = torch.empty((lib.plx_rms_bwd_blocks(rows), d), dtype=torch.float32, device=s.device)
+        if ds is None:
+            _native.check(lib.plx_rms_backward(s.data_ptr(), w.data_ptr(), dy.data_ptr(), rstd.data_ptr(), dx.data_ptr(),
+                                               part.data_ptr(), rows, d, _stream()), "plx_rms_backward")
+        else:
+            ds = ds.contiguous().to(s.dtype)
+            _native.check(lib.plx_add_rms_backward(s.data_ptr(), w.data_ptr(), dy.data_ptr(), rstd.data_ptr(),
+                                                   ds.data_ptr(), dx.data_ptr(), part.data_ptr(), rows, d, _stream()),
+                          "plx_add_rms_backward")
+        return dx, dx, _param_grads([part], [ctx.param], d)[0], None
+
+
+def add_rms_norm(x: torch.Tensor, res: torch.Tensor, weight: torch.Tensor, eps: float = 1e-5):
+    """(s, y) = (x + res, RMSNorm(s)): the pre-norm residual add fused into the next RMSNorm for bf16 GPU rows; the
+    separate add and :func:`rms_norm` otherwise."""
+    if (supported(x) and res.dtype == x.dtype and res.shape == x.shape and x.is_contiguous() and res.is_contiguous()
+            and os.environ.get("PLX_ADD_LN", "1") != "0"):
+        return _AddRMSNorm.apply(x, res, weight, eps)
+    s = x + res
+    return s, rms_norm(s, weight, eps)
+
+
 def supported(x: torch.Tensor) -> bool:
     d = x.shape[-1]
     return x.is_cuda and x.dtype == torch.bfloat16 and d % 8 == 0 and d <= 8192

@@ -9,9 +9,12 @@ import torch.nn.functional as F
 
 
 def host_us(fn, n=200):
+    for _ in range(5):  # library handles, heuristics and allocator warm
+        fn()
     torch.cuda.synchronize()
-    big = torch.empty(1 << 28, dtype=torch.uint8, device="cuda")
-    big.fill_(1)  # ~a few ms of GPU work queued first: the loop below measures enqueue time only
+    big = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    for _ in range(20):
+        big.fill_(1)  # several ms of GPU work queued first: the loop below measures enqueue time only
     t0 = time.perf_counter()
     for _ in range(n):
         fn()

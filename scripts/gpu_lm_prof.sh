@@ -14,7 +14,7 @@ python scripts/lm_step_streams.py "$db" --steps 2 > gpurun_out/${TAG}_streams.md
 cat gpurun_out/${TAG}_streams.md
 if [ -n "${NEIGHBORS:-}" ]; then  # comma-separated kernel-name patterns: who launches them
   IFS=',' read -ra pats <<< "$NEIGHBORS"
-  for p in "${pats[@]}"; do python scripts/kernel_neighbors.py "$db" "$p" --n 2 --skip 40; done > gpurun_out/${TAG}_neighbors.txt
+  for p in "${pats[@]}"; do python scripts/kernel_neighbors.py "$db" "$p" --n 2 ${NEIGHBORS_ARGS:---skip 40}; done > gpurun_out/${TAG}_neighbors.txt
   cat gpurun_out/${TAG}_neighbors.txt
 fi
 grep tokens_per_s gpurun_out/${TAG}.log | tail -1 | cut -c1-200

@@ -115,22 +115,31 @@ def test_add_layernorm_matches_fp32(cuda, rows, d):
     torch.testing.assert_close(b.grad, br.grad, rtol=2e-2, atol=2e-2 * rows ** 0.5)
 
 
-def test_gpt2_fused_residual_norm_path_matches_block_path(cuda):
-    """Transformer.forward's GPT-2 path (every residual add fused into the next LayerNorm) against the plain
+@pytest.mark.parametrize("arch", ["gpt2", "llama"])
+def test_fused_residual_norm_path_matches_block_path(cuda, arch):
+    """Transformer.forward (every residual add fused into the next LayerNorm / RMSNorm) against the plain
     Block.forward loop on the same weights: logits and the loss gradient of every parameter."""
-    from polyaxon_amd.models.transformer import Transformer, gpt2_125m, lm_loss
+    from polyaxon_amd.models.transformer import Transformer, gpt2_125m, lm_loss, tiny_llama
 
     torch.manual_seed(0)
-    cfg = gpt2_125m(vocab_size=512, n_layers=2, d_model=256, n_heads=4, d_ff=1024, max_seq_len=128)
+    cfg = (gpt2_125m(vocab_size=512, n_layers=2, d_model=256, n_heads=4, d_ff=1024, max_seq_len=128) if arch == "gpt2"
+           else tiny_llama(vocab_size=512, d_model=256, n_heads=4, n_kv_heads=2, d_ff=512, max_seq_len=128))
     with torch.device(cuda):
         model = Transformer(cfg)
     tok = torch.randint(0, 512, (2, 128), device=cuda)
 
     def block_path(m):
-        x = m.embed(tok) + m.pos(torch.arange(tok.shape[1], device=cuda))[None]
+        x = m.embed(tok)
+        rope = None
+        if m.pos is not None:
+            x = x + m.pos(torch.arange(tok.shape[1], device=cuda))[None]
+        else:
+            m(tok[:, :2])  # builds the rope cache
+            rope = (m._rope[0][:tok.shape[1]], m._rope[1][:tok.shape[1]])
         for blk in m.blocks:
-            x = blk(x, None)
-        return torch.nn.functional.linear(m.norm(x), m.embed.weight)
+            x = blk(x, rope)
+        x = m.norm(x)
+        return torch.nn.functional.linear(x, m.embed.weight if m.head is None else m.head.weight)
 
     out = {}
     for name, fn in (("fused", model), ("blocks", block_path)):
@@ -144,3 +153,31 @@ def test_gpt2_fused_residual_norm_path_matches_block_path(cuda):
     for n, g in out["blocks"][1].items():
         gf = out["fused"][1][n]
         assert float((gf - g).norm()) <= 0.03 * float(g.norm()) + 1e-6, n
+
+
+
+@pytest.mark.parametrize("rows,d", [(37, 4096), (300, 264)])
+def test_add_rmsnorm_matches_fp32(cuda, rows, d):
+    """Fused residual add + RMSNorm (plx_add_rms_forward / _backward) vs the bf16 add then the fp32 reference: both
+    outputs, the gradient of both inputs (norm backward + residual gradient in one pass) and dweight."""
+    from polyaxon_amd.ops.rmsnorm import add_rms_norm, rms_norm_reference
+
+    torch.manual_seed(2)
+    x = torch.randn(rows, d, device=cuda).to(torch.bfloat16).requires_grad_()
+    r = torch.randn(rows, d, device=cuda).to(torch.bfloat16).requires_grad_()
+    w = (torch.rand(d, device=cuda) + 0.5).requires_grad_()
+    s, y = add_rms_norm(x, r, w, 1e-5)
+    sr = (x.detach() + r.detach()).float().requires_grad_()
+    wr = w.detach().clone().requires_grad_()
+    xf = sr
+    yr = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    assert torch.equal(s, (x + r).detach())
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=3e-2)
+    gs = torch.randn(rows, d, device=cuda).to(torch.bfloat16)
+    gy = torch.randn(rows, d, device=cuda).to(torch.bfloat16)
+    torch.autograd.backward([s, y], [gs, gy])
+    yr.backward(gy.float())
+    ref_dx = sr.grad + gs.float()
+    torch.testing.assert_close(x.grad.float(), ref_dx, rtol=3e-2, atol=3e-2 * float(ref_dx.abs().max()))
+    torch.testing.assert_close(r.grad.float(), ref_dx, rtol=3e-2, atol=3e-2 * float(ref_dx.abs().max()))
+    torch.testing.assert_close(w.grad, wr.grad, rtol=2e-2, atol=2e-2 * rows ** 0.5)
