@@ -942,9 +942,17 @@ inline bool nt_single(bool bwd, bool conv, int K, int nwg) {
 }
 
 // m-slicing of the weight-gradient GEMM
-struct TnPlan { int kchunk, slices, groups, per_group, blocks; };
+struct TnPlan { int kchunk, slices, groups, per_group, blocks, bn1, bn2; };
 
-inline void tn_tile(int N1, int N2, int& bn1, int& bn2) {
+// Wide weight-gradient tiles (plx_set_tn_wide): 256 x 128 (or 128 x 256) outputs per 4-wave block with 32-row
+// double-buffered stages -- 48 KB of LDS (the 128 x 128 double buffer takes 64 KB) and 85 instead of 64 MFMA FLOP
+// per staged byte, so the side stream moves a quarter fewer L2 -> LDS bytes beside the data-gradient chain.  Only
+// where the wide plan still launches at least min(CUs, narrow plan's blocks) blocks.
+int g_tn_wide = 0;
+
+inline void tn_tile(int N1, int N2, int& bn1, int& bn2, bool wide = false) {
+    if (wide && N1 % 256 == 0 && N2 % 128 == 0) { bn1 = 256; bn2 = 128; return; }
+    if (wide && N2 % 256 == 0 && N1 % 128 == 0) { bn1 = 128; bn2 = 256; return; }
     bn1 = N1 % 128 == 0 ? 128 : 64;
     bn2 = N2 % 128 == 0 ? 128 : 64;
 }
@@ -960,9 +968,9 @@ int g_tn_bpc_big = 3, g_tn_bpc_mid = 1;  // by-size plan: 56x56 layers, 28x28 la
 long g_tn_slab_bytes = 16l << 20;
 
 // bpc > 0 overrides the blocks-per-CU target (the stem's weight gradient runs alone at the end of the backward)
-inline TnPlan tn_plan(int M, int N1, int N2, int num_cus, int bpc = 0) {
+inline TnPlan tn_plan_tile(int M, int N1, int N2, int num_cus, int bpc, bool wide) {
     int bn1, bn2;
-    tn_tile(N1, N2, bn1, bn2);
+    tn_tile(N1, N2, bn1, bn2, wide);
     const int ntiles = (N1 / bn1) * (N2 / bn2);
     const long plane = (long)N1 * N2;
     // ~4 blocks per CU (one 4-wave block per CU leaves each SIMD a single wave: latency-bound), >= 4
@@ -990,7 +998,18 @@ inline TnPlan tn_plan(int M, int N1, int N2, int num_cus, int bpc = 0) {
     if (groups < 1) groups = 1;
     const int per_group = (slices + groups - 1) / groups;
     groups = (slices + per_group - 1) / per_group;
-    return {kchunk, slices, groups, per_group, blocks};
+    return {kchunk, slices, groups, per_group, blocks, bn1, bn2};
+}
+
+inline TnPlan tn_plan(int M, int N1, int N2, int num_cus, int bpc = 0) {
+    const TnPlan narrow = tn_plan_tile(M, N1, N2, num_cus, bpc, false);
+    if (!g_tn_wide || bpc > 0) return narrow;
+    const TnPlan wide = tn_plan_tile(M, N1, N2, num_cus, bpc, true);
+    if (wide.bn1 == narrow.bn1 && wide.bn2 == narrow.bn2) return narrow;
+    const long nb = (long)(N1 / narrow.bn1) * (N2 / narrow.bn2) * narrow.slices;
+    const long wb = (long)(N1 / wide.bn1) * (N2 / wide.bn2) * wide.slices;
+    const long floor_blocks = nb < (num_cus > 0 ? num_cus : 256) ? nb : (num_cus > 0 ? num_cus : 256);
+    return wb >= floor_blocks ? wide : narrow;
 }
 
 // Rows per stage of the weight-gradient GEMM (A/B knob plx_set_tn_stages' second argument: 64 or 32)
@@ -1103,6 +1122,9 @@ void plx_set_tn_stages(int n, int bk) {
     if (bk == 32 || bk == 64) g_tn_bk = bk;
 }
 
+// A/B knob: wide (256 x 128 / 128 x 256) weight-gradient tiles (see g_tn_wide); set before sizing workspaces
+void plx_set_tn_wide(int on) { g_tn_wide = on ? 1 : 0; }
+
 // weight-gradient slicing knobs; workspace sizes follow them, so set before sizing / launching
 void plx_set_tn_plan(int blocks_per_cu, int slab_mb) {
     if (blocks_per_cu >= 0) g_tn_blocks_per_cu = blocks_per_cu;  // 0: by problem size (tn_plan)
@@ -1118,8 +1140,10 @@ void plx_set_tn_sizes(int big, int mid) {
 // floats of slab workspace plx_gemm_tn needs for this problem
 long plx_gemm_tn_workspace(int M, int N1, int N2, int num_cus) {
     if (M <= 0 || N1 % 64 || N2 % 64) return -1;
-    const TnPlan p = tn_plan(M, N1, N2, num_cus);
-    return (long)(p.slices + (p.groups > 1 ? p.groups : 0)) * N1 * N2;
+    // the larger of the narrow and wide plans, whatever the knob: a size memoised before plx_set_tn_wide still fits
+    const TnPlan a = tn_plan_tile(M, N1, N2, num_cus, 0, false), b = tn_plan_tile(M, N1, N2, num_cus, 0, true);
+    const long na = a.slices + (a.groups > 1 ? a.groups : 0), nb = b.slices + (b.groups > 1 ? b.groups : 0);
+    return (na > nb ? na : nb) * N1 * N2;
 }
 
 }  // extern "C"
@@ -1130,7 +1154,11 @@ int run_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int
            const void* zero, int num_cus, int accumulate, hipStream_t s, ConvGeom geo, int bpc = 0) {
     const TnPlan plan = tn_plan(M, N1, N2, num_cus, bpc);
     int rc;
-    if (N1 % 128 == 0 && N2 % 128 == 0)
+    if (plan.bn1 == 256)
+        rc = launch_tn_st<256, 128, 2, 2, CONV, 2, 32>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
+    else if (plan.bn2 == 256)
+        rc = launch_tn_st<128, 256, 2, 2, CONV, 2, 32>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
+    else if (N1 % 128 == 0 && N2 % 128 == 0)
         rc = launch_tn<128, 128, 2, 2, CONV>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
     else if (N1 % 128 == 0)
         rc = launch_tn<128, 64, 4, 1, CONV>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);

@@ -175,6 +175,8 @@ def lib(name: str) -> ctypes.CDLL:
         if name == "plx_conv" and os.environ.get("PLX_TN_STAGES"):  # A/B knob: weight-gradient LDS ring depth
             st, _, bk = os.environ["PLX_TN_STAGES"].partition(",")  # "stages[,rows per stage]"
             handle.plx_set_tn_stages(int(st), int(bk or 0))
+        if name == "plx_conv" and os.environ.get("PLX_TN_WIDE"):  # A/B knob: 256x128 weight-gradient tiles
+            handle.plx_set_tn_wide(int(os.environ["PLX_TN_WIDE"]))
         if name == "plx_bn" and os.environ.get("PLX_STEM_BWD_CAP"):  # A/B knob: stem backward partials-pass rows
             handle.plx_set_stem_bwd_cap(int(os.environ["PLX_STEM_BWD_CAP"]))
         if name == "plx_rms" and os.environ.get("PLX_LN_WAVE"):  # A/B knob: wave-per-row LayerNorm (d <= 1024)
@@ -267,6 +269,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_set_nt_single_stage": [_I],
         "plx_set_halo": [_I],
         "plx_set_tn_stages": [_I, _I],
+        "plx_set_tn_wide": [_I],
         "plx_set_nt_tall": [_I, _I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],

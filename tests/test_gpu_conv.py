@@ -498,3 +498,30 @@ def test_gemm_tn_stage_rings(cuda, stages, bk):
     w = conv.weight.detach().float().requires_grad_()
     F.conv2d(x.detach().float(), w, None, 1, 1).backward(g)
     torch.testing.assert_close(conv.weight.grad.float(), w.grad, rtol=2e-2, atol=2e-2 * float(w.grad.abs().max()))
+
+
+def test_gemm_tn_wide_tiles(cuda):
+    """Wide weight-gradient tiles (plx_set_tn_wide: 256x128 and 128x256 with 32-row stages) against fp32: dense shapes
+    that take each orientation (ragged reductions), and a 3x3 convolution weight gradient whose 256-channel taps take
+    the 128x256 tile through the gather."""
+    from polyaxon_amd.ops import _native
+    from polyaxon_amd.ops.conv import ConvKxK
+    from polyaxon_amd.ops.conv1x1 import gemm_tn
+
+    lib = _native.lib("plx_conv")
+    lib.plx_set_tn_wide(1)
+    try:
+        torch.manual_seed(3)
+        for m, n1, n2 in ((50000 + 37, 256, 128), (40000 + 5, 128, 512), (30000, 512, 256), (777, 256, 256)):
+            a, b = _bf(m, n1, dev=cuda), _bf(m, n2, dev=cuda)
+            torch.testing.assert_close(gemm_tn(a, b), a.float().t() @ b.float(), rtol=1e-3, atol=1e-3 * m ** 0.5)
+        conv = ConvKxK(256, 128, 3, 1).to(cuda)
+        x = torch.randn(8, 256, 30, 29, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y = conv(x.requires_grad_())
+        g = torch.randn_like(y.float())
+        y.backward(g.to(torch.bfloat16))
+    finally:
+        lib.plx_set_tn_wide(0)
+    w = conv.weight.detach().float().requires_grad_()
+    F.conv2d(x.detach().float(), w, None, 1, 1).backward(g)
+    torch.testing.assert_close(conv.weight.grad.float(), w.grad, rtol=2e-2, atol=2e-2 * float(w.grad.abs().max()))
