@@ -448,8 +448,12 @@ def main() -> int:
     if dev.type == "cuda" and os.environ.get("PLX_BENCH_RCCL", "1") != "0":
         from polyaxon_amd.parallel.rccl import RcclComm
 
-        comm = (RcclComm.from_torch_distributed() if world > 1
-                else RcclComm(RcclComm.new_unique_id(), 1, 0, local))
+        try:
+            comm = (RcclComm.from_torch_distributed() if world > 1
+                    else RcclComm(RcclComm.new_unique_id(), 1, 0, local))
+        except Exception as e:  # a communicator that cannot be built must not cost the measured result
+            print(f"bench: RCCL communicator unavailable ({e}); per-rank gather over gloo", file=sys.stderr)
+            comm = None
     if comm is not None:
         t = torch.tensor(mine, dtype=torch.float64, device=dev)
         per_rank = comm.all_gather(t).cpu().tolist()

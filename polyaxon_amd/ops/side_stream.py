@@ -69,6 +69,11 @@ def _stream_for(dev: torch.device) -> "torch.cuda.Stream":
     return s
 
 
+def stream_for(dev: torch.device) -> "torch.cuda.Stream":
+    """The device's side stream (created on first use)."""
+    return _stream_for(dev)
+
+
 def run(fn: Callable[[], None], tensors: Iterable[torch.Tensor], dev: torch.device) -> None:
     if not enabled() or dev.type != "cuda" or (capturing() and not _CAPTURE_FORK):
         fn()

@@ -44,13 +44,7 @@ class SyntheticImages:
     def next(self) -> None:
         """Refill ``x``/``y`` in place with the next batch of the stream."""
         if self.is_cuda:
-            if not self.x.is_contiguous(memory_format=torch.channels_last):
-                raise ValueError("device generator writes NHWC (channels_last) images")
-            rc = _native.lib("plx_train").plx_synth_images(
-                self.x.data_ptr(), self.y.data_ptr(), self.batch, self.image, self.image, self.proto.data_ptr(),
-                self.active, self.grid, self.signal, self.seed & 0xFFFFFFFFFFFFFFFF, self.counter.data_ptr(),
-                torch.cuda.current_stream(self.device).cuda_stream)
-            _native.check(rc, "plx_synth_images")
+            self.next_into(self.x, self.y, torch.cuda.current_stream(self.device))
             return
         y = torch.randint(0, self.active, (self.batch,), generator=self._cpu_gen)
         mean = self.expected_mean(y)
@@ -58,6 +52,22 @@ class SyntheticImages:
         self.x.copy_(mean + noise)
         self.y.copy_(y)
         self.counter += 1
+
+    def next_into(self, x: torch.Tensor, y: torch.Tensor, stream: "torch.cuda.Stream") -> None:
+        """Device path: write the next batch of the stream into ``x``/``y`` (shaped as ``self.x``/``self.y``) on
+        ``stream``.  The batch counter advances on that stream, so every launch of one stream of batches must be
+        ordered after the previous one (the executor's prefetch keeps them all on one side stream after the first)."""
+        if not self.is_cuda:
+            raise RuntimeError("next_into is the device generator's path")
+        if not x.is_contiguous(memory_format=torch.channels_last):
+            raise ValueError("device generator writes NHWC (channels_last) images")
+        if x.shape != self.x.shape or x.dtype != self.x.dtype or y.shape != self.y.shape or y.dtype != self.y.dtype:
+            raise ValueError("batch buffers must match the generator's x / y")
+        rc = _native.lib("plx_train").plx_synth_images(
+            x.data_ptr(), y.data_ptr(), self.batch, self.image, self.image, self.proto.data_ptr(),
+            self.active, self.grid, self.signal, self.seed & 0xFFFFFFFFFFFFFFFF, self.counter.data_ptr(),
+            stream.cuda_stream)
+        _native.check(rc, "plx_synth_images")
 
     def expected_mean(self, y: torch.Tensor) -> torch.Tensor:
         """``signal * upsample(proto[y])`` as an NCHW fp32 tensor (the noise-free image of each label)."""

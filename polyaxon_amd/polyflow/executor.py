@@ -83,6 +83,16 @@ class ResidentTrialExecutor:
         self._init_spec = spec
         self._init_tables = self.flat.init_tables(spec) if (spec is not None and self.is_cuda) else None
         self.use_graph = use_graph and self.is_cuda
+        # Eager device path: batch k+1 is generated on the side stream while step k's backward ends (the side
+        # stream idles once its last weight gradient is done, beside the main stream's stem chain and optimizer),
+        # into the other of two batch buffers; step k+1's forward waits on an event instead of running the
+        # generator.  A graph-captured step keeps the generator inside the graph.  PLX_PREFETCH_BATCH=0: off.
+        self._prefetch = (self.is_cuda and not self.use_graph and self.data is not None
+                          and hasattr(self.data, "next_into") and side_stream.enabled()
+                          and os.environ.get("PLX_PREFETCH_BATCH", "1") != "0")
+        self._bufs = None          # [(x, y), (x, y)] when prefetching
+        self._cur = 0              # buffer the next step consumes
+        self._ready = None         # event after the generator wrote self._bufs[self._cur], or None
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_rejected = False
         self.graph_check_error: Optional[float] = None
@@ -114,7 +124,20 @@ class ResidentTrialExecutor:
 
     # ------------------------------------------------------------------ the step
     def _train_step(self) -> None:
-        if self.data is not None:
+        prefetch = self._prefetch and not torch.cuda.is_current_stream_capturing()
+        if prefetch:
+            main = torch.cuda.current_stream(self.device)
+            if self._bufs is None:
+                self._bufs = [(self.data.x, self.data.y), (torch.empty_like(self.data.x), torch.empty_like(self.data.y))]
+            if self._ready is None:
+                self.data.next_into(*self._bufs[self._cur], main)
+            else:
+                main.wait_event(self._ready)
+            self.x, self.y = self._bufs[self._cur]
+            # every earlier step's use of the other buffer is complete in main-stream order from here
+            step_start = torch.cuda.Event()
+            step_start.record(main)
+        elif self.data is not None:
             self.data.next()
         if self.wcache is not None:
             self.wcache.activate()
@@ -131,6 +154,15 @@ class ResidentTrialExecutor:
             if self.wcache is not None:
                 self.wcache.deactivate()
         side_stream.join(self.device)  # weight-gradient GEMMs overlapped on the side stream (ops/side_stream.py)
+        if prefetch:
+            # queued after the join: the main stream does not wait for it before the optimizer
+            side = side_stream.stream_for(self.device)
+            side.wait_event(step_start)
+            nxt = self._cur ^ 1
+            self.data.next_into(*self._bufs[nxt], side)
+            self._ready = torch.cuda.Event()
+            self._ready.record(side)
+            self._cur = nxt
         self.opt.step_()
         self._record(loss.detach())
 

@@ -54,3 +54,29 @@ def test_executor_learns_fresh_synthetic_task(cuda):
     losses = ex.losses()
     assert float(losses[:5].mean()) > 1.8
     assert float(losses[-10:].mean()) < 1.0, losses[-10:]
+
+
+def test_executor_batch_prefetch_matches_inline(cuda):
+    """Side-stream prefetch of the next batch (executor._prefetch, eager path): the same batch stream, the same
+    training trajectory and the same per-step losses as generating each batch inline on the main stream."""
+    from polyaxon_amd.models.resnet import resnet50
+    from polyaxon_amd.ops.synth import SyntheticImages
+    from polyaxon_amd.polyflow.executor import ResidentTrialExecutor
+
+    out = {}
+    for prefetch in (False, True):
+        torch.manual_seed(0)
+        data = SyntheticImages(4, 64, cuda, classes=1000, active_classes=100, grid=7, signal=0.5, seed=5)
+        ex = ResidentTrialExecutor(resnet50(), data, cuda, use_graph=False)
+        ex._prefetch = prefetch
+        ex.reset(seed=1)
+        ex.set_hparams(lr=0.05, momentum=0.9, weight_decay=1e-4)
+        ex.run(4)
+        torch.cuda.synchronize()
+        out[prefetch] = (ex.losses(), ex.flat.params.detach().float().clone(), int(data.counter.item()))
+        if prefetch:
+            assert ex._ready is not None and ex._bufs is not None  # the prefetch path really ran
+        del ex
+    assert out[True][2] == out[False][2] + 1  # one batch generated ahead
+    torch.testing.assert_close(out[True][0], out[False][0], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(out[True][1], out[False][1], rtol=1e-4, atol=1e-5)
