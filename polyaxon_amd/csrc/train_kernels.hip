@@ -113,6 +113,17 @@ __device__ __forceinline__ unsigned short f_to_bf16(float f) {  // hardware RNE 
   return __builtin_bit_cast(unsigned short, (__bf16)f);
 }
 
+// One mixed-precision AdamW element, with every rounding step explicit (no contraction left to the compiler), so the
+// 4-wide and 8-wide kernels -- and per-bucket launches that mix them -- give bitwise the same update
+__device__ __forceinline__ float adamw_elem(float p, float& m, float& v, float g, float b1, float b2, float eps,
+                                            float step_size, float inv_sqrt_bc2, float decay) {
+#pragma clang fp contract(off)
+  m = fmaf(b1, m, (1.f - b1) * g);
+  v = fmaf(b2, v, ((1.f - b2) * g) * g);
+  const float denom = fmaf(sqrtf(v), inv_sqrt_bc2, eps);
+  return fmaf(p, decay, -((step_size * m) / denom));
+}
+
 __global__ __launch_bounds__(kBlock) void adamw_mixed_kernel(float4* __restrict__ p, u16x4* __restrict__ g,
                                                              float4* __restrict__ m, float4* __restrict__ v,
                                                              u16x4* __restrict__ plp, int64_t n_vec, int decay_on,
@@ -131,11 +142,7 @@ __global__ __launch_bounds__(kBlock) void adamw_mixed_kernel(float4* __restrict_
     u16x4 lo;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float gg = bf16_to_f(gv[k]);
-      mm[k] = b1 * mm[k] + (1.f - b1) * gg;
-      vq[k] = b2 * vq[k] + (1.f - b2) * gg * gg;
-      const float denom = sqrtf(vq[k]) * inv_sqrt_bc2 + eps;
-      pp[k] = pp[k] * decay - step_size * mm[k] / denom;
+      pp[k] = adamw_elem(pp[k], mm[k], vq[k], bf16_to_f(gv[k]), b1, b2, eps, step_size, inv_sqrt_bc2, decay);
       lo[k] = f_to_bf16(pp[k]);
     }
     p[i] = make_float4(pp[0], pp[1], pp[2], pp[3]);
@@ -145,6 +152,57 @@ __global__ __launch_bounds__(kBlock) void adamw_mixed_kernel(float4* __restrict_
     g[i] = u16x4{0, 0, 0, 0};
   }
 }
+
+// Same update, 8 elements per thread: the bf16 gradient / model-copy accesses become 16-B vectors (4 x 16 B + 2 x
+// 16 B per lane instead of 3 x 16 B + 3 x 8 B per 4 elements) and every stream is non-temporal -- each of the ~30 B
+// per parameter is touched once per step, far past the caches.  Used when n % 8 == 0 and every pointer is 16-B
+// aligned (plx_set_adamw_wide A/B knob).
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x8v __attribute__((ext_vector_type(8)));
+
+__global__ __launch_bounds__(kBlock) void adamw_mixed8_kernel(f32x4v* __restrict__ p, u16x8v* __restrict__ g,
+                                                              f32x4v* __restrict__ m, f32x4v* __restrict__ v,
+                                                              u16x8v* __restrict__ plp, int64_t n8, int decay_on,
+                                                              const float* __restrict__ hp,
+                                                              const int* __restrict__ step_ptr) {
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4];
+  const float t = (float)(*step_ptr + 1);
+  const float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
+  const float step_size = lr / bc1, inv_sqrt_bc2 = rsqrtf(bc2);
+  const float decay = decay_on ? (1.f - lr * wd) : 1.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    f32x4v pv[2], mv[2], vv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      pv[h] = __builtin_nontemporal_load(p + 2 * i + h);
+      mv[h] = __builtin_nontemporal_load(m + 2 * i + h);
+      vv[h] = __builtin_nontemporal_load(v + 2 * i + h);
+    }
+    const u16x8v gv = __builtin_nontemporal_load(g + i);
+    u16x8v lo;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int h = k >> 2, e = k & 3;
+      float mk = mv[h][e], vk = vv[h][e];
+      const float pk = adamw_elem(pv[h][e], mk, vk, bf16_to_f(gv[k]), b1, b2, eps, step_size, inv_sqrt_bc2, decay);
+      mv[h][e] = mk;
+      vv[h][e] = vk;
+      pv[h][e] = pk;
+      lo[k] = f_to_bf16(pk);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __builtin_nontemporal_store(pv[h], p + 2 * i + h);
+      __builtin_nontemporal_store(mv[h], m + 2 * i + h);
+      __builtin_nontemporal_store(vv[h], v + 2 * i + h);
+    }
+    __builtin_nontemporal_store(lo, plp + i);
+    __builtin_nontemporal_store(u16x8v{0, 0, 0, 0, 0, 0, 0, 0}, g + i);
+  }
+}
+
+int g_adamw_wide = 0;
 
 // fp32 master -> bf16 model copy (after re-initialisation, checkpoint load or a parameter broadcast)
 __global__ __launch_bounds__(kBlock) void cast_lp_kernel(const float4* __restrict__ p, u16x4* __restrict__ plp,
@@ -340,11 +398,21 @@ PLX_API int plx_adamw_flat(float* p, float* g, float* m, float* v, int64_t n, in
   return (int)hipGetLastError();
 }
 
+// A/B knob: 8-wide non-temporal mixed-precision AdamW (1) or the 4-wide kernel (0, default)
+PLX_API void plx_set_adamw_wide(int on) { g_adamw_wide = on ? 1 : 0; }
+
 PLX_API void plx_set_adamw_grid_cap(int blocks) { g_adamw_grid_cap = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks); }
 
 PLX_API int plx_adamw_mixed(float* p, void* g, float* m, float* v, void* plp, int64_t n, int decay_on,
                             const float* hp, const int* step, hipStream_t stream) {
   if (n & 3) return 1;
+  const bool aligned = ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v | (uintptr_t)plp) % 16 == 0;
+  if (g_adamw_wide && (n & 7) == 0 && aligned) {
+    const int64_t n8 = n >> 3;
+    hipLaunchKernelGGL(adamw_mixed8_kernel, dim3(grid_for(n8, g_adamw_grid_cap)), dim3(kBlock), 0, stream,
+                       (f32x4v*)p, (u16x8v*)g, (f32x4v*)m, (f32x4v*)v, (u16x8v*)plp, n8, decay_on, hp, step);
+    return (int)hipGetLastError();
+  }
   const int64_t nv = n >> 2;
   hipLaunchKernelGGL(adamw_mixed_kernel, dim3(grid_for(nv, g_adamw_grid_cap)), dim3(kBlock), 0, stream, (float4*)p, (u16x4*)g,
                      (float4*)m, (float4*)v, (u16x4*)plp, nv, decay_on, hp, step);

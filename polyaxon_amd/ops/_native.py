@@ -175,6 +175,8 @@ def lib(name: str) -> ctypes.CDLL:
         if name == "plx_conv" and os.environ.get("PLX_TN_STAGES"):  # A/B knob: weight-gradient LDS ring depth
             st, _, bk = os.environ["PLX_TN_STAGES"].partition(",")  # "stages[,rows per stage]"
             handle.plx_set_tn_stages(int(st), int(bk or 0))
+        if name == "plx_train" and os.environ.get("PLX_ADAMW_WIDE"):  # A/B knob: 8-wide non-temporal AdamW
+            handle.plx_set_adamw_wide(int(os.environ["PLX_ADAMW_WIDE"]))
         if name == "plx_conv" and os.environ.get("PLX_TN_WIDE"):  # A/B knob: 256x128 weight-gradient tiles
             handle.plx_set_tn_wide(int(os.environ["PLX_TN_WIDE"]))
         if name == "plx_bn" and os.environ.get("PLX_STEM_BWD_CAP"):  # A/B knob: stem backward partials-pass rows
@@ -217,6 +219,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_commit_metric": [_P, _P, _I, _I, _P, _I, _P],
         "plx_synth_images": [_P, _P, _I, _I, _I, _P, _I, _I, _F, _U64, _P, _P],
         "plx_set_adamw_grid_cap": [_I],
+        "plx_set_adamw_wide": [_I],
     },
     "plx_bn": {
         "plx_bn_workspace": [_L, _I],
@@ -354,7 +357,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_partial_colsum_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_set_stem_bwd_cap": None, "plx_set_bn_fin_threads": None, "plx_set_ln_wave": None, "plx_set_adamw_grid_cap": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_partial_colsum_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_set_stem_bwd_cap": None, "plx_set_bn_fin_threads": None, "plx_set_ln_wave": None, "plx_set_adamw_grid_cap": None, "plx_set_adamw_wide": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

@@ -62,11 +62,12 @@ def test_adamw_flat_matches_torch(cuda):
     torch.testing.assert_close(p, torch.cat([pa.detach(), pb.detach()]), rtol=1e-5, atol=1e-6)
 
 
-def test_adamw_mixed_matches_torch(cuda):
+@pytest.mark.parametrize("n", [4096 * 9 + 4, 4096 * 9 + 8])
+def test_adamw_mixed_matches_torch(cuda, n):
     """bf16 grads + fp32 master: same update as torch AdamW fed the (bf16-exact) grads; the bf16 model copy is
-    the round-to-nearest-even of the master; the bf16 grads are zeroed."""
+    the round-to-nearest-even of the master; the bf16 grads are zeroed.  n % 8 == 4 takes the 4-wide kernel, n % 8
+    == 0 the 8-wide non-temporal one."""
     lib = _native.lib("plx_train")
-    n = 4096 * 9 + 4
     p = torch.randn(n, device=cuda)
     m = torch.zeros(n, device=cuda)
     v = torch.zeros(n, device=cuda)
@@ -235,3 +236,30 @@ def test_maxpool3s2_matches_torch(cuda, shape):
     y.backward(g)
     yr.backward(g)
     torch.testing.assert_close(xa.grad.float(), xr.grad.float(), rtol=1e-2, atol=1e-2)
+
+
+def test_adamw_mixed_wide_matches_narrow(cuda):
+    """The 8-wide non-temporal AdamW kernel (plx_set_adamw_wide 1) is bitwise the 4-wide one: both run adamw_elem,
+    whose rounding steps are explicit (per-bucket launches mixing the two must equal one monolithic launch)."""
+    lib = _native.lib("plx_train")
+    n = 8192 * 5
+    torch.manual_seed(4)
+    p0, m0, v0 = torch.randn(n, device=cuda), torch.randn(n, device=cuda) * 0.1, torch.rand(n, device=cuda) * 0.01
+    g0 = torch.randn(n, device=cuda).to(torch.bfloat16)
+    hp = torch.tensor([1e-3, 0.9, 0.95, 1e-8, 0.1, 0, 0, 0], device=cuda)
+    step = torch.full((1,), 7, dtype=torch.int32, device=cuda)
+    res = {}
+    try:
+        for wide in (0, 1):
+            lib.plx_set_adamw_wide(wide)
+            p, m, v, g = p0.clone(), m0.clone(), v0.clone(), g0.clone()
+            plp = torch.empty(n, dtype=torch.bfloat16, device=cuda)
+            _native.check(lib.plx_adamw_mixed(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), plp.data_ptr(),
+                                              n, 1, hp.data_ptr(), step.data_ptr(), _stream()), "adamw_mixed")
+            torch.cuda.synchronize()
+            res[wide] = (p, m, v, plp, g)
+    finally:
+        lib.plx_set_adamw_wide(0)  # the library default
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+    assert float(res[1][4].float().abs().max()) == 0.0
