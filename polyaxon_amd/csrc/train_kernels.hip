@@ -160,6 +160,7 @@ __global__ __launch_bounds__(kBlock) void adamw_mixed_kernel(float4* __restrict_
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef unsigned short u16x8v __attribute__((ext_vector_type(8)));
 
+template <bool NT>
 __global__ __launch_bounds__(kBlock) void adamw_mixed8_kernel(f32x4v* __restrict__ p, u16x8v* __restrict__ g,
                                                               f32x4v* __restrict__ m, f32x4v* __restrict__ v,
                                                               u16x8v* __restrict__ plp, int64_t n8, int decay_on,
@@ -175,11 +176,11 @@ __global__ __launch_bounds__(kBlock) void adamw_mixed8_kernel(f32x4v* __restrict
     f32x4v pv[2], mv[2], vv[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      pv[h] = __builtin_nontemporal_load(p + 2 * i + h);
-      mv[h] = __builtin_nontemporal_load(m + 2 * i + h);
-      vv[h] = __builtin_nontemporal_load(v + 2 * i + h);
+      pv[h] = NT ? __builtin_nontemporal_load(p + 2 * i + h) : p[2 * i + h];
+      mv[h] = NT ? __builtin_nontemporal_load(m + 2 * i + h) : m[2 * i + h];
+      vv[h] = NT ? __builtin_nontemporal_load(v + 2 * i + h) : v[2 * i + h];
     }
-    const u16x8v gv = __builtin_nontemporal_load(g + i);
+    const u16x8v gv = NT ? __builtin_nontemporal_load(g + i) : g[i];
     u16x8v lo;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -191,14 +192,25 @@ __global__ __launch_bounds__(kBlock) void adamw_mixed8_kernel(f32x4v* __restrict
       pv[h][e] = pk;
       lo[k] = f_to_bf16(pk);
     }
+    if constexpr (NT) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      __builtin_nontemporal_store(pv[h], p + 2 * i + h);
-      __builtin_nontemporal_store(mv[h], m + 2 * i + h);
-      __builtin_nontemporal_store(vv[h], v + 2 * i + h);
+      for (int h = 0; h < 2; ++h) {
+        __builtin_nontemporal_store(pv[h], p + 2 * i + h);
+        __builtin_nontemporal_store(mv[h], m + 2 * i + h);
+        __builtin_nontemporal_store(vv[h], v + 2 * i + h);
+      }
+      __builtin_nontemporal_store(lo, plp + i);
+      __builtin_nontemporal_store(u16x8v{0, 0, 0, 0, 0, 0, 0, 0}, g + i);
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        p[2 * i + h] = pv[h];
+        m[2 * i + h] = mv[h];
+        v[2 * i + h] = vv[h];
+      }
+      plp[i] = lo;
+      g[i] = u16x8v{0, 0, 0, 0, 0, 0, 0, 0};
     }
-    __builtin_nontemporal_store(lo, plp + i);
-    __builtin_nontemporal_store(u16x8v{0, 0, 0, 0, 0, 0, 0, 0}, g + i);
   }
 }
 
@@ -398,8 +410,9 @@ PLX_API int plx_adamw_flat(float* p, float* g, float* m, float* v, int64_t n, in
   return (int)hipGetLastError();
 }
 
-// A/B knob: 8-wide non-temporal mixed-precision AdamW (1) or the 4-wide kernel (0, default)
-PLX_API void plx_set_adamw_wide(int on) { g_adamw_wide = on ? 1 : 0; }
+// A/B knob: 8-wide mixed-precision AdamW with non-temporal streams (1), with plain loads / stores (2), or the
+// 4-wide kernel (0, default)
+PLX_API void plx_set_adamw_wide(int on) { g_adamw_wide = on < 0 ? 0 : (on > 2 ? 2 : on); }
 
 PLX_API void plx_set_adamw_grid_cap(int blocks) { g_adamw_grid_cap = blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks); }
 
@@ -409,7 +422,7 @@ PLX_API int plx_adamw_mixed(float* p, void* g, float* m, float* v, void* plp, in
   const bool aligned = ((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v | (uintptr_t)plp) % 16 == 0;
   if (g_adamw_wide && (n & 7) == 0 && aligned) {
     const int64_t n8 = n >> 3;
-    hipLaunchKernelGGL(adamw_mixed8_kernel, dim3(grid_for(n8, g_adamw_grid_cap)), dim3(kBlock), 0, stream,
+    hipLaunchKernelGGL(g_adamw_wide == 2 ? adamw_mixed8_kernel<false> : adamw_mixed8_kernel<true>, dim3(grid_for(n8, g_adamw_grid_cap)), dim3(kBlock), 0, stream,
                        (f32x4v*)p, (u16x8v*)g, (f32x4v*)m, (f32x4v*)v, (u16x8v*)plp, n8, decay_on, hp, step);
     return (int)hipGetLastError();
   }

@@ -250,7 +250,7 @@ def test_adamw_mixed_wide_matches_narrow(cuda):
     step = torch.full((1,), 7, dtype=torch.int32, device=cuda)
     res = {}
     try:
-        for wide in (0, 1):
+        for wide in (0, 1, 2):
             lib.plx_set_adamw_wide(wide)
             p, m, v, g = p0.clone(), m0.clone(), v0.clone(), g0.clone()
             plp = torch.empty(n, dtype=torch.bfloat16, device=cuda)
@@ -260,6 +260,7 @@ def test_adamw_mixed_wide_matches_narrow(cuda):
             res[wide] = (p, m, v, plp, g)
     finally:
         lib.plx_set_adamw_wide(0)  # the library default
-    for a, b in zip(res[0], res[1]):
-        assert torch.equal(a, b)
-    assert float(res[1][4].float().abs().max()) == 0.0
+    for wide in (1, 2):
+        for a, b in zip(res[0], res[wide]):
+            assert torch.equal(a, b)
+        assert float(res[wide][4].float().abs().max()) == 0.0
