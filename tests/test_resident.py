@@ -89,7 +89,7 @@ def _worker_thread(program="resnet_tiny", params=TINY, max_active=8):
     return w, sched, t
 
 
-def _collect(sched, n_brackets, timeout=120):
+def _collect(sched, n_brackets, timeout=300):  # generous: CPU training slows under a loaded parallel run
     evs = []
     done = 0
     end = time.time() + timeout
