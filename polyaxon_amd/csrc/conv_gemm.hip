@@ -53,7 +53,20 @@ struct ConvGeom {
     // the taps at (hv[i], wv[j]): a row's in-image tap mask is 6 compares and 9 selects (NT GEMM staging)
     int nh, nw, hv[3], wv[3];
     uint32_t pat[9];
+    // reduction order of the NT GEMM's stages: 0 tap-major (k = t * C + ch, tap outer), 1 tap-inner (all taps of a
+    // 64-channel chunk back to back: the shifted A rows of consecutive stages overlap and are re-read from L1)
+    int tap_inner;
 };
+
+// v[t] for a wave-uniform runtime t < 9 as a select chain: indexing the by-value ConvGeom's arrays with a runtime
+// index made hipcc copy the struct to scratch and reload from it per stage (a VMEM load whose wait, vmcnt(0), also
+// drained every LDS-DMA in flight)
+__device__ __forceinline__ int pick9(const int (&v)[9], int t) {
+    int r = v[0];
+#pragma unroll
+    for (int i = 1; i < 9; ++i) r = t == i ? v[i] : r;
+    return r;
+}
 
 inline uint32_t div_magic(int d) { return d <= 1 ? 0u : (uint32_t)((1ull << 32) / (unsigned)d + 1); }
 
@@ -114,6 +127,11 @@ __device__ __forceinline__ size_t out_row(const ConvGeom& g, int m) {
 }
 constexpr int NTHREADS = 256;   // 4 waves
 
+template <int V>
+struct IC {
+    static constexpr int value = V;
+};
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     // consecutive logical ids on one XCD (blocks are dealt round-robin over the 8 XCDs); bijective for any nwg
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -158,8 +176,12 @@ __device__ __forceinline__ int nt_swz(int row) { return (row >> 1) & 7; }
 // chunk as a halo (the block's BM output pixels +- (W + 1) flattened pixels) and read by all 9 taps from LDS at a
 // per-tap row shift; only the weights are staged per tap.  Mode 1 re-stages the gathered A rows for every tap: 9x the
 // input bytes through the per-CU LDS-DMA path, which bounds those layers (~52 GB/s per CU, 34 % of MFMA peak).
-template <int BM, int BN, int WGM, int WGN, int MODE, int MINB = 2, int NBUF = 2, bool BWD = false>
-__global__ void __launch_bounds__(NTHREADS, MINB)
+// NTH = 512 with NBUF = 3 is the pipelined kernel (PIPE): 8 waves as WGM x WGN over a 256 x 128 tile, a 3-stage LDS
+// ring whose DMAs stay in flight across the phase barriers behind a counted vmcnt, and the two 4-wave groups one
+// barrier apart (ping-pong), so each SIMD overlaps one wave's MFMAs with the other wave's fragment reads / DMA issue
+// (csrc/gemm256.hip's schedule with the implicit-conv row gather as the A loader)
+template <int BM, int BN, int WGM, int WGN, int MODE, int MINB = 2, int NBUF = 2, bool BWD = false, int NTH = NTHREADS>
+__global__ void __launch_bounds__(NTH, MINB)
 gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
                int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
                float* __restrict__ stats, ConvGeom geo, const __bf16* __restrict__ D, int ldd, BnBwd bnr,
@@ -168,6 +190,11 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     // relu(a * scale[k] + bias[k]) between the LDS read and the MFMA (scale / bias = bnr.mean / bnr.invstd in this
     // forward-only mode).  Prototype of the BN-apply prologue fusion (plx_gemm_nt_prologue).
     constexpr bool CONV = MODE == 1 || MODE == 3, STEM = MODE == 2, HALO = MODE == 3, PRO = MODE == 4;
+    constexpr bool PIPE = NBUF == 3;
+    constexpr int NW = NTH / 64;                           // waves
+    static_assert(WGM * WGN == NW, "one wave per wave tile");
+    static_assert(!PIPE || (NTH == 512 && !HALO && !PRO && !STEM), "the ring schedule is the 8-wave dense/conv kernel");
+    static_assert(PIPE || NTH == 256, "the lock-step kernels are 4 waves");
     constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
     constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -186,11 +213,12 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     // source pixel is inside the image (else the zero page is read: the zero padding).  A stage then costs one
     // bit test, one add and a select per row -- the per-stage bounds checks and 64-bit address math were ~20
     // VALU per row and, beside 32 MFMAs per wave and stage, set the loop's pace.
-    int a_off[BM / 32];                                     // byte offsets
-    uint32_t a_ok[BM / 32];
+    constexpr int AI = BM / (8 * NW), BI = BN / (8 * NW);  // LDS-DMA instructions per wave per stage (A, B)
+    int a_off[AI];                                          // byte offsets
+    uint32_t a_ok[AI];
 #pragma unroll
-    for (int i = 0; i < (HALO ? 0 : BM / 32); ++i) {
-        const int row = (i * 4 + wave) * 8 + (lane >> 3);
+    for (int i = 0; i < (HALO ? 0 : AI); ++i) {
+        const int row = (i * NW + wave) * 8 + (lane >> 3);
         const int lc = (lane & 7) ^ nt_swz(row);
         const int gm = m0 + row;
         if constexpr (CONV) {
@@ -229,36 +257,43 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
             a_ok[i] = gm < M ? 1u : 0u;
         }
     }
-    int b_off[BN / 32];
+    int b_off[BI];
 #pragma unroll
-    for (int i = 0; i < BN / 32; ++i) {
-        const int row = (i * 4 + wave) * 8 + (lane >> 3);
+    for (int i = 0; i < BI; ++i) {
+        const int row = (i * NW + wave) * 8 + (lane >> 3);
         b_off[i] = ((n0 + row) * ldb + ((lane & 7) ^ nt_swz(row)) * 8) * 2;
     }
     const __amdgpu_buffer_rsrc_t ra = buf_rsrc(A), rb = buf_rsrc(B);
 
     // staging: each wave instruction moves 1024 B = 8 rows x 8 chunks.  (t, c0): tap and channel offset of
     // reduction index k0 = t * C + c0 (conv mode; t = 0, c0 = k0 otherwise)
-    auto stage = [&](int buf, int k0, int t, int c0) {
+    auto stage_a = [&](int buf, int k0, int t, int c0) {
         char* base = smem + buf * STAGE;
-        int a_add = k0 * 2, bk0 = k0 * 2, bit = 0;
+        int a_add = k0 * 2, bit = 0;
         if constexpr (CONV) {                               // lda == C in conv mode
-            a_add = geo.tap_a[t] + c0 * 2;
-            bk0 = geo.tap_b[t] + c0 * 2;
+            a_add = pick9(geo.tap_a, t) + c0 * 2;
             bit = t;
         }
         if constexpr (STEM) bit = k0 / BK;
 #pragma unroll
-        for (int i = 0; i < BM / 32; ++i) {                 // A: BM rows / 8 rows per instr / 4 waves
+        for (int i = 0; i < AI; ++i) {                      // A: BM rows / 8 rows per instr / NW waves
             if constexpr (STEM) {                           // this lane's chunk = tap t of the 7 x 4 super-pixel window
-                const int t = bit * 8 + ((lane & 7) ^ nt_swz((i * 4 + wave) * 8 + (lane >> 3)));
+                const int t = bit * 8 + ((lane & 7) ^ nt_swz((i * NW + wave) * 8 + (lane >> 3)));
                 a_add = ((t >> 2) * geo.W + (t & 3)) * 16;
             }
             const uint32_t off = (a_ok[i] >> bit) & 1u ? (uint32_t)(a_off[i] + a_add) : OOB;
-            blds16(ra, off, base + (i * 4 + wave) * 1024);
+            blds16(ra, off, base + (i * NW + wave) * 1024);
         }
+    };
+    auto stage_b = [&](int buf, int k0, int t, int c0) {
+        char* base = smem + buf * STAGE;
+        const int bk0 = CONV ? pick9(geo.tap_b, t) + c0 * 2 : k0 * 2;
 #pragma unroll
-        for (int i = 0; i < BN / 32; ++i) blds16(rb, (uint32_t)(b_off[i] + bk0), base + A_BYTES + (i * 4 + wave) * 1024);
+        for (int i = 0; i < BI; ++i) blds16(rb, (uint32_t)(b_off[i] + bk0), base + A_BYTES + (i * NW + wave) * 1024);
+    };
+    auto stage = [&](int buf, int k0, int t, int c0) {
+        stage_a(buf, k0, t, c0);
+        stage_b(buf, k0, t, c0);
     };
 
     f32x4 acc[RN][RM];
@@ -350,27 +385,122 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                 }
             }
         }
+    } else if constexpr (PIPE) {
+        // ---- ring schedule.  Tile kt lives in LDS buffer kt % 3.  Each tile runs 2 phases (kk = 0, 1: 16 MFMAs per
+        // wave each); phase 0 issues the A rows of tile kt + 2 into buffer (kt + 2) % 3 (= tile kt - 1's, whose last
+        // reads retired before the previous barrier), phase 1 its B rows and then waits until tile kt + 1 has landed
+        // (counted vmcnt: tile kt + 2's AI + BI DMAs may stay in flight).  Tile kt + 1 is first read one phase after
+        // that wait (RAW), also by the lagging group, whose wait precedes the barrier the leading group reads behind.
+        // Never __syncthreads() here: its fence would drain vmcnt.
+        const int nk = K / BK;
+        const int cdim = CONV ? geo.C : K;
+        const int grp = wave / 4;                           // waves w and w + 4 share a SIMD
+        int st = 0, sc = 0, kis = 0;                        // (tap, channel offset, k) of the next tile to issue
+        const bool tap_inner = CONV && geo.tap_inner;
+        auto advance = [&]() {                              // selects, no branches: a branchy form made hipcc keep
+            kis += BK;                                      // (st, sc) on the stack behind flat pointers
+            const bool wt = st + 1 == geo.ntaps, wc = sc + BK == cdim;
+            const int st_i = wt ? 0 : st + 1, sc_i = wt ? sc + BK : sc;
+            const int st_m = wc ? st + 1 : st, sc_m = wc ? 0 : sc + BK;
+            st = tap_inner ? st_i : st_m;
+            sc = tap_inner ? sc_i : sc_m;
+        };
+        auto phase = [&](const char* As, const char* Bs, int kk, bf16x8 (&fa)[RN], bf16x8 (&fb)[RM]) {
+#pragma unroll
+            for (int rn = 0; rn < RN; ++rn) {
+                const int row = wn * WTN + rn * 16 + fr;
+                fa[rn] = *(const bf16x8*)(Bs + row * 128 + (((kk * 4 + fq) ^ nt_swz(row)) * 16));
+            }
+#pragma unroll
+            for (int rm = 0; rm < RM; ++rm) {
+                const int row = wm * WTM + rm * 16 + fr;
+                fb[rm] = *(const bf16x8*)(As + row * 128 + (((kk * 4 + fq) ^ nt_swz(row)) * 16));
+            }
+        };
+        auto mfma = [&](const bf16x8 (&fa)[RN], const bf16x8 (&fb)[RM]) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int rn = 0; rn < RN; ++rn)
+#pragma unroll
+                for (int rm = 0; rm < RM; ++rm)
+                    acc[rn][rm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rn], fb[rm], acc[rn][rm], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+        };
+        constexpr int INFL = AI + BI;                       // one tile's DMAs per wave
+        static_assert(INFL == 6, "vmcnt immediates below assume 4 + 2 DMAs per wave per tile");
+        auto tile = [&](auto cb, int kt) {
+            constexpr int CB = decltype(cb)::value, NB = (CB + 2) % 3;
+            const char* As = smem + CB * STAGE;
+            const char* Bs = As + A_BYTES;
+            const bool more = kt + 2 < nk;
+            {
+                bf16x8 fa[RN], fb[RM];
+                phase(As, Bs, 0, fa, fb);
+                if (more) stage_a(NB, kis, st, sc);
+                mfma(fa, fb);
+            }
+            {
+                bf16x8 fa[RN], fb[RM];
+                phase(As, Bs, 1, fa, fb);
+                if (more) {
+                    stage_b(NB, kis, st, sc);
+                    advance();
+                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                mfma(fa, fb);
+            }
+        };
+        stage(0, kis, st, sc);
+        advance();
+        if (nk > 1) {
+            stage(1, kis, st, sc);
+            advance();
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        if (grp == 1) __builtin_amdgcn_s_barrier();        // ping-pong: group 1 runs one barrier behind
+        for (int kt = 0; kt < nk; kt += 3) {
+            tile(IC<0>{}, kt);
+            if (kt + 1 < nk) tile(IC<1>{}, kt + 1);
+            if (kt + 2 < nk) tile(IC<2>{}, kt + 2);
+        }
+        if (grp == 0) __builtin_amdgcn_s_barrier();        // every wave executes the same number of barriers
     } else {
     const int nk = K / BK;
     const int cdim = CONV ? geo.C : K;                      // channels per tap
+    int st = 0, sc = 0;                                     // (tap, channel offset) of the next stage
+    const bool tap_inner = CONV && geo.tap_inner;           // uniform
+    auto advance = [&]() {                                  // selects, no branches (see the ring loop's advance)
+        const bool wt = st + 1 == geo.ntaps, wc = sc + BK == cdim;
+        const int st_i = wt ? 0 : st + 1, sc_i = wt ? sc + BK : sc;
+        const int st_m = wc ? st + 1 : st, sc_m = wc ? 0 : sc + BK;
+        st = tap_inner ? st_i : st_m;
+        sc = tap_inner ? sc_i : sc_m;
+    };
     stage(0, 0, 0, 0);
-    int st = 0, sc = BK;                                    // (tap, channel offset) of the next stage
-    if (sc == cdim) { sc = 0; ++st; }
+    advance();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = NBUF == 2 ? kt & 1 : 0;
         if (NBUF == 1 && kt > 0) {                          // restage the single buffer (the loop's tail barrier
             stage(0, kt * BK, st, sc);                      // retired its readers)
-            sc += BK;
-            if (sc == cdim) { sc = 0; ++st; }
+            advance();
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
         }
         if (NBUF == 2 && kt + 1 < nk) {
             stage(cur ^ 1, (kt + 1) * BK, st, sc);
-            sc += BK;
-            if (sc == cdim) { sc = 0; ++st; }
+            advance();
         }
         const char* As = smem + cur * STAGE;
         const char* Bs = As + A_BYTES;
@@ -420,8 +550,8 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     // pass (rows past M are clamped to a valid row and discarded: no per-row branch around a load).
     constexpr int CROW = BN * 2 + 16;
     constexpr int CHUNKS = BN / 8;                          // 16-B chunks per output row
-    static_assert(NTHREADS % CHUNKS == 0, "a thread keeps one chunk column over the store loop");
-    constexpr int RSTEP = NTHREADS / CHUNKS, ITERS = BM / RSTEP;
+    static_assert(NTH % CHUNKS == 0, "a thread keeps one chunk column over the store loop");
+    constexpr int RSTEP = NTH / CHUNKS, ITERS = BM / RSTEP;
     const int rows = min(BM, M - m0);
     const int cc = tid % CHUNKS, r0 = tid / CHUNKS;
     const int ch0 = n0 + cc * 8;                            // this thread's 8 channels
@@ -545,7 +675,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     // ways) and every thread then sums ONE (chunk column, value) pair over the RSTEP rows -- 16 loads per thread
     // instead of 16 threads each walking 15 x 16 dependent loads while the rest of the block waits.
     auto reduce_store = [&](const float* va, const float* vb, float* dst_a, float* dst_b) {
-        float* red = (float*)smem;                          // [NTHREADS][17], over the staged tile: its reads
+        float* red = (float*)smem;                          // [NTH][17], over the staged tile: its reads
         __syncthreads();                                    // (the store loop) must be done
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -571,7 +701,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     const int srow = m0 / SROWS, nsr = (M + SROWS - 1) / SROWS;
     auto zero_rows = [&](float* base_a, float* base_b, int ld) {  // rows srow+1 .. srow+SPB-1 (those < nsr)
         if constexpr (SPB > 1) {
-            for (int i = tid; i < (SPB - 1) * BN; i += NTHREADS) {
+            for (int i = tid; i < (SPB - 1) * BN; i += NTH) {
                 const int r = srow + 1 + i / BN, c = i % BN;
                 if (r < nsr) {
                     base_a[(size_t)(r - srow) * ld + c] = 0.f;
@@ -849,27 +979,29 @@ template <int BM, int BN, int WGM, int WGN, int CONV = 0, int NBUF = 2>
 int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
               const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}, const void* D = nullptr,
               int ldd = 0, BnBwd bnr = {}, const uint8_t* dmask = nullptr) {
-    constexpr int TILE = BM * (BN * 2 + 16), RED = NTHREADS * 17 * 4;
+    constexpr int NTH = NBUF == 3 ? 512 : NTHREADS;         // NBUF 3: the 8-wave ring kernel
+    constexpr int TILE = BM * (BN * 2 + 16), RED = NTH * 17 * 4;
     constexpr int EPI = TILE > RED ? TILE : RED;            // the reduction reuses the tile's LDS
     constexpr int KLOOP = NBUF * (BM + BN) * BK * 2;
     constexpr int LDS = KLOOP > EPI ? KLOOP : EPI;
-    static_assert(NBUF == 2 || NBUF == 1, "one or two K stages");
+    static_assert(NBUF >= 1 && NBUF <= 3, "one or two K stages, or the 3-stage ring");
     static_assert(NBUF == 1 || EPI <= KLOOP, "epilogue staging must fit the k-loop LDS");
+    static_assert(LDS <= 160 * 1024, "LDS");
     constexpr int PER_CU = (160 * 1024) / LDS;
     // blocks per CU the registers are asked to allow (128 VGPRs at 4): the double-buffered data-gradient kernel
     // keeps its accumulators live through the epilogue prefetch (~178 VGPRs), the single-buffer one parks them in
     // LDS first (LATE in gemm_nt_kernel)
     constexpr int CAP = CONV != 0 && BN == 64 ? 3 : 4;     // the 256x64 conv staging spills 7-8 VGPRs at 4
-    constexpr int MIN_F = NBUF == 1 ? (PER_CU < CAP ? PER_CU : CAP) : 2, MIN_B = MIN_F;
-    auto kf = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_F, NBUF, false>;
-    auto kb = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_B, NBUF, true>;
+    constexpr int MIN_F = NBUF == 1 ? (PER_CU < CAP ? PER_CU : CAP) : NBUF == 3 ? 1 : 2, MIN_B = MIN_F;
+    auto kf = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_F, NBUF, false, NTH>;
+    auto kb = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_B, NBUF, true, NTH>;
     static int attr = set_lds(kf, LDS) | set_lds(kb, LDS);
     if (attr) return attr;
     const bool bwd = D != nullptr || bnr.part != nullptr;
     if (bwd && stats != nullptr) return -1;
     auto k = bwd ? kb : kf;
     const int nwg = ((M + BM - 1) / BM) * (N / BN);
-    hipLaunchKernelGGL(k, dim3(nwg), dim3(NTHREADS), LDS, s, (const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N,
+    hipLaunchKernelGGL(k, dim3(nwg), dim3(NTH), LDS, s, (const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N,
                        K, lda, ldb, ldc, (const __bf16*)zero, stats, geo, (const __bf16*)D, ldd, bnr, dmask);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
@@ -903,6 +1035,12 @@ int launch_halo(const void* A, const void* B, void* C, int M, int N, int lda, in
 // Off by default: measured 0.99-1.17x the gather mode's time on the ResNet-50 3x3 layers (the halo image costs
 // occupancy: 2 blocks/CU instead of 4), see profiles/r3_negative_results.md.
 int g_halo = 0;
+
+// reduction order of the implicit-GEMM convolutions (A/B knob plx_set_tap_inner): see ConvGeom::tap_inner
+int g_tap_inner = 0;
+
+// the 8-wave ring kernel (NBUF 3, 256 x 128 tiles) for convolutions with N % 128 == 0 (A/B knob plx_set_conv_v2)
+int g_conv_v2 = 0;
 
 inline bool halo_ok(const ConvGeom& g) {
     if (!g_halo || g.ntaps != 9 || g.S != 1 || g.OS != 0 || g.Hr != g.H || g.Wr != g.W || g.C % BK) return false;
@@ -1110,6 +1248,12 @@ void plx_set_nt_single_stage(int mode) { g_nt_single_stage = mode; }
 // A/B knob: halo mode for the stride-1 3x3 convolutions (1 on, 0 the per-tap gather)
 void plx_set_halo(int on) { g_halo = on ? 1 : 0; }
 
+// A/B knob: tap-inner reduction order of the implicit-GEMM convolutions (1) or tap-major (0)
+void plx_set_tap_inner(int on) { g_tap_inner = on ? 1 : 0; }
+
+// A/B knob: the 8-wave ring kernel for the convolutions with N % 128 == 0 (1) or the 4-wave kernels (0)
+void plx_set_conv_v2(int on) { g_conv_v2 = on ? 1 : 0; }
+
 // A/B knob: 256 x 128 NT tiles (0 off, 1 forward, 2 forward + data gradient), see nt_tall
 void plx_set_nt_tall(int mode, int min_k) {
     g_nt_tall = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
@@ -1278,8 +1422,10 @@ int nt_conv(const void* A, const void* B, void* C, int M, int N, const ConvGeom&
 
 inline int nt_rows_per_block(int N) { return N % 128 == 0 ? 128 : 256; }
 
-int nt_conv_any(const void* A, const void* B, void* C, int M, int N, const ConvGeom& g, int ldb, int ldc,
+int nt_conv_any(const void* A, const void* B, void* C, int M, int N, const ConvGeom& g_in, int ldb, int ldc,
                 const void* zero, float* stats, hipStream_t s, const void* D = nullptr, const BnBwd& bnr = {}) {
+    ConvGeom g = g_in;
+    g.tap_inner = g_tap_inner;
     const bool bwd = D != nullptr || bnr.part != nullptr;
     const int K = g.ntaps * g.C;
     if (halo_ok(g)) {
@@ -1288,6 +1434,7 @@ int nt_conv_any(const void* A, const void* B, void* C, int M, int N, const ConvG
             return launch_halo<128, 128, 2, 2, 2>(A, B, C, M, N, g.C, ldb, ldc, zero, stats, s, g, D, ldd, bnr);
         return launch_halo<256, 64, 4, 1, 2>(A, B, C, M, N, g.C, ldb, ldc, zero, stats, s, g, D, ldd, bnr);
     }
+    if (g_conv_v2 && N % 128 == 0) return nt_conv<256, 128, 4, 2, 3>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
     if (nt_tall(bwd, M, N, K)) return nt_conv<256, 128, 2, 2, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
     if (N % 128 == 0)
         return nt_single(bwd, true, K, ((M + 127) / 128) * (N / 128))

@@ -236,8 +236,12 @@ class HyperbandDriver(GroupDriver):
         it.experiments_metrics = [(x, v) for x, v in ((x, self.metric_of(x, metric))
                                                       for x in it.experiment_ids) if v is not None]
         self.store.update_iteration(b["iid"], it.to_dict())
-        if not self.m.should_reduce_configs(it.iteration, it.bracket_iteration):
-            b["done"] = True  # this bracket's last rung
+        # this bracket's last rung: the reference's create_iteration (iteration_managers/hyperband.py:25-36) moves on
+        # to the next bracket as soon as should_reschedule holds, before it considers reducing; only the last bracket
+        # (nothing to reschedule to) keeps reducing while configs remain to keep
+        if (self.m.should_reschedule(it.iteration, it.bracket_iteration)
+                or not self.m.should_reduce_configs(it.iteration, it.bracket_iteration)):
+            b["done"] = True
             return
         keep_ids = self.m.reduce(it)
         nxt = HyperbandIterationConfig(iteration=it.iteration, bracket_iteration=it.bracket_iteration + 1)

@@ -126,9 +126,10 @@ def bracket_units(max_iter: float, eta: float, iteration: int, resume: bool) -> 
         ri = r * eta ** i
         total += n * ((ri - prev) if (resume and i) else ri)
         prev = ri
-        # keep after rung i, exactly as HyperbandSearchManager.get_n_config_to_keep_for_iteration (including the
-        # reference quirk that the last bracket, s = 0, still reduces once: keep(n0, 0) = int(n0 / eta) > 0)
-        n = 0 if i == s + 1 else int(n0 * (eta ** -i) / eta)
+        # the reference's create_iteration: a bracket with a successor ends at rung s (should_reschedule); the last
+        # bracket (s = 0) takes one more reduction, keep = int(n0 / eta) (the reference quirk), and none after it
+        # (get_n_config_to_keep_for_iteration is 0 at rung s + 1)
+        n = 0 if (i >= s and iteration < s_max) or i == s + 1 else int(n0 * (eta ** -i) / eta)
         i += 1
     return total
 

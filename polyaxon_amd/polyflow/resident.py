@@ -587,7 +587,10 @@ class ResidentWorker:
             m = br.manager
             ran = [rec for rec in records if rec[1] is br]
             metrics = [[cid, vals[row][slot]] for (_, _, slot, cid, _, _, _) in ran if not math.isnan(vals[row][slot])]
-            keep = m.get_n_config_to_keep_for_iteration(br.iteration, br.rung)
+            # bracket ends where the reference's create_iteration reschedules (hpsearch/iteration_managers/
+            # hyperband.py:25-36): only the last bracket takes reduce steps past its own rung count
+            keep = (0 if m.should_reschedule(br.iteration, br.rung)
+                    else m.get_n_config_to_keep_for_iteration(br.iteration, br.rung))
             ranked = [br.active[i] for i in orders_h[br.maximize][row]
                       if 0 <= i < len(br.active) and not math.isnan(vals[row][i])]
             br.early_stopped = br.early_stopped or early.get(row, False)

@@ -525,3 +525,52 @@ def test_gemm_tn_wide_tiles(cuda):
     w = conv.weight.detach().float().requires_grad_()
     F.conv2d(x.detach().float(), w, None, 1, 1).backward(g)
     torch.testing.assert_close(conv.weight.grad.float(), w.grad, rtol=2e-2, atol=2e-2 * float(w.grad.abs().max()))
+
+
+@pytest.mark.parametrize("shape,cout,stride", [((2, 128, 28, 28), 128, 1), ((3, 256, 14, 14), 256, 1),
+                                               ((5, 512, 7, 7), 512, 1), ((3, 128, 9, 11), 128, 1),
+                                               ((2, 128, 14, 14), 128, 2), ((3, 256, 13, 9), 256, 2),
+                                               ((2, 64, 9, 7), 128, 1), ((2, 128, 5, 5), 384, 2)])
+def test_conv_ring_kernel_and_tap_order(cuda, shape, cout, stride):
+    """The 8-wave ring kernel (plx_set_conv_v2: 256 x 128 tiles, 3-stage LDS ring, ping-pong wave groups) and the
+    tap-inner reduction order (plx_set_tap_inner) against the 4-wave tap-major kernels and fp32 F.conv2d: forward with
+    the BN channel-stat epilogue, data gradient (stride 2: the parity-class GEMMs with scattered rows), ragged last
+    tiles, and a BN -> conv chain whose BN-backward partials come from the data-gradient epilogue."""
+    from polyaxon_amd.ops import _native
+    from polyaxon_amd.ops.conv import ConvKxK, conv_k
+
+    lib = _native.lib("plx_conv")
+    torch.manual_seed(13)
+    conv = ConvKxK(shape[1], cout, 3, stride).to(cuda)
+    conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
+    x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = {}
+    try:
+        for v2, ti in ((0, 0), (1, 0), (1, 1), (0, 1)):
+            lib.plx_set_conv_v2(v2)
+            lib.plx_set_tap_inner(ti)
+            xa = x.clone().requires_grad_()
+            y = conv_k(xa, conv.weight, stride, with_stats=True)
+            st, nblk = y._plx_channel_stats
+            g = torch.randn(y.shape, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3)).to(y.dtype)
+            y.backward(g)
+            chain = _bn_chain_grads(cuda, lambda: ConvKxK(shape[1], cout, 3, stride), shape, link=True)
+            res[(v2, ti)] = (y.float(), st.view(2, nblk, cout).sum(1), xa.grad.float(), g, chain)
+    finally:
+        lib.plx_set_conv_v2(int(os.environ.get("PLX_CONV_V2", "0")))
+        lib.plx_set_tap_inner(int(os.environ.get("PLX_TAP_INNER", "0")))
+    xr = x.float().clone().requires_grad_()
+    yr = F.conv2d(xr, conv.weight.detach().to(torch.bfloat16).float(), stride=stride, padding=1)
+    yr.backward(res[(0, 0)][3].float())
+    base = res[(0, 0)]
+    for key, (y, st, dx, _, chain) in res.items():
+        torch.testing.assert_close(y, yr, rtol=2e-2, atol=8e-2, msg=str(key))
+        torch.testing.assert_close(dx, xr.grad, rtol=2e-2, atol=8e-2, msg=str(key))
+        yf = y.permute(0, 2, 3, 1).reshape(-1, cout)
+        torch.testing.assert_close(st[0], yf.sum(0), rtol=1e-3, atol=1e-1, msg=str(key))
+        torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1, msg=str(key))
+        # same bf16 rounding points, a different fp32 summation order at most
+        torch.testing.assert_close(y, base[0], rtol=1e-2, atol=2e-2, msg=str(key))
+        torch.testing.assert_close(dx, base[2], rtol=1e-2, atol=2e-2, msg=str(key))
+        for a, b, name in zip(chain, base[4], ("dx", "dgamma", "dbeta", "dw")):
+            torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2 * float(b.abs().max()), msg=f"{key} {name}")

@@ -170,6 +170,48 @@ def test_hyperband_group_promotions(tmp_path):
         flow.shutdown()
 
 
+def _reference_hyperband_schedule(max_iter, eta):
+    """(iteration, bracket_iteration) pairs the reference's create_iteration visits
+    (hpsearch/iteration_managers/hyperband.py:14-50): reschedule first, then reduce."""
+    from polyaxon_amd.polytune.managers import HyperbandSearchManager
+    from polyaxon_amd.spec.hptuning import HPTuningConfig
+
+    m = HyperbandSearchManager(HPTuningConfig.from_dict(
+        {"hyperband": {"max_iter": max_iter, "eta": eta, "resource": {"name": "steps", "type": "int"},
+                       "metric": {"name": "loss", "optimization": "minimize"}},
+         "matrix": {"lr": {"uniform": [0, 1]}}}))
+    seq, it = [], m.next_iteration(None)
+    while True:
+        seq.append((it.iteration, it.bracket_iteration))
+        if m.is_done(it):
+            return m, seq
+        it = m.next_iteration(it)
+
+
+def test_hyperband_brackets_end_where_the_reference_reschedules(tmp_path):
+    """max_iter 8, eta 2: bracket 2's rung 1 has both should_reduce and should_reschedule true; the reference moves
+    to the next bracket there (no third rung at 16 units > max_iter), only the last bracket keeps reducing."""
+    m, ref = _reference_hyperband_schedule(8, 2)
+    assert (2, 1) in ref and (2, 2) not in ref and (3, 1) in ref
+    flow = _flow(tmp_path, n_gpus=8)
+    try:
+        hb = {"hyperband": {"max_iter": 8, "eta": 2, "resource": {"name": "steps", "type": "int"},
+                            "metric": {"name": "loss", "optimization": "minimize"}, "resume": True}, "seed": 4}
+        spec = _group(hb, {"lr": {"uniform": [0.0, 1.0]}, "sleep": {"values": [0.01]}}, _trial_cmd(), concurrency=8)
+        g = flow.submit(spec)
+        assert flow.wait("group", g["id"], timeout=180) == "succeeded"
+        its = flow.store.iterations(g["id"])
+        assert sorted((i["data"]["iteration"], i["data"]["bracket_iteration"]) for i in its) == sorted(ref)
+        for i in its:
+            d = i["data"]
+            want = int(m.get_n_resources_for_iteration(d["iteration"], d["bracket_iteration"]))
+            got = {flow.store.get_experiment(x)["declarations"]["steps"] for x in d["experiment_ids"]}
+            assert got == {want}
+        assert max(x["declarations"]["steps"] for x in flow.store.list_experiments(group_id=g["id"])) <= 2 * 8
+    finally:
+        flow.shutdown()
+
+
 def test_random_group_early_stopping(tmp_path):
     flow = _flow(tmp_path, n_gpus=1)
     try:

@@ -61,18 +61,22 @@ def test_bracket_units_follow_reference_arithmetic():
     from polyaxon_amd.polytune.managers import HyperbandSearchManager
     from polyaxon_amd.spec.hptuning import HPTuningConfig
 
-    for max_iter, eta, resume in ((9, 3, True), (9, 3, False), (81, 3, True), (10, 3, False), (27, 3, True)):
+    for max_iter, eta, resume in ((9, 3, True), (9, 3, False), (81, 3, True), (10, 3, False), (27, 3, True),
+                                  (8, 2, True), (16, 2, False)):
         m = HyperbandSearchManager(HPTuningConfig.from_dict(_hp(max_iter=max_iter, eta=eta, resume=resume)))
+        totals, prev, n = {}, {}, {}
+        cur = m.next_iteration(None)
+        while True:  # walk the reference state machine (reschedule before reduce)
+            it, rung = cur.iteration, cur.bracket_iteration
+            cnt = m.get_n_configs(m.get_bracket(it)) if rung == 0 else n[it]
+            r = m.get_n_resources_for_iteration(it, rung)
+            totals[it] = totals.get(it, 0.0) + cnt * ((r - prev[it]) if (resume and rung) else r)
+            prev[it], n[it] = r, m.get_n_config_to_keep_for_iteration(it, rung)
+            if m.is_done(cur):
+                break
+            cur = m.next_iteration(cur)
         for it in range(m.s_max + 1):
-            # walk the reference state machine for this bracket
-            n, rung, total, prev = m.get_n_configs(m.get_bracket(it)), 0, 0.0, 0.0
-            while n > 0:
-                r = m.get_n_resources_for_iteration(it, rung)
-                total += n * ((r - prev) if (resume and rung) else r)
-                prev = r
-                n = m.get_n_config_to_keep_for_iteration(it, rung)
-                rung += 1
-            assert bracket_units(max_iter, eta, it, resume) == pytest.approx(total)
+            assert bracket_units(max_iter, eta, it, resume) == pytest.approx(totals[it])
 
 
 def _worker_thread(program="resnet_tiny", params=TINY, max_active=8):
@@ -101,6 +105,35 @@ def _collect(sched, n_brackets, timeout=300):  # generous: CPU training slows un
             done += 1
         assert m["ev"] != "error", m
     return evs
+
+
+def test_worker_brackets_end_where_the_reference_reschedules():
+    """eta 2 / max_iter 8: each bracket runs exactly the rungs of the reference state machine
+    (hpsearch/iteration_managers/hyperband.py:25-36: reschedule before reduce)."""
+    from polyaxon_amd.polytune.managers import HyperbandIterationConfig, HyperbandSearchManager
+    from polyaxon_amd.spec.hptuning import HPTuningConfig
+
+    hp = _hp(max_iter=8, eta=2)
+    m = HyperbandSearchManager(HPTuningConfig.from_dict(hp))
+    ref, it = {}, m.next_iteration(None)
+    while True:
+        ref.setdefault(it.iteration, []).append(it.bracket_iteration)
+        if m.is_done(it):
+            break
+        it = m.next_iteration(it)
+    assert ref[2] == [0, 1]  # the case the concurrent driver used to extend to a third rung
+    w, sched, t = _worker_thread()
+    for it in range(m.s_max + 1):
+        sugg = m.get_suggestions(HyperbandIterationConfig(iteration=it))
+        sched.send({"op": "bracket", "key": f"b{it}", "hptuning": hp, "iteration": it, "seed": 5,
+                    "configs": [{"cid": i, "params": {k: v for k, v in s.items() if k != "units"}}
+                                for i, s in enumerate(sugg)]})
+    evs = _collect(sched, m.s_max + 1)
+    ran = {}
+    for e in evs:
+        if e["ev"] == "trial_start":
+            ran.setdefault(int(e["key"][1:]), set()).add(e["rung"])
+    assert {k: sorted(v) for k, v in ran.items()} == ref
 
 
 def test_worker_runs_concurrent_brackets_with_reference_promotions():
