@@ -1037,7 +1037,7 @@ int launch_halo(const void* A, const void* B, void* C, int M, int N, int lda, in
 int g_halo = 0;
 
 // reduction order of the implicit-GEMM convolutions (A/B knob plx_set_tap_inner): see ConvGeom::tap_inner
-int g_tap_inner = 0;
+int g_tap_inner = 1;
 
 // the 8-wave ring kernel (NBUF 3, 256 x 128 tiles) for convolutions with N % 128 == 0 (A/B knob plx_set_conv_v2)
 int g_conv_v2 = 0;

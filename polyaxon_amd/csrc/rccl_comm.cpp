@@ -17,6 +17,9 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <mutex>
+#include <unordered_set>
+
 #define PLX_API extern "C" __attribute__((visibility("default")))
 
 namespace {
@@ -46,6 +49,17 @@ struct Comm {
   int nranks, rank, device;
 };
 
+// Live communicators: every entry point validates its handle here, so a call on a destroyed (or never created)
+// communicator returns ncclInvalidArgument instead of dereferencing freed memory.
+std::mutex g_mu;
+std::unordered_set<Comm*> g_live;
+
+Comm* live(void* h) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Comm* c = static_cast<Comm*>(h);
+  return g_live.count(c) ? c : nullptr;
+}
+
 }  // namespace
 
 PLX_API int plx_rccl_unique_id(char* out) {
@@ -73,51 +87,77 @@ PLX_API void* plx_rccl_init(const char* id_bytes, int nranks, int rank, int devi
     return nullptr;
   }
   *err = 0;
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_live.insert(c);
   return c;
 }
 
 PLX_API int plx_rccl_all_reduce(void* h, const void* send, void* recv, int64_t count, int dtype, int op,
                                 hipStream_t stream) {
-  Comm* c = static_cast<Comm*>(h);
+  Comm* c = live(h);
+  if (!c) return (int)ncclInvalidArgument;
   return (int)ncclAllReduce(send, recv, (size_t)count, dtype_of(dtype), op_of(op), c->comm, stream);
 }
 
 PLX_API int plx_rccl_all_gather(void* h, const void* send, void* recv, int64_t count_per_rank, int dtype,
                                 hipStream_t stream) {
-  Comm* c = static_cast<Comm*>(h);
+  Comm* c = live(h);
+  if (!c) return (int)ncclInvalidArgument;
   return (int)ncclAllGather(send, recv, (size_t)count_per_rank, dtype_of(dtype), c->comm, stream);
 }
 
 PLX_API int plx_rccl_reduce_scatter(void* h, const void* send, void* recv, int64_t count_per_rank, int dtype, int op,
                                     hipStream_t stream) {
-  Comm* c = static_cast<Comm*>(h);
+  Comm* c = live(h);
+  if (!c) return (int)ncclInvalidArgument;
   return (int)ncclReduceScatter(send, recv, (size_t)count_per_rank, dtype_of(dtype), op_of(op), c->comm, stream);
 }
 
 PLX_API int plx_rccl_broadcast(void* h, const void* send, void* recv, int64_t count, int dtype, int root,
                                hipStream_t stream) {
-  Comm* c = static_cast<Comm*>(h);
+  Comm* c = live(h);
+  if (!c) return (int)ncclInvalidArgument;
   return (int)ncclBroadcast(send, recv, (size_t)count, dtype_of(dtype), root, c->comm, stream);
 }
 
 // All-reduce bandwidth probe on a device buffer of `bytes`: returns algbw and busbw (GB/s) like rccl-tests
-// (busbw = algbw * 2 (n-1) / n).
+// (busbw = algbw * 2 (n-1) / n).  Every collective's and HIP call's status is checked: a failing collective (or a
+// destroyed communicator) returns its error code and reports no bandwidth.
 PLX_API int plx_rccl_bus_bw(void* h, void* buf, int64_t bytes, int iters, hipStream_t stream, double* algbw,
                             double* busbw) {
-  Comm* c = static_cast<Comm*>(h);
+  *algbw = *busbw = 0.0;
+  Comm* c = live(h);
+  if (!c) return (int)ncclInvalidArgument;
+  if (bytes < 4 || iters < 1) return (int)ncclInvalidArgument;
   const size_t count = (size_t)bytes / 4;
-  for (int i = 0; i < 3; ++i) ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c->comm, stream);
+  for (int i = 0; i < 3; ++i) {
+    const ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c->comm, stream);
+    if (r != ncclSuccess) return (int)r;
+  }
   hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
-  hipEventRecord(a, stream);
-  for (int i = 0; i < iters; ++i) ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c->comm, stream);
-  hipEventRecord(b, stream);
-  hipEventSynchronize(b);
+  if (hipEventCreate(&a) != hipSuccess) return (int)ncclUnhandledCudaError;
+  if (hipEventCreate(&b) != hipSuccess) {
+    hipEventDestroy(a);
+    return (int)ncclUnhandledCudaError;
+  }
+  int rc = 0;
   float ms = 0.f;
-  hipEventElapsedTime(&ms, a, b);
+  if (hipEventRecord(a, stream) != hipSuccess) rc = (int)ncclUnhandledCudaError;
+  for (int i = 0; i < iters && rc == 0; ++i) {
+    const ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, c->comm, stream);
+    if (r != ncclSuccess) rc = (int)r;
+  }
+  if (rc == 0 && (hipEventRecord(b, stream) != hipSuccess || hipEventSynchronize(b) != hipSuccess ||
+                  hipEventElapsedTime(&ms, a, b) != hipSuccess))
+    rc = (int)ncclUnhandledCudaError;
+  if (rc == 0) {  // an asynchronous failure of the enqueued collectives surfaces here
+    ncclResult_t async = ncclSuccess;
+    if (ncclCommGetAsyncError(c->comm, &async) != ncclSuccess || async != ncclSuccess)
+      rc = (int)(async != ncclSuccess ? async : ncclInternalError);
+  }
   hipEventDestroy(a);
   hipEventDestroy(b);
+  if (rc) return rc;
   const double sec = ms / 1e3 / iters;
   *algbw = (double)bytes / sec / 1e9;
   *busbw = *algbw * 2.0 * (c->nranks - 1) / c->nranks;
@@ -125,8 +165,12 @@ PLX_API int plx_rccl_bus_bw(void* h, void* buf, int64_t bytes, int iters, hipStr
 }
 
 PLX_API int plx_rccl_destroy(void* h) {
-  Comm* c = static_cast<Comm*>(h);
-  if (!c) return 0;
+  Comm* c = live(h);
+  if (!c) return h ? (int)ncclInvalidArgument : 0;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_live.erase(c);
+  }
   ncclResult_t r = ncclCommDestroy(c->comm);
   delete c;
   return (int)r;

@@ -57,7 +57,7 @@ SUBJECTS = {
     "repo": ["created", "new_commit", "downloaded"],
     "cluster": ["created", "updated", "resources_updated", "node_created", "node_updated", "node_deleted",
                 "node_gpu", "node_gpu_unhealthy", "event"],
-    "resident_executor": ["started", "stopped", "lost"],
+    "resident_executor": ["started", "stopped", "lost", "yielded"],
     "user": ["registered", "updated", "activated", "deactivated", "deleted", "viewed", "password_changed",
              "logged_in", "logged_out", "sso_logged_in"],
     "superuser": ["role_granted", "role_revoked"],

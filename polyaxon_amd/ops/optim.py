@@ -146,6 +146,17 @@ class FusedAdamW:
         self.exp_avg.zero_()
         self.exp_avg_sq.zero_()
 
+    def shard_state(self, numel: int) -> None:
+        """ZeRO-1 (FlatDDP(shard_optimizer=True)): keep the moments only for the ``numel`` flat elements this rank
+        updates, packed; every update then names its range's offset in that packed state (``step_range_(state_off=)``).
+        The full-size moments are released."""
+        dev = self.flat.device
+        self.exp_avg = torch.zeros(numel, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(numel, dtype=torch.float32, device=dev)
+        self.sharded = True
+
+    sharded = False
+
     # set by FlatDDP(optimizer=...): the update runs per gradient bucket during the backward (step_range_), and
     # step_() only closes the step's bookkeeping
     in_backward = False
@@ -155,6 +166,8 @@ class FusedAdamW:
         f.grads_consumed()  # every kernel below zeroes the gradients it reads
         if self.in_backward:
             return  # every bucket was already updated (FlatDDP.finish joined the optimizer stream)
+        if self.sharded:
+            raise RuntimeError("sharded AdamW state is updated per bucket by FlatDDP; step_() alone would skip it")
         if not f.params.is_cuda:
             self._step_reference()
             return
@@ -179,18 +192,20 @@ class FusedAdamW:
                 self.exp_avg_sq.data_ptr() + off, f.numel - nd, 0, self.hp.data_ptr(), self.step.data_ptr(), st),
                 "plx_adamw_flat")
 
-    def step_range_(self, lo: int, hi: int, stream: Optional[int] = None) -> None:
+    def step_range_(self, lo: int, hi: int, stream: Optional[int] = None, state_off: Optional[int] = None) -> None:
         """AdamW over flat elements [lo, hi) on ``stream`` (a FlatDDP bucket: 4-aligned, and in lp mode entirely
         inside the bf16 decay segment or entirely inside the fp32 tail).  The same per-element update as
-        :meth:`step_`; weight decay applies to the elements below ``n_decay``; the range's gradients are zeroed."""
+        :meth:`step_`; weight decay applies to the elements below ``n_decay``; the range's gradients are zeroed.
+        ``state_off``: where the range's moments start in the packed (sharded) state; default ``lo``."""
         f = self.flat
+        so = lo if state_off is None else state_off
         if not f.params.is_cuda:
-            self._step_reference(lo, hi)
+            self._step_reference_range(lo, hi, so)
             return
         lib = _native.lib("plx_train")
         st = stream if stream is not None else _stream_ptr(f.params)
         nd, n = f.n_decay, hi - lo
-        p, m, v = f.params.data_ptr() + 4 * lo, self.exp_avg.data_ptr() + 4 * lo, self.exp_avg_sq.data_ptr() + 4 * lo
+        p, m, v = f.params.data_ptr() + 4 * lo, self.exp_avg.data_ptr() + 4 * so, self.exp_avg_sq.data_ptr() + 4 * so
         if f.lp_params is None:
             rc = lib.plx_adamw_flat(p, f.grads.data_ptr() + 4 * lo, m, v, n, max(0, min(hi, nd) - lo),
                                     self.hp.data_ptr(), self.step.data_ptr(), st)
@@ -225,7 +240,7 @@ class FusedAdamW:
         f.sync_lp()
 
     @torch.no_grad()
-    def _step_reference_range(self, lo: int, hi: int) -> None:
+    def _step_reference_range(self, lo: int, hi: int, so: Optional[int] = None) -> None:
         """The reference update restricted to [lo, hi) (CPU).  It runs inside the backward (FlatDDP optimizer mode),
         so it writes through ``.data``: the parameters are views of the flat buffers and share their autograd version
         counter, which an in-place op on any slice would bump under the tensors other layers saved for backward (the
@@ -233,8 +248,9 @@ class FusedAdamW:
         f = self.flat
         lr, b1, b2, eps, wd = (float(self.hp[i]) for i in range(5))
         t = int(self.step.item()) + 1
+        so = lo if so is None else so
         g = f.grad_view(lo, hi).data
-        p, m, v = f.params.data[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi]
+        p, m, v = f.params.data[lo:hi], self.exp_avg[so:so + hi - lo], self.exp_avg_sq[so:so + hi - lo]
         nd = max(0, min(hi, f.n_decay) - lo)
         if nd:
             p[:nd].mul_(1.0 - lr * wd)

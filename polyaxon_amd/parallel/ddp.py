@@ -14,8 +14,7 @@ WORLD_SIZE and call NCCL themselves.  This module is what a polyflow DP trial us
   all-reduce moves half the bytes; buckets never straddle the bf16 / fp32-tail boundary.  Direct-gradient
   ops (ops/lm.py, ops/rmsnorm.py: GEMM-written weights, bias / norm sums written into the slots) return None and
   are still counted by autograd's post-accumulate hook, which runs once per parameter per backward after every
-  Function feeding it; each segment counts its bucket down once per step.  (Optimizer-state sharding / ZeRO-1 is
-  not implemented: an 8B model's fp32 master + moments are 96 GB, which one 288 GB MI355X holds unsharded.)
+  Function feeding it; each segment counts its bucket down once per step.
 * optimizer in the backward (``optimizer=``, a FusedAdamW): the moment a bucket's gradient is complete (and, with
   DP, its all-reduce is done) the AdamW update of that bucket runs on a side stream, overlapped with the rest of
   the backward instead of one HBM-bound pass over every parameter after it (~41 ms of a 227 ms Llama-3 8B step on
@@ -24,12 +23,22 @@ WORLD_SIZE and call NCCL themselves.  This module is what a polyflow DP trial us
   bucket counts down (its AccumulateGrad hook runs after every Function that reads the weight), and ``finish()``
   makes the main stream wait for the optimizer stream before the next forward reads the updated bf16 weights.
   Same per-element update as the monolithic step.
+* ZeRO-1 (``shard_optimizer=True``, with ``optimizer``): each bucket's gradient is reduce-scattered instead of
+  all-reduced -- rank r receives the averaged gradient of the r-th W-th of the bucket (in place, in its own slice of
+  the flat gradient buffer) --, AdamW updates only that slice (its moments live in a packed 1/W-size state), and the
+  updated weights are all-gathered back (the bf16 model copy in lp mode, the fp32 parameters otherwise) before the
+  next forward.  Reduce-scatter + all-gather move the bytes of one all-reduce; the update pass and the AdamW moments
+  shrink W-fold (Llama-3 8B at DP 8: 64 GB of moments -> 8 GB per rank, ~42 ms of update -> ~5 ms).  The last
+  ``numel % 4W`` elements of a bucket are all-reduced and updated identically on every rank.  In lp mode the fp32
+  master of the slices other ranks own goes stale (only the bf16 copy is gathered): ``gather_master()`` refreshes it
+  for a checkpoint.
 Backend ``"nccl"`` is RCCL on ROCm; ``"gloo"`` works for CPU tests.
 """
 from __future__ import annotations
 
 import datetime
 import os
+from contextlib import nullcontext as _nullcontext
 from typing import List, Optional
 
 import torch
@@ -98,11 +107,13 @@ class MetricReducer:
 
 class FlatDDP:
     def __init__(self, flat: FlatParams, process_group=None, bucket_mb: float = 64.0, overlap: bool = True,
-                 force_collectives: bool = False, optimizer=None):
+                 force_collectives: bool = False, optimizer=None, shard_optimizer: bool = False):
         """``force_collectives``: launch every bucket's all-reduce even at world 1 (hooks on), so a single-GPU
         test executes the real RCCL path and can count the launches (``launched``).  ``optimizer``: a FusedAdamW
         whose update then runs per bucket inside the backward (``step_range_``); its ``step_()`` only closes the
-        step."""
+        step.  ``shard_optimizer``: ZeRO-1 over the optimizer's state (see the module docstring)."""
+        if shard_optimizer and optimizer is None:
+            raise ValueError("shard_optimizer needs the optimizer that runs inside the backward")
         self.flat = flat
         self.opt = optimizer
         if optimizer is not None:
@@ -119,7 +130,9 @@ class FlatDDP:
             flat.enable_direct_grads(False)
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
         self.force = bool(force_collectives) and dist.is_initialized()
+        self.nccl = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
         self.overlap = (overlap and (self.world > 1 or self.force)) or optimizer is not None
         self.launched = 0
         self.avg_supported = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
@@ -140,6 +153,11 @@ class FlatDDP:
                 cur, size = [], 0
         if cur:
             self._close(cur)
+        self.zero = bool(shard_optimizer)
+        self.shards: List[tuple] = []           # ZeRO-1, per bucket: (slice length s, reduce-scattered length, state offset)
+        if self.zero:
+            self.shards, state = self.plan_shards(self.buckets, self.world)
+            optimizer.shard_state(state)
         self._pending = [0] * len(self.buckets)
         self._handles: List = []
         self._hooks = []
@@ -152,6 +170,17 @@ class FlatDDP:
                 p = flat.parameter(seg.name)
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(self.seg_bucket[seg.name], i)))
         self.reset()
+
+    @staticmethod
+    def plan_shards(buckets, world: int):
+        """ZeRO-1 layout: per bucket (slice length s, reduce-scattered length W s, offset of the rank's packed
+        state), and the packed state's total length: s + the bucket's sub-4W remainder per bucket."""
+        shards, off = [], 0
+        for lo, hi, _ in buckets:
+            main = ((hi - lo) // (4 * world)) * 4 * world
+            shards.append((main // world, main, off))
+            off += main // world + (hi - lo - main)
+        return shards, off
 
     def _close(self, segs) -> None:
         lo = min(s.offset for s in segs)
@@ -177,6 +206,9 @@ class FlatDDP:
         return hook
 
     def _launch(self, b: int) -> None:
+        if self.zero:
+            self._launch_sharded(b)
+            return
         lo, hi, _ = self.buckets[b]
         view = self.flat.grad_view(lo, hi)
         h, div = None, None
@@ -206,6 +238,73 @@ class FlatDDP:
             if div is not None:
                 div.div_(self.world)
             self.opt.step_range_(lo, hi, self._side.cuda_stream)
+
+    def _launch_sharded(self, b: int) -> None:
+        """ZeRO-1 bucket: reduce-scatter (+ all-reduce of the sub-4W remainder) -> AdamW on this rank's slice ->
+        all-gather of the updated weights.  GPU: the collectives run on RCCL's streams and the update on the optimizer
+        stream, each waiting for the previous one on the device (the host never blocks); CPU: synchronous."""
+        f, opt = self.flat, self.opt
+        lo, hi, _ = self.buckets[b]
+        s, main, so = self.shards[b]
+        r, w = self.rank, self.world
+        own_lo, own_hi, rem_lo = lo + r * s, lo + (r + 1) * s, lo + main
+        coll = self.world > 1 or self.force
+        lp = f.lp_params is not None and hi <= f.n_decay
+        gv = lambda a, z: f.grad_view(a, z).data  # noqa: E731  (no autograd version bumps inside the backward)
+        op = dist.ReduceOp.AVG if self.avg_supported else dist.ReduceOp.SUM
+        self.stepped += 1
+        cuda = self._side is not None
+        if cuda:
+            self._side.wait_stream(torch.cuda.current_stream(f.device))
+        ctx = torch.cuda.stream(self._side) if cuda else _nullcontext()
+        with ctx:
+            if coll:
+                self.launched += 1
+                if main:
+                    out, inp = gv(own_lo, own_hi), gv(lo, rem_lo)
+                    if self.nccl:  # in place: the output is this rank's slice of the input (NCCL's in-place form)
+                        dist.reduce_scatter_tensor(out, inp, op=op, group=self.pg, async_op=True).wait()
+                    else:
+                        tmp = torch.empty_like(out)
+                        dist.reduce_scatter_tensor(tmp, inp, op=op, group=self.pg)
+                        out.copy_(tmp)
+                    if not self.avg_supported:
+                        out.div_(w)
+                if rem_lo < hi:
+                    rv = gv(rem_lo, hi)
+                    dist.all_reduce(rv, op=op, group=self.pg, async_op=cuda).wait() if cuda else \
+                        dist.all_reduce(rv, op=op, group=self.pg)
+                    if not self.avg_supported:
+                        rv.div_(w)
+            st = self._side.cuda_stream if cuda else None
+            if main:
+                opt.step_range_(own_lo, own_hi, st, state_off=so)
+                # the other ranks' slices of the gradient are not read here: zero them for the next accumulation
+                if own_lo > lo:
+                    gv(lo, own_lo).zero_()
+                if rem_lo > own_hi:
+                    gv(own_hi, rem_lo).zero_()
+            if rem_lo < hi:
+                opt.step_range_(rem_lo, hi, st, state_off=so + s)
+            if coll and main:
+                buf = f.lp_params.data if lp else f.params.data
+                full, mine = buf[lo:rem_lo], buf[own_lo:own_hi]
+                if self.nccl:  # in place: this rank's slice already sits at its place in the output
+                    self._handles.append((dist.all_gather_into_tensor(full, mine, group=self.pg, async_op=True), None))
+                else:
+                    dist.all_gather_into_tensor(full, mine.clone(), group=self.pg)
+
+    def gather_master(self) -> None:
+        """ZeRO-1 in lp mode: refresh the fp32 master of the slices other ranks own (all-gather per bucket), e.g.
+        before a checkpoint; the bf16 model weights are always current."""
+        if not self.zero or not (self.world > 1 or self.force):
+            return
+        f = self.flat
+        for (lo, hi, _), (s, main, _) in zip(self.buckets, self.shards):
+            if main and f.lp_params is not None and hi <= f.n_decay:
+                own = f.params.data[lo + self.rank * s: lo + (self.rank + 1) * s]
+                dist.all_gather_into_tensor(f.params.data[lo:lo + main], own if self.nccl else own.clone(),
+                                            group=self.pg)
 
     def finish(self) -> None:
         """Call after backward(): launches any bucket not fired by hooks, waits, averages (and, with an optimizer
@@ -238,3 +337,5 @@ class FlatDDP:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        if self.opt is not None:  # the optimizer steps on its own again (it silently skipped updates)
+            self.opt.in_backward = False

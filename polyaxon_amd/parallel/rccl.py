@@ -54,6 +54,8 @@ class RcclComm:
         return cls(obj[0], world, rank, torch.cuda.current_device())
 
     def _check(self, rc: int, what: str) -> None:
+        if not self.h:
+            raise RcclError(f"{what}: communicator is closed")
         if rc != 0:
             raise RcclError(f"{what}: {self.lib.plx_rccl_error(rc).decode()}")
 

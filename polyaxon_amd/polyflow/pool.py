@@ -10,7 +10,10 @@ The pool lives on the polyflow thread.  It
   greedy: every new bracket goes to the least-loaded executor the group may use);
 * turns worker messages into calls on the owning group driver (reader thread per worker -> ``flow.post``), and
   a lost worker (process died, socket closed) into failed trials and released devices;
-* shuts idle spawned workers down after ``idle_s`` so their GPUs return to process-mode runs.
+* shuts idle spawned workers down after ``idle_s`` so their GPUs return to process-mode runs -- at once when a
+  multi-device run (a DP gang) waits for devices the idle executors hold, and spawns none into a gang's
+  reservation (the reference counts concurrency against the cluster's capacity the same way for every run,
+  polyaxon/db/models/experiment_groups.py:193-197; warm executors must not starve a DP=8 job).
 """
 from __future__ import annotations
 
@@ -96,6 +99,11 @@ class ResidentPool:
     def _spawn(self, key, program, params, gpu, hbm_gb, max_active) -> Optional[WorkerHandle]:
         wid = self._next
         owner = f"resident:{wid}"
+        reserve = self.flow._gang_reservation()
+        if reserve is not None:  # a gang holds a reservation: a new executor must leave its devices free
+            need = 1 if gpu >= 1.0 - 1e-9 else 0
+            if len(self.flow.alloc.free_whole()) - need < reserve[1]:
+                return None
         try:
             a = self.flow.alloc.allocate(owner, gpu, hbm_gb)
         except ValueError as e:
@@ -321,6 +329,31 @@ class ResidentPool:
                 driver.on_bracket_lost(h, key, reason)
             except Exception:
                 log.exception("bracket loss handler failed")
+
+    def yield_to_gangs(self) -> int:
+        """A multi-device run waits for devices: shut down idle spawned executors (no brackets) until it would fit,
+        if releasing them is enough to place it.  Returns the number of executors asked to exit."""
+        g = self.flow.waiting_gang()
+        if g is None:
+            return 0
+        _, whole = g
+        free = len(self.flow.alloc.free_whole())
+        if free >= whole:
+            return 0
+        idle = [w for w in sorted(self.workers.values(), key=lambda h: h.wid)
+                if w.alive and not w.external and not w.brackets and not w.closing]
+        if free + sum(len(w.devices) for w in idle) < whole:
+            return 0  # not enough even with every idle executor gone: keep them warm for now
+        n = 0
+        for w in idle:
+            if free >= whole:
+                break
+            self.shutdown(w.wid)
+            free += len(w.devices)
+            n += 1
+            self.flow.auditor.record("resident_executor.yielded", "executor", w.wid, devices=w.devices,
+                                     gang=g[0])
+        return n
 
     # ------------------------------------------------------------------ idle reaping
     def _arm_reaper(self) -> None:

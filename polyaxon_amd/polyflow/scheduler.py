@@ -651,6 +651,23 @@ class Polyflow:
         finally:
             still.extend(self.pending)
             self.pending = still
+        if self.pending and self._pool is not None:
+            self._pool.yield_to_gangs()
+
+    def waiting_gang(self) -> Optional[Tuple[str, int]]:
+        """(owner, whole devices) of the oldest pending multi-device run, however long it has waited: idle resident
+        executors are released for it at once (polyflow/pool.py ``yield_to_gangs``)."""
+        for owner in self.pending:
+            run = self.runs.get(owner)
+            if run is None or run.final_status is not None:
+                continue
+            try:
+                whole = sum(int(round(g)) for _, _, g in self._requirements(run) if g >= 1.0 - 1e-9)
+            except Exception:
+                continue
+            if whole > 1:
+                return owner, whole
+        return None
 
     def _gang_reservation(self) -> Optional[Tuple[str, int]]:
         """(owner, devices) of the gang that holds a reservation, if one has waited long enough."""

@@ -184,6 +184,9 @@ def train_lm(argv=None) -> float:
                     help="model computes from fp32 weights under autocast (default on GPU: bf16 weights/grads with "
                          "an fp32 master copy in the optimizer)")
     ap.add_argument("--fixed_batch", action="store_true", help="reuse one synthetic batch every step")
+    ap.add_argument("--zero1", action="store_true",
+                    help="ZeRO-1: reduce-scatter each gradient bucket, AdamW on this rank's 1/W slice inside the "
+                         "backward, all-gather the bf16 weights (parallel/ddp.py); also PLX_ZERO1=1")
     args = _parse(ap, argv)
     backend = "gloo" if args.cpu or not torch.cuda.is_available() else "nccl"
     info = init_from_env(backend)
@@ -207,8 +210,9 @@ def train_lm(argv=None) -> float:
     # (parallel/ddp.py).  Off by default: bitwise the same trajectory, but on one MI355X the HBM-bound update only
     # moved time from itself to the backward's memory-bound kernels (Llama-3 8B 18.17k vs 18.03k tokens/s with a
     # full-chip grid, slower with a capped one; profiles/r3_negative_results.md)
-    in_bwd = dev.type == "cuda" and os.environ.get("PLX_OPT_IN_BACKWARD", "0") == "1"
-    ddp = FlatDDP(flat, bucket_mb=args.bucket_mb, optimizer=opt if in_bwd else None)
+    zero1 = args.zero1 or os.environ.get("PLX_ZERO1", "0") == "1"
+    in_bwd = zero1 or (dev.type == "cuda" and os.environ.get("PLX_OPT_IN_BACKWARD", "0") == "1")
+    ddp = FlatDDP(flat, bucket_mb=args.bucket_mb, optimizer=opt if in_bwd else None, shard_optimizer=zero1)
     ddp.broadcast_params()
     metrics = MetricReducer(dev)  # cross-rank mean of the logged loss (RCCL communicator on the GPU)
     g = torch.Generator(device=dev).manual_seed(args.seed + 1000 * info["rank"])

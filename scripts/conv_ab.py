@@ -7,6 +7,9 @@ rule 24).  The first run of every variant is checked against an fp32 ``F.conv2d`
 TFLOP/s of each variant.
 
     python scripts/conv_ab.py [variants=base,tap_inner] [rounds=7] [passes=fwd,dgrad] [shapes=all|s1|s2]
+
+CONV_AB_DATA=relu (default: the input is post-ReLU, half zeros, as in training -- the chip holds a higher clock on
+such data, cdna_hip_programming.md §5.4 rule 25) or randn.
 """
 import json
 import os
@@ -26,6 +29,7 @@ S1 = [(256, 64, 64, 56, 1), (256, 128, 128, 28, 1), (256, 256, 256, 14, 1), (256
 S2 = [(256, 128, 128, 56, 2), (256, 256, 256, 28, 2), (256, 512, 512, 14, 2)]
 
 VARIANTS = {
+    "r3": {},  # the round-3 kernels (libplx_conv_r3ref.so, built from git history into _native/ when present)
     "base": {"plx_set_tap_inner": 0, "plx_set_conv_v2": 0},
     "tap_inner": {"plx_set_tap_inner": 1, "plx_set_conv_v2": 0},
     "v2": {"plx_set_tap_inner": 0, "plx_set_conv_v2": 1},
@@ -45,10 +49,21 @@ def main():
     shapes = (S1 if which in ("all", "s1") else []) + (S2 if which in ("all", "s2") else [])
     dev = torch.device("cuda", 0)
     lib = _native.lib("plx_conv")
+    libs = {v: lib for v in variants}
+    if "r3" in variants:
+        import ctypes
+
+        r3 = ctypes.CDLL(str(_native.OUT / "libplx_conv_r3ref.so"))
+        _native._declare("plx_conv", r3)
+        libs["r3"] = r3
+    relu = os.environ.get("CONV_AB_DATA", "relu") == "relu"  # post-ReLU activations, as in training
     st = torch.cuda.current_stream().cuda_stream
     zero = _zero_page(dev).data_ptr()
 
+    cur = {"lib": lib}
+
     def apply(v):
+        cur["lib"] = libs[v]
         for fn, val in VARIANTS[v].items():
             if hasattr(lib, fn):
                 getattr(lib, fn)(val)
@@ -56,7 +71,8 @@ def main():
     torch.manual_seed(0)
     for n, ci, co, h, s in shapes:
         ho = (h + 2 - 3) // s + 1
-        x = torch.randn(n, h, h, ci, device=dev).to(torch.bfloat16)
+        x = torch.randn(n, h, h, ci, device=dev)
+        x = (x.clamp_min(0) if relu else x).to(torch.bfloat16)
         w = torch.randn(co, ci, 3, 3, device=dev) * (1.0 / (9 * ci) ** 0.5)
         wf, wd = weight_prep_k(w)
         y = torch.empty(n, ho, ho, co, device=dev, dtype=torch.bfloat16)
@@ -71,6 +87,7 @@ def main():
                 0, 2, 3, 1)
 
         def run(p):
+            lib = cur["lib"]
             if p == "fwd":
                 rc = lib.plx_conv_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), n, h, h, ci, co, 3, s, zero, None, st)
             else:

@@ -55,3 +55,21 @@ def test_killed_worker_fails_the_dp_experiment(tmp_path):
         assert flow.call(lambda: dict(flow.alloc.allocations)) == {}
     finally:
         flow.shutdown()
+
+
+def test_dp2_lm_trainer_zero1_through_polyflow(tmp_path):
+    """The same DP=2 job with ``--zero1`` (reduce-scatter, AdamW on each rank's half, all-gather): it succeeds and
+    lands the same final loss as the all-reduce run (ZeRO-1 is bitwise the unsharded trajectory)."""
+    flow = _flow(tmp_path)
+    try:
+        losses = {}
+        for zero in (False, True):
+            spec = _spec(6)
+            if zero:
+                spec["run"]["cmd"] += " --zero1"
+            r = flow.submit(spec, project="dist")
+            assert flow.wait("experiment", r["id"], timeout=240) == "succeeded", flow.logs("experiment", r["id"])[-3000:]
+            losses[zero] = flow.store.get_experiment(r["id"])["last_metric"]["loss"]
+        assert losses[True] == losses[False]
+    finally:
+        flow.shutdown()

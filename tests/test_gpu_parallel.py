@@ -44,8 +44,24 @@ def test_rccl_comm_single_rank_collectives():
         mx = comm.all_reduce(torch.tensor([5.0], device="cuda"), op="max")
         torch.cuda.synchronize()
         alg, bus = comm.bus_bandwidth(64 << 20, iters=5)
+        raw = comm.h
         comm.close()
-        print(json.dumps({"sum_ok": bool(torch.equal(x, torch.arange(1024, dtype=torch.float32, device="cuda"))),
+        import ctypes
+        from polyaxon_amd.parallel.rccl import RcclError
+        try:  # the Python face refuses a closed communicator
+            comm.bus_bandwidth(1 << 20, iters=1)
+            closed_raises = False
+        except RcclError:
+            closed_raises = True
+        # the C++ probe itself refuses the destroyed handle (live-communicator registry), reporting no bandwidth
+        buf = torch.ones(1 << 18, device="cuda")
+        a2, b2 = ctypes.c_double(-1), ctypes.c_double(-1)
+        rc_dead = comm.lib.plx_rccl_bus_bw(raw, buf.data_ptr(), buf.numel() * 4, 1,
+                                           torch.cuda.current_stream().cuda_stream, ctypes.byref(a2), ctypes.byref(b2))
+        print(json.dumps({"closed_raises": closed_raises, "rc_dead": rc_dead, "alg_dead": a2.value,
+                          "ar_dead": comm.lib.plx_rccl_all_reduce(raw, buf.data_ptr(), buf.data_ptr(), 4, 0, 0,
+                                                                  torch.cuda.current_stream().cuda_stream),
+                          "sum_ok": bool(torch.equal(x, torch.arange(1024, dtype=torch.float32, device="cuda"))),
                           "gather": g.shape[0], "gather_ok": bool((g == 3).all()), "rs": rs.numel(),
                           "rs_ok": bool((rs == 1).all()), "bcast_ok": bool((b.float() == 7).all()),
                           "max": float(mx[0]), "algbw": alg, "busbw": bus,
@@ -54,6 +70,7 @@ def test_rccl_comm_single_rank_collectives():
     assert res["sum_ok"] and res["gather"] == 1 and res["gather_ok"] and res["rs"] == 16 and res["rs_ok"]
     assert res["bcast_ok"] and res["max"] == 5.0 and res["loaded"]
     assert res["algbw"] > 0
+    assert res["closed_raises"] and res["rc_dead"] != 0 and res["alg_dead"] == 0.0 and res["ar_dead"] != 0
 
 
 def test_flat_ddp_on_rccl_backend_world1():
@@ -99,3 +116,54 @@ def test_flat_ddp_on_rccl_backend_world1():
     assert res["backend"] == "nccl" and res["buckets"] > 1 and res["launched"] == res["buckets"]
     assert res["norm"] > 0 and res["err"] < 1e-5
     assert res["rccl"] and res["loaded"] and abs(res["loss_mean"] - res["loss"]) < 1e-6
+
+
+def test_zero1_on_rccl_backend_world1_matches_unsharded():
+    """ZeRO-1 at world 1 with force_collectives on the nccl (RCCL) backend: every bucket runs the in-place
+    reduce-scatter, the AdamW update of its slice on the optimizer stream and the in-place all-gather of the bf16
+    weights, and three steps of the tiny Llama in lp mode (bf16 weights, direct GEMM gradients) follow the unsharded
+    in-backward trajectory bitwise."""
+    res = _run("""
+        import json, torch
+        import torch.distributed as dist
+        from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+        from polyaxon_amd.ops.flat import FlatParams
+        from polyaxon_amd.ops.optim import FusedAdamW
+        from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
+        import os
+        os.environ["WORLD_SIZE"] = "1"
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        info = init_from_env("nccl")
+        out = {}
+        for zero in (False, True):
+            torch.manual_seed(0)
+            m = Transformer(tiny_llama()).cuda()
+            flat = FlatParams(m, info["device"], channels_last=False, lp_dtype=torch.bfloat16)
+            flat.enable_direct_grads(True)
+            opt = FusedAdamW(flat, lr=1e-2, weight_decay=0.1)
+            ddp = FlatDDP(flat, bucket_mb=0.01, force_collectives=True, optimizer=opt, shard_optimizer=zero)
+            gen = torch.Generator(device="cuda").manual_seed(5)
+            losses = []
+            for _ in range(3):
+                tok = torch.randint(0, 256, (4, 16), device="cuda", generator=gen)
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = lm_loss(m(tok), tok)
+                loss.backward()
+                ddp.finish()
+                opt.step_()
+                opt.step += 1
+                losses.append(float(loss))
+            ddp.gather_master()
+            torch.cuda.synchronize()
+            out[zero] = (losses, flat.params.clone(), flat.lp_params.clone(), ddp.launched, len(ddp.buckets),
+                         opt.exp_avg.numel(), flat.numel)
+            ddp.remove_hooks()
+        a, b = out[False], out[True]
+        print(json.dumps({"losses_equal": a[0] == b[0], "master_equal": bool(torch.equal(a[1], b[1])),
+                          "lp_equal": bool(torch.equal(a[2], b[2])), "launched": b[3], "buckets": b[4],
+                          "state": b[5], "numel": b[6], "losses": b[0]}))
+        dist.destroy_process_group()
+    """)
+    assert res["losses_equal"] and res["master_equal"] and res["lp_equal"], res
+    assert res["buckets"] > 1 and res["launched"] == 3 * res["buckets"]
+    assert res["state"] == res["numel"]  # world 1: the slice is the whole bucket

@@ -363,3 +363,96 @@ def test_optimizer_in_backward_gloo_world2():
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
     assert all(r[1] and r[2] and r[3] for r in res), res
+
+
+def _zero_worker(rank, world, port, q, lp):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.ops.optim import FusedAdamW
+    from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
+
+    init_from_env("gloo")
+    out = {}
+    for zero in (False, True):
+        torch.manual_seed(0)
+        model = Transformer(tiny_llama())
+        flat = FlatParams(model, "cpu", channels_last=False, lp_dtype=lp)
+        opt = FusedAdamW(flat, lr=1e-2, weight_decay=0.1)
+        ddp = FlatDDP(flat, bucket_mb=0.01, optimizer=opt, shard_optimizer=zero)
+        ddp.broadcast_params()
+        gen = torch.Generator().manual_seed(100 + rank)  # different data per rank
+        losses = []
+        for _ in range(3):
+            tok = torch.randint(0, 256, (4, 16), generator=gen)
+            loss = lm_loss(model(tok), torch.randint(0, 256, (4, 16), generator=gen))
+            loss.backward()
+            ddp.finish()
+            opt.step_()
+            opt.step += 1
+            losses.append(float(loss))
+        lp_copy = flat.lp_params.clone() if lp is not None else None
+        ddp.gather_master()
+        grads_zero = float(flat.grads.abs().max()) == 0.0 and (lp is None or float(flat.lp_grads.abs().max()) == 0.0)
+        out[zero] = (losses, flat.params.clone(), lp_copy, opt.exp_avg.numel(), flat.numel, grads_zero,
+                     ddp.launched, len(ddp.buckets))
+        ddp.remove_hooks()
+    (la, pa, lpa, na, numel, za, _, _), (lb, pb, lpb, nb, _, zb, launched, nbuck) = out[False], out[True]
+    res = {"rank": rank, "losses_equal": la == lb, "master_equal": bool(torch.equal(pa, pb)),
+           "lp_equal": lpa is None or bool(torch.equal(lpa, lpb)), "state_full": na, "state_sharded": nb,
+           "numel": numel, "grads_zero": za and zb, "launched": launched, "buckets": nbuck,
+           "max_diff": float((pa - pb).abs().max())}
+    gathered = [torch.zeros_like(pb) for _ in range(world)]
+    dist.all_gather(gathered, pb)
+    res["ranks_equal"] = all(torch.equal(gathered[0], x) for x in gathered)
+    q.put(res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,lp", [(2, None), (2, torch.bfloat16), (4, None), (4, torch.bfloat16)])
+def test_zero1_sharded_adamw_matches_unsharded(world, lp):
+    """ZeRO-1 (FlatDDP(shard_optimizer=True)): reduce-scatter -> AdamW on this rank's 1/W of each bucket ->
+    all-gather of the updated weights follows the unsharded (all-reduce, every rank updates everything) trajectory
+    bitwise -- losses, fp32 master (after gather_master), bf16 model copy -- with the ranks identical, the gradients
+    left zeroed, and the AdamW moments W times smaller (up to the all-reduced sub-4W remainders)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_zero_worker, args=(r, world, port, q, lp)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for r in res:
+        assert r["losses_equal"] and r["master_equal"] and r["lp_equal"] and r["ranks_equal"], r
+        assert r["grads_zero"] and r["launched"] == 3 * r["buckets"], r
+        assert r["state_full"] == r["numel"]
+        # each bucket keeps at most 4W - 1 replicated remainder elements beside its 1/W slice
+        assert r["state_sharded"] <= r["numel"] / world + (4 * world) * r["buckets"], r
+        assert r["state_sharded"] < 0.75 * r["numel"], r
+
+
+def test_zero1_llama3_8b_state_shrinks_by_world_size():
+    """The Llama-3 8B flat layout (built on the meta device: no memory) under ZeRO-1 with 64 MB buckets: every
+    rank's packed AdamW state is numel / W exactly at W = 2, 4, 8 (the buckets divide evenly), i.e. the 64 GB of fp32
+    moments become 8 GB per rank at DP 8; a shard never straddles a bucket."""
+    from polyaxon_amd.models.transformer import Transformer, llama3_8b
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.parallel.ddp import FlatDDP
+
+    with torch.device("meta"):
+        model = Transformer(llama3_8b())
+    flat = FlatParams(model, torch.device("meta"), channels_last=False, lp_dtype=torch.bfloat16)
+    ddp = FlatDDP(flat, bucket_mb=64)
+    assert flat.numel > 8.0e9
+    for w in (2, 4, 8):
+        shards, state = FlatDDP.plan_shards(ddp.buckets, w)
+        assert state <= flat.numel / w + 4 * w * len(ddp.buckets)
+        assert 2 * state * 4 / 2 ** 30 <= 64 / w * 1.001 * (flat.numel * 8 / 2 ** 30) / 64  # moments bytes / W
+        for (lo, hi, _), (s, main, off) in zip(ddp.buckets, shards):
+            assert main == s * w and main <= hi - lo and s % 4 == 0

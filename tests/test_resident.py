@@ -540,3 +540,37 @@ def test_bench_cpu_under_torchrun_like_the_driver():
     assert res["n_gpus"] == 2 and res["steps"] == 1 and res["warmup"] == 0
     assert res["trials"] == 46 and res["trials_succeeded"] == 46 and res["store_fsm_history_ok"] is True
     assert res["value"] > 0 and res["higher_is_better"] is True and res["scaling"] == "weak"
+
+
+def test_idle_resident_executors_yield_to_a_waiting_gang(tmp_path, monkeypatch):
+    """A DP=8 experiment submitted while a resident Hyperband group holds executors on 2 of 8 (virtual) devices waits
+    for devices; the moment the group's last bracket ends, its idle executors are released (not after the 300 s idle
+    timeout) and the gang starts within a reconcile tick (reference: concurrency is counted against the cluster for
+    every run, polyaxon/db/models/experiment_groups.py:193-197)."""
+    from polyaxon_amd.polyflow.scheduler import Polyflow
+
+    monkeypatch.setenv("PLX_NUM_GPUS", "8")
+    monkeypatch.setenv("PLX_CPU_ONLY", "1")
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    gang = {"version": 1, "kind": "experiment", "run": {"cmd": f"{sys.executable} -c \"print('dp8 up')\""},
+            "environment": {"pytorch": {"n_workers": 7}, "resources": {"gpu": 1}}}
+    with Polyflow(str(tmp_path), reconcile_s=1.0) as flow:
+        g = flow.submit(_group(concurrency=2))
+        end = time.time() + 120
+        while time.time() < end and not any(x["status"] == "running" for x in flow.store.list_experiments(group_id=g["id"])):
+            time.sleep(0.05)
+        # the executors hold 2 devices: a DP=8 gang cannot start yet, and waits behind them
+        x = flow.submit(gang, project="dp")
+        time.sleep(0.5)
+        assert flow.store.get_experiment(x["id"])["status"] == "created"
+        assert flow.wait("group", g["id"], timeout=300) == "succeeded"
+        t_group = time.time()
+        assert flow.wait("experiment", x["id"], timeout=60) == "succeeded", flow.logs("experiment", x["id"])[-2000:]
+        st = {s["status"]: s["created_at"] for s in flow.store.experiment_statuses(x["id"])}
+        started = st.get("scheduled") or st.get("starting")
+        assert started is not None and started - t_group < 10.0, (started, t_group)
+        jobs = flow.store.experiment_jobs(x["id"])
+        assert len(jobs) == 8 and sorted(d for j in jobs for d in j["devices"]) == list(range(8))
+        acts = [a["event_type"] for a in flow.store.activity_logs(limit=500)] if hasattr(flow.store, "activity_logs") \
+            else []
+        assert not acts or "resident_executor.yielded" in acts
