@@ -235,13 +235,23 @@ class ControlServer:
                    default=None)
         # per sweep: its best metric and when that sweep first reached the target (the calibration of --target:
         # a target near the task's floor is reached by a minority of sweeps, so the time to it spans several)
+        # training steps each trial ran (its metric rows' last step: resumed trials train only the increment)
+        trial_steps = {int(r["experiment_id"]): int(r["s"] or 0) for r in st.execute(
+            f"SELECT m.experiment_id, MAX(m.step) AS s FROM experiment_metrics m JOIN experiments e "
+            f"ON e.id = m.experiment_id WHERE e.group_id IN ({q}) GROUP BY m.experiment_id", gids).fetchall()}
         per_sweep = []
         for g in gids:
             gx = [x for x in xs if x["group_id"] == g and (x.get("last_metric") or {}).get("loss") is not None]
             b = min((x["last_metric"]["loss"] for x in gx), default=None)
             h = [x["finished_at"] for x in gx if x["last_metric"]["loss"] <= target]
+            hit = min(h) if h else None
+            # the sweep's own training up to (and including) the trial that first reached the target: a time to
+            # target that does not depend on how many sweeps share the GPU (they are submitted together)
+            to_hit = sum(trial_steps.get(x["id"], 0) for x in gx if hit is not None and x["finished_at"] <= hit)
             per_sweep.append({"group": g, "best": round(b, 4) if b is not None else None,
-                              "hit_s": round(min(h) - t0_wall, 2) if h else None})
+                              "hit_s": round(hit - t0_wall, 2) if hit is not None else None,
+                              "steps_to_hit": to_hit if hit is not None else None,
+                              "steps": sum(trial_steps.get(x["id"], 0) for x in gx)})
         # per training budget (resource units): trials and their best / median metric -- what each rung bought
         by_units: dict = {}
         for x in xs:
@@ -294,6 +304,13 @@ def _spawn_control(argv):
 
 
 # ----------------------------------------------------------------------------- launcher (no GPU calls here)
+def _median(v):
+    v = sorted(v)
+    if not v:
+        return None
+    return v[len(v) // 2] if len(v) % 2 else round((v[len(v) // 2 - 1] + v[len(v) // 2]) / 2, 3)
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -513,6 +530,17 @@ def main() -> int:
             "best_loss": round(res["best"], 4) if res["best"] is not None else None,
             "sweeps_reaching_target": sum(1 for p in res["per_sweep"] if p["hit_s"] is not None),
             "sweep_best_loss": [p["best"] for p in res["per_sweep"]],
+            # time to target as a distribution over the timed sweeps: wall seconds from the timed region's start
+            # (sweeps share the GPU, so these grow with the number submitted together) and the sweep's own training
+            # up to its first hit converted at the measured step rate (comparable across search strategies)
+            "sweep_hit_s": [p["hit_s"] for p in res["per_sweep"]],
+            "target_hit_fraction": round(sum(1 for p in res["per_sweep"] if p["hit_s"] is not None)
+                                         / max(1, len(res["per_sweep"])), 3),
+            "median_time_to_target_s": _median([p["hit_s"] for p in res["per_sweep"] if p["hit_s"] is not None]),
+            "median_train_s_to_target": _median([round(p["steps_to_hit"] * elapsed_max / max(1, res["train_steps"])
+                                                       * world, 3)
+                                                 for p in res["per_sweep"] if p["steps_to_hit"] is not None]),
+            "sweep_steps_to_target": [p["steps_to_hit"] for p in res["per_sweep"]],
             "loss_by_units": res["per_units"],
             "store_fsm_history_ok": res["fsm_ok"],
             "path": "polyflow scheduler (own process) + SQLite store + resident executors (same path as plx run)",

@@ -192,6 +192,9 @@ class ResidentWorker:
     """The GPU side.  Owns one TrialProgram; runs the brackets (and ASHA shards) it is handed, in rounds."""
 
     def __init__(self, program: str, params: Optional[Dict[str, Any]] = None, device=None, max_active: int = 8):
+        # ASHA jobs per shard per round (A/B knob PLX_ASHA_JOBS): each round ends in one device->host read of the
+        # round's results; one job per shard per round made that read a quarter of an ASHA sweep's wall time
+        self.asha_jobs = max(1, int(os.environ.get("PLX_ASHA_JOBS", "4")))
         self.program_name = program
         self.params = dict(params or {})
         self.device = device
@@ -495,14 +498,23 @@ class ResidentWorker:
                 if br.resume and more:
                     ex.snapshot((br.key, cid))
                 records.append((row, br, slot, cid, steps, t_start, self._event()))
-        # ---- ASHA shards: one job each, decided from the previous round's device rankings
+        # ---- ASHA shards: up to asha_jobs jobs each, decided from the previous round's device rankings (next_job marks
+        # a promotion as taken when it hands it out, so a round never runs one twice; a shard is finished only when
+        # its first job of a round finds nothing runnable -- later ones may wait for this round's results)
         asha_records = []
         finished = []
+        jobs = []
         for sh in shards:
+            for j in range(self.asha_jobs):
+                job = None if (sh.stopped or sh.early_stopped) else sh.next_job()
+                if job is None:
+                    if j == 0:
+                        finished.append(sh)
+                    break
+                jobs.append((sh, job))
+        for sh, job in jobs:
             self._poll_control(chan)
-            job = None if (sh.stopped or sh.early_stopped) else sh.next_job()
-            if job is None:
-                finished.append(sh)
+            if sh.stopped:
                 continue
             cid, rung = job
             col = sorted(sh.configs).index(cid)
