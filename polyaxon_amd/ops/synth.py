@@ -79,3 +79,55 @@ class SyntheticImages:
     @property
     def chance_loss(self) -> float:
         return math.log(self.classes)
+
+
+class SyntheticTokens:
+    """Synthetic, learnable token batches for the language-model trial programs, a fresh batch every step.
+
+    Each sequence is a random ``period``-token phrase repeated to ``seq`` tokens: the first period is noise (loss
+    ln V per token) and every later token is predictable by copying from ``period`` positions back, so the loss
+    floor is about ``period / seq * ln V`` and reaching it needs the model to learn induction -- hyper-parameter
+    sensitive (learning rate, warm-up, weight decay), unlike uniform random tokens whose loss never leaves ln V.
+    The phrases come from a counter-based integer hash of (seed, step counter, position) computed with plain tensor
+    ops on the device: graph-capturable (the counter is device data, bumped in place), identical on CPU and GPU.
+    ``y`` is ``x`` (next-token targets are the shifted tokens, ``models.transformer.lm_loss``)."""
+
+    M32 = 0xFFFFFFFF
+
+    def __init__(self, batch: int, seq: int, vocab: int, device, period: int = 64, seed: int = 0):
+        if seq % period:
+            raise ValueError("seq must be a multiple of period")
+        self.device = torch.device(device)
+        self.batch, self.seq, self.vocab, self.period, self.seed = batch, seq, vocab, period, int(seed)
+        self.x = torch.zeros(batch, seq, dtype=torch.int64, device=self.device)
+        self.y = self.x
+        self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._idx = torch.arange(batch * period, dtype=torch.int64, device=self.device)
+        self._h = torch.empty_like(self._idx)
+        self._t = torch.empty_like(self._idx)
+
+    def next(self) -> None:
+        """Refill ``x`` in place with the next batch of the stream (and advance the device counter)."""
+        m, h, t = self.M32, self._h, self._t
+        torch.mul(self._idx, 0x9E3779B1, out=h)
+        h.add_(self.counter * 0x85EBCA77 + (self.seed * 0xC2B2AE3D) % (1 << 32))
+        h.bitwise_and_(m)
+        for mult in (0x7FEB352D, 0x846CA68B):  # lowbias32 finaliser
+            torch.bitwise_right_shift(h, 16, out=t)
+            h.bitwise_xor_(t)
+            h.mul_(mult).bitwise_and_(m)
+        torch.bitwise_right_shift(h, 15, out=t)
+        h.bitwise_xor_(t)
+        h.remainder_(self.vocab)
+        self.x.view(self.batch, self.seq // self.period, self.period).copy_(
+            h.view(self.batch, 1, self.period).expand(self.batch, self.seq // self.period, self.period))
+        self.counter.add_(1)
+
+    @property
+    def floor_loss(self) -> float:
+        """Expected loss of a perfect copier: only the first period (minus its first token) is unpredictable."""
+        return (self.period - 1) / (self.seq - 1) * math.log(self.vocab)
+
+    @property
+    def chance_loss(self) -> float:
+        return math.log(self.vocab)

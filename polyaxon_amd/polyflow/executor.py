@@ -52,13 +52,17 @@ class ResidentTrialExecutor:
     def __init__(self, model: nn.Module, batch: Tuple[torch.Tensor, torch.Tensor], device,
                  loss_fn: Optional[Callable] = None, optimizer: str = "sgd", use_graph: bool = True,
                  amp_dtype: Optional[torch.dtype] = torch.bfloat16, channels_last: bool = True,
-                 ring_size: int = 4096, init_spec: Optional[Callable] = None):
+                 ring_size: int = 4096, init_spec: Optional[Callable] = None,
+                 lp_dtype: Optional[torch.dtype] = None):
+        """``lp_dtype`` (the language models, GPU): the model computes from bf16 weights with bf16 gradients and the
+        optimizer keeps the fp32 master (ops/flat.py lp mode); every re-init / restore refreshes the bf16 copy."""
         self.device = torch.device(device)
         self.is_cuda = self.device.type == "cuda"
         if channels_last:
             model = model.to(memory_format=torch.channels_last)
         self.model = model
-        self.flat = FlatParams(model, self.device, channels_last=channels_last)
+        self.flat = FlatParams(model, self.device, channels_last=channels_last,
+                               lp_dtype=lp_dtype if self.is_cuda else None)
         self.flat.enable_direct_grads(True)  # native ops accumulate weight grads straight into flat.grads
         self._flatten_buffers()
         self.step = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -243,9 +247,16 @@ class ResidentTrialExecutor:
             elif self._init_spec is not None:
                 self.flat.init_reference(self._init_spec, seed)
             self.opt.reset_state()
-            self.flat.grads.zero_()
+            self._zero_grads()
+            self.flat.sync_lp()
             self.buffers.copy_(self._buffer_init)
             self.step.zero_()
+
+    def _zero_grads(self) -> None:
+        self.flat.grads.zero_()
+        if self.flat.lp_grads is not None:
+            self.flat.lp_grads.zero_()
+        self.flat.grads_consumed()
 
     def set_hparams(self, **hp) -> None:
         self.opt.set_hparams(**{k: v for k, v in hp.items() if k in self.opt.HP})
@@ -300,7 +311,8 @@ class ResidentTrialExecutor:
             v.copy_(st.opt[k], non_blocking=True)
         self.buffers.copy_(st.buffers, non_blocking=True)
         self.step.copy_(st.step, non_blocking=True)
-        self.flat.grads.zero_()
+        self._zero_grads()
+        self.flat.sync_lp()
 
     def drop(self, key) -> None:
         self.snapshots.pop(key, None)

@@ -386,6 +386,9 @@ class ResidentDriver(GroupDriver):
     def make_units(self) -> None:
         raise NotImplementedError
 
+    def unit_done(self, key: str, br: Dict[str, Any]) -> None:
+        """A unit ended (any status); drivers whose next units depend on results add them here."""
+
     def _new_unit(self, key: str, iteration: int, configs: List[Dict[str, Any]], units: float) -> None:
         self.brackets[key] = {"iteration": iteration, "configs": configs, "status": None, "wid": None, "xids": {},
                               "root": {}, "open": set(), "units": units, "retries": 0, "last_rung": None,
@@ -471,6 +474,7 @@ class ResidentDriver(GroupDriver):
             self._close_open(br, "failed" if msg.get("status") == "failed" else "stopped",
                              f"bracket {msg.get('status')}")
             br["status"] = msg.get("status") or "succeeded"
+            self.unit_done(msg.get("key"), br)  # may add units (the next BO batch) before the finish check
             self._dispatch()
             self._check_finished()
         elif ev == "error":
@@ -694,16 +698,99 @@ class ResidentAshaDriver(ResidentDriver):
         return max((h[0] for h in br["history"]), default=0)
 
 
+class ResidentBODriver(ResidentDriver):
+    """Bayesian optimisation on resident executors (BASELINE.json config 4: BO over GPT-2 hyper-parameters).  The
+    reference runs one BO iteration at a time, every suggestion a pod, and fits the GP after the whole iteration
+    (polyaxon/hpsearch/tasks/bo.py:7-70, search_managers/bayesian_optimization/manager.py:17-33).  Here every
+    suggestion is a ``trials`` unit of ``executor.params.trial_units`` resource units (default 25) that the pool
+    places on a warm executor -- weights re-initialised in place, AdamW hyper-parameters as device data, no process
+    start -- and after the initial random batch each iteration asks the GP for ``max(bo.n_suggestions,
+    concurrency)`` points (constant-liar batch), so every executor the group may use has a trial.  One iteration
+    row per BO iteration, as in process mode (``BODriver``)."""
+
+    OP = "trials"
+
+    def make_units(self) -> None:
+        from polyaxon_amd.polytune.bo import BOIterationConfig
+
+        self.BOIterationConfig = BOIterationConfig
+        self.iteration = 0
+        self.trial_units = float(self.ex.params.get("trial_units", 25))
+        self.old_configs: List = []
+        self.old_metrics: List = []
+        self.batch: List[str] = []
+        self._launch(self.manager.get_suggestions(None) or [])
+
+    def _launch(self, suggestions: List[Dict[str, Any]]) -> None:
+        self.batch = []
+        for i, params in enumerate(suggestions):
+            key = f"{self.gid}.bo{self.iteration}.{i}"
+            self._new_unit(key, self.iteration, [{"cid": 0, "params": dict(params)}], self.trial_units)
+            self.batch.append(key)
+        self.iteration_id = self.store.create_iteration(self.gid, {"iteration": self.iteration,
+                                                                   "experiment_ids": [], "unit": self.OP})
+
+    @property
+    def metric_name(self) -> str:
+        return self.hp.bo.metric.name
+
+    @property
+    def resume_enabled(self) -> bool:
+        return False
+
+    def unit_message(self, key, br):
+        early = [{"metric": r.metric, "value": r.value, "optimization": r.optimization}
+                 for r in self.hp.early_stopping]
+        return {"op": self.OP, "key": key, "configs": br["configs"], "units": self.trial_units,
+                "metric": self.metric_name, "maximize": Optimization.maximize(self.hp.bo.metric.optimization),
+                "seed": int(self.hp.seed or 0) + 7919 * self.gid + 104729 * br["iteration"] +
+                int(key.rsplit(".", 1)[1]), "early_stopping": early}
+
+    def _rung_done(self, br, msg) -> None:  # one BO iteration row per batch (unit_done), not one per trial
+        br["last_rung"] = int(msg["rung"])
+        if msg.get("early_stop") and not self.stopped:
+            self.flow.auditor.record("experiment_group.stopped", "experiment_group", self.gid, reason="early_stopping")
+            self.stop(pending_only=not self.stop_running_on_early_stop, message="Early stopping")
+
+    def unit_done(self, key: str, br: Dict[str, Any]) -> None:
+        if key not in self.batch or any(self.brackets[k]["status"] is None for k in self.batch):
+            return
+        ids = []
+        for k in self.batch:
+            b = self.brackets[k]
+            xid = b["xids"].get((0, 0))
+            if xid is None:
+                continue
+            ids.append(xid)
+            v = self.metric_of(xid, self.metric_name)
+            if v is not None:
+                self.old_configs.append((xid, dict(b["configs"][0]["params"])))
+                self.old_metrics.append((xid, v))
+        self.store.update_iteration(self.iteration_id, {
+            "iteration": self.iteration, "experiment_ids": ids, "unit": self.OP,
+            "experiments_metrics": [list(m) for m in self.old_metrics if m[0] in ids]})
+        if self.stopped or not self.manager.should_reschedule(self.iteration) or not self.old_metrics:
+            self.batch = []
+            return
+        self.iteration += 1
+        cfg = self.BOIterationConfig(iteration=self.iteration, old_experiments_configs=list(self.old_configs),
+                                     old_experiments_metrics=list(self.old_metrics))
+        n = max(int(self.hp.bo.n_suggestions or 1), int(self.concurrency))
+        self._launch(self.manager.get_suggestions(cfg, n=n) or [])
+
+
 def make_group_driver(flow, gid: int, spec: GroupSpecification, project: Dict, user: str, cwd: str) -> GroupDriver:
     algo = spec.search_algorithm
     ex = spec.environment.executor if spec.environment is not None else None
     if ex is not None and ex.resident:
         if algo == SearchAlgorithms.ASHA:
             return ResidentAshaDriver(flow, gid, spec, project, user, cwd)
+        if algo == SearchAlgorithms.BO:
+            return ResidentBODriver(flow, gid, spec, project, user, cwd)
         if algo != SearchAlgorithms.HYPERBAND:
             from polyaxon_amd.spec.specification import PolyaxonfileError
 
-            raise PolyaxonfileError(f"resident executors run hyperband and asha groups; {algo} groups use "
+            raise PolyaxonfileError(f"resident executors run hyperband, asha and bo groups; {algo} groups use "
                                     "executor: process")
         return ResidentHyperbandDriver(flow, gid, spec, project, user, cwd)
     cls = {SearchAlgorithms.GRID: GridRandomDriver, SearchAlgorithms.RANDOM: GridRandomDriver,

@@ -8,7 +8,7 @@ trials (hyper-parameters, random init seed, Hyperband resource) is device data t
 (polyaxon/scheduler/spawners/experiment_spawner.py:108-179); the program is what stays warm instead.
 
 Registry: ``resnet50`` (BASELINE.json config 3), ``resnet_tiny`` (same code path, CPU-test sized), ``mlp``
-(config 2).  ``module:callable`` names any user factory with the same signature ``(params, device) -> TrialProgram``.
+(config 2), ``gpt2`` (config 4's GPT-2 125M trial), ``gpt2_tiny`` (same code path, CPU-test sized).  ``module:callable`` names any user factory with the same signature ``(params, device) -> TrialProgram``.
 """
 from __future__ import annotations
 
@@ -84,7 +84,45 @@ def _mlp(params: Dict[str, Any], device) -> TrialProgram:
                               "images_per_step": bs})
 
 
+def _gpt2(params: Dict[str, Any], device, tiny: bool) -> TrialProgram:
+    """GPT-2 125M (BASELINE.json config 4's trial) on the synthetic copy-task token stream (ops/synth.py
+    SyntheticTokens): bf16 weights / gradients with an fp32 master and fused AdamW (the LM trainer's numerics),
+    every trial re-initialised in place (GPT-2 init via plx_init_flat), AdamW hyper-parameters as device data."""
+    from polyaxon_amd.models.transformer import Transformer, gpt2_125m, lm_loss
+    from polyaxon_amd.ops.synth import SyntheticTokens
+    from polyaxon_amd.polyflow.executor import ResidentTrialExecutor
+
+    dev = torch.device(device)
+    if tiny:
+        cfg = gpt2_125m(vocab_size=int(params.get("vocab", 256)), n_layers=2, d_model=64, n_heads=2, d_ff=256,
+                        max_seq_len=int(params.get("seq", 32)))
+    else:
+        cfg = gpt2_125m(vocab_size=int(params.get("vocab", 50257)))
+    batch = int(params.get("batch", 2 if tiny else 16))
+    seq = int(params.get("seq", 32 if tiny else 1024))
+    data = SyntheticTokens(batch, seq, cfg.vocab_size, dev, period=int(params.get("period", 8 if tiny else 64)),
+                           seed=int(params.get("data_seed", 0)))
+    if dev.type == "cuda":
+        with torch.device(dev):
+            model = Transformer(cfg)
+    else:
+        model = Transformer(cfg)
+    ex = ResidentTrialExecutor(model, data, dev, loss_fn=lm_loss, optimizer="adamw",
+                               use_graph=bool(params.get("graph", False)), channels_last=False,
+                               lp_dtype=torch.bfloat16)
+    return TrialProgram(ex, unit_steps=int(params.get("unit_steps", 4 if tiny else 10)),
+                        window=int(params.get("window", 4)),
+                        hp_keys=("lr", "beta1", "beta2", "eps", "weight_decay"),
+                        info={"model": "gpt2_tiny" if tiny else "gpt2_125m", "batch": batch, "seq": seq,
+                              "vocab": cfg.vocab_size, "data": "synthetic copy task, fresh per step (ops/synth.py)",
+                              "warm_hparams": {"lr": 3e-4, "beta1": 0.9, "beta2": 0.95, "eps": 1e-8,
+                                               "weight_decay": 0.1},
+                              "tokens_per_step": batch * seq, "floor_loss": data.floor_loss})
+
+
 PROGRAMS: Dict[str, Callable[[Dict[str, Any], Any], TrialProgram]] = {
+    "gpt2": lambda p, d: _gpt2(p, d, tiny=False),
+    "gpt2_tiny": lambda p, d: _gpt2(p, d, tiny=True),
     "resnet50": lambda p, d: _resnet(p, d, tiny=False),
     "resnet_tiny": lambda p, d: _resnet(p, d, tiny=True),
     "mlp": _mlp,

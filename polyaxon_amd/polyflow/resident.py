@@ -145,6 +145,31 @@ class _Bracket:
     early_stopped: bool = False
 
 
+class _FixedBudget:
+    """The manager of a ``trials`` unit (a BO batch, or any list of independent fixed-budget trials): one rung of
+    ``units`` resource units, no promotion -- the bracket machinery runs it like a one-rung bracket."""
+
+    def __init__(self, units: float):
+        self.units = units
+
+    def get_n_resources_for_iteration(self, iteration: int, rung: int) -> float:
+        return self.units
+
+    def get_n_config_to_keep_for_iteration(self, iteration: int, rung: int) -> int:
+        return 0
+
+    def should_reschedule(self, iteration: int, rung: int) -> bool:
+        return True
+
+
+class _Units:
+    """Resource declaration of a ``trials`` unit: whole units stay ints in the trial's declarations."""
+
+    @staticmethod
+    def cast_value(v: float):
+        return int(round(v)) if abs(v - round(v)) < 1e-9 else float(v)
+
+
 @dataclass
 class _AshaShard:
     """One asynchronous successive-halving search (Li et al. 2018, "Massively parallel hyperparameter tuning") over
@@ -273,6 +298,8 @@ class ResidentWorker:
             self.queue.append(self._make_bracket(msg))
         elif op == "asha":
             self.asha_queue.append(self._make_shard(msg))
+        elif op == "trials":
+            self.queue.append(self._make_trials(msg))
         elif op == "stop_bracket":
             for q in (self.queue, self.asha_queue):
                 for br in list(q):
@@ -322,6 +349,22 @@ class ResidentWorker:
         br.rung = int(msg.get("start_rung", 0))
         br.active = [int(c) for c in msg["active"]] if msg.get("active") is not None else sorted(configs)
         return br
+
+    def _make_trials(self, msg: Dict[str, Any]) -> _Bracket:
+        """``{"op": "trials", "key", "configs": [{cid, params}], "units", "maximize", "seed", "early_stopping"}``:
+        independent trials of ``units`` resource units each (a BO batch), run as a one-rung bracket."""
+        from polyaxon_amd.spec.hptuning import Optimization
+
+        if msg.get("metric", self.program.metric) != self.program.metric:
+            raise ValueError(f"metric {msg.get('metric')!r} is not what program {self.program_name} reports "
+                             f"({self.program.metric!r})")
+        rules = [(0, float(r["value"]), Optimization.maximize(r["optimization"]))
+                 for r in msg.get("early_stopping") or [] if r["metric"] == self.program.metric]
+        configs = {int(c["cid"]): dict(c["params"]) for c in msg["configs"]}
+        return _Bracket(key=msg["key"], manager=_FixedBudget(float(msg["units"])), iteration=0, configs=configs,
+                        resource_name=str(msg.get("resource", "units")), resource=_Units(),
+                        maximize=bool(msg.get("maximize", False)), resume=False, seed=int(msg.get("seed", 0)),
+                        rules=rules, active=sorted(configs))
 
     def _make_shard(self, msg: Dict[str, Any]) -> _AshaShard:
         from polyaxon_amd.spec.hptuning import HPTuningConfig, Optimization
@@ -375,7 +418,7 @@ class ResidentWorker:
                 except Exception as e:  # bad bracket message: report, keep serving
                     chan.send({"ev": "error", "fatal": False, "key": msg.get("key"), "message": repr(e),
                                "traceback": traceback.format_exc()})
-                    if msg.get("op") == "bracket":
+                    if msg.get("op") in ("bracket", "trials"):
                         chan.send({"ev": "bracket_done", "key": msg.get("key"), "status": "failed"})
                     r = None
                 if r is not None:
@@ -409,7 +452,7 @@ class ResidentWorker:
             except Exception as e:
                 chan.send({"ev": "error", "fatal": False, "key": msg.get("key"), "message": repr(e),
                            "traceback": traceback.format_exc()})
-                if msg.get("op") == "bracket":
+                if msg.get("op") in ("bracket", "trials"):
                     chan.send({"ev": "bracket_done", "key": msg.get("key"), "status": "failed"})
                 r = None
             if r is not None:

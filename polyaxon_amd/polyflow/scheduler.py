@@ -400,8 +400,8 @@ class Polyflow:
 
             ex = spec.environment.executor
             if ex is not None and ex.resident:
-                if spec.search_algorithm not in ("hyperband", "asha"):
-                    raise PolyaxonfileError(f"resident executors run hyperband and asha groups; "
+                if spec.search_algorithm not in ("hyperband", "asha", "bo"):
+                    raise PolyaxonfileError(f"resident executors run hyperband, asha and bo groups; "
                                             f"{spec.search_algorithm} groups use executor: process")
                 if spec.resources is not None and spec.resources.gpu is not None and spec.resources.gpu.value > 1:
                     raise PolyaxonfileError("a resident executor runs on one device (resources.gpu <= 1)")

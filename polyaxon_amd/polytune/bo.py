@@ -727,7 +727,9 @@ class BOSearchManager(BaseSearchAlgorithmManager):
         self.n_iterations = hptuning_config.bo.n_iterations
         self.backend = backend
 
-    def get_suggestions(self, iteration_config=None):
+    def get_suggestions(self, iteration_config=None, n: Optional[int] = None):
+        """``n``: batch size of a BO iteration (default ``bo.n_suggestions``; a resident group asks for enough to
+        fill its concurrency, constant liar)."""
         cfg = self.hptuning_config
         if not iteration_config:
             return get_random_suggestions(cfg.matrix, self.n_initial_trials, seed=cfg.seed)
@@ -739,7 +741,7 @@ class BOSearchManager(BaseSearchAlgorithmManager):
             metrics.append(metrics_by_id[key])
         opt = BOOptimizer(cfg, backend=self.backend)
         opt.add_observations(configs, metrics)
-        n = max(1, cfg.bo.n_suggestions)
+        n = max(1, int(n if n is not None else cfg.bo.n_suggestions))
         sugg = opt.get_suggestions(n) if n > 1 else [opt.get_suggestion()]
         sugg = [s for s in sugg if s]
         return sugg or None

@@ -447,7 +447,7 @@ def test_resident_spec_validation():
     assert specification_for(_group()).get_experiment_spec({"lr": 0.01, "momentum": 0.9, "units": 1}).run is None
 
 
-def test_resident_rejects_grid_random_bo(tmp_path, cpu_pool_env):
+def test_resident_rejects_grid_random(tmp_path, cpu_pool_env):
     from polyaxon_amd.polyflow.scheduler import Polyflow
     from polyaxon_amd.spec.specification import PolyaxonfileError
 
@@ -574,3 +574,47 @@ def test_idle_resident_executors_yield_to_a_waiting_gang(tmp_path, monkeypatch):
         acts = [a["event_type"] for a in flow.store.activity_logs(limit=500)] if hasattr(flow.store, "activity_logs") \
             else []
         assert not acts or "resident_executor.yielded" in acts
+
+
+def _bo_group(concurrency=2, n_initial=3, n_iterations=2, trial_units=3):
+    hp = {"seed": 5, "concurrency": concurrency,
+          "bo": {"n_initial_trials": n_initial, "n_iterations": n_iterations,
+                 "metric": {"name": "loss", "optimization": "minimize"},
+                 "utility_function": {"acquisition_function": "ucb", "kappa": 1.5,
+                                      "gaussian_process": {"kernel": "matern", "length_scale": 1.0, "nu": 1.5},
+                                      "n_warmup": 100, "n_iter": 3}},
+          "matrix": {"lr": {"loguniform": [-9, -3]}, "weight_decay": {"uniform": [0.0, 0.2]}}}
+    return {"version": 1, "kind": "group", "project": "rbo", "hptuning": hp,
+            "environment": {"resources": {"gpu": 1},
+                            "executor": {"kind": "resident", "program": "gpt2_tiny",
+                                         "params": {"batch": 2, "seq": 32, "unit_steps": 2,
+                                                    "trial_units": trial_units}}}}
+
+
+def test_polyflow_resident_bo_group_over_gpt2(tmp_path, cpu_pool_env):
+    """BO (BASELINE config 4) on resident GPT-2 executors: the initial random batch, then GP batches of
+    ``concurrency`` constant-liar suggestions, every trial an experiment with its FSM history and metric, one
+    iteration row per BO iteration with the metrics the GP was fitted on, both executors used."""
+    from polyaxon_amd.polyflow.scheduler import Polyflow
+
+    with Polyflow(str(tmp_path), reconcile_s=0) as flow:
+        r = flow.submit(_bo_group())
+        assert flow.wait("group", r["id"], timeout=300) == "succeeded"
+        st = flow.store
+        xs = st.list_experiments(group_id=r["id"])
+        assert len(xs) == 3 + 2 * 2  # n_initial + n_iterations x max(n_suggestions, concurrency)
+        for x in xs:
+            assert x["status"] == "succeeded"
+            assert [s["status"] for s in st.experiment_statuses(x["id"])] == [
+                "created", "scheduled", "starting", "running", "succeeded"]
+            assert x["declarations"]["units"] == 3 and "lr" in x["declarations"]
+            assert x["last_metric"]["loss"] > 0
+        its = sorted(st.iterations(r["id"]), key=lambda i: i["data"]["iteration"])
+        assert [i["data"]["iteration"] for i in its] == [0, 1, 2]
+        assert [len(i["data"]["experiment_ids"]) for i in its] == [3, 2, 2]
+        assert all(len(i["data"]["experiments_metrics"]) == len(i["data"]["experiment_ids"]) for i in its)
+        # GP suggestions after the random batch: new points, not repeats of the initial ones
+        first = {round(x["declarations"]["lr"], 12) for x in xs if x["id"] in its[0]["data"]["experiment_ids"]}
+        later = {round(x["declarations"]["lr"], 12) for x in xs if x["id"] in its[1]["data"]["experiment_ids"]}
+        assert not (first & later)
+        assert {tuple(j["devices"]) for x in xs for j in st.experiment_jobs(x["id"])} == {(0,), (1,)}
