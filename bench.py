@@ -47,6 +47,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 T0 = time.perf_counter()
 METRIC = "HPO trials/hour (whole node) + wall-clock-to-target, ResNet-50 Hyperband sweep"
+METRIC_BO = "HPO trials/hour (whole node) + best loss, GPT-2 125M Bayesian-GP search"
 MAX_ITER, ETA = 9, 3
 # ASHA's largest rung: the reference's Hyperband (r_i = r * eta^i, polytune/managers.py) trains its last bracket's
 # survivor 27 units at max_iter 9, so ASHA gets the same top budget to be comparable
@@ -59,6 +60,14 @@ def _args(argv=None):
     ap.add_argument("--steps", type=int, default=3, help="timed sweeps per GPU (hyperband: 3 brackets, 23 trials)")
     ap.add_argument("--warmup", type=int, default=1, help="untimed sweeps per GPU through the same path")
     ap.add_argument("--search", choices=("hyperband", "asha"), default="hyperband")
+    ap.add_argument("--config", choices=("resnet50_hb", "gpt2_bo"), default="resnet50_hb",
+                    help="gpt2_bo: BASELINE config 4 on one node -- a Bayesian-GP search over GPT-2 125M AdamW "
+                         "hyper-parameters on resident executors (each timed step = one BO group of "
+                         "--bo-initial + --bo-iterations x --bo-concurrency trials per GPU)")
+    ap.add_argument("--bo-initial", type=int, default=4)
+    ap.add_argument("--bo-iterations", type=int, default=3)
+    ap.add_argument("--bo-concurrency", type=int, default=4, help="trials per BO batch (constant liar) per GPU")
+    ap.add_argument("--trial-units", type=int, default=10, help="gpt2_bo: resource units (x --unit-steps) per trial")
     ap.add_argument("--asha-n", type=int, default=29,
                     help="configs per ASHA sweep (29 at min 1 / max 27 / eta 3 with resume ~ the 87 units of a "
                          "Hyperband sweep)")
@@ -81,12 +90,34 @@ def _args(argv=None):
 
 
 def program_params(args):
+    if args.config == "gpt2_bo":
+        if args.cpu:
+            return "gpt2_tiny", {"batch": 2, "seq": 32, "unit_steps": 1, "trial_units": 2, "data_seed": 1234}
+        return "gpt2", {"batch": 16, "seq": 1024, "unit_steps": args.unit_steps, "trial_units": args.trial_units,
+                        "graph": bool(args.graph), "data_seed": 1234}
     if args.cpu:
         return "resnet_tiny", {"batch": min(args.batch, 8), "image": min(args.image, 32),
                                "unit_steps": min(args.unit_steps, 1), "grid": 4, "signal": args.signal,
                                "active_classes": min(args.active_classes, 10), "data_seed": 1234}
     return "resnet50", {"batch": args.batch, "image": args.image, "unit_steps": args.unit_steps, "signal": args.signal,
                         "active_classes": args.active_classes, "graph": bool(args.graph), "data_seed": 1234}
+
+
+def bo_group_spec(seed: int, program: str, params: dict, args, world: int) -> dict:
+    """BASELINE config 4: GP-UCB over GPT-2's AdamW learning rate, weight decay and beta2."""
+    hp = {"seed": seed, "concurrency": args.bo_concurrency * world,
+          "matrix": {"lr": {"loguniform": [math.log(1e-4), math.log(3e-3)]},
+                     "weight_decay": {"uniform": [0.0, 0.2]},
+                     "beta2": {"uniform": [0.9, 0.999]}},
+          "bo": {"n_initial_trials": args.bo_initial * world, "n_iterations": args.bo_iterations,
+                 "metric": {"name": "loss", "optimization": "minimize"},
+                 "utility_function": {"acquisition_function": "ucb", "kappa": 1.5,
+                                      "gaussian_process": {"kernel": "matern", "length_scale": 1.0, "nu": 2.5},
+                                      "n_warmup": 10000, "n_iter": 8}}}
+    return {"version": 1, "kind": "group", "project": "bench_gpt2_bo", "hptuning": hp,
+            "environment": {"resources": {"gpu": 1},
+                            "executor": {"kind": "resident", "program": program, "params": params,
+                                         "max_active_brackets": args.max_active}}}
 
 
 def group_spec(seed: int, program: str, params: dict, concurrency: int, max_active: int, search: str = "hyperband",
@@ -161,9 +192,13 @@ class ControlServer:
 
     def _sweeps(self, n: int, seed0: int):
         gids = []
-        for i in range(n):
-            spec = group_spec(seed0 + i, self.program, self.params, self.world, self.args.max_active,
-                              self.args.search, self.args.asha_n)
+        n_groups = n // self.world if self.args.config == "gpt2_bo" else n  # one BO group spans every GPU
+        for i in range(n_groups):
+            if self.args.config == "gpt2_bo":
+                spec = bo_group_spec(seed0 + i, self.program, self.params, self.args, self.world)
+            else:
+                spec = group_spec(seed0 + i, self.program, self.params, self.world, self.args.max_active,
+                                  self.args.search, self.args.asha_n)
             gids.append(self.flow.submit(spec)["id"])
         for g in gids:
             st = self.flow.wait("group", g, timeout=7200, poll_s=0.05)
@@ -432,8 +467,15 @@ def main() -> int:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    early_comm = None
+    if dev.type == "cuda" and os.environ.get("PLX_BENCH_RCCL") == "early":
+        # diagnostic (profiles/r4_rccl_slowdown.md): a communicator alive for the whole run, as in a DP trial
+        from polyaxon_amd.parallel.rccl import RcclComm
+
+        early_comm = (RcclComm.from_torch_distributed() if world > 1
+                      else RcclComm(RcclComm.new_unique_id(), 1, 0, local))
     worker = ResidentWorker(program, params, device=dev, max_active=args.max_active)
-    log(f"building {program} executors (batch {params['batch']}, image {params['image']}, search {args.search})")
+    log(f"building {program} executors (batch {params['batch']}, image {params.get('image')}, config {args.config})")
     worker._ready_info = worker.build()
     log(f"executor ready in {worker._ready_info['build_s']} s")
     chan = Channel.connect(host, int(port), timeout=300)
@@ -461,8 +503,8 @@ def main() -> int:
             float(os.getpid())] + [worker.stats[k] - s0[k] for k in ("idle_s", "round_s", "sync_s")]
     # framework-owned collective (csrc/rccl_comm.cpp) for the per-rank gather on the GPU path, on a communicator
     # created only now (see the process-group note above).
-    comm = None
-    if dev.type == "cuda" and os.environ.get("PLX_BENCH_RCCL", "1") != "0":
+    comm = early_comm
+    if comm is None and dev.type == "cuda" and os.environ.get("PLX_BENCH_RCCL", "1") != "0":
         from polyaxon_amd.parallel.rccl import RcclComm
 
         try:
@@ -492,8 +534,13 @@ def main() -> int:
         search = (f"hyperband max_iter={MAX_ITER} eta={ETA} resume=true, 3 brackets / 23 trials per sweep"
                   if args.search == "hyperband" else
                   f"asha min_resource=1 max_resource={ASHA_MAX} eta={ETA} resume=true, {args.asha_n} configs per sweep")
+        gpt2 = args.config == "gpt2_bo"
+        if gpt2:
+            search = (f"bo (GP-UCB, matern 2.5) over lr / weight_decay / beta2: {args.bo_initial * world} random + "
+                      f"{args.bo_iterations} x {args.bo_concurrency * world} constant-liar suggestions per group, "
+                      f"{params['trial_units'] * params['unit_steps']} AdamW steps per trial")
         out = {
-            "metric": METRIC,
+            "metric": METRIC_BO if gpt2 else METRIC,
             "value": round(value, 2),
             "unit": "trials/hour",
             "n_gpus": world,
@@ -504,14 +551,17 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if dev.type == "cuda" else "fp32",
-            "data": "synthetic ImageNet-shape (224x224x3, 1000 classes), fresh learnable batch generated on the "
-                    "device every step (ops/synth.py); random-init weights",
+            "data": ("synthetic copy-task tokens (64-token phrases repeated to 1024, vocab 50257), fresh batch "
+                     "generated on the device every step (ops/synth.py SyntheticTokens); random-init weights" if gpt2
+                     else "synthetic ImageNet-shape (224x224x3, 1000 classes), fresh learnable batch generated on "
+                          "the device every step (ops/synth.py); random-init weights"),
             "config": {
-                "model": "resnet50" if dev.type == "cuda" else "resnet18ish (CPU rehearsal)",
+                "model": (("gpt2_125m" if dev.type == "cuda" else "gpt2 tiny (CPU rehearsal)") if gpt2 else
+                          ("resnet50" if dev.type == "cuda" else "resnet18ish (CPU rehearsal)")),
                 "global_batch": params["batch"] * world,
                 "per_trial_batch": params["batch"],
-                "seq_len": None,
-                "image_size": params["image"],
+                "seq_len": params.get("seq"),
+                "image_size": params.get("image"),
                 "parallelism": f"trial-parallel x{world} (resident executor per GPU, brackets balanced by polyflow)",
                 "search": search,
                 "unit_steps": params["unit_steps"],
@@ -519,7 +569,7 @@ def main() -> int:
                 "sweeps": res["groups"],
                 "brackets": res["brackets"],
                 "signal": args.signal,
-                "active_classes": params["active_classes"],
+                "active_classes": params.get("active_classes"),
             },
             "trials": res["trials"],
             "trials_succeeded": res["succeeded"],
