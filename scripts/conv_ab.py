@@ -54,7 +54,11 @@ def main():
         import ctypes
 
         r3 = ctypes.CDLL(str(_native.OUT / "libplx_conv_r3ref.so"))
-        _native._declare("plx_conv", r3)
+        for fn, argtypes in _native.SIGNATURES["plx_conv"].items():
+            if hasattr(r3, fn):
+                f = getattr(r3, fn)
+                f.argtypes = argtypes
+                f.restype = _native.RESTYPES.get(fn, ctypes.c_int)
         libs["r3"] = r3
     relu = os.environ.get("CONV_AB_DATA", "relu") == "relu"  # post-ReLU activations, as in training
     st = torch.cuda.current_stream().cuda_stream
@@ -65,8 +69,7 @@ def main():
     def apply(v):
         cur["lib"] = libs[v]
         for fn, val in VARIANTS[v].items():
-            if hasattr(lib, fn):
-                getattr(lib, fn)(val)
+            getattr(lib, fn)(val)
 
     torch.manual_seed(0)
     for n, ci, co, h, s in shapes:

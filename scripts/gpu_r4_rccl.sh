@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 4: why a live RCCL communicator slows the ResNet-50 bench (verdict r3 weak #3).  Alternating 3-sweep bench
+# runs with the communicator created before the warm-up (PLX_BENCH_RCCL=early) or after the timed region (default),
+# then with more HIP hardware queues, then a kernel trace of the early-communicator run.
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+AB_LIST="${AB_LIST:-PLX_BENCH_RCCL=early;;PLX_BENCH_RCCL=early GPU_MAX_HW_QUEUES=8;GPU_MAX_HW_QUEUES=8;PLX_BENCH_RCCL=early}" \
+  TAG=r4rccl bash scripts/gpu_ab_multi.sh || exit 1
+if [ "${PROF:-1}" = "1" ]; then
+  PLX_BENCH_RCCL=early PROF_TAG=r4rccl_early_resnet50_hb STEPS=2 bash scripts/prof_only.sh || exit 1
+  head -20 gpurun_out/r4rccl_early_resnet50_hb_steady_state.md
+fi

@@ -375,6 +375,7 @@ def _zero_worker(rank, world, port, q, lp):
     from polyaxon_amd.ops.optim import FusedAdamW
     from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
 
+    torch.set_num_threads(2)  # W ranks share the CPU with the rest of the suite
     init_from_env("gloo")
     out = {}
     for zero in (False, True):

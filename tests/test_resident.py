@@ -618,3 +618,32 @@ def test_polyflow_resident_bo_group_over_gpt2(tmp_path, cpu_pool_env):
         later = {round(x["declarations"]["lr"], 12) for x in xs if x["id"] in its[1]["data"]["experiment_ids"]}
         assert not (first & later)
         assert {tuple(j["devices"]) for x in xs for j in st.experiment_jobs(x["id"])} == {(0,), (1,)}
+
+
+def test_polyflow_resident_bo_group_on_a_dp2_gang(tmp_path, cpu_pool_env):
+    """BASELINE config 4's shape on CPU: a BO group whose trials are DP=2 (``resources.gpu: 2``) runs on ONE resident
+    executor spanning a 2-rank gang (gloo; polyflow wires the ranks): every trial trains data-parallel (FlatDDP), the
+    ranks follow rank 0's control stream and decide from the cross-rank mean metric, each trial is an experiment with
+    its FSM history whose job holds both devices, and the gang stays warm for the whole group."""
+    from polyaxon_amd.polyflow.scheduler import Polyflow
+
+    g = _bo_group(concurrency=1, n_initial=2, n_iterations=2)
+    g["environment"]["resources"] = {"gpu": 2}
+    with Polyflow(str(tmp_path), reconcile_s=0) as flow:
+        r = flow.submit(g)
+        assert flow.wait("group", r["id"], timeout=300) == "succeeded", flow.store.get_group(r["id"])
+        st = flow.store
+        xs = st.list_experiments(group_id=r["id"])
+        assert len(xs) == 2 + 2 * 1
+        for x in xs:
+            assert [s["status"] for s in st.experiment_statuses(x["id"])] == [
+                "created", "scheduled", "starting", "running", "succeeded"]
+            jobs = st.experiment_jobs(x["id"])
+            assert len(jobs) == 1 and sorted(jobs[0]["devices"]) == [0, 1]
+            assert x["last_metric"]["loss"] > 0
+        pool = flow.call(lambda: flow.resident_pool().snapshot())
+        assert len(pool) == 1 and sorted(pool[0]["devices"]) == [0, 1]
+        wid = pool[0]["wid"]
+        info = flow.call(lambda: dict(flow.resident_pool().workers[wid].info))
+        assert info.get("dp_world") == 2
+    assert flow.alloc.allocations == {}
