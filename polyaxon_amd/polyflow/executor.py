@@ -108,6 +108,18 @@ class ResidentTrialExecutor:
             self.wcache = cache if len(cache) else None
         self.model.train()
 
+    def enable_dp(self, bucket_mb: float = 64.0) -> None:
+        """Data parallel over the default process group (a resident DP gang, polyflow/resident.py): bucketed,
+        backward-overlapped gradient all-reduce (parallel/ddp.py FlatDDP) before every optimizer step; the DP step
+        runs eagerly."""
+        from polyaxon_amd.parallel.ddp import FlatDDP
+
+        self.ddp = FlatDDP(self.flat, bucket_mb=bucket_mb)
+        self.use_graph = False
+        self._prefetch = False
+
+    ddp = None
+
     # ------------------------------------------------------------------ buffers (BN running stats)
     def _flatten_buffers(self) -> None:
         bufs = [(n, b) for n, b in self.model.named_buffers() if b.dtype == torch.float32]
@@ -158,6 +170,8 @@ class ResidentTrialExecutor:
             if self.wcache is not None:
                 self.wcache.deactivate()
         side_stream.join(self.device)  # weight-gradient GEMMs overlapped on the side stream (ops/side_stream.py)
+        if self.ddp is not None:
+            self.ddp.finish()  # the gang's averaged gradients
         if prefetch:
             # queued after the join: the main stream does not wait for it before the optimizer
             side = side_stream.stream_for(self.device)

@@ -367,8 +367,8 @@ class ResidentDriver(GroupDriver):
         res = self.spec.environment.resources
         g = res.gpu.value if (res is not None and res.gpu is not None) else 1.0
         self.gpu = g if g > 0 else 1.0
-        if self.gpu > 1:
-            raise ValueError("a resident executor runs on one device (resources.gpu <= 1)")
+        if self.gpu > 1 and abs(self.gpu - round(self.gpu)) > 1e-9:
+            raise ValueError("a resident DP gang takes whole devices (resources.gpu <= 1 or an integer)")
         self.hbm = res.hbm_gb if res is not None else 0.0
         self.brackets: Dict[str, Dict[str, Any]] = {}
         self.pending_keys: List[str] = []

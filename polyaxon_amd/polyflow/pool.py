@@ -52,6 +52,7 @@ class WorkerHandle:
     assigned_units: float = 0.0                              # cumulative training units / units of work assigned
     assigned_count: int = 0
     waiters: Dict[str, Callable[[Dict[str, Any]], None]] = field(default_factory=dict)
+    peers: List[Any] = field(default_factory=list)             # DP gang: (Popen, Channel) of ranks 1..N-1
 
     @property
     def owner(self) -> str:
@@ -101,7 +102,7 @@ class ResidentPool:
         owner = f"resident:{wid}"
         reserve = self.flow._gang_reservation()
         if reserve is not None:  # a gang holds a reservation: a new executor must leave its devices free
-            need = 1 if gpu >= 1.0 - 1e-9 else 0
+            need = int(round(gpu)) if gpu >= 1.0 - 1e-9 else 0
             if len(self.flow.alloc.free_whole()) - need < reserve[1]:
                 return None
         try:
@@ -118,6 +119,9 @@ class ResidentPool:
                 self.placement_error = f"no healthy device with {hbm_gb} GB of HBM"
             return None
         self._next += 1
+        world = len(a.devices) if gpu > 1.0 + 1e-9 else 1
+        if world > 1:
+            return self._spawn_gang(wid, owner, a, key, program, params, max_active)
         parent, child = socket.socketpair()
         env = dict(os.environ)
         env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in a.devices)
@@ -159,6 +163,92 @@ class ResidentPool:
         self._arm_reaper()
         self.flow.auditor.record("resident_executor.started", "executor", wid, devices=a.devices, program=program)
         return h
+
+    def _worker_env(self, devices: List[int]) -> Dict[str, str]:
+        env = dict(os.environ)
+        env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devices)
+        env.pop("ROCR_VISIBLE_DEVICES", None)
+        env["PYTHONUNBUFFERED"] = "1"
+        env.pop("PLX_HBM_GB", None)
+        env.pop("PLX_HBM_FRACTION", None)
+        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = pkg_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        return env
+
+    def _spawn_gang(self, wid, owner, a, key, program, params, max_active) -> Optional[WorkerHandle]:
+        """A resident executor spanning a DP gang (``resources.gpu: N``): one worker process per device, ranks wired
+        with the torch.distributed env contract (MASTER_ADDR / MASTER_PORT / rank / world, as polyflow/env.py gives a
+        process-mode PyTorch job); rank 0's channel is the executor's, the others only carry the init handshake."""
+        world = len(a.devices)
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        log_dir = os.path.join(self.flow.paths.root, "executors")
+        os.makedirs(log_dir, exist_ok=True)
+        ranks = []
+        argv = [self.flow.python, "-m", "polyaxon_amd.polyflow.resident", "--fd"]
+        cpu = self.flow.alloc.n_devices and os.environ.get("PLX_CPU_ONLY") == "1"
+        try:
+            for r, dev in enumerate(a.devices):
+                parent, child = socket.socketpair()
+                env = self._worker_env([dev])
+                env.update(PLX_RESIDENT_RANK=str(r), PLX_RESIDENT_WORLD=str(world), MASTER_ADDR="127.0.0.1",
+                           MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0")
+                path = os.path.join(log_dir, f"worker{wid}.rank{r}.log")
+                with open(path, "ab") as logf:
+                    proc = subprocess.Popen(argv + [str(child.fileno())] + (["--cpu"] if cpu else []), env=env,
+                                            pass_fds=(child.fileno(),), stdout=logf, stderr=subprocess.STDOUT,
+                                            stdin=subprocess.DEVNULL, start_new_session=True)
+                child.close()
+                ranks.append((proc, Channel(parent), path))
+        except OSError as e:
+            for proc, ch, _ in ranks:
+                ch.close()
+                try:
+                    os.killpg(proc.pid, 9)
+                except OSError:
+                    pass
+            self.flow.alloc.release(owner)
+            log.error("cannot start resident DP gang: %s", e)
+            self.flow.store.add_cluster_event("resident_executor", "error", f"gang spawn failed: {e}")
+            return None
+        if getattr(self.flow, "numa_bind", False):
+            for (proc, _, _), dev in zip(ranks, a.devices):
+                self.flow._bind_cpus(proc.pid, [dev])
+        proc0, chan0, path0 = ranks[0]
+        h = WorkerHandle(wid, key, program, dict(params), list(a.devices), chan0, proc=proc0)
+        h.info["log_path"] = path0
+        h.peers = [(proc, ch) for proc, ch, _ in ranks[1:]]
+        self.workers[wid] = h
+        init = {"op": "init", "program": program, "params": params, "max_active": max_active}
+        for _, ch, _ in ranks:
+            ch.send(init)
+        self._start_reader(h)
+        for proc, ch in h.peers:
+            self._start_peer_reader(h, proc, ch)
+        self._arm_reaper()
+        self.flow.auditor.record("resident_executor.started", "executor", wid, devices=a.devices, program=program,
+                                 dp_world=world)
+        return h
+
+    def _start_peer_reader(self, h: WorkerHandle, proc, chan: Channel) -> None:
+        """A gang's rank > 0: its only messages are the ready handshake or a fatal error; its exit loses the gang."""
+        def reader():
+            while True:
+                try:
+                    msg = chan.recv()
+                except (ChannelClosed, OSError, ValueError):
+                    break
+                if msg is not None and msg.get("ev") == "error" and msg.get("fatal"):
+                    self.flow.post(self._lost, h, f"gang rank failed: {msg.get('message')}")
+            try:
+                proc.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                proc.kill()
+            self.flow.post(self._lost, h, f"gang rank exited ({proc.returncode})")
+
+        threading.Thread(target=reader, name=f"resident-peer-{h.wid}", daemon=True).start()
 
     def attach(self, chan: Channel, device: int, program: str, params: Optional[Dict[str, Any]] = None,
                max_active: int = 8, gpu: float = 1.0) -> WorkerHandle:
@@ -312,10 +402,16 @@ class ResidentPool:
             h.chan.close()
         except Exception:
             pass
-        if h.proc is not None and h.proc.poll() is None:
+        for proc in [h.proc] + [p for p, _ in h.peers]:
+            if proc is not None and proc.poll() is None:
+                try:
+                    os.killpg(proc.pid, 9)
+                except OSError:
+                    pass
+        for _, ch in h.peers:
             try:
-                os.killpg(h.proc.pid, 9)
-            except OSError:
+                ch.close()
+            except Exception:
                 pass
         lost = dict(h.brackets)
         h.brackets.clear()

@@ -240,6 +240,18 @@ class ResidentWorker:
         self._base_ev = None
         self._base_wall = 0.0
         self._shutdown: Optional[str] = None
+        self.gang: Optional[_GangGroup] = None
+
+    def join_gang(self, rank: int, world: int) -> None:
+        """Become rank ``rank`` of a DP gang (before ``build``): the program trains with FlatDDP over the gang,
+        each rank on its own slice of the data stream."""
+        import torch
+
+        if self.device is None:
+            self.device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+        if torch.device(self.device).type == "cuda":
+            torch.cuda.set_device(self.device)
+        self.gang = _GangGroup(rank, world, self.device)
 
     # ------------------------------------------------------------------ build
     def build(self) -> Dict[str, Any]:
@@ -255,12 +267,19 @@ class ResidentWorker:
             self.device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
         if torch.device(self.device).type == "cuda":
             apply_hbm_budget(self.device)
-        self.program = build_program(self.program_name, self.params, self.device)
+        params = dict(self.params)
+        if self.gang is not None:  # each rank draws its own batches of the same task
+            params["data_seed"] = int(params.get("data_seed", 0)) + 1000003 * self.gang.rank
+            params["graph"] = False  # the DP step runs eagerly (its collectives ride RCCL's own streams)
+        self.program = build_program(self.program_name, params, self.device)
+        if self.gang is not None:
+            self.program.executor.enable_dp()
         self.program.warm()
         ex = self.program.executor
         self.metrics = BracketMetrics(self.max_active, 32, ex.device)
         self._reset_clock()
         return {"ev": "ready", "program": self.program_name, "device": str(ex.device), "pid": os.getpid(),
+                "dp_world": self.gang.world if self.gang is not None else 1,
                 "build_s": round(time.time() - t0, 3), "snapshot_bytes": ex.snapshot_bytes(),
                 "metric": self.program.metric, "unit_steps": self.program.unit_steps, "info": self.program.info,
                 "hip_graph": ex.graph is not None, "graph_check_error": ex.graph_check_error,
@@ -584,6 +603,11 @@ class ResidentWorker:
             asha_records.append((sh, rung, cid, col, steps, t_start, self._event()))
         # ---- the round's decision: one top-k launch per optimisation direction over every active bracket
         n = len(brs)
+        if self.gang is not None:  # DP gang: every rank decides from the cross-rank mean of the round's metrics
+            if n:
+                self.gang.mean_(self.metrics.values[:n])
+            if self.asha_metrics is not None and asha_records:
+                self.gang.mean_(self.asha_metrics.values)
         orders = {}
         if n:
             vals_dev = self.metrics.values[:n]
@@ -696,6 +720,86 @@ class ResidentWorker:
         chan.send({"ev": "bracket_done", "key": sh.key, "status": status})
 
 
+class _GangGroup:
+    """A DP gang of resident workers (``environment.resources.gpu: N`` with a resident executor): one process per
+    device, ranks from the pool's env (PLX_RESIDENT_RANK / _WORLD, MASTER_ADDR / MASTER_PORT).  Gradients go over the
+    data process group (``nccl`` = RCCL on the GPU, gloo on CPU); the control stream -- the scheduler messages rank 0
+    receives -- is re-broadcast to the other ranks over a gloo group, so every rank handles the same messages at the
+    same program points and runs the same trials in the same order."""
+
+    def __init__(self, rank: int, world: int, device):
+        import datetime
+
+        import torch
+        import torch.distributed as dist
+
+        self.rank, self.world = rank, world
+        cuda = torch.device(device).type == "cuda"
+        long = datetime.timedelta(days=7)  # an idle executor blocks in the control broadcast between groups
+        dist.init_process_group("nccl" if cuda else "gloo", rank=rank, world_size=world, timeout=long,
+                                **({"device_id": torch.device(device)} if cuda else {}))
+        self.data = None  # the default group
+        self.ctl = dist.new_group(backend="gloo", timeout=long) if cuda else None
+
+    def broadcast(self, obj):
+        import torch.distributed as dist
+
+        box = [obj]
+        dist.broadcast_object_list(box, src=0, group=self.ctl)
+        return box[0]
+
+    def mean_(self, t) -> None:
+        """In-place cross-rank mean of a metric table (every rank then takes the same promotion decisions)."""
+        import torch.distributed as dist
+
+        if t.is_cuda:
+            dist.all_reduce(t, op=dist.ReduceOp.AVG)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            t.div_(self.world)
+
+
+class _LeaderChannel:
+    """Rank 0's scheduler channel: every ``recv`` result (or its absence) is re-broadcast to the followers."""
+
+    def __init__(self, chan: Channel, gang: _GangGroup):
+        self.chan, self.gang = chan, gang
+
+    def recv(self, timeout: Optional[float] = None):
+        try:
+            msg = self.chan.recv(timeout)
+        except ChannelClosed:
+            self.gang.broadcast({"__eof__": True})
+            raise
+        self.gang.broadcast(msg)
+        return msg
+
+    def send(self, msg: Dict[str, Any]) -> None:
+        self.chan.send(msg)
+
+    def close(self) -> None:
+        self.chan.close()
+
+
+class _FollowerChannel:
+    """A follower rank's view of the control stream: rank 0's broadcasts; its events go nowhere (rank 0 reports)."""
+
+    def __init__(self, gang: _GangGroup):
+        self.gang = gang
+
+    def recv(self, timeout: Optional[float] = None):
+        msg = self.gang.broadcast(None)
+        if isinstance(msg, dict) and msg.get("__eof__"):
+            raise ChannelClosed("leader closed the control stream")
+        return msg
+
+    def send(self, msg: Dict[str, Any]) -> None:
+        pass
+
+    def close(self) -> None:
+        pass
+
+
 def serve_forever(worker: ResidentWorker, chan: Channel) -> str:
     """Worker process main loop: first message must be ``init``; then serve until shutdown / EOF."""
     msg = chan.recv()
@@ -705,13 +809,20 @@ def serve_forever(worker: ResidentWorker, chan: Channel) -> str:
     worker.program_name = msg.get("program", worker.program_name)
     worker.params = dict(msg.get("params") or {})
     worker.max_active = int(msg.get("max_active", worker.max_active))
+    world = int(os.environ.get("PLX_RESIDENT_WORLD", "1"))
     try:
+        if world > 1:
+            worker.join_gang(int(os.environ["PLX_RESIDENT_RANK"]), world)
         worker._ready_info = worker.build()
     except Exception as e:
         chan.send({"ev": "error", "fatal": True, "message": f"program build failed: {e!r}",
                    "traceback": traceback.format_exc()})
         return "error"
     chan.send(worker._ready_info)
+    if worker.gang is not None:
+        # the scheduler talks to rank 0; the other ranks follow its control stream (their own channel only carries
+        # the init handshake, and their exit is how the pool notices a lost rank)
+        chan = _LeaderChannel(chan, worker.gang) if worker.gang.rank == 0 else _FollowerChannel(worker.gang)
     while True:
         r = worker.serve(chan)
         if r in ("shutdown", "eof"):

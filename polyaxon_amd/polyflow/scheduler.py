@@ -403,8 +403,10 @@ class Polyflow:
                 if spec.search_algorithm not in ("hyperband", "asha", "bo"):
                     raise PolyaxonfileError(f"resident executors run hyperband, asha and bo groups; "
                                             f"{spec.search_algorithm} groups use executor: process")
-                if spec.resources is not None and spec.resources.gpu is not None and spec.resources.gpu.value > 1:
-                    raise PolyaxonfileError("a resident executor runs on one device (resources.gpu <= 1)")
+                g = spec.resources.gpu.value if (spec.resources is not None and spec.resources.gpu is not None) else 1
+                if g > 1 and abs(g - round(g)) > 1e-9:
+                    raise PolyaxonfileError("a resident DP gang takes whole devices (resources.gpu <= 1 or an "
+                                            "integer)")
 
             gid = self.store.create_group(proj["id"], spec.raw_data, spec.hptuning.to_dict(), user=user,
                                           name=name or spec.name, description=description, tags=spec.tags,

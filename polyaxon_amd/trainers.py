@@ -184,6 +184,10 @@ def train_lm(argv=None) -> float:
                     help="model computes from fp32 weights under autocast (default on GPU: bf16 weights/grads with "
                          "an fp32 master copy in the optimizer)")
     ap.add_argument("--fixed_batch", action="store_true", help="reuse one synthetic batch every step")
+    ap.add_argument("--world1_collectives", action="store_true",
+                    help="world 1 on the GPU: still create the nccl (RCCL) process group, run every gradient "
+                         "bucket's all-reduce and the metric reducer's RCCL communicator (the DP path's overheads "
+                         "measured on one GPU)")
     ap.add_argument("--zero1", action="store_true",
                     help="ZeRO-1: reduce-scatter each gradient bucket, AdamW on this rank's 1/W slice inside the "
                          "backward, all-gather the bf16 weights (parallel/ddp.py); also PLX_ZERO1=1")
@@ -191,6 +195,13 @@ def train_lm(argv=None) -> float:
     backend = "gloo" if args.cpu or not torch.cuda.is_available() else "nccl"
     info = init_from_env(backend)
     dev = info["device"]
+    force = bool(args.world1_collectives) and dev.type == "cuda" and info["world"] == 1
+    if force:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     if dev.type == "cuda":
         from polyaxon_amd.client.budget import apply_hbm_budget
 
@@ -212,9 +223,10 @@ def train_lm(argv=None) -> float:
     # full-chip grid, slower with a capped one; profiles/r3_negative_results.md)
     zero1 = args.zero1 or os.environ.get("PLX_ZERO1", "0") == "1"
     in_bwd = zero1 or (dev.type == "cuda" and os.environ.get("PLX_OPT_IN_BACKWARD", "0") == "1")
-    ddp = FlatDDP(flat, bucket_mb=args.bucket_mb, optimizer=opt if in_bwd else None, shard_optimizer=zero1)
+    ddp = FlatDDP(flat, bucket_mb=args.bucket_mb, optimizer=opt if in_bwd else None, shard_optimizer=zero1,
+                  force_collectives=force)
     ddp.broadcast_params()
-    metrics = MetricReducer(dev)  # cross-rank mean of the logged loss (RCCL communicator on the GPU)
+    metrics = MetricReducer(dev, force_comm=force)  # cross-rank mean of the logged loss (RCCL communicator, GPU)
     g = torch.Generator(device=dev).manual_seed(args.seed + 1000 * info["rank"])
 
     def batch():  # synthetic tokens drawn on the device: a fresh batch per step costs one tiny kernel
@@ -259,11 +271,12 @@ def train_lm(argv=None) -> float:
 
         dec = _gemm.decisions()
         print(json.dumps({"loss": loss_val, "tokens_per_s": round(tok_s, 1), "world": info["world"],
+                          "world1_collectives": force, "zero1": zero1, "bucket_launches": ddp.launched,
                           "params_m": round(sum(s.numel for s in flat.segments) / 1e6, 1),
                           "lm_gemm": {"mode": _gemm.mode(), "native_shapes": sum(1 for d in dec.values() if d["native"]),
                                       "shapes": len(dec), "decisions": dec}}))
     metrics.close()
-    if info["world"] > 1:
+    if info["world"] > 1 or force:
         import torch.distributed as dist
 
         dist.destroy_process_group()
