@@ -13,10 +13,12 @@ epilogue adds to the bf16 slot in place, so a weight used twice needs no separat
 Shapes the kernel does not take (a dimension not a multiple of 256, or K of 64) go to ``torch`` (hipBLASLt) —
 :func:`supported` says which; on a GPU box a missing library raises instead of falling back (ops/_native.py).
 
-Dispatch (``PLX_LM_GEMM``): ``1`` always the MFMA kernel, ``0`` always hipBLASLt, ``auto`` (default) times both
-once per (M, N, K, layout) on first use and keeps the faster -- measured on MI355X the kernel wins the narrow
-weight gradients (split-K, 1.1-1.4x) and trails hipBLASLt by 10-25 % on the large forward / data-gradient shapes
-(profiles/r3_lm_gemm.md), so ``auto`` is what the trainers run.  :func:`decisions` lists what was chosen.
+Dispatch (``PLX_LM_GEMM``): ``1`` always the MFMA kernel, ``0`` always hipBLASLt, ``auto`` (default) takes the
+measured decision table ``TABLE`` for the GPT-2 125M / Llama-3 8B shapes (profiles/r3_lm_gemm.md: the kernel wins the
+narrow weight gradients, split-K 1.1-1.4x, and trails hipBLASLt by 10-25 % on the large forward / data-gradient
+shapes), so runs are reproducible and every DP rank runs the same kernel; any other shape is timed once on first use
+(both, 3 calls each) and, under torch.distributed, rank 0's choice is broadcast so the ranks agree.
+``PLX_LM_GEMM_TABLE=0`` times every shape.  :func:`decisions` lists what was chosen.
 """
 from __future__ import annotations
 
@@ -32,6 +34,25 @@ _ws: Dict[Tuple[str, int], torch.Tensor] = {}
 
 
 _choice: Dict[Tuple[int, int, int, bool, bool], Tuple[bool, float, float]] = {}
+
+# (M, N, K, A K-major, B K-major) -> the MFMA kernel is the faster one, from profiles/r3_lm_gemm.md (ping-pong kernel
+# vs hipBLASLt, one MI355X): GPT-2 125M at 16 x 1024 tokens and Llama-3 8B at 1 x 4096 tokens
+TABLE: Dict[Tuple[int, int, int, bool, bool], bool] = {}
+for _M, _N, _K, _win in (
+        # GPT-2: (qkv, proj, up, down) x (fwd, dgrad, wgrad)
+        (16384, 2304, 768, False), (16384, 768, 2304, False), (2304, 768, 16384, True),
+        (16384, 768, 768, False), (768, 768, 16384, True),
+        (16384, 3072, 768, False), (16384, 768, 3072, False), (3072, 768, 16384, True),
+        (768, 3072, 16384, True),
+        # Llama-3 8B
+        (4096, 6144, 4096, False), (4096, 4096, 6144, False), (6144, 4096, 4096, False),
+        (4096, 4096, 4096, False), (4096, 28672, 4096, False), (4096, 4096, 28672, False),
+        (28672, 4096, 4096, False), (4096, 4096, 14336, False), (4096, 14336, 4096, False),
+        (14336, 4096, 4096, False)):
+    # the shapes are listed by (M, N, K); the pass fixes the layout: fwd (K, K), dgrad (K, MN), wgrad (MN, MN)
+    for _ak, _bk in ((True, True), (True, False), (False, False)):
+        TABLE.setdefault((_M, _N, _K, _ak, _bk), _win)
+# the GPT-2 proj fwd / dgrad share 16384x768x768: hipBLASLt for both
 
 
 def mode() -> str:
@@ -70,6 +91,8 @@ def _use_native(a, b, M, N, K, a_kmajor, b_kmajor) -> bool:
         return m == "1"
     key = (M, N, K, bool(a_kmajor), bool(b_kmajor))
     hit = _choice.get(key)
+    if hit is None and key in TABLE and os.environ.get("PLX_LM_GEMM_TABLE", "1") != "0":
+        hit = _choice[key] = (TABLE[key], float("nan"), float("nan"))
     if hit is None:
         ts = []
         for native in (True, False):
@@ -83,7 +106,14 @@ def _use_native(a, b, M, N, K, a_kmajor, b_kmajor) -> bool:
             e1.record()
             e1.synchronize()
             ts.append(e0.elapsed_time(e1) / 3)
-        hit = _choice[key] = (ts[0] <= ts[1], round(ts[0], 4), round(ts[1], 4))
+        native = ts[0] <= ts[1]
+        import torch.distributed as dist
+
+        if dist.is_initialized() and dist.get_world_size() > 1:  # every rank runs rank 0's choice
+            flag = torch.tensor([1 if native else 0], dtype=torch.int32, device=a.device)
+            dist.broadcast(flag, src=0)
+            native = bool(int(flag.item()))
+        hit = _choice[key] = (native, round(ts[0], 4), round(ts[1], 4))
     return hit[0]
 
 

@@ -68,3 +68,21 @@ def test_torch_path_layouts_match_reference():
             out = torch.ones(M, N)
             gemm._torch_gemm(a, b, M, N, K, ak, bk, out=out, accumulate=True)
             torch.testing.assert_close(out, ref + 1)
+
+
+def test_auto_mode_takes_the_measured_table_without_timing(monkeypatch):
+    """``auto`` decides the GPT-2 / Llama-3 8B shapes from the measured table (reproducible; every DP rank the same
+    kernel): the narrow GPT-2 weight gradients on the MFMA kernel, the large Llama shapes on hipBLASLt -- no timing
+    (and so no CUDA call) on the way."""
+    from polyaxon_amd.ops import gemm
+
+    monkeypatch.setenv("PLX_LM_GEMM", "auto")
+    monkeypatch.delenv("PLX_LM_GEMM_TABLE", raising=False)
+    gemm._choice.clear()
+    x = torch.empty(0)
+    assert gemm._use_native(x, x, 2304, 768, 16384, False, False) is True       # GPT-2 qkv wgrad (split-K)
+    assert gemm._use_native(x, x, 16384, 3072, 768, True, True) is False        # GPT-2 up fwd
+    assert gemm._use_native(x, x, 4096, 28672, 4096, True, True) is False       # Llama up fwd
+    d = gemm.decisions()
+    assert d["2304x768x16384:MN"]["native"] is True and len(d) == 3
+    gemm._choice.clear()
