@@ -19,6 +19,8 @@
 //   plx_bn_bwd_dx        dx (and d_residual = dz) in one pass, optionally with the reduction partials of the
 //                        BatchNorm that produced the residual (ResBn: a downsampling branch's BN skips its reduce)
 #include <hip/hip_runtime.h>
+
+#include "handoff.h"
 #include <stdint.h>
 
 #define PLX_API extern "C" __attribute__((visibility("default")))
@@ -303,8 +305,10 @@ __device__ __forceinline__ bool reduce_l2_last(const float* __restrict__ part, i
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
   __syncthreads();
   if (threadIdx.x == 0) {
+    plx_handoff_release();  // no-op unless built with PLX_HANDOFF_FENCES (csrc/handoff.h: the hardware assumption)
     const unsigned old = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == (unsigned)(S - 1);
+    if (last) plx_handoff_acquire();
     if (last) __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = last;
   }

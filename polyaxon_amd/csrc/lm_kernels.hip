@@ -28,6 +28,8 @@
 // the first half of a head row and the matching chunk of the second half, so the pair it rotates is in
 // registers.  Grid-strided, 256-thread blocks, capped at 8192 blocks (>> 256 CUs x 8 waves).
 #include <hip/hip_runtime.h>
+
+#include "handoff.h"
 #include <stdint.h>
 
 #define PLX_API extern "C" __attribute__((visibility("default")))
@@ -382,8 +384,10 @@ __global__ __launch_bounds__(kBlock) void colsum_kernel(const bf16x8* __restrict
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+    plx_handoff_release();  // no-op unless built with PLX_HANDOFF_FENCES (csrc/handoff.h: the hardware assumption)
     const unsigned old = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == (unsigned)(R - 1);
+    if (last) plx_handoff_acquire();
     if (last) __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = last;
   }

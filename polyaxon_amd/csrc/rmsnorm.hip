@@ -12,6 +12,8 @@
 // wave64 shuffle + LDS reductions, fp32 math.  d % 8 == 0 and d <= 8192 (column partials of dw live in
 // registers: d / 8 / 256 vectors per lane).
 #include <hip/hip_runtime.h>
+
+#include "handoff.h"
 #include <stdint.h>
 
 #define PLX_API extern "C" __attribute__((visibility("default")))
@@ -447,8 +449,10 @@ __global__ __launch_bounds__(kBlock) void partial_colsum_kernel(const float* __r
   __syncthreads();
   unsigned* ctr = cnt + (int64_t)z * gridDim.x + blockIdx.x;
   if (threadIdx.x == 0) {
+    plx_handoff_release();  // no-op unless built with PLX_HANDOFF_FENCES (csrc/handoff.h: the hardware assumption)
     const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == (unsigned)(R - 1);
+    if (last) plx_handoff_acquire();
     if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = last;
   }

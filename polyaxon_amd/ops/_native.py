@@ -64,7 +64,9 @@ def _digest(sources: Iterable[Path], flags: List[str]) -> str:
 def _flags(kind: str) -> List[str]:
     common = ["-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-Wno-unused-function", f"-I{CSRC}"]
     if kind == "hip":
-        return common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+        # PLX_HANDOFF_FENCES=1: the in-launch partial-row hand-offs use release / acquire fences (csrc/handoff.h)
+        fences = ["-DPLX_HANDOFF_FENCES=1"] if os.environ.get("PLX_HANDOFF_FENCES") == "1" else []
+        return common + [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + fences
     if kind == "hip_host":  # host C++ that links the HIP runtime (streams, events, pinned memory, RCCL)
         return common + [f"-I{ROCM / 'include'}", "-D__HIP_PLATFORM_AMD__"]
     return common  # plain host C++

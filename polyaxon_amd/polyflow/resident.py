@@ -596,7 +596,8 @@ class ResidentWorker:
             ex.set_hparams(**{k: v for k, v in params.items() if k in self.program.hp_keys})
             ex.run(steps)
             ex.commit(self.asha_metrics.values[sh.row0 + rung], col, self.program.window)
-            if rung < sh.n_rungs - 1:
+            if rung < sh.n_rungs - 1 and self._snapshot_room():
+                # over the snapshot budget the config is not snapshotted: a later promotion re-trains it (RESTART)
                 ex.snapshot((sh.key, cid))
                 sh.snap_rung[cid] = rung
             self.stats["asha_jobs"] += 1
@@ -699,8 +700,42 @@ class ResidentWorker:
                                   if 0 <= i < len(cols) and cols[i] in sh.results[rung]]
             if a_early.get(sh.key):
                 sh.early_stopped = True
+            self._drop_hopeless_snapshots(sh)
         for sh in finished:
             self._finish_shard(sh, chan)
+
+    def _snapshot_room(self) -> bool:
+        """HBM budget of the resume snapshots (PLX_SNAPSHOT_GB, default 40 % of the device): one more fits?"""
+        import torch
+
+        ex = self.program.executor
+        if self._snap_budget is None:
+            gb = os.environ.get("PLX_SNAPSHOT_GB")
+            if gb:
+                self._snap_budget = float(gb) * 2 ** 30
+            elif ex.is_cuda:
+                self._snap_budget = 0.4 * torch.cuda.get_device_properties(ex.device).total_memory
+            else:
+                self._snap_budget = float("inf")
+        return (len(ex.snapshots) + 1) * ex.snapshot_bytes() <= self._snap_budget
+
+    _snap_budget = None
+
+    def _drop_hopeless_snapshots(self, sh: _AshaShard) -> None:
+        """Release the HBM snapshots of configs that can no longer be promoted: rung 0's result set is final
+        once no config is pending (every job of a round completes within the round), rung k+1's once rung k is final
+        and its whole top floor(n_k / eta) has been promoted; a config below its final rung's top set never resumes."""
+        final = not sh.pending
+        for rung in range(sh.n_rungs - 1):
+            if not final:
+                break
+            k = int(len(sh.results[rung]) / sh.eta)
+            top = set(sh.order[rung][:k])
+            for cid, r in list(sh.snap_rung.items()):
+                if r == rung and cid not in top:
+                    self.program.executor.drop((sh.key, cid))
+                    del sh.snap_rung[cid]
+            final = top <= sh.promoted[rung]
 
     def _finish_shard(self, sh: _AshaShard, chan: Channel) -> None:
         """Rung summaries (one ``rung_done`` per rung: its results and the configs promoted out of it), snapshots

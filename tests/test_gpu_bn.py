@@ -139,6 +139,48 @@ def test_reduce_finalize_one_launch_matches_two(cuda):
     torch.testing.assert_close(ref_f[:c].double(), mean, rtol=1e-5, atol=1e-6)
 
 
+def test_fence_free_handoff_stress(cuda):
+    """csrc/handoff.h's hardware assumption under load: 200 back-to-back one-launch reduce + finalize calls
+    over fresh partials, each grid (C/64 x S = 8 x 64 blocks of 1024 threads) larger than one workgroup per CU, while a
+    second stream keeps every CU busy with a streaming copy (uneven load, consumers L1-warm from the previous call):
+    every result bitwise equals the two-launch path (whose hand-off is a kernel boundary)."""
+    from polyaxon_amd.ops import _native
+
+    lib = _native.lib("plx_bn")
+    torch.manual_seed(11)
+    m, c, nblk = 128 * 4096, 512, 4096
+    f32 = dict(dtype=torch.float32, device=cuda)
+    x = torch.randn(m, c, device=cuda).to(torch.bfloat16)
+    l2 = torch.empty(int(lib.plx_bn_l2_workspace(nblk, c)), **f32)
+    cnt = torch.zeros(64, dtype=torch.int32, device=cuda)
+    w, b = torch.rand(c, **f32) + 0.5, torch.randn(c, **f32)
+    side = torch.cuda.Stream()
+    big = torch.empty(64 << 20, **f32)
+    bigo = torch.empty_like(big)
+    parts = [torch.rand(2 * nblk * c, **f32) * 4.0 for _ in range(4)]
+
+    def fwd(part, counters):
+        stats, rm, rv = torch.empty(4 * c, **f32), torch.zeros(c, **f32), torch.ones(c, **f32)
+        rc = lib.plx_bn_forward_from_partials(x.data_ptr(), None, None, m, c, w.data_ptr(), b.data_ptr(), 1e-5, 0.1,
+                                              rm.data_ptr(), rv.data_ptr(), stats.data_ptr(), stats[c:].data_ptr(),
+                                              stats[2 * c:].data_ptr(), part.data_ptr(), nblk, l2.data_ptr(), None, 0,
+                                              None, counters, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        return torch.cat([stats, rm, rv])
+
+    refs = [fwd(p, None) for p in parts]
+    got = []
+    for i in range(200):
+        if i % 10 == 0:
+            with torch.cuda.stream(side):  # every CU streaming beside the hand-offs
+                bigo.copy_(big)
+        got.append(fwd(parts[i % 4], cnt.data_ptr()))
+    torch.cuda.synchronize()
+    bad = [i for i, g in enumerate(got) if not torch.equal(g, refs[i % 4])]
+    assert not bad, f"{len(bad)} of 200 calls differ from the two-launch path (first: {bad[:5]})"
+    assert int(cnt.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 64, 15, 17), (2, 128, 9, 8), (2, 8, 6, 5)])
 def test_stem_bn_relu_pool_matches_unfused(cuda, shape):
     """ops.stem: BN + ReLU + max-pool in one forward pass and two backward passes (csrc/bn_kernels.hip) gives the

@@ -647,3 +647,43 @@ def test_polyflow_resident_bo_group_on_a_dp2_gang(tmp_path, cpu_pool_env):
         info = flow.call(lambda: dict(flow.resident_pool().workers[wid].info))
         assert info.get("dp_world") == 2
     assert flow.alloc.allocations == {}
+
+
+def test_asha_drops_snapshots_of_configs_that_can_no_longer_be_promoted():
+    """ADVICE r3: once rung 0 is final (nothing pending) the configs below its top floor(n/eta) lose their HBM snapshot;
+    rung 1 becomes final when rung 0's whole top set was promoted, and so on; the top sets keep theirs."""
+    from polyaxon_amd.polyflow.resident import ResidentWorker, _AshaShard
+
+    class Ex:
+        def __init__(self):
+            self.snapshots = {}
+
+        def drop(self, key):
+            self.snapshots.pop(key, None)
+
+    class Prog:
+        executor = Ex()
+
+    w = ResidentWorker("resnet_tiny", device="cpu")
+    w.program = Prog()
+    sh = _AshaShard(key="s", configs={i: {} for i in range(9)}, pending=[], n_rungs=3, eta=3.0, min_r=1, max_r=9,
+                    resource_name="units", resource=None, maximize=False, resume=True, seed=0)
+    sh.results = [{i: float(i) for i in range(9)}, {0: 0.5, 1: 0.7, 2: 0.1}, {}]
+    sh.order = [list(range(9)), [2, 0, 1], []]
+    sh.promoted = [{0, 1, 2}, set(), set()]
+    for cid in range(9):
+        sh.snap_rung[cid] = 0
+        Prog.executor.snapshots[("s", cid)] = object()
+    for cid in (0, 1, 2):  # the promoted ones were re-snapshotted at rung 1
+        sh.snap_rung[cid] = 1
+    w._drop_hopeless_snapshots(sh)
+    # rung 0 final: 3..8 are below its top 3 -> dropped; rung 1 final (top 3 of rung 0 promoted): top 1 of 3 = {2}
+    assert sorted(sh.snap_rung) == [2]
+    assert set(Prog.executor.snapshots) == {("s", 2)}
+    # with configs still pending nothing is final: nothing is dropped
+    sh2 = _AshaShard(key="t", configs={0: {}, 1: {}}, pending=[1], n_rungs=2, eta=3.0, min_r=1, max_r=3,
+                     resource_name="units", resource=None, maximize=False, resume=True, seed=0)
+    sh2.results, sh2.order, sh2.promoted = [{0: 1.0}, {}], [[0], []], [set(), set()]
+    sh2.snap_rung[0] = 0
+    w._drop_hopeless_snapshots(sh2)
+    assert sh2.snap_rung == {0: 0}
