@@ -363,6 +363,203 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// 4-wave variant: the same 256 x 256 x 64 tile, LDS layout and DMA engine, but 4 waves as 2 (M) x 2 (N), each
+// owning a 128 x 128 block of C as 8 x 8 MFMA tiles.  That is a third fewer LDS fragment bytes per MFMA than the
+// 8-wave kernel (each wave reads 2 x 128 x 64 bf16 per K-tile for 128 MFMAs instead of 192 x 64 for 64) and one
+// wave per SIMD, so the overlap comes from software pipelining inside the wave instead of ping-pong:
+//   * accumulators: 256 fp32 per lane, which only fits as AGPRs.  With __builtin_amdgcn_mfma_* hipcc keeps part of
+//     them in VGPRs and shuttles them through v_accvgpr_read/write around the MFMAs (r3_negative_results.md); the
+//     MFMAs are therefore issued as inline asm with the accumulator bound to an AGPR tuple ("+a"), which pins the
+//     whole accumulator block in AGPRs.  The compiler does not know these are MFMAs, so the two hazards it would
+//     otherwise cover are handled here: the zero-initialised AGPRs are first read many instructions later (DMA
+//     issue, waits, barriers) and the epilogue's AGPR reads follow an explicit s_nop run (mfma_drain).
+//   * phases: a K-tile is four 64 x 64 quadrants of the wave's block, 32 MFMAs each, in the order (0,0) (0,1)
+//     (1,1) (1,0).  Quarters are numbered seq = 4 t + o in READ order (o: 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi) and
+//     global phase g (= 4 t + p) issues the ds_reads of seq g + 2 (the fragments phase g + 1 needs) before its own
+//     MFMAs, so an LDS read always has a full phase of MFMAs to land.  Fragment sets: A-lo, A-hi and two B sets
+//     that swap roles every K-tile (B-lo of tile t + 1 is read into the set B-hi of tile t just released).
+//   * DMA ring: seq q's slot is free once its reads retired (lgkmcnt(0) at the end of phase q - 2 + barrier), so
+//     phase g restages seq g + 9 into the slot of seq g + 1; the end of phase g waits (counted vmcnt) for seq
+//     g + 3, the quarter phase g + 1 reads.  Six quarters (24 DMAs per wave) stay in flight; one barrier per phase.
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int NTH4 = 256;
+
+__device__ __forceinline__ void mfma_agpr(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// XDL write -> VALU / memory read of the result needs up to 18 wait states; the compiler cannot see the asm MFMAs
+__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
+
+__device__ __forceinline__ void wait_vm4(int n) {  // n = DMAs allowed in flight (multiple of 4), wave-uniform
+  if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (n >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool AK, bool BKM, bool ACC, bool SLAB>
+__global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntn = p.N / BN, ntm = p.M / BM;
+  const int id = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = id / ntn, tn = id % ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kt0 = blockIdx.y * p.kt_per_split;
+  const int nk = min(p.kt_per_split, p.K / BK - kt0);
+  const size_t k0 = (size_t)kt0 * BK;
+
+  const __bf16* abase = AK ? p.A + (size_t)m0 * p.lda + k0 : p.A + k0 * p.lda + m0;
+  const __bf16* bbase = BKM ? p.B + (size_t)n0 * p.ldb + k0 : p.B + k0 * p.ldb + n0;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(abase), rb = rsrc(bbase);
+  const uint32_t astep = AK ? BK * 2 : (uint32_t)(BK * p.lda * 2);
+  const uint32_t bstep = BKM ? BK * 2 : (uint32_t)(BK * p.ldb * 2);
+
+  // Quarter images: A-lo / A-hi hold rows 0-63 / 64-127 of each wave row's 128, B-lo / B-hi columns 0-63 / 64-127
+  // of each wave column's 128 (tile_idx<true> for both operands).  LDS slot of kind o: buffer * BUF + o * QUARTER.
+  // Per-lane source offsets of this wave's 4 pieces (wave + 4 pc) of each kind.
+  uint32_t src[4][4];
+#pragma unroll
+  for (int pc = 0; pc < 4; ++pc) {
+    src[0][pc] = src_off<true, AK>(0, wave + 4 * pc, lane, p.lda);
+    src[1][pc] = src_off<true, BKM>(0, wave + 4 * pc, lane, p.ldb);
+    src[2][pc] = src_off<true, BKM>(1, wave + 4 * pc, lane, p.ldb);
+    src[3][pc] = src_off<true, AK>(1, wave + 4 * pc, lane, p.lda);
+  }
+  const int S = 4 * nk;
+  // DMA of quarter seq q = 4 t + o (o compile-time after unrolling)
+  auto issue = [&](auto ko, int q) {
+    constexpr int O = decltype(ko)::value;
+    constexpr bool ISA = O == 0 || O == 3;
+    const int t = q >> 2;
+    char* dst = smem + (t & 1) * BUF + O * QUARTER;
+    const uint32_t koff = (uint32_t)t * (ISA ? astep : bstep);
+    const __amdgpu_buffer_rsrc_t r = ISA ? ra : rb;
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc) glds(r, src[O][pc] + koff, dst + (wave + 4 * pc) * 1024);
+  };
+
+  f32x4 acc[8][8];  // [n tile: 8 x 16 = the wave's 128 columns][m tile: 8 x 16 = its 128 rows]
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int aoff[4], boff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    aoff[i] = frag_off<AK>(wm * 64, AK ? (i & 1) : i, lane);
+    boff[i] = frag_off<BKM>(wn * 64, BKM ? (i & 1) : i, lane);
+  }
+  // one quarter's fragments for this wave: 4 tiles of 16 (rows of A or columns of B) x 2 k-steps
+  auto read_q = [&](const char* img, const int (&off)[4], auto kmaj) {
+    constexpr bool KM = decltype(kmaj)::value;
+    FragA f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) f.v[t][s] = KM ? ld_frag_k(img + off[s] + t * 2048) : ld_frag_t(img + off[t] + s * 8192);
+    return f;
+  };
+  auto read_seq = [&](auto ko, int q) {
+    constexpr int O = decltype(ko)::value;
+    const char* img = smem + ((q >> 2) & 1) * BUF + O * QUARTER;
+    if constexpr (O == 0 || O == 3) return read_q(img, aoff, IC<AK>{});
+    else return read_q(img, boff, IC<BKM>{});
+  };
+
+  // prologue: seq 0 .. min(8, S) - 1 (tiles 0 and 1), read seq 0 (A-lo) and 1 (B-lo) of tile 0, then seq 8
+  // into seq 0's slot once every wave's reads of it retired
+  auto pro = [&](auto qc) {
+    constexpr int Q = decltype(qc)::value;
+    if (Q < S) issue(IC<(Q & 3)>{}, Q);
+  };
+  pro(IC<0>{}), pro(IC<1>{}), pro(IC<2>{}), pro(IC<3>{}), pro(IC<4>{}), pro(IC<5>{}), pro(IC<6>{}), pro(IC<7>{});
+  wait_vm4(4 * (min(8, S) - 2));
+  __builtin_amdgcn_s_barrier();
+  FragA a_lo = read_seq(IC<0>{}, 0);
+  FragA b_lo = read_seq(IC<1>{}, 1);
+  FragA a_hi, b_hi;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (S > 8) issue(IC<0>{}, 8);
+  wait_vm4(4 * (min(8, S - 1) - 2));
+  __builtin_amdgcn_s_barrier();
+
+  // One phase g = 4 kt + P: ds_reads of seq g + 2 into `nxt`, DMA of seq g + 9, the quadrant's 32 MFMAs, then
+  // lgkmcnt(0) + vmcnt for seq g + 3 + barrier.
+  auto phase = [&](auto ph, int kt, const FragA& fa, const FragA& fb, FragA& nxt, auto mi_, auto ni_) {
+    constexpr int P = decltype(ph)::value, MI = decltype(mi_)::value, NI = decltype(ni_)::value;
+    const int g = 4 * kt + P;
+    nxt = read_seq(IC<((P + 2) & 3)>{}, g + 2);  // past the last tile: stale LDS into a dead set, harmless
+    if (g + 9 < S) issue(IC<((P + 1) & 3)>{}, g + 9);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) mfma_agpr(acc[NI * 4 + a][MI * 4 + b], fb.v[a][s], fa.v[b][s]);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_vm4(4 * (min(g + 9, S - 1) - (g + 3)));
+    __builtin_amdgcn_s_barrier();
+  };
+  // tile kt: quadrants (0,0) (0,1) (1,0) (1,1), so the last phase uses (A-hi, B-hi) and the sets the next tile's
+  // first phase needs (A-lo, B-lo) are free for phases 2 and 3 to refill: every set keeps its role
+  auto tile = [&](int kt) {
+    phase(IC<0>{}, kt, a_lo, b_lo, b_hi, IC<0>{}, IC<0>{});  // reads B-hi(kt)
+    phase(IC<1>{}, kt, a_lo, b_hi, a_hi, IC<0>{}, IC<1>{});  // reads A-hi(kt)
+    phase(IC<2>{}, kt, a_hi, b_lo, a_lo, IC<1>{}, IC<0>{});  // reads A-lo(kt + 1)
+    phase(IC<3>{}, kt, a_hi, b_hi, b_lo, IC<1>{}, IC<1>{});  // reads B-lo(kt + 1)
+  };
+#pragma unroll 1
+  for (int kt = 0; kt < nk; ++kt) tile(kt);
+  mfma_drain();
+
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      const int m = m0 + wm * 128 + (mt >> 2) * 64 + (mt & 3) * 16 + fr;
+      const int n = n0 + wn * 128 + (nt >> 2) * 64 + (nt & 3) * 16 + 4 * fq;
+      f32x4 v = acc[nt][mt];
+      if (SLAB) {
+        *(f32x4*)((float*)p.C + ((size_t)blockIdx.y * p.M + m) * p.N + n) = v;
+      } else {
+        __bf16* dst = (__bf16*)p.C + (size_t)m * p.ldc + n;
+        if (ACC) {
+          const uint2 o = *(const uint2*)dst;
+          v[0] = p.alpha * v[0] + __uint_as_float(o.x << 16);
+          v[1] = p.alpha * v[1] + __uint_as_float(o.x & 0xffff0000u);
+          v[2] = p.alpha * v[2] + __uint_as_float(o.y << 16);
+          v[3] = p.alpha * v[3] + __uint_as_float(o.y & 0xffff0000u);
+        } else {
+          v *= p.alpha;
+          if (p.bias != nullptr) v += *(const f32x4*)(p.bias + n);
+        }
+        uint2 packed;
+        packed.x = pack_bf16x2(v[0], v[1]);
+        packed.y = pack_bf16x2(v[2], v[3]);
+        *(uint2*)dst = packed;
+        if (!ACC && p.C2 != nullptr) {
+          uint2 gl;
+          gl.x = pack_bf16x2(gelu_tanh(bf16_round(v[0])), gelu_tanh(bf16_round(v[1])));
+          gl.y = pack_bf16x2(gelu_tanh(bf16_round(v[2])), gelu_tanh(bf16_round(v[3])));
+          *(uint2*)((__bf16*)p.C2 + (size_t)m * p.ldc + n) = gl;
+        }
+      }
+    }
+}
+
 // C (bf16, ldc) = alpha * sum over splits of the fp32 slabs (+ C when accumulating); 8 elements per thread
 template <bool ACC>
 __global__ void __launch_bounds__(256) gemm256_reduce(const float* __restrict__ ws, __bf16* __restrict__ C, int M,
@@ -413,13 +610,24 @@ __global__ void __launch_bounds__(256) gemm256_reduce(const float* __restrict__ 
   }
 }
 
+int g_waves = 8;  // 8: the ping-pong kernel, 4: gemm256w4_kernel (plx_gemm256_set_waves)
+
 template <bool AK, bool BKM, bool ACC, bool SLAB>
 int launch(const Gemm256Args& a, int splits, hipStream_t st) {
+  const dim3 grid((a.M / BM) * (a.N / BN), splits);
+  if (g_waves == 4) {
+    auto k = gemm256w4_kernel<AK, BKM, ACC, SLAB>;
+    static const int attr = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                LDS_BYTES) == hipSuccess ? 0 : -4;
+    if (attr) return attr;
+    hipLaunchKernelGGL(k, grid, dim3(NTH4), LDS_BYTES, st, a);
+    return 0;
+  }
   auto k = gemm256_kernel<AK, BKM, ACC, SLAB>;
   static const int attr =
       hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess ? 0 : -4;
   if (attr) return attr;
-  hipLaunchKernelGGL(k, dim3((a.M / BM) * (a.N / BN), splits), dim3(NTH), LDS_BYTES, st, a);
+  hipLaunchKernelGGL(k, grid, dim3(NTH), LDS_BYTES, st, a);
   return 0;
 }
 
@@ -452,6 +660,13 @@ PLX_API int plx_gemm256_splits(int M, int N, int K) {
 
 // A/B knob: blocks the split-K planner aims for (0 disables splitting)
 PLX_API void plx_gemm256_set_split_target(int blocks) { g_split_target = blocks; }
+
+// A/B knob: 8 (the 8-wave ping-pong kernel) or 4 (the 4-wave AGPR-accumulator kernel); returns the previous value
+PLX_API int plx_gemm256_set_waves(int waves) {
+  const int prev = g_waves;
+  if (waves == 4 || waves == 8) g_waves = waves;
+  return prev;
+}
 
 // C[M][N] (bf16, ldc) = alpha * A . B (+ bias[n]) (+ C when accumulate), layouts per a_kmajor / b_kmajor (see the
 // file header).  bias: fp32 [N], 16-byte aligned, or null (not combined with accumulate).

@@ -1,8 +1,9 @@
 """Time the 256x256 MFMA GEMM (csrc/gemm256.hip) against torch (hipBLASLt) on the LM linears' shapes.
 
-    python scripts/gemm_bench.py [--models gpt2,llama] [--reps 20]
+    python scripts/gemm_bench.py [--models gpt2,llama] [--reps 20] [--waves 8,4]
 
 One JSON line per (model, linear, pass): ms and TFLOP/s of both, and the max |diff| relative to the output scale.
+``--waves 8,4`` times both kernel variants (plx_gemm256_set_waves) in the same process, interleaved per shape.
 Passes: fwd (x . W^T), dgrad (dy . W), wgrad (dy^T . x, K = tokens).
 """
 from __future__ import annotations
@@ -42,10 +43,13 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--models", default="gpt2,llama")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--waves", default="8")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    tot = {"native": 0.0, "torch": 0.0}
+    tot = {"torch": 0.0}
+    waves = [int(w) for w in args.waves.split(",")]
+    lib = gemm._native.lib("plx_gemm")
     for model in args.models.split(","):
         T, linears = MODELS[model]
         for name, fin, fout in linears:
@@ -58,19 +62,26 @@ def main() -> None:
                 ("wgrad", fout, fin, T, lambda: gemm.wgrad(dy, x), lambda: dy.t() @ x),
             ]
             for pas, M, N, K, nat, ref in cases:
-                a, b = nat(), ref()
-                err = ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6)).item()
-                tn, tt = timed(nat, args.reps), timed(ref, args.reps)
-                tot["native"] += tn
-                tot["torch"] += tt
+                b = ref()
                 fl = 2.0 * M * N * K
-                print(json.dumps({"model": model, "linear": name, "pass": pas, "M": M, "N": N, "K": K,
-                                  "splits": gemm._native.size("plx_gemm", "plx_gemm256_splits", M, N, K),
-                                  "native_ms": round(tn, 4), "torch_ms": round(tt, 4),
-                                  "native_tflops": round(fl / tn / 1e9, 1), "torch_tflops": round(fl / tt / 1e9, 1),
-                                  "speedup": round(tt / tn, 3), "rel_err": round(err, 5)}), flush=True)
+                tt = timed(ref, args.reps)
+                tot["torch"] += tt
+                rec = {"model": model, "linear": name, "pass": pas, "M": M, "N": N, "K": K,
+                       "splits": gemm._native.size("plx_gemm", "plx_gemm256_splits", M, N, K),
+                       "torch_ms": round(tt, 4), "torch_tflops": round(fl / tt / 1e9, 1)}
+                for wv in waves:
+                    lib.plx_gemm256_set_waves(wv)
+                    a = nat()
+                    err = ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6)).item()
+                    tn = timed(nat, args.reps)
+                    sfx = "" if len(waves) == 1 else f"_w{wv}"
+                    tot["native" + sfx] = tot.get("native" + sfx, 0.0) + tn
+                    rec.update({f"native{sfx}_ms": round(tn, 4), f"native{sfx}_tflops": round(fl / tn / 1e9, 1),
+                                f"speedup{sfx}": round(tt / tn, 3), f"rel_err{sfx}": round(err, 5)})
+                print(json.dumps(rec), flush=True)
             del x, w, dy
-    print(json.dumps({"total_native_ms": round(tot["native"], 3), "total_torch_ms": round(tot["torch"], 3)}))
+    lib.plx_gemm256_set_waves(waves[0])
+    print(json.dumps({f"total_{k}_ms": round(v, 3) for k, v in tot.items()}))
 
 
 if __name__ == "__main__":

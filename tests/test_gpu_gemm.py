@@ -75,6 +75,58 @@ def test_gemm256_bias_epilogue(cuda, M, N, K):
         _check(out, ref, K)
 
 
+@pytest.fixture
+def four_waves(cuda):
+    from polyaxon_amd.ops import _native
+
+    lib = _native.lib("plx_gemm")
+    prev = lib.plx_gemm256_set_waves(4)
+    yield
+    lib.plx_gemm256_set_waves(prev)
+
+
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (768, 512, 1024), (256, 512, 8192)])
+def test_gemm256_four_wave_kernel_matches_fp32(cuda, four_waves, a_kmajor, b_kmajor, M, N, K):
+    """The 4-wave kernel (AGPR accumulators through inline-asm MFMAs): every layout, 1 / odd / many K-tiles, and the
+    split-K slabs (256 x 512 x 8192), plain and accumulating with alpha."""
+    from polyaxon_amd.ops import gemm
+
+    a = _rand((M, K) if a_kmajor else (K, M), cuda, 11)
+    b = _rand((N, K) if b_kmajor else (K, N), cuda, 12)
+    af = a.float() if a_kmajor else a.float().t()
+    bf = b.float() if b_kmajor else b.float().t()
+    out = gemm.gemm(a, b, M, N, K, a_kmajor, b_kmajor)
+    torch.cuda.synchronize()
+    _check(out, af @ bf.t(), K)
+    c0 = _rand((M, N), cuda, 13)
+    acc = c0.clone()
+    gemm.gemm(a, b, M, N, K, a_kmajor, b_kmajor, out=acc, accumulate=True, alpha=0.5)
+    torch.cuda.synchronize()
+    _check(acc, 0.5 * (af @ bf.t()) + c0.float(), K)
+
+
+def test_gemm256_four_wave_epilogues_and_repeat(cuda, four_waves):
+    """Bias + GELU epilogue on the 4-wave kernel, and 20 back-to-back launches bitwise equal (a DMA / read race
+    shows up as run-to-run differences)."""
+    from polyaxon_amd.ops import gemm
+
+    M, N, K = 512, 768, 2048
+    a, b = _rand((M, K), cuda, 14), _rand((N, K), cuda, 15)
+    bias = torch.randn(N, device=cuda)
+    h = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    g = torch.empty_like(h)
+    gemm.gemm(a, b, M, N, K, True, True, out=h, bias=bias, gelu_out=g)
+    ref = a.float() @ b.float().t() + bias
+    torch.cuda.synchronize()
+    _check(h, ref, K)
+    _check(g, F.gelu(h.float(), approximate="tanh"), K)
+    first = gemm.gemm(a, b, M, N, K, True, True)
+    for _ in range(20):
+        again = gemm.gemm(a, b, M, N, K, True, True)
+        assert torch.equal(first, again)
+
+
 def test_gemm256_strided_output(cuda):
     """out may be a column block of a wider matrix (ldc > N)."""
     from polyaxon_amd.ops import gemm
