@@ -402,7 +402,7 @@ __device__ __forceinline__ void wait_vm4(int n) {  // n = DMAs allowed in flight
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool AK, bool BKM, bool ACC, bool SLAB>
+template <bool AK, bool BKM, bool ACC, bool SLAB, bool PAIR>
 __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -489,8 +489,12 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
   FragA a_hi, b_hi;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  if (S > 8) issue(IC<0>{}, 8);
-  wait_vm4(4 * (min(8, S - 1) - 2));
+  if (PAIR) {  // phases 0 and 1 read seq 2 and 3 after the next barrier
+    wait_vm4(4 * (min(8, S) - 1 - 3));
+  } else {
+    if (S > 8) issue(IC<0>{}, 8);
+    wait_vm4(4 * (min(8, S - 1) - 2));
+  }
   __builtin_amdgcn_s_barrier();
 
   // One phase g = 4 kt + P: ds_reads of seq g + 2 into `nxt`, DMA of seq g + 9, the quadrant's 32 MFMAs, then
@@ -499,7 +503,8 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
     constexpr int P = decltype(ph)::value, MI = decltype(mi_)::value, NI = decltype(ni_)::value;
     const int g = 4 * kt + P;
     nxt = read_seq(IC<((P + 2) & 3)>{}, g + 2);  // past the last tile: stale LDS into a dead set, harmless
-    if (g + 9 < S) issue(IC<((P + 1) & 3)>{}, g + 9);
+    constexpr int AHEAD = PAIR ? 8 : 9;
+    if (g + AHEAD < S) issue(IC<((P + AHEAD) & 3)>{}, g + AHEAD);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -508,9 +513,15 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) mfma_agpr(acc[NI * 4 + a][MI * 4 + b], fb.v[a][s], fa.v[b][s]);
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wait_vm4(4 * (min(g + 9, S - 1) - (g + 3)));
-    __builtin_amdgcn_s_barrier();
+    if constexpr (!PAIR) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_vm4(4 * (min(g + 9, S - 1) - (g + 3)));
+      __builtin_amdgcn_s_barrier();
+    } else if constexpr (P & 1) {  // seqs g + 3 and g + 4 are read in the next two phases
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_vm4(4 * (min(g + 8, S - 1) - (g + 4)));
+      __builtin_amdgcn_s_barrier();
+    }
   };
   // tile kt: quadrants (0,0) (0,1) (1,0) (1,1), so the last phase uses (A-hi, B-hi) and the sets the next tile's
   // first phase needs (A-lo, B-lo) are free for phases 2 and 3 to refill: every set keeps its role
@@ -611,16 +622,20 @@ __global__ void __launch_bounds__(256) gemm256_reduce(const float* __restrict__ 
 }
 
 int g_waves = 8;  // 8: the ping-pong kernel, 4: gemm256w4_kernel (plx_gemm256_set_waves)
+int g_pair = 0;   // 4-wave kernel: 1 = one barrier per two phases (plx_gemm256_set_waves(5))
 
 template <bool AK, bool BKM, bool ACC, bool SLAB>
 int launch(const Gemm256Args& a, int splits, hipStream_t st) {
   const dim3 grid((a.M / BM) * (a.N / BN), splits);
   if (g_waves == 4) {
-    auto k = gemm256w4_kernel<AK, BKM, ACC, SLAB>;
-    static const int attr = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                LDS_BYTES) == hipSuccess ? 0 : -4;
+    auto k0 = gemm256w4_kernel<AK, BKM, ACC, SLAB, false>;
+    auto k1 = gemm256w4_kernel<AK, BKM, ACC, SLAB, true>;
+    static const int attr =
+        (hipFuncSetAttribute((const void*)k0, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
+         hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess)
+            ? 0 : -4;
     if (attr) return attr;
-    hipLaunchKernelGGL(k, grid, dim3(NTH4), LDS_BYTES, st, a);
+    hipLaunchKernelGGL(g_pair ? k1 : k0, grid, dim3(NTH4), LDS_BYTES, st, a);
     return 0;
   }
   auto k = gemm256_kernel<AK, BKM, ACC, SLAB>;
@@ -661,10 +676,12 @@ PLX_API int plx_gemm256_splits(int M, int N, int K) {
 // A/B knob: blocks the split-K planner aims for (0 disables splitting)
 PLX_API void plx_gemm256_set_split_target(int blocks) { g_split_target = blocks; }
 
-// A/B knob: 8 (the 8-wave ping-pong kernel) or 4 (the 4-wave AGPR-accumulator kernel); returns the previous value
+// A/B knob: 8 (the 8-wave ping-pong kernel), 4 (the 4-wave AGPR-accumulator kernel, a barrier per phase) or 5 (the
+// same with one barrier per two phases); returns the previous value
 PLX_API int plx_gemm256_set_waves(int waves) {
-  const int prev = g_waves;
-  if (waves == 4 || waves == 8) g_waves = waves;
+  const int prev = g_waves == 4 && g_pair ? 5 : g_waves;
+  if (waves == 4 || waves == 8) g_waves = waves, g_pair = 0;
+  if (waves == 5) g_waves = 4, g_pair = 1;
   return prev;
 }
 

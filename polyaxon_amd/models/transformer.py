@@ -46,6 +46,10 @@ class TransformerConfig:
     norm_eps: float = 1e-5
     bias: bool = True
     checkpoint: bool = False
+    # embedding / head rows are padded to a multiple of this (GPT-2's 50257 -> 50432 = 197 x 256, so the logits,
+    # their data gradient and the tied-weight gradient are gemm256 shapes); the padded logits carry a -inf bias, so
+    # the softmax, the loss and every gradient of the real vocabulary are unchanged and the padded rows get 0
+    vocab_multiple: int = 256
 
     @property
     def kv_heads(self) -> int:
@@ -54,6 +58,11 @@ class TransformerConfig:
     @property
     def head_dim(self) -> int:
         return self.d_model // self.n_heads
+
+    @property
+    def vocab_rows(self) -> int:
+        m = max(1, self.vocab_multiple)
+        return (self.vocab_size + m - 1) // m * m
 
 
 def gpt2_125m(**kw) -> TransformerConfig:
@@ -167,11 +176,18 @@ class Transformer(nn.Module):
     def __init__(self, cfg: TransformerConfig):
         super().__init__()
         self.cfg = cfg
-        self.embed = nn.Embedding(cfg.vocab_size, cfg.d_model)
+        rows = cfg.vocab_rows
+        self.embed = nn.Embedding(rows, cfg.d_model)
         self.pos = nn.Embedding(cfg.max_seq_len, cfg.d_model) if cfg.pos == "learned" else None
         self.blocks = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layers)])
         self.norm = RMSNorm(cfg.d_model, cfg.norm_eps) if cfg.norm == "rmsnorm" else _rms.LayerNorm(cfg.d_model)
-        self.head = None if cfg.tie_embeddings else nn.Linear(cfg.d_model, cfg.vocab_size, bias=False)
+        self.head = None if cfg.tie_embeddings else nn.Linear(cfg.d_model, rows, bias=False)
+        if rows > cfg.vocab_size:  # fp32 logit bias: 0 on the vocabulary, -inf on the padding rows
+            mask = torch.zeros(rows)
+            mask[cfg.vocab_size:] = float("-inf")
+            self.register_buffer("logit_mask", mask, persistent=False)
+        else:
+            self.logit_mask = None
         self._rope = None
         self.reset_parameters()
 
@@ -223,9 +239,10 @@ class Transformer(nn.Module):
                 else:
                     x = blk(x, rope)
             x = self.norm(x)
-        if self.head is None:  # tied: the embedding's gradient also arrives through autograd, keep F.linear
-            return F.linear(x, self.embed.weight)
-        return lm_ops.linear(x, self.head.weight)
+        # tied: the head's weight gradient is written first (into the flat slot, or returned to autograd) and the
+        # embedding's arrives after it through autograd's accumulation, so both paths add up
+        w = self.embed.weight if self.head is None else self.head.weight
+        return lm_ops.linear(x, w, self.logit_mask)
 
     @staticmethod
     def _add_norm(x, r, norm):

@@ -242,9 +242,10 @@ class _LinearDirect(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, slot, flat, act=None):
-        ctx.slot, ctx.flat, ctx.has_bias = slot, flat, bias is not None
+        # a bias that takes no gradient (the logit mask of a padded vocabulary) skips the column-sum pass
+        ctx.slot, ctx.flat, ctx.has_bias = slot, flat, bias is not None and bias.requires_grad
         ctx.bias, ctx.act = bias, act
-        y = F.linear(x, weight, bias)
+        y = F.linear(x, weight, bias if bias is None or bias.dtype == x.dtype else bias.to(x.dtype))
         if act is None:
             ctx.save_for_backward(x, weight)
             return y
@@ -278,7 +279,7 @@ class _LinearMfma(torch.autograd.Function):
         from polyaxon_amd.ops import gemm
 
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
-        ctx.slot, ctx.flat, ctx.has_bias, ctx.xshape = slot, flat, bias is not None, x.shape
+        ctx.slot, ctx.flat, ctx.has_bias, ctx.xshape = slot, flat, bias is not None and bias.requires_grad, x.shape
         ctx.bias, ctx.act = bias, act
         if act is None:
             y = gemm.forward(x2, weight, bias)
@@ -328,5 +329,5 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
         return _LinearMfma.apply(x, weight, bias, None, None, act)
     if direct:
         return _LinearDirect.apply(x, weight, bias, slot, flat, act)
-    y = F.linear(x, weight, bias)
+    y = F.linear(x, weight, bias if bias is None or bias.dtype == x.dtype else bias.to(x.dtype))
     return y if act is None else F.gelu(y, approximate="tanh")

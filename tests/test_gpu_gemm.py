@@ -75,12 +75,12 @@ def test_gemm256_bias_epilogue(cuda, M, N, K):
         _check(out, ref, K)
 
 
-@pytest.fixture
-def four_waves(cuda):
+@pytest.fixture(params=[4, 5], ids=["barrier_per_phase", "barrier_per_two_phases"])
+def four_waves(cuda, request):
     from polyaxon_amd.ops import _native
 
     lib = _native.lib("plx_gemm")
-    prev = lib.plx_gemm256_set_waves(4)
+    prev = lib.plx_gemm256_set_waves(request.param)
     yield
     lib.plx_gemm256_set_waves(prev)
 

@@ -181,3 +181,34 @@ def test_add_rmsnorm_matches_fp32(cuda, rows, d):
     torch.testing.assert_close(x.grad.float(), ref_dx, rtol=3e-2, atol=3e-2 * float(ref_dx.abs().max()))
     torch.testing.assert_close(r.grad.float(), ref_dx, rtol=3e-2, atol=3e-2 * float(ref_dx.abs().max()))
     torch.testing.assert_close(w.grad, wr.grad, rtol=2e-2, atol=2e-2 * rows ** 0.5)
+
+
+def test_padded_gpt2_vocab_head_on_gemm256(cuda, monkeypatch):
+    """GPT-2's real vocabulary (50257) padded to 50432 rows: the tied head, its data gradient and the tied-weight
+    gradient run on gemm256 (PLX_LM_GEMM=1) with the -inf logit bias in the epilogue; loss and gradients match the
+    unpadded model (head on hipBLASLt, 50257 is no gemm256 shape), the padding rows get a zero gradient."""
+    from polyaxon_amd.models.transformer import Transformer, gpt2_125m, lm_loss
+    from polyaxon_amd.ops import gemm
+
+    monkeypatch.setenv("PLX_LM_GEMM", "1")
+    kw = dict(n_layers=1, d_model=256, n_heads=4, d_ff=1024, max_seq_len=256)
+    torch.manual_seed(0)
+    with torch.device(cuda):
+        mp = Transformer(gpt2_125m(**kw)).to(torch.bfloat16)
+        mu = Transformer(gpt2_125m(vocab_multiple=1, **kw)).to(torch.bfloat16)
+    sd = mp.state_dict()
+    sd["embed.weight"] = sd["embed.weight"][:50257]
+    mu.load_state_dict(sd)
+    assert gemm.supported(512, 50432, 256) and not gemm.supported(512, 50257, 256)
+    tok = torch.randint(0, 50257, (2, 256), device=cuda)
+    res = {}
+    for name, m in (("padded", mp), ("plain", mu)):
+        logits = m(tok)
+        assert ("Mfma" in type(logits.grad_fn).__name__) == (name == "padded"), type(logits.grad_fn).__name__
+        loss = lm_loss(logits, tok)
+        loss.backward()
+        res[name] = (float(loss), m.embed.weight.grad.float())
+    assert abs(res["padded"][0] - res["plain"][0]) <= 2e-2 * abs(res["plain"][0])
+    gp, gu = res["padded"][1], res["plain"][1]
+    assert float(gp[50257:].abs().max()) == 0.0
+    assert float((gp[:50257] - gu).norm()) <= 0.03 * float(gu.norm())
