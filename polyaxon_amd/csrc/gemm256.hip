@@ -37,6 +37,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #define PLX_API extern "C" __attribute__((visibility("default")))
 
 namespace {
@@ -135,6 +137,12 @@ template <int V>
 struct IC {
   static constexpr int value = V;
 };
+
+// f(IC<0>{}), f(IC<1>{}), ... in order
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for(F& f, std::integer_sequence<int, Is...>) {
+  (f(IC<Is>{}), ...);
+}
 
 struct Gemm256Args {
   const __bf16* A;
@@ -402,7 +410,7 @@ __device__ __forceinline__ void wait_vm4(int n) {  // n = DMAs allowed in flight
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool AK, bool BKM, bool ACC, bool SLAB, bool PAIR>
+template <bool AK, bool BKM, bool ACC, bool SLAB, bool PAIR, bool ILV>
 __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -445,6 +453,13 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
 #pragma unroll
     for (int pc = 0; pc < 4; ++pc) glds(r, src[O][pc] + koff, dst + (wave + 4 * pc) * 1024);
   };
+  auto issue_piece = [&](auto ko, int q, auto pcc) {  // one of the 4 DMAs of `issue`
+    constexpr int O = decltype(ko)::value, PC = decltype(pcc)::value;
+    constexpr bool ISA = O == 0 || O == 3;
+    const int t = q >> 2;
+    const uint32_t koff = (uint32_t)t * (ISA ? astep : bstep);
+    glds(ISA ? ra : rb, src[O][PC] + koff, smem + (t & 1) * BUF + O * QUARTER + (wave + 4 * PC) * 1024);
+  };
 
   f32x4 acc[8][8];  // [n tile: 8 x 16 = the wave's 128 columns][m tile: 8 x 16 = its 128 rows]
 #pragma unroll
@@ -473,6 +488,13 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
     const char* img = smem + ((q >> 2) & 1) * BUF + O * QUARTER;
     if constexpr (O == 0 || O == 3) return read_q(img, aoff, IC<AK>{});
     else return read_q(img, boff, IC<BKM>{});
+  };
+  auto read_one = [&](auto ko, int q, auto tc, auto sc) {  // fragment (t, s) of `read_seq`
+    constexpr int O = decltype(ko)::value, T = decltype(tc)::value, SS = decltype(sc)::value;
+    constexpr bool KM = (O == 0 || O == 3) ? AK : BKM;
+    const int(&off)[4] = (O == 0 || O == 3) ? aoff : boff;
+    const char* img = smem + ((q >> 2) & 1) * BUF + O * QUARTER;
+    return KM ? ld_frag_k(img + off[SS] + T * 2048) : ld_frag_t(img + off[T] + SS * 8192);
   };
 
   // prologue: seq 0 .. min(8, S) - 1 (tiles 0 and 1), read seq 0 (A-lo) and 1 (B-lo) of tile 0, then seq 8
@@ -503,15 +525,32 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
     constexpr int P = decltype(ph)::value, MI = decltype(mi_)::value, NI = decltype(ni_)::value;
     const int g = 4 * kt + P;
     nxt = read_seq(IC<((P + 2) & 3)>{}, g + 2);  // past the last tile: stale LDS into a dead set, harmless
-    constexpr int AHEAD = PAIR ? 8 : 9;
-    if (g + AHEAD < S) issue(IC<((P + AHEAD) & 3)>{}, g + AHEAD);
-    __builtin_amdgcn_sched_barrier(0);
+    constexpr int AHEAD = PAIR ? 8 : 9, RO = (P + 2) & 3, DO = (P + AHEAD) & 3;
+    const bool dma = g + AHEAD < S;
+    if constexpr (!ILV) {
+      nxt = read_seq(IC<RO>{}, g + 2);  // past the last tile: stale LDS into a dead set, harmless
+      if (dma) issue(IC<DO>{}, g + AHEAD);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) mfma_agpr(acc[NI * 4 + a][MI * 4 + b], fb.v[a][s], fa.v[b][s]);
+          for (int b = 0; b < 4; ++b) mfma_agpr(acc[NI * 4 + a][MI * 4 + b], fb.v[a][s], fa.v[b][s]);
+    } else {
+      // interleaved: MFMA i is followed by fragment read i (i < 8) or DMA piece i - 8 (8 <= i < 12), so the
+      // reads and DMA issue run in the shadow of this wave's own MFMAs instead of ahead of them
+      auto step = [&](auto ic) {
+        constexpr int I = decltype(ic)::value, SS = I >> 4, A = (I >> 2) & 3, B = I & 3;
+        mfma_agpr(acc[NI * 4 + A][MI * 4 + B], fb.v[A][SS], fa.v[B][SS]);
+        if constexpr (I < 8) nxt.v[I >> 1][I & 1] = read_one(IC<RO>{}, g + 2, IC<(I >> 1)>{}, IC<(I & 1)>{});
+        else if constexpr (I < 12) {
+          if (dma) issue_piece(IC<DO>{}, g + AHEAD, IC<(I - 8)>{});
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      static_for(step, std::make_integer_sequence<int, 32>{});
+    }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (!PAIR) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -622,20 +661,25 @@ __global__ void __launch_bounds__(256) gemm256_reduce(const float* __restrict__ 
 }
 
 int g_waves = 8;  // 8: the ping-pong kernel, 4: gemm256w4_kernel (plx_gemm256_set_waves)
-int g_pair = 0;   // 4-wave kernel: 1 = one barrier per two phases (plx_gemm256_set_waves(5))
+int g_w4 = 0;     // 4-wave kernel schedule bits: 1 = one barrier per two phases, 2 = reads / DMAs interleaved
+                  // with the MFMAs (plx_gemm256_set_waves(4 + bits))
 
 template <bool AK, bool BKM, bool ACC, bool SLAB>
 int launch(const Gemm256Args& a, int splits, hipStream_t st) {
   const dim3 grid((a.M / BM) * (a.N / BN), splits);
   if (g_waves == 4) {
-    auto k0 = gemm256w4_kernel<AK, BKM, ACC, SLAB, false>;
-    auto k1 = gemm256w4_kernel<AK, BKM, ACC, SLAB, true>;
-    static const int attr =
-        (hipFuncSetAttribute((const void*)k0, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess &&
-         hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess)
-            ? 0 : -4;
+    void (*ks[4])(Gemm256Args) = {gemm256w4_kernel<AK, BKM, ACC, SLAB, false, false>,
+                                   gemm256w4_kernel<AK, BKM, ACC, SLAB, true, false>,
+                                   gemm256w4_kernel<AK, BKM, ACC, SLAB, false, true>,
+                                   gemm256w4_kernel<AK, BKM, ACC, SLAB, true, true>};
+    static const int attr = [&] {
+      for (auto k : ks)
+        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) != hipSuccess)
+          return -4;
+      return 0;
+    }();
     if (attr) return attr;
-    hipLaunchKernelGGL(g_pair ? k1 : k0, grid, dim3(NTH4), LDS_BYTES, st, a);
+    hipLaunchKernelGGL(ks[g_w4 & 3], grid, dim3(NTH4), LDS_BYTES, st, a);
     return 0;
   }
   auto k = gemm256_kernel<AK, BKM, ACC, SLAB>;
@@ -676,12 +720,13 @@ PLX_API int plx_gemm256_splits(int M, int N, int K) {
 // A/B knob: blocks the split-K planner aims for (0 disables splitting)
 PLX_API void plx_gemm256_set_split_target(int blocks) { g_split_target = blocks; }
 
-// A/B knob: 8 (the 8-wave ping-pong kernel), 4 (the 4-wave AGPR-accumulator kernel, a barrier per phase) or 5 (the
-// same with one barrier per two phases); returns the previous value
+// A/B knob: 8 (the 8-wave ping-pong kernel) or 4 + bits (the 4-wave AGPR-accumulator kernel; bit 0: one barrier per
+// two phases instead of one per phase, bit 1: fragment reads and DMAs interleaved with the MFMAs); returns the
+// previous value
 PLX_API int plx_gemm256_set_waves(int waves) {
-  const int prev = g_waves == 4 && g_pair ? 5 : g_waves;
-  if (waves == 4 || waves == 8) g_waves = waves, g_pair = 0;
-  if (waves == 5) g_waves = 4, g_pair = 1;
+  const int prev = g_waves == 4 ? 4 + g_w4 : g_waves;
+  if (waves == 8) g_waves = 8;
+  if (waves >= 4 && waves <= 7) g_waves = 4, g_w4 = waves - 4;
   return prev;
 }
 
