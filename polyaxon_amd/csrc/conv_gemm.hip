@@ -15,6 +15,8 @@
 // of M and the taps of a convolution that fall outside the image get an out-of-range offset and read zeros, so
 // partial tiles and padding need no branches around the DMA; the TN GEMM reads a zero page instead.
 #include <hip/hip_runtime.h>
+
+#include <utility>
 #include <stdint.h>
 
 namespace {
@@ -127,10 +129,35 @@ __device__ __forceinline__ size_t out_row(const ConvGeom& g, int m) {
 }
 constexpr int NTHREADS = 256;   // 4 waves
 
+// vmcnt(n) with a run-time n in [0, 4 * step] in multiples of `step` (the counter is an instruction immediate)
+template <int STEP>
+__device__ __forceinline__ void wait_vm_stages(int stages) {
+    if (stages >= 4 && 4 * STEP <= 63) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * STEP < 63 ? 4 * STEP : 63) : "memory");
+    else if (stages >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * STEP) : "memory");
+    else if (stages == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * STEP) : "memory");
+    else if (stages == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int V>
 struct IC {
     static constexpr int value = V;
 };
+
+// MFMA with the accumulator pinned to an AGPR tuple ("+a"): with the builtin, hipcc moved the software-pipelined
+// kernel's accumulators between AGPRs around every MFMA (phi copies of the two-phase loop).  The compiler does not
+// see an MFMA here, so the consumer of the accumulators runs after mfma_drain() (XDL write -> read: <= 18 wait
+// states) and the first MFMA after their zero-initialisation is far behind it (prologue DMAs, waits, barriers).
+__device__ __forceinline__ void mfma_agpr(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
+
+// f(IC<0>{}), f(IC<1>{}), ... in order (compile-time indices for unrolled schedules)
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for(F& f, std::integer_sequence<int, Is...>) {
+    (f(IC<Is>{}), ...);
+}
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     // consecutive logical ids on one XCD (blocks are dealt round-robin over the 8 XCDs); bijective for any nwg
@@ -190,10 +217,11 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     // relu(a * scale[k] + bias[k]) between the LDS read and the MFMA (scale / bias = bnr.mean / bnr.invstd in this
     // forward-only mode).  Prototype of the BN-apply prologue fusion (plx_gemm_nt_prologue).
     constexpr bool CONV = MODE == 1 || MODE == 3, STEM = MODE == 2, HALO = MODE == 3, PRO = MODE == 4;
-    constexpr bool PIPE = NBUF == 3;
+    constexpr bool PIPE = NBUF == 3, SWP = NBUF >= 4;
     constexpr int NW = NTH / 64;                           // waves
     static_assert(WGM * WGN == NW, "one wave per wave tile");
     static_assert(!PIPE || (NTH == 512 && !HALO && !PRO && !STEM), "the ring schedule is the 8-wave dense/conv kernel");
+    static_assert(!SWP || (NTH == 256 && !HALO && !PRO && !STEM), "the software-pipelined schedule is dense/conv");
     static_assert(PIPE || NTH == 256, "the lock-step kernels are 4 waves");
     constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
     constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
@@ -474,6 +502,121 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
             if (kt + 2 < nk) tile(IC<2>{}, kt + 2);
         }
         if (grp == 0) __builtin_amdgcn_s_barrier();        // every wave executes the same number of barriers
+    } else if constexpr (SWP) {
+        // ---- software-pipelined schedule: one block per CU (one wave per SIMD) over an NST-stage LDS ring (tile j in
+        // slot j % NST).  Phase kt runs tile kt's MFMAs from registers and, one per MFMA, issues the ds_reads of tile
+        // kt + 1's fragments (into the other register set) and the DMAs of tile kt + NST into tile kt's slot (its
+        // fragments were read in phase kt - 1 and retired before that phase's barrier: WAR).  The phase ends with
+        // lgkmcnt(0), a counted vmcnt that retires tile kt + 2 (read in the next phase: RAW) and one barrier, so
+        // NST - 2 tiles of DMAs stay in flight across it and the MFMA pipe never waits on a whole-stage drain.
+        constexpr int NST = NBUF, INFL = AI + BI, NFR = 2 * (RN + RM), NMF = 2 * RN * RM;
+        static_assert(NFR + INFL <= NMF, "one fragment read or DMA per MFMA");
+        static_assert(NST <= 5 && INFL * (NST - 1) <= 63, "vmcnt immediates");
+        const int nk = K / BK;
+        // loop bounds as opaque SGPRs (no kernel-argument reload inside the loop)
+        int cdim = CONV ? geo.C : K, ntaps = geo.ntaps;
+        asm volatile("" : "+s"(cdim), "+s"(ntaps));
+        int st = 0, sc = 0, kis = 0;                        // (tap, channel offset, k) of the next tile to issue
+        const bool tap_inner = CONV && geo.tap_inner;
+        auto advance = [&]() {                              // selects, no branches (see the ring schedule)
+            kis += BK;
+            const bool wt = st + 1 == ntaps, wc = sc + BK == cdim;
+            const int st_i = wt ? 0 : st + 1, sc_i = wt ? sc + BK : sc;
+            const int st_m = wc ? st + 1 : st, sc_m = wc ? 0 : sc + BK;
+            st = tap_inner ? st_i : st_m;
+            sc = tap_inner ? sc_i : sc_m;
+        };
+        struct Frags {
+            bf16x8 a[2][RN];                                // MFMA A operand = B rows (output channel n), per kk
+            bf16x8 b[2][RM];                                // MFMA B operand = A rows (pixel m)
+        };
+        auto read_frag = [&](Frags& f, const char* As, auto ic) {
+            constexpr int I = decltype(ic)::value, KK = I / (RN + RM), J = I % (RN + RM);
+            if constexpr (J < RN) {
+                const int row = wn * WTN + J * 16 + fr;
+                f.a[KK][J] = *(const bf16x8*)(As + A_BYTES + row * 128 + (((KK * 4 + fq) ^ nt_swz(row)) * 16));
+            } else {
+                const int row = wm * WTM + (J - RN) * 16 + fr;
+                f.b[KK][J - RN] = *(const bf16x8*)(As + row * 128 + (((KK * 4 + fq) ^ nt_swz(row)) * 16));
+            }
+        };
+        // DMA arguments of the next tile to issue (kis, st, sc), then one of its AI + BI per-wave DMAs
+        auto dma_args = [&](int& a_add, int& bit, int& bk0) {
+            a_add = kis * 2;
+            bit = 0;
+            if constexpr (CONV) {
+                a_add = pick9(geo.tap_a, st) + sc * 2;
+                bit = st;
+            }
+            bk0 = CONV ? pick9(geo.tap_b, st) + sc * 2 : kis * 2;
+        };
+        // The tap lookup is a scalar load from the kernel arguments, and its wait (lgkmcnt) would also retire every
+        // fragment read in flight: the next tile's DMA arguments are therefore computed at the end of the previous
+        // phase (after its lgkmcnt(0)) and pinned there.
+        int na = 0, nbit = 0, nbk = 0;
+        auto next_args = [&]() {
+            dma_args(na, nbit, nbk);
+            asm volatile("" : "+v"(na), "+s"(nbit), "+s"(nbk));
+        };
+        auto dma_piece = [&](char* base, int a_add, int bit, int bk0, auto ic) {
+            constexpr int P = decltype(ic)::value;
+            if constexpr (P < AI) {
+                const uint32_t off = (a_ok[P] >> bit) & 1u ? (uint32_t)(a_off[P] + a_add) : OOB;
+                blds16(ra, off, base + (P * NW + wave) * 1024);
+            } else {
+                constexpr int Q = P - AI;
+                blds16(rb, (uint32_t)(b_off[Q] + bk0), base + A_BYTES + (Q * NW + wave) * 1024);
+            }
+        };
+        auto dma_tile = [&](char* base) {
+            int a_add, bit, bk0;
+            dma_args(a_add, bit, bk0);
+            auto one = [&](auto ic) { dma_piece(base, a_add, bit, bk0, ic); };
+            static_for(one, std::make_integer_sequence<int, INFL>{});
+            advance();
+        };
+        auto phase = [&](const Frags& fc, Frags& fn, int kt) {
+            const char* rimg = smem + ((kt + 1) % NST) * STAGE;  // past the last tile: stale reads into a dead set
+            char* dimg = smem + (kt % NST) * STAGE;
+            const bool dma = kt + NST < nk;                 // uniform
+            const int a_add = na, bit = nbit, bk0 = nbk;
+            auto step = [&](auto ic) {
+                constexpr int I = decltype(ic)::value, KK = I / (RN * RM), X = (I / RM) % RN, Y = I % RM;
+                mfma_agpr(acc[X][Y], fc.a[KK][X], fc.b[KK][Y]);
+                if constexpr (I < NFR) {
+                    read_frag(fn, rimg, IC<I>{});
+                } else if constexpr (I < NFR + INFL) {
+                    if (dma) dma_piece(dimg, a_add, bit, bk0, IC<I - NFR>{});
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            };
+            static_for(step, std::make_integer_sequence<int, NMF>{});
+            if (dma) advance();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            next_args();
+            wait_vm_stages<INFL>(min(kt + NST, nk - 1) - (kt + 2));
+            __builtin_amdgcn_s_barrier();
+        };
+        // prologue: tiles 0 .. min(NST, nk) - 1; tile 0's fragments; tile 1 landed before the first phase
+#pragma unroll
+        for (int j = 0; j < NST; ++j)
+            if (j < nk) dma_tile(smem + j * STAGE);
+        wait_vm_stages<INFL>(min(NST, nk) - 1);
+        __builtin_amdgcn_s_barrier();
+        Frags f0, f1;
+        {
+            auto rd = [&](auto ic) { read_frag(f0, smem, ic); };
+            static_for(rd, std::make_integer_sequence<int, NFR>{});
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        next_args();
+        wait_vm_stages<INFL>(min(NST, nk) - 2);
+        __builtin_amdgcn_s_barrier();
+        for (int kt = 0; kt < nk; kt += 2) {
+            phase(f0, f1, kt);
+            if (kt + 1 < nk) phase(f1, f0, kt + 1);
+        }
+        mfma_drain();
     } else {
     const int nk = K / BK;
     const int cdim = CONV ? geo.C : K;                      // channels per tap
@@ -784,14 +927,6 @@ __device__ __forceinline__ void stage_rows(char* img, __amdgpu_buffer_rsrc_t rsr
     }
 }
 
-// vmcnt(n) with a run-time n in [0, 3 * step] in multiples of `step` (the counter is an instruction immediate)
-template <int STEP>
-__device__ __forceinline__ void wait_vm_stages(int stages) {
-    if (stages >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * STEP) : "memory");
-    else if (stages == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * STEP) : "memory");
-    else if (stages == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEP) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
 
 // CONV: 0 dense, 1 3x3 gather (tap per N2 tile), 2 the stem's super-pixel window (plx_stem_conv_wgrad)
 // NST: K-stages in the LDS ring.  2 = double buffering (stage k+1 in flight while k computes, vmcnt(0) + barrier
@@ -979,12 +1114,12 @@ template <int BM, int BN, int WGM, int WGN, int CONV = 0, int NBUF = 2>
 int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
               const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}, const void* D = nullptr,
               int ldd = 0, BnBwd bnr = {}, const uint8_t* dmask = nullptr) {
-    constexpr int NTH = NBUF == 3 ? 512 : NTHREADS;         // NBUF 3: the 8-wave ring kernel
+    constexpr int NTH = NBUF == 3 ? 512 : NTHREADS;         // NBUF 3: the 8-wave ring kernel; 4-5: software pipeline
     constexpr int TILE = BM * (BN * 2 + 16), RED = NTH * 17 * 4;
     constexpr int EPI = TILE > RED ? TILE : RED;            // the reduction reuses the tile's LDS
     constexpr int KLOOP = NBUF * (BM + BN) * BK * 2;
     constexpr int LDS = KLOOP > EPI ? KLOOP : EPI;
-    static_assert(NBUF >= 1 && NBUF <= 3, "one or two K stages, or the 3-stage ring");
+    static_assert(NBUF >= 1 && NBUF <= 5, "one or two K stages, the 3-stage ring, or the 4-5 stage pipeline");
     static_assert(NBUF == 1 || EPI <= KLOOP, "epilogue staging must fit the k-loop LDS");
     static_assert(LDS <= 160 * 1024, "LDS");
     constexpr int PER_CU = (160 * 1024) / LDS;
@@ -992,7 +1127,7 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
     // keeps its accumulators live through the epilogue prefetch (~178 VGPRs), the single-buffer one parks them in
     // LDS first (LATE in gemm_nt_kernel)
     constexpr int CAP = CONV != 0 && BN == 64 ? 3 : 4;     // the 256x64 conv staging spills 7-8 VGPRs at 4
-    constexpr int MIN_F = NBUF == 1 ? (PER_CU < CAP ? PER_CU : CAP) : NBUF == 3 ? 1 : 2, MIN_B = MIN_F;
+    constexpr int MIN_F = NBUF == 1 ? (PER_CU < CAP ? PER_CU : CAP) : NBUF >= 3 ? 1 : 2, MIN_B = MIN_F;
     auto kf = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_F, NBUF, false, NTH>;
     auto kb = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_B, NBUF, true, NTH>;
     static int attr = set_lds(kf, LDS) | set_lds(kb, LDS);
@@ -1041,6 +1176,10 @@ int g_tap_inner = 1;
 
 // the 8-wave ring kernel (NBUF 3, 256 x 128 tiles) for convolutions with N % 128 == 0 (A/B knob plx_set_conv_v2)
 int g_conv_v2 = 0;
+
+// the software-pipelined 4-wave kernel (NBUF 4-5 = LDS ring stages, one block per CU) for the implicit-GEMM
+// convolutions and for the dense (1x1) GEMMs: 0 off, else the stage count (A/B knob plx_set_swp)
+int g_conv_swp = 0, g_dense_swp = 0;
 
 inline bool halo_ok(const ConvGeom& g) {
     if (!g_halo || g.ntaps != 9 || g.S != 1 || g.OS != 0 || g.Hr != g.H || g.Wr != g.W || g.C % BK) return false;
@@ -1209,6 +1348,13 @@ int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int 
     const bool bwd = D != nullptr || bnr != nullptr;
     if (nt_tall(bwd, M, N, K))
         return launch_nt<256, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
+    if (g_dense_swp && K > BK) {
+        if (N % 128)
+            return launch_nt<256, 64, 4, 1, false, 4>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
+        return g_dense_swp >= 5
+                   ? launch_nt<128, 128, 2, 2, false, 5>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask)
+                   : launch_nt<128, 128, 2, 2, false, 4>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
+    }
     if (N % 128 == 0) {
         const bool one = nt_single(bwd, false, K, ((M + 127) / 128) * (N / 128));
         return one ? launch_nt<128, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b,
@@ -1253,6 +1399,11 @@ void plx_set_tap_inner(int on) { g_tap_inner = on ? 1 : 0; }
 
 // A/B knob: the 8-wave ring kernel for the convolutions with N % 128 == 0 (1) or the 4-wave kernels (0)
 void plx_set_conv_v2(int on) { g_conv_v2 = on ? 1 : 0; }
+// software-pipelined NT kernels: LDS ring stages (0 = off, 4 or 5) for the convolutions and the dense GEMMs
+void plx_set_swp(int conv_stages, int dense_stages) {
+    g_conv_swp = conv_stages <= 0 ? 0 : conv_stages >= 5 ? 5 : 4;
+    g_dense_swp = dense_stages <= 0 ? 0 : dense_stages >= 5 ? 5 : 4;
+}
 
 // A/B knob: 256 x 128 NT tiles (0 off, 1 forward, 2 forward + data gradient), see nt_tall
 void plx_set_nt_tall(int mode, int min_k) {
@@ -1435,6 +1586,11 @@ int nt_conv_any(const void* A, const void* B, void* C, int M, int N, const ConvG
         return launch_halo<256, 64, 4, 1, 2>(A, B, C, M, N, g.C, ldb, ldc, zero, stats, s, g, D, ldd, bnr);
     }
     if (g_conv_v2 && N % 128 == 0) return nt_conv<256, 128, 4, 2, 3>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
+    if (g_conv_swp) {
+        if (N % 128) return nt_conv<256, 64, 4, 1, 4>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
+        return g_conv_swp >= 5 ? nt_conv<128, 128, 2, 2, 5>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr)
+                               : nt_conv<128, 128, 2, 2, 4>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
+    }
     if (nt_tall(bwd, M, N, K)) return nt_conv<256, 128, 2, 2, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
     if (N % 128 == 0)
         return nt_single(bwd, true, K, ((M + 127) / 128) * (N / 128))

@@ -178,6 +178,9 @@ def lib(name: str) -> ctypes.CDLL:
             handle.plx_set_tap_inner(int(os.environ["PLX_TAP_INNER"]))
         if name == "plx_conv" and os.environ.get("PLX_CONV_V2"):  # A/B knob: 8-wave ring conv kernel
             handle.plx_set_conv_v2(int(os.environ["PLX_CONV_V2"]))
+        if name == "plx_conv" and os.environ.get("PLX_SWP"):  # A/B knob: "conv,dense" software-pipelined stages
+            cs, ds = (int(v) for v in (os.environ["PLX_SWP"] + ",0").split(",")[:2])
+            handle.plx_set_swp(cs, ds)
         if name == "plx_conv" and os.environ.get("PLX_TN_STAGES"):  # A/B knob: weight-gradient LDS ring depth
             st, _, bk = os.environ["PLX_TN_STAGES"].partition(",")  # "stages[,rows per stage]"
             handle.plx_set_tn_stages(int(st), int(bk or 0))
@@ -281,6 +284,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_set_halo": [_I],
         "plx_set_tap_inner": [_I],
         "plx_set_conv_v2": [_I],
+        "plx_set_swp": [_I, _I],
         "plx_set_tn_stages": [_I, _I],
         "plx_set_tn_wide": [_I],
         "plx_set_nt_tall": [_I, _I],
@@ -368,7 +372,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_partial_colsum_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_set_tap_inner": None, "plx_set_conv_v2": None, "plx_set_stem_bwd_cap": None, "plx_set_bn_fin_threads": None, "plx_set_ln_wave": None, "plx_set_adamw_grid_cap": None, "plx_set_adamw_wide": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_partial_colsum_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_set_tap_inner": None, "plx_set_conv_v2": None, "plx_set_swp": None, "plx_set_stem_bwd_cap": None, "plx_set_bn_fin_threads": None, "plx_set_ln_wave": None, "plx_set_adamw_grid_cap": None, "plx_set_adamw_wide": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

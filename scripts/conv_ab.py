@@ -34,6 +34,9 @@ VARIANTS = {
     "tap_inner": {"plx_set_tap_inner": 1, "plx_set_conv_v2": 0},
     "v2": {"plx_set_tap_inner": 0, "plx_set_conv_v2": 1},
     "v2_tap_inner": {"plx_set_tap_inner": 1, "plx_set_conv_v2": 1},
+    "swp4": {"plx_set_tap_inner": 1, "plx_set_conv_v2": 0, "plx_set_swp": (4, 4)},
+    "swp5": {"plx_set_tap_inner": 1, "plx_set_conv_v2": 0, "plx_set_swp": (5, 5)},
+    "ti": {"plx_set_tap_inner": 1, "plx_set_conv_v2": 0, "plx_set_swp": (0, 0)},
 }
 
 
@@ -69,7 +72,7 @@ def main():
     def apply(v):
         cur["lib"] = libs[v]
         for fn, val in VARIANTS[v].items():
-            getattr(lib, fn)(val)
+            getattr(lib, fn)(*(val if isinstance(val, tuple) else (val,)))
 
     torch.manual_seed(0)
     for n, ci, co, h, s in shapes:
