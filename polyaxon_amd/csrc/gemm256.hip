@@ -664,10 +664,12 @@ int g_waves = 8;  // 8: the ping-pong kernel, 4: gemm256w4_kernel (plx_gemm256_s
 int g_w4 = 0;     // 4-wave kernel schedule bits: 1 = one barrier per two phases, 2 = reads / DMAs interleaved
                   // with the MFMAs (plx_gemm256_set_waves(4 + bits))
 
+// variant: 8 = the ping-pong kernel, 4 + bits = the 4-wave kernel (see plx_gemm256_set_waves), 0 = the global knob
 template <bool AK, bool BKM, bool ACC, bool SLAB>
-int launch(const Gemm256Args& a, int splits, hipStream_t st) {
+int launch(const Gemm256Args& a, int splits, hipStream_t st, int variant) {
   const dim3 grid((a.M / BM) * (a.N / BN), splits);
-  if (g_waves == 4) {
+  const int v = variant >= 4 && variant <= 8 ? variant : (g_waves == 4 ? 4 + g_w4 : 8);
+  if (v < 8) {
     void (*ks[4])(Gemm256Args) = {gemm256w4_kernel<AK, BKM, ACC, SLAB, false, false>,
                                    gemm256w4_kernel<AK, BKM, ACC, SLAB, true, false>,
                                    gemm256w4_kernel<AK, BKM, ACC, SLAB, false, true>,
@@ -679,7 +681,7 @@ int launch(const Gemm256Args& a, int splits, hipStream_t st) {
       return 0;
     }();
     if (attr) return attr;
-    hipLaunchKernelGGL(ks[g_w4 & 3], grid, dim3(NTH4), LDS_BYTES, st, a);
+    hipLaunchKernelGGL(ks[(v - 4) & 3], grid, dim3(NTH4), LDS_BYTES, st, a);
     return 0;
   }
   auto k = gemm256_kernel<AK, BKM, ACC, SLAB>;
@@ -691,9 +693,9 @@ int launch(const Gemm256Args& a, int splits, hipStream_t st) {
 }
 
 template <bool AK, bool BKM>
-int dispatch(const Gemm256Args& a, int splits, int accumulate, hipStream_t st) {
-  if (splits > 1) return launch<AK, BKM, false, true>(a, splits, st);
-  return accumulate ? launch<AK, BKM, true, false>(a, 1, st) : launch<AK, BKM, false, false>(a, 1, st);
+int dispatch(const Gemm256Args& a, int splits, int accumulate, hipStream_t st, int variant) {
+  if (splits > 1) return launch<AK, BKM, false, true>(a, splits, st, variant);
+  return accumulate ? launch<AK, BKM, true, false>(a, 1, st, variant) : launch<AK, BKM, false, false>(a, 1, st, variant);
 }
 
 int g_split_target = 256;  // blocks the split-K planner aims for (one per CU: splitting a grid that already
@@ -735,9 +737,10 @@ PLX_API int plx_gemm256_set_waves(int waves) {
 // ws: fp32 workspace of plx_gemm256_splits(M, N, K) * M * N floats when that is > 1 (may be null otherwise).
 // Returns 0, or < 0 on a shape / layout the kernel does not take (nothing launched).
 // gelu_out: bf16 [M][ldc] (same layout as C, 16-byte aligned) receiving gelu_tanh(C), or null (not with accumulate).
-PLX_API int plx_gemm256_ex(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb,
-                           int ldc, int a_kmajor, int b_kmajor, float alpha, int accumulate, const float* bias,
-                           void* gelu_out, void* stream) {
+// variant: the kernel schedule for this call (8, or 4..7: see plx_gemm256_set_waves; 0 = the global knob)
+PLX_API int plx_gemm256_exv(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb,
+                            int ldc, int a_kmajor, int b_kmajor, float alpha, int accumulate, const float* bias,
+                            void* gelu_out, int variant, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return -1;
   if (bias != nullptr && (accumulate || (uintptr_t)bias % 16)) return -1;
   if (gelu_out != nullptr && (accumulate || (uintptr_t)gelu_out % 16)) return -1;
@@ -753,10 +756,10 @@ PLX_API int plx_gemm256_ex(const void* A, const void* B, void* C, void* ws, int 
                 splits > 1 ? nullptr : gelu_out};
   hipStream_t st = (hipStream_t)stream;
   int rc;
-  if (a_kmajor && b_kmajor) rc = dispatch<true, true>(a, splits, accumulate, st);
-  else if (a_kmajor) rc = dispatch<true, false>(a, splits, accumulate, st);
-  else if (b_kmajor) rc = dispatch<false, true>(a, splits, accumulate, st);
-  else rc = dispatch<false, false>(a, splits, accumulate, st);
+  if (a_kmajor && b_kmajor) rc = dispatch<true, true>(a, splits, accumulate, st, variant);
+  else if (a_kmajor) rc = dispatch<true, false>(a, splits, accumulate, st, variant);
+  else if (b_kmajor) rc = dispatch<false, true>(a, splits, accumulate, st, variant);
+  else rc = dispatch<false, false>(a, splits, accumulate, st, variant);
   if (rc) return rc;
   if (splits > 1) {
     const size_t total8 = (size_t)M * N / 8;
@@ -769,6 +772,13 @@ PLX_API int plx_gemm256_ex(const void* A, const void* B, void* C, void* ws, int 
                          splits, alpha, bias, (__bf16*)gelu_out);
   }
   return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+PLX_API int plx_gemm256_ex(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb,
+                           int ldc, int a_kmajor, int b_kmajor, float alpha, int accumulate, const float* bias,
+                           void* gelu_out, void* stream) {
+  return plx_gemm256_exv(A, B, C, ws, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor, alpha, accumulate, bias, gelu_out, 0,
+                         stream);
 }
 
 PLX_API int plx_gemm256_bias(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb,

@@ -319,6 +319,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gemm256": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P],
         "plx_gemm256_bias": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P],
         "plx_gemm256_ex": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P, _P],
+        "plx_gemm256_exv": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P, _I, _P],
         "plx_gemm256_splits": [_I, _I, _I],
         "plx_gemm256_set_split_target": [_I],
         "plx_gemm256_set_waves": [_I],

@@ -11,14 +11,16 @@ The weight gradient can be written straight into a flat gradient slot (``out=``,
 epilogue adds to the bf16 slot in place, so a weight used twice needs no separate gradient tensor.
 
 Shapes the kernel does not take (a dimension not a multiple of 256, or K of 64) go to ``torch`` (hipBLASLt) —
-:func:`supported` says which; on a GPU box a missing library raises instead of falling back (ops/_native.py).
+:func:`supported` says which; on a GPU box a missing library raises instead of falling back (ops/_native.py).  The
+LM trainers' shapes all fit (GPT-2's vocabulary is padded to 50432 rows, models/transformer.py).
 
-Dispatch (``PLX_LM_GEMM``): ``1`` always the MFMA kernel, ``0`` always hipBLASLt, ``auto`` (default) takes the
-measured decision table ``TABLE`` for the GPT-2 125M / Llama-3 8B shapes (profiles/r3_lm_gemm.md: the kernel wins the
-narrow weight gradients, split-K 1.1-1.4x, and trails hipBLASLt by 10-25 % on the large forward / data-gradient
-shapes), so runs are reproducible and every DP rank runs the same kernel; any other shape is timed once on first use
-(both, 3 calls each) and, under torch.distributed, rank 0's choice is broadcast so the ranks agree.
-``PLX_LM_GEMM_TABLE=0`` times every shape.  :func:`decisions` lists what was chosen.
+Every supported shape runs the kernel: round 4 measured it at 0.98-1.08x hipBLASLt on the large GPT-2 125M / Llama-3
+8B linears and 1.3-2.0x on the split-K weight gradients, 4.8 % less total time over the 24 shapes
+(profiles/r4_lm_gemm.md).  ``SCHEDULE`` holds the kernel schedule measured fastest per shape (8 = the 8-wave
+ping-pong kernel, 4-7 = the 4-wave AGPR kernel's variants, csrc/gemm256.hip ``plx_gemm256_set_waves``); other shapes
+take ``PLX_GEMM_WAVES`` (default 8).  The choice is a pure function of the shape, so runs are reproducible and every
+DP rank runs the same kernel.  ``PLX_LM_GEMM=0`` routes the linears to hipBLASLt for A/B measurements only;
+:func:`decisions` lists the shapes seen and their schedule.
 """
 from __future__ import annotations
 
@@ -32,32 +34,28 @@ from polyaxon_amd.ops import _native
 TILE = 256
 _ws: Dict[Tuple[str, int], torch.Tensor] = {}
 
+_seen: Dict[Tuple[int, int, int, bool, bool], int] = {}
 
-_choice: Dict[Tuple[int, int, int, bool, bool], Tuple[bool, float, float]] = {}
-
-# (M, N, K, A K-major, B K-major) -> the MFMA kernel is the faster one, from profiles/r3_lm_gemm.md (ping-pong kernel
-# vs hipBLASLt, one MI355X): GPT-2 125M at 16 x 1024 tokens and Llama-3 8B at 1 x 4096 tokens
-TABLE: Dict[Tuple[int, int, int, bool, bool], bool] = {}
-for _M, _N, _K, _win in (
-        # GPT-2: (qkv, proj, up, down) x (fwd, dgrad, wgrad)
-        (16384, 2304, 768, False), (16384, 768, 2304, False), (2304, 768, 16384, True),
-        (16384, 768, 768, False), (768, 768, 16384, True),
-        (16384, 3072, 768, False), (16384, 768, 3072, False), (3072, 768, 16384, True),
-        (768, 3072, 16384, True),
-        # Llama-3 8B
-        (4096, 6144, 4096, False), (4096, 4096, 6144, False), (6144, 4096, 4096, False),
-        (4096, 4096, 4096, False), (4096, 28672, 4096, False), (4096, 4096, 28672, False),
-        (28672, 4096, 4096, False), (4096, 4096, 14336, False), (4096, 14336, 4096, False),
-        (14336, 4096, 4096, False)):
-    # the shapes are listed by (M, N, K); the pass fixes the layout: fwd (K, K), dgrad (K, MN), wgrad (MN, MN)
-    for _ak, _bk in ((True, True), (True, False), (False, False)):
-        TABLE.setdefault((_M, _N, _K, _ak, _bk), _win)
-# the GPT-2 proj fwd / dgrad share 16384x768x768: hipBLASLt for both
+# (M, N, K, A K-major, B K-major) -> kernel schedule, the fastest of the five in-process on one MI355X
+# (scripts/gemm_bench.py --waves 8,4,5,6,7; profiles/r4_lm_gemm.md).  fwd = (K, K), dgrad = (K, MN), wgrad = (MN, MN)
+_FWD, _DGRAD, _WGRAD = (True, True), (True, False), (False, False)
+SCHEDULE: Dict[Tuple[int, int, int, bool, bool], int] = {
+    (M, N, K) + lay: v for (M, N, K, lay, v) in (
+        # GPT-2 125M, 16 x 1024 tokens
+        (16384, 2304, 768, _FWD, 7), (16384, 768, 2304, _DGRAD, 7), (2304, 768, 16384, _WGRAD, 5),
+        (16384, 768, 768, _FWD, 7), (16384, 768, 768, _DGRAD, 7), (768, 768, 16384, _WGRAD, 5),
+        (16384, 3072, 768, _FWD, 7), (16384, 768, 3072, _DGRAD, 7), (3072, 768, 16384, _WGRAD, 5),
+        (16384, 768, 3072, _FWD, 8), (16384, 3072, 768, _DGRAD, 7), (768, 3072, 16384, _WGRAD, 5),
+        # Llama-3 8B, 1 x 4096 tokens
+        (4096, 6144, 4096, _FWD, 7), (4096, 4096, 6144, _DGRAD, 8), (6144, 4096, 4096, _WGRAD, 7),
+        (4096, 4096, 4096, _FWD, 7), (4096, 4096, 4096, _DGRAD, 7), (4096, 4096, 4096, _WGRAD, 5),
+        (4096, 28672, 4096, _FWD, 6), (4096, 4096, 28672, _DGRAD, 4), (28672, 4096, 4096, _WGRAD, 7),
+        (4096, 4096, 14336, _FWD, 8), (4096, 14336, 4096, _DGRAD, 8), (4096, 14336, 4096, _WGRAD, 5))}
 
 
 def mode() -> str:
-    m = os.environ.get("PLX_LM_GEMM", "auto")
-    return m if m in ("0", "1", "auto") else "auto"
+    m = os.environ.get("PLX_LM_GEMM", "1")
+    return "0" if m == "0" else "1"
 
 
 def enabled() -> bool:
@@ -65,10 +63,15 @@ def enabled() -> bool:
     return mode() != "0"
 
 
+def schedule(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> int:
+    """The kernel schedule for a shape: the measured table, else 0 (the library's global knob, PLX_GEMM_WAVES)."""
+    return SCHEDULE.get((M, N, K, bool(a_kmajor), bool(b_kmajor)), 0)
+
+
 def decisions() -> Dict[str, Dict[str, object]]:
-    """Per shape measured by ``auto``: which GEMM runs and both times (ms)."""
-    return {f"{M}x{N}x{K}:{'K' if ak else 'M'}{'K' if bk else 'N'}": {"native": nat, "native_ms": tn, "torch_ms": tt}
-            for (M, N, K, ak, bk), (nat, tn, tt) in _choice.items()}
+    """Shapes this process ran on the kernel and their schedule (0 = the library default)."""
+    return {f"{M}x{N}x{K}:{'K' if ak else 'M'}{'K' if bk else 'N'}": {"native": True, "schedule": v}
+            for (M, N, K, ak, bk), v in _seen.items()}
 
 
 def _torch_gemm(a, b, M, N, K, a_kmajor, b_kmajor, out=None, accumulate=False, alpha=1.0):
@@ -85,41 +88,9 @@ def _torch_gemm(a, b, M, N, K, a_kmajor, b_kmajor, out=None, accumulate=False, a
     return out
 
 
-def _use_native(a, b, M, N, K, a_kmajor, b_kmajor) -> bool:
-    m = mode()
-    if m != "auto":
-        return m == "1"
-    key = (M, N, K, bool(a_kmajor), bool(b_kmajor))
-    hit = _choice.get(key)
-    if hit is None and key in TABLE and os.environ.get("PLX_LM_GEMM_TABLE", "1") != "0":
-        hit = _choice[key] = (TABLE[key], float("nan"), float("nan"))
-    if hit is None:
-        ts = []
-        for native in (True, False):
-            fn = (lambda: gemm(a, b, M, N, K, a_kmajor, b_kmajor)) if native else (
-                lambda: _torch_gemm(a, b, M, N, K, a_kmajor, b_kmajor))
-            fn()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(3):
-                fn()
-            e1.record()
-            e1.synchronize()
-            ts.append(e0.elapsed_time(e1) / 3)
-        native = ts[0] <= ts[1]
-        import torch.distributed as dist
-
-        if dist.is_initialized() and dist.get_world_size() > 1:  # every rank runs rank 0's choice
-            flag = torch.tensor([1 if native else 0], dtype=torch.int32, device=a.device)
-            dist.broadcast(flag, src=0)
-            native = bool(int(flag.item()))
-        hit = _choice[key] = (native, round(ts[0], 4), round(ts[1], 4))
-    return hit[0]
-
-
 def matmul(a, b, M, N, K, a_kmajor, b_kmajor, out=None, accumulate=False) -> torch.Tensor:
-    """:func:`gemm` semantics on whichever of the MFMA kernel / hipBLASLt the dispatch mode picks."""
-    if _use_native(a, b, M, N, K, a_kmajor, b_kmajor):
+    """:func:`gemm` semantics: the MFMA kernel for every supported shape (hipBLASLt only with PLX_LM_GEMM=0)."""
+    if enabled() and a.is_cuda and supported(M, N, K):
         return gemm(a, b, M, N, K, a_kmajor, b_kmajor, out=out, accumulate=accumulate)
     return _torch_gemm(a, b, M, N, K, a_kmajor, b_kmajor, out=out, accumulate=accumulate)
 
@@ -171,10 +142,14 @@ def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: boo
     ws = _workspace(a.device, splits * M * N).data_ptr() if splits > 1 else None
     lda = K if a_kmajor else M
     ldb = K if b_kmajor else N
-    rc = lib.plx_gemm256_ex(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, M, N, K, lda, ldb, out.stride(0),
-                            int(a_kmajor), int(b_kmajor), float(alpha), int(accumulate),
-                            bias.data_ptr() if bias is not None else None,
-                            gelu_out.data_ptr() if gelu_out is not None else None, _native.current_stream())
+    key = (M, N, K, bool(a_kmajor), bool(b_kmajor))
+    v = _seen.get(key)
+    if v is None:
+        v = _seen[key] = schedule(*key)
+    rc = lib.plx_gemm256_exv(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, M, N, K, lda, ldb, out.stride(0),
+                             int(a_kmajor), int(b_kmajor), float(alpha), int(accumulate),
+                             bias.data_ptr() if bias is not None else None,
+                             gelu_out.data_ptr() if gelu_out is not None else None, v, _native.current_stream())
     if rc != 0:
         raise RuntimeError(f"plx_gemm256 failed ({rc}) for {M}x{N}x{K} a_kmajor={a_kmajor} b_kmajor={b_kmajor}")
     return out
@@ -194,7 +169,7 @@ def forward(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]
     N = weight.shape[0]
     if bias is None:
         return matmul(x2, weight, T, N, fin, True, True)
-    if _use_native(x2, weight, T, N, fin, True, True):
+    if enabled() and x2.is_cuda and supported(T, N, fin):
         return gemm(x2, weight, T, N, fin, True, True, bias=bias)
     return torch.addmm(bias.to(x2.dtype), x2, weight.t())
 
@@ -207,7 +182,7 @@ def forward_gelu(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Te
     epilogue (no separate pass reading h back); on hipBLASLt addmm then F.gelu."""
     T, fin = x2.shape
     N = weight.shape[0]
-    if _GELU_EPILOGUE and _use_native(x2, weight, T, N, fin, True, True):
+    if _GELU_EPILOGUE and enabled() and x2.is_cuda and supported(T, N, fin):
         h = torch.empty(T, N, dtype=torch.bfloat16, device=x2.device)
         a = torch.empty_like(h)
         gemm(x2, weight, T, N, fin, True, True, out=h, bias=bias, gelu_out=a)

@@ -49,9 +49,9 @@ def test_knob_modes(monkeypatch):
     monkeypatch.setenv("PLX_LM_GEMM", "1")
     assert gemm.enabled() and gemm.mode() == "1"
     monkeypatch.delenv("PLX_LM_GEMM")
-    assert gemm.mode() == "auto" and gemm.enabled()
-    monkeypatch.setenv("PLX_LM_GEMM", "bogus")
-    assert gemm.mode() == "auto"
+    assert gemm.mode() == "1" and gemm.enabled()   # the kernel is the default; hipBLASLt only as an A/B knob
+    monkeypatch.setenv("PLX_LM_GEMM", "auto")      # the retired timing mode now means the kernel
+    assert gemm.mode() == "1"
 
 
 def test_torch_path_layouts_match_reference():
@@ -70,19 +70,15 @@ def test_torch_path_layouts_match_reference():
             torch.testing.assert_close(out, ref + 1)
 
 
-def test_auto_mode_takes_the_measured_table_without_timing(monkeypatch):
-    """``auto`` decides the GPT-2 / Llama-3 8B shapes from the measured table (reproducible; every DP rank the same
-    kernel): the narrow GPT-2 weight gradients on the MFMA kernel, the large Llama shapes on hipBLASLt -- no timing
-    (and so no CUDA call) on the way."""
-    from polyaxon_amd.ops import gemm
-
-    monkeypatch.setenv("PLX_LM_GEMM", "auto")
-    monkeypatch.delenv("PLX_LM_GEMM_TABLE", raising=False)
-    gemm._choice.clear()
-    x = torch.empty(0)
-    assert gemm._use_native(x, x, 2304, 768, 16384, False, False) is True       # GPT-2 qkv wgrad (split-K)
-    assert gemm._use_native(x, x, 16384, 3072, 768, True, True) is False        # GPT-2 up fwd
-    assert gemm._use_native(x, x, 4096, 28672, 4096, True, True) is False       # Llama up fwd
-    d = gemm.decisions()
-    assert d["2304x768x16384:MN"]["native"] is True and len(d) == 3
-    gemm._choice.clear()
+def test_schedule_table_is_a_pure_function_of_the_shape():
+    """Every GPT-2 125M / Llama-3 8B linear has a measured kernel schedule (8 = ping-pong, 4-7 = the 4-wave AGPR
+    variants); other shapes get 0 (the library default).  No timing, no CUDA call: reproducible across runs and
+    identical on every DP rank."""
+    assert len(gemm.SCHEDULE) == 24 and set(gemm.SCHEDULE.values()) <= {4, 5, 6, 7, 8}
+    assert gemm.schedule(2304, 768, 16384, False, False) == 5      # GPT-2 qkv wgrad (split-K)
+    assert gemm.schedule(16384, 768, 3072, True, True) == 8        # GPT-2 down fwd
+    assert gemm.schedule(4096, 28672, 4096, True, True) == 6       # Llama up fwd
+    assert gemm.schedule(16384, 768, 768, True, True) != 0 and gemm.schedule(16384, 768, 768, True, False) != 0
+    assert gemm.schedule(512, 512, 512, True, True) == 0
+    for (M, N, K, ak, bk) in gemm.SCHEDULE:
+        assert gemm.supported(M, N, K)

@@ -226,21 +226,19 @@ def test_transformer_step_uses_mfma_linears(cuda, monkeypatch):
     assert torch.isfinite(x.grad.float()).all()
 
 
-def test_auto_dispatch_times_both_and_matches(cuda, monkeypatch):
-    """PLX_LM_GEMM=auto: the first call of a shape times the kernel and hipBLASLt, records the choice, and either
-    way the result matches fp32."""
+def test_per_shape_schedule_runs_and_matches(cuda, monkeypatch):
+    """The default dispatch runs every supported shape on the kernel with its measured schedule (a table shape gets
+    its variant through plx_gemm256_exv, others the library default) and matches fp32 either way."""
     from polyaxon_amd.ops import gemm
 
-    monkeypatch.setenv("PLX_LM_GEMM", "auto")
-    T, fin, fout = 1024, 768, 2304
-    x, w = _rand((T, fin), cuda, 17), _rand((fout, fin), cuda, 18)
-    y = gemm.forward(x, w)
-    dec = gemm.decisions()
-    assert f"{T}x{fout}x{fin}:KK" in dec
-    d = dec[f"{T}x{fout}x{fin}:KK"]
-    assert d["native_ms"] > 0 and d["torch_ms"] > 0
-    torch.cuda.synchronize()
-    _check(y, x.float() @ w.float().t(), fin)
+    monkeypatch.delenv("PLX_LM_GEMM", raising=False)
+    for T, fin, fout in ((16384, 768, 2304), (1024, 768, 2304)):
+        x, w = _rand((T, fin), cuda, 17), _rand((fout, fin), cuda, 18)
+        y = gemm.forward(x, w)
+        d = gemm.decisions()[f"{T}x{fout}x{fin}:KK"]
+        assert d["native"] and d["schedule"] == gemm.schedule(T, fout, fin, True, True)
+        torch.cuda.synchronize()
+        _check(y, x.float() @ w.float().t(), fin)
 
 
 def test_autocast_fp32_input_takes_mfma_path(cuda, monkeypatch):

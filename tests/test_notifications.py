@@ -2,6 +2,7 @@
 and e-mail, delivered asynchronously by the auditor, configured from PLX_NOTIFICATIONS. Local HTTP and SMTP
 servers stand in for the external services (reference tests patch safe_request / send_mass_template_mail)."""
 import json
+import time
 import socketserver
 import sys
 import threading
@@ -137,7 +138,11 @@ def test_notifications_from_env_config(tmp_path, monkeypatch):
         try:
             x = flow.submit({"version": 1, "kind": "experiment", "run": {"cmd": f"{sys.executable} -c 'pass'"}})
             assert flow.wait("experiment", x["id"], timeout=30) == "succeeded"
-            flow.auditor.flush()
+            # the scheduler records the event right after the status it waits on: flush until it has arrived
+            deadline = time.monotonic() + 10
+            while not got and time.monotonic() < deadline:
+                flow.auditor.flush()
+                time.sleep(0.05)
             assert [p for p, _ in got] == ["/hook"] and got[0][1]["subject"] == "experiment.succeeded"
         finally:
             flow.shutdown()
