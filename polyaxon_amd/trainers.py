@@ -184,6 +184,10 @@ def train_lm(argv=None) -> float:
                     help="model computes from fp32 weights under autocast (default on GPU: bf16 weights/grads with "
                          "an fp32 master copy in the optimizer)")
     ap.add_argument("--fixed_batch", action="store_true", help="reuse one synthetic batch every step")
+    ap.add_argument("--data", choices=["random", "copy"], default="random",
+                    help="synthetic tokens: uniform random (loss stays ln V), or the copy task of the resident GPT-2 "
+                         "program (ops/synth.py SyntheticTokens: learnable, hyper-parameter sensitive)")
+    ap.add_argument("--period", type=int, default=64, help="copy task: phrase length (seq must be a multiple)")
     ap.add_argument("--world1_collectives", action="store_true",
                     help="world 1 on the GPU: still create the nccl (RCCL) process group, run every gradient "
                          "bucket's all-reduce and the metric reducer's RCCL communicator (the DP path's overheads "
@@ -231,6 +235,16 @@ def train_lm(argv=None) -> float:
 
     def batch():  # synthetic tokens drawn on the device: a fresh batch per step costs one tiny kernel
         return torch.randint(0, cfg.vocab_size, (args.bs, seq), generator=g, device=dev)
+
+    if args.data == "copy":
+        from polyaxon_amd.ops.synth import SyntheticTokens
+
+        src = SyntheticTokens(args.bs, seq, cfg.vocab_size, dev, period=args.period,
+                              seed=args.seed + 1000 * info["rank"])
+
+        def batch():  # noqa: F811 -- the copy task, refilled in place on the device
+            src.next()
+            return src.x
 
     tokens = batch()
     xp = _tracker() if info["rank"] == 0 else None

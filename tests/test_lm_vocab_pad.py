@@ -43,3 +43,15 @@ def test_padded_vocab_is_the_same_function():
                 assert float(g[300:].abs().max()) == 0.0, n
                 g = g[:300]
             torch.testing.assert_close(g, gu[n].grad, rtol=1e-4, atol=1e-6, msg=n)
+
+
+def test_lm_trainer_copy_task_learns_on_cpu():
+    """``trainers lm --data copy`` (the copy-task stream of the resident GPT-2 program, used by the process-mode BO
+    comparison scripts/gpt2_bo_process.py): the loss falls below chance (ln V) within a few hundred steps."""
+    import math
+
+    from polyaxon_amd.trainers import train_lm
+
+    loss = train_lm(["--model", "tiny", "--cpu", "--bs", "8", "--seq", "64", "--period", "16", "--steps", "300",
+                     "--lr", "3e-3", "--data", "copy", "--log_every", "300"])
+    assert math.isfinite(loss) and loss < 0.97 * math.log(256), loss
