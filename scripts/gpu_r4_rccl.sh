@@ -9,6 +9,11 @@ mkdir -p gpurun_out
 AB_LIST="${AB_LIST:-PLX_BENCH_RCCL=early;;PLX_BENCH_RCCL=early GPU_MAX_HW_QUEUES=8;GPU_MAX_HW_QUEUES=8;PLX_BENCH_RCCL=early}" \
   TAG=r4rccl bash scripts/gpu_ab_multi.sh || exit 1
 if [ "${PROF:-1}" = "1" ]; then
+  PROF_TAG=r4rccl_base_resnet50_hb STEPS=2 bash scripts/prof_only.sh || exit 1
   PLX_BENCH_RCCL=early PROF_TAG=r4rccl_early_resnet50_hb STEPS=2 bash scripts/prof_only.sh || exit 1
-  head -20 gpurun_out/r4rccl_early_resnet50_hb_steady_state.md
+  head -16 gpurun_out/r4rccl_base_resnet50_hb_steady_state.md
+  head -16 gpurun_out/r4rccl_early_resnet50_hb_steady_state.md
+  python scripts/kernel_stats_diff.py gpurun_out/r4rccl_base_resnet50_hb_kernel_stats.csv \
+    gpurun_out/r4rccl_early_resnet50_hb_kernel_stats.csv > gpurun_out/r4rccl_kernel_diff.md
+  head -30 gpurun_out/r4rccl_kernel_diff.md
 fi

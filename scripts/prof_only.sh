@@ -6,6 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${PROF_TAG:-prof}
+rm -rf /tmp/plx_prof  # one trace per run: the summary below picks the first trace directory it finds
 timeout -k 10 300 python -c "from polyaxon_amd.ops import _native; _native.build_all()" > gpurun_out/pbuild.log 2>&1 \
 && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/plx_prof -o run --output-format csv -- python bench.py --steps ${STEPS:-2} --warmup 1 ${BENCH_ARGS:-} > gpurun_out/$TAG.log 2>&1
 rc=$?
