@@ -53,6 +53,10 @@ SCHEDULE: Dict[Tuple[int, int, int, bool, bool], int] = {
         (4096, 4096, 14336, _FWD, 8), (4096, 14336, 4096, _DGRAD, 8), (4096, 14336, 4096, _WGRAD, 5))}
 
 
+# A/B override of the schedule for every call (scripts/gemm_bench.py --waves); 0 = the table
+FORCE_SCHEDULE = 0
+
+
 def mode() -> str:
     m = os.environ.get("PLX_LM_GEMM", "1")
     return "0" if m == "0" else "1"
@@ -146,6 +150,8 @@ def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: boo
     v = _seen.get(key)
     if v is None:
         v = _seen[key] = schedule(*key)
+    if FORCE_SCHEDULE:
+        v = FORCE_SCHEDULE
     rc = lib.plx_gemm256_exv(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, M, N, K, lda, ldb, out.stride(0),
                              int(a_kmajor), int(b_kmajor), float(alpha), int(accumulate),
                              bias.data_ptr() if bias is not None else None,

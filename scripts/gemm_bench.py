@@ -3,7 +3,8 @@
     python scripts/gemm_bench.py [--models gpt2,llama] [--reps 20] [--waves 8,4]
 
 One JSON line per (model, linear, pass): ms and TFLOP/s of both, and the max |diff| relative to the output scale.
-``--waves 8,4`` times both kernel variants (plx_gemm256_set_waves) in the same process, interleaved per shape.
+``--waves 8,4`` times both kernel schedules (ops/gemm.py FORCE_SCHEDULE) in the same process, interleaved per shape;
+``--waves table`` times the per-shape table (ops/gemm.py SCHEDULE).
 Passes: fwd (x . W^T), dgrad (dy . W), wgrad (dy^T . x, K = tokens).
 """
 from __future__ import annotations
@@ -44,22 +45,38 @@ def main() -> None:
     ap.add_argument("--models", default="gpt2,llama")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--waves", default="8")
+    ap.add_argument("--cold", type=int, default=0,
+                    help="rotate each call through this many operand copies (>= 1 GB in total defeats the 256 MB "
+                         "infinity cache: the operands stream from HBM as in a training step)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     tot = {"torch": 0.0}
-    waves = [int(w) for w in args.waves.split(",")]
-    lib = gemm._native.lib("plx_gemm")
+    waves = [0 if w == "table" else int(w) for w in args.waves.split(",")]
     for model in args.models.split(","):
         T, linears = MODELS[model]
         for name, fin, fout in linears:
             x = torch.randn(T, fin, device=dev).to(torch.bfloat16)
             w = (torch.randn(fout, fin, device=dev) * 0.02).to(torch.bfloat16)
             dy = torch.randn(T, fout, device=dev).to(torch.bfloat16)
+            n = max(1, args.cold)
+            xs, ws, dys = [x] + [x.clone() for _ in range(n - 1)], [w] + [w.clone() for _ in range(n - 1)], \
+                [dy] + [dy.clone() for _ in range(n - 1)]
+            it = {"i": 0}
+
+            def nxt():  # the operand copy of this call (round robin)
+                it["i"] = (it["i"] + 1) % n
+                return xs[it["i"]], ws[it["i"]], dys[it["i"]]
+
+            def op(f):
+                def run():
+                    a_, b_, c_ = nxt()
+                    return f(a_, b_, c_)
+                return run
             cases = [
-                ("fwd", T, fout, fin, lambda: gemm.forward(x, w), lambda: x @ w.t()),
-                ("dgrad", T, fin, fout, lambda: gemm.dgrad(dy, w), lambda: dy @ w),
-                ("wgrad", fout, fin, T, lambda: gemm.wgrad(dy, x), lambda: dy.t() @ x),
+                ("fwd", T, fout, fin, op(lambda x, w, dy: gemm.forward(x, w)), op(lambda x, w, dy: x @ w.t())),
+                ("dgrad", T, fin, fout, op(lambda x, w, dy: gemm.dgrad(dy, w)), op(lambda x, w, dy: dy @ w)),
+                ("wgrad", fout, fin, T, op(lambda x, w, dy: gemm.wgrad(dy, x)), op(lambda x, w, dy: dy.t() @ x)),
             ]
             for pas, M, N, K, nat, ref in cases:
                 b = ref()
@@ -70,7 +87,7 @@ def main() -> None:
                        "splits": gemm._native.size("plx_gemm", "plx_gemm256_splits", M, N, K),
                        "torch_ms": round(tt, 4), "torch_tflops": round(fl / tt / 1e9, 1)}
                 for wv in waves:
-                    lib.plx_gemm256_set_waves(wv)
+                    gemm.FORCE_SCHEDULE = wv
                     a = nat()
                     err = ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6)).item()
                     tn = timed(nat, args.reps)
@@ -79,8 +96,8 @@ def main() -> None:
                     rec.update({f"native{sfx}_ms": round(tn, 4), f"native{sfx}_tflops": round(fl / tn / 1e9, 1),
                                 f"speedup{sfx}": round(tt / tn, 3), f"rel_err{sfx}": round(err, 5)})
                 print(json.dumps(rec), flush=True)
-            del x, w, dy
-    lib.plx_gemm256_set_waves(waves[0])
+            del x, w, dy, xs, ws, dys
+    gemm.FORCE_SCHEDULE = 0
     print(json.dumps({f"total_{k}_ms": round(v, 3) for k, v in tot.items()}))
 
 
