@@ -22,7 +22,8 @@ from polyaxon_amd.ops import gemm  # noqa: E402
 
 # (model, tokens, [(linear, in, out)])
 MODELS = {
-    "gpt2": (16 * 1024, [("qkv", 768, 2304), ("proj", 768, 768), ("up", 768, 3072), ("down", 3072, 768)]),
+    "gpt2": (16 * 1024, [("qkv", 768, 2304), ("proj", 768, 768), ("up", 768, 3072), ("down", 3072, 768),
+                        ("head", 768, 50432)]),
     "llama": (4096, [("qkv", 4096, 6144), ("proj", 4096, 4096), ("up", 4096, 28672), ("down", 14336, 4096)]),
 }
 
