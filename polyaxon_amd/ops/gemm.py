@@ -14,13 +14,17 @@ Shapes the kernel does not take (a dimension not a multiple of 256, or K of 64) 
 :func:`supported` says which; on a GPU box a missing library raises instead of falling back (ops/_native.py).  The
 LM trainers' shapes all fit (GPT-2's vocabulary is padded to 50432 rows, models/transformer.py).
 
-Every supported shape runs the kernel: round 4 measured it at 0.98-1.08x hipBLASLt on the large GPT-2 125M / Llama-3
-8B linears and 1.3-2.0x on the split-K weight gradients, 4.8 % less total time over the 24 shapes
-(profiles/r4_lm_gemm.md).  ``SCHEDULE`` holds the kernel schedule measured fastest per shape (8 = the 8-wave
-ping-pong kernel, 4-7 = the 4-wave AGPR kernel's variants, csrc/gemm256.hip ``plx_gemm256_set_waves``); other shapes
-take ``PLX_GEMM_WAVES`` (default 8).  The choice is a pure function of the shape, so runs are reproducible and every
-DP rank runs the same kernel.  ``PLX_LM_GEMM=0`` routes the linears to hipBLASLt for A/B measurements only;
-:func:`decisions` lists the shapes seen and their schedule.
+Dispatch (``PLX_LM_GEMM``): ``auto`` (default) runs the kernel where it wins on every MI355X box measured and
+hipBLASLt elsewhere; ``1`` always the kernel (the GPU tests), ``0`` always hipBLASLt.  Round 4 measured the kernel
+and hipBLASLt on three boxes / cache states (profiles/r4_lm_gemm.md): the split-K weight gradients of the narrow
+GPT-2 layers (and the tied head's) win 1.05-1.95x everywhere, a few Llama-3 8B weight / data gradients win by a few
+percent, and the large forward / data-gradient shapes swing between 1.05x and 0.79x with the box (the kernel is
+more clock-sensitive than hipBLASLt's), losing in the Llama training step (16.0k vs 18.0k tokens/s all-kernel vs
+all-hipBLASLt on one box).  ``SCHEDULE`` holds the shapes that go to the kernel and the schedule each runs
+(8 = the 8-wave ping-pong kernel, 4-7 = the 4-wave AGPR kernel's variants, csrc/gemm256.hip); any other supported
+shape goes to the kernel when it is a split-K shape (``plx_gemm256_splits > 1``: the narrow-output, long-reduction
+weight gradients) and to hipBLASLt otherwise.  The choice is a pure function of the shape -- reproducible, and the
+same kernel on every DP rank.  :func:`decisions` lists the shapes seen and what ran.
 """
 from __future__ import annotations
 
@@ -34,32 +38,29 @@ from polyaxon_amd.ops import _native
 TILE = 256
 _ws: Dict[Tuple[str, int], torch.Tensor] = {}
 
-_seen: Dict[Tuple[int, int, int, bool, bool], int] = {}
+_seen: Dict[Tuple[int, int, int, bool, bool], int] = {}  # shape -> schedule (-1 = hipBLASLt)
 
-# (M, N, K, A K-major, B K-major) -> kernel schedule, the fastest of the five in-process on one MI355X
-# (scripts/gemm_bench.py --waves 8,4,5,6,7; profiles/r4_lm_gemm.md).  fwd = (K, K), dgrad = (K, MN), wgrad = (MN, MN)
+# (M, N, K, A K-major, B K-major) -> kernel schedule, for the GPT-2 125M (16 x 1024 tokens) / Llama-3 8B (1 x 4096)
+# linears where the kernel beat hipBLASLt on every box (min ratio >= 0.98, mean >= 1.0 over
+# profiles/r4_lm_gemm_variants_vs_hipblaslt.jsonl, r4_lm_gemm_hot.jsonl, r4_lm_gemm_cold.jsonl).
+# fwd = (K, K), dgrad = (K, MN), wgrad = (MN, MN)
 _FWD, _DGRAD, _WGRAD = (True, True), (True, False), (False, False)
 SCHEDULE: Dict[Tuple[int, int, int, bool, bool], int] = {
     (M, N, K) + lay: v for (M, N, K, lay, v) in (
-        # GPT-2 125M, 16 x 1024 tokens
-        (16384, 2304, 768, _FWD, 7), (16384, 768, 2304, _DGRAD, 7), (2304, 768, 16384, _WGRAD, 5),
-        (16384, 768, 768, _FWD, 7), (16384, 768, 768, _DGRAD, 7), (768, 768, 16384, _WGRAD, 5),
-        (16384, 3072, 768, _FWD, 7), (16384, 768, 3072, _DGRAD, 7), (3072, 768, 16384, _WGRAD, 5),
-        (16384, 768, 3072, _FWD, 8), (16384, 3072, 768, _DGRAD, 7), (768, 3072, 16384, _WGRAD, 5),
-        # Llama-3 8B, 1 x 4096 tokens
-        (4096, 6144, 4096, _FWD, 7), (4096, 4096, 6144, _DGRAD, 8), (6144, 4096, 4096, _WGRAD, 7),
-        (4096, 4096, 4096, _FWD, 7), (4096, 4096, 4096, _DGRAD, 7), (4096, 4096, 4096, _WGRAD, 5),
-        (4096, 28672, 4096, _FWD, 6), (4096, 4096, 28672, _DGRAD, 4), (28672, 4096, 4096, _WGRAD, 7),
-        (4096, 4096, 14336, _FWD, 8), (4096, 14336, 4096, _DGRAD, 8), (4096, 14336, 4096, _WGRAD, 5))}
+        # GPT-2: every weight gradient (split-K), the tied head's, the attention projection's data gradient
+        (2304, 768, 16384, _WGRAD, 5), (768, 768, 16384, _WGRAD, 5), (3072, 768, 16384, _WGRAD, 5),
+        (768, 3072, 16384, _WGRAD, 5), (50432, 768, 16384, _WGRAD, 5), (16384, 768, 768, _DGRAD, 5),
+        # Llama-3 8B: the weight gradients and the QKV data gradient
+        (6144, 4096, 4096, _WGRAD, 5), (4096, 4096, 4096, _WGRAD, 5), (28672, 4096, 4096, _WGRAD, 5),
+        (4096, 14336, 4096, _WGRAD, 5), (4096, 4096, 6144, _DGRAD, 5))}
 
-
-# A/B override of the schedule for every call (scripts/gemm_bench.py --waves); 0 = the table
+# A/B override of the schedule for every kernel call (scripts/gemm_bench.py --waves); 0 = the table
 FORCE_SCHEDULE = 0
 
 
 def mode() -> str:
-    m = os.environ.get("PLX_LM_GEMM", "1")
-    return "0" if m == "0" else "1"
+    m = os.environ.get("PLX_LM_GEMM", "auto")
+    return m if m in ("0", "1", "auto") else "auto"
 
 
 def enabled() -> bool:
@@ -67,14 +68,33 @@ def enabled() -> bool:
     return mode() != "0"
 
 
+def splits(M: int, N: int, K: int) -> int:
+    return _native.size("plx_gemm", "plx_gemm256_splits", M, N, K)
+
+
 def schedule(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> int:
-    """The kernel schedule for a shape: the measured table, else 0 (the library's global knob, PLX_GEMM_WAVES)."""
-    return SCHEDULE.get((M, N, K, bool(a_kmajor), bool(b_kmajor)), 0)
+    """What ``auto`` runs for a supported shape: the table's schedule, 0 (the library default) for a split-K shape
+    outside it, -1 (hipBLASLt) otherwise."""
+    v = SCHEDULE.get((M, N, K, bool(a_kmajor), bool(b_kmajor)))
+    if v is not None:
+        return v
+    return 0 if splits(M, N, K) > 1 else -1
+
+
+def _use_native(M, N, K, a_kmajor, b_kmajor) -> bool:
+    m = mode()
+    if m != "auto":
+        return m == "1"
+    key = (M, N, K, bool(a_kmajor), bool(b_kmajor))
+    v = _seen.get(key)
+    if v is None:
+        v = _seen[key] = schedule(*key)
+    return v >= 0
 
 
 def decisions() -> Dict[str, Dict[str, object]]:
-    """Shapes this process ran on the kernel and their schedule (0 = the library default)."""
-    return {f"{M}x{N}x{K}:{'K' if ak else 'M'}{'K' if bk else 'N'}": {"native": True, "schedule": v}
+    """Shapes this process dispatched in ``auto`` mode: kernel (with its schedule) or hipBLASLt."""
+    return {f"{M}x{N}x{K}:{'K' if ak else 'M'}{'K' if bk else 'N'}": {"native": v >= 0, "schedule": v}
             for (M, N, K, ak, bk), v in _seen.items()}
 
 
@@ -93,8 +113,8 @@ def _torch_gemm(a, b, M, N, K, a_kmajor, b_kmajor, out=None, accumulate=False, a
 
 
 def matmul(a, b, M, N, K, a_kmajor, b_kmajor, out=None, accumulate=False) -> torch.Tensor:
-    """:func:`gemm` semantics: the MFMA kernel for every supported shape (hipBLASLt only with PLX_LM_GEMM=0)."""
-    if enabled() and a.is_cuda and supported(M, N, K):
+    """:func:`gemm` semantics on whichever of the MFMA kernel / hipBLASLt the dispatch picks."""
+    if a.is_cuda and supported(M, N, K) and _use_native(M, N, K, a_kmajor, b_kmajor):
         return gemm(a, b, M, N, K, a_kmajor, b_kmajor, out=out, accumulate=accumulate)
     return _torch_gemm(a, b, M, N, K, a_kmajor, b_kmajor, out=out, accumulate=accumulate)
 
@@ -142,16 +162,11 @@ def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: boo
                                  or gelu_out.stride() != out.stride() or gelu_out.data_ptr() % 16):
         raise ValueError("gelu_out must be a bf16 tensor laid out like out (and no accumulate)")
     lib = _native.lib("plx_gemm")
-    splits = _native.size("plx_gemm", "plx_gemm256_splits", M, N, K)
-    ws = _workspace(a.device, splits * M * N).data_ptr() if splits > 1 else None
+    ns = splits(M, N, K)
+    ws = _workspace(a.device, ns * M * N).data_ptr() if ns > 1 else None
     lda = K if a_kmajor else M
     ldb = K if b_kmajor else N
-    key = (M, N, K, bool(a_kmajor), bool(b_kmajor))
-    v = _seen.get(key)
-    if v is None:
-        v = _seen[key] = schedule(*key)
-    if FORCE_SCHEDULE:
-        v = FORCE_SCHEDULE
+    v = FORCE_SCHEDULE or max(0, SCHEDULE.get((M, N, K, bool(a_kmajor), bool(b_kmajor)), 0))
     rc = lib.plx_gemm256_exv(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, M, N, K, lda, ldb, out.stride(0),
                              int(a_kmajor), int(b_kmajor), float(alpha), int(accumulate),
                              bias.data_ptr() if bias is not None else None,
@@ -175,7 +190,7 @@ def forward(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]
     N = weight.shape[0]
     if bias is None:
         return matmul(x2, weight, T, N, fin, True, True)
-    if enabled() and x2.is_cuda and supported(T, N, fin):
+    if x2.is_cuda and supported(T, N, fin) and _use_native(T, N, fin, True, True):
         return gemm(x2, weight, T, N, fin, True, True, bias=bias)
     return torch.addmm(bias.to(x2.dtype), x2, weight.t())
 
@@ -188,7 +203,7 @@ def forward_gelu(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Te
     epilogue (no separate pass reading h back); on hipBLASLt addmm then F.gelu."""
     T, fin = x2.shape
     N = weight.shape[0]
-    if _GELU_EPILOGUE and enabled() and x2.is_cuda and supported(T, N, fin):
+    if _GELU_EPILOGUE and x2.is_cuda and supported(T, N, fin) and _use_native(T, N, fin, True, True):
         h = torch.empty(T, N, dtype=torch.bfloat16, device=x2.device)
         a = torch.empty_like(h)
         gemm(x2, weight, T, N, fin, True, True, out=h, bias=bias, gelu_out=a)

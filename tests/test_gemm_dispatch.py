@@ -49,9 +49,9 @@ def test_knob_modes(monkeypatch):
     monkeypatch.setenv("PLX_LM_GEMM", "1")
     assert gemm.enabled() and gemm.mode() == "1"
     monkeypatch.delenv("PLX_LM_GEMM")
-    assert gemm.mode() == "1" and gemm.enabled()   # the kernel is the default; hipBLASLt only as an A/B knob
-    monkeypatch.setenv("PLX_LM_GEMM", "auto")      # the retired timing mode now means the kernel
-    assert gemm.mode() == "1"
+    assert gemm.mode() == "auto" and gemm.enabled()
+    monkeypatch.setenv("PLX_LM_GEMM", "bogus")
+    assert gemm.mode() == "auto"
 
 
 def test_torch_path_layouts_match_reference():
@@ -70,15 +70,23 @@ def test_torch_path_layouts_match_reference():
             torch.testing.assert_close(out, ref + 1)
 
 
-def test_schedule_table_is_a_pure_function_of_the_shape():
-    """Every GPT-2 125M / Llama-3 8B linear has a measured kernel schedule (8 = ping-pong, 4-7 = the 4-wave AGPR
-    variants); other shapes get 0 (the library default).  No timing, no CUDA call: reproducible across runs and
-    identical on every DP rank."""
-    assert len(gemm.SCHEDULE) == 24 and set(gemm.SCHEDULE.values()) <= {4, 5, 6, 7, 8}
+def test_auto_dispatch_is_a_pure_function_of_the_shape(monkeypatch):
+    """``auto``: the measured table's shapes on the kernel with their schedule, any other split-K shape on the kernel
+    (schedule 0 = library default), the rest on hipBLASLt (-1).  No timing, no CUDA call: reproducible across runs
+    and identical on every DP rank."""
+    monkeypatch.setenv("PLX_LM_GEMM", "auto")
+    assert set(gemm.SCHEDULE.values()) <= {4, 5, 6, 7, 8}
     assert gemm.schedule(2304, 768, 16384, False, False) == 5      # GPT-2 qkv wgrad (split-K)
-    assert gemm.schedule(16384, 768, 3072, True, True) == 8        # GPT-2 down fwd
-    assert gemm.schedule(4096, 28672, 4096, True, True) == 6       # Llama up fwd
-    assert gemm.schedule(16384, 768, 768, True, True) != 0 and gemm.schedule(16384, 768, 768, True, False) != 0
-    assert gemm.schedule(512, 512, 512, True, True) == 0
+    assert gemm.schedule(50432, 768, 16384, False, False) == 5     # GPT-2 tied head wgrad
+    assert gemm.schedule(16384, 768, 3072, True, True) == -1       # GPT-2 down fwd: hipBLASLt
+    assert gemm.schedule(4096, 28672, 4096, True, True) == -1      # Llama up fwd: hipBLASLt
+    assert gemm.schedule(28672, 4096, 4096, False, False) == 5     # Llama up wgrad
+    assert gemm.splits(256, 256, 8192) > 1 and gemm.schedule(256, 256, 8192, False, False) == 0
+    assert gemm.splits(4096, 4096, 512) == 1 and gemm.schedule(4096, 4096, 512, True, True) == -1
     for (M, N, K, ak, bk) in gemm.SCHEDULE:
         assert gemm.supported(M, N, K)
+    gemm._seen.clear()
+    assert gemm._use_native(2304, 768, 16384, False, False) and not gemm._use_native(16384, 3072, 768, True, True)
+    d = gemm.decisions()
+    assert d["2304x768x16384:MN"] == {"native": True, "schedule": 5} and d["16384x3072x768:KK"]["native"] is False
+    gemm._seen.clear()

@@ -226,19 +226,24 @@ def test_transformer_step_uses_mfma_linears(cuda, monkeypatch):
     assert torch.isfinite(x.grad.float()).all()
 
 
-def test_per_shape_schedule_runs_and_matches(cuda, monkeypatch):
-    """The default dispatch runs every supported shape on the kernel with its measured schedule (a table shape gets
-    its variant through plx_gemm256_exv, others the library default) and matches fp32 either way."""
+def test_auto_dispatch_runs_both_paths_and_matches(cuda, monkeypatch):
+    """``auto``: a table / split-K shape runs the kernel, a large forward shape hipBLASLt; both match fp32."""
     from polyaxon_amd.ops import gemm
 
-    monkeypatch.delenv("PLX_LM_GEMM", raising=False)
-    for T, fin, fout in ((16384, 768, 2304), (1024, 768, 2304)):
-        x, w = _rand((T, fin), cuda, 17), _rand((fout, fin), cuda, 18)
-        y = gemm.forward(x, w)
-        d = gemm.decisions()[f"{T}x{fout}x{fin}:KK"]
-        assert d["native"] and d["schedule"] == gemm.schedule(T, fout, fin, True, True)
-        torch.cuda.synchronize()
-        _check(y, x.float() @ w.float().t(), fin)
+    monkeypatch.setenv("PLX_LM_GEMM", "auto")
+    gemm._seen.clear()
+    T, fin, fout = 16384, 768, 2304
+    x, w = _rand((T, fin), cuda, 17), _rand((fout, fin), cuda, 18)
+    dy = _rand((T, fout), cuda, 19)
+    y = gemm.forward(x, w)
+    dw = gemm.wgrad(dy, x)
+    dec = gemm.decisions()
+    assert dec[f"{T}x{fout}x{fin}:KK"]["native"] is False
+    assert dec[f"{fout}x{fin}x{T}:MN"] == {"native": True, "schedule": 5}
+    torch.cuda.synchronize()
+    _check(y, x.float() @ w.float().t(), fin)
+    _check(dw, dy.float().t() @ x.float(), T)
+    gemm._seen.clear()
 
 
 def test_autocast_fp32_input_takes_mfma_path(cuda, monkeypatch):
