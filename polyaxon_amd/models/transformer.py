@@ -16,6 +16,7 @@ can be exercised on the named configs with random weights and synthetic tokens.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -49,7 +50,7 @@ class TransformerConfig:
     # embedding / head rows are padded to a multiple of this (GPT-2's 50257 -> 50432 = 197 x 256, so the logits,
     # their data gradient and the tied-weight gradient are gemm256 shapes); the padded logits carry a -inf bias, so
     # the softmax, the loss and every gradient of the real vocabulary are unchanged and the padded rows get 0
-    vocab_multiple: int = 256
+    vocab_multiple: int = int(os.environ.get("PLX_VOCAB_MULTIPLE", "256"))  # A/B knob: 1 = no padding
 
     @property
     def kv_heads(self) -> int:
