@@ -188,10 +188,10 @@ def train_lm(argv=None) -> float:
                     help="synthetic tokens: uniform random (loss stays ln V), or the copy task of the resident GPT-2 "
                          "program (ops/synth.py SyntheticTokens: learnable, hyper-parameter sensitive)")
     ap.add_argument("--period", type=int, default=64, help="copy task: phrase length (seq must be a multiple)")
-    ap.add_argument("--world1_collectives", action="store_true",
-                    help="world 1 on the GPU: still create the nccl (RCCL) process group, run every gradient "
-                         "bucket's all-reduce and the metric reducer's RCCL communicator (the DP path's overheads "
-                         "measured on one GPU)")
+    ap.add_argument("--world1_collectives", nargs="?", const="all", default="", choices=["", "all", "metric"],
+                    help="world 1 on the GPU: still create the nccl (RCCL) process group and the metric reducer's RCCL "
+                         "communicator; 'all' (the bare flag) also runs every gradient bucket's all-reduce (the DP "
+                         "path's overheads measured on one GPU)")
     ap.add_argument("--zero1", action="store_true",
                     help="ZeRO-1: reduce-scatter each gradient bucket, AdamW on this rank's 1/W slice inside the "
                          "backward, all-gather the bf16 weights (parallel/ddp.py); also PLX_ZERO1=1")
@@ -200,6 +200,7 @@ def train_lm(argv=None) -> float:
     info = init_from_env(backend)
     dev = info["device"]
     force = bool(args.world1_collectives) and dev.type == "cuda" and info["world"] == 1
+    force_buckets = force and args.world1_collectives == "all"
     if force:
         import torch.distributed as dist
 
@@ -228,7 +229,7 @@ def train_lm(argv=None) -> float:
     zero1 = args.zero1 or os.environ.get("PLX_ZERO1", "0") == "1"
     in_bwd = zero1 or (dev.type == "cuda" and os.environ.get("PLX_OPT_IN_BACKWARD", "0") == "1")
     ddp = FlatDDP(flat, bucket_mb=args.bucket_mb, optimizer=opt if in_bwd else None, shard_optimizer=zero1,
-                  force_collectives=force)
+                  force_collectives=force_buckets)
     ddp.broadcast_params()
     metrics = MetricReducer(dev, force_comm=force)  # cross-rank mean of the logged loss (RCCL communicator, GPU)
     g = torch.Generator(device=dev).manual_seed(args.seed + 1000 * info["rank"])
@@ -285,7 +286,7 @@ def train_lm(argv=None) -> float:
 
         dec = _gemm.decisions()
         print(json.dumps({"loss": loss_val, "tokens_per_s": round(tok_s, 1), "world": info["world"],
-                          "world1_collectives": force, "zero1": zero1, "bucket_launches": ddp.launched,
+                          "world1_collectives": args.world1_collectives if force else "", "zero1": zero1, "bucket_launches": ddp.launched,
                           "params_m": round(sum(s.numel for s in flat.segments) / 1e6, 1),
                           "lm_gemm": {"mode": _gemm.mode(), "native_shapes": sum(1 for d in dec.values() if d["native"]),
                                       "shapes": len(dec), "decisions": dec}}))
