@@ -43,6 +43,10 @@ import tempfile
 import threading
 import time
 
+# eight hardware queues before any GPU call: the RCCL communicator's streams + compute + side streams (see
+# polyaxon_amd/__init__.py and profiles/r4_rccl_slowdown.md)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 T0 = time.perf_counter()
