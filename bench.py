@@ -43,9 +43,10 @@ import tempfile
 import threading
 import time
 
-# eight hardware queues before any GPU call: the RCCL communicator's streams + compute + side streams (see
-# polyaxon_amd/__init__.py and profiles/r4_rccl_slowdown.md)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# at least eight hardware queues before any GPU call: the RCCL communicator's streams + compute + side streams
+# (the same rule as polyaxon_amd/__init__.py; profiles/r4_rccl_slowdown.md)
+if int(os.environ.get("PLX_HW_QUEUES", "8") or 0) > int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0):
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(int(os.environ.get("PLX_HW_QUEUES", "8")), 32))
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 

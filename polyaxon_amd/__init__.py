@@ -14,6 +14,19 @@ __version__ = "0.3.0"
 # bucket updates) ran out of queues: the side stream landed on the compute stream's queue and the two serialised --
 # the ResNet-50 bench lost 17 % with a live communicator, the Llama-3 8B step 8 % with per-bucket all-reduces
 # (profiles/r4_rccl_slowdown.md).  Eight queues give every stream its own.  Read by the HIP runtime at its first
-# initialisation, so this must run before any GPU call (importing the package first is enough); an explicit value
-# in the environment wins, and child processes (trials, executors) inherit it.
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# initialisation, so this must run before any GPU call (importing the package first is enough).  The queue count is
+# raised to PLX_HW_QUEUES (default 8; 0 leaves the environment alone), never lowered; child processes (trials,
+# executors) inherit it.
+
+
+def _raise_hw_queues() -> None:
+    want = int(_os.environ.get("PLX_HW_QUEUES", "8") or 0)
+    try:
+        have = int(_os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)
+    except ValueError:
+        have = 0
+    if want > have:
+        _os.environ["GPU_MAX_HW_QUEUES"] = str(min(want, 32))
+
+
+_raise_hw_queues()
