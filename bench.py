@@ -472,13 +472,19 @@ def main() -> int:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    # PLX_BENCH_RCCL: "early" (default) -- the framework's RCCL communicator is alive for the whole run, as in a DP
+    # trial (with 4 hardware queues it serialised the side stream with compute, -17 %; at the package's 8 queues it
+    # costs <= 0.2 %: profiles/r4_rccl_slowdown.md); "late" / "1" -- created after the timed region; "0" -- gloo only
+    rccl_mode = os.environ.get("PLX_BENCH_RCCL", "early")
     early_comm = None
-    if dev.type == "cuda" and os.environ.get("PLX_BENCH_RCCL") == "early":
-        # diagnostic (profiles/r4_rccl_slowdown.md): a communicator alive for the whole run, as in a DP trial
+    if dev.type == "cuda" and rccl_mode == "early":
         from polyaxon_amd.parallel.rccl import RcclComm
 
-        early_comm = (RcclComm.from_torch_distributed() if world > 1
-                      else RcclComm(RcclComm.new_unique_id(), 1, 0, local))
+        try:
+            early_comm = (RcclComm.from_torch_distributed() if world > 1
+                          else RcclComm(RcclComm.new_unique_id(), 1, 0, local))
+        except Exception as e:  # built again after the timed region (or gloo) rather than fail the run
+            print(f"bench: early RCCL communicator unavailable ({e})", file=sys.stderr)
     worker = ResidentWorker(program, params, device=dev, max_active=args.max_active)
     log(f"building {program} executors (batch {params['batch']}, image {params.get('image')}, config {args.config})")
     worker._ready_info = worker.build()
@@ -506,10 +512,10 @@ def main() -> int:
         raise RuntimeError(f"executor stopped during the timed region: {r}")
     mine = [elapsed, worker.stats["trials"] - s0["trials"], worker.stats["train_steps"] - s0["train_steps"],
             float(os.getpid())] + [worker.stats[k] - s0[k] for k in ("idle_s", "round_s", "sync_s")]
-    # framework-owned collective (csrc/rccl_comm.cpp) for the per-rank gather on the GPU path, on a communicator
-    # created only now (see the process-group note above).
+    # framework-owned collective (csrc/rccl_comm.cpp) for the per-rank gather on the GPU path (the early communicator,
+    # or one created now).
     comm = early_comm
-    if comm is None and dev.type == "cuda" and os.environ.get("PLX_BENCH_RCCL", "1") != "0":
+    if comm is None and dev.type == "cuda" and rccl_mode != "0":
         from polyaxon_amd.parallel.rccl import RcclComm
 
         try:
