@@ -65,6 +65,20 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
+// Tile of logical id (consecutive ids share an XCD, xcd_remap): ids walk `group` M-tiles of one N-column, then the
+// next column -- the ~32 blocks an XCD holds at once cover a group x (32 / group) patch, so each A slab is read by
+// 32 / group of them and each B slab by `group` from that XCD's L2.  group 1 (row-major: every concurrent block a
+// different B tile) left the Llama MLP-up forward at a 51 % L2 hit rate against hipBLASLt's 79 %
+// (profiles/r4_lm_gemm.md).
+__device__ __forceinline__ void tile_of(int id, int ntm, int ntn, int group, int& tm, int& tn) {
+  const int per = group * ntn;
+  const int first = (id / per) * group;
+  const int gs = min(ntm - first, group);
+  const int r = id - (id / per) * per;
+  tm = first + r % gs;
+  tn = r / gs;
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7ffffff0, 0x00020000);
 }
@@ -153,6 +167,7 @@ struct Gemm256Args {
   float alpha;
   const float* bias;  // fp32 [N] added after alpha in the bf16 epilogue (the Linear bias), or null
   void* C2;           // bf16 [M][ldc]: gelu_tanh of the stored (bf16-rounded) C, or null (GPT-2's up-projection)
+  int group;          // M-tiles per tile group (tile_of)
 };
 
 // GELU, tanh approximation, of the bf16-rounded value (what a separate activation pass reading C would compute);
@@ -172,8 +187,8 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int ntn = p.N / BN, ntm = p.M / BM;
-  const int id = xcd_remap(blockIdx.x, ntm * ntn);
-  const int tm = id / ntn, tn = id % ntn;
+  int tm, tn;
+  tile_of(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, p.group, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int kt0 = blockIdx.y * p.kt_per_split;
   const int nk = min(p.kt_per_split, p.K / BK - kt0);
@@ -417,8 +432,8 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int ntn = p.N / BN, ntm = p.M / BM;
-  const int id = xcd_remap(blockIdx.x, ntm * ntn);
-  const int tm = id / ntn, tn = id % ntn;
+  int tm, tn;
+  tile_of(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, p.group, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int kt0 = blockIdx.y * p.kt_per_split;
   const int nk = min(p.kt_per_split, p.K / BK - kt0);
@@ -698,6 +713,7 @@ int dispatch(const Gemm256Args& a, int splits, int accumulate, hipStream_t st, i
   return accumulate ? launch<AK, BKM, true, false>(a, 1, st, variant) : launch<AK, BKM, false, false>(a, 1, st, variant);
 }
 
+int g_group = 4;  // M-tiles per tile group (tile_of; plx_gemm256_set_group, 1 = row-major order)
 int g_split_target = 256;  // blocks the split-K planner aims for (one per CU: splitting a grid that already
                            // fills the chip measured slower); plx_gemm256_set_split_target
 
@@ -721,6 +737,13 @@ PLX_API int plx_gemm256_splits(int M, int N, int K) {
 
 // A/B knob: blocks the split-K planner aims for (0 disables splitting)
 PLX_API void plx_gemm256_set_split_target(int blocks) { g_split_target = blocks; }
+
+// A/B knob: M-tiles per tile group of the block order (1 = row-major); returns the previous value
+PLX_API int plx_gemm256_set_group(int group) {
+  const int prev = g_group;
+  if (group >= 1 && group <= 64) g_group = group;
+  return prev;
+}
 
 // A/B knob: 8 (the 8-wave ping-pong kernel) or 4 + bits (the 4-wave AGPR-accumulator kernel; bit 0: one barrier per
 // two phases instead of one per phase, bit 1: fragment reads and DMAs interleaved with the MFMAs); returns the
@@ -753,7 +776,7 @@ PLX_API int plx_gemm256_exv(const void* A, const void* B, void* C, void* ws, int
   const int splits = (K / BK + kps - 1) / kps;
   if (splits > 1 && !ws) return -5;
   Gemm256Args a{(const __bf16*)A, (const __bf16*)B, splits > 1 ? ws : C, M, N, K, lda, ldb, ldc, kps, alpha, bias,
-                splits > 1 ? nullptr : gelu_out};
+                splits > 1 ? nullptr : gelu_out, g_group > 0 ? g_group : 1};
   hipStream_t st = (hipStream_t)stream;
   int rc;
   if (a_kmajor && b_kmajor) rc = dispatch<true, true>(a, splits, accumulate, st, variant);

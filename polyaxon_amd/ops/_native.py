@@ -198,6 +198,8 @@ def lib(name: str) -> ctypes.CDLL:
             handle.plx_set_nt_tall(int(os.environ["PLX_NT_TALL"]), int(os.environ.get("PLX_NT_TALL_K", "0")))
         if name == "plx_gemm" and os.environ.get("PLX_GEMM_SPLIT_TARGET"):  # A/B knob: split-K planner target
             handle.plx_gemm256_set_split_target(int(os.environ["PLX_GEMM_SPLIT_TARGET"]))
+        if name == "plx_gemm" and os.environ.get("PLX_GEMM_GROUP"):  # A/B knob: M-tiles per tile group
+            handle.plx_gemm256_set_group(int(os.environ["PLX_GEMM_GROUP"]))
         if name == "plx_gemm" and os.environ.get("PLX_GEMM_WAVES"):  # 8 = ping-pong kernel, 4 = AGPR 4-wave kernel
             handle.plx_gemm256_set_waves(int(os.environ["PLX_GEMM_WAVES"]))
         if name == "plx_conv" and os.environ.get("PLX_TN_PLAN"):  # A/B knob: "blocks_per_cu,slab_mb"
@@ -323,6 +325,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gemm256_splits": [_I, _I, _I],
         "plx_gemm256_set_split_target": [_I],
         "plx_gemm256_set_waves": [_I],
+        "plx_gemm256_set_group": [_I],
         "plx_gemm256_tile": [],
     },
     "plx_attn": {

@@ -46,6 +46,7 @@ def main() -> None:
     ap.add_argument("--models", default="gpt2,llama")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--waves", default="8")
+    ap.add_argument("--groups", default="", help="tile-group sizes to A/B (plx_gemm256_set_group), e.g. 1,4,8")
     ap.add_argument("--cold", type=int, default=0,
                     help="rotate each call through this many operand copies (>= 1 GB in total defeats the 256 MB "
                          "infinity cache: the operands stream from HBM as in a training step)")
@@ -54,6 +55,8 @@ def main() -> None:
     torch.manual_seed(0)
     tot = {"torch": 0.0}
     waves = [0 if w == "table" else int(w) for w in args.waves.split(",")]
+    groups = [int(g) for g in args.groups.split(",")] if args.groups else [0]
+    lib = gemm._native.lib("plx_gemm")
     for model in args.models.split(","):
         T, linears = MODELS[model]
         for name, fin, fout in linears:
@@ -87,12 +90,14 @@ def main() -> None:
                 rec = {"model": model, "linear": name, "pass": pas, "M": M, "N": N, "K": K,
                        "splits": gemm._native.size("plx_gemm", "plx_gemm256_splits", M, N, K),
                        "torch_ms": round(tt, 4), "torch_tflops": round(fl / tt / 1e9, 1)}
-                for wv in waves:
+                for wv, grp in [(w_, g_) for g_ in groups for w_ in waves]:
                     gemm.FORCE_SCHEDULE = wv
+                    if grp:
+                        lib.plx_gemm256_set_group(grp)
                     a = nat()
                     err = ((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6)).item()
                     tn = timed(nat, args.reps)
-                    sfx = "" if len(waves) == 1 else f"_w{wv}"
+                    sfx = ("" if len(waves) == 1 else f"_w{wv}") + (f"_g{grp}" if grp else "")
                     tot["native" + sfx] = tot.get("native" + sfx, 0.0) + tn
                     rec.update({f"native{sfx}_ms": round(tn, 4), f"native{sfx}_tflops": round(fl / tn / 1e9, 1),
                                 f"speedup{sfx}": round(tt / tn, 3), f"rel_err{sfx}": round(err, 5)})
