@@ -539,7 +539,6 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
   auto phase = [&](auto ph, int kt, const FragA& fa, const FragA& fb, FragA& nxt, auto mi_, auto ni_) {
     constexpr int P = decltype(ph)::value, MI = decltype(mi_)::value, NI = decltype(ni_)::value;
     const int g = 4 * kt + P;
-    nxt = read_seq(IC<((P + 2) & 3)>{}, g + 2);  // past the last tile: stale LDS into a dead set, harmless
     constexpr int AHEAD = PAIR ? 8 : 9, RO = (P + 2) & 3, DO = (P + AHEAD) & 3;
     const bool dma = g + AHEAD < S;
     if constexpr (!ILV) {
