@@ -94,6 +94,9 @@ class ResidentTrialExecutor:
         self._prefetch = (self.is_cuda and not self.use_graph and self.data is not None
                           and hasattr(self.data, "next_into") and side_stream.enabled()
                           and os.environ.get("PLX_PREFETCH_BATCH", "1") != "0")
+        # PLX_PREFETCH_AT=start: queue batch k+1 on the side stream at the start of step k (it runs beside the
+        # forward, where the side stream is otherwise idle) instead of after the backward (beside its tail)
+        self._prefetch_at_start = os.environ.get("PLX_PREFETCH_AT", "end") == "start"
         self._bufs = None          # [(x, y), (x, y)] when prefetching
         self._cur = 0              # buffer the next step consumes
         self._ready = None         # event after the generator wrote self._bufs[self._cur], or None
@@ -153,6 +156,8 @@ class ResidentTrialExecutor:
             # every earlier step's use of the other buffer is complete in main-stream order from here
             step_start = torch.cuda.Event()
             step_start.record(main)
+            if self._prefetch_at_start:
+                self._queue_next_batch(step_start)
         elif self.data is not None:
             self.data.next()
         if self.wcache is not None:
@@ -172,17 +177,22 @@ class ResidentTrialExecutor:
         side_stream.join(self.device)  # weight-gradient GEMMs overlapped on the side stream (ops/side_stream.py)
         if self.ddp is not None:
             self.ddp.finish()  # the gang's averaged gradients
-        if prefetch:
+        if prefetch and not self._prefetch_at_start:
             # queued after the join: the main stream does not wait for it before the optimizer
-            side = side_stream.stream_for(self.device)
-            side.wait_event(step_start)
-            nxt = self._cur ^ 1
-            self.data.next_into(*self._bufs[nxt], side)
-            self._ready = torch.cuda.Event()
-            self._ready.record(side)
-            self._cur = nxt
+            self._queue_next_batch(step_start)
         self.opt.step_()
         self._record(loss.detach())
+
+    def _queue_next_batch(self, step_start) -> None:
+        """Generate the next batch into the other buffer on the side stream, after ``step_start`` (the main-stream
+        point from which every earlier step's use of that buffer is complete); the next step waits on ``_ready``."""
+        side = side_stream.stream_for(self.device)
+        side.wait_event(step_start)
+        nxt = self._cur ^ 1
+        self.data.next_into(*self._bufs[nxt], side)
+        self._ready = torch.cuda.Event()
+        self._ready.record(side)
+        self._cur = nxt
 
     def _record(self, loss: torch.Tensor) -> None:
         if self.is_cuda:

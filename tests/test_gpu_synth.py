@@ -64,19 +64,36 @@ def test_executor_batch_prefetch_matches_inline(cuda):
     from polyaxon_amd.polyflow.executor import ResidentTrialExecutor
 
     out = {}
-    for prefetch in (False, True):
+    for mode in ("inline", "end", "start"):  # PLX_PREFETCH_AT: after the backward (default) / at the step's start
         torch.manual_seed(0)
         data = SyntheticImages(4, 64, cuda, classes=1000, active_classes=100, grid=7, signal=0.5, seed=5)
         ex = ResidentTrialExecutor(resnet50(), data, cuda, use_graph=False)
-        ex._prefetch = prefetch
+        ex._prefetch = mode != "inline"
+        ex._prefetch_at_start = mode == "start"
         ex.reset(seed=1)
         ex.set_hparams(lr=0.05, momentum=0.9, weight_decay=1e-4)
         ex.run(4)
         torch.cuda.synchronize()
-        out[prefetch] = (ex.losses(), ex.flat.params.detach().float().clone(), int(data.counter.item()))
-        if prefetch:
+        out[mode] = (ex.losses(), ex.flat.params.detach().float().clone(), int(data.counter.item()))
+        if mode != "inline":
             assert ex._ready is not None and ex._bufs is not None  # the prefetch path really ran
         del ex
-    assert out[True][2] == out[False][2] + 1  # one batch generated ahead
-    torch.testing.assert_close(out[True][0], out[False][0], rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(out[True][1], out[False][1], rtol=1e-4, atol=1e-5)
+    for mode in ("end", "start"):
+        assert out[mode][2] == out["inline"][2] + 1  # one batch generated ahead
+        torch.testing.assert_close(out[mode][0], out["inline"][0], rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(out[mode][1], out["inline"][1], rtol=1e-4, atol=1e-5)
+
+
+def test_synth_images_odd_sizes_match_the_pattern(cuda):
+    """Image sides that the pattern grid does not divide, chunks that cross pixel rows (H*W*3 % 8 == 0 only):
+    the incremental (h, w) walk and the LDS cell table give the same noise-free image as the fp32 reference."""
+    from polyaxon_amd.ops.synth import SyntheticImages
+
+    for image, grid in ((40, 7), (24, 5), (56, 3)):
+        d = SyntheticImages(32, image, cuda, classes=10, active_classes=10, grid=grid, signal=4.0, seed=11)
+        d.next()
+        torch.cuda.synchronize()
+        noise = d.x.float().cpu() - d.expected_mean(d.y.cpu()).cpu()
+        # a wrong cell would leave pattern residue of variance ~ signal^2 in the noise
+        assert abs(float(noise.std()) - 1.0) < 0.03, (image, grid, float(noise.std()))
+        assert abs(float(noise.mean())) < 0.03
