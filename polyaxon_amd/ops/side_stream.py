@@ -60,11 +60,39 @@ def _masked_stream(idx: int, ncu: int) -> "torch.cuda.Stream":
     return torch.cuda.ExternalStream(handle.value, device=torch.device("cuda", idx))
 
 
+def priority_stream(idx: int, priority: int) -> "torch.cuda.Stream":
+    """A HIP stream created with ``hipStreamCreateWithPriority`` (lower = higher priority; HIP maps -1 / 0 / 1 to
+    the high / normal / low hardware-queue priority, which the command processor uses when it picks the next queue
+    to dispatch workgroups from).  torch clamps ``torch.cuda.Stream(priority=)`` to the range HIP reports, which is
+    not the full one on every ROCm release, hence the direct call."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    handle = ctypes.c_void_p()
+    with torch.cuda.device(idx):
+        # hipStreamNonBlocking (1), as torch's own streams: a blocking stream would synchronise with every launch on
+        # the null stream, the main stream of the step when it is the caller's
+        rc = hip.hipStreamCreateWithPriority(ctypes.byref(handle), ctypes.c_uint(1), ctypes.c_int(priority))
+    if rc != 0:
+        raise RuntimeError(f"hipStreamCreateWithPriority failed ({rc})")
+    return torch.cuda.ExternalStream(handle.value, device=torch.device("cuda", idx))
+
+
+# PLX_WGRAD_PRIORITY=p: the side stream is created with HIP priority p (1 = low: the weight gradients yield workgroup
+# slots to the main stream's critical path); unset: default priority
+_WGRAD_PRIORITY = os.environ.get("PLX_WGRAD_PRIORITY", "")
+
+
 def _stream_for(dev: torch.device) -> "torch.cuda.Stream":
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     s = _side.get(idx)
     if s is None:
-        s = _masked_stream(idx, _WGRAD_CUS) if _WGRAD_CUS > 0 else torch.cuda.Stream(device=idx)
+        if _WGRAD_CUS > 0:
+            s = _masked_stream(idx, _WGRAD_CUS)
+        elif _WGRAD_PRIORITY:
+            s = priority_stream(idx, int(_WGRAD_PRIORITY))
+        else:
+            s = torch.cuda.Stream(device=idx)
         _side[idx] = s
     return s
 

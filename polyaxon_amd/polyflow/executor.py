@@ -285,12 +285,27 @@ class ResidentTrialExecutor:
     def set_hparams(self, **hp) -> None:
         self.opt.set_hparams(**{k: v for k, v in hp.items() if k in self.opt.HP})
 
+    _main_stream = None
+
     def run(self, n_steps: int) -> None:
-        for _ in range(n_steps):
-            if self.graph is not None:
-                self.graph.replay()
-            else:
+        hp = os.environ.get("PLX_MAIN_PRIORITY", "")
+        if not (hp and self.is_cuda and self.graph is None):
+            for _ in range(n_steps):
+                if self.graph is not None:
+                    self.graph.replay()
+                else:
+                    self._train_step()
+            return
+        # PLX_MAIN_PRIORITY=p: the eager steps run on a stream of HIP priority p (-1 = high), forked from and joined
+        # back into the caller's stream, so the critical path's workgroups are dispatched ahead of the side stream's
+        if self._main_stream is None:
+            self._main_stream = side_stream.priority_stream(self.device.index or 0, int(hp))
+        cur = torch.cuda.current_stream(self.device)
+        self._main_stream.wait_stream(cur)
+        with torch.cuda.stream(self._main_stream):
+            for _ in range(n_steps):
                 self._train_step()
+        cur.wait_stream(self._main_stream)
 
     def commit(self, out: torch.Tensor, slot: int, window: int = 10) -> None:
         """out[slot] = mean loss over the last ``window`` steps, computed on the device."""
