@@ -4,8 +4,8 @@ The reference provides no collectives; its PyTorch experiments
 WORLD_SIZE and call NCCL themselves.  This module is what a polyflow DP trial uses on MI355X:
 
 * gradients already live in ONE flat fp32 buffer (ops/flat.py); it is cut into contiguous buckets of
-  ``bucket_mb`` (default 64 MB: large enough that each RCCL ring/tree step saturates the 7 xGMI links
-  of an MI355X, small enough that the first bucket is ready early in the backward);
+  ``bucket_mb`` (default ``"auto"``: the xGMI cost model of parallel/comm_plan.py -- the smallest bucket whose ring
+  all-reduce runs at >= 90 % of the W - 1 links' bandwidth, capped so >= 4 buckets overlap the backward);
 * a post-accumulate-grad hook on every parameter counts down its bucket; the moment a bucket is complete
   its ``all_reduce(AVG)`` is launched asynchronously (``async_op=True``: RCCL runs on its own stream),
   so communication overlaps the rest of the backward; ``finish()`` waits for the tail;
@@ -106,9 +106,11 @@ class MetricReducer:
 
 
 class FlatDDP:
-    def __init__(self, flat: FlatParams, process_group=None, bucket_mb: float = 64.0, overlap: bool = True,
+    def __init__(self, flat: FlatParams, process_group=None, bucket_mb="auto", overlap: bool = True,
                  force_collectives: bool = False, optimizer=None, shard_optimizer: bool = False):
-        """``force_collectives``: launch every bucket's all-reduce even at world 1 (hooks on), so a single-GPU
+        """``bucket_mb``: bucket size in MB of fp32-sized elements, or ``"auto"``: planned from the gradient bytes
+        and the world size by the xGMI cost model (parallel/comm_plan.py; ``self.plan`` keeps its numbers).
+        ``force_collectives``: launch every bucket's all-reduce even at world 1 (hooks on), so a single-GPU
         test executes the real RCCL path and can count the launches (``launched``).  ``optimizer``: a FusedAdamW
         whose update then runs per bucket inside the backward (``step_range_``); its ``step_()`` only closes the
         step.  ``shard_optimizer``: ZeRO-1 over the optimizer's state (see the module docstring)."""
@@ -136,7 +138,15 @@ class FlatDDP:
         self.overlap = (overlap and (self.world > 1 or self.force)) or optimizer is not None
         self.launched = 0
         self.avg_supported = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
-        bucket_elems = max(1, int(bucket_mb * 2 ** 20 / 4))
+        self.plan = None
+        if bucket_mb is None or bucket_mb == "auto":
+            from polyaxon_amd.parallel.comm_plan import plan as _plan
+
+            elem = 2 if flat.lp_grads is not None else 4  # bytes per gradient element on the wire (bf16 / fp32)
+            self.plan = _plan(flat.numel * elem, self.world)
+            bucket_elems = max(1, self.plan["bucket_bytes"] // elem)
+        else:
+            bucket_elems = max(1, int(float(bucket_mb) * 2 ** 20 / 4))
         segs = list(reversed(flat.segments))
         self.buckets: List[tuple] = []          # (lo, hi) element ranges of the flat buffer
         self.seg_bucket = {}

@@ -111,7 +111,7 @@ class ResidentTrialExecutor:
             self.wcache = cache if len(cache) else None
         self.model.train()
 
-    def enable_dp(self, bucket_mb: float = 64.0) -> None:
+    def enable_dp(self, bucket_mb="auto") -> None:
         """Data parallel over the default process group (a resident DP gang, polyflow/resident.py): bucketed,
         backward-overlapped gradient all-reduce (parallel/ddp.py FlatDDP) before every optimizer step; the DP step
         runs eagerly."""

@@ -177,7 +177,9 @@ def train_lm(argv=None) -> float:
     ap.add_argument("--model", default="gpt2_125m", choices=["gpt2_125m", "llama3_8b", "tiny"])
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--warmup_steps", type=int, default=0)
-    ap.add_argument("--bucket_mb", type=float, default=64.0)
+    ap.add_argument("--bucket_mb", type=lambda v: v if v == "auto" else float(v), default="auto",
+                    help="gradient bucket size in MB, or 'auto': planned for the world size over xGMI "
+                         "(parallel/comm_plan.py)")
     ap.add_argument("--checkpoint_activations", action="store_true")
     ap.add_argument("--beta2", type=float, default=0.95)
     ap.add_argument("--fp32_weights", action="store_true",
@@ -287,6 +289,7 @@ def train_lm(argv=None) -> float:
         dec = _gemm.decisions()
         print(json.dumps({"loss": loss_val, "tokens_per_s": round(tok_s, 1), "world": info["world"],
                           "world1_collectives": args.world1_collectives if force else "", "zero1": zero1, "bucket_launches": ddp.launched,
+                          "buckets": len(ddp.buckets), "bucket_plan": ddp.plan,
                           "params_m": round(sum(s.numel for s in flat.segments) / 1e6, 1),
                           "lm_gemm": {"mode": _gemm.mode(), "native_shapes": sum(1 for d in dec.values() if d["native"]),
                                       "shapes": len(dec), "decisions": dec}}))
