@@ -105,6 +105,18 @@ class MetricReducer:
             self.comm = None
 
 
+class _StreamWork:
+    """A collective issued on our own stream: ``wait()`` orders the CURRENT stream after it (the host never blocks),
+    as ProcessGroupNCCL's ``Work.wait()`` does."""
+
+    def __init__(self, stream: "torch.cuda.Stream"):
+        self.event = torch.cuda.Event()
+        self.event.record(stream)
+
+    def wait(self) -> None:
+        torch.cuda.current_stream().wait_event(self.event)
+
+
 class FlatDDP:
     def __init__(self, flat: FlatParams, process_group=None, bucket_mb="auto", overlap: bool = True,
                  force_collectives: bool = False, optimizer=None, shard_optimizer: bool = False):
@@ -137,7 +149,18 @@ class FlatDDP:
         self.nccl = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
         self.overlap = (overlap and (self.world > 1 or self.force)) or optimizer is not None
         self.launched = 0
-        self.avg_supported = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
+        # RCCL's AVG (a pre-multiplied sum) vs SUM + our own 1/W scale; PLX_DDP_AVG=0 selects the latter (A/B)
+        self.avg_supported = (dist.is_initialized() and dist.get_backend(process_group) == "nccl"
+                              and os.environ.get("PLX_DDP_AVG", "1") != "0")
+        # PLX_DDP_COMM=rccl: the (non-ZeRO) bucket all-reduces go through the framework's C++ RCCL communicator on a
+        # stream of their own (event-ordered after the bucket's gradient) instead of ProcessGroupNCCL's work objects
+        self._comm = self._comm_stream = None
+        if (self.nccl and (self.world > 1 or self.force) and not shard_optimizer and flat.params.is_cuda
+                and os.environ.get("PLX_DDP_COMM", "") == "rccl"):
+            from polyaxon_amd.parallel.rccl import RcclComm
+
+            self._comm = RcclComm.from_torch_distributed(process_group)
+            self._comm_stream = torch.cuda.Stream(device=flat.device)
         self.plan = None
         if bucket_mb is None or bucket_mb == "auto":
             from polyaxon_amd.parallel.comm_plan import plan as _plan
@@ -222,7 +245,14 @@ class FlatDDP:
         lo, hi, _ = self.buckets[b]
         view = self.flat.grad_view(lo, hi)
         h, div = None, None
-        if self.world > 1 or self.force:
+        if self._comm is not None:
+            self.launched += 1
+            cur = torch.cuda.current_stream(self.flat.device)
+            self._comm_stream.wait_stream(cur)
+            with torch.cuda.stream(self._comm_stream):
+                self._comm.all_reduce(view.data, op="avg")
+            h = _StreamWork(self._comm_stream)
+        elif self.world > 1 or self.force:
             self.launched += 1
             if self.avg_supported:
                 h = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)
@@ -342,6 +372,12 @@ class FlatDDP:
         if self.world > 1 or self.force:
             dist.broadcast(self.flat.params, src=src, group=self.pg)
             self.flat.sync_lp()
+
+    def close(self) -> None:
+        """Release the framework communicator (PLX_DDP_COMM=rccl)."""
+        if self._comm is not None:
+            self._comm.close()
+            self._comm = None
 
     def remove_hooks(self) -> None:
         for h in self._hooks:

@@ -118,6 +118,43 @@ def test_flat_ddp_on_rccl_backend_world1():
     assert res["rccl"] and res["loaded"] and abs(res["loss_mean"] - res["loss"]) < 1e-6
 
 
+def test_flat_ddp_bucket_all_reduce_on_the_framework_communicator():
+    """PLX_DDP_COMM=rccl: the bucket all-reduces run on csrc/rccl_comm.cpp's communicator on their own stream
+    (event-ordered) instead of ProcessGroupNCCL; at world 1 the averaged gradient equals the single-process one."""
+    res = _run("""
+        import json, os, torch
+        os.environ["PLX_DDP_COMM"] = "rccl"
+        os.environ["WORLD_SIZE"] = "1"
+        import torch.distributed as dist
+        from polyaxon_amd.models.transformer import Transformer, lm_loss, tiny_llama
+        from polyaxon_amd.ops.flat import FlatParams
+        from polyaxon_amd.ops import _native
+        from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        info = init_from_env("nccl")
+        torch.manual_seed(0)
+        m = Transformer(tiny_llama()).cuda()
+        flat = FlatParams(m, info["device"], channels_last=False)
+        ddp = FlatDDP(flat, bucket_mb=0.01, force_collectives=True)
+        tok = torch.randint(0, 256, (4, 16), device="cuda")
+        lm_loss(m(tok), tok).backward()
+        ddp.finish()
+        torch.cuda.synchronize()
+        g = flat.grads.clone()
+        torch.manual_seed(0)
+        m2 = Transformer(tiny_llama()).cuda()
+        f2 = FlatParams(m2, info["device"], channels_last=False)
+        lm_loss(m2(tok), tok).backward()
+        print(json.dumps({"own_comm": ddp._comm is not None, "buckets": len(ddp.buckets), "launched": ddp.launched,
+                          "err": float((g - f2.grads).abs().max()), "norm": float(g.norm()),
+                          "loaded": "plx_rccl" in _native._loaded}))
+        ddp.close()
+        dist.destroy_process_group()
+    """)
+    assert res["own_comm"] and res["loaded"] and res["buckets"] > 1 and res["launched"] == res["buckets"]
+    assert res["norm"] > 0 and res["err"] < 1e-5
+
+
 def test_zero1_on_rccl_backend_world1_matches_unsharded():
     """ZeRO-1 at world 1 with force_collectives on the nccl (RCCL) backend: every bucket runs the in-place
     reduce-scatter, the AdamW update of its slice on the optimizer stream and the in-place all-gather of the bf16
