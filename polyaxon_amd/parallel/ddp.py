@@ -152,11 +152,14 @@ class FlatDDP:
         # RCCL's AVG (a pre-multiplied sum) vs SUM + our own 1/W scale; PLX_DDP_AVG=0 selects the latter (A/B)
         self.avg_supported = (dist.is_initialized() and dist.get_backend(process_group) == "nccl"
                               and os.environ.get("PLX_DDP_AVG", "1") != "0")
-        # PLX_DDP_COMM=rccl: the (non-ZeRO) bucket all-reduces go through the framework's C++ RCCL communicator on a
-        # stream of their own (event-ordered after the bucket's gradient) instead of ProcessGroupNCCL's work objects
+        # The (non-ZeRO) bucket all-reduces go through the framework's C++ RCCL communicator on a stream of their own
+        # (event-ordered after the bucket's gradient), not through ProcessGroupNCCL's work objects: on the GPT-2 step
+        # with every bucket all-reduced at world 1 the process-group path cost 35 % of the step (a host / dispatch
+        # stall, not GPU work) and this one 3.4 % (profiles/r4_gpt2_world1_collectives.md).  PLX_DDP_COMM=pg: the
+        # process group's all_reduce.
         self._comm = self._comm_stream = None
         if (self.nccl and (self.world > 1 or self.force) and not shard_optimizer and flat.params.is_cuda
-                and os.environ.get("PLX_DDP_COMM", "") == "rccl"):
+                and os.environ.get("PLX_DDP_COMM", "rccl") == "rccl"):
             from polyaxon_amd.parallel.rccl import RcclComm
 
             self._comm = RcclComm.from_torch_distributed(process_group)
