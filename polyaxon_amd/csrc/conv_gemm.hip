@@ -891,6 +891,18 @@ __device__ __forceinline__ s16x4 tr_read(const char* img, int row, int col /* el
         (__attribute__((address_space(3))) s16x4*)(img + row * ROWB + pc * 16 + half * 8));
 }
 
+// 32-bit LDS address of a pointer into the dynamic LDS (for inline-asm ds instructions)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// ds_read_b64_tr_b16 the compiler cannot see (no waitcnt inserted for it; the caller waits lgkmcnt itself)
+__device__ __forceinline__ s16x4 ds_tr(uint32_t addr) {
+    s16x4 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr) : "memory");
+    return r;
+}
+
 // GATHER: 0 dense rows, 1 the pixel shifted by (dh, dw) (3x3 weight gradient), 2 the stem's packed super-pixel
 // window: chunk k / 8 of row (n, r, c) is super-pixel (2r - 3 + t / 4, c - 2 + t % 4), t = k / 8 (plx_stem_conv_fwd)
 template <int ROWB, int GATHER = 0, int BKR = BK>
@@ -1082,6 +1094,251 @@ __global__ void slab_final_kernel(const float* __restrict__ S, float* __restrict
         }
         *(float4*)dst = acc;
     }
+}
+
+// ------------------------------------------------------------------------------------------- TN GEMM, v2
+// W[slice][N1][N2] (fp32 slab per m-slice) = sum_{m in slice} A[m][N1] * Bg[m][N2] with the same gathers as v1 (CONV 0
+// dense, 1 the pixel shifted by the column's tap, 2 the stem's super-pixel window), summed by the same slab reducer.
+//
+// Why v1 is slow: one 4-wave block per CU (the slab budget keeps the grid near one block per CU) with ONE 32 KB stage
+// in flight; an L2 -> LDS fill of that size takes ~1.5 us under load against ~0.2 us of MFMAs, so v1 ran at
+// ~360 TFLOP/s on the 3x3 layers.  The per-CU LDS-DMA path needs ~100 KB in flight to run at its rate.
+//
+// v2: one block of NW = KS * NA * NB waves per CU.  Wave (g, w1, w2) owns the 64 x 64 output sub-tile (w1, w2) of a
+// (64 NA) x (64 NB) tile, and of the K-stages it computes every KS-th, starting at g: the K range is split across the
+// block's KS wave groups, whose accumulators are summed through LDS once at the end (several waves per SIMD without
+// multiplying the slab bytes).  Operands are staged as 64-column sub-images [BKT rows][128 B] (NA of A, NB of B per
+// stage; the ds_read_b64_tr_b16 swizzle of v1's 64-wide images) by buffer-resource LDS-DMA.  Each group owns RING / KS
+// slots of the LDS ring and stages its own stages into them (its waves issue the DMAs), RING / KS - 1 of them in flight
+// behind a counted vmcnt while it computes one.  Ping-pong (cdna_hip_programming.md T5): the second half of the waves
+// (the SIMD partners of the first half; KS even, so every group lies in one half) runs one barrier behind, and an
+// iteration has two barriers, [wait; barrier; MFMAs; barrier; refill DMAs], so on every SIMD one wave's MFMAs overlap
+// its partner's DMA issue, gather address math and wait.  A group refills a slot right after the barrier that follows
+// its own last read of it.  A 64-column sub-image lies inside one tap of a 3x3 gather (C % 64 == 0), so tiles may span
+// taps: the gathered B tile of a C = 64 layer is 3 taps wide.
+template <int NA, int NB, int KS, int CONV, int BKT, int RING>
+__global__ void __launch_bounds__(64 * KS * NA * NB, 1)
+wgrad_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float* __restrict__ W, int M, int N1, int N2,
+             int lda, int ldb, int kchunk, ConvGeom geo) {
+    constexpr int GW = NA * NB;                      // waves per group
+    constexpr int NW = KS * GW;
+    constexpr int R2 = RING / KS;                    // slots per group
+    constexpr int SUB = BKT * 128;                   // one 64-column sub-image
+    constexpr int STAGE = (NA + NB) * SUB;
+    constexpr int PPS = SUB / 1024;                  // 1 KB DMA pieces per sub-image (8 rows each)
+    static_assert(BKT == 32 || BKT == 64, "32- or 64-row stages");
+    static_assert(KS % 2 == 0, "ping-pong pairs the two halves of the wave groups");
+    static_assert(RING % KS == 0 && R2 >= 2, "every group owns >= 2 ring slots");
+    static_assert(RING * STAGE <= 160 * 1024, "LDS ring exceeds the CU's LDS");
+    static_assert((KS - 1) * GW * 16384 <= RING * STAGE, "the wave-group reduction reuses the ring");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr int BN1 = 64 * NA, BN2 = 64 * NB;
+    const int nt1 = N1 / BN1, nt2 = N2 / BN2, ntiles = nt1 * nt2;
+    const int nslices = (M + kchunk - 1) / kchunk;
+    const int id = xcd_remap(blockIdx.x, ntiles * nslices);   // consecutive ids (one slice's tiles) share an XCD
+    const int tile = id % ntiles, slice = id / ntiles;
+    const int n10 = (tile / nt2) * BN1, n20 = (tile % nt2) * BN2;
+    const int kbeg = slice * kchunk, kend = min(M, kbeg + kchunk);
+    const int nk = kend > kbeg ? (kend - kbeg + BKT - 1) / BKT : 0;
+    const int grp = wave / GW, wg = wave % GW, w1 = wg / NB, w2 = wg % NB;
+    const int nu = nk > grp ? (nk - grp + KS - 1) / KS : 0;   // this group's stages: s = grp + KS u, u < nu
+    const int nit = (nk + KS - 1) / KS;                        // iterations (the same for every wave: barriers)
+    const bool lag = wave >= NW / 2;
+
+    // this wave's share of its group's DMA pieces of every stage, A and B separately (a run-time choice between the
+    // two buffer resources put both in scratch): A piece pa = wg + i * GW < PA, B piece pb = wg + i * GW < PB; LDS
+    // destination (A: pa, B: PA + pb) * 1024 in the stage's slot; row (pa % PPS) * 8 + lane / 8 of sub-image pa / PPS,
+    // logical 16-B chunk (lane % 8) ^ swizzle(row)
+    constexpr int PA = NA * PPS, PB = NB * PPS;
+    constexpr int IA = (PA + GW - 1) / GW, IB = (PB + GW - 1) / GW;
+    int cnta = 0, cntb = 0, arow[IA], acol[IA], brow[IB], bcol[IB], bdh[IB], bdw[IB];
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+        const int pa = wg + i * GW, row = (pa % PPS) * 8 + (lane >> 3);
+        cnta += pa < PA ? 1 : 0;
+        arow[i] = row;
+        acol[i] = n10 + (pa / PPS) * 64 + (((lane & 7) ^ tr_swz<128>(row)) * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+        const int pb = wg + i * GW, row = (pb % PPS) * 8 + (lane >> 3);
+        const int col = n20 + (pb / PPS) * 64, lc8 = ((lane & 7) ^ tr_swz<128>(row)) * 8;
+        cntb += pb < PB ? 1 : 0;
+        brow[i] = row;
+        bdh[i] = bdw[i] = 0;
+        bcol[i] = col + lc8;
+        if constexpr (CONV == 1) {                          // a 64-column chunk lies inside one tap: (tap, channel)
+            const int t = col / geo.C;
+            bdh[i] = geo.offh[t];
+            bdw[i] = geo.offw[t];
+            bcol[i] = col - t * geo.C + lc8;
+        }
+    }
+    cnta = __builtin_amdgcn_readfirstlane(cnta);
+    cntb = __builtin_amdgcn_readfirstlane(cntb);
+    const int cnt = cnta + cntb;                            // DMAs per wave per stage
+    const __amdgpu_buffer_rsrc_t ra = buf_rsrc(A), rb = buf_rsrc(B);
+    // the gather's geometry as scalars
+    const int gH = geo.H, gW = geo.W, gS = geo.S, gWr = geo.Wr, gHr = geo.Hr;
+    const uint32_t gmWr = geo.mWr, gmHr = geo.mHr;
+    auto coords = [=](int m, int& n, int& r, int& c) {
+        const int qq = gmWr ? (int)__umulhi((uint32_t)m, gmWr) : m;
+        c = m - qq * gWr;
+        n = gmHr ? (int)__umulhi((uint32_t)qq, gmHr) : qq;
+        r = qq - n * gHr;
+    };
+    char* const gslots = smem + grp * R2 * STAGE;           // this group's slots
+
+    // stage u of this group (s = grp + KS u) into slot u % R2
+    auto issue = [&](int u) {
+        char* base = gslots + (u % R2) * STAGE;
+        const int k0 = kbeg + (grp + KS * u) * BKT;
+#pragma unroll
+        for (int i = 0; i < IA; ++i) {
+            if (i < cnta) {                                 // wave-uniform
+                const int gr = k0 + arow[i];
+                blds16(ra, gr < kend ? (uint32_t)((gr * lda + acol[i]) * 2) : OOB, base + (wg + i * GW) * 1024);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < IB; ++i) {
+            if (i < cntb) {
+                const int gr = k0 + brow[i];
+                uint32_t off;
+                if constexpr (CONV == 1) {
+                    int n, r, c;
+                    coords(gr, n, r, c);
+                    const int ih = r * gS + bdh[i], iw = c * gS + bdw[i];
+                    const bool ok = gr < kend && (unsigned)ih < (unsigned)gH && (unsigned)iw < (unsigned)gW;
+                    off = ok ? (uint32_t)((((n * gH + ih) * gW + iw) * ldb + bcol[i]) * 2) : OOB;
+                } else if constexpr (CONV == 2) {               // the stem's super-pixel window, chunk t = column / 8
+                    int n, r, c;
+                    coords(gr, n, r, c);
+                    const int t = bcol[i] >> 3, ih = 2 * r - 3 + (t >> 2), sc = c - 2 + (t & 3);
+                    const bool ok = gr < kend && t < 28 && (unsigned)ih < (unsigned)gH && (unsigned)sc < (unsigned)gW;
+                    off = ok ? (uint32_t)(((n * gH + ih) * gW + sc) * 16) : OOB;
+                } else {
+                    off = gr < kend ? (uint32_t)((gr * ldb + bcol[i]) * 2) : OOB;
+                }
+                blds16(rb, off, base + (PA + wg + i * GW) * 1024);
+            }
+        }
+    };
+    // s_waitcnt vmcnt(n) for a wave-uniform run-time n (the counter is an instruction immediate)
+    auto vm_wait = [&](int n) {
+        switch (n < 0 ? 0 : n) {
+#define PLX_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+            PLX_VMW(1) PLX_VMW(2) PLX_VMW(3) PLX_VMW(4) PLX_VMW(5) PLX_VMW(6) PLX_VMW(7) PLX_VMW(8)
+            PLX_VMW(9) PLX_VMW(10) PLX_VMW(11) PLX_VMW(12) PLX_VMW(13) PLX_VMW(14) PLX_VMW(15) PLX_VMW(16)
+            PLX_VMW(17) PLX_VMW(18) PLX_VMW(19) PLX_VMW(20) PLX_VMW(21) PLX_VMW(22) PLX_VMW(23) PLX_VMW(24)
+            PLX_VMW(25) PLX_VMW(26) PLX_VMW(27) PLX_VMW(28) PLX_VMW(29) PLX_VMW(30) PLX_VMW(31) PLX_VMW(32)
+#undef PLX_VMW
+            default:
+                if (n > 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    };
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int gi = lane & 15, g4 = lane >> 4, q = gi >> 2, pp = gi & 3;
+    // byte offsets (within a stage slot) of this lane's ds_read_b64_tr_b16 for fragment r of its A / B sub-image:
+    // T10 addressing, k-row 8 (lane / 16) + (lane % 16) / 4, columns r * 16 + 4 (lane % 4) (BKT = 32: one k-step);
+    // the second half of a fragment is 4 k-rows down, +512 B (the swizzle does not change over those rows)
+    static_assert(BKT == 32, "the asm fragment path reads one 32-deep k-step per stage");
+    uint32_t aoffr[4], boffr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int kb = 8 * g4 + q, col = r * 16 + 4 * pp;
+        const int off = kb * 128 + (((col >> 3) ^ tr_swz<128>(kb)) << 4) + ((col >> 2) & 1) * 8;
+        aoffr[r] = (uint32_t)(w1 * SUB + off);
+        boffr[r] = (uint32_t)((NA + w2) * SUB + off);
+    }
+
+    for (int u = 0; u < R2 && u < nu; ++u) issue(u);
+    if (lag) __builtin_amdgcn_s_barrier();                  // ping-pong: this half runs one barrier behind
+    for (int it = 0; it < nit; ++it) {
+        // stages [0, it] of the group must have landed; [0, min(nu, R2 + it)) were issued
+        vm_wait(cnt * (min(nu, R2 + it) - min(nu, it + 1)));
+        __builtin_amdgcn_s_barrier();                       // every wave of the group waited for its DMAs
+        if (it < nu) {                                      // wave-uniform
+            // fragment reads as inline asm: with the builtin, hipcc could not tell this slot from the ones the ring's
+            // DMAs are filling and put s_waitcnt vmcnt(0) in front of the reads -- every stage in flight drained per
+            // phase.  The asm wait below carries the fragments, so no MFMA can be scheduled above it.
+            const uint32_t sa = lds_addr(gslots + (it % R2) * STAGE);
+            s16x4 alo[4], ahi[4], blo[4], bhi[4];
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                alo[r] = ds_tr(sa + aoffr[r]);
+                ahi[r] = ds_tr(sa + aoffr[r] + 512);
+                blo[r] = ds_tr(sa + boffr[r]);
+                bhi[r] = ds_tr(sa + boffr[r] + 512);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(alo[0]), "+v"(alo[1]), "+v"(alo[2]), "+v"(alo[3]), "+v"(ahi[0]), "+v"(ahi[1]),
+                           "+v"(ahi[2]), "+v"(ahi[3]), "+v"(blo[0]), "+v"(blo[1]), "+v"(blo[2]), "+v"(blo[3]),
+                           "+v"(bhi[0]), "+v"(bhi[1]), "+v"(bhi[2]), "+v"(bhi[3]));
+            bf16x8 fa[4], fb[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                fa[r] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(alo[r], ahi[r], 0, 1, 2, 3, 4, 5, 6, 7));
+                fb[r] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo[r], bhi[r], 0, 1, 2, 3, 4, 5, 6, 7));
+            }
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the slot are done
+        __builtin_amdgcn_s_barrier();                       // ... and every wave's of the group
+        if (it + R2 < nu) issue(it + R2);                   // refill the slot just read
+    }
+    if (!lag) __builtin_amdgcn_s_barrier();                 // every wave executes the same number of barriers
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    // groups 1..KS-1 hand their sums to group 0 through LDS (lane-contiguous, no conflicts), summed in group order
+    float* red = (float*)smem;
+    if (grp > 0) {
+        float* dst = red + ((grp - 1) * GW + wg) * 4096 + lane;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dst[((a * 4 + b) * 4 + r) * 64] = acc[a][b][r];
+    }
+    __syncthreads();
+    if (grp > 0) return;
+#pragma unroll 1
+    for (int g = 1; g < KS; ++g) {
+        const float* src = red + ((g - 1) * GW + wg) * 4096 + lane;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[a][b][r] += src[((a * 4 + b) * 4 + r) * 64];
+    }
+    // D[n1][n2]: lane holds column n2 = lane & 15, rows n1 = 4 (lane >> 4) + r
+    float* slab = W + (size_t)slice * N1 * N2;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int c2 = n20 + w2 * 64 + b * 16 + gi;
+            const int r1 = n10 + w1 * 64 + a * 16 + 4 * g4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) slab[(size_t)(r1 + r) * N2 + c2] = acc[a][b][r];
+        }
 }
 
 // fp32 W[Cout][Cin] -> bf16 W[Cout][Cin] and bf16 W^T[Cin][Cout] (both used by the 1x1 conv passes)
@@ -1312,6 +1569,102 @@ int launch_tn_st(const void* A, const void* B, float* W, int M, int N1, int N2, 
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+// ---- v2 weight-gradient plan (wgrad_kernel): one block per CU, tile by the output shape, slices by a cost model
+int g_tn_v2 = 1;        // 1: wgrad_kernel (v2), 0: gemm_tn_kernel (v1)          (A/B knob plx_set_tn_v2)
+int g_tn_v2_wide = 0;   // 128-divisible outputs: 0 = 128 x 128 tiles with K split over 2 wave groups, 1 = 256 x 128 /
+                        // 128 x 256 tiles where they divide (more FLOP per staged byte, twice the slab bytes per block)
+
+struct V2Cfg { int na, nb, ks; };
+
+// 64-column sub-images per operand and wave groups: always 8 waves except the C = 64 3x3 (3 x 2 = 6)
+inline V2Cfg v2_cfg(int N1, int N2) {
+    if (N1 % 128 == 0 && N2 % 128 == 0) return {2, 2, 2};
+    if (N1 % 128 != 0) {  // N1 an odd multiple of 64 (64: ResNet layer 1)
+        if (N1 == 64 && N2 % 256 == 0) return {1, 4, 2};
+        if (N1 == 64 && N2 % 192 == 0) return {1, 3, 2};
+        if (N1 == 64 && N2 % 128 == 0) return {1, 2, 4};
+        return {1, 1, 8};
+    }
+    return N1 % 256 == 0 ? V2Cfg{4, 1, 2} : V2Cfg{2, 1, 4};  // N2 an odd multiple of 64
+}
+
+// slab reducer sizing (shared by both plans): ~1024 blocks; many slabs are first summed in groups of >= 8
+inline void plan_reducer(TnPlan& p, long plane) {
+    const long total4 = plane / 4;
+    int blocks = (int)((total4 + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    int groups = 1024 / blocks;
+    if (groups > p.slices / 8) groups = p.slices / 8;
+    if (groups < 1) groups = 1;
+    const int per_group = (p.slices + groups - 1) / groups;
+    p.groups = (p.slices + per_group - 1) / per_group;
+    p.per_group = per_group;
+    p.blocks = blocks;
+}
+
+// Slices: the grid runs one block per CU, so slices s put ceil(tiles * s / CUs) blocks on the busiest CU.  Modelled
+// time = compute (FLOP / chip rate, stretched by that quantisation) + a per-block fixed cost (ring fill + epilogue)
+// per round of blocks + the slab bytes (s + 1 planes: written, read back by the reducer) when s > 1.  Rates are
+// round numbers from the v2 isolated runs (profiles/r5_wgrad_v2.md).
+constexpr double kTnCuFlops = 3.2e12, kTnBlockUs = 2.5, kTnSlabBw = 4.5e12;
+
+inline TnPlan tn2_plan(int M, int N1, int N2, int num_cus, const V2Cfg& c) {
+    const int bn1 = 64 * c.na, bn2 = 64 * c.nb;
+    const int ntiles = (N1 / bn1) * (N2 / bn2);
+    const int cus = num_cus > 0 ? num_cus : 256;
+    const int step = 32 * c.ks;                       // rows per iteration
+    const long plane = (long)N1 * N2;
+    const double flops = 2.0 * M * plane;
+    int by_depth = M / (4 * step);                    // >= 4 iterations per block
+    if (by_depth < 1) by_depth = 1;
+    if (by_depth > 1024) by_depth = 1024;
+    int best = 1;
+    double best_t = 1e30;
+    for (int s = 1; s <= by_depth; ++s) {
+        const long blocks = (long)ntiles * s;
+        const long rounds = (blocks + cus - 1) / cus;
+        const double t = flops / (kTnCuFlops * cus) * ((double)rounds * cus / blocks) + rounds * kTnBlockUs * 1e-6 +
+                         (s > 1 ? (double)(s + 1) * plane * 4 / kTnSlabBw : 0.0);
+        if (t < best_t * 0.995) best_t = t, best = s;
+    }
+    int kchunk = (M + best - 1) / best;
+    kchunk = ((kchunk + step - 1) / step) * step;
+    TnPlan p{kchunk, (M + kchunk - 1) / kchunk, 1, 1, 0, bn1, bn2};
+    plan_reducer(p, plane);
+    return p;
+}
+
+template <int NA, int NB, int KS, int CONV>
+int launch_tn2(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
+               hipStream_t s, const ConvGeom& geo) {
+    constexpr int BKT = 32, STAGE = (NA + NB) * BKT * 128;
+    constexpr int R0 = (128 * 1024) / STAGE, R1 = R0 > 16 ? 16 : R0, RING = R1 - R1 % KS;  // <= 128 KB of ring
+    constexpr int LDS = RING * STAGE;
+    auto k = wgrad_kernel<NA, NB, KS, CONV, BKT, RING>;
+    static int attr = set_lds(k, LDS);
+    if (attr) return attr;
+    const int ntiles = (N1 / (64 * NA)) * (N2 / (64 * NB));
+    hipLaunchKernelGGL(k, dim3(ntiles * plan.slices), dim3(64 * NA * NB * KS), LDS, s, (const __bf16*)A,
+                       (const __bf16*)B, W, M, N1, N2, lda, ldb, plan.kchunk, geo);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <int CONV>
+int dispatch_tn2(const V2Cfg& c, const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb,
+                 const TnPlan& plan, hipStream_t s, const ConvGeom& geo) {
+    if constexpr (CONV == 2) {  // the stem: 64 x 256
+        if (c.na == 1 && c.nb == 4 && c.ks == 2) return launch_tn2<1, 4, 2, 2>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo);
+        return -1;
+    } else {
+#define PLX_TN2(a, b, k) \
+    if (c.na == a && c.nb == b && c.ks == k) return launch_tn2<a, b, k, CONV>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo);
+        PLX_TN2(2, 2, 2) PLX_TN2(1, 4, 2) PLX_TN2(1, 3, 2) PLX_TN2(1, 2, 4) PLX_TN2(1, 1, 8) PLX_TN2(4, 1, 2)
+        PLX_TN2(2, 1, 4)
+#undef PLX_TN2
+        return -1;
+    }
+}
+
 template <int BN1, int BN2, int WG1, int WG2, int CONV = 0>
 int launch_tn(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
               const void* zero, hipStream_t s, ConvGeom geo = {}) {
@@ -1420,6 +1773,13 @@ void plx_set_tn_stages(int n, int bk) {
 // A/B knob: wide (256 x 128 / 128 x 256) weight-gradient tiles (see g_tn_wide); set before sizing workspaces
 void plx_set_tn_wide(int on) { g_tn_wide = on ? 1 : 0; }
 
+// A/B knob: weight-gradient kernel v2 (wgrad_kernel, 1) or v1 (gemm_tn_kernel, 0); wide: v2's 256 x 128 tiles
+// (workspace queries size for every plan, so either may be toggled after sizing)
+void plx_set_tn_v2(int on, int wide) {
+    g_tn_v2 = on ? 1 : 0;
+    if (wide >= 0) g_tn_v2_wide = wide ? 1 : 0;
+}
+
 // weight-gradient slicing knobs; workspace sizes follow them, so set before sizing / launching
 void plx_set_tn_plan(int blocks_per_cu, int slab_mb) {
     if (blocks_per_cu >= 0) g_tn_blocks_per_cu = blocks_per_cu;  // 0: by problem size (tn_plan)
@@ -1437,8 +1797,18 @@ long plx_gemm_tn_workspace(int M, int N1, int N2, int num_cus) {
     if (M <= 0 || N1 % 64 || N2 % 64) return -1;
     // the larger of the narrow and wide plans, whatever the knob: a size memoised before plx_set_tn_wide still fits
     const TnPlan a = tn_plan_tile(M, N1, N2, num_cus, 0, false), b = tn_plan_tile(M, N1, N2, num_cus, 0, true);
-    const long na = a.slices + (a.groups > 1 ? a.groups : 0), nb = b.slices + (b.groups > 1 ? b.groups : 0);
-    return (na > nb ? na : nb) * N1 * N2;
+    long n = a.slices + (a.groups > 1 ? a.groups : 0);
+    const long nb = b.slices + (b.groups > 1 ? b.groups : 0);
+    if (nb > n) n = nb;
+    for (int wide = 0; wide < 2; ++wide) {  // both v2 tilings, whatever the knobs
+        const int keep = g_tn_v2_wide;
+        g_tn_v2_wide = wide;
+        const TnPlan c = tn2_plan(M, N1, N2, num_cus, v2_cfg(N1, N2));
+        g_tn_v2_wide = keep;
+        const long nc = c.slices + (c.groups > 1 ? c.groups : 0);
+        if (nc > n) n = nc;
+    }
+    return n * N1 * N2;
 }
 
 }  // extern "C"
@@ -1447,9 +1817,13 @@ namespace {
 template <int CONV>
 int run_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int N2, int lda, int ldb, int ldc,
            const void* zero, int num_cus, int accumulate, hipStream_t s, ConvGeom geo, int bpc = 0) {
-    const TnPlan plan = tn_plan(M, N1, N2, num_cus, bpc);
+    const bool v2 = g_tn_v2 != 0;
+    const V2Cfg cfg = v2_cfg(N1, N2);
+    const TnPlan plan = v2 ? tn2_plan(M, N1, N2, num_cus, cfg) : tn_plan(M, N1, N2, num_cus, bpc);
     int rc;
-    if (plan.bn1 == 256)
+    if (v2)
+        rc = dispatch_tn2<CONV>(cfg, A, B, ws, M, N1, N2, lda, ldb, plan, s, geo);
+    else if (plan.bn1 == 256)
         rc = launch_tn_st<256, 128, 2, 2, CONV, 2, 32>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
     else if (plan.bn2 == 256)
         rc = launch_tn_st<128, 256, 2, 2, CONV, 2, 32>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
@@ -1783,11 +2157,18 @@ int plx_stem_pack_weight(const float* w, long s_co, long s_ci, long s_kh, long s
 
 constexpr int kStemWgradBpc = 4;  // blocks per CU for the stem's weight gradient (alone on the GPU at the end)
 
+// slab planes (slices + reducer groups) of the stem's weight gradient under either plan
+static long stem_slabs(int M, int num_cus) {
+    const TnPlan p = tn_plan(M, 64, 256, num_cus, kStemWgradBpc);
+    const TnPlan q = tn2_plan(M, 64, 256, num_cus, v2_cfg(64, 256));
+    const long a = p.slices + (p.groups > 1 ? p.groups : 0), b = q.slices + (q.groups > 1 ? q.groups : 0);
+    return a > b ? a : b;
+}
+
 // floats of workspace plx_stem_conv_wgrad needs: the slab reduction's (as plx_gemm_tn_workspace) + dW packed [64][256]
 long plx_stem_conv_wgrad_workspace(int N, int H, int W, int num_cus) {
     const int M = N * ((H - 1) / 2 + 1) * ((W - 1) / 2 + 1);
-    const TnPlan p = tn_plan(M, 64, 256, num_cus, kStemWgradBpc);
-    return (long)(p.slices + (p.groups > 1 ? p.groups : 0)) * 64 * 256 + 64 * 256;
+    return stem_slabs(M, num_cus) * 64 * 256 + 64 * 256;
 }
 
 // dw (fp32 [64][3][7][7], strides s_*; (+)= with accumulate) = the stem's weight gradient from dy (NHWC bf16
@@ -1804,8 +2185,7 @@ int plx_stem_conv_wgrad(const void* dy, const void* xp, float* dw, long s_co, lo
     g.mWr = div_magic(g.Wr);
     g.mHr = div_magic(g.Hr);
     const int M = N * g.Hr * g.Wr;
-    const TnPlan p = tn_plan(M, 64, 256, num_cus, kStemWgradBpc);
-    float* packed = ws + (long)(p.slices + (p.groups > 1 ? p.groups : 0)) * 64 * 256;
+    float* packed = ws + stem_slabs(M, num_cus) * 64 * 256;
     hipStream_t s = (hipStream_t)stream;
     const int rc = run_tn<2>(dy, xp, packed, ws, M, 64, 256, 64, 8, 256, zero, num_cus, 0, s, g, kStemWgradBpc);
     if (rc) return rc;

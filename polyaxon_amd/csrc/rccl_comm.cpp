@@ -8,7 +8,7 @@
 // so it overlaps compute and can be captured in a hipGraph.
 //
 //   plx_rccl_unique_id(out[128])                          rank 0 creates, ships via any side channel
-//   plx_rccl_init(id, nranks, rank, device) -> comm*
+//   plx_rccl_init(id, nranks, rank, device) -> handle (an integer id, never reused)
 //   plx_rccl_all_reduce / all_gather / reduce_scatter / broadcast (dtype: 0 f32, 1 bf16, 2 f16, 3 f64, 4 i32)
 //   plx_rccl_bus_bw(comm, bytes, iters, stream) -> measured algorithm + bus bandwidth of all-reduce
 //   plx_rccl_destroy(comm)
@@ -18,7 +18,8 @@
 #include <string.h>
 
 #include <mutex>
-#include <unordered_set>
+#include <memory>
+#include <unordered_map>
 
 #define PLX_API extern "C" __attribute__((visibility("default")))
 
@@ -45,19 +46,25 @@ ncclRedOp_t op_of(int o) {
 }
 
 struct Comm {
-  ncclComm_t comm;
-  int nranks, rank, device;
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0, device = 0;
+  ~Comm() {
+    if (comm) ncclCommDestroy(comm);  // the last holder of a destroyed handle (see plx_rccl_destroy)
+  }
 };
 
-// Live communicators: every entry point validates its handle here, so a call on a destroyed (or never created)
-// communicator returns ncclInvalidArgument instead of dereferencing freed memory.
+// Live communicators by handle.  A handle is a monotonically increasing integer (never an address), so a destroyed
+// handle can never alias a later communicator; every entry point takes a shared_ptr copy under the lock and runs its
+// collective on that copy, so a plx_rccl_destroy on another thread cannot free the communicator mid-call: the
+// ncclComm is destroyed when the last in-flight call drops its reference.
 std::mutex g_mu;
-std::unordered_set<Comm*> g_live;
+std::unordered_map<uintptr_t, std::shared_ptr<Comm>> g_live;
+uintptr_t g_next = 1;
 
-Comm* live(void* h) {
+std::shared_ptr<Comm> live(void* h) {
   std::lock_guard<std::mutex> lk(g_mu);
-  Comm* c = static_cast<Comm*>(h);
-  return g_live.count(c) ? c : nullptr;
+  auto it = g_live.find(reinterpret_cast<uintptr_t>(h));
+  return it == g_live.end() ? nullptr : it->second;
 }
 
 }  // namespace
@@ -79,43 +86,48 @@ PLX_API void* plx_rccl_init(const char* id_bytes, int nranks, int rank, int devi
   }
   ncclUniqueId id;
   memcpy(&id, id_bytes, sizeof(id));
-  Comm* c = new Comm{nullptr, nranks, rank, device};
-  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  auto c = std::make_shared<Comm>();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  ncclComm_t comm = nullptr;
+  ncclResult_t r = ncclCommInitRank(&comm, nranks, id, rank);
   if (r != ncclSuccess) {
     *err = (int)r;
-    delete c;
     return nullptr;
   }
+  c->comm = comm;
   *err = 0;
   std::lock_guard<std::mutex> lk(g_mu);
-  g_live.insert(c);
-  return c;
+  const uintptr_t h = g_next++;
+  g_live.emplace(h, std::move(c));
+  return reinterpret_cast<void*>(h);
 }
 
 PLX_API int plx_rccl_all_reduce(void* h, const void* send, void* recv, int64_t count, int dtype, int op,
                                 hipStream_t stream) {
-  Comm* c = live(h);
+  const std::shared_ptr<Comm> c = live(h);
   if (!c) return (int)ncclInvalidArgument;
   return (int)ncclAllReduce(send, recv, (size_t)count, dtype_of(dtype), op_of(op), c->comm, stream);
 }
 
 PLX_API int plx_rccl_all_gather(void* h, const void* send, void* recv, int64_t count_per_rank, int dtype,
                                 hipStream_t stream) {
-  Comm* c = live(h);
+  const std::shared_ptr<Comm> c = live(h);
   if (!c) return (int)ncclInvalidArgument;
   return (int)ncclAllGather(send, recv, (size_t)count_per_rank, dtype_of(dtype), c->comm, stream);
 }
 
 PLX_API int plx_rccl_reduce_scatter(void* h, const void* send, void* recv, int64_t count_per_rank, int dtype, int op,
                                     hipStream_t stream) {
-  Comm* c = live(h);
+  const std::shared_ptr<Comm> c = live(h);
   if (!c) return (int)ncclInvalidArgument;
   return (int)ncclReduceScatter(send, recv, (size_t)count_per_rank, dtype_of(dtype), op_of(op), c->comm, stream);
 }
 
 PLX_API int plx_rccl_broadcast(void* h, const void* send, void* recv, int64_t count, int dtype, int root,
                                hipStream_t stream) {
-  Comm* c = live(h);
+  const std::shared_ptr<Comm> c = live(h);
   if (!c) return (int)ncclInvalidArgument;
   return (int)ncclBroadcast(send, recv, (size_t)count, dtype_of(dtype), root, c->comm, stream);
 }
@@ -126,7 +138,7 @@ PLX_API int plx_rccl_broadcast(void* h, const void* send, void* recv, int64_t co
 PLX_API int plx_rccl_bus_bw(void* h, void* buf, int64_t bytes, int iters, hipStream_t stream, double* algbw,
                             double* busbw) {
   *algbw = *busbw = 0.0;
-  Comm* c = live(h);
+  const std::shared_ptr<Comm> c = live(h);
   if (!c) return (int)ncclInvalidArgument;
   if (bytes < 4 || iters < 1) return (int)ncclInvalidArgument;
   const size_t count = (size_t)bytes / 4;
@@ -165,14 +177,17 @@ PLX_API int plx_rccl_bus_bw(void* h, void* buf, int64_t bytes, int iters, hipStr
 }
 
 PLX_API int plx_rccl_destroy(void* h) {
-  Comm* c = live(h);
-  if (!c) return h ? (int)ncclInvalidArgument : 0;
+  std::shared_ptr<Comm> c;
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    g_live.erase(c);
+    auto it = g_live.find(reinterpret_cast<uintptr_t>(h));
+    if (it == g_live.end()) return h ? (int)ncclInvalidArgument : 0;
+    c = std::move(it->second);
+    g_live.erase(it);
   }
-  ncclResult_t r = ncclCommDestroy(c->comm);
-  delete c;
+  if (c.use_count() > 1) return 0;  // a call in flight holds it: destroyed when that call returns (~Comm)
+  const ncclResult_t r = ncclCommDestroy(c->comm);
+  c->comm = nullptr;
   return (int)r;
 }
 

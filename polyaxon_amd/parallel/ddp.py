@@ -49,14 +49,16 @@ from polyaxon_amd.ops.flat import FlatParams
 
 def init_from_env(backend: Optional[str] = None, device: Optional[torch.device] = None) -> dict:
     """Initialise torch.distributed from the polyflow / torchrun env contract (RANK, WORLD_SIZE,
-    MASTER_ADDR, MASTER_PORT, LOCAL_RANK). Returns {rank, world, local_rank, device}."""
+    MASTER_ADDR, MASTER_PORT, LOCAL_RANK). Returns {rank, world, local_rank, device}.  The default backend is gloo:
+    the process group is the rendezvous (it ships the RCCL unique id and the host-side control traffic); a DP trial's
+    device collectives run on ONE framework communicator (parallel/comm.py), not on ProcessGroupNCCL's."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:  # the rendezvous: device collectives go through parallel/comm.py's communicator
+        backend = "gloo"
     if device is None:
-        device = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
+        device = torch.device("cuda", local) if (backend == "nccl" or torch.cuda.is_available()) else torch.device("cpu")
     if device.type == "cuda":
         torch.cuda.set_device(device)
     if world > 1 and not dist.is_initialized():
@@ -74,34 +76,35 @@ def init_from_env(backend: Optional[str] = None, device: Optional[torch.device] 
 class MetricReducer:
     """Cross-rank mean of a DP trial's scalar metrics (the loss the tracking client logs, the final result).
 
-    SURVEY.md §2.3 names the metric all-reduce as a framework-owned collective: on the GPU it runs on the C++ RCCL
-    communicator (csrc/rccl_comm.cpp, one ``ncclAllReduce(avg)`` of a few floats on the current HIP stream, no
-    ProcessGroup layer and no host sync); on the CPU (gloo tests) through torch.distributed.  World 1: identity."""
+    SURVEY.md §2.3 names the metric all-reduce as a framework-owned collective: it runs on the process's shared
+    communicator (parallel/comm.py: RCCL on the GPU -- one ``ncclAllReduce(avg)`` of a few floats on the current HIP
+    stream, no host sync --, the gloo shim on the CPU), the same one FlatDDP uses.  World 1: identity."""
 
     def __init__(self, device: torch.device, process_group=None, force_comm: bool = False):
-        """``force_comm``: build the RCCL communicator even at world 1 (a single-GPU test of the real path)."""
+        """``force_comm``: take the communicator even at world 1 (a single-GPU test of the real path)."""
         self.device = device
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.comm = None
-        if (self.world > 1 or force_comm) and device.type == "cuda" and dist.is_initialized():
-            from polyaxon_amd.parallel.rccl import RcclComm
+        if (self.world > 1 or force_comm) and dist.is_initialized():
+            from polyaxon_amd.parallel import comm as _comm
 
-            self.comm = RcclComm.from_torch_distributed(process_group)
+            self.comm = _comm.acquire(process_group, device)
 
     def mean(self, t: torch.Tensor) -> torch.Tensor:
         """Mean over ranks of a small float tensor (returned new; the input is untouched)."""
         out = t.detach().float().reshape(-1).clone()
-        if self.comm is not None:
-            return self.comm.all_reduce(out, op="avg")
-        if self.world == 1:
+        if self.comm is None:
             return out
-        dist.all_reduce(out, op=dist.ReduceOp.SUM, group=self.pg)
-        return out.div_(self.world)
+        if self.comm.native_avg:
+            return self.comm.all_reduce(out, op="avg")
+        return self.comm.all_reduce(out, op="sum").div_(self.world)
 
     def close(self) -> None:
         if self.comm is not None:
-            self.comm.close()
+            from polyaxon_amd.parallel import comm as _comm
+
+            _comm.release(self.comm)
             self.comm = None
 
 
@@ -146,24 +149,29 @@ class FlatDDP:
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
         self.force = bool(force_collectives) and dist.is_initialized()
+        self.coll = self.world > 1 or self.force            # collectives run (world > 1, or forced at world 1)
         self.nccl = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
-        self.overlap = (overlap and (self.world > 1 or self.force)) or optimizer is not None
+        self.overlap = (overlap and self.coll) or optimizer is not None
         self.launched = 0
-        # RCCL's AVG (a pre-multiplied sum) vs SUM + our own 1/W scale; PLX_DDP_AVG=0 selects the latter (A/B)
-        self.avg_supported = (dist.is_initialized() and dist.get_backend(process_group) == "nccl"
-                              and os.environ.get("PLX_DDP_AVG", "1") != "0")
-        # The (non-ZeRO) bucket all-reduces go through the framework's C++ RCCL communicator on a stream of their own
-        # (event-ordered after the bucket's gradient), not through ProcessGroupNCCL's work objects: on the GPT-2 step
-        # with every bucket all-reduced at world 1 the process-group path cost 35 % of the step (a host / dispatch
-        # stall, not GPU work) and this one 3.4 % (profiles/r4_gpt2_world1_collectives.md).  PLX_DDP_COMM=pg: the
-        # process group's all_reduce.
+        # Every collective of the trial -- bucket all-reduces, ZeRO-1's reduce-scatter / all-gather, the parameter
+        # broadcast -- runs on the process's ONE framework communicator (parallel/comm.py: RCCL on the GPU, the gloo
+        # shim on the CPU, so the CPU tests execute this same path).  GPU bucket all-reduces run on a stream of their
+        # own, event-ordered after the bucket's gradient: through ProcessGroupNCCL's work objects the GPT-2 step lost
+        # 35 % at world 1 to a host / dispatch stall, this way 3.4 % (profiles/r4_gpt2_world1_collectives.md).
+        # PLX_DDP_COMM=pg: torch.distributed's own collectives over the process group (A/B).
         self._comm = self._comm_stream = None
-        if (self.nccl and (self.world > 1 or self.force) and not shard_optimizer and flat.params.is_cuda
-                and os.environ.get("PLX_DDP_COMM", "rccl") == "rccl"):
-            from polyaxon_amd.parallel.rccl import RcclComm
+        if self.coll and os.environ.get("PLX_DDP_COMM", "comm") != "pg":
+            from polyaxon_amd.parallel import comm as _comm
 
-            self._comm = RcclComm.from_torch_distributed(process_group)
-            self._comm_stream = torch.cuda.Stream(device=flat.device)
+            self._comm = _comm.acquire(process_group, flat.device)
+            if not self._comm.synchronous and not shard_optimizer:
+                self._comm_stream = torch.cuda.Stream(device=flat.device)
+        # an average in the collective (RCCL's AVG: a pre-multiplied sum) vs SUM + our own 1/W scale; PLX_DDP_AVG=0
+        # selects the latter (A/B, read by RcclComm.native_avg)
+        if self._comm is not None:
+            self.avg_supported = bool(self._comm.native_avg)
+        else:
+            self.avg_supported = self.nccl and os.environ.get("PLX_DDP_AVG", "1") != "0"
         self.plan = None
         if bucket_mb is None or bucket_mb == "auto":
             from polyaxon_amd.parallel.comm_plan import plan as _plan
@@ -250,12 +258,19 @@ class FlatDDP:
         h, div = None, None
         if self._comm is not None:
             self.launched += 1
-            cur = torch.cuda.current_stream(self.flat.device)
-            self._comm_stream.wait_stream(cur)
-            with torch.cuda.stream(self._comm_stream):
-                self._comm.all_reduce(view.data, op="avg")
-            h = _StreamWork(self._comm_stream)
-        elif self.world > 1 or self.force:
+            op = "avg" if self.avg_supported else "sum"
+            if self._comm.synchronous:
+                self._comm.all_reduce(view.data, op=op)
+                div = None if self.avg_supported else view
+            else:
+                cur = torch.cuda.current_stream(self.flat.device)
+                self._comm_stream.wait_stream(cur)
+                with torch.cuda.stream(self._comm_stream):
+                    self._comm.all_reduce(view.data, op=op)
+                    if not self.avg_supported:
+                        view.data.div_(self.world)  # on the collective's stream, before anyone waits on it
+                h = _StreamWork(self._comm_stream)
+        elif self.coll:
             self.launched += 1
             if self.avg_supported:
                 h = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)
@@ -300,12 +315,16 @@ class FlatDDP:
         if cuda:
             self._side.wait_stream(torch.cuda.current_stream(f.device))
         ctx = torch.cuda.stream(self._side) if cuda else _nullcontext()
+        c = self._comm
         with ctx:
             if coll:
                 self.launched += 1
+                cop = "avg" if self.avg_supported else "sum"
                 if main:
                     out, inp = gv(own_lo, own_hi), gv(lo, rem_lo)
-                    if self.nccl:  # in place: the output is this rank's slice of the input (NCCL's in-place form)
+                    if c is not None:  # in place: the output is this rank's slice of the input (NCCL's in-place form)
+                        c.reduce_scatter_into(out, inp, op=cop)
+                    elif self.nccl:
                         dist.reduce_scatter_tensor(out, inp, op=op, group=self.pg, async_op=True).wait()
                     else:
                         tmp = torch.empty_like(out)
@@ -315,7 +334,11 @@ class FlatDDP:
                         out.div_(w)
                 if rem_lo < hi:
                     rv = gv(rem_lo, hi)
-                    dist.all_reduce(rv, op=op, group=self.pg, async_op=cuda).wait() if cuda else \
+                    if c is not None:
+                        c.all_reduce(rv, op=cop)
+                    elif cuda:
+                        dist.all_reduce(rv, op=op, group=self.pg, async_op=True).wait()
+                    else:
                         dist.all_reduce(rv, op=op, group=self.pg)
                     if not self.avg_supported:
                         rv.div_(w)
@@ -332,7 +355,9 @@ class FlatDDP:
             if coll and main:
                 buf = f.lp_params.data if lp else f.params.data
                 full, mine = buf[lo:rem_lo], buf[own_lo:own_hi]
-                if self.nccl:  # in place: this rank's slice already sits at its place in the output
+                if c is not None:  # GPU: on the optimizer stream, after the update (finish() joins that stream)
+                    c.all_gather_into(full, mine)
+                elif self.nccl:  # in place: this rank's slice already sits at its place in the output
                     self._handles.append((dist.all_gather_into_tensor(full, mine, group=self.pg, async_op=True), None))
                 else:
                     dist.all_gather_into_tensor(full, mine.clone(), group=self.pg)
@@ -340,19 +365,22 @@ class FlatDDP:
     def gather_master(self) -> None:
         """ZeRO-1 in lp mode: refresh the fp32 master of the slices other ranks own (all-gather per bucket), e.g.
         before a checkpoint; the bf16 model weights are always current."""
-        if not self.zero or not (self.world > 1 or self.force):
+        if not self.zero or not self.coll:
             return
         f = self.flat
         for (lo, hi, _), (s, main, _) in zip(self.buckets, self.shards):
             if main and f.lp_params is not None and hi <= f.n_decay:
                 own = f.params.data[lo + self.rank * s: lo + (self.rank + 1) * s]
-                dist.all_gather_into_tensor(f.params.data[lo:lo + main], own if self.nccl else own.clone(),
-                                            group=self.pg)
+                if self._comm is not None:
+                    self._comm.all_gather_into(f.params.data[lo:lo + main], own)
+                else:
+                    dist.all_gather_into_tensor(f.params.data[lo:lo + main], own if self.nccl else own.clone(),
+                                                group=self.pg)
 
     def finish(self) -> None:
         """Call after backward(): launches any bucket not fired by hooks, waits, averages (and, with an optimizer
         in the backward, has the main stream wait for every bucket's update)."""
-        if self.world == 1 and not self.force and self.opt is None:
+        if not self.coll and self.opt is None:
             return
         if not self.overlap:
             for b in range(len(self.buckets)):
@@ -372,14 +400,22 @@ class FlatDDP:
 
     def broadcast_params(self, src: int = 0) -> None:
         """Make every rank start from rank ``src``'s weights (one collective over the flat buffer)."""
-        if self.world > 1 or self.force:
+        if not self.coll:
+            return
+        if self._comm is not None:
+            self._comm.broadcast(self.flat.params.data, root=src)
+        else:
             dist.broadcast(self.flat.params, src=src, group=self.pg)
-            self.flat.sync_lp()
+        self.flat.sync_lp()
 
     def close(self) -> None:
-        """Release the framework communicator (PLX_DDP_COMM=rccl)."""
+        """Drop this FlatDDP's hold on the process's framework communicator (the last holder closes it)."""
         if self._comm is not None:
-            self._comm.close()
+            from polyaxon_amd.parallel import comm as _comm
+
+            if self._comm_stream is not None:
+                self._comm_stream.synchronize()
+            _comm.release(self._comm)
             self._comm = None
 
     def remove_hooks(self) -> None:

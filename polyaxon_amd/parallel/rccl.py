@@ -1,6 +1,6 @@
 """Python face of the framework RCCL communicator (csrc/rccl_comm.cpp) + an xGMI bandwidth probe.
 
-    comm = RcclComm.from_torch_distributed()          # id shipped over the existing process group
+    comm = RcclComm.from_torch_distributed()          # id shipped over the process group (the gloo rendezvous)
     comm.all_reduce(t)                                  # in place, on the current HIP stream
     python -m torch.distributed.run --nproc-per-node 8 -m polyaxon_amd.parallel.rccl   # busbw table
 
@@ -27,6 +27,10 @@ class RcclError(RuntimeError):
 
 
 class RcclComm:
+    synchronous = False  # collectives are enqueued on the current HIP stream
+    # RCCL's AVG (a pre-multiplied sum) vs SUM + the caller's 1/W scale (PLX_DDP_AVG=0, A/B)
+    native_avg = os.environ.get("PLX_DDP_AVG", "1") != "0"
+
     def __init__(self, unique_id: bytes, nranks: int, rank: int, device: int):
         self.lib = _native.lib("plx_rccl")
         err = ctypes.c_int(0)
@@ -45,13 +49,19 @@ class RcclComm:
         return buf.raw
 
     @classmethod
-    def from_torch_distributed(cls, group=None) -> "RcclComm":
+    def from_torch_distributed(cls, group=None, device=None) -> "RcclComm":
+        """Rank 0 of ``group`` creates the unique id and ships it over the group (gloo or nccl: any backend that
+        carries Python objects); ``device`` defaults to the current one."""
         import torch.distributed as dist
+
+        from polyaxon_amd.parallel.comm import group_rank0
 
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         obj: List = [cls.new_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0, group=group)
-        return cls(obj[0], world, rank, torch.cuda.current_device())
+        # src is a GLOBAL rank: the group's rank 0 (a subgroup without global rank 0 hung or errored with src=0)
+        dist.broadcast_object_list(obj, src=group_rank0(group), group=group)
+        idx = torch.device(device).index if device is not None else None
+        return cls(obj[0], world, rank, torch.cuda.current_device() if idx is None else idx)
 
     def _check(self, rc: int, what: str) -> None:
         if not self.h:
@@ -82,6 +92,24 @@ class RcclComm:
                                                      DTYPES[t.dtype], OPS[op], self._stream()), "reduce_scatter")
         return out
 
+    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        """``out`` (numel n) = this rank's n-slice of the reduction of ``inp`` (numel n * W); in place when ``out`` is
+        that slice of ``inp`` (NCCL's in-place form)."""
+        if inp.numel() != out.numel() * self.nranks:
+            raise ValueError("reduce_scatter_into: input numel must be W x output numel")
+        self._check(self.lib.plx_rccl_reduce_scatter(self.h, inp.data_ptr(), out.data_ptr(), out.numel(),
+                                                     DTYPES[out.dtype], OPS[op], self._stream()), "reduce_scatter")
+        return out
+
+    def all_gather_into(self, full: torch.Tensor, mine: torch.Tensor) -> torch.Tensor:
+        """``full`` (numel n * W) = every rank's ``mine`` (numel n) in rank order; in place when ``mine`` is this rank's
+        slice of ``full``."""
+        if full.numel() != mine.numel() * self.nranks:
+            raise ValueError("all_gather_into: output numel must be W x input numel")
+        self._check(self.lib.plx_rccl_all_gather(self.h, mine.data_ptr(), full.data_ptr(), mine.numel(),
+                                                 DTYPES[mine.dtype], self._stream()), "all_gather")
+        return full
+
     def broadcast(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
         self._check(self.lib.plx_rccl_broadcast(self.h, t.data_ptr(), t.data_ptr(), t.numel(), DTYPES[t.dtype], root,
                                                 self._stream()), "broadcast")
@@ -105,8 +133,8 @@ def main() -> None:
 
     from polyaxon_amd.parallel.ddp import init_from_env
 
-    info = init_from_env("nccl")
-    comm = RcclComm.from_torch_distributed()
+    info = init_from_env("gloo", device=torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0"))))
+    comm = RcclComm.from_torch_distributed(device=info["device"])
     x = torch.full((1024,), float(info["rank"] + 1), device=info["device"])
     comm.all_reduce(x)
     torch.cuda.synchronize()

@@ -253,6 +253,17 @@ class ResidentWorker:
             torch.cuda.set_device(self.device)
         self.gang = _GangGroup(rank, world, self.device)
 
+    def close_gang(self) -> None:
+        """Release the gang's framework communicator (the executor's FlatDDP hold and the metric mean's) and the
+        rendezvous; a no-op outside a gang."""
+        if self.gang is None:
+            return
+        ex = getattr(getattr(self, "program", None), "executor", None)
+        if ex is not None and ex.ddp is not None:
+            ex.ddp.close()
+        self.gang.close()
+        self.gang = None
+
     # ------------------------------------------------------------------ build
     def build(self) -> Dict[str, Any]:
         import torch
@@ -757,10 +768,11 @@ class ResidentWorker:
 
 class _GangGroup:
     """A DP gang of resident workers (``environment.resources.gpu: N`` with a resident executor): one process per
-    device, ranks from the pool's env (PLX_RESIDENT_RANK / _WORLD, MASTER_ADDR / MASTER_PORT).  Gradients go over the
-    data process group (``nccl`` = RCCL on the GPU, gloo on CPU); the control stream -- the scheduler messages rank 0
-    receives -- is re-broadcast to the other ranks over a gloo group, so every rank handles the same messages at the
-    same program points and runs the same trials in the same order."""
+    device, ranks from the pool's env (PLX_RESIDENT_RANK / _WORLD, MASTER_ADDR / MASTER_PORT).  The process group is a
+    gloo rendezvous: it carries the control stream -- the scheduler messages rank 0 receives, re-broadcast to the other
+    ranks so every rank handles the same messages at the same program points and runs the same trials in the same
+    order -- and ships the RCCL unique id.  Every device collective (the executor's gradient buckets, the metric-table
+    mean before each rung decision) runs on the process's one framework communicator (parallel/comm.py)."""
 
     def __init__(self, rank: int, world: int, device):
         import datetime
@@ -769,29 +781,39 @@ class _GangGroup:
         import torch.distributed as dist
 
         self.rank, self.world = rank, world
-        cuda = torch.device(device).type == "cuda"
+        self.device = torch.device(device)
         long = datetime.timedelta(days=7)  # an idle executor blocks in the control broadcast between groups
-        dist.init_process_group("nccl" if cuda else "gloo", rank=rank, world_size=world, timeout=long,
-                                **({"device_id": torch.device(device)} if cuda else {}))
-        self.data = None  # the default group
-        self.ctl = dist.new_group(backend="gloo", timeout=long) if cuda else None
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=long)
+        self.comm = None  # acquired on first use (collective: every rank reaches it at the same program point)
 
     def broadcast(self, obj):
         import torch.distributed as dist
 
         box = [obj]
-        dist.broadcast_object_list(box, src=0, group=self.ctl)
+        dist.broadcast_object_list(box, src=0)
         return box[0]
 
     def mean_(self, t) -> None:
         """In-place cross-rank mean of a metric table (every rank then takes the same promotion decisions)."""
+        from polyaxon_amd.parallel import comm as _comm
+
+        if self.comm is None:
+            self.comm = _comm.acquire(None, t.device)
+        if self.comm.native_avg:
+            self.comm.all_reduce(t, op="avg")
+        else:
+            self.comm.all_reduce(t, op="sum").div_(self.world)
+
+    def close(self) -> None:
         import torch.distributed as dist
 
-        if t.is_cuda:
-            dist.all_reduce(t, op=dist.ReduceOp.AVG)
-        else:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            t.div_(self.world)
+        from polyaxon_amd.parallel import comm as _comm
+
+        if self.comm is not None:
+            _comm.release(self.comm)
+            self.comm = None
+        if dist.is_initialized():
+            dist.destroy_process_group()
 
 
 class _LeaderChannel:
@@ -858,10 +880,13 @@ def serve_forever(worker: ResidentWorker, chan: Channel) -> str:
         # the scheduler talks to rank 0; the other ranks follow its control stream (their own channel only carries
         # the init handshake, and their exit is how the pool notices a lost rank)
         chan = _LeaderChannel(chan, worker.gang) if worker.gang.rank == 0 else _FollowerChannel(worker.gang)
-    while True:
-        r = worker.serve(chan)
-        if r in ("shutdown", "eof"):
-            return r
+    try:
+        while True:
+            r = worker.serve(chan)
+            if r in ("shutdown", "eof"):
+                return r
+    finally:
+        worker.close_gang()
 
 
 def main(argv=None) -> int:

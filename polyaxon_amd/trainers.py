@@ -191,15 +191,18 @@ def train_lm(argv=None) -> float:
                          "program (ops/synth.py SyntheticTokens: learnable, hyper-parameter sensitive)")
     ap.add_argument("--period", type=int, default=64, help="copy task: phrase length (seq must be a multiple)")
     ap.add_argument("--world1_collectives", nargs="?", const="all", default="", choices=["", "all", "metric"],
-                    help="world 1 on the GPU: still create the nccl (RCCL) process group and the metric reducer's RCCL "
-                         "communicator; 'all' (the bare flag) also runs every gradient bucket's all-reduce (the DP "
-                         "path's overheads measured on one GPU)")
+                    help="world 1 on the GPU: still create the gloo rendezvous and the trial's RCCL communicator (metric "
+                         "mean); 'all' (the bare flag) also runs every gradient bucket's collective on it (the DP path's "
+                         "overheads measured on one GPU)")
     ap.add_argument("--zero1", action="store_true",
                     help="ZeRO-1: reduce-scatter each gradient bucket, AdamW on this rank's 1/W slice inside the "
                          "backward, all-gather the bf16 weights (parallel/ddp.py); also PLX_ZERO1=1")
     args = _parse(ap, argv)
-    backend = "gloo" if args.cpu or not torch.cuda.is_available() else "nccl"
-    info = init_from_env(backend)
+    # the process group is the gloo rendezvous; every device collective of the trial (gradient buckets, ZeRO-1,
+    # the parameter broadcast, the metric mean) runs on ONE framework RCCL communicator (parallel/comm.py)
+    cuda = not args.cpu and torch.cuda.is_available()
+    info = init_from_env("gloo", device=torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0"))) if cuda
+                         else torch.device("cpu"))
     dev = info["device"]
     force = bool(args.world1_collectives) and dev.type == "cuda" and info["world"] == 1
     force_buckets = force and args.world1_collectives == "all"
@@ -208,7 +211,7 @@ def train_lm(argv=None) -> float:
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        dist.init_process_group("gloo", rank=0, world_size=1)
     if dev.type == "cuda":
         from polyaxon_amd.client.budget import apply_hbm_budget
 
@@ -293,6 +296,7 @@ def train_lm(argv=None) -> float:
                           "params_m": round(sum(s.numel for s in flat.segments) / 1e6, 1),
                           "lm_gemm": {"mode": _gemm.mode(), "native_shapes": sum(1 for d in dec.values() if d["native"]),
                                       "shapes": len(dec), "decisions": dec}}))
+    ddp.close()
     metrics.close()
     if info["world"] > 1 or force:
         import torch.distributed as dist
