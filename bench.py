@@ -43,10 +43,11 @@ import tempfile
 import threading
 import time
 
-# at least eight hardware queues before any GPU call: the RCCL communicator's streams + compute + side streams
-# (the same rule as polyaxon_amd/__init__.py; profiles/r4_rccl_slowdown.md)
-if int(os.environ.get("PLX_HW_QUEUES", "8") or 0) > int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0):
-    os.environ["GPU_MAX_HW_QUEUES"] = str(min(int(os.environ.get("PLX_HW_QUEUES", "8")), 32))
+# The box's own hardware-queue count is used (HIP's default 4): the trial process's streams fit it (one RCCL
+# communicator; the weight-gradient side stream on a priority level of its own, ops/side_stream.py).  PLX_HW_QUEUES=n
+# is an explicit opt-in to raise GPU_MAX_HW_QUEUES before any GPU call (the round-4 setting was 8).
+if int(os.environ.get("PLX_HW_QUEUES", "0") or 0) > int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0):
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(int(os.environ.get("PLX_HW_QUEUES")), 32))
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -258,6 +259,8 @@ class ControlServer:
         return rc
 
     def _summarise(self, gids, t0_wall: float, base) -> dict:
+        from polyaxon_amd.polyflow.scheduler import device_footprint
+
         st = self.flow.store
         q = ",".join("?" * len(gids))
         xs = st.list_experiments(ids=[r["id"] for r in st.execute(
@@ -321,7 +324,7 @@ class ControlServer:
         return {"trials": trials, "succeeded": ok, "train_steps": steps, "ttt": ttt, "best": best, "per_sweep": per_sweep,
                 "per_units": per_units,
                 "fsm_ok": fsm_ok, "resumed": resumed, "brackets": units, "groups": len(gids), "executors": execs,
-                "control_pid": os.getpid()}
+                "control_pid": os.getpid(), "control_device_footprint": device_footprint()}
 
 
 def control_main(args) -> int:
@@ -454,10 +457,9 @@ def main() -> int:
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     if world > 1:
-        # The ranks' own control traffic (control address, barriers around the timed region) is a few bytes: it
-        # goes over gloo.  No RCCL communicator may exist while the sweeps run -- one created before the timed
-        # region measured 17 % fewer trials/h on one GPU (profiles/r3_negative_results.md) -- so the only RCCL
-        # collective, the per-rank gather, is made on a communicator created after the timed region.
+        # The process group is the gloo rendezvous: the ranks' control traffic (control address, barriers around the
+        # timed region) and the RCCL unique id; the per-rank gather runs on the framework RCCL communicator
+        # (parallel/comm.py), alive for the whole run by default (PLX_BENCH_RCCL below).
         dist.init_process_group("gloo")
         addr = [ctl_addr]
         dist.broadcast_object_list(addr, src=0)
@@ -473,16 +475,21 @@ def main() -> int:
             torch.cuda.synchronize(dev)
 
     # PLX_BENCH_RCCL: "early" (default) -- the framework's RCCL communicator is alive for the whole run, as in a DP
-    # trial (with 4 hardware queues it serialised the side stream with compute, -17 %; at the package's 8 queues it
-    # costs <= 0.2 %: profiles/r4_rccl_slowdown.md); "late" / "1" -- created after the timed region; "0" -- gloo only
+    # trial (round 4: with 4 hardware queues its streams pushed the side stream onto the compute stream's queue,
+    # -17 %, profiles/r4_rccl_slowdown.md; the side stream now has a queue of its own, profiles/r5_hw_queues.md);
+    # "late" / "1" -- created after the timed region; "0" -- gloo only
     rccl_mode = os.environ.get("PLX_BENCH_RCCL", "early")
     early_comm = None
     if dev.type == "cuda" and rccl_mode == "early":
         from polyaxon_amd.parallel.rccl import RcclComm
 
         try:
-            early_comm = (RcclComm.from_torch_distributed() if world > 1
-                          else RcclComm(RcclComm.new_unique_id(), 1, 0, local))
+            if world > 1:
+                from polyaxon_amd.parallel import comm as _comm
+
+                early_comm = _comm.acquire(None, dev)
+            else:
+                early_comm = RcclComm(RcclComm.new_unique_id(), 1, 0, local)
         except Exception as e:  # built again after the timed region (or gloo) rather than fail the run
             print(f"bench: early RCCL communicator unavailable ({e})", file=sys.stderr)
     worker = ResidentWorker(program, params, device=dev, max_active=args.max_active)
@@ -611,6 +618,8 @@ def main() -> int:
                           "sync_s": round(p[6], 3)} for i, p in enumerate(per_rank)],
             "executors": res["executors"],
             "control_pid": res["control_pid"],
+            # the scheduler process (polyflow + BO GP requests to the executors) holds no GPU state
+            "control_device_footprint": res.get("control_device_footprint"),
             "cpus_pinned": len(pinned),
         }
         print(json.dumps(out), file=result_out, flush=True)

@@ -84,17 +84,29 @@ def device_cpus(index: int, sysfs: str = "/sys") -> Optional[List[int]]:
     return cpus or None
 
 
-def detect_devices() -> List[Device]:
-    """Visible HIP devices without initialising the GPU runtime (``device_count`` only)."""
+def detect_devices(sysfs: str = "/sys") -> List[Device]:
+    """Visible HIP devices from the KFD topology (sysfs) -- no HIP runtime, no torch: the scheduler process that
+    calls this never loads either.  HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES (comma lists of indices) narrow the
+    set as they do for HIP; PLX_NUM_GPUS overrides (tests, CPU rehearsals)."""
     n = os.environ.get("PLX_NUM_GPUS")
     if n is not None:
         return [Device(i) for i in range(int(n))]
-    try:
-        import torch
+    from polyaxon_amd.obs.nodes import kfd_gpus
 
-        count = torch.cuda.device_count()
-    except Exception:
-        count = 0
+    gpus = kfd_gpus(sysfs)
+    if os.path.isdir("/dev/dri"):  # a container sees the render nodes of the GPUs it was given (ROCr opens them)
+        gpus = [g for g in gpus if not g.get("drm_render_minor")
+                or os.path.exists(f"/dev/dri/renderD{g['drm_render_minor']}")]
+    count = len(gpus)
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        vis = os.environ.get(var)
+        if vis is None:
+            continue
+        ids = [v for v in vis.split(",") if v.strip() != ""]
+        try:
+            count = len([i for i in ids if 0 <= int(i) < count])
+        except ValueError:  # UUID lists: trust their length
+            count = min(count, len(ids))
     return [Device(i) for i in range(count)]
 
 

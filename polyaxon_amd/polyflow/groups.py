@@ -137,9 +137,8 @@ class GroupDriver:
                         return True
             return False
         import numpy as np
-        import torch
 
-        from polyaxon_amd.polytune.kernels import early_stop_any
+        from polyaxon_amd.polytune.utils import early_stop_any_host
 
         names = sorted({r.metric for r in rules})
         rows = self.store.execute("SELECT last_metric FROM experiments WHERE group_id = ?", (self.gid,)).fetchall()
@@ -150,8 +149,9 @@ class GroupDriver:
                 v = last.get(n)
                 if isinstance(v, (int, float)):
                     mat[i, j] = v
-        flags = early_stop_any(torch.from_numpy(mat), [(names.index(r.metric), float(r.value),
-                                                        Optimization.maximize(r.optimization)) for r in rules])
+        # the host path of the device kernel (the scheduler process stays free of torch and HIP)
+        flags = early_stop_any_host(mat, [(names.index(r.metric), float(r.value),
+                                           Optimization.maximize(r.optimization)) for r in rules])
         return any(flags)
 
     def stop(self, pending_only: bool = False, message: str = "Stopped") -> None:
@@ -721,14 +721,17 @@ class ResidentBODriver(ResidentDriver):
         self.batch: List[str] = []
         self._launch(self.manager.get_suggestions(None) or [])
 
-    def _launch(self, suggestions: List[Dict[str, Any]]) -> None:
+    def _launch(self, suggestions: List[Dict[str, Any]], suggest: Optional[Dict[str, Any]] = None) -> None:
         self.batch = []
         for i, params in enumerate(suggestions):
             key = f"{self.gid}.bo{self.iteration}.{i}"
             self._new_unit(key, self.iteration, [{"cid": 0, "params": dict(params)}], self.trial_units)
             self.batch.append(key)
-        self.iteration_id = self.store.create_iteration(self.gid, {"iteration": self.iteration,
-                                                                   "experiment_ids": [], "unit": self.OP})
+        self.suggest_info = suggest  # where this iteration's GP ran (kept in the iteration row)
+        data = {"iteration": self.iteration, "experiment_ids": [], "unit": self.OP}
+        if suggest is not None:
+            data["suggest"] = suggest
+        self.iteration_id = self.store.create_iteration(self.gid, data)
 
     @property
     def metric_name(self) -> str:
@@ -766,17 +769,82 @@ class ResidentBODriver(ResidentDriver):
             if v is not None:
                 self.old_configs.append((xid, dict(b["configs"][0]["params"])))
                 self.old_metrics.append((xid, v))
-        self.store.update_iteration(self.iteration_id, {
-            "iteration": self.iteration, "experiment_ids": ids, "unit": self.OP,
-            "experiments_metrics": [list(m) for m in self.old_metrics if m[0] in ids]})
+        data = {"iteration": self.iteration, "experiment_ids": ids, "unit": self.OP,
+                "experiments_metrics": [list(m) for m in self.old_metrics if m[0] in ids]}
+        if getattr(self, "suggest_info", None) is not None:
+            data["suggest"] = self.suggest_info
+        self.store.update_iteration(self.iteration_id, data)
         if self.stopped or not self.manager.should_reschedule(self.iteration) or not self.old_metrics:
             self.batch = []
             return
         self.iteration += 1
         cfg = self.BOIterationConfig(iteration=self.iteration, old_experiments_configs=list(self.old_configs),
                                      old_experiments_metrics=list(self.old_metrics))
-        n = max(int(self.hp.bo.n_suggestions or 1), int(self.concurrency))
-        self._launch(self.manager.get_suggestions(cfg, n=n) or [])
+        self._request_suggestions(cfg, max(int(self.hp.bo.n_suggestions or 1), int(self.concurrency)))
+
+    # ------------------------------------------------------------------ the GP runs on an executor, not here
+    awaiting: Optional[str] = None  # key of the outstanding bo_suggest request
+
+    def _observations(self, cfg):
+        configs_by_id = dict(cfg.combined_experiments_configs)
+        metrics_by_id = dict(cfg.combined_experiments_metrics)
+        keys = list(metrics_by_id)
+        return [configs_by_id[k] for k in keys], [float(metrics_by_id[k]) for k in keys]
+
+    def _request_suggestions(self, cfg, n: int) -> None:
+        """The GP fit and the acquisition search run on one of the group's executors (``bo_suggest``: the HIP kernels
+        on its device), so the scheduler process never initialises HIP (the reference runs hpsearch on a CPU worker
+        queue of its own, apart from the trial pods: celery_settings.py:398-419).  No executor to ask: numpy here."""
+        configs, metrics = self._observations(cfg)
+        key = f"{self.gid}.bo{self.iteration}.suggest"
+        msg = {"op": "bo_suggest", "key": key, "hptuning": self.hp.to_dict(), "configs": configs,
+               "metrics": metrics, "n": int(n)}
+        pool = self.flow.resident_pool()
+        allowed = sorted(self.used_workers) or None
+        self.awaiting = key
+        self._pending_cfg = (cfg, n)
+        if pool.request(self, msg, key=self.program_key, allowed=allowed) is None:
+            self._suggest_here("no live executor of the group")
+
+    def _suggest_here(self, why: str) -> None:
+        from polyaxon_amd.polytune.bo import suggest
+
+        cfg, n = self._pending_cfg
+        self.awaiting = None
+        log.warning("group %s: BO iteration %d on the scheduler's numpy backend (%s)", self.gid, self.iteration, why)
+        configs, metrics = self._observations(cfg)
+        out = suggest(self.hp, configs, metrics, n, backend="numpy")
+        self._suggested(out, {"backend": "numpy", "where": "scheduler", "reason": why})
+
+    def _suggested(self, suggestions, info: Dict[str, Any]) -> None:
+        if self.stopped:
+            self._check_finished()
+            return
+        self._launch(suggestions or [], info)
+        self._dispatch()
+        self._check_finished()
+
+    def has_more_work(self) -> bool:
+        return self.awaiting is not None or super().has_more_work()
+
+    def on_resident_event(self, h, msg: Dict[str, Any]) -> None:
+        key = msg.get("key")
+        if key is not None and key == self.awaiting:
+            self.awaiting = None
+            if msg.get("ev") == "bo_suggestions":
+                self._suggested(msg.get("suggestions") or [], {"backend": msg.get("backend"), "where": f"executor {h.wid}",
+                                                               "ms": msg.get("ms")})
+            else:  # the executor could not compute it (error reply): do it here
+                self.awaiting = key
+                self._suggest_here(f"executor {h.wid}: {msg.get('message')}")
+            return
+        super().on_resident_event(h, msg)
+
+    def on_bracket_lost(self, h, key: str, reason: str) -> None:
+        if key == self.awaiting:
+            self._suggest_here(f"executor {h.wid} lost: {reason}")
+            return
+        super().on_bracket_lost(h, key, reason)
 
 
 def make_group_driver(flow, gid: int, spec: GroupSpecification, project: Dict, user: str, cwd: str) -> GroupDriver:

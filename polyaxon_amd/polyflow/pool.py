@@ -287,6 +287,25 @@ class ResidentPool:
             return None
         return w
 
+    def request(self, driver, msg: Dict[str, Any], key: Optional[str] = None,
+                allowed: Optional[List[int]] = None) -> Optional[WorkerHandle]:
+        """Send a one-shot request (``bo_suggest``) to the least-loaded live executor of ``key``; its reply (same
+        ``key`` field) is routed to ``driver.on_resident_event``, and a lost executor to ``on_bracket_lost``."""
+        cands = [w for w in self.workers.values() if w.alive and w.ready and (key is None or w.key == key)
+                 and (allowed is None or w.wid in allowed)]
+        if not cands and allowed is not None:
+            cands = [w for w in self.workers.values() if w.alive and w.ready and (key is None or w.key == key)]
+        if not cands:
+            return None
+        w = min(cands, key=lambda h: (h.load, h.wid))
+        w.brackets[msg["key"]] = driver
+        try:
+            w.chan.send(msg)
+        except OSError:
+            self._lost(w, "send failed")
+            return None
+        return w
+
     def send(self, wid: int, msg: Dict[str, Any]) -> bool:
         w = self.workers.get(wid)
         if w is None or not w.alive:
@@ -387,6 +406,8 @@ class ResidentPool:
                 # outstanding work shrinks as trials finish (keeps the balancing estimate honest)
                 h.units[key] = max(0.0, h.units.get(key, 0.0) - float(msg.get("steps", 0)) /
                                    max(1.0, float(h.info.get("unit_steps", 1) or 1)))
+            if ev == "bo_suggestions" or (ev == "error" and key.endswith(".suggest")):
+                h.brackets.pop(key, None)  # one-shot request answered
             if ev == "bracket_done":
                 h.brackets.pop(key, None)
                 h.units.pop(key, None)

@@ -17,7 +17,8 @@ import math
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, Optional, Tuple
 
-import torch
+# torch is imported inside the builders: the scheduler imports this module for program_key / bracket_units, and the
+# scheduler process never loads torch or the HIP runtime (tests/test_gpu_free_scheduler.py)
 
 
 @dataclass
@@ -31,6 +32,8 @@ class TrialProgram:
 
     def warm(self, steps: int = 2) -> None:
         """Pay one-time costs (kernel selection, allocator growth, library page-in) before the first trial."""
+        import torch
+
         ex = self.executor
         if ex.use_graph:
             ex.capture(warmup=steps)
@@ -46,6 +49,8 @@ class TrialProgram:
 
 
 def _resnet(params: Dict[str, Any], device, tiny: bool) -> TrialProgram:
+    import torch
+
     from polyaxon_amd.models.resnet import resnet18ish, resnet50
     from polyaxon_amd.ops.synth import SyntheticImages
     from polyaxon_amd.polyflow.executor import ResidentTrialExecutor
@@ -69,6 +74,8 @@ def _resnet(params: Dict[str, Any], device, tiny: bool) -> TrialProgram:
 
 
 def _mlp(params: Dict[str, Any], device) -> TrialProgram:
+    import torch
+
     from polyaxon_amd.polyflow.executor import ResidentTrialExecutor
     from polyaxon_amd.trainers import MLP
 
@@ -85,6 +92,8 @@ def _mlp(params: Dict[str, Any], device) -> TrialProgram:
 
 
 def _gpt2(params: Dict[str, Any], device, tiny: bool) -> TrialProgram:
+    import torch
+
     """GPT-2 125M (BASELINE.json config 4's trial) on the synthetic copy-task token stream (ops/synth.py
     SyntheticTokens): bf16 weights / gradients with an fp32 master and fused AdamW (the LM trainer's numerics),
     every trial re-initialised in place (GPT-2 init via plx_init_flat), AdamW hyper-parameters as device data."""

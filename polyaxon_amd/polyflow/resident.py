@@ -345,6 +345,8 @@ class ResidentWorker:
             return "shutdown"
         elif op == "ping":
             chan.send({"ev": "pong", "stats": dict(self.stats)})
+        elif op == "bo_suggest":
+            chan.send(self._bo_suggest(msg))
         elif op == "init":
             if msg.get("program") != self.program_name:
                 chan.send({"ev": "error", "fatal": True,
@@ -354,6 +356,21 @@ class ResidentWorker:
         else:
             chan.send({"ev": "error", "fatal": False, "message": f"unknown op {op!r}"})
         return None
+
+    def _bo_suggest(self, msg: Dict[str, Any]) -> Dict[str, Any]:
+        """A BO group's next batch: GP fit + acquisition search with the HIP kernels on this executor's device (the
+        scheduler that asks stays GPU-free), numpy on a CPU executor."""
+        from polyaxon_amd.polytune.bo import suggest
+        from polyaxon_amd.spec.hptuning import HPTuningConfig
+
+        t0 = time.perf_counter()
+        ex = self.program.executor
+        backend = "hip" if ex.is_cuda else "numpy"
+        out = suggest(HPTuningConfig.from_dict(msg["hptuning"]), list(msg["configs"]), list(msg["metrics"]),
+                      int(msg["n"]), backend=backend)
+        plain = [{k: (v.item() if hasattr(v, "item") else v) for k, v in s.items()} for s in out]
+        return {"ev": "bo_suggestions", "key": msg["key"], "suggestions": plain, "backend": backend,
+                "ms": round((time.perf_counter() - t0) * 1e3, 2)}
 
     def _make_bracket(self, msg: Dict[str, Any]) -> _Bracket:
         from polyaxon_amd.polytune.managers import HyperbandSearchManager

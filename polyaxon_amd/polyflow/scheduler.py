@@ -135,6 +135,28 @@ def _command(spec: BaseSpecification) -> str:
     return " && ".join(spec.run.commands)
 
 
+def device_footprint() -> Dict[str, bool]:
+    """Does THIS process hold any GPU state?  The scheduler must not: torch never imported, the HIP runtime not
+    mapped, no /dev/kfd descriptor (reported by the bench's control process, checked by
+    tests/test_gpu_free_scheduler.py)."""
+    import sys
+
+    try:
+        maps = open("/proc/self/maps").read()
+    except OSError:
+        maps = ""
+    kfd = False
+    try:
+        for f in os.listdir("/proc/self/fd"):
+            try:
+                kfd = kfd or "/dev/kfd" in os.readlink(f"/proc/self/fd/{f}")
+            except OSError:
+                pass
+    except OSError:
+        pass
+    return {"torch_imported": "torch" in sys.modules, "hip_mapped": "libamdhip64" in maps, "kfd_open": kfd}
+
+
 class Polyflow:
     """Node scheduler. Public methods are thread-safe (they post commands to the scheduler thread)."""
 
@@ -149,6 +171,11 @@ class Polyflow:
             reconcile_s = settings.get("scheduler.reconcile_interval_s") if reconcile_s == 5.0 else reconcile_s
             stop_grace_s = settings.get("scheduler.stop_grace_s") if stop_grace_s == 10.0 else stop_grace_s
         self.settings = settings
+        # the scheduler process never initialises HIP: a BO group's GP runs on its resident executors, or on numpy
+        from polyaxon_amd.polytune import bo as _bo
+
+        self._device_allowed_before = _bo.device_allowed()
+        _bo.set_device_allowed(False)
         self.numa_bind = settings.get("scheduler.numa_bind") if settings is not None else True
         self.build_reuse_s = settings.get("scheduler.build_reuse_s") if settings is not None else BUILD_REUSE_S
         self.build_backend = settings.get("build.backend") if settings is not None else "native"
@@ -274,6 +301,9 @@ class Polyflow:
         self.pm.wake()
         self._thread.join(timeout=timeout)
         self._thread = None
+        from polyaxon_amd.polytune import bo as _bo
+
+        _bo.set_device_allowed(self._device_allowed_before)
         try:
             os.unlink(os.path.join(self.paths.root, "scheduler.pid"))
         except OSError:

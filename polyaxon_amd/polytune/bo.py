@@ -31,6 +31,20 @@ from polyaxon_amd.polytune.managers import BaseSearchAlgorithmManager
 from polyaxon_amd.polytune.utils import get_random_generator, get_random_suggestions
 from polyaxon_amd.spec.hptuning import HPTuningConfig, Optimization, SearchAlgorithms
 
+# May this process run the GP on the GPU?  The scheduler (control) process says no at start: it stays HIP-free (no
+# device context outside the allocator's accounting), like the reference's hpsearch workers, which run on their own
+# CPU queue apart from the trial pods (/root/reference/polyaxon/polyaxon/config_settings/celery_settings.py:398-419).
+_DEVICE_ALLOWED = True
+
+
+def set_device_allowed(allowed: bool) -> None:
+    global _DEVICE_ALLOWED
+    _DEVICE_ALLOWED = bool(allowed)
+
+
+def device_allowed() -> bool:
+    return _DEVICE_ALLOWED
+
 KIND_IDS = {"rbf": 0, "matern05": 1, "matern15": 2, "matern25": 3, "matern_nu": 4}
 
 
@@ -476,8 +490,13 @@ class UtilityFunction:
 
     @staticmethod
     def resolve_backend(backend: str) -> str:
+        """``auto``: the HIP kernels when this process may do device work and has a GPU, else numpy.  The polyflow
+        scheduler process forbids device work (:func:`set_device_allowed`): it must never initialise HIP -- its
+        GP work runs on a resident executor of the group (``bo_suggest``), or on numpy."""
         if backend != "auto":
             return backend
+        if not device_allowed():
+            return "numpy"
         try:
             import torch
 
@@ -739,12 +758,19 @@ class BOSearchManager(BaseSearchAlgorithmManager):
         for key in metrics_by_id:
             configs.append(configs_by_id[key])
             metrics.append(metrics_by_id[key])
-        opt = BOOptimizer(cfg, backend=self.backend)
-        opt.add_observations(configs, metrics)
-        n = max(1, int(n if n is not None else cfg.bo.n_suggestions))
-        sugg = opt.get_suggestions(n) if n > 1 else [opt.get_suggestion()]
-        sugg = [s for s in sugg if s]
-        return sugg or None
+        return suggest(cfg, configs, metrics, n if n is not None else cfg.bo.n_suggestions, self.backend) or None
 
     def should_reschedule(self, iteration: int) -> bool:
         return iteration < self.n_iterations
+
+
+def suggest(cfg: HPTuningConfig, configs: List[Dict[str, Any]], metrics: List[float], n: int,
+            backend: str = "auto") -> List[Dict[str, Any]]:
+    """One BO iteration's suggestions (``n`` > 1: a constant-liar batch) from the finished trials' configs and
+    metrics -- what BOSearchManager.get_suggestions computes, callable where the GPU is (a resident executor's
+    ``bo_suggest`` op)."""
+    opt = BOOptimizer(cfg, backend=backend)
+    opt.add_observations(configs, metrics)
+    n = max(1, int(n))
+    sugg = opt.get_suggestions(n) if n > 1 else [opt.get_suggestion()]
+    return [s for s in sugg if s]

@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from polyaxon_amd.ops import _native
+from polyaxon_amd.polytune.utils import early_stop_any_host
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -86,13 +87,7 @@ def early_stop_any(metrics: torch.Tensor, rules: Sequence[Tuple[int, float, bool
             len(rules), flags.data_ptr(), _stream(metrics))
         _native.check(rc, "plx_early_stop_any")
         return [bool(x) for x in flags.cpu().tolist()]
-    m = metrics.numpy()
-    out = []
-    for c, v, mxm in rules:
-        colv = m[:, c]
-        ok = ~np.isnan(colv)
-        out.append(bool(np.any((colv[ok] >= v) if mxm else (colv[ok] <= v))))
-    return out
+    return early_stop_any_host(metrics.numpy(), rules)
 
 
 class BracketMetrics:

@@ -66,3 +66,17 @@ def get_random_suggestions(matrix, n_suggestions: int, suggestion_params: Option
             out.append(params)
             n_suggestions -= 1
     return out
+
+
+def early_stop_any_host(m, rules) -> list:
+    """Early-stopping rules over a host metric matrix ``m`` [experiments, metrics] (NaN = unreported); ``rules``
+    (column, threshold, maximize) -> triggered per rule.  The host path of polytune.kernels.early_stop_any, torch-free
+    for the scheduler process."""
+    import numpy as np
+
+    out = []
+    for c, v, mxm in rules:
+        colv = m[:, c]
+        ok = ~np.isnan(colv)
+        out.append(bool(np.any((colv[ok] >= v) if mxm else (colv[ok] <= v))))
+    return out

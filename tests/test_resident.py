@@ -618,6 +618,10 @@ def test_polyflow_resident_bo_group_over_gpt2(tmp_path, cpu_pool_env):
         later = {round(x["declarations"]["lr"], 12) for x in xs if x["id"] in its[1]["data"]["experiment_ids"]}
         assert not (first & later)
         assert {tuple(j["devices"]) for x in xs for j in st.experiment_jobs(x["id"])} == {(0,), (1,)}
+        # the GP of every BO iteration ran on an executor (numpy on these CPU executors, the HIP kernels on a GPU),
+        # never in the scheduler process, which stays free of device work
+        assert [i["data"]["suggest"]["where"].startswith("executor") for i in its[1:]] == [True, True], its
+        assert "suggest" not in its[0]["data"]  # the initial batch is random
 
 
 def test_polyflow_resident_bo_group_on_a_dp2_gang(tmp_path, cpu_pool_env):
