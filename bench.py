@@ -73,15 +73,19 @@ def _args(argv=None):
     ap.add_argument("--bo-initial", type=int, default=4)
     ap.add_argument("--bo-iterations", type=int, default=3)
     ap.add_argument("--bo-concurrency", type=int, default=4, help="trials per BO batch (constant liar) per GPU")
-    ap.add_argument("--trial-units", type=int, default=10, help="gpt2_bo: resource units (x --unit-steps) per trial")
+    ap.add_argument("--trial-units", type=int, default=25, help="gpt2_bo: resource units (x --unit-steps) per trial")
+    ap.add_argument("--active-vocab", type=int, default=4096,
+                    help="gpt2_bo: token ids the copy-task phrases draw from (a unigram distribution to learn before "
+                         "the copying; 0 = the whole vocabulary, whose loss does not leave ln V within a trial)")
     ap.add_argument("--asha-n", type=int, default=29,
                     help="configs per ASHA sweep (29 at min 1 / max 27 / eta 3 with resume ~ the 87 units of a "
                          "Hyperband sweep)")
     ap.add_argument("--batch", type=int, default=256, help="per-trial batch (one trial per GPU at a time)")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--unit-steps", type=int, default=4, help="training steps per resource unit")
-    ap.add_argument("--target", type=float, default=0.03,
-                    help="loss target for wall-clock-to-target: near the synthetic task's floor at a sweep's budget "
+    ap.add_argument("--target", type=float, default=None,
+                    help="loss target for wall-clock-to-target (default 0.03 for resnet50_hb, 8.0 for gpt2_bo): "
+                         "near the synthetic task's floor at a sweep's budget "
                          "(Hyperband sweeps reach 0.015-0.1), so only some sweeps reach it")
     ap.add_argument("--signal", type=float, default=0.5, help="class-pattern amplitude of the synthetic data")
     ap.add_argument("--active-classes", type=int, default=100, help="classes the synthetic task draws from")
@@ -92,7 +96,10 @@ def _args(argv=None):
     ap.add_argument("--cpu", action="store_true", help="CPU rehearsal (gloo, small ResNet, tiny images)")
     ap.add_argument("--control-only", action="store_true", help=argparse.SUPPRESS)  # internal: the scheduler process
     ap.add_argument("--verbose", action="store_true")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.target is None:
+        args.target = 8.0 if args.config == "gpt2_bo" else 0.03
+    return args
 
 
 def program_params(args):
@@ -100,7 +107,7 @@ def program_params(args):
         if args.cpu:
             return "gpt2_tiny", {"batch": 2, "seq": 32, "unit_steps": 1, "trial_units": 2, "data_seed": 1234}
         return "gpt2", {"batch": 16, "seq": 1024, "unit_steps": args.unit_steps, "trial_units": args.trial_units,
-                        "graph": bool(args.graph), "data_seed": 1234}
+                        "graph": bool(args.graph), "data_seed": 1234, "active_vocab": args.active_vocab}
     if args.cpu:
         return "resnet_tiny", {"batch": min(args.batch, 8), "image": min(args.image, 32),
                                "unit_steps": min(args.unit_steps, 1), "grid": 4, "signal": args.signal,
@@ -321,7 +328,22 @@ class ControlServer:
             execs.append({"wid": w["wid"], "devices": w["devices"], "pid": w["pid"],
                           "load_units": round(w["assigned_units"] - w0.get("assigned_units", 0.0), 3),
                           "units_of_work": w["assigned"] - w0.get("assigned", 0)})
+        bo_groups = []
+        if self.args.config == "gpt2_bo":  # per BO group: the random batch's best vs the GP iterations' best
+            for g in gids:
+                its = sorted(st.iterations(g), key=lambda i: i["data"]["iteration"])
+                loss = {x["id"]: x["last_metric"]["loss"] for x in xs
+                        if x["group_id"] == g and (x.get("last_metric") or {}).get("loss") is not None}
+                rnd = [loss[i] for i in (its[0]["data"]["experiment_ids"] if its else []) if i in loss]
+                bo = [loss[i] for it in its[1:] for i in it["data"]["experiment_ids"] if i in loss]
+                allv = list(loss.values())
+                bo_groups.append({"group": g, "random_best": round(min(rnd), 4) if rnd else None,
+                                  "bo_best": round(min(bo), 4) if bo else None,
+                                  "bo_beats_random": bool(rnd and bo and min(bo) < min(rnd)),
+                                  "spread": round(max(allv) - min(allv), 4) if allv else None,
+                                  "suggest": [it["data"].get("suggest") for it in its[1:]]})
         return {"trials": trials, "succeeded": ok, "train_steps": steps, "ttt": ttt, "best": best, "per_sweep": per_sweep,
+                "bo_groups": bo_groups,
                 "per_units": per_units,
                 "fsm_ok": fsm_ok, "resumed": resumed, "brackets": units, "groups": len(gids), "executors": execs,
                 "control_pid": os.getpid(), "control_device_footprint": device_footprint()}
@@ -610,6 +632,11 @@ def main() -> int:
                                                  for p in res["per_sweep"] if p["steps_to_hit"] is not None]),
             "sweep_steps_to_target": [p["steps_to_hit"] for p in res["per_sweep"]],
             "loss_by_units": res["per_units"],
+            **({"bo_groups": res["bo_groups"],
+                "bo_beats_random_fraction": round(sum(1 for b in res["bo_groups"] if b["bo_beats_random"])
+                                                  / max(1, len(res["bo_groups"])), 3),
+                "trial_loss_spread_median": _median([b["spread"] for b in res["bo_groups"] if b["spread"] is not None]),
+                "chance_loss": round(math.log(50257), 4)} if gpt2 else {}),
             "store_fsm_history_ok": res["fsm_ok"],
             "path": "polyflow scheduler (own process) + SQLite store + resident executors (same path as plx run)",
             "hip_graph": bool(worker._ready_info.get("hip_graph")),

@@ -1570,9 +1570,10 @@ int launch_tn_st(const void* A, const void* B, float* W, int M, int N1, int N2, 
 }
 
 // ---- v2 weight-gradient plan (wgrad_kernel): one block per CU, tile by the output shape, slices by a cost model
-int g_tn_v2 = 1;        // 1: wgrad_kernel (v2), 0: gemm_tn_kernel (v1)          (A/B knob plx_set_tn_v2)
-int g_tn_v2_wide = 0;   // 128-divisible outputs: 0 = 128 x 128 tiles with K split over 2 wave groups, 1 = 256 x 128 /
-                        // 128 x 256 tiles where they divide (more FLOP per staged byte, twice the slab bytes per block)
+int g_tn_v2 = 1;        // 1: wgrad_kernel (v2), 0: gemm_tn_kernel (v1), 2: v2 for the gathered convolutions only
+                        // (A/B knob plx_set_tn_v2)
+int g_tn2_lds_kb = 128; // LDS ring budget of a v2 block: 128 KB (one block per CU) or 64 KB (two per CU, or room for the
+                        // main stream's blocks beside it); configurations whose groups would get < 2 slots keep 128
 
 struct V2Cfg { int na, nb, ks; };
 
@@ -1608,10 +1609,20 @@ inline void plan_reducer(TnPlan& p, long plane) {
 // round numbers from the v2 isolated runs (profiles/r5_wgrad_v2.md).
 constexpr double kTnCuFlops = 3.2e12, kTnBlockUs = 2.5, kTnSlabBw = 4.5e12;
 
+// ring slots of a v2 block within an LDS budget (a multiple of KS, <= 16); 0 when a group would get < 2 slots
+constexpr int tn2_ring(int na, int nb, int ks, int lds_kb) {
+    const int stage = (na + nb) * 32 * 128, r0 = (lds_kb * 1024) / stage, r1 = r0 > 16 ? 16 : r0, r = r1 - r1 % ks;
+    return r / ks >= 2 && (ks - 1) * na * nb * 16384 <= r * stage ? r : 0;
+}
+
+inline int tn2_ring_kb(const V2Cfg& c) {
+    return g_tn2_lds_kb <= 64 && tn2_ring(c.na, c.nb, c.ks, 64) ? 64 : 128;
+}
+
 inline TnPlan tn2_plan(int M, int N1, int N2, int num_cus, const V2Cfg& c) {
     const int bn1 = 64 * c.na, bn2 = 64 * c.nb;
     const int ntiles = (N1 / bn1) * (N2 / bn2);
-    const int cus = num_cus > 0 ? num_cus : 256;
+    const int cus = (num_cus > 0 ? num_cus : 256) * (tn2_ring_kb(c) <= 64 ? 2 : 1);  // resident blocks
     const int step = 32 * c.ks;                       // rows per iteration
     const long plane = (long)N1 * N2;
     const double flops = 2.0 * M * plane;
@@ -1634,11 +1645,12 @@ inline TnPlan tn2_plan(int M, int N1, int N2, int num_cus, const V2Cfg& c) {
     return p;
 }
 
-template <int NA, int NB, int KS, int CONV>
-int launch_tn2(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
-               hipStream_t s, const ConvGeom& geo) {
+template <int NA, int NB, int KS, int CONV, int LDSK>
+int launch_tn2_k(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
+                 hipStream_t s, const ConvGeom& geo) {
     constexpr int BKT = 32, STAGE = (NA + NB) * BKT * 128;
-    constexpr int R0 = (128 * 1024) / STAGE, R1 = R0 > 16 ? 16 : R0, RING = R1 - R1 % KS;  // <= 128 KB of ring
+    constexpr int RING = tn2_ring(NA, NB, KS, LDSK);
+    static_assert(RING > 0, "ring budget too small for this configuration");
     constexpr int LDS = RING * STAGE;
     auto k = wgrad_kernel<NA, NB, KS, CONV, BKT, RING>;
     static int attr = set_lds(k, LDS);
@@ -1647,6 +1659,16 @@ int launch_tn2(const void* A, const void* B, float* W, int M, int N1, int N2, in
     hipLaunchKernelGGL(k, dim3(ntiles * plan.slices), dim3(64 * NA * NB * KS), LDS, s, (const __bf16*)A,
                        (const __bf16*)B, W, M, N1, N2, lda, ldb, plan.kchunk, geo);
     return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+template <int NA, int NB, int KS, int CONV>
+int launch_tn2(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
+               hipStream_t s, const ConvGeom& geo) {
+    if constexpr (tn2_ring(NA, NB, KS, 64) > 0) {
+        if (tn2_ring_kb(V2Cfg{NA, NB, KS}) <= 64)
+            return launch_tn2_k<NA, NB, KS, CONV, 64>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo);
+    }
+    return launch_tn2_k<NA, NB, KS, CONV, 128>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo);
 }
 
 template <int CONV>
@@ -1773,11 +1795,11 @@ void plx_set_tn_stages(int n, int bk) {
 // A/B knob: wide (256 x 128 / 128 x 256) weight-gradient tiles (see g_tn_wide); set before sizing workspaces
 void plx_set_tn_wide(int on) { g_tn_wide = on ? 1 : 0; }
 
-// A/B knob: weight-gradient kernel v2 (wgrad_kernel, 1) or v1 (gemm_tn_kernel, 0); wide: v2's 256 x 128 tiles
-// (workspace queries size for every plan, so either may be toggled after sizing)
-void plx_set_tn_v2(int on, int wide) {
-    g_tn_v2 = on ? 1 : 0;
-    if (wide >= 0) g_tn_v2_wide = wide ? 1 : 0;
+// A/B knob: weight-gradient kernel v2 (wgrad_kernel, 1) or v1 (gemm_tn_kernel, 0); lds_kb: v2's ring budget (64 or
+// 128, <= 0 keeps it; workspace queries size for every plan, so either may be toggled after sizing)
+void plx_set_tn_v2(int on, int lds_kb) {
+    g_tn_v2 = on < 0 ? 0 : (on > 2 ? 2 : on);
+    if (lds_kb > 0) g_tn2_lds_kb = lds_kb <= 64 ? 64 : 128;
 }
 
 // weight-gradient slicing knobs; workspace sizes follow them, so set before sizing / launching
@@ -1800,11 +1822,11 @@ long plx_gemm_tn_workspace(int M, int N1, int N2, int num_cus) {
     long n = a.slices + (a.groups > 1 ? a.groups : 0);
     const long nb = b.slices + (b.groups > 1 ? b.groups : 0);
     if (nb > n) n = nb;
-    for (int wide = 0; wide < 2; ++wide) {  // both v2 tilings, whatever the knobs
-        const int keep = g_tn_v2_wide;
-        g_tn_v2_wide = wide;
+    for (int kb = 64; kb <= 128; kb += 64) {  // both v2 ring budgets, whatever the knob
+        const int keep = g_tn2_lds_kb;
+        g_tn2_lds_kb = kb;
         const TnPlan c = tn2_plan(M, N1, N2, num_cus, v2_cfg(N1, N2));
-        g_tn_v2_wide = keep;
+        g_tn2_lds_kb = keep;
         const long nc = c.slices + (c.groups > 1 ? c.groups : 0);
         if (nc > n) n = nc;
     }
@@ -1817,7 +1839,7 @@ namespace {
 template <int CONV>
 int run_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int N2, int lda, int ldb, int ldc,
            const void* zero, int num_cus, int accumulate, hipStream_t s, ConvGeom geo, int bpc = 0) {
-    const bool v2 = g_tn_v2 != 0;
+    const bool v2 = g_tn_v2 == 1 || (g_tn_v2 == 2 && CONV != 0);  // 2: v2 for the gathered (KxK / strided) ones
     const V2Cfg cfg = v2_cfg(N1, N2);
     const TnPlan plan = v2 ? tn2_plan(M, N1, N2, num_cus, cfg) : tn_plan(M, N1, N2, num_cus, bpc);
     int rc;

@@ -186,9 +186,9 @@ def lib(name: str) -> ctypes.CDLL:
             handle.plx_set_tn_stages(int(st), int(bk or 0))
         if name == "plx_train" and os.environ.get("PLX_ADAMW_WIDE"):  # A/B knob: 8-wide non-temporal AdamW
             handle.plx_set_adamw_wide(int(os.environ["PLX_ADAMW_WIDE"]))
-        if name == "plx_conv" and os.environ.get("PLX_TN_V2"):  # A/B knob: "v2[,wide]" weight-gradient kernel
-            v2, _, wide = os.environ["PLX_TN_V2"].partition(",")
-            handle.plx_set_tn_v2(int(v2), int(wide) if wide else -1)
+        if name == "plx_conv" and os.environ.get("PLX_TN_V2"):  # A/B knob: "v2[,ring KB]" weight-gradient kernel
+            v2, _, kb = os.environ["PLX_TN_V2"].partition(",")
+            handle.plx_set_tn_v2(int(v2), int(kb) if kb else -1)
         if name == "plx_conv" and os.environ.get("PLX_TN_WIDE"):  # A/B knob: 256x128 weight-gradient tiles
             handle.plx_set_tn_wide(int(os.environ["PLX_TN_WIDE"]))
         if name == "plx_bn" and os.environ.get("PLX_STEM_BWD_CAP"):  # A/B knob: stem backward partials-pass rows

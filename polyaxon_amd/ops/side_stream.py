@@ -78,9 +78,13 @@ def priority_stream(idx: int, priority: int) -> "torch.cuda.Stream":
     return torch.cuda.ExternalStream(handle.value, device=torch.device("cuda", idx))
 
 
-# PLX_WGRAD_PRIORITY=p: the side stream is created with HIP priority p (1 = low: the weight gradients yield workgroup
-# slots to the main stream's critical path); unset: default priority
-_WGRAD_PRIORITY = os.environ.get("PLX_WGRAD_PRIORITY", "")
+# PLX_WGRAD_PRIORITY=p: the side stream is created with HIP priority p (1 = low, the default; -1 high; empty: the
+# default priority).  HIP keeps a hardware-queue pool per priority level, so a low-priority side stream gets a queue
+# of its own even when the compute stream, RCCL's streams and torch's share the box's 4 (GPU_MAX_HW_QUEUES) normal
+# queues: with a live communicator and 4 queues the default-priority side stream landed on the compute stream's queue
+# and the two serialised (ResNet-50 bench 10.65k / 10.68k trials/h), low priority 11.52k, 8 queues 11.54k
+# (profiles/r5_hw_queues.md)
+_WGRAD_PRIORITY = os.environ.get("PLX_WGRAD_PRIORITY", "1")
 
 
 def _stream_for(dev: torch.device) -> "torch.cuda.Stream":

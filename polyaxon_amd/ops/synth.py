@@ -94,11 +94,16 @@ class SyntheticTokens:
 
     M32 = 0xFFFFFFFF
 
-    def __init__(self, batch: int, seq: int, vocab: int, device, period: int = 64, seed: int = 0):
+    def __init__(self, batch: int, seq: int, vocab: int, device, period: int = 64, seed: int = 0,
+                 active_vocab: int = 0):
+        """``active_vocab`` (0 = all): the phrases draw from the first ``active_vocab`` token ids only, so a model
+        also has a unigram distribution to learn (ln V -> ln active_vocab within tens of steps at a good learning
+        rate) before the copying: a budget of ~100 steps separates learning rates by nats, not hundredths."""
         if seq % period:
             raise ValueError("seq must be a multiple of period")
         self.device = torch.device(device)
         self.batch, self.seq, self.vocab, self.period, self.seed = batch, seq, vocab, period, int(seed)
+        self.active_vocab = int(active_vocab) if 0 < int(active_vocab) < vocab else vocab
         self.x = torch.zeros(batch, seq, dtype=torch.int64, device=self.device)
         self.y = self.x
         self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -118,7 +123,7 @@ class SyntheticTokens:
             h.mul_(mult).bitwise_and_(m)
         torch.bitwise_right_shift(h, 15, out=t)
         h.bitwise_xor_(t)
-        h.remainder_(self.vocab)
+        h.remainder_(self.active_vocab)
         self.x.view(self.batch, self.seq // self.period, self.period).copy_(
             h.view(self.batch, 1, self.period).expand(self.batch, self.seq // self.period, self.period))
         self.counter.add_(1)
@@ -126,7 +131,12 @@ class SyntheticTokens:
     @property
     def floor_loss(self) -> float:
         """Expected loss of a perfect copier: only the first period (minus its first token) is unpredictable."""
-        return (self.period - 1) / (self.seq - 1) * math.log(self.vocab)
+        return (self.period - 1) / (self.seq - 1) * math.log(self.active_vocab)
+
+    @property
+    def unigram_loss(self) -> float:
+        """Loss of a model that learned which tokens occur but does not copy."""
+        return math.log(self.active_vocab)
 
     @property
     def chance_loss(self) -> float:

@@ -110,7 +110,7 @@ def _gpt2(params: Dict[str, Any], device, tiny: bool) -> TrialProgram:
     batch = int(params.get("batch", 2 if tiny else 16))
     seq = int(params.get("seq", 32 if tiny else 1024))
     data = SyntheticTokens(batch, seq, cfg.vocab_size, dev, period=int(params.get("period", 8 if tiny else 64)),
-                           seed=int(params.get("data_seed", 0)))
+                           seed=int(params.get("data_seed", 0)), active_vocab=int(params.get("active_vocab", 0)))
     if dev.type == "cuda":
         with torch.device(dev):
             model = Transformer(cfg)
@@ -126,7 +126,9 @@ def _gpt2(params: Dict[str, Any], device, tiny: bool) -> TrialProgram:
                               "vocab": cfg.vocab_size, "data": "synthetic copy task, fresh per step (ops/synth.py)",
                               "warm_hparams": {"lr": 3e-4, "beta1": 0.9, "beta2": 0.95, "eps": 1e-8,
                                                "weight_decay": 0.1},
-                              "tokens_per_step": batch * seq, "floor_loss": data.floor_loss})
+                              "tokens_per_step": batch * seq, "floor_loss": data.floor_loss,
+                              "unigram_loss": data.unigram_loss, "chance_loss": data.chance_loss,
+                              "active_vocab": data.active_vocab})
 
 
 PROGRAMS: Dict[str, Callable[[Dict[str, Any], Any], TrialProgram]] = {

@@ -4,8 +4,8 @@ JSON line per (shape, variant) and a step-weighted summary.
 
     python scripts/wgrad_bench.py [--variants v1,v2,v2w] [--rounds 5] [--reps 10] [--check 1]
 
-Variants: v1 = the round-4 kernel and plan, v2 = wgrad_kernel with 128 x 128 tiles (K split over two wave
-groups), v2w = wgrad_kernel with 256 x 128 / 128 x 256 tiles where they divide.
+Variants: v1 = the round-4 kernel and plan, v2 = wgrad_kernel with a 128 KB LDS ring (one block per CU), v2s = the
+same with a 64 KB ring (two blocks per CU, or room for other kernels' blocks beside it).
 """
 import argparse
 import json
@@ -27,12 +27,12 @@ SHAPES = [(256, 64, 56, 56, 256, 1, 1), (256, 256, 56, 56, 64, 1, 1), (256, 64, 
           (256, 512, 7, 7, 512, 3, 1), (256, 128, 56, 56, 128, 3, 2), (256, 256, 28, 28, 256, 3, 2),
           (256, 512, 14, 14, 512, 3, 2)]
 COUNT = [4, 2, 1, 1, 3, 4, 1, 5, 6, 1, 2, 3, 1, 1, 1, 3, 3, 5, 2, 1, 1, 1]
-VARIANTS = {"v1": (0, 0), "v2": (1, 0), "v2w": (1, 1)}
+VARIANTS = {"v1": (0, -1), "v2": (1, 128), "v2s": (1, 64)}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="v1,v2,v2w")
+    ap.add_argument("--variants", default="v1,v2,v2s")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--check", type=int, default=1)
@@ -103,7 +103,7 @@ def main():
                 torch.cuda.synchronize()
                 res[v][ci].append(st.elapsed_time(en) / args.reps)
         print(f"# round {rnd} done", file=sys.stderr, flush=True)
-    lib.plx_set_tn_v2(1, 0)
+    lib.plx_set_tn_v2(1, 128)
     tot = {v: 0.0 for v in variants}
     flops_tot = 0.0
     for case in cases:
