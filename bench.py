@@ -74,9 +74,13 @@ def _args(argv=None):
     ap.add_argument("--bo-iterations", type=int, default=3)
     ap.add_argument("--bo-concurrency", type=int, default=4, help="trials per BO batch (constant liar) per GPU")
     ap.add_argument("--trial-units", type=int, default=25, help="gpt2_bo: resource units (x --unit-steps) per trial")
+    ap.add_argument("--task", choices=("chain", "copy"), default="chain",
+                    help="gpt2_bo: the synthetic objective.  chain (default): x_{t+1} = (a x_t + b) mod 4093, a transition "
+                         "table to memorise -- within a 100-step trial the loss ends between ~0.01 and ~8 nats by learning "
+                         "rate; copy: repeated 64-token phrases, whose copying is not learned within a trial budget (every "
+                         "trial ends near the unigram loss: profiles/r5_config4_search.md)")
     ap.add_argument("--active-vocab", type=int, default=4096,
-                    help="gpt2_bo: token ids the copy-task phrases draw from (a unigram distribution to learn before "
-                         "the copying; 0 = the whole vocabulary, whose loss does not leave ln V within a trial)")
+                    help="gpt2_bo copy task: token ids the phrases draw from (0 = the whole vocabulary)")
     ap.add_argument("--asha-n", type=int, default=29,
                     help="configs per ASHA sweep (29 at min 1 / max 27 / eta 3 with resume ~ the 87 units of a "
                          "Hyperband sweep)")
@@ -84,7 +88,7 @@ def _args(argv=None):
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--unit-steps", type=int, default=4, help="training steps per resource unit")
     ap.add_argument("--target", type=float, default=None,
-                    help="loss target for wall-clock-to-target (default 0.03 for resnet50_hb, 8.0 for gpt2_bo): "
+                    help="loss target for wall-clock-to-target (default 0.03 for resnet50_hb, 0.5 for gpt2_bo): "
                          "near the synthetic task's floor at a sweep's budget "
                          "(Hyperband sweeps reach 0.015-0.1), so only some sweeps reach it")
     ap.add_argument("--signal", type=float, default=0.5, help="class-pattern amplitude of the synthetic data")
@@ -98,16 +102,18 @@ def _args(argv=None):
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args(argv)
     if args.target is None:
-        args.target = 8.0 if args.config == "gpt2_bo" else 0.03
+        args.target = 0.5 if args.config == "gpt2_bo" else 0.03
     return args
 
 
 def program_params(args):
     if args.config == "gpt2_bo":
         if args.cpu:
-            return "gpt2_tiny", {"batch": 2, "seq": 32, "unit_steps": 1, "trial_units": 2, "data_seed": 1234}
+            return "gpt2_tiny", {"batch": 2, "seq": 32, "unit_steps": 1, "trial_units": 2, "data_seed": 1234,
+                                 "task": args.task}
         return "gpt2", {"batch": 16, "seq": 1024, "unit_steps": args.unit_steps, "trial_units": args.trial_units,
-                        "graph": bool(args.graph), "data_seed": 1234, "active_vocab": args.active_vocab}
+                        "graph": bool(args.graph), "data_seed": 1234, "active_vocab": args.active_vocab,
+                        "task": args.task}
     if args.cpu:
         return "resnet_tiny", {"batch": min(args.batch, 8), "image": min(args.image, 32),
                                "unit_steps": min(args.unit_steps, 1), "grid": 4, "signal": args.signal,
@@ -119,7 +125,7 @@ def program_params(args):
 def bo_group_spec(seed: int, program: str, params: dict, args, world: int) -> dict:
     """BASELINE config 4: GP-UCB over GPT-2's AdamW learning rate, weight decay and beta2."""
     hp = {"seed": seed, "concurrency": args.bo_concurrency * world,
-          "matrix": {"lr": {"loguniform": [math.log(1e-4), math.log(3e-3)]},
+          "matrix": {"lr": {"loguniform": [math.log(1e-5), math.log(3e-3)]},
                      "weight_decay": {"uniform": [0.0, 0.2]},
                      "beta2": {"uniform": [0.9, 0.999]}},
           "bo": {"n_initial_trials": args.bo_initial * world, "n_iterations": args.bo_iterations,
@@ -591,8 +597,11 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if dev.type == "cuda" else "fp32",
-            "data": ("synthetic copy-task tokens (64-token phrases repeated to 1024, vocab 50257), fresh batch "
-                     "generated on the device every step (ops/synth.py SyntheticTokens); random-init weights" if gpt2
+            "data": (("synthetic chain tokens (x_{t+1} = (a x_t + b) mod 4093 from a random start, 1024 per sequence, "
+                      "vocab 50257; ops/synth.py SyntheticChain)" if args.task == "chain" else
+                      "synthetic copy-task tokens (64-token phrases repeated to 1024, vocab 50257; ops/synth.py "
+                      "SyntheticTokens)") + ", fresh batch generated on the device every step; random-init weights"
+                     if gpt2
                      else "synthetic ImageNet-shape (224x224x3, 1000 classes), fresh learnable batch generated on "
                           "the device every step (ops/synth.py); random-init weights"),
             "config": {

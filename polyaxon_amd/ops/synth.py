@@ -141,3 +141,67 @@ class SyntheticTokens:
     @property
     def chance_loss(self) -> float:
         return math.log(self.vocab)
+
+
+class SyntheticChain:
+    """A deterministic token chain for the language-model trial programs (config 4's objective): each sequence starts
+    at a random token x0 of [0, p) (p prime) and continues x_{t+1} = (a x_t + b) mod p, so every target is a fixed
+    function of the previous token -- a p-entry transition table the model has to memorise.  Each transition occurs
+    ~batch * seq / p times per step, so within ~100 steps the loss falls from ln V by several nats at a good
+    learning rate and stays near ln p at a poor one (the copy task's induction is not learned within a trial budget:
+    profiles/r5_config4_search.md).  The chain has a closed form, x_t = (A_t x0 + B_t) mod p with A_t = a^t and
+    B_t = b (a^t - 1) / (a - 1) tabulated on the host, so a batch is four tensor ops on the device: graph-capturable
+    (the start tokens come from the same counter hash as SyntheticTokens), identical on CPU and GPU."""
+
+    M32 = 0xFFFFFFFF
+
+    def __init__(self, batch: int, seq: int, vocab: int, device, p: int = 4093, a: int = 1103, b: int = 12345,
+                 seed: int = 0):
+        if not (2 < p <= vocab) or any(p % d == 0 for d in range(2, int(p ** 0.5) + 1)):
+            raise ValueError("p must be a prime <= vocab")
+        self.device = torch.device(device)
+        self.batch, self.seq, self.vocab, self.p, self.seed = batch, seq, vocab, p, int(seed)
+        self.active_vocab = p
+        A, B = [1], [0]
+        for _ in range(seq - 1):  # x_{t+1} = a x_t + b: A_{t+1} = a A_t, B_{t+1} = a B_t + b
+            A.append(A[-1] * a % p)
+            B.append((B[-1] * a + b) % p)
+        self._A = torch.tensor(A, dtype=torch.int64, device=self.device).view(1, seq)
+        self._B = torch.tensor(B, dtype=torch.int64, device=self.device).view(1, seq)
+        self.x = torch.zeros(batch, seq, dtype=torch.int64, device=self.device)
+        self.y = self.x
+        self.counter = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._idx = torch.arange(batch, dtype=torch.int64, device=self.device).view(batch, 1)
+        self._h = torch.empty_like(self._idx)
+        self._t = torch.empty_like(self._idx)
+
+    def next(self) -> None:
+        """Refill ``x`` in place with the next batch of the stream (and advance the device counter)."""
+        m, h, t = self.M32, self._h, self._t
+        torch.mul(self._idx, 0x9E3779B1, out=h)
+        h.add_(self.counter * 0x85EBCA77 + (self.seed * 0xC2B2AE3D) % (1 << 32))
+        h.bitwise_and_(m)
+        for mult in (0x7FEB352D, 0x846CA68B):  # lowbias32 finaliser
+            torch.bitwise_right_shift(h, 16, out=t)
+            h.bitwise_xor_(t)
+            h.mul_(mult).bitwise_and_(m)
+        torch.bitwise_right_shift(h, 15, out=t)
+        h.bitwise_xor_(t)
+        h.remainder_(self.p)
+        torch.mul(self._A, h, out=self.x)
+        self.x.add_(self._B).remainder_(self.p)
+        self.counter.add_(1)
+
+    @property
+    def floor_loss(self) -> float:
+        """A model that knows the table predicts every target but none for the first token (it has none)."""
+        return 0.0
+
+    @property
+    def unigram_loss(self) -> float:
+        """Loss of a model that learned which tokens occur but not the transitions."""
+        return math.log(self.p)
+
+    @property
+    def chance_loss(self) -> float:
+        return math.log(self.vocab)

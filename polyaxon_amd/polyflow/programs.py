@@ -98,7 +98,7 @@ def _gpt2(params: Dict[str, Any], device, tiny: bool) -> TrialProgram:
     SyntheticTokens): bf16 weights / gradients with an fp32 master and fused AdamW (the LM trainer's numerics),
     every trial re-initialised in place (GPT-2 init via plx_init_flat), AdamW hyper-parameters as device data."""
     from polyaxon_amd.models.transformer import Transformer, gpt2_125m, lm_loss
-    from polyaxon_amd.ops.synth import SyntheticTokens
+    from polyaxon_amd.ops.synth import SyntheticChain, SyntheticTokens
     from polyaxon_amd.polyflow.executor import ResidentTrialExecutor
 
     dev = torch.device(device)
@@ -109,8 +109,13 @@ def _gpt2(params: Dict[str, Any], device, tiny: bool) -> TrialProgram:
         cfg = gpt2_125m(vocab_size=int(params.get("vocab", 50257)))
     batch = int(params.get("batch", 2 if tiny else 16))
     seq = int(params.get("seq", 32 if tiny else 1024))
-    data = SyntheticTokens(batch, seq, cfg.vocab_size, dev, period=int(params.get("period", 8 if tiny else 64)),
-                           seed=int(params.get("data_seed", 0)), active_vocab=int(params.get("active_vocab", 0)))
+    task = str(params.get("task", "copy"))
+    if task == "chain":  # a memorised transition table: learning-rate sensitive within ~100 steps
+        data = SyntheticChain(batch, seq, cfg.vocab_size, dev, p=int(params.get("chain_p", 251 if tiny else 4093)),
+                              seed=int(params.get("data_seed", 0)))
+    else:
+        data = SyntheticTokens(batch, seq, cfg.vocab_size, dev, period=int(params.get("period", 8 if tiny else 64)),
+                               seed=int(params.get("data_seed", 0)), active_vocab=int(params.get("active_vocab", 0)))
     if dev.type == "cuda":
         with torch.device(dev):
             model = Transformer(cfg)
@@ -123,7 +128,7 @@ def _gpt2(params: Dict[str, Any], device, tiny: bool) -> TrialProgram:
                         window=int(params.get("window", 4)),
                         hp_keys=("lr", "beta1", "beta2", "eps", "weight_decay"),
                         info={"model": "gpt2_tiny" if tiny else "gpt2_125m", "batch": batch, "seq": seq,
-                              "vocab": cfg.vocab_size, "data": "synthetic copy task, fresh per step (ops/synth.py)",
+                              "vocab": cfg.vocab_size, "data": f"synthetic {task} task, fresh per step (ops/synth.py)",
                               "warm_hparams": {"lr": 3e-4, "beta1": 0.9, "beta2": 0.95, "eps": 1e-8,
                                                "weight_decay": 0.1},
                               "tokens_per_step": batch * seq, "floor_loss": data.floor_loss,
