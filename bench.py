@@ -219,8 +219,21 @@ class ControlServer:
                 spec = group_spec(seed0 + i, self.program, self.params, self.world, self.args.max_active,
                                   self.args.search, self.args.asha_n)
             gids.append(self.flow.submit(spec)["id"])
+        t_log = time.time()
         for g in gids:
-            st = self.flow.wait("group", g, timeout=7200, poll_s=0.05)
+            end = time.time() + 7200
+            while True:  # a progress line at least every 30 s (a silent multi-minute region looks hung)
+                try:
+                    st = self.flow.wait("group", g, timeout=min(30.0, max(0.1, end - time.time())), poll_s=0.05)
+                    break
+                except TimeoutError:
+                    st = "timeout"
+                    if time.time() >= end:
+                        break
+                if time.time() - t_log >= 30:
+                    t_log = time.time()
+                    done = sum(1 for x in self.flow.store.list_experiments(group_id=g) if x["status"] == "succeeded")
+                    self.log(f"group {g}: {done} trials done")
             if st != "succeeded":
                 raise RuntimeError(f"group {g} ended {st}")
         return gids
