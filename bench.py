@@ -129,6 +129,7 @@ def bo_group_spec(seed: int, program: str, params: dict, args, world: int) -> di
                      "weight_decay": {"uniform": [0.0, 0.2]},
                      "beta2": {"uniform": [0.9, 0.999]}},
           "bo": {"n_initial_trials": args.bo_initial * world, "n_iterations": args.bo_iterations,
+                 "space": "unit",  # lr over decades: the GP works in log-lr, every dimension scaled to [0, 1]
                  "metric": {"name": "loss", "optimization": "minimize"},
                  "utility_function": {"acquisition_function": "ucb", "kappa": 1.5,
                                       "gaussian_process": {"kernel": "matern", "length_scale": 1.0, "nu": 2.5},
@@ -595,7 +596,8 @@ def main() -> int:
                   f"asha min_resource=1 max_resource={ASHA_MAX} eta={ETA} resume=true, {args.asha_n} configs per sweep")
         gpt2 = args.config == "gpt2_bo"
         if gpt2:
-            search = (f"bo (GP-UCB, matern 2.5) over lr / weight_decay / beta2: {args.bo_initial * world} random + "
+            search = (f"bo (GP-UCB, matern 2.5, unit space: log-lr) over lr / weight_decay / beta2: "
+                      f"{args.bo_initial * world} random + "
                       f"{args.bo_iterations} x {args.bo_concurrency * world} constant-liar suggestions per group, "
                       f"{params['trial_units'] * params['unit_steps']} AdamW steps per trial")
         out = {

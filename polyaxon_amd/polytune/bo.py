@@ -62,6 +62,9 @@ class SearchSpace:
         self.x = np.zeros((0, 0))
         self.y = np.zeros(0)
         bounds = []
+        bo = hptuning_config.bo
+        unit = bo is not None and getattr(bo, "space", "raw") == "unit"
+        self.scale: Dict[str, Tuple[bool, float, float]] = {}  # unit space: feature -> (log, lo, hi) in model units
         for key in sorted(hptuning_config.matrix):
             v = hptuning_config.matrix[key]
             self.features.append(key)
@@ -71,14 +74,34 @@ class SearchSpace:
                     bounds.append((0, 1))
                 self.categorical_features[key] = {"values": values, "number": len(values)}
                 self.dim += len(values)
-            elif v.is_discrete:
-                bounds.append((v.min, v.max))
+                continue
+            lo, hi = float(v.min), float(v.max)
+            if v.is_discrete:
                 self.discrete_features[key] = {"values": v.to_numpy()}
-                self.dim += 1
+            if unit:
+                log = getattr(v, "option", None) in ("loguniform", "qloguniform", "lognormal", "qlognormal") and lo > 0
+                if log:
+                    lo, hi = math.log(lo), math.log(hi)
+                self.scale[key] = (log, lo, hi if hi > lo else lo + 1.0)
+                bounds.append((0.0, 1.0))
             else:
-                bounds.append((float(v.min), float(v.max)))
-                self.dim += 1
+                bounds.append((lo, hi) if not v.is_discrete else (v.min, v.max))
+            self.dim += 1
         self.bounds = np.asarray(bounds, dtype=np.float64)
+
+    def _to_model(self, f: str, val: float) -> float:
+        if f not in self.scale:
+            return val
+        log, lo, hi = self.scale[f]
+        x = math.log(val) if log else float(val)
+        return (x - lo) / (hi - lo)
+
+    def _from_model(self, f: str, x: float) -> float:
+        if f not in self.scale:
+            return x
+        log, lo, hi = self.scale[f]
+        v = lo + float(x) * (hi - lo)
+        return math.exp(v) if log else v
 
     def _maximize(self) -> bool:
         return Optimization.maximize(self.hptuning_config.bo.metric.optimization)
@@ -98,7 +121,7 @@ class SearchSpace:
                 if f in self.categorical_features:
                     row += [1 if v == cfg[f] else 0 for v in self.categorical_features[f]["values"]]
                 else:
-                    row.append(cfg[f])
+                    row.append(self._to_model(f, cfg[f]))
             rows.append(row)
         return np.array(rows, dtype=np.float64)
 
@@ -116,14 +139,14 @@ class SearchSpace:
         for f in self.features:
             if f in self.discrete_features:
                 vals = self.discrete_features[f]["values"]
-                v = vals[int(np.argmin(np.abs(np.subtract(vals, x[c]))))]
+                v = vals[int(np.argmin(np.abs(np.subtract(vals, self._from_model(f, x[c])))))]
                 c += 1
             elif f in self.categorical_features:
                 n = self.categorical_features[f]["number"]
                 v = self.categorical_features[f]["values"][int(np.argmax(x[c:c + n]))]
                 c += n
             else:
-                v = x[c]
+                v = self._from_model(f, x[c])
                 c += 1
             out[f] = v.item() if hasattr(v, "item") else v
         return out

@@ -224,18 +224,29 @@ class BOConfig:
     metric: SearchMetricConfig
     utility_function: UtilityFunctionConfig
     n_suggestions: int = 1
+    # the GP's input space: "raw" (the reference's: every continuous dimension in its own units), or "unit" (our
+    # addition): log-distributed dimensions (loguniform, qloguniform, lognormal, qlognormal) in log space, then every
+    # continuous / discrete dimension min-max scaled to [0, 1], so one isotropic length scale fits a learning rate
+    # over decades beside a beta2 over [0.9, 0.999]
+    space: str = "raw"
 
     @classmethod
     def from_dict(cls, d):
+        space = d.get("space", "raw")
+        if space not in ("raw", "unit"):
+            raise MatrixValidationError(f"bo.space must be raw or unit, got {space!r}")
         return cls(n_iterations=int(d["n_iterations"]), n_initial_trials=int(d["n_initial_trials"]),
                    metric=SearchMetricConfig.from_dict(d["metric"]),
                    utility_function=UtilityFunctionConfig.from_dict(d.get("utility_function")),
-                   n_suggestions=int(d.get("n_suggestions", 1)))
+                   n_suggestions=int(d.get("n_suggestions", 1)), space=space)
 
     def to_dict(self):
-        return dict(n_iterations=self.n_iterations, n_initial_trials=self.n_initial_trials,
-                    metric=self.metric.to_dict(), utility_function=self.utility_function.to_dict(),
-                    n_suggestions=self.n_suggestions)
+        out = dict(n_iterations=self.n_iterations, n_initial_trials=self.n_initial_trials,
+                   metric=self.metric.to_dict(), utility_function=self.utility_function.to_dict(),
+                   n_suggestions=self.n_suggestions)
+        if self.space != "raw":
+            out["space"] = self.space
+        return out
 
 
 @dataclass

@@ -142,3 +142,49 @@ def test_batch_suggestions_constant_liar():
     opt.add_observations([{"feature1": 1, "feature2": 1.0, "feature3": 1},
                           {"feature1": 3, "feature2": 2.0, "feature3": 4}], [1.0, 0.2])
     assert len(opt.get_suggestions(3)) == 3
+
+
+def test_unit_space_maps_log_dimensions_and_roundtrips():
+    """bo.space: unit -- log-distributed dimensions in log space, every continuous one scaled to [0, 1]: a config
+    maps into the unit box and back, and a BO search over a learning rate spanning decades finds the optimum of a
+    bowl in log-lr (the raw space's bounds are dominated by the large learning rates)."""
+    import math
+
+    import numpy as np
+
+    from polyaxon_amd.polytune.bo import BOSearchManager, BOIterationConfig, SearchSpace
+    from polyaxon_amd.spec.hptuning import HPTuningConfig
+
+    def cfg(space):
+        return HPTuningConfig.from_dict({
+            "seed": 3, "matrix": {"lr": {"loguniform": [math.log(1e-5), math.log(3e-3)]},
+                                  "wd": {"uniform": [0.0, 0.2]}},
+            "bo": {"n_initial_trials": 4, "n_iterations": 6, "space": space,
+                   "metric": {"name": "loss", "optimization": "minimize"},
+                   "utility_function": {"acquisition_function": "ucb", "kappa": 1.0,
+                                        "gaussian_process": {"kernel": "matern", "length_scale": 0.3, "nu": 2.5},
+                                        "n_warmup": 2000, "n_iter": 4}}})
+
+    sp = SearchSpace(cfg("unit"))
+    x = sp.parse_x([{"lr": 1e-4, "wd": 0.1}])[0]
+    assert np.all((x >= 0) & (x <= 1)) and abs(sp.get_suggestion(x)["lr"] - 1e-4) < 1e-12
+    assert sp.to_dict() if hasattr(sp, "to_dict") else True
+
+    def loss(p):
+        return (math.log10(p["lr"]) + 4.0) ** 2 + 0.1 * p["wd"]
+
+    best = {}
+    for space in ("raw", "unit"):
+        m = BOSearchManager(cfg(space), backend="numpy")
+        configs = list(enumerate(m.get_suggestions()))
+        metrics = [(i, loss(c)) for i, c in configs]
+        for it in range(1, 4):
+            sugg = m.get_suggestions(BOIterationConfig(iteration=it, old_experiments_configs=configs,
+                                                       old_experiments_metrics=metrics), n=2)
+            for c in sugg:
+                i = len(configs)
+                assert 1e-5 * 0.999 <= c["lr"] <= 3e-3 * 1.001
+                configs.append((i, c))
+                metrics.append((i, loss(c)))
+        best[space] = min(v for _, v in metrics)
+    assert best["unit"] < 0.05 and best["unit"] <= best["raw"], best
