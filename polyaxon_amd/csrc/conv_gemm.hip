@@ -16,7 +16,6 @@
 // partial tiles and padding need no branches around the DMA; the TN GEMM reads a zero page instead.
 #include <hip/hip_runtime.h>
 
-#include <utility>
 #include <stdint.h>
 
 namespace {
@@ -139,26 +138,6 @@ __device__ __forceinline__ void wait_vm_stages(int stages) {
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int V>
-struct IC {
-    static constexpr int value = V;
-};
-
-// MFMA with the accumulator pinned to an AGPR tuple ("+a"): with the builtin, hipcc moved the software-pipelined
-// kernel's accumulators between AGPRs around every MFMA (phi copies of the two-phase loop).  The compiler does not
-// see an MFMA here, so the consumer of the accumulators runs after mfma_drain() (XDL write -> read: <= 18 wait
-// states) and the first MFMA after their zero-initialisation is far behind it (prologue DMAs, waits, barriers).
-__device__ __forceinline__ void mfma_agpr(f32x4& acc, const bf16x8& a, const bf16x8& b) {
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
-
-// f(IC<0>{}), f(IC<1>{}), ... in order (compile-time indices for unrolled schedules)
-template <typename F, int... Is>
-__device__ __forceinline__ void static_for(F& f, std::integer_sequence<int, Is...>) {
-    (f(IC<Is>{}), ...);
-}
-
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     // consecutive logical ids on one XCD (blocks are dealt round-robin over the 8 XCDs); bijective for any nwg
     const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -203,10 +182,9 @@ __device__ __forceinline__ int nt_swz(int row) { return (row >> 1) & 7; }
 // chunk as a halo (the block's BM output pixels +- (W + 1) flattened pixels) and read by all 9 taps from LDS at a
 // per-tap row shift; only the weights are staged per tap.  Mode 1 re-stages the gathered A rows for every tap: 9x the
 // input bytes through the per-CU LDS-DMA path, which bounds those layers (~52 GB/s per CU, 34 % of MFMA peak).
-// NTH = 512 with NBUF = 3 is the pipelined kernel (PIPE): 8 waves as WGM x WGN over a 256 x 128 tile, a 3-stage LDS
-// ring whose DMAs stay in flight across the phase barriers behind a counted vmcnt, and the two 4-wave groups one
-// barrier apart (ping-pong), so each SIMD overlaps one wave's MFMAs with the other wave's fragment reads / DMA issue
-// (csrc/gemm256.hip's schedule with the implicit-conv row gather as the A loader)
+// (Round 5 removed the 8-wave 3-stage ring variant (NBUF 3) and the 4-5 stage software pipeline (NBUF 4-5): both
+// measured slower in the training step than these lock-step kernels, profiles/r4_conv3x3_scratch_fix_ring_ab.jsonl,
+// r4_conv3x3_swp_ab.jsonl, r4_bench_swp4_conv.json.)
 template <int BM, int BN, int WGM, int WGN, int MODE, int MINB = 2, int NBUF = 2, bool BWD = false, int NTH = NTHREADS>
 __global__ void __launch_bounds__(NTH, MINB)
 gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf16* __restrict__ C,
@@ -217,12 +195,9 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     // relu(a * scale[k] + bias[k]) between the LDS read and the MFMA (scale / bias = bnr.mean / bnr.invstd in this
     // forward-only mode).  Prototype of the BN-apply prologue fusion (plx_gemm_nt_prologue).
     constexpr bool CONV = MODE == 1 || MODE == 3, STEM = MODE == 2, HALO = MODE == 3, PRO = MODE == 4;
-    constexpr bool PIPE = NBUF == 3, SWP = NBUF >= 4;
     constexpr int NW = NTH / 64;                           // waves
     static_assert(WGM * WGN == NW, "one wave per wave tile");
-    static_assert(!PIPE || (NTH == 512 && !HALO && !PRO && !STEM), "the ring schedule is the 8-wave dense/conv kernel");
-    static_assert(!SWP || (NTH == 256 && !HALO && !PRO && !STEM), "the software-pipelined schedule is dense/conv");
-    static_assert(PIPE || NTH == 256, "the lock-step kernels are 4 waves");
+    static_assert(NTH == 256 && NBUF >= 1 && NBUF <= 2, "4-wave kernels, one or two K stages");
     constexpr int WTM = BM / WGM, WTN = BN / WGN;          // wave tile
     constexpr int RM = WTM / 16, RN = WTN / 16;            // 16x16 MFMA repeats
     constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -413,210 +388,6 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                 }
             }
         }
-    } else if constexpr (PIPE) {
-        // ---- ring schedule.  Tile kt lives in LDS buffer kt % 3.  Each tile runs 2 phases (kk = 0, 1: 16 MFMAs per
-        // wave each); phase 0 issues the A rows of tile kt + 2 into buffer (kt + 2) % 3 (= tile kt - 1's, whose last
-        // reads retired before the previous barrier), phase 1 its B rows and then waits until tile kt + 1 has landed
-        // (counted vmcnt: tile kt + 2's AI + BI DMAs may stay in flight).  Tile kt + 1 is first read one phase after
-        // that wait (RAW), also by the lagging group, whose wait precedes the barrier the leading group reads behind.
-        // Never __syncthreads() here: its fence would drain vmcnt.
-        const int nk = K / BK;
-        const int cdim = CONV ? geo.C : K;
-        const int grp = wave / 4;                           // waves w and w + 4 share a SIMD
-        int st = 0, sc = 0, kis = 0;                        // (tap, channel offset, k) of the next tile to issue
-        const bool tap_inner = CONV && geo.tap_inner;
-        auto advance = [&]() {                              // selects, no branches: a branchy form made hipcc keep
-            kis += BK;                                      // (st, sc) on the stack behind flat pointers
-            const bool wt = st + 1 == geo.ntaps, wc = sc + BK == cdim;
-            const int st_i = wt ? 0 : st + 1, sc_i = wt ? sc + BK : sc;
-            const int st_m = wc ? st + 1 : st, sc_m = wc ? 0 : sc + BK;
-            st = tap_inner ? st_i : st_m;
-            sc = tap_inner ? sc_i : sc_m;
-        };
-        auto phase = [&](const char* As, const char* Bs, int kk, bf16x8 (&fa)[RN], bf16x8 (&fb)[RM]) {
-#pragma unroll
-            for (int rn = 0; rn < RN; ++rn) {
-                const int row = wn * WTN + rn * 16 + fr;
-                fa[rn] = *(const bf16x8*)(Bs + row * 128 + (((kk * 4 + fq) ^ nt_swz(row)) * 16));
-            }
-#pragma unroll
-            for (int rm = 0; rm < RM; ++rm) {
-                const int row = wm * WTM + rm * 16 + fr;
-                fb[rm] = *(const bf16x8*)(As + row * 128 + (((kk * 4 + fq) ^ nt_swz(row)) * 16));
-            }
-        };
-        auto mfma = [&](const bf16x8 (&fa)[RN], const bf16x8 (&fb)[RM]) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-            for (int rn = 0; rn < RN; ++rn)
-#pragma unroll
-                for (int rm = 0; rm < RM; ++rm)
-                    acc[rn][rm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rn], fb[rm], acc[rn][rm], 0, 0, 0);
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-        };
-        constexpr int INFL = AI + BI;                       // one tile's DMAs per wave
-        static_assert(INFL == 6, "vmcnt immediates below assume 4 + 2 DMAs per wave per tile");
-        auto tile = [&](auto cb, int kt) {
-            constexpr int CB = decltype(cb)::value, NB = (CB + 2) % 3;
-            const char* As = smem + CB * STAGE;
-            const char* Bs = As + A_BYTES;
-            const bool more = kt + 2 < nk;
-            {
-                bf16x8 fa[RN], fb[RM];
-                phase(As, Bs, 0, fa, fb);
-                if (more) stage_a(NB, kis, st, sc);
-                mfma(fa, fb);
-            }
-            {
-                bf16x8 fa[RN], fb[RM];
-                phase(As, Bs, 1, fa, fb);
-                if (more) {
-                    stage_b(NB, kis, st, sc);
-                    advance();
-                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                mfma(fa, fb);
-            }
-        };
-        stage(0, kis, st, sc);
-        advance();
-        if (nk > 1) {
-            stage(1, kis, st, sc);
-            advance();
-            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();
-        if (grp == 1) __builtin_amdgcn_s_barrier();        // ping-pong: group 1 runs one barrier behind
-        for (int kt = 0; kt < nk; kt += 3) {
-            tile(IC<0>{}, kt);
-            if (kt + 1 < nk) tile(IC<1>{}, kt + 1);
-            if (kt + 2 < nk) tile(IC<2>{}, kt + 2);
-        }
-        if (grp == 0) __builtin_amdgcn_s_barrier();        // every wave executes the same number of barriers
-    } else if constexpr (SWP) {
-        // ---- software-pipelined schedule: one block per CU (one wave per SIMD) over an NST-stage LDS ring (tile j in
-        // slot j % NST).  Phase kt runs tile kt's MFMAs from registers and, one per MFMA, issues the ds_reads of tile
-        // kt + 1's fragments (into the other register set) and the DMAs of tile kt + NST into tile kt's slot (its
-        // fragments were read in phase kt - 1 and retired before that phase's barrier: WAR).  The phase ends with
-        // lgkmcnt(0), a counted vmcnt that retires tile kt + 2 (read in the next phase: RAW) and one barrier, so
-        // NST - 2 tiles of DMAs stay in flight across it and the MFMA pipe never waits on a whole-stage drain.
-        constexpr int NST = NBUF, INFL = AI + BI, NFR = 2 * (RN + RM), NMF = 2 * RN * RM;
-        static_assert(NFR + INFL <= NMF, "one fragment read or DMA per MFMA");
-        static_assert(NST <= 5 && INFL * (NST - 1) <= 63, "vmcnt immediates");
-        const int nk = K / BK;
-        // loop bounds as opaque SGPRs (no kernel-argument reload inside the loop)
-        int cdim = CONV ? geo.C : K, ntaps = geo.ntaps;
-        asm volatile("" : "+s"(cdim), "+s"(ntaps));
-        int st = 0, sc = 0, kis = 0;                        // (tap, channel offset, k) of the next tile to issue
-        const bool tap_inner = CONV && geo.tap_inner;
-        auto advance = [&]() {                              // selects, no branches (see the ring schedule)
-            kis += BK;
-            const bool wt = st + 1 == ntaps, wc = sc + BK == cdim;
-            const int st_i = wt ? 0 : st + 1, sc_i = wt ? sc + BK : sc;
-            const int st_m = wc ? st + 1 : st, sc_m = wc ? 0 : sc + BK;
-            st = tap_inner ? st_i : st_m;
-            sc = tap_inner ? sc_i : sc_m;
-        };
-        struct Frags {
-            bf16x8 a[2][RN];                                // MFMA A operand = B rows (output channel n), per kk
-            bf16x8 b[2][RM];                                // MFMA B operand = A rows (pixel m)
-        };
-        auto read_frag = [&](Frags& f, const char* As, auto ic) {
-            constexpr int I = decltype(ic)::value, KK = I / (RN + RM), J = I % (RN + RM);
-            if constexpr (J < RN) {
-                const int row = wn * WTN + J * 16 + fr;
-                f.a[KK][J] = *(const bf16x8*)(As + A_BYTES + row * 128 + (((KK * 4 + fq) ^ nt_swz(row)) * 16));
-            } else {
-                const int row = wm * WTM + (J - RN) * 16 + fr;
-                f.b[KK][J - RN] = *(const bf16x8*)(As + row * 128 + (((KK * 4 + fq) ^ nt_swz(row)) * 16));
-            }
-        };
-        // DMA arguments of the next tile to issue (kis, st, sc), then one of its AI + BI per-wave DMAs
-        auto dma_args = [&](int& a_add, int& bit, int& bk0) {
-            a_add = kis * 2;
-            bit = 0;
-            if constexpr (CONV) {
-                a_add = pick9(geo.tap_a, st) + sc * 2;
-                bit = st;
-            }
-            bk0 = CONV ? pick9(geo.tap_b, st) + sc * 2 : kis * 2;
-        };
-        // The tap lookup is a scalar load from the kernel arguments, and its wait (lgkmcnt) would also retire every
-        // fragment read in flight: the next tile's DMA arguments are therefore computed at the end of the previous
-        // phase (after its lgkmcnt(0)) and pinned there.
-        int na = 0, nbit = 0, nbk = 0;
-        auto next_args = [&]() {
-            dma_args(na, nbit, nbk);
-            asm volatile("" : "+v"(na), "+s"(nbit), "+s"(nbk));
-        };
-        auto dma_piece = [&](char* base, int a_add, int bit, int bk0, auto ic) {
-            constexpr int P = decltype(ic)::value;
-            if constexpr (P < AI) {
-                const uint32_t off = (a_ok[P] >> bit) & 1u ? (uint32_t)(a_off[P] + a_add) : OOB;
-                blds16(ra, off, base + (P * NW + wave) * 1024);
-            } else {
-                constexpr int Q = P - AI;
-                blds16(rb, (uint32_t)(b_off[Q] + bk0), base + A_BYTES + (Q * NW + wave) * 1024);
-            }
-        };
-        auto dma_tile = [&](char* base) {
-            int a_add, bit, bk0;
-            dma_args(a_add, bit, bk0);
-            auto one = [&](auto ic) { dma_piece(base, a_add, bit, bk0, ic); };
-            static_for(one, std::make_integer_sequence<int, INFL>{});
-            advance();
-        };
-        auto phase = [&](const Frags& fc, Frags& fn, int kt) {
-            const char* rimg = smem + ((kt + 1) % NST) * STAGE;  // past the last tile: stale reads into a dead set
-            char* dimg = smem + (kt % NST) * STAGE;
-            const bool dma = kt + NST < nk;                 // uniform
-            const int a_add = na, bit = nbit, bk0 = nbk;
-            auto step = [&](auto ic) {
-                constexpr int I = decltype(ic)::value, KK = I / (RN * RM), X = (I / RM) % RN, Y = I % RM;
-                mfma_agpr(acc[X][Y], fc.a[KK][X], fc.b[KK][Y]);
-                if constexpr (I < NFR) {
-                    read_frag(fn, rimg, IC<I>{});
-                } else if constexpr (I < NFR + INFL) {
-                    if (dma) dma_piece(dimg, a_add, bit, bk0, IC<I - NFR>{});
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            };
-            static_for(step, std::make_integer_sequence<int, NMF>{});
-            if (dma) advance();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            next_args();
-            wait_vm_stages<INFL>(min(kt + NST, nk - 1) - (kt + 2));
-            __builtin_amdgcn_s_barrier();
-        };
-        // prologue: tiles 0 .. min(NST, nk) - 1; tile 0's fragments; tile 1 landed before the first phase
-#pragma unroll
-        for (int j = 0; j < NST; ++j)
-            if (j < nk) dma_tile(smem + j * STAGE);
-        wait_vm_stages<INFL>(min(NST, nk) - 1);
-        __builtin_amdgcn_s_barrier();
-        Frags f0, f1;
-        {
-            auto rd = [&](auto ic) { read_frag(f0, smem, ic); };
-            static_for(rd, std::make_integer_sequence<int, NFR>{});
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        next_args();
-        wait_vm_stages<INFL>(min(NST, nk) - 2);
-        __builtin_amdgcn_s_barrier();
-        for (int kt = 0; kt < nk; kt += 2) {
-            phase(f0, f1, kt);
-            if (kt + 1 < nk) phase(f1, f0, kt + 1);
-        }
-        mfma_drain();
     } else {
     const int nk = K / BK;
     const int cdim = CONV ? geo.C : K;                      // channels per tap
@@ -1371,12 +1142,12 @@ template <int BM, int BN, int WGM, int WGN, int CONV = 0, int NBUF = 2>
 int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
               const void* zero, float* stats, hipStream_t s, ConvGeom geo = {}, const void* D = nullptr,
               int ldd = 0, BnBwd bnr = {}, const uint8_t* dmask = nullptr) {
-    constexpr int NTH = NBUF == 3 ? 512 : NTHREADS;         // NBUF 3: the 8-wave ring kernel; 4-5: software pipeline
+    constexpr int NTH = NTHREADS;
     constexpr int TILE = BM * (BN * 2 + 16), RED = NTH * 17 * 4;
     constexpr int EPI = TILE > RED ? TILE : RED;            // the reduction reuses the tile's LDS
     constexpr int KLOOP = NBUF * (BM + BN) * BK * 2;
     constexpr int LDS = KLOOP > EPI ? KLOOP : EPI;
-    static_assert(NBUF >= 1 && NBUF <= 5, "one or two K stages, the 3-stage ring, or the 4-5 stage pipeline");
+    static_assert(NBUF >= 1 && NBUF <= 2, "one or two K stages");
     static_assert(NBUF == 1 || EPI <= KLOOP, "epilogue staging must fit the k-loop LDS");
     static_assert(LDS <= 160 * 1024, "LDS");
     constexpr int PER_CU = (160 * 1024) / LDS;
@@ -1384,7 +1155,7 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
     // keeps its accumulators live through the epilogue prefetch (~178 VGPRs), the single-buffer one parks them in
     // LDS first (LATE in gemm_nt_kernel)
     constexpr int CAP = CONV != 0 && BN == 64 ? 3 : 4;     // the 256x64 conv staging spills 7-8 VGPRs at 4
-    constexpr int MIN_F = NBUF == 1 ? (PER_CU < CAP ? PER_CU : CAP) : NBUF >= 3 ? 1 : 2, MIN_B = MIN_F;
+    constexpr int MIN_F = NBUF == 1 ? (PER_CU < CAP ? PER_CU : CAP) : 2, MIN_B = MIN_F;
     auto kf = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_F, NBUF, false, NTH>;
     auto kb = gemm_nt_kernel<BM, BN, WGM, WGN, CONV, MIN_B, NBUF, true, NTH>;
     static int attr = set_lds(kf, LDS) | set_lds(kb, LDS);
@@ -1430,13 +1201,6 @@ int g_halo = 0;
 
 // reduction order of the implicit-GEMM convolutions (A/B knob plx_set_tap_inner): see ConvGeom::tap_inner
 int g_tap_inner = 1;
-
-// the 8-wave ring kernel (NBUF 3, 256 x 128 tiles) for convolutions with N % 128 == 0 (A/B knob plx_set_conv_v2)
-int g_conv_v2 = 0;
-
-// the software-pipelined 4-wave kernel (NBUF 4-5 = LDS ring stages, one block per CU) for the implicit-GEMM
-// convolutions and for the dense (1x1) GEMMs: 0 off, else the stage count (A/B knob plx_set_swp)
-int g_conv_swp = 0, g_dense_swp = 0;
 
 inline bool halo_ok(const ConvGeom& g) {
     if (!g_halo || g.ntaps != 9 || g.S != 1 || g.OS != 0 || g.Hr != g.H || g.Wr != g.W || g.C % BK) return false;
@@ -1619,10 +1383,14 @@ inline int tn2_ring_kb(const V2Cfg& c) {
     return g_tn2_lds_kb <= 64 && tn2_ring(c.na, c.nb, c.ks, 64) ? 64 : 128;
 }
 
+// blocks per CU the v2 plan aims for (0: as many as the ring budget lets reside, 2 at 64 KB, 1 at 128 KB); 1 with the
+// 64 KB ring leaves half of every CU's registers and LDS to the main stream's kernels (A/B knob plx_set_tn2_bpc)
+int g_tn2_bpc = 0;
+
 inline TnPlan tn2_plan(int M, int N1, int N2, int num_cus, const V2Cfg& c) {
     const int bn1 = 64 * c.na, bn2 = 64 * c.nb;
     const int ntiles = (N1 / bn1) * (N2 / bn2);
-    const int cus = (num_cus > 0 ? num_cus : 256) * (tn2_ring_kb(c) <= 64 ? 2 : 1);  // resident blocks
+    const int cus = (num_cus > 0 ? num_cus : 256) * (g_tn2_bpc > 0 ? g_tn2_bpc : tn2_ring_kb(c) <= 64 ? 2 : 1);
     const int step = 32 * c.ks;                       // rows per iteration
     const long plane = (long)N1 * N2;
     const double flops = 2.0 * M * plane;
@@ -1723,13 +1491,6 @@ int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int 
     const bool bwd = D != nullptr || bnr != nullptr;
     if (nt_tall(bwd, M, N, K))
         return launch_nt<256, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
-    if (g_dense_swp && K > BK) {
-        if (N % 128)
-            return launch_nt<256, 64, 4, 1, false, 4>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
-        return g_dense_swp >= 5
-                   ? launch_nt<128, 128, 2, 2, false, 5>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask)
-                   : launch_nt<128, 128, 2, 2, false, 4>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
-    }
     if (N % 128 == 0) {
         const bool one = nt_single(bwd, false, K, ((M + 127) / 128) * (N / 128));
         return one ? launch_nt<128, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b,
@@ -1772,14 +1533,6 @@ void plx_set_halo(int on) { g_halo = on ? 1 : 0; }
 // A/B knob: tap-inner reduction order of the implicit-GEMM convolutions (1) or tap-major (0)
 void plx_set_tap_inner(int on) { g_tap_inner = on ? 1 : 0; }
 
-// A/B knob: the 8-wave ring kernel for the convolutions with N % 128 == 0 (1) or the 4-wave kernels (0)
-void plx_set_conv_v2(int on) { g_conv_v2 = on ? 1 : 0; }
-// software-pipelined NT kernels: LDS ring stages (0 = off, 4 or 5) for the convolutions and the dense GEMMs
-void plx_set_swp(int conv_stages, int dense_stages) {
-    g_conv_swp = conv_stages <= 0 ? 0 : conv_stages >= 5 ? 5 : 4;
-    g_dense_swp = dense_stages <= 0 ? 0 : dense_stages >= 5 ? 5 : 4;
-}
-
 // A/B knob: 256 x 128 NT tiles (0 off, 1 forward, 2 forward + data gradient), see nt_tall
 void plx_set_nt_tall(int mode, int min_k) {
     g_nt_tall = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
@@ -1797,6 +1550,8 @@ void plx_set_tn_wide(int on) { g_tn_wide = on ? 1 : 0; }
 
 // A/B knob: weight-gradient kernel v2 (wgrad_kernel, 1) or v1 (gemm_tn_kernel, 0); lds_kb: v2's ring budget (64 or
 // 128, <= 0 keeps it; workspace queries size for every plan, so either may be toggled after sizing)
+void plx_set_tn2_bpc(int bpc) { g_tn2_bpc = bpc < 0 ? 0 : (bpc > 2 ? 2 : bpc); }
+
 void plx_set_tn_v2(int on, int lds_kb) {
     g_tn_v2 = on < 0 ? 0 : (on > 2 ? 2 : on);
     if (lds_kb > 0) g_tn2_lds_kb = lds_kb <= 64 ? 64 : 128;
@@ -1980,12 +1735,6 @@ int nt_conv_any(const void* A, const void* B, void* C, int M, int N, const ConvG
         if (N % 128 == 0)
             return launch_halo<128, 128, 2, 2, 2>(A, B, C, M, N, g.C, ldb, ldc, zero, stats, s, g, D, ldd, bnr);
         return launch_halo<256, 64, 4, 1, 2>(A, B, C, M, N, g.C, ldb, ldc, zero, stats, s, g, D, ldd, bnr);
-    }
-    if (g_conv_v2 && N % 128 == 0) return nt_conv<256, 128, 4, 2, 3>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
-    if (g_conv_swp) {
-        if (N % 128) return nt_conv<256, 64, 4, 1, 4>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
-        return g_conv_swp >= 5 ? nt_conv<128, 128, 2, 2, 5>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr)
-                               : nt_conv<128, 128, 2, 2, 4>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
     }
     if (nt_tall(bwd, M, N, K)) return nt_conv<256, 128, 2, 2, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
     if (N % 128 == 0)

@@ -37,8 +37,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <utility>
-
 #define PLX_API extern "C" __attribute__((visibility("default")))
 
 namespace {
@@ -151,12 +149,6 @@ template <int V>
 struct IC {
   static constexpr int value = V;
 };
-
-// f(IC<0>{}), f(IC<1>{}), ... in order
-template <typename F, int... Is>
-__device__ __forceinline__ void static_for(F& f, std::integer_sequence<int, Is...>) {
-  (f(IC<Is>{}), ...);
-}
 
 struct Gemm256Args {
   const __bf16* A;
@@ -398,13 +390,15 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
 //     otherwise cover are handled here: the zero-initialised AGPRs are first read many instructions later (DMA
 //     issue, waits, barriers) and the epilogue's AGPR reads follow an explicit s_nop run (mfma_drain).
 //   * phases: a K-tile is four 64 x 64 quadrants of the wave's block, 32 MFMAs each, in the order (0,0) (0,1)
-//     (1,1) (1,0).  Quarters are numbered seq = 4 t + o in READ order (o: 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi) and
+//     (1,0) (1,1).  Quarters are numbered seq = 4 t + o in READ order (o: 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi) and
 //     global phase g (= 4 t + p) issues the ds_reads of seq g + 2 (the fragments phase g + 1 needs) before its own
 //     MFMAs, so an LDS read always has a full phase of MFMAs to land.  Fragment sets: A-lo, A-hi and two B sets
 //     that swap roles every K-tile (B-lo of tile t + 1 is read into the set B-hi of tile t just released).
-//   * DMA ring: seq q's slot is free once its reads retired (lgkmcnt(0) at the end of phase q - 2 + barrier), so
-//     phase g restages seq g + 9 into the slot of seq g + 1; the end of phase g waits (counted vmcnt) for seq
-//     g + 3, the quarter phase g + 1 reads.  Six quarters (24 DMAs per wave) stay in flight; one barrier per phase.
+//   * DMA ring: one barrier per TWO phases.  Seq q's slot is free once its reads retired (lgkmcnt(0) at the end of
+//     an odd phase + barrier), so phase g restages seq g + 8; the end of each odd phase g waits (counted vmcnt) for
+//     seq g + 4, the last quarter the next two phases read.
+//   (Round 5 removed the one-barrier-per-phase and the MFMA-interleaved read/DMA variants of this schedule, measured
+//   slower on every LM shape: profiles/r4_lm_gemm.md, r4_lm_gemm_variants_vs_hipblaslt.jsonl.)
 // ---------------------------------------------------------------------------------------------------------------
 constexpr int NTH4 = 256;
 
@@ -425,7 +419,7 @@ __device__ __forceinline__ void wait_vm4(int n) {  // n = DMAs allowed in flight
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool AK, bool BKM, bool ACC, bool SLAB, bool PAIR, bool ILV>
+template <bool AK, bool BKM, bool ACC, bool SLAB>
 __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -468,13 +462,6 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
 #pragma unroll
     for (int pc = 0; pc < 4; ++pc) glds(r, src[O][pc] + koff, dst + (wave + 4 * pc) * 1024);
   };
-  auto issue_piece = [&](auto ko, int q, auto pcc) {  // one of the 4 DMAs of `issue`
-    constexpr int O = decltype(ko)::value, PC = decltype(pcc)::value;
-    constexpr bool ISA = O == 0 || O == 3;
-    const int t = q >> 2;
-    const uint32_t koff = (uint32_t)t * (ISA ? astep : bstep);
-    glds(ISA ? ra : rb, src[O][PC] + koff, smem + (t & 1) * BUF + O * QUARTER + (wave + 4 * PC) * 1024);
-  };
 
   f32x4 acc[8][8];  // [n tile: 8 x 16 = the wave's 128 columns][m tile: 8 x 16 = its 128 rows]
 #pragma unroll
@@ -504,16 +491,8 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
     if constexpr (O == 0 || O == 3) return read_q(img, aoff, IC<AK>{});
     else return read_q(img, boff, IC<BKM>{});
   };
-  auto read_one = [&](auto ko, int q, auto tc, auto sc) {  // fragment (t, s) of `read_seq`
-    constexpr int O = decltype(ko)::value, T = decltype(tc)::value, SS = decltype(sc)::value;
-    constexpr bool KM = (O == 0 || O == 3) ? AK : BKM;
-    const int(&off)[4] = (O == 0 || O == 3) ? aoff : boff;
-    const char* img = smem + ((q >> 2) & 1) * BUF + O * QUARTER;
-    return KM ? ld_frag_k(img + off[SS] + T * 2048) : ld_frag_t(img + off[T] + SS * 8192);
-  };
 
-  // prologue: seq 0 .. min(8, S) - 1 (tiles 0 and 1), read seq 0 (A-lo) and 1 (B-lo) of tile 0, then seq 8
-  // into seq 0's slot once every wave's reads of it retired
+  // prologue: seq 0 .. min(8, S) - 1 (tiles 0 and 1), read seq 0 (A-lo) and 1 (B-lo) of tile 0
   auto pro = [&](auto qc) {
     constexpr int Q = decltype(qc)::value;
     if (Q < S) issue(IC<(Q & 3)>{}, Q);
@@ -526,51 +505,26 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
   FragA a_hi, b_hi;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  if (PAIR) {  // phases 0 and 1 read seq 2 and 3 after the next barrier
-    wait_vm4(4 * (min(8, S) - 1 - 3));
-  } else {
-    if (S > 8) issue(IC<0>{}, 8);
-    wait_vm4(4 * (min(8, S - 1) - 2));
-  }
+  wait_vm4(4 * (min(8, S) - 1 - 3));  // phases 0 and 1 read seq 2 and 3 after the next barrier
   __builtin_amdgcn_s_barrier();
 
-  // One phase g = 4 kt + P: ds_reads of seq g + 2 into `nxt`, DMA of seq g + 9, the quadrant's 32 MFMAs, then
-  // lgkmcnt(0) + vmcnt for seq g + 3 + barrier.
+  // One phase g = 4 kt + P: ds_reads of seq g + 2 into `nxt`, DMA of seq g + 8, the quadrant's 32 MFMAs, then
+  // (odd phases) lgkmcnt(0) + vmcnt for seq g + 4 + barrier.
   auto phase = [&](auto ph, int kt, const FragA& fa, const FragA& fb, FragA& nxt, auto mi_, auto ni_) {
     constexpr int P = decltype(ph)::value, MI = decltype(mi_)::value, NI = decltype(ni_)::value;
     const int g = 4 * kt + P;
-    constexpr int AHEAD = PAIR ? 8 : 9, RO = (P + 2) & 3, DO = (P + AHEAD) & 3;
-    const bool dma = g + AHEAD < S;
-    if constexpr (!ILV) {
-      nxt = read_seq(IC<RO>{}, g + 2);  // past the last tile: stale LDS into a dead set, harmless
-      if (dma) issue(IC<DO>{}, g + AHEAD);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 4; ++b) mfma_agpr(acc[NI * 4 + a][MI * 4 + b], fb.v[a][s], fa.v[b][s]);
-    } else {
-      // interleaved: MFMA i is followed by fragment read i (i < 8) or DMA piece i - 8 (8 <= i < 12), so the
-      // reads and DMA issue run in the shadow of this wave's own MFMAs instead of ahead of them
-      auto step = [&](auto ic) {
-        constexpr int I = decltype(ic)::value, SS = I >> 4, A = (I >> 2) & 3, B = I & 3;
-        mfma_agpr(acc[NI * 4 + A][MI * 4 + B], fb.v[A][SS], fa.v[B][SS]);
-        if constexpr (I < 8) nxt.v[I >> 1][I & 1] = read_one(IC<RO>{}, g + 2, IC<(I >> 1)>{}, IC<(I & 1)>{});
-        else if constexpr (I < 12) {
-          if (dma) issue_piece(IC<DO>{}, g + AHEAD, IC<(I - 8)>{});
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      static_for(step, std::make_integer_sequence<int, 32>{});
-    }
+    constexpr int AHEAD = 8, RO = (P + 2) & 3, DO = (P + AHEAD) & 3;
+    nxt = read_seq(IC<RO>{}, g + 2);  // past the last tile: stale LDS into a dead set, harmless
+    if (g + AHEAD < S) issue(IC<DO>{}, g + AHEAD);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (!PAIR) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      wait_vm4(4 * (min(g + 9, S - 1) - (g + 3)));
-      __builtin_amdgcn_s_barrier();
-    } else if constexpr (P & 1) {  // seqs g + 3 and g + 4 are read in the next two phases
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) mfma_agpr(acc[NI * 4 + a][MI * 4 + b], fb.v[a][s], fa.v[b][s]);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (P & 1) {  // seqs g + 3 and g + 4 are read in the next two phases
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       wait_vm4(4 * (min(g + 8, S - 1) - (g + 4)));
       __builtin_amdgcn_s_barrier();
@@ -674,28 +628,20 @@ __global__ void __launch_bounds__(256) gemm256_reduce(const float* __restrict__ 
   }
 }
 
-int g_waves = 8;  // 8: the ping-pong kernel, 4: gemm256w4_kernel (plx_gemm256_set_waves)
-int g_w4 = 0;     // 4-wave kernel schedule bits: 1 = one barrier per two phases, 2 = reads / DMAs interleaved
-                  // with the MFMAs (plx_gemm256_set_waves(4 + bits))
+int g_waves = 8;  // 8: the ping-pong kernel, 4: gemm256w4_kernel (plx_gemm256_set_waves 8 / 5)
 
-// variant: 8 = the ping-pong kernel, 4 + bits = the 4-wave kernel (see plx_gemm256_set_waves), 0 = the global knob
+// variant: 8 = the ping-pong kernel, 5 = the 4-wave kernel, 0 = the global knob
 template <bool AK, bool BKM, bool ACC, bool SLAB>
 int launch(const Gemm256Args& a, int splits, hipStream_t st, int variant) {
   const dim3 grid((a.M / BM) * (a.N / BN), splits);
-  const int v = variant >= 4 && variant <= 8 ? variant : (g_waves == 4 ? 4 + g_w4 : 8);
-  if (v < 8) {
-    void (*ks[4])(Gemm256Args) = {gemm256w4_kernel<AK, BKM, ACC, SLAB, false, false>,
-                                   gemm256w4_kernel<AK, BKM, ACC, SLAB, true, false>,
-                                   gemm256w4_kernel<AK, BKM, ACC, SLAB, false, true>,
-                                   gemm256w4_kernel<AK, BKM, ACC, SLAB, true, true>};
-    static const int attr = [&] {
-      for (auto k : ks)
-        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) != hipSuccess)
-          return -4;
-      return 0;
-    }();
+  const bool four = variant == 5 || (variant != 8 && g_waves == 4);
+  if (four) {
+    auto k = gemm256w4_kernel<AK, BKM, ACC, SLAB>;
+    static const int attr =
+        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess ? 0
+                                                                                                                 : -4;
     if (attr) return attr;
-    hipLaunchKernelGGL(ks[(v - 4) & 3], grid, dim3(NTH4), LDS_BYTES, st, a);
+    hipLaunchKernelGGL(k, grid, dim3(NTH4), LDS_BYTES, st, a);
     return 0;
   }
   auto k = gemm256_kernel<AK, BKM, ACC, SLAB>;
@@ -744,13 +690,12 @@ PLX_API int plx_gemm256_set_group(int group) {
   return prev;
 }
 
-// A/B knob: 8 (the 8-wave ping-pong kernel) or 4 + bits (the 4-wave AGPR-accumulator kernel; bit 0: one barrier per
-// two phases instead of one per phase, bit 1: fragment reads and DMAs interleaved with the MFMAs); returns the
-// previous value
+// A/B knob: 8 (the 8-wave ping-pong kernel) or 5 (the 4-wave AGPR-accumulator kernel, one barrier per two phases)
+// for calls without a per-call variant; returns the previous value
 PLX_API int plx_gemm256_set_waves(int waves) {
-  const int prev = g_waves == 4 ? 4 + g_w4 : g_waves;
+  const int prev = g_waves == 4 ? 5 : 8;
   if (waves == 8) g_waves = 8;
-  if (waves >= 4 && waves <= 7) g_waves = 4, g_w4 = waves - 4;
+  if (waves == 5) g_waves = 4;
   return prev;
 }
 
@@ -759,7 +704,7 @@ PLX_API int plx_gemm256_set_waves(int waves) {
 // ws: fp32 workspace of plx_gemm256_splits(M, N, K) * M * N floats when that is > 1 (may be null otherwise).
 // Returns 0, or < 0 on a shape / layout the kernel does not take (nothing launched).
 // gelu_out: bf16 [M][ldc] (same layout as C, 16-byte aligned) receiving gelu_tanh(C), or null (not with accumulate).
-// variant: the kernel schedule for this call (8, or 4..7: see plx_gemm256_set_waves; 0 = the global knob)
+// variant: the kernel schedule for this call (8 or 5: see plx_gemm256_set_waves; 0 = the global knob)
 PLX_API int plx_gemm256_exv(const void* A, const void* B, void* C, void* ws, int M, int N, int K, int lda, int ldb,
                             int ldc, int a_kmajor, int b_kmajor, float alpha, int accumulate, const float* bias,
                             void* gelu_out, int variant, void* stream) {

@@ -21,7 +21,7 @@ GPT-2 layers (and the tied head's) win 1.05-1.95x everywhere, a few Llama-3 8B w
 percent, and the large forward / data-gradient shapes swing between 1.05x and 0.79x with the box (the kernel is
 more clock-sensitive than hipBLASLt's), losing in the Llama training step (16.0k vs 18.0k tokens/s all-kernel vs
 all-hipBLASLt on one box).  ``SCHEDULE`` holds the shapes that go to the kernel and the schedule each runs
-(8 = the 8-wave ping-pong kernel, 4-7 = the 4-wave AGPR kernel's variants, csrc/gemm256.hip); any other supported
+(8 = the 8-wave ping-pong kernel, 5 = the 4-wave AGPR kernel, csrc/gemm256.hip); any other supported
 shape goes to the kernel when it is a split-K shape (``plx_gemm256_splits > 1``: the narrow-output, long-reduction
 weight gradients) and to hipBLASLt otherwise.  The choice is a pure function of the shape -- reproducible, and the
 same kernel on every DP rank.  :func:`decisions` lists the shapes seen and what ran.

@@ -23,6 +23,20 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def hw_queue_env(env: Dict[str, str]) -> Dict[str, str]:
+    """PLX_HW_QUEUES=n (opt-in): raise GPU_MAX_HW_QUEUES to n (at most 32) in the environment of a process polyflow
+    launches; never lowered, and nothing changes without it (the framework's streams fit the box's default 4 queues:
+    profiles/r5_hw_queues.md).  Returns ``env``."""
+    try:
+        want = int(env.get("PLX_HW_QUEUES", "0") or 0)
+        have = int(env.get("GPU_MAX_HW_QUEUES", "0") or 0)
+    except ValueError:
+        return env
+    if want > have:
+        env["GPU_MAX_HW_QUEUES"] = str(min(want, 32))
+    return env
+
+
 def cluster_def(framework: Optional[str], cluster: Dict[str, int], base_port: int) -> Dict[str, List[str]]:
     """POLYAXON_CLUSTER: {role: [host:port, ...]} for every replica (all on 127.0.0.1, distinct ports)."""
     out: Dict[str, List[str]] = {}
@@ -114,6 +128,7 @@ def trial_env(*, base_env: Optional[Dict[str, str]] = None, experiment: Dict[str
     env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in devices)
     env["LOCAL_RANK"] = str(local_rank)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    hw_queue_env(env)
     n_ranks = sum(len(v) for v in cluster.values()) if cluster else 1
     if n_ranks > 1:
         # RCCL watchdog: a rank that dies or hangs inside a collective tears the process group

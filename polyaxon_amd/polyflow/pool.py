@@ -27,6 +27,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
+from polyaxon_amd.polyflow.env import hw_queue_env
 from polyaxon_amd.polyflow.resident import Channel, ChannelClosed
 
 log = logging.getLogger("polyaxon_amd.polyflow.pool")
@@ -123,18 +124,11 @@ class ResidentPool:
         if world > 1:
             return self._spawn_gang(wid, owner, a, key, program, params, max_active)
         parent, child = socket.socketpair()
-        env = dict(os.environ)
-        env["HIP_VISIBLE_DEVICES"] = ",".join(str(d) for d in a.devices)
-        env.pop("ROCR_VISIBLE_DEVICES", None)
-        env["PYTHONUNBUFFERED"] = "1"
-        env.pop("PLX_HBM_GB", None)
-        env.pop("PLX_HBM_FRACTION", None)
+        env = self._worker_env(a.devices)
         if hbm_gb > 0:  # the executor's HBM budget (client/budget.py, applied in ResidentWorker.build)
             env["PLX_HBM_GB"] = f"{hbm_gb:g}"
         elif 0 < gpu < 1:
             env["PLX_HBM_FRACTION"] = f"{gpu:g}"
-        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        env["PYTHONPATH"] = pkg_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
         log_dir = os.path.join(self.flow.paths.root, "executors")
         os.makedirs(log_dir, exist_ok=True)
         log_path = os.path.join(log_dir, f"worker{wid}.log")
@@ -173,17 +167,21 @@ class ResidentPool:
         env.pop("PLX_HBM_FRACTION", None)
         pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = pkg_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        hw_queue_env(env)
         return env
 
     def _spawn_gang(self, wid, owner, a, key, program, params, max_active) -> Optional[WorkerHandle]:
         """A resident executor spanning a DP gang (``resources.gpu: N``): one worker process per device, ranks wired
         with the torch.distributed env contract (MASTER_ADDR / MASTER_PORT / rank / world, as polyflow/env.py gives a
-        process-mode PyTorch job); rank 0's channel is the executor's, the others only carry the init handshake."""
+        process-mode PyTorch job); rank 0's channel is the executor's, the others only carry the init handshake.
+        The rendezvous port is bound and listening HERE and rank 0 inherits the listening socket
+        (PLX_MASTER_LISTEN_FD, the TCPStore's master_listen_fd): picking a free port and closing it before rank 0
+        binds it again would race with any other process binding ports on the node."""
         world = len(a.devices)
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-        s.close()
+        listener = socket.socket()
+        listener.bind(("127.0.0.1", 0))
+        listener.listen(128)
+        port = listener.getsockname()[1]
         log_dir = os.path.join(self.flow.paths.root, "executors")
         os.makedirs(log_dir, exist_ok=True)
         ranks = []
@@ -195,10 +193,14 @@ class ResidentPool:
                 env = self._worker_env([dev])
                 env.update(PLX_RESIDENT_RANK=str(r), PLX_RESIDENT_WORLD=str(world), MASTER_ADDR="127.0.0.1",
                            MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0")
+                fds = (child.fileno(),)
+                if r == 0:
+                    env["PLX_MASTER_LISTEN_FD"] = str(listener.fileno())
+                    fds += (listener.fileno(),)
                 path = os.path.join(log_dir, f"worker{wid}.rank{r}.log")
                 with open(path, "ab") as logf:
                     proc = subprocess.Popen(argv + [str(child.fileno())] + (["--cpu"] if cpu else []), env=env,
-                                            pass_fds=(child.fileno(),), stdout=logf, stderr=subprocess.STDOUT,
+                                            pass_fds=fds, stdout=logf, stderr=subprocess.STDOUT,
                                             stdin=subprocess.DEVNULL, start_new_session=True)
                 child.close()
                 ranks.append((proc, Channel(parent), path))
@@ -213,6 +215,8 @@ class ResidentPool:
             log.error("cannot start resident DP gang: %s", e)
             self.flow.store.add_cluster_event("resident_executor", "error", f"gang spawn failed: {e}")
             return None
+        finally:
+            listener.close()  # rank 0 holds its own copy
         if getattr(self.flow, "numa_bind", False):
             for (proc, _, _), dev in zip(ranks, a.devices):
                 self.flow._bind_cpus(proc.pid, [dev])

@@ -800,7 +800,13 @@ class _GangGroup:
         self.rank, self.world = rank, world
         self.device = torch.device(device)
         long = datetime.timedelta(days=7)  # an idle executor blocks in the control broadcast between groups
-        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=long)
+        # rank 0 serves the store on the pool's already-listening socket (polyflow/pool.py _spawn_gang); every rank
+        # builds its store explicitly so all of them see the same (unprefixed) key space
+        fd = os.environ.get("PLX_MASTER_LISTEN_FD") if rank == 0 else None
+        kw = {"master_listen_fd": int(fd)} if fd else {}
+        store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]), world,
+                              rank == 0, timeout=long, **kw)
+        dist.init_process_group("gloo", store=store, rank=rank, world_size=world, timeout=long)
         self.comm = None  # acquired on first use (collective: every rank reaches it at the same program point)
 
     def broadcast(self, obj):

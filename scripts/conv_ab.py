@@ -30,13 +30,8 @@ S2 = [(256, 128, 128, 56, 2), (256, 256, 256, 28, 2), (256, 512, 512, 14, 2)]
 
 VARIANTS = {
     "r3": {},  # the round-3 kernels (libplx_conv_r3ref.so, built from git history into _native/ when present)
-    "base": {"plx_set_tap_inner": 0, "plx_set_conv_v2": 0},
-    "tap_inner": {"plx_set_tap_inner": 1, "plx_set_conv_v2": 0},
-    "v2": {"plx_set_tap_inner": 0, "plx_set_conv_v2": 1},
-    "v2_tap_inner": {"plx_set_tap_inner": 1, "plx_set_conv_v2": 1},
-    "swp4": {"plx_set_tap_inner": 1, "plx_set_conv_v2": 0, "plx_set_swp": (4, 4)},
-    "swp5": {"plx_set_tap_inner": 1, "plx_set_conv_v2": 0, "plx_set_swp": (5, 5)},
-    "ti": {"plx_set_tap_inner": 1, "plx_set_conv_v2": 0, "plx_set_swp": (0, 0)},
+    "base": {"plx_set_tap_inner": 0},
+    "tap_inner": {"plx_set_tap_inner": 1},
 }
 
 
