@@ -1383,14 +1383,16 @@ inline int tn2_ring_kb(const V2Cfg& c) {
     return g_tn2_lds_kb <= 64 && tn2_ring(c.na, c.nb, c.ks, 64) ? 64 : 128;
 }
 
-// blocks per CU the v2 plan aims for (0: as many as the ring budget lets reside, 2 at 64 KB, 1 at 128 KB); 1 with the
-// 64 KB ring leaves half of every CU's registers and LDS to the main stream's kernels (A/B knob plx_set_tn2_bpc)
+// blocks the v2 plan aims for: 1 or 2 per CU, or (> 2) a total block count; 0: as many as the ring budget lets
+// reside (2 per CU at 64 KB, 1 at 128 KB).  1 per CU with the 64 KB ring leaves half of every CU's registers and LDS to
+// the main stream's kernels; a total below the CU count leaves whole CUs to them (A/B knob plx_set_tn2_bpc)
 int g_tn2_bpc = 0;
 
 inline TnPlan tn2_plan(int M, int N1, int N2, int num_cus, const V2Cfg& c) {
     const int bn1 = 64 * c.na, bn2 = 64 * c.nb;
     const int ntiles = (N1 / bn1) * (N2 / bn2);
-    const int cus = (num_cus > 0 ? num_cus : 256) * (g_tn2_bpc > 0 ? g_tn2_bpc : tn2_ring_kb(c) <= 64 ? 2 : 1);
+    const int cus = g_tn2_bpc > 2 ? g_tn2_bpc
+                                  : (num_cus > 0 ? num_cus : 256) * (g_tn2_bpc > 0 ? g_tn2_bpc : tn2_ring_kb(c) <= 64 ? 2 : 1);
     const int step = 32 * c.ks;                       // rows per iteration
     const long plane = (long)N1 * N2;
     const double flops = 2.0 * M * plane;
@@ -1550,7 +1552,7 @@ void plx_set_tn_wide(int on) { g_tn_wide = on ? 1 : 0; }
 
 // A/B knob: weight-gradient kernel v2 (wgrad_kernel, 1) or v1 (gemm_tn_kernel, 0); lds_kb: v2's ring budget (64 or
 // 128, <= 0 keeps it; workspace queries size for every plan, so either may be toggled after sizing)
-void plx_set_tn2_bpc(int bpc) { g_tn2_bpc = bpc < 0 ? 0 : (bpc > 2 ? 2 : bpc); }
+void plx_set_tn2_bpc(int bpc) { g_tn2_bpc = bpc < 0 ? 0 : (bpc > 4096 ? 4096 : bpc); }
 
 void plx_set_tn_v2(int on, int lds_kb) {
     g_tn_v2 = on < 0 ? 0 : (on > 2 ? 2 : on);

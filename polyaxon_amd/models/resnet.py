@@ -55,7 +55,7 @@ class Bottleneck(nn.Module):
         return self.bn3(self.conv3(out, bn_link=True), identity, residual_link=True)
 
 
-_DEFER_DOWN_BN = os.environ.get("PLX_DEFER_DOWN_BN", "1") != "0"  # A/B knob (scripts/ab_check.sh)
+_DEFER_DOWN_BN = os.environ.get("PLX_DEFER_DOWN_BN", "1") != "0"  # A/B knob (scripts/gpu.sh ab)
 _STEM_FUSED = os.environ.get("PLX_STEM_FUSED", "1") != "0"  # A/B knob: stem BN + ReLU + max-pool in one op
 _STEM_CONV = os.environ.get("PLX_STEM_CONV", "1") != "0"  # A/B knob: native stem convolution
 

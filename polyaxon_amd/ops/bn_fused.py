@@ -19,7 +19,7 @@ from polyaxon_amd.ops.conv1x1 import BnLink
 from polyaxon_amd.ops.flat import direct_grad
 
 
-_MASKED_RESGRAD = os.environ.get("PLX_MASKED_RESGRAD", "1") != "0"  # A/B knob (scripts/ab_check.sh)
+_MASKED_RESGRAD = os.environ.get("PLX_MASKED_RESGRAD", "1") != "0"  # A/B knob (scripts/gpu.sh ab)
 
 
 def _stream() -> int:

@@ -4,7 +4,7 @@ POLYAXON_DECLARATIONS / CLI flags, report metrics through the tracking client).
     python -m polyaxon_amd.trainers mlp     --lr 0.01 --bs 256 --steps 200          (config 2)
     python -m polyaxon_amd.trainers resnet  --lr 0.1 --steps 80                     (config 3, process mode)
     python -m polyaxon_amd.trainers lm --model gpt2_125m --steps 50                  (config 4, DP=N ranks)
-    python -m polyaxon_amd.trainers lm --model llama3_8b --seq 2048 --bs 1           (config 5, DP=8)
+    python -m polyaxon_amd.trainers lm --model llama3_8b --seq 4096 --bs 1 --zero1   (config 5, DP=8)
 
 Every trainer: flat fp32 master weights + fused HIP optimizer, bf16 autocast, synthetic data of the real
 shape, metrics streamed from the GPU (tracking client MetricStream), DP through FlatDDP (RCCL) when

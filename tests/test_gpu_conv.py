@@ -567,3 +567,45 @@ def test_conv_tap_order(cuda, shape, cout, stride):
         yf = y.permute(0, 2, 3, 1).reshape(-1, cout)
         torch.testing.assert_close(st[0], yf.sum(0), rtol=1e-3, atol=1e-1, msg=str(key))
         torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1, msg=str(key))
+
+
+@pytest.mark.parametrize("variant", [(0, -1), (1, 64), (1, 128)], ids=["v1", "v2_64k", "v2_128k"])
+def test_wgrad_kernels_every_class(cuda, variant):
+    """Both weight-gradient kernels (plx_set_tn_v2: v1 gemm_tn_kernel; v2 wgrad_kernel with a 64 or 128 KB LDS ring)
+    on every ResNet-50 wgrad class against fp32 F.conv2d weight gradients: dense 1x1 (ragged pixel counts), 3x3
+    stride 1 and 2 (the row gather, taps at the image border), 1x1 stride 2 (downsample), and the 7x7 stem."""
+    from polyaxon_amd.ops import _native
+    from polyaxon_amd.ops.conv import ConvKxK
+    from polyaxon_amd.ops.conv1x1 import Conv1x1
+    from polyaxon_amd.ops.stem import StemConv
+
+    cases = [("1x1", (4, 256, 14, 14), 64, 1), ("1x1", (3, 64, 17, 11), 256, 1), ("1x1", (2, 512, 7, 9), 1024, 1),
+             ("3x3", (2, 64, 28, 28), 64, 1), ("3x3", (3, 128, 13, 9), 128, 1), ("3x3", (2, 256, 14, 14), 256, 2),
+             ("3x3", (5, 512, 7, 7), 512, 1), ("1x1", (2, 256, 14, 14), 512, 2), ("1x1", (3, 512, 9, 7), 1024, 2),
+             ("stem", (2, 3, 64, 48), 64, 2)]
+    lib = _native.lib("plx_conv")
+    lib.plx_set_tn_v2(*variant)
+    try:
+        for kind, shape, cout, stride in cases:
+            torch.manual_seed(5)
+            cin = shape[1]
+            if kind == "stem":
+                conv, k, pad = StemConv().to(cuda), 7, 3
+            elif kind == "1x1" and stride == 1:
+                conv, k, pad = Conv1x1(cin, cout).to(cuda), 1, 0
+            else:
+                k = 3 if kind == "3x3" else 1
+                conv, pad = ConvKxK(cin, cout, k, stride).to(cuda), k // 2
+            conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
+            x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            y = conv(x.clone().requires_grad_())
+            g = torch.randn(y.shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            y.backward(g)
+            torch.cuda.synchronize()
+            w = conv.weight.detach().float().requires_grad_()
+            F.conv2d(x.float(), w, None, stride, pad).backward(g.float())
+            got = conv.weight.grad.float()
+            torch.testing.assert_close(got, w.grad, rtol=2e-2, atol=2e-2 * float(w.grad.abs().max()),
+                                       msg=f"{kind} {shape} -> {cout} s{stride}")
+    finally:
+        lib.plx_set_tn_v2(int(os.environ.get("PLX_TN_V2", "1").partition(",")[0]), -1)
