@@ -1371,7 +1371,10 @@ inline void plan_reducer(TnPlan& p, long plane) {
 // time = compute (FLOP / chip rate, stretched by that quantisation) + a per-block fixed cost (ring fill + epilogue)
 // per round of blocks + the slab bytes (s + 1 planes: written, read back by the reducer) when s > 1.  Rates are
 // round numbers from the v2 isolated runs (profiles/r5_wgrad_v2.md).
-constexpr double kTnCuFlops = 3.2e12, kTnBlockUs = 2.5, kTnSlabBw = 4.5e12;
+constexpr double kTnCuFlops = 3.2e12, kTnBlockUs = 2.5;
+// slab bandwidth the plan prices (A/B knob plx_set_tn2_slab_bw): 4.5 TB/s is the isolated rate, but in the training
+// step the slab write + reduce passes compete with the main stream's memory-bound BatchNorm kernels
+double g_tn2_slab_bw = 4.5e12;
 
 // ring slots of a v2 block within an LDS budget (a multiple of KS, <= 16); 0 when a group would get < 2 slots
 constexpr int tn2_ring(int na, int nb, int ks, int lds_kb) {
@@ -1405,7 +1408,7 @@ inline TnPlan tn2_plan(int M, int N1, int N2, int num_cus, const V2Cfg& c) {
         const long blocks = (long)ntiles * s;
         const long rounds = (blocks + cus - 1) / cus;
         const double t = flops / (kTnCuFlops * cus) * ((double)rounds * cus / blocks) + rounds * kTnBlockUs * 1e-6 +
-                         (s > 1 ? (double)(s + 1) * plane * 4 / kTnSlabBw : 0.0);
+                         (s > 1 ? (double)(s + 1) * plane * 4 / g_tn2_slab_bw : 0.0);
         if (t < best_t * 0.995) best_t = t, best = s;
     }
     int kchunk = (M + best - 1) / best;
@@ -1552,6 +1555,13 @@ void plx_set_tn_wide(int on) { g_tn_wide = on ? 1 : 0; }
 
 // A/B knob: weight-gradient kernel v2 (wgrad_kernel, 1) or v1 (gemm_tn_kernel, 0); lds_kb: v2's ring budget (64 or
 // 128, <= 0 keeps it; workspace queries size for every plan, so either may be toggled after sizing)
+// diagnostics: K slices (fp32 slabs) the weight-gradient plan of this problem uses (v2: wgrad_kernel's plan)
+int plx_tn_plan_slices(int M, int N1, int N2, int num_cus, int v2) {
+    if (M <= 0 || N1 % 64 || N2 % 64) return -1;
+    return v2 ? tn2_plan(M, N1, N2, num_cus, v2_cfg(N1, N2)).slices : tn_plan(M, N1, N2, num_cus).slices;
+}
+
+void plx_set_tn2_slab_bw(int gb_per_s) { if (gb_per_s > 0) g_tn2_slab_bw = gb_per_s * 1e9; }
 void plx_set_tn2_bpc(int bpc) { g_tn2_bpc = bpc < 0 ? 0 : (bpc > 4096 ? 4096 : bpc); }
 
 void plx_set_tn_v2(int on, int lds_kb) {
