@@ -1334,9 +1334,12 @@ int launch_tn_st(const void* A, const void* B, float* W, int M, int N1, int N2, 
 }
 
 // ---- v2 weight-gradient plan (wgrad_kernel): one block per CU, tile by the output shape, slices by a cost model
+// In the training step (weight gradients on the side stream beside the data-gradient chain) v2 with a 64 KB ring and
+// 3/4 of the CUs' worth of blocks measured +0.7 % trials/h over v1 (4 runs each on 2 boxes); with a 128 KB ring or
+// one block on every CU it was 2-4 % slower, although faster in isolation (profiles/r5_wgrad_v2.md)
 int g_tn_v2 = 1;        // 1: wgrad_kernel (v2), 0: gemm_tn_kernel (v1), 2: v2 for the gathered convolutions only
                         // (A/B knob plx_set_tn_v2)
-int g_tn2_lds_kb = 128; // LDS ring budget of a v2 block: 128 KB (one block per CU) or 64 KB (two per CU, or room for the
+int g_tn2_lds_kb = 64;  // LDS ring budget of a v2 block: 128 KB (one block per CU) or 64 KB (two per CU, or room for the
                         // main stream's blocks beside it); configurations whose groups would get < 2 slots keep 128
 
 struct V2Cfg { int na, nb, ks; };
@@ -1386,16 +1389,16 @@ inline int tn2_ring_kb(const V2Cfg& c) {
     return g_tn2_lds_kb <= 64 && tn2_ring(c.na, c.nb, c.ks, 64) ? 64 : 128;
 }
 
-// blocks the v2 plan aims for: 1 or 2 per CU, or (> 2) a total block count; 0: as many as the ring budget lets
-// reside (2 per CU at 64 KB, 1 at 128 KB).  1 per CU with the 64 KB ring leaves half of every CU's registers and LDS to
-// the main stream's kernels; a total below the CU count leaves whole CUs to them (A/B knob plx_set_tn2_bpc)
+// blocks the v2 plan aims for: 1 or 2 per CU, or (> 2) a total block count; 0 (default): 3/4 of the CUs, which leaves
+// a quarter of the CUs whole to the main stream's kernels (in-step sweep over 128-256 blocks: 192 best, 176 / 208 /
+// 224 / 256 at or below v1; A/B knob plx_set_tn2_bpc)
 int g_tn2_bpc = 0;
 
 inline TnPlan tn2_plan(int M, int N1, int N2, int num_cus, const V2Cfg& c) {
     const int bn1 = 64 * c.na, bn2 = 64 * c.nb;
     const int ntiles = (N1 / bn1) * (N2 / bn2);
-    const int cus = g_tn2_bpc > 2 ? g_tn2_bpc
-                                  : (num_cus > 0 ? num_cus : 256) * (g_tn2_bpc > 0 ? g_tn2_bpc : tn2_ring_kb(c) <= 64 ? 2 : 1);
+    const int ncu = num_cus > 0 ? num_cus : 256;
+    const int cus = g_tn2_bpc > 2 ? g_tn2_bpc : g_tn2_bpc > 0 ? ncu * g_tn2_bpc : (ncu * 3) / 4;
     const int step = 32 * c.ks;                       // rows per iteration
     const long plane = (long)N1 * N2;
     const double flops = 2.0 * M * plane;

@@ -608,4 +608,5 @@ def test_wgrad_kernels_every_class(cuda, variant):
             torch.testing.assert_close(got, w.grad, rtol=2e-2, atol=2e-2 * float(w.grad.abs().max()),
                                        msg=f"{kind} {shape} -> {cout} s{stride}")
     finally:
-        lib.plx_set_tn_v2(int(os.environ.get("PLX_TN_V2", "1").partition(",")[0]), -1)
+        v2, _, kb = os.environ.get("PLX_TN_V2", "1,64").partition(",")
+        lib.plx_set_tn_v2(int(v2), int(kb) if kb else 64)
