@@ -678,7 +678,12 @@ def main() -> int:
     if bench is not None:
         bench.close()
     if comm is not None:
-        comm.close()
+        if comm is early_comm and world > 1:
+            from polyaxon_amd.parallel import comm as _comm
+
+            _comm.release(comm)  # acquired from the registry above
+        else:
+            comm.close()
     if world > 1:
         dist.destroy_process_group()
     if ctl_proc is not None:
