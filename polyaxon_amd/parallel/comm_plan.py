@@ -18,6 +18,10 @@ instead of a constant tuned for a switched fabric:
   link bandwidth grows with W, so does the bucket (a 2-rank gang wants ~10 MB, 8 ranks ~300 MB).  The size is
   clamped so the backward still overlaps at least ``min_buckets`` collectives (the last bucket, the first layers'
   gradients, is the exposed one) and to at least ``min_mb``.
+* **Measured at start-up.**  With ``bucket_mb="auto"`` at world > 1, :class:`~polyaxon_amd.parallel.ddp.FlatDDP`
+  first times a few all-reduces on the trial's own communicator (:func:`calibrate`: 1-64 MB on the GPU, ~0.1 s),
+  averages the times over the ranks (so every rank fits the same numbers and cuts the same buckets) and plans with
+  that fit (``source: "measured"``).  ``PLX_COMM_CALIBRATE=0`` keeps the analytic link model.
 * **Measured table.**  ``python -m torch.distributed.run --nproc-per-node W -m polyaxon_amd.parallel.rccl``
   prints the node's all-reduce algbw per message size; :func:`fit_table` turns those rows into (alpha, busbw) by a
   least-squares fit of ``t(B) = a + b B``, and ``PLX_COMM_TABLE=<that JSON>`` makes :func:`plan` use the fit for
@@ -63,6 +67,7 @@ class FittedModel:
     world: int
     alpha_s_: float
     busbw: float
+    measured: bool = False  # timed at start-up on the trial's communicator (calibrate), not read from a table
 
     def busbw_GBps(self, world: int) -> float:
         return self.busbw
@@ -112,6 +117,53 @@ def load_table(path: str, world: int) -> Optional[FittedModel]:
     return None
 
 
+def calibrate(comm, world: int, device, sizes: Optional[Sequence[int]] = None, reps: int = 5,
+              retry: bool = True) -> Optional[FittedModel]:
+    """Fit (alpha, busbw) from all-reduces of ``sizes`` bytes timed on ``comm`` (a parallel/comm.py communicator:
+    RCCL on the GPU, the gloo shim on the CPU).  Collective: every rank of the group calls it with the same
+    arguments.  Each size runs once untimed, then ``reps`` timed single calls (median); the per-rank times are averaged over the ranks
+    with one more all-reduce, so the fit -- and every plan made from it -- is the same on every rank.  None when the
+    rows do not fit a line (e.g. a noisy CPU run); the caller keeps the link model then."""
+    import time
+
+    import torch
+
+    if world <= 1:
+        return None
+    cuda = getattr(device, "type", str(device)) == "cuda"
+    if sizes is None:
+        sizes = [1 * MB, 4 * MB, 16 * MB, 64 * MB] if cuda else [256 * 1024, 1 * MB, 4 * MB]
+    buf = torch.zeros(max(sizes) // 4, dtype=torch.float32, device=device)
+    times = []
+    for nbytes in sizes:
+        view = buf[: nbytes // 4]
+        comm.all_reduce(view, op="sum")  # warm: algorithm / channel set-up for this size
+        if cuda:
+            torch.cuda.synchronize(device)
+        samples = []
+        for _ in range(reps):  # the median of single calls: robust to a descheduled rank on a busy host
+            t0 = time.perf_counter()
+            comm.all_reduce(view, op="sum")
+            if cuda:
+                torch.cuda.synchronize(device)
+            samples.append(time.perf_counter() - t0)
+        times.append(sorted(samples)[len(samples) // 2])
+    t = torch.tensor(times, dtype=torch.float64 if not cuda else torch.float32, device=device)
+    comm.all_reduce(t, op="sum")
+    if cuda:
+        torch.cuda.synchronize(device)
+    mean = [float(v) / world for v in t.cpu().tolist()]
+    rows = [{"bytes": b, "algbw_GBps": b / max(tt, 1e-9) / 1e9} for b, tt in zip(sizes, mean)]
+    try:
+        fit = fit_table(rows, world)
+    except ValueError:  # noise swamped the size dependence: once more with 4x larger messages
+        if retry:
+            return calibrate(comm, world, device, [4 * b for b in sizes], reps, retry=False)
+        return None
+    fit.measured = True
+    return fit
+
+
 def plan(grad_bytes: float, world: int, target: float = 0.9, min_buckets: int = 4, min_mb: float = 4.0,
          model=None) -> Dict:
     """Bucket size (bytes) for ``grad_bytes`` of gradients all-reduced over ``world`` ranks, with the numbers that
@@ -120,7 +172,8 @@ def plan(grad_bytes: float, world: int, target: float = 0.9, min_buckets: int = 
         table = os.environ.get("PLX_COMM_TABLE", "")
         if table and os.path.exists(table) and world > 1:
             model = load_table(table, world)
-    source = "table" if isinstance(model, FittedModel) else "link-model"
+    source = ("measured" if getattr(model, "measured", False) else "table") if isinstance(model, FittedModel) \
+        else "link-model"
     m = model or LinkModel()
     if world <= 1:
         b = max(min_mb * MB, grad_bytes / max(1, min_buckets))

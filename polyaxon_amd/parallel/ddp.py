@@ -177,7 +177,14 @@ class FlatDDP:
             from polyaxon_amd.parallel.comm_plan import plan as _plan
 
             elem = 2 if flat.lp_grads is not None else 4  # bytes per gradient element on the wire (bf16 / fp32)
-            self.plan = _plan(flat.numel * elem, self.world)
+            model = None
+            if (self.world > 1 and self._comm is not None and not os.environ.get("PLX_COMM_TABLE")
+                    and os.environ.get("PLX_COMM_CALIBRATE", "1") != "0"):
+                # the node's own link, timed on this trial's communicator (same fit on every rank)
+                from polyaxon_amd.parallel.comm_plan import calibrate
+
+                model = calibrate(self._comm, self.world, flat.device)
+            self.plan = _plan(flat.numel * elem, self.world, model=model)
             bucket_elems = max(1, self.plan["bucket_bytes"] // elem)
         else:
             bucket_elems = max(1, int(float(bucket_mb) * 2 ** 20 / 4))

@@ -149,3 +149,32 @@ def test_group_collectives_use_the_groups_own_rank0():
         assert r["src"] == 1 and r["bcast"] == [1.0] * 3, r
         assert r["avg"] == [1.5] * 4 and r["gather"] == [1.0, 1.0, 2.0, 2.0], r
     assert all(r["live"] == 0 for r in res)
+
+
+def _calib_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    from polyaxon_amd.models.transformer import Transformer, tiny_llama
+    from polyaxon_amd.ops.flat import FlatParams
+    from polyaxon_amd.parallel.ddp import FlatDDP, init_from_env
+
+    torch.set_num_threads(2)
+    init_from_env("gloo")
+    flat = FlatParams(Transformer(tiny_llama()), "cpu", channels_last=False)
+    ddp = FlatDDP(flat, bucket_mb="auto")
+    q.put({"rank": rank, "plan": ddp.plan, "buckets": ddp.buckets})
+    ddp.remove_hooks()
+    ddp.close()
+    dist.destroy_process_group()
+
+
+def test_auto_buckets_are_planned_from_a_measured_link_and_agree_across_ranks():
+    """bucket_mb="auto" at world > 1 times all-reduces on the trial's communicator (comm_plan.calibrate) and plans
+    with that fit; the times are averaged over the ranks first, so every rank cuts the same buckets."""
+    res = _run(_calib_worker, 2)
+    a, b = res[0], res[1]
+    assert a["plan"]["source"] == "measured", a["plan"]
+    assert a["plan"] == b["plan"] and a["buckets"] == b["buckets"]
+    assert a["plan"]["busbw_GBps"] > 0 and a["plan"]["bucket_bytes"] >= 4 * 2 ** 20

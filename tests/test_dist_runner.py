@@ -34,8 +34,11 @@ def test_dp2_lm_trainer_through_polyflow(tmp_path):
         assert "loss" in last and "tokens_per_s" in last
         logs = flow.logs("experiment", r["id"])
         assert '"world": 2' in logs  # rank 0 reports the DP world it trained in
-        # gradient buckets planned for 2 ranks over xGMI (parallel/comm_plan.py; the trainer's --bucket_mb auto)
-        assert '"bucket_plan": {"bucket_bytes"' in logs and '"world": 2, "source": "link-model"' in logs
+        # gradient buckets planned for 2 ranks from all-reduces timed on the trial's communicator at start-up
+        # (parallel/comm_plan.py calibrate; the trainer's --bucket_mb auto), or the xGMI link model when the timings
+        # of a loaded CPU host do not fit a line
+        assert '"bucket_plan": {"bucket_bytes"' in logs
+        assert '"world": 2, "source": "measured"' in logs or '"world": 2, "source": "link-model"' in logs
         steps = [m["step"] for m in flow.store.get_metrics(r["id"])]
         assert 6 in steps
     finally:
