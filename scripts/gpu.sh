@@ -8,7 +8,10 @@
 #   final                    the driver's round-end tiers on the in-tree .so files: pytest -m gpu, smoke(), bench.py
 #   bench                    one bench.py run (BENCH_ARGS, default --steps 3 --warmup 1)
 #   ab                       bench.py once per variant of AB_LIST (';'-separated env assignments, "" = defaults, in
-#                            the order given: list A;B;A;B to interleave), one JSON line each in $TAG.jsonl
+#                            the order given: list A;B;A;B to interleave), one JSON line each in $TAG.jsonl; CMD
+#                            replaces "bench.py $BENCH_ARGS" (any python argv printing a JSON line last, e.g.
+#                            CMD="-m polyaxon_amd.trainers lm --model gpt2_125m"), and a variant may append arguments
+#                            after a '|' ("PLX_X=1|--zero1")
 #   ablib                    the same, swapping two builds of one library in place: LIB=plx_bn expects
 #                            polyaxon_amd/_native/lib<LIB>_{new,old}.so, runs TESTS with "new", then new/old x ROUNDS
 #   prof                     rocprofv3 kernel trace of bench.py (BENCH_ARGS), summarised on the box: steady-state
@@ -35,7 +38,8 @@ bench_line() {  # JSON line of a bench.py output file, with the variant label
   python3 - "$1" "$2" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-keep = ("value", "ms_per_step", "train_images_per_s", "tokens_per_s", "best_loss", "control_device_footprint")
+keep = ("value", "ms_per_step", "train_images_per_s", "tokens_per_s", "best_loss", "control_device_footprint", "zero1",
+        "world1_collectives", "bucket_launches", "buckets")
 print(json.dumps({"variant": sys.argv[1], **{k: d[k] for k in keep if k in d}}))
 PY
 }
@@ -66,9 +70,9 @@ bench)
 ab)
   variants; : > $O.jsonl; i=0
   for v in "${V[@]}"; do
-    i=$((i + 1))
-    env $v timeout -k 10 ${LIMIT:-600} python -u bench.py ${BENCH_ARGS:---steps 3 --warmup 1} > ${O}_$i.json \
-      2> ${O}_$i.err || fail "variant '$v'" $? ${O}_$i.err
+    i=$((i + 1)); e=${v%%|*}; extra=""; [ "$e" != "$v" ] && extra=${v#*|}
+    env $e timeout -k 10 ${LIMIT:-600} python -u ${CMD:-bench.py ${BENCH_ARGS:---steps 3 --warmup 1}} $extra \
+      > ${O}_$i.json 2> ${O}_$i.err || fail "variant '$v'" $? ${O}_$i.err
     bench_line "$v" ${O}_$i.json >> $O.jsonl
     tail -1 $O.jsonl
   done ;;
