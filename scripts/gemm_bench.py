@@ -77,10 +77,16 @@ def main() -> None:
                     a_, b_, c_ = nxt()
                     return f(a_, b_, c_)
                 return run
+            # the kernel itself (gemm.gemm), not gemm.forward / dgrad / wgrad: those dispatch through ``auto``, which
+            # sends the shapes outside ops/gemm.py's table to hipBLASLt (round 4's per-shape numbers for the forward
+            # and most data gradients were hipBLASLt against itself)
             cases = [
-                ("fwd", T, fout, fin, op(lambda x, w, dy: gemm.forward(x, w)), op(lambda x, w, dy: x @ w.t())),
-                ("dgrad", T, fin, fout, op(lambda x, w, dy: gemm.dgrad(dy, w)), op(lambda x, w, dy: dy @ w)),
-                ("wgrad", fout, fin, T, op(lambda x, w, dy: gemm.wgrad(dy, x)), op(lambda x, w, dy: dy.t() @ x)),
+                ("fwd", T, fout, fin, op(lambda x, w, dy: gemm.gemm(x, w, T, fout, fin, True, True)),
+                 op(lambda x, w, dy: x @ w.t())),
+                ("dgrad", T, fin, fout, op(lambda x, w, dy: gemm.gemm(dy, w, T, fin, fout, True, False)),
+                 op(lambda x, w, dy: dy @ w)),
+                ("wgrad", fout, fin, T, op(lambda x, w, dy: gemm.gemm(dy, x, fout, fin, T, False, False)),
+                 op(lambda x, w, dy: dy.t() @ x)),
             ]
             for pas, M, N, K, nat, ref in cases:
                 b = ref()
