@@ -1394,11 +1394,22 @@ inline int tn2_ring_kb(const V2Cfg& c) {
 // 224 / 256 at or below v1; A/B knob plx_set_tn2_bpc)
 int g_tn2_bpc = 0;
 
-inline TnPlan tn2_plan(int M, int N1, int N2, int num_cus, const V2Cfg& c) {
+// the stem's weight gradient (CONV 2), which runs alone on the main stream at the very end of the backward: 0 v1
+// (gemm_tn_kernel, 4 blocks per CU), 1 v2 planned for 2 blocks on every CU, 2 v2 with the side stream's block target
+// (A/B knob plx_set_tn2_stem)
+int g_tn2_stem = 0;
+constexpr int kStemV2Bpc = 2;
+
+// full_bpc > 0: plan for that many blocks on EVERY CU (the stem's weight gradient, alone on the GPU at the end of the
+// backward), whatever the block target
+inline TnPlan tn2_plan(int M, int N1, int N2, int num_cus, const V2Cfg& c, int full_bpc = 0) {
     const int bn1 = 64 * c.na, bn2 = 64 * c.nb;
     const int ntiles = (N1 / bn1) * (N2 / bn2);
     const int ncu = num_cus > 0 ? num_cus : 256;
-    const int cus = g_tn2_bpc > 2 ? g_tn2_bpc : g_tn2_bpc > 0 ? ncu * g_tn2_bpc : (ncu * 3) / 4;
+    const int cus = full_bpc > 0     ? ncu * full_bpc
+                    : g_tn2_bpc > 2  ? g_tn2_bpc
+                    : g_tn2_bpc > 0  ? ncu * g_tn2_bpc
+                                     : (ncu * 3) / 4;
     const int step = 32 * c.ks;                       // rows per iteration
     const long plane = (long)N1 * N2;
     const double flops = 2.0 * M * plane;
@@ -1564,6 +1575,8 @@ int plx_tn_plan_slices(int M, int N1, int N2, int num_cus, int v2) {
     return v2 ? tn2_plan(M, N1, N2, num_cus, v2_cfg(N1, N2)).slices : tn_plan(M, N1, N2, num_cus).slices;
 }
 
+void plx_set_tn2_stem(int mode) { g_tn2_stem = mode < 0 ? 0 : (mode > 2 ? 2 : mode); }
+
 void plx_set_tn2_slab_bw(int gb_per_s) { if (gb_per_s > 0) g_tn2_slab_bw = gb_per_s * 1e9; }
 void plx_set_tn2_bpc(int bpc) { g_tn2_bpc = bpc < 0 ? 0 : (bpc > 4096 ? 4096 : bpc); }
 
@@ -1609,9 +1622,11 @@ namespace {
 template <int CONV>
 int run_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int N2, int lda, int ldb, int ldc,
            const void* zero, int num_cus, int accumulate, hipStream_t s, ConvGeom geo, int bpc = 0) {
-    const bool v2 = g_tn_v2 == 1 || (g_tn_v2 == 2 && CONV != 0);  // 2: v2 for the gathered (KxK / strided) ones
+    // 2: v2 for the gathered (KxK / strided) ones; the stem (CONV 2) by its own knob g_tn2_stem
+    const bool v2 = CONV == 2 ? g_tn2_stem > 0 : (g_tn_v2 == 1 || (g_tn_v2 == 2 && CONV != 0));
     const V2Cfg cfg = v2_cfg(N1, N2);
-    const TnPlan plan = v2 ? tn2_plan(M, N1, N2, num_cus, cfg) : tn_plan(M, N1, N2, num_cus, bpc);
+    const TnPlan plan = v2 ? tn2_plan(M, N1, N2, num_cus, cfg, CONV == 2 && g_tn2_stem == 1 ? kStemV2Bpc : 0)
+                           : tn_plan(M, N1, N2, num_cus, bpc);
     int rc;
     if (v2)
         rc = dispatch_tn2<CONV>(cfg, A, B, ws, M, N1, N2, lda, ldb, plan, s, geo);
@@ -1947,8 +1962,10 @@ constexpr int kStemWgradBpc = 4;  // blocks per CU for the stem's weight gradien
 static long stem_slabs(int M, int num_cus) {
     const TnPlan p = tn_plan(M, 64, 256, num_cus, kStemWgradBpc);
     const TnPlan q = tn2_plan(M, 64, 256, num_cus, v2_cfg(64, 256));
+    const TnPlan r = tn2_plan(M, 64, 256, num_cus, v2_cfg(64, 256), kStemV2Bpc);
     const long a = p.slices + (p.groups > 1 ? p.groups : 0), b = q.slices + (q.groups > 1 ? q.groups : 0);
-    return a > b ? a : b;
+    const long c = r.slices + (r.groups > 1 ? r.groups : 0);
+    return a > b ? (a > c ? a : c) : (b > c ? b : c);
 }
 
 // floats of workspace plx_stem_conv_wgrad needs: the slab reduction's (as plx_gemm_tn_workspace) + dW packed [64][256]

@@ -51,7 +51,8 @@ variants() {  # AB_LIST split on ';' into the array V
 
 case $MODE in
 tests)
-  timeout -k 10 ${LIMIT:-1000} python -u -m pytest ${@:-tests -m gpu} -x -q --timeout 120 --timeout-method thread \
+  if [ $# -gt 0 ]; then args=("$@"); else args=(tests -m gpu); fi
+  timeout -k 10 ${LIMIT:-1000} python -u -m pytest "${args[@]}" -x -q --timeout 120 --timeout-method thread \
     > $O.log 2>&1 || fail pytest $? $O.log
   tail -2 $O.log ;;
 final)

@@ -573,7 +573,8 @@ def test_conv_tap_order(cuda, shape, cout, stride):
 def test_wgrad_kernels_every_class(cuda, variant):
     """Both weight-gradient kernels (plx_set_tn_v2: v1 gemm_tn_kernel; v2 wgrad_kernel with a 64 or 128 KB LDS ring)
     on every ResNet-50 wgrad class against fp32 F.conv2d weight gradients: dense 1x1 (ragged pixel counts), 3x3
-    stride 1 and 2 (the row gather, taps at the image border), 1x1 stride 2 (downsample), and the 7x7 stem."""
+    stride 1 and 2 (the row gather, taps at the image border), 1x1 stride 2 (downsample), and the 7x7 stem (its own
+    knob plx_set_tn2_stem: v1, v2 on every CU, v2 with the side-stream block target)."""
     from polyaxon_amd.ops import _native
     from polyaxon_amd.ops.conv import ConvKxK
     from polyaxon_amd.ops.conv1x1 import Conv1x1
@@ -585,6 +586,7 @@ def test_wgrad_kernels_every_class(cuda, variant):
              ("stem", (2, 3, 64, 48), 64, 2)]
     lib = _native.lib("plx_conv")
     lib.plx_set_tn_v2(*variant)
+    lib.plx_set_tn2_stem({(0, -1): 0, (1, 64): 1, (1, 128): 2}[variant])  # the stem's own kernel choice, all three
     try:
         for kind, shape, cout, stride in cases:
             torch.manual_seed(5)
@@ -610,3 +612,4 @@ def test_wgrad_kernels_every_class(cuda, variant):
     finally:
         v2, _, kb = os.environ.get("PLX_TN_V2", "1,64").partition(",")
         lib.plx_set_tn_v2(int(v2), int(kb) if kb else 64)
+        lib.plx_set_tn2_stem(int(os.environ.get("PLX_TN2_STEM", "0")))
