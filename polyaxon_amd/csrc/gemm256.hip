@@ -171,6 +171,74 @@ __device__ __forceinline__ float gelu_tanh(float h) {
 
 __device__ __forceinline__ float bf16_round(float f) { return (float)(__bf16)f; }
 
+// Epilogue store layout.  An MFMA tile's lane holds 4 consecutive columns of one row, so storing tiles one by one
+// writes 8 bytes per lane and 32 contiguous bytes per row: the memory side then sees 32-byte partial-line writes
+// (PMC on the GPT-2 head forward: 1.85x hipBLASLt's TCC_EA0_WRREQ for the same output; profiles/r5_lm_gemm.md).
+// pair_permute regroups two column-adjacent tiles a (columns 0-15) and b (16-31) with two cross-lane swaps per
+// register (gfx950 v_permlane32_swap / v_permlane16_swap, VALU, no LDS): afterwards lane quarter q = lane >> 4 holds
+// columns 8q..8q+3 in a and 8q+4..8q+7 in b, so each lane stores 16 contiguous bytes and a row gets 64.
+//   permlane32_swap(a, b): a's quarters 2, 3 <-> b's quarters 0, 1  ->  a = [a0 a1 b0 b1], b = [a2 a3 b2 b3]
+//   permlane16_swap(a, b): a's quarters 1, 3 <-> b's quarters 0, 2  ->  a = [a0 a2 b0 b2], b = [a1 a3 b1 b3]
+// (xk = quarter k of x: columns 4k..4k+3 of its tile), i.e. quarter q holds columns 8q..8q+7 of the 32.
+__device__ __forceinline__ void pair_permute(f32x4& a, f32x4& b) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a[j]), __float_as_uint(b[j]), false, false);
+    const auto t = __builtin_amdgcn_permlane16_swap(r[0], r[1], false, false);
+    a[j] = __uint_as_float(t[0]);
+    b[j] = __uint_as_float(t[1]);
+  }
+}
+
+// the bias of a lane's 8 columns n8..n8+7 (zeros without one), loaded once per column pair outside the row loop: in
+// the row loop the loads were re-issued for every row (no restrict on the bias / C pointers) and each waited on
+// its own round trip, +22 us on the GPT-2 QKV forward and +317 us on the head (r5_lm_gemm_epilogue_ab.jsonl)
+__device__ __forceinline__ void load_bias8(const Gemm256Args& p, int n8, f32x4& ba, f32x4& bb) {
+  if (p.bias != nullptr) {  // uniform branch; 32-byte aligned (bias 16-byte aligned, n8 % 8 == 0)
+    ba = *(const f32x4*)(p.bias + n8);
+    bb = *(const f32x4*)(p.bias + n8 + 4);
+  } else {
+    ba = f32x4{0.f, 0.f, 0.f, 0.f};
+    bb = ba;
+  }
+}
+
+// bf16 epilogue of one permuted tile pair at row m, columns n8..n8+7 (n8 % 8 == 0: 16-byte aligned stores);
+// ba / bb: load_bias8 of n8 (ignored when accumulating)
+template <bool ACC>
+__device__ __forceinline__ void store_pair(const Gemm256Args& p, f32x4 a, f32x4 b, int m, int n8, const f32x4& ba,
+                                           const f32x4& bb) {
+  __bf16* dst = (__bf16*)p.C + (size_t)m * p.ldc + n8;
+  if (ACC) {
+    const uint4 o = *(const uint4*)dst;
+    a[0] = p.alpha * a[0] + __uint_as_float(o.x << 16);
+    a[1] = p.alpha * a[1] + __uint_as_float(o.x & 0xffff0000u);
+    a[2] = p.alpha * a[2] + __uint_as_float(o.y << 16);
+    a[3] = p.alpha * a[3] + __uint_as_float(o.y & 0xffff0000u);
+    b[0] = p.alpha * b[0] + __uint_as_float(o.z << 16);
+    b[1] = p.alpha * b[1] + __uint_as_float(o.z & 0xffff0000u);
+    b[2] = p.alpha * b[2] + __uint_as_float(o.w << 16);
+    b[3] = p.alpha * b[3] + __uint_as_float(o.w & 0xffff0000u);
+  } else {
+    a = a * p.alpha + ba;
+    b = b * p.alpha + bb;
+  }
+  uint4 packed;
+  packed.x = pack_bf16x2(a[0], a[1]);
+  packed.y = pack_bf16x2(a[2], a[3]);
+  packed.z = pack_bf16x2(b[0], b[1]);
+  packed.w = pack_bf16x2(b[2], b[3]);
+  *(uint4*)dst = packed;
+  if (!ACC && p.C2 != nullptr) {  // uniform branch
+    uint4 g;
+    g.x = pack_bf16x2(gelu_tanh(bf16_round(a[0])), gelu_tanh(bf16_round(a[1])));
+    g.y = pack_bf16x2(gelu_tanh(bf16_round(a[2])), gelu_tanh(bf16_round(a[3])));
+    g.z = pack_bf16x2(gelu_tanh(bf16_round(b[0])), gelu_tanh(bf16_round(b[1])));
+    g.w = pack_bf16x2(gelu_tanh(bf16_round(b[2])), gelu_tanh(bf16_round(b[3])));
+    *(uint4*)((__bf16*)p.C2 + (size_t)m * p.ldc + n8) = g;
+  }
+}
+
 // ACC: C += alpha * AB (bf16 read-modify-write); SLAB: write fp32 partials (split K)
 template <bool AK, bool BKM, bool ACC, bool SLAB>
 __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
@@ -342,40 +410,29 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
 
   // epilogue: acc[nt][mt] is a 16 x 16 tile D[n][m]: m = lane & 15, n = 4 (lane >> 4) + j, j = 0..3
   const int fr = lane & 15, fq = lane >> 4;
+  if (SLAB) {
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt)
+    for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
-      const int m = m0 + wm * 128 + mt * 16 + fr;
-      const int n = n0 + wn * 64 + nt * 16 + 4 * fq;
-      f32x4 v = acc[nt][mt];
-      if (SLAB) {
-        float* dst = (float*)p.C + ((size_t)blockIdx.y * p.M + m) * p.N + n;
-        *(f32x4*)dst = v;
-      } else {
-        __bf16* dst = (__bf16*)p.C + (size_t)m * p.ldc + n;
-        if (ACC) {
-          const uint2 o = *(const uint2*)dst;
-          v[0] = p.alpha * v[0] + __uint_as_float(o.x << 16);
-          v[1] = p.alpha * v[1] + __uint_as_float(o.x & 0xffff0000u);
-          v[2] = p.alpha * v[2] + __uint_as_float(o.y << 16);
-          v[3] = p.alpha * v[3] + __uint_as_float(o.y & 0xffff0000u);
-        } else {
-          v *= p.alpha;
-          if (p.bias != nullptr) v += *(const f32x4*)(p.bias + n);  // uniform branch; 16-byte aligned (n % 4 == 0)
-        }
-        uint2 packed;
-        packed.x = pack_bf16x2(v[0], v[1]);
-        packed.y = pack_bf16x2(v[2], v[3]);
-        *(uint2*)dst = packed;
-        if (!ACC && p.C2 != nullptr) {  // uniform branch
-          uint2 g;
-          g.x = pack_bf16x2(gelu_tanh(bf16_round(v[0])), gelu_tanh(bf16_round(v[1])));
-          g.y = pack_bf16x2(gelu_tanh(bf16_round(v[2])), gelu_tanh(bf16_round(v[3])));
-          *(uint2*)((__bf16*)p.C2 + (size_t)m * p.ldc + n) = g;
-        }
+      for (int mt = 0; mt < 8; ++mt) {
+        const int m = m0 + wm * 128 + mt * 16 + fr;
+        const int n = n0 + wn * 64 + nt * 16 + 4 * fq;
+        *(f32x4*)((float*)p.C + ((size_t)blockIdx.y * p.M + m) * p.N + n) = acc[nt][mt];
+      }
+  } else {
+#pragma unroll
+    for (int np = 0; np < 2; ++np) {  // column-adjacent tile pairs (nt, nt + 1), 16-byte stores (pair_permute)
+      const int n8 = n0 + wn * 64 + np * 32 + 8 * fq;
+      f32x4 ba, bb;
+      load_bias8(p, n8, ba, bb);
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        f32x4 a = acc[2 * np][mt], b = acc[2 * np + 1][mt];
+        pair_permute(a, b);
+        store_pair<ACC>(p, a, b, m0 + wm * 128 + mt * 16 + fr, n8, ba, bb);
       }
     }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -543,39 +600,29 @@ __global__ void __launch_bounds__(NTH4, 1) gemm256w4_kernel(Gemm256Args p) {
   mfma_drain();
 
   const int fr = lane & 15, fq = lane >> 4;
+  if (SLAB) {
 #pragma unroll
-  for (int nt = 0; nt < 8; ++nt)
+    for (int nt = 0; nt < 8; ++nt)
 #pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
-      const int m = m0 + wm * 128 + (mt >> 2) * 64 + (mt & 3) * 16 + fr;
-      const int n = n0 + wn * 128 + (nt >> 2) * 64 + (nt & 3) * 16 + 4 * fq;
-      f32x4 v = acc[nt][mt];
-      if (SLAB) {
-        *(f32x4*)((float*)p.C + ((size_t)blockIdx.y * p.M + m) * p.N + n) = v;
-      } else {
-        __bf16* dst = (__bf16*)p.C + (size_t)m * p.ldc + n;
-        if (ACC) {
-          const uint2 o = *(const uint2*)dst;
-          v[0] = p.alpha * v[0] + __uint_as_float(o.x << 16);
-          v[1] = p.alpha * v[1] + __uint_as_float(o.x & 0xffff0000u);
-          v[2] = p.alpha * v[2] + __uint_as_float(o.y << 16);
-          v[3] = p.alpha * v[3] + __uint_as_float(o.y & 0xffff0000u);
-        } else {
-          v *= p.alpha;
-          if (p.bias != nullptr) v += *(const f32x4*)(p.bias + n);
-        }
-        uint2 packed;
-        packed.x = pack_bf16x2(v[0], v[1]);
-        packed.y = pack_bf16x2(v[2], v[3]);
-        *(uint2*)dst = packed;
-        if (!ACC && p.C2 != nullptr) {
-          uint2 gl;
-          gl.x = pack_bf16x2(gelu_tanh(bf16_round(v[0])), gelu_tanh(bf16_round(v[1])));
-          gl.y = pack_bf16x2(gelu_tanh(bf16_round(v[2])), gelu_tanh(bf16_round(v[3])));
-          *(uint2*)((__bf16*)p.C2 + (size_t)m * p.ldc + n) = gl;
-        }
+      for (int mt = 0; mt < 8; ++mt) {
+        const int m = m0 + wm * 128 + (mt >> 2) * 64 + (mt & 3) * 16 + fr;
+        const int n = n0 + wn * 128 + (nt >> 2) * 64 + (nt & 3) * 16 + 4 * fq;
+        *(f32x4*)((float*)p.C + ((size_t)blockIdx.y * p.M + m) * p.N + n) = acc[nt][mt];
+      }
+  } else {
+#pragma unroll
+    for (int np = 0; np < 4; ++np) {  // column-adjacent tile pairs (2 np, 2 np + 1): same 64-column half
+      const int n8 = n0 + wn * 128 + (np >> 1) * 64 + (np & 1) * 32 + 8 * fq;
+      f32x4 ba, bb;
+      load_bias8(p, n8, ba, bb);
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        f32x4 a = acc[2 * np][mt], b = acc[2 * np + 1][mt];
+        pair_permute(a, b);
+        store_pair<ACC>(p, a, b, m0 + wm * 128 + (mt >> 2) * 64 + (mt & 3) * 16 + fr, n8, ba, bb);
       }
     }
+  }
 }
 
 // C (bf16, ldc) = alpha * sum over splits of the fp32 slabs (+ C when accumulating); 8 elements per thread

@@ -57,6 +57,22 @@ SCHEDULE: Dict[Tuple[int, int, int, bool, bool], int] = {
 # A/B override of the schedule for every kernel call (scripts/gemm_bench.py --waves); 0 = the table
 FORCE_SCHEDULE = 0
 
+# schedule of a kernel call outside the table, by layout (PLX_LM_GEMM=1, split-K shapes): the 8-wave ping-pong kernel
+# for the forward (both operands K-major: 4.63 vs 4.91 ms per GPT-2 step, 42.3 vs 47.1 Llama), the 4-wave one for the
+# data and weight gradients (4.40 vs 5.09, 45.2 vs 51.5; profiles/r5_lm_gemm.md).  PLX_GEMM_WAVES overrides it.
+_LAYOUT_SCHEDULE = {_FWD: 8, _DGRAD: 5, _WGRAD: 5}
+
+
+def _schedule_of(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> int:
+    if FORCE_SCHEDULE:
+        return FORCE_SCHEDULE
+    v = SCHEDULE.get((M, N, K, bool(a_kmajor), bool(b_kmajor)))
+    if v:
+        return v
+    if os.environ.get("PLX_GEMM_WAVES"):
+        return 0  # the library's global knob
+    return _LAYOUT_SCHEDULE.get((bool(a_kmajor), bool(b_kmajor)), 0)
+
 
 def mode() -> str:
     m = os.environ.get("PLX_LM_GEMM", "auto")
@@ -166,7 +182,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: boo
     ws = _workspace(a.device, ns * M * N).data_ptr() if ns > 1 else None
     lda = K if a_kmajor else M
     ldb = K if b_kmajor else N
-    v = FORCE_SCHEDULE or max(0, SCHEDULE.get((M, N, K, bool(a_kmajor), bool(b_kmajor)), 0))
+    v = _schedule_of(M, N, K, a_kmajor, b_kmajor)
     rc = lib.plx_gemm256_exv(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, M, N, K, lda, ldb, out.stride(0),
                              int(a_kmajor), int(b_kmajor), float(alpha), int(accumulate),
                              bias.data_ptr() if bias is not None else None,
