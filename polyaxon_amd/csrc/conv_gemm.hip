@@ -1398,6 +1398,10 @@ int g_tn2_bpc = 0;
 // (gemm_tn_kernel, 4 blocks per CU), 1 v2 planned for 2 blocks on every CU, 2 v2 with the side stream's block target
 // (A/B knob plx_set_tn2_stem)
 int g_tn2_stem = 0;
+
+// v2 for the 6-wave configuration (N1 = 64, N2 a multiple of 192: the C = 64 3x3 weight gradients); A/B knob
+// plx_set_tn2_c64
+int g_tn2_c64 = 0;
 constexpr int kStemV2Bpc = 2;
 
 // full_bpc > 0: plan for that many blocks on EVERY CU (the stem's weight gradient, alone on the GPU at the end of the
@@ -1575,6 +1579,8 @@ int plx_tn_plan_slices(int M, int N1, int N2, int num_cus, int v2) {
     return v2 ? tn2_plan(M, N1, N2, num_cus, v2_cfg(N1, N2)).slices : tn_plan(M, N1, N2, num_cus).slices;
 }
 
+void plx_set_tn2_c64(int on) { g_tn2_c64 = on ? 1 : 0; }
+
 void plx_set_tn2_stem(int mode) { g_tn2_stem = mode < 0 ? 0 : (mode > 2 ? 2 : mode); }
 
 void plx_set_tn2_slab_bw(int gb_per_s) { if (gb_per_s > 0) g_tn2_slab_bw = gb_per_s * 1e9; }
@@ -1623,8 +1629,12 @@ template <int CONV>
 int run_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int N2, int lda, int ldb, int ldc,
            const void* zero, int num_cus, int accumulate, hipStream_t s, ConvGeom geo, int bpc = 0) {
     // 2: v2 for the gathered (KxK / strided) ones; the stem (CONV 2) by its own knob g_tn2_stem
-    const bool v2 = CONV == 2 ? g_tn2_stem > 0 : (g_tn_v2 == 1 || (g_tn_v2 == 2 && CONV != 0));
     const V2Cfg cfg = v2_cfg(N1, N2);
+    // the 6-wave configuration (the C = 64 3x3 layers: N2 = 9 x 64) is slower than v1 in isolation (144 vs 127 us)
+    // and held the side stream 1.5 ms/step in the step (3 calls at ~500 us); it stays on v1 unless g_tn2_c64
+    const bool six = cfg.na == 1 && cfg.nb == 3;
+    const bool v2 = CONV == 2 ? g_tn2_stem > 0
+                              : (g_tn_v2 == 1 || (g_tn_v2 == 2 && CONV != 0)) && (!six || g_tn2_c64);
     const TnPlan plan = v2 ? tn2_plan(M, N1, N2, num_cus, cfg, CONV == 2 && g_tn2_stem == 1 ? kStemV2Bpc : 0)
                            : tn_plan(M, N1, N2, num_cus, bpc);
     int rc;

@@ -186,6 +186,8 @@ def lib(name: str) -> ctypes.CDLL:
             handle.plx_set_tn_v2(int(v2), int(kb) if kb else -1)
         if name == "plx_conv" and os.environ.get("PLX_TN2_BPC"):  # A/B knob: v2 blocks per CU (plan)
             handle.plx_set_tn2_bpc(int(os.environ["PLX_TN2_BPC"]))
+        if name == "plx_conv" and os.environ.get("PLX_TN2_C64"):  # A/B knob: v2 for the C = 64 3x3 wgrads
+            handle.plx_set_tn2_c64(int(os.environ["PLX_TN2_C64"]))
         if name == "plx_conv" and os.environ.get("PLX_TN2_STEM"):  # A/B knob: the stem's weight-gradient kernel
             handle.plx_set_tn2_stem(int(os.environ["PLX_TN2_STEM"]))
         if name == "plx_conv" and os.environ.get("PLX_TN2_SLAB_BW"):  # A/B knob: slab GB/s the v2 plan prices
@@ -295,6 +297,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_set_tn2_bpc": [_I],
         "plx_set_tn2_slab_bw": [_I],
         "plx_set_tn2_stem": [_I],
+        "plx_set_tn2_c64": [_I],
         "plx_tn_plan_slices": [_I, _I, _I, _I, _I],
         "plx_set_nt_tall": [_I, _I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
@@ -383,7 +386,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_partial_colsum_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_v2": None, "plx_set_tn2_bpc": None, "plx_set_tn2_slab_bw": None, "plx_set_tn2_stem": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_set_tap_inner": None, "plx_set_stem_bwd_cap": None, "plx_set_bn_fin_threads": None, "plx_set_ln_wave": None, "plx_set_adamw_grid_cap": None, "plx_set_adamw_wide": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_partial_colsum_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_v2": None, "plx_set_tn2_bpc": None, "plx_set_tn2_slab_bw": None, "plx_set_tn2_stem": None, "plx_set_tn2_c64": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_set_tap_inner": None, "plx_set_stem_bwd_cap": None, "plx_set_bn_fin_threads": None, "plx_set_ln_wave": None, "plx_set_adamw_grid_cap": None, "plx_set_adamw_wide": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

@@ -587,6 +587,7 @@ def test_wgrad_kernels_every_class(cuda, variant):
     lib = _native.lib("plx_conv")
     lib.plx_set_tn_v2(*variant)
     lib.plx_set_tn2_stem({(0, -1): 0, (1, 64): 1, (1, 128): 2}[variant])  # the stem's own kernel choice, all three
+    lib.plx_set_tn2_c64(1 if variant[0] else 0)  # v2's 6-wave configuration (C = 64 3x3) too
     try:
         for kind, shape, cout, stride in cases:
             torch.manual_seed(5)
@@ -613,3 +614,4 @@ def test_wgrad_kernels_every_class(cuda, variant):
         v2, _, kb = os.environ.get("PLX_TN_V2", "1,64").partition(",")
         lib.plx_set_tn_v2(int(v2), int(kb) if kb else 64)
         lib.plx_set_tn2_stem(int(os.environ.get("PLX_TN2_STEM", "0")))
+        lib.plx_set_tn2_c64(int(os.environ.get("PLX_TN2_C64", "0")))
