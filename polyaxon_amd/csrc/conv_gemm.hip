@@ -1401,7 +1401,7 @@ int g_tn2_stem = 0;
 
 // v2 for the 6-wave configuration (N1 = 64, N2 a multiple of 192: the C = 64 3x3 weight gradients); A/B knob
 // plx_set_tn2_c64
-int g_tn2_c64 = 0;
+int g_tn2_c64 = 1;
 constexpr int kStemV2Bpc = 2;
 
 // full_bpc > 0: plan for that many blocks on EVERY CU (the stem's weight gradient, alone on the GPU at the end of the
@@ -1631,7 +1631,8 @@ int run_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int
     // 2: v2 for the gathered (KxK / strided) ones; the stem (CONV 2) by its own knob g_tn2_stem
     const V2Cfg cfg = v2_cfg(N1, N2);
     // the 6-wave configuration (the C = 64 3x3 layers: N2 = 9 x 64) is slower than v1 in isolation (144 vs 127 us)
-    // and held the side stream 1.5 ms/step in the step (3 calls at ~500 us); it stays on v1 unless g_tn2_c64
+    // and holds the side stream 1.5 ms/step in the step (3 calls at ~500 us), yet the step is faster with it
+    // (12.38-12.41k vs 12.35k trials/h, r5_wgrad_c64_ab.jsonl): g_tn2_c64 = 0 moves it back to v1 (A/B)
     const bool six = cfg.na == 1 && cfg.nb == 3;
     const bool v2 = CONV == 2 ? g_tn2_stem > 0
                               : (g_tn_v2 == 1 || (g_tn_v2 == 2 && CONV != 0)) && (!six || g_tn2_c64);

@@ -614,4 +614,4 @@ def test_wgrad_kernels_every_class(cuda, variant):
         v2, _, kb = os.environ.get("PLX_TN_V2", "1,64").partition(",")
         lib.plx_set_tn_v2(int(v2), int(kb) if kb else 64)
         lib.plx_set_tn2_stem(int(os.environ.get("PLX_TN2_STEM", "0")))
-        lib.plx_set_tn2_c64(int(os.environ.get("PLX_TN2_C64", "0")))
+        lib.plx_set_tn2_c64(int(os.environ.get("PLX_TN2_C64", "1")))
