@@ -323,6 +323,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_swiglu_bwd": [_P, _P, _P, _L, _I, _P],
         "plx_xent_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
         "plx_xent_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+        "plx_xent_cls_fwd": [_P, _P, _P, _P, _I, _I, _P],
+        "plx_xent_cls_bwd": [_P, _P, _P, _P, _P, _I, _I, _P],
         "plx_colsum_splits": [_L, _I],
         "plx_colsum": [_P, _L, _I, _P, _P, _P, _I, _P],
         "plx_gelu_bwd_colsum": [_P, _P, _P, _L, _I, _P, _P, _P, _I, _P],

@@ -166,6 +166,43 @@ def next_token_xent(logits: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
     return F.cross_entropy(logits[:, :-1].reshape(-1, logits.shape[-1]).float(), tokens[:, 1:].reshape(-1))
 
 
+class _ClassXent(torch.autograd.Function):
+    """mean over rows of lse(logits[r]) - logits[r, labels[r]] from bf16 logits [N][V] (csrc/lm_kernels.hip
+    plx_xent_cls_fwd / plx_xent_cls_bwd): replaces F.cross_entropy(logits.float(), labels)'s fp32 cast, log-softmax,
+    NLL and their three backward kernels with one kernel each way (the ResNet head, polyflow/executor.py)."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        lib = _native.lib("plx_lm")
+        N, V = logits.shape
+        lse = torch.empty(N, dtype=torch.float32, device=logits.device)
+        loss = torch.empty(N, dtype=torch.float32, device=logits.device)
+        _native.check(lib.plx_xent_cls_fwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), loss.data_ptr(), N, V,
+                                           _stream()), "plx_xent_cls_fwd")
+        ctx.save_for_backward(logits, labels, lse)
+        return loss.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _native.lib("plx_lm")
+        logits, labels, lse = ctx.saved_tensors
+        N, V = logits.shape
+        grad = torch.empty_like(logits)
+        g = g.detach().to(torch.float32).reshape(1).contiguous()
+        _native.check(lib.plx_xent_cls_bwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), g.data_ptr(),
+                                           grad.data_ptr(), N, V, _stream()), "plx_xent_cls_bwd")
+        return grad, None
+
+
+def class_xent(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """Classification cross entropy, mean over the N rows: the fused HIP pair on bf16 CUDA logits [N, V] (contiguous)
+    with int64 labels [N]; F.cross_entropy on fp32 logits otherwise."""
+    if (logits.is_cuda and logits.dtype == torch.bfloat16 and logits.dim() == 2 and logits.is_contiguous()
+            and labels.dtype == torch.int64 and labels.is_contiguous() and labels.shape == logits.shape[:1]):
+        return _ClassXent.apply(logits, labels)
+    return F.cross_entropy(logits.float(), labels)
+
+
 # ---------------------------------------------------------------------------------------------- bias gradient
 _COLSUM = os.environ.get("PLX_COLSUM", "1") != "0"  # A/B knob: 0 = torch's column reduction
 

@@ -72,6 +72,13 @@ class ResidentTrialExecutor:
             self.opt = FusedAdamW(self.flat, step_counter=self.step)
         else:
             raise ValueError(f"unknown optimizer {optimizer!r}")
+        # default: cross entropy of the fp32-cast logits; on the GPU in one fused HIP kernel each way (ops/lm.py
+        # class_xent: no fp32 logits copy, log-softmax or NLL kernels between the head GEMM and its backward, where the
+        # host launching them was the bottleneck of the forward -> backward hand-off).  PLX_CLASS_XENT=0: F.cross_entropy
+        if loss_fn is None and os.environ.get("PLX_CLASS_XENT", "1") != "0":
+            from polyaxon_amd.ops.lm import class_xent
+
+            loss_fn = class_xent
         self.loss_fn = loss_fn or (lambda out, y: F.cross_entropy(out.float(), y))
         # ``batch`` is either a fixed (x, y) pair or a data source with in-place ``next()`` (ops/synth.py) that the
         # step refills before every forward: a fresh device-generated batch per step, inside the captured graph

@@ -148,6 +148,26 @@ def test_next_token_xent_matches_fp32(cuda, B, S, V):
     torch.testing.assert_close(g, gr, rtol=1e-2, atol=1e-2 * float(gr.abs().max()))
 
 
+@pytest.mark.parametrize("N,V", [(256, 1000), (8, 10), (3, 1001), (1, 7), (64, 50257)])
+def test_class_xent_matches_fp32(cuda, N, V):
+    """The classification variant of the fused cross entropy (plx_xent_cls_fwd / _bwd: the ResNet head's loss in the
+    resident executor) against F.cross_entropy of the same logits in fp32: loss and logits gradient with a non-unit
+    incoming gradient, row lengths that are not a multiple of 8 bf16 (rows start mid-chunk)."""
+    from polyaxon_amd.ops.lm import class_xent
+
+    torch.manual_seed(1)
+    logits = (torch.randn(N, V, device=cuda) * 3).to(torch.bfloat16).requires_grad_()
+    labels = torch.randint(0, V, (N,), device=cuda)
+    loss = class_xent(logits, labels)
+    (loss * 1.7).backward()
+    ref_in = logits.detach().float().requires_grad_()
+    ref = F.cross_entropy(ref_in, labels)
+    (ref * 1.7).backward()
+    assert abs(float(loss) - float(ref)) < 1e-4 * max(1.0, abs(float(ref)))
+    g, gr = logits.grad.float(), ref_in.grad
+    torch.testing.assert_close(g, gr, rtol=1e-2, atol=1e-2 * float(gr.abs().max()))
+
+
 @pytest.mark.parametrize("T,N", [(16384, 768), (16384, 3072), (1000, 2304), (37, 264), (1, 8)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_bias_grad_colsum_matches_fp32(cuda, T, N, dtype):
