@@ -17,7 +17,7 @@ import torch.nn as nn
 from polyaxon_amd.ops.conv1x1 import Conv1x1, GradMailbox
 from polyaxon_amd.ops.conv import Conv3x3, ConvKxK
 from polyaxon_amd.ops.norm import BatchNormAct
-from polyaxon_amd.ops.pool import MaxPool3s2
+from polyaxon_amd.ops.pool import MaxPool3s2, global_avg_pool
 from polyaxon_amd.ops.stem import StemConv, stem_bn_relu_pool
 
 
@@ -136,7 +136,7 @@ class ResNet(nn.Module):
         # BN + ReLU + max-pool fused (ops/stem.py): the 112x112 BatchNorm output is never materialised
         x = stem_bn_relu_pool(x, self.stem_bn, self.pool) if _STEM_FUSED else self.pool(self.stem_bn(x))
         x = self.stages(x)
-        x = torch.flatten(x.mean((2, 3)), 1) if x.is_contiguous() else x.mean((2, 3))
+        x = torch.flatten(x.mean((2, 3)), 1) if x.is_contiguous() else global_avg_pool(x)
         return self.fc(x)
 
 

@@ -5,6 +5,8 @@ gather (each input pixel sums the dy of the <= 4 windows whose argmax it is), so
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -58,3 +60,31 @@ class MaxPool3s2(nn.MaxPool2d):
         if self.native and supported(x):
             return _MaxPool3s2.apply(x)
         return F.max_pool2d(x, 3, 2, 1)
+
+
+class _GlobalAvgPoolNHWC(torch.autograd.Function):
+    """Mean over H x W of a channels_last [N, C, H, W] tensor -> [N, C], with the backward written straight in the
+    input's NHWC layout.  Autograd's own x.mean((2, 3)) backward expanded the gradient into an NCHW-strided tensor,
+    which the BatchNorm backward then had to transpose into channels_last: a generic strided-copy kernel of ~80 us
+    plus the division pass, ~100 us per ResNet-50 step at the forward -> backward hand-off (scripts/trace_window.py)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        n, c, h, w = x.shape
+        ctx.shape = (n, c, h, w)
+        return x.permute(0, 2, 3, 1).reshape(n, h * w, c).mean(1)  # a contiguous NHWC view: column means
+
+    @staticmethod
+    def backward(ctx, g):
+        n, c, h, w = ctx.shape
+        dx = (g / (h * w)).unsqueeze(1).expand(n, h * w, c).contiguous()  # one broadcast write, NHWC
+        return dx.view(n, h, w, c).permute(0, 3, 1, 2)  # channels_last [N, C, H, W], no copy
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """x.mean((2, 3)) for a 4-D tensor; the NHWC-native autograd function when x is channels_last (and not NCHW
+    contiguous, i.e. C > 1 and H * W > 1)."""
+    if (x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)
+            and os.environ.get("PLX_NHWC_AVGPOOL", "1") != "0"):
+        return _GlobalAvgPoolNHWC.apply(x)
+    return x.mean((2, 3))
