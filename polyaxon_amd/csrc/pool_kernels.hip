@@ -144,7 +144,59 @@ inline dim3 grid_for(int row_elems, int rows) {
   return dim3((row_elems + 255) / 256, rows < 65535 ? rows : 65535);
 }
 
+// Global average pool over H x W of NHWC bf16 x [N][HW][C] (the ResNet head): one thread = 8 channels of one image,
+// fp32 sums over the HW pixels (each a coalesced 16-byte row read across the threads), the mean rounded to bf16.
+__global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16x8* __restrict__ x, bf16x8* __restrict__ y, int N, int HW,
+                                                      int G, float inv) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // (n, g)
+  if (i >= N * G) return;
+  const int n = i / G, g = i - n * G;
+  const bf16x8* p = x + (size_t)n * HW * G + g;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < HW; ++k) {
+    const bf16x8 v = p[(size_t)k * G];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += bf2f(v.v[j]);
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o.v[j] = f2bf(acc[j] * inv);
+  y[i] = o;
+}
+
+// its backward: dx[n][k][c] = dy[n][c] / HW for every pixel k, one 16-byte store per thread and pixel
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const bf16x8* __restrict__ dy, bf16x8* __restrict__ dx, int N, int HW,
+                                                      int G, float inv) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // (n, g)
+  if (i >= N * G) return;
+  const int n = i / G, g = i - n * G;
+  const bf16x8 v = dy[i];
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o.v[j] = f2bf(bf2f(v.v[j]) * inv);
+  bf16x8* q = dx + (size_t)n * HW * G + g;
+  for (int k = 0; k < HW; ++k) q[(size_t)k * G] = o;
+}
+
 }  // namespace
+
+// y[N][C] = mean over the HW pixels of x[N][HW][C] (NHWC bf16, C % 8 == 0, 16-byte aligned)
+PLX_API int plx_gap_forward(const void* x, void* y, int N, int HW, int C, hipStream_t s) {
+  if (N <= 0 || HW <= 0 || C <= 0 || C % 8) return 1;
+  const int G = C / 8;
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3((N * G + 255) / 256), dim3(256), 0, s, (const bf16x8*)x, (bf16x8*)y, N, HW, G,
+                     1.f / (float)HW);
+  return (int)hipGetLastError();
+}
+
+// dx[N][HW][C] = dy[N][C] / HW broadcast over the pixels (bf16)
+PLX_API int plx_gap_backward(const void* dy, void* dx, int N, int HW, int C, hipStream_t s) {
+  if (N <= 0 || HW <= 0 || C <= 0 || C % 8) return 1;
+  const int G = C / 8;
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3((N * G + 255) / 256), dim3(256), 0, s, (const bf16x8*)dy, (bf16x8*)dx, N, HW, G,
+                     1.f / (float)HW);
+  return (int)hipGetLastError();
+}
 
 PLX_API int plx_maxpool3s2_forward(const void* x, void* y, void* idx, int N, int H, int W, int C, hipStream_t s) {
   if (C % 8 || N <= 0 || H <= 0 || W <= 0) return 1;

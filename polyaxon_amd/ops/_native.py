@@ -351,6 +351,8 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
     },
     "plx_pool": {
         "plx_maxpool3s2_forward": [_P, _P, _P, _I, _I, _I, _I, _P],
+        "plx_gap_forward": [_P, _P, _I, _I, _I, _P],
+        "plx_gap_backward": [_P, _P, _I, _I, _I, _P],
         "plx_maxpool3s2_backward": [_P, _P, _P, _I, _I, _I, _I, _P],
     },
     "plx_rms": {

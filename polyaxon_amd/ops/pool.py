@@ -66,17 +66,30 @@ class _GlobalAvgPoolNHWC(torch.autograd.Function):
     """Mean over H x W of a channels_last [N, C, H, W] tensor -> [N, C], with the backward written straight in the
     input's NHWC layout.  Autograd's own x.mean((2, 3)) backward expanded the gradient into an NCHW-strided tensor,
     which the BatchNorm backward then had to transpose into channels_last: a generic strided-copy kernel of ~80 us
-    plus the division pass, ~100 us per ResNet-50 step at the forward -> backward hand-off (scripts/trace_window.py)."""
+    plus the division pass, ~100 us per ResNet-50 step at the forward -> backward hand-off (scripts/trace_window.py).
+    bf16 on the GPU: one HIP kernel each way (csrc/pool_kernels.hip plx_gap_forward / plx_gap_backward: 16-byte
+    rows, fp32 sums); otherwise torch ops on the NHWC view."""
 
     @staticmethod
     def forward(ctx, x):
         n, c, h, w = x.shape
         ctx.shape = (n, c, h, w)
+        if x.is_cuda and x.dtype == torch.bfloat16 and c % 8 == 0 and x.data_ptr() % 16 == 0:
+            y = torch.empty((n, c), dtype=x.dtype, device=x.device)
+            _native.check(_native.lib("plx_pool").plx_gap_forward(x.data_ptr(), y.data_ptr(), n, h * w, c, _stream()),
+                          "plx_gap_forward")
+            return y
         return x.permute(0, 2, 3, 1).reshape(n, h * w, c).mean(1)  # a contiguous NHWC view: column means
 
     @staticmethod
     def backward(ctx, g):
         n, c, h, w = ctx.shape
+        if g.is_cuda and g.dtype == torch.bfloat16 and c % 8 == 0:
+            g = g.contiguous()
+            dx = torch.empty((n, c, h, w), dtype=g.dtype, device=g.device, memory_format=torch.channels_last)
+            _native.check(_native.lib("plx_pool").plx_gap_backward(g.data_ptr(), dx.data_ptr(), n, h * w, c,
+                                                                   _stream()), "plx_gap_backward")
+            return dx
         dx = (g / (h * w)).unsqueeze(1).expand(n, h * w, c).contiguous()  # one broadcast write, NHWC
         return dx.view(n, h, w, c).permute(0, 3, 1, 2)  # channels_last [N, C, H, W], no copy
 

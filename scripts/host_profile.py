@@ -23,7 +23,7 @@ def main() -> None:
     ap.add_argument("--sort", default="tottime")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    prog = build_program("resnet", {"batch": 256}, dev)
+    prog = build_program("resnet50", {"batch": 256}, dev)
     prog.warm()
     ex = prog.executor
     ex.reset(seed=1)

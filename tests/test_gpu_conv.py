@@ -615,3 +615,23 @@ def test_wgrad_kernels_every_class(cuda, variant):
         lib.plx_set_tn_v2(int(v2), int(kb) if kb else 64)
         lib.plx_set_tn2_stem(int(os.environ.get("PLX_TN2_STEM", "0")))
         lib.plx_set_tn2_c64(int(os.environ.get("PLX_TN2_C64", "1")))
+
+
+@pytest.mark.parametrize("shape", [(256, 2048, 7, 7), (3, 64, 5, 9), (2, 8, 1, 1)])
+def test_global_avg_pool_kernels_match_fp32(cuda, shape):
+    """The ResNet head's NHWC global average pool on the GPU (csrc/pool_kernels.hip plx_gap_forward / _backward)
+    against an fp32 mean over H x W of the same bf16 input: values, gradient, channels_last gradient layout."""
+    from polyaxon_amd.ops.pool import _GlobalAvgPoolNHWC
+
+    torch.manual_seed(4)
+    x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xa = x.clone().requires_grad_()
+    y = _GlobalAvgPoolNHWC.apply(xa)
+    g = torch.randn(y.shape, device=cuda).to(torch.bfloat16)
+    y.backward(g)
+    xr = x.float().requires_grad_()
+    yr = xr.mean((2, 3))
+    yr.backward(g.float())
+    torch.testing.assert_close(y.float(), yr, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(xa.grad.float(), xr.grad, rtol=1e-2, atol=1e-3)
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last)
