@@ -131,13 +131,21 @@ class ResNet(nn.Module):
             if isinstance(mod, BatchNormAct):
                 mod.reset_running_stats()
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward_features(self, x: torch.Tensor) -> torch.Tensor:
+        """Everything before the classifier head: the last stage's [N, C, H, W] output (channels_last on the GPU)."""
         x = self.stem(x)
         # BN + ReLU + max-pool fused (ops/stem.py): the 112x112 BatchNorm output is never materialised
         x = stem_bn_relu_pool(x, self.stem_bn, self.pool) if _STEM_FUSED else self.pool(self.stem_bn(x))
-        x = self.stages(x)
+        return self.stages(x)
+
+    def forward_head(self, x: torch.Tensor) -> torch.Tensor:
+        """Global average pool + fc (the resident executor can instead run the head's forward AND backward in one
+        go, ops/head.py)."""
         x = torch.flatten(x.mean((2, 3)), 1) if x.is_contiguous() else global_avg_pool(x)
         return self.fc(x)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.forward_head(self.forward_features(x))
 
 
 def resnet50(num_classes: int = 1000, fused: bool = True, **kw) -> ResNet:

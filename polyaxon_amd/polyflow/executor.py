@@ -75,11 +75,21 @@ class ResidentTrialExecutor:
         # default: cross entropy of the fp32-cast logits; on the GPU in one fused HIP kernel each way (ops/lm.py
         # class_xent: no fp32 logits copy, log-softmax or NLL kernels between the head GEMM and its backward, where the
         # host launching them was the bottleneck of the forward -> backward hand-off).  PLX_CLASS_XENT=0: F.cross_entropy
+        default_loss = loss_fn is None
         if loss_fn is None and os.environ.get("PLX_CLASS_XENT", "1") != "0":
             from polyaxon_amd.ops.lm import class_xent
 
             loss_fn = class_xent
         self.loss_fn = loss_fn or (lambda out, y: F.cross_entropy(out.float(), y))
+        # Fused classifier head (ops/head.py): a model with forward_features / forward_head and an nn.Linear fc, the
+        # default cross entropy and bf16 autocast on the GPU run the head's forward and backward in the forward
+        # pass and start autograd at the features.  PLX_FUSED_HEAD=0: through autograd
+        self._fused_head = (default_loss and self.is_cuda and amp_dtype == torch.bfloat16
+                            and hasattr(model, "forward_features") and hasattr(model, "forward_head")
+                            and isinstance(getattr(model, "fc", None), nn.Linear)
+                            and os.environ.get("PLX_FUSED_HEAD", "1") != "0")
+        self._ones = torch.ones(1, dtype=torch.float32, device=self.device) if self._fused_head else None
+        self.fused_head_steps = 0
         # ``batch`` is either a fixed (x, y) pair or a data source with in-place ``next()`` (ops/synth.py) that the
         # step refills before every forward: a fresh device-generated batch per step, inside the captured graph
         self.data = batch if hasattr(batch, "next") else None
@@ -170,14 +180,28 @@ class ResidentTrialExecutor:
         if self.wcache is not None:
             self.wcache.activate()
         try:
-            if self.amp_dtype is not None:
+            if self._fused_head:
+                from polyaxon_amd.ops import head
+
+                with torch.autocast("cuda", dtype=self.amp_dtype):
+                    feats = self.model.forward_features(self.x)
+                if head.supported(feats, self.model.fc, self.y):
+                    loss, dfeat = head.classifier_head_step(feats.detach(), self.model.fc, self.y, self._ones)
+                    feats.backward(dfeat)
+                    self.fused_head_steps += 1
+                else:
+                    with torch.autocast("cuda", dtype=self.amp_dtype):
+                        loss = self.loss_fn(self.model.forward_head(feats), self.y)
+                    loss.backward()
+            elif self.amp_dtype is not None:
                 with torch.autocast("cuda", dtype=self.amp_dtype):
                     out = self.model(self.x)
                     loss = self.loss_fn(out, self.y)
+                loss.backward()
             else:
                 out = self.model(self.x)
                 loss = self.loss_fn(out, self.y)
-            loss.backward()
+                loss.backward()
         finally:
             if self.wcache is not None:
                 self.wcache.deactivate()

@@ -16,7 +16,8 @@
 #                            polyaxon_amd/_native/lib<LIB>_{new,old}.so, runs TESTS with "new", then new/old x ROUNDS
 #   prof                     rocprofv3 kernel trace of bench.py (BENCH_ARGS), summarised on the box: steady-state
 #                            kernel table (prof_summary.py) and step phases (step_phases.py); AB_LIST as for ab;
-#                            WINDOW=<kernel substring>: the launch sequence around it (trace_window.py)
+#                            WINDOW=<kernel substring>: the launch sequence around it (trace_window.py); the
+#                            all-stream idle intervals by neighbouring kernels (gap_report.py)
 #   pmc CMD...               PMC passes over CMD (each counter set its own KILL-limited run, COUNTER_SETS ';'-separated,
 #                            default: issue / LDS / MFMA / L2 sets), summarised by pmc_summary.py (MATCH = kernel filter)
 #   py SCRIPT [args]         a python script under a time limit (LIMIT seconds), stdout to $TAG.out
@@ -108,6 +109,7 @@ prof)
     [ -n "$stats" ] && cp "$stats" ${O}_${i}_kernel_stats.csv
     python3 scripts/prof_summary.py "$trace" --steps ${PROF_STEPS:-40} --top 40 --markdown > ${O}_${i}_steady_state.md
     python3 scripts/step_phases.py "$trace" --steps ${PROF_STEPS:-40} --markdown > ${O}_${i}_phases.md
+    python3 scripts/gap_report.py "$trace" > ${O}_${i}_gaps.jsonl
     if [ -n "${WINDOW:-}" ]; then  # kernel sequence around a kernel (scripts/trace_window.py --match $WINDOW)
       python3 scripts/trace_window.py "$trace" --match "$WINDOW" --before ${WBEFORE:-20} --after ${WAFTER:-30} \
         > ${O}_${i}_window.txt
