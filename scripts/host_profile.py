@@ -36,10 +36,13 @@ def main() -> None:
     t_host = time.perf_counter() - t0
     torch.cuda.synchronize()
     t_wall = time.perf_counter() - t0
+    # backward on this thread (not the autograd engine's device thread), so cProfile sees its Python too
+    torch.autograd.set_multithreading_enabled(False)
     pr = cProfile.Profile()
     pr.enable()
     ex.run(a.steps)
     pr.disable()
+    torch.autograd.set_multithreading_enabled(True)
     torch.cuda.synchronize()
     print(json.dumps({"steps": a.steps, "host_ms_per_step": round(t_host / a.steps * 1e3, 2),
                       "wall_ms_per_step": round(t_wall / a.steps * 1e3, 2)}), flush=True)
