@@ -136,6 +136,13 @@ def trial_env(*, base_env: Optional[Dict[str, str]] = None, experiment: Dict[str
         # the scheduler then sees the failure and tears down the surviving ranks.
         env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         env.setdefault("PLX_COLLECTIVE_TIMEOUT_S", "600")
+        # RCCL channel count of the DP ranks' communicators (several channels spread a ring
+        # collective over the node's 7 xGMI links per GPU).  PLX_RCCL_MIN_CHANNELS=n on the scheduler sets
+        # NCCL_MIN_NCHANNELS=n for every multi-rank trial unless its own environment already does; unset: RCCL's
+        # topology-based choice.  The bucket planner times the result at start-up (parallel/comm_plan.py calibrate).
+        ch = os.environ.get("PLX_RCCL_MIN_CHANNELS", "")
+        if ch.isdigit() and int(ch) > 0:
+            env.setdefault("NCCL_MIN_NCHANNELS", ch)
     if not devices:
         env["PLX_CPU_ONLY"] = "1"
     # HBM budget of the replica (client/budget.py enforces it in the trial process): the reserved GB, else the

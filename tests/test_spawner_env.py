@@ -123,6 +123,20 @@ def test_multi_rank_trials_get_the_rccl_watchdog():
     assert e["PLX_COLLECTIVE_TIMEOUT_S"] == "30"  # operator override wins
 
 
+def test_rccl_channel_count_is_opt_in_and_multi_rank_only(monkeypatch):
+    """PLX_RCCL_MIN_CHANNELS (operator side) becomes NCCL_MIN_NCHANNELS for multi-rank trials only; a value the
+    trial's own env already carries is kept."""
+    c = cluster_def("pytorch", {"master": 1, "worker": 1}, 6000)
+    assert "NCCL_MIN_NCHANNELS" not in _env(framework="pytorch", cluster=c)
+    monkeypatch.setenv("PLX_RCCL_MIN_CHANNELS", "32")
+    assert _env(framework="pytorch", cluster=c)["NCCL_MIN_NCHANNELS"] == "32"
+    assert "NCCL_MIN_NCHANNELS" not in _env()  # single rank: no collectives
+    e = _env(framework="pytorch", cluster=c, base_env={"NCCL_MIN_NCHANNELS": "8"})
+    assert e["NCCL_MIN_NCHANNELS"] == "8"
+    monkeypatch.setenv("PLX_RCCL_MIN_CHANNELS", "lots")
+    assert "NCCL_MIN_NCHANNELS" not in _env(framework="pytorch", cluster=c)
+
+
 def test_trial_env_carries_the_hbm_budget():
     """resources.hbm (GB) and fractional gpu shares reach the trial as PLX_HBM_GB / PLX_HBM_FRACTION, which
     client/budget.py turns into a caching-allocator cap (set_per_process_memory_fraction)."""
