@@ -1017,27 +1017,6 @@ PLX_API int plx_bn_backward_from_partials(const void* x, const uint8_t* mask, co
   return (int)hipGetLastError();
 }
 
-// The passes left once the producing GEMM finalized the BatchNorm inside its own launch (conv_gemm.hip bn_fin_tail):
-// the forward's apply from the scale | bias it wrote (+ the ReLU mask, + a deferred residual's res_sb), and the
-// backward's dx pass from the coefficients it wrote.
-PLX_API int plx_bn_apply_train(const void* x, const void* res, void* y, int64_t M, int C, const float* scale_bias,
-                               int relu, uint8_t* mask, const float* res_sb, hipStream_t stream) {
-  Plan p;
-  if (!plan_for(M, C, &p) || M < 1 || (relu && mask == nullptr)) return 1;
-  launch_apply(stream, M * p.G, p.G, x, res, y, scale_bias, scale_bias + C, relu, relu ? mask : nullptr, res_sb);
-  return (int)hipGetLastError();
-}
-
-PLX_API int plx_bn_dx(const void* x, const uint8_t* mask, const void* dy, void* dx, void* dres, int64_t M, int C,
-                      const float* coef, int relu, const ResBn* resbn, hipStream_t stream) {
-  Plan p;
-  if (!plan_for(M, C, &p) || M < 1 || (relu && mask == nullptr)) return 1;
-  if (resbn != nullptr && (dres == nullptr || resbn->part == nullptr)) return 1;
-  const ResBn rb = resbn != nullptr ? *resbn : ResBn{};
-  launch_dx(stream, M * p.G, p.G, x, mask, dy, dx, dres, coef, relu, rb);
-  return (int)hipGetLastError();
-}
-
 // ---- ResNet stem BatchNorm + ReLU + 3x3/s2/p1 max-pool (see stem_apply_pool_kernel)
 // Forward: statistics (workspace `partials`: plx_bn_workspace(N*H*W, C) floats) -> mean / invstd / scale|bias ->
 // y [N][OH][OW][C] bf16 and idx [N*OH*OW*C] window positions.

@@ -16,7 +16,6 @@
 // partial tiles and padding need no branches around the DMA; the TN GEMM reads a zero page instead.
 #include <hip/hip_runtime.h>
 
-#include "handoff.h"
 #include <stdint.h>
 
 namespace {
@@ -97,145 +96,14 @@ inline ConvGeom finish_geom(ConvGeom g) {
 // the epilogue adds per-block partials of  sum dz  and  sum dz * (x - mean) * invstd  (dz = dy * mask) to
 // part[blk_off + tm][n] and part[part_ld + blk_off + tm][n], so the BatchNorm backward skips its reduce pass
 // (one full read of dy) -- the same hand-off the forward does with its channel stats.
-//
-// l2 != nullptr: the BatchNorm's finalize runs inside this launch too (bn_fin_tail), on the partial rows of the
-// backward (part) or of the forward channel stats (the GEMM's `stats`): the launch then leaves the BatchNorm's
-// dx coefficients (backward) or its mean / invstd / scale / bias and running statistics (forward) and the
-// BatchNorm skips its own reduce + finalize launch.  Needs the launch to write every partial row of the
-// BatchNorm (one GEMM: blk_off == 0, part_ld == its row count).
 struct BnBwd {
     const __bf16* x;
     const uint8_t* mask;   // nullptr: no ReLU
-    const float* mean;     // backward: the forward's saved mean / invstd (also the finalize's)
+    const float* mean;
     const float* invstd;
     float* part;           // nullptr: disabled
     int part_ld, blk_off;
-    // ---- in-launch finalize (l2 == nullptr: off)
-    float* l2;             // fp32 [2][ceil(rows / 64)][N] level-2 rows
-    unsigned* cnt;         // >= (N / 64) * (ceil(rows / 64) + 1) zeroed tickets; the last arrivers re-zero them
-    long long count;       // elements per channel (the BatchNorm's M)
-    const float* gamma;
-    const float* beta;     // forward
-    float eps, momentum;   // forward
-    float* running_mean;   // forward, nullable
-    float* running_var;
-    float* out;            // forward: [4][N] mean | invstd | scale | bias; backward: coef [3][N] (A | B | D)
-    float* dgamma;         // backward
-    float* dbeta;
-    int accumulate;        // backward: dgamma / dbeta += (else =)
 };
-
-// The in-launch BatchNorm finalize, run by every workgroup after it published its partial rows (agent-scope atomic
-// stores, csrc/handoff.h's recipe): a ticket per (channel tile, group of 64 partial rows) elects the group's last
-// workgroup, which sums the group's rows for its BN channels into one level-2 row; a ticket per channel tile elects
-// the last of those, which sums the level-2 rows in fp64 and writes the finalize's outputs for its channels.  Sums
-// run in a fixed row order, so the result does not depend on which workgroup arrives last.  Replaces the separate
-// reduce + finalize launch (bn_kernels.hip reduce_l2_last) between this GEMM and the BatchNorm's own pass: 5-13 us
-// plus a launch boundary on the critical path, 53 times per direction in a ResNet-50 step.
-template <int BN, int SPB, bool BWD>
-__device__ __forceinline__ void bn_fin_tail(const BnBwd& f, const float* __restrict__ part, int nsr, int N, int tm,
-                                            int ntm, int tn, int ntn, char* smem) {
-    constexpr int NTH = 256, P = 2 * BN, R = NTH / P, TPG = 64 / SPB;
-    static_assert(NTH % P == 0 && 64 % SPB == 0, "tail layout");
-    const int tid = threadIdx.x;
-    const int ng = (nsr + 63) / 64, g = tm / TPG;
-    const int n0 = tn * BN;
-    int* flag = (int*)smem;
-    float* red = (float*)(smem + 256);
-    double* dred = (double*)(smem + 256 + NTH * 4);
-    auto ticket = [&](unsigned* c, int expect) -> bool {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's published rows retired
-        __syncthreads();
-        if (tid == 0) {
-            plx_handoff_release();
-            const unsigned old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int last = old == (unsigned)(expect - 1);
-            if (last) {
-                plx_handoff_acquire();
-                __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            flag[0] = last;
-        }
-        __syncthreads();
-        return flag[0] != 0;
-    };
-    if (!ticket(f.cnt + tn * ng + g, min(TPG, ntm - g * TPG))) return;
-    // level 1: thread (p, rl) sums rows rl, rl + R, ... of value p = (which sum, channel) of the group, 8 loads in flight
-    const int p = tid % P, rl = tid / P, which = p / BN, c = p % BN;
-    const int r0 = g * 64, r1 = min(r0 + 64, nsr);
-    // KU loads in flight per trip: each trip is one cross-XCD round trip on the launch's tail (8 per trip cost
-    // ~12 us per GEMM at 64 rows, profiles/r5_bn_fin_in_gemm.md)
-    constexpr int KU = 16;
-    const float* src = part + (size_t)which * nsr * N + n0 + c;
-    float a = 0.f;
-    for (int r = r0 + rl; r < r1; r += KU * R) {
-        float x[KU];
-#pragma unroll
-        for (int u = 0; u < KU; ++u) {
-            const int rr = r + u * R;
-            x[u] = rr < r1 ? __hip_atomic_load(src + (size_t)rr * N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < KU; ++u) a += x[u];
-    }
-    if constexpr (R > 1) {
-        red[tid] = a;
-        __syncthreads();
-    }
-    if (tid < P) {
-#pragma unroll
-        for (int j = 1; j < R; ++j) a += red[tid + j * P];
-        __hip_atomic_store(f.l2 + ((size_t)which * ng + g) * N + n0 + c, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (!ticket(f.cnt + ntn * ng + tn, ng)) return;
-    // level 2 (fp64): the ng rows of this channel tile
-    const float* src2 = f.l2 + (size_t)which * ng * N + n0 + c;
-    double d = 0.0;
-    for (int r = rl; r < ng; r += KU * R) {
-        float x[KU];
-#pragma unroll
-        for (int u = 0; u < KU; ++u) {
-            const int rr = r + u * R;
-            x[u] = rr < ng ? __hip_atomic_load(src2 + (size_t)rr * N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < KU; ++u) d += x[u];
-    }
-    dred[tid] = d;
-    __syncthreads();
-    if (tid >= BN) return;
-    double A = 0.0, B = 0.0;
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-        A += dred[tid + j * P];
-        B += dred[BN + tid + j * P];
-    }
-    const int ch = n0 + tid;
-    if constexpr (BWD) {  // bn_kernels.hip bwd_finalize: dx = A*dz + B*x + D
-        const float db = (float)A, dg = (float)B;
-        f.dbeta[ch] = f.accumulate ? f.dbeta[ch] + db : db;
-        f.dgamma[ch] = f.accumulate ? f.dgamma[ch] + dg : dg;
-        const float is = f.invstd[ch], k1 = f.gamma[ch] * is;
-        const float k2 = db / (float)f.count, k3 = dg / (float)f.count;
-        f.out[ch] = k1;
-        f.out[N + ch] = -k1 * k3 * is;
-        f.out[2 * N + ch] = -k1 * k2 + k1 * k3 * is * f.mean[ch];
-    } else {              // bn_kernels.hip fwd_finalize (unshifted producer sums)
-        const double m = A / (double)f.count;
-        double var = B / (double)f.count - m * m;
-        if (var < 0.0) var = 0.0;
-        const float mean = (float)m, invstd = rsqrtf((float)var + f.eps), gm = f.gamma[ch];
-        f.out[ch] = mean;
-        f.out[N + ch] = invstd;
-        f.out[2 * N + ch] = gm * invstd;
-        f.out[3 * N + ch] = f.beta[ch] - mean * gm * invstd;
-        if (f.running_mean != nullptr) {
-            const float unbiased = f.count > 1 ? (float)(var * (double)f.count / (double)(f.count - 1)) : (float)var;
-            f.running_mean[ch] = (1.f - f.momentum) * f.running_mean[ch] + f.momentum * mean;
-            f.running_var[ch] = (1.f - f.momentum) * f.running_var[ch] + f.momentum * unbiased;
-        }
-    }
-}
 
 __device__ __forceinline__ void row_coords(int m, int Hr, int Wr, int& n, int& r, int& c) {
     const int q = m / Wr;
@@ -720,12 +588,6 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     // (8 channels x 2 sums).  They go through LDS over the staged tile (rows of 17 floats: conflict-free both
     // ways) and every thread then sums ONE (chunk column, value) pair over the RSTEP rows -- 16 loads per thread
     // instead of 16 threads each walking 15 x 16 dependent loads while the rest of the block waits.
-    // fin_on: the rows are read back inside this launch (bn_fin_tail): published with agent-scope atomic stores
-    const bool fin_on = bnr.l2 != nullptr && (bnr_on || stats_on);
-    auto put = [&](float* p, float v) {
-        if (fin_on) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else *p = v;
-    };
     auto reduce_store = [&](const float* va, const float* vb, float* dst_a, float* dst_b) {
         float* red = (float*)smem;                          // [NTH][17], over the staged tile: its reads
         __syncthreads();                                    // (the store loop) must be done
@@ -740,8 +602,8 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
             float sum = 0.f;
 #pragma unroll 4
             for (int j = 0; j < RSTEP; ++j) sum += red[(j * CHUNKS + c) * 17 + v];
-            if (v < 8) put(dst_a + c * 8 + v, sum);
-            else put(dst_b + c * 8 + v - 8, sum);
+            if (v < 8) dst_a[c * 8 + v] = sum;
+            else dst_b[c * 8 + v - 8] = sum;
         }
         __syncthreads();                                    // red is reused by the next reduction
     };
@@ -756,8 +618,8 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
             for (int i = tid; i < (SPB - 1) * BN; i += NTH) {
                 const int r = srow + 1 + i / BN, c = i % BN;
                 if (r < nsr) {
-                    put(base_a + (size_t)(r - srow) * ld + c, 0.f);
-                    put(base_b + (size_t)(r - srow) * ld + c, 0.f);
+                    base_a[(size_t)(r - srow) * ld + c] = 0.f;
+                    base_b[(size_t)(r - srow) * ld + c] = 0.f;
                 }
             }
         }
@@ -767,7 +629,6 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         float* pb = bnr.part + (size_t)(bnr.part_ld + bnr.blk_off + srow) * ldc + n0;
         reduce_store(sa, sb, pa, pb);
         zero_rows(pa, pb, ldc);
-        if (fin_on) bn_fin_tail<BN, SPB, true>(bnr, bnr.part, nsr, N, tm, ntm, tn, ntn, smem);
     }
     // per-channel partial sum / sum of squares -> stats[0][srow][n], stats[1][srow][n] (the BatchNorm that consumes
     // this conv skips its stats pass)
@@ -776,7 +637,6 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         float* pb = stats + (size_t)(nsr + srow) * N + n0;
         reduce_store(s1, s2, pa, pb);
         zero_rows(pa, pb, N);
-        if (fin_on) bn_fin_tail<BN, SPB, false>(bnr, stats, nsr, N, tm, ntm, tn, ntn, smem);
     }
 }
 
@@ -1632,28 +1492,12 @@ int launch_tn(const void* A, const void* B, float* W, int M, int N1, int N2, int
     return launch_tn_st<BN1, BN2, WG1, WG2, CONV, 2>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo);
 }
 
-// an in-launch finalize request (BnBwd::l2) for an M x N GEMM: one launch writes all of the BatchNorm's partial rows
-inline bool fin_ok(const BnBwd& b, const float* stats, int M, int N) {
-    if (b.cnt == nullptr || b.count != M || b.gamma == nullptr || b.out == nullptr) return false;
-    if (b.part == nullptr)  // forward: the channel stats
-        return stats != nullptr && b.beta != nullptr;
-    const int rpb = N % 128 == 0 ? 128 : 256;
-    return stats == nullptr && b.blk_off == 0 && b.part_ld == (M + rpb - 1) / rpb && b.mean != nullptr &&
-           b.invstd != nullptr && b.dgamma != nullptr && b.dbeta != nullptr;
-}
-
 }  // namespace
 
 extern "C" {
 
 // tile selection: wide-N problems use 128x128, N == 64 uses 256x64 (pixels x channels)
 int plx_gemm_nt_rows_per_block(int N) { return N % 128 == 0 ? 128 : 256; }
-
-// zeroed tickets an in-launch finalize (BnBwd::cnt) needs for an M x N GEMM
-int plx_bn_fin_tickets(int M, int N) {
-    const int rpb = N % 128 == 0 ? 128 : 256, nsr = (M + rpb - 1) / rpb;
-    return (N / 64) * ((nsr + 63) / 64 + 1);
-}
 
 // stats (nullable): fp32 [2][ceil(M / rows_per_block)][N] per-block channel sums / sums of squares of C
 // D (nullable, bf16 [M][N], ldd): added to the product (C = A.B^T + D); not reflected in stats
@@ -1664,11 +1508,10 @@ int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int 
                 void* stream) {
     if (M <= 0 || N % 64 || K % BK || lda % 8 || ldb % 8 || ldc % 8 || (D != nullptr && ldd % 8)) return -1;
     if (dmask != nullptr && (D == nullptr || ldd != N)) return -1;
+    if (bnr != nullptr && (ldc != N || bnr->part == nullptr)) return -1;
     const BnBwd b = bnr != nullptr ? *bnr : BnBwd{};
-    if (b.part != nullptr && ldc != N) return -1;
-    if (b.l2 != nullptr && !fin_ok(b, stats, M, N)) return -1;
     hipStream_t s = (hipStream_t)stream;
-    const bool bwd = D != nullptr || b.part != nullptr;
+    const bool bwd = D != nullptr || bnr != nullptr;
     if (nt_tall(bwd, M, N, K))
         return launch_nt<256, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
     if (N % 128 == 0) {
@@ -1995,17 +1838,6 @@ int plx_conv_fwd(const void* x, const void* wf, void* y, int Nb, int H, int W, i
     return nt_conv_any(x, wf, y, Nb * g.Hr * g.Wr, Cout, g, K * K * Cin, Cout, zero, stats, (hipStream_t)stream);
 }
 
-// plx_conv_fwd whose launch also finalizes the following BatchNorm from its channel stats (fin: BnBwd with l2 set,
-// part == nullptr; see bn_fin_tail)
-int plx_conv_fwd_bn(const void* x, const void* wf, void* y, int Nb, int H, int W, int Cin, int Cout, int K, int S,
-                    const void* zero, float* stats, const BnBwd* fin, void* stream) {
-    if (Nb <= 0 || Cin % 64 || Cout % 64 || (K != 1 && K != 3) || (S != 1 && S != 2) || fin == nullptr) return -1;
-    const ConvGeom g = fwd_geom(H, W, Cin, K, S);
-    const int M = Nb * g.Hr * g.Wr;
-    if (fin->l2 == nullptr || fin->part != nullptr || !fin_ok(*fin, stats, M, Cout)) return -1;
-    return nt_conv_any(x, wf, y, M, Cout, g, K * K * Cin, Cout, zero, stats, (hipStream_t)stream, nullptr, *fin);
-}
-
 // dx[Nb*H*W][Cin] = conv^T(dy[Nb*Ho*Wo][Cout], Wd[Cin][K*K][Cout]) (+ D, bf16 [Nb*H*W][Cin], may alias dx).
 // For S == 2 and K == 1 only the even-even pixels are written: the caller passes a zeroed dx, or D == dx (the
 // other rows then keep D).  bnr (nullable): fused BatchNorm-backward partials of dx, one block row per GEMM
@@ -2016,8 +1848,6 @@ int plx_conv_dgrad(const void* dy, const void* wd, void* dx, int Nb, int H, int 
     if (bnr != nullptr && (S == 2 && K == 1)) return -1;
     hipStream_t st = (hipStream_t)stream;
     BnBwd b = bnr != nullptr ? *bnr : BnBwd{};
-    // in-launch finalize: one GEMM (stride 1) writing all the partial rows
-    if (b.l2 != nullptr && (S != 1 || !fin_ok(b, nullptr, Nb * H * W, Cin))) return -1;
     const int rpb = nt_rows_per_block(Cin);
     return for_each_dgrad_gemm(Nb, H, W, Cin, Cout, K, S, [&](const ConvGeom& g, int M) {
         const int rc = nt_conv_any(dy, wd, dx, M, Cin, g, K * K * Cout, Cin, zero, nullptr, st, D, b);

@@ -44,15 +44,15 @@ class Bottleneck(nn.Module):
         if self.downsample is None:
             # identity block: bn3's residual gradient is added inside conv1's dgrad GEMM (ops.conv1x1.GradMailbox),
             # so conv1's dgrad is x's whole gradient and serves the previous block's bn3 its backward partials
-            out = self.bn1(self.conv1(x, grad_box=box, bn_link=True, bn=self.bn1))
-            out = self.bn2(self.conv2(out, bn_link=True, bn=self.bn2))
-            return self.bn3(self.conv3(out, bn_link=True, bn=self.bn3), x, residual_grad_box=box)
+            out = self.bn1(self.conv1(x, grad_box=box, bn_link=True))
+            out = self.bn2(self.conv2(out, bn_link=True))
+            return self.bn3(self.conv3(out, bn_link=True), x, residual_grad_box=box)
         # downsampling block: conv1's data gradient is deferred into the downsample conv's dgrad epilogue, and the
         # downsample BatchNorm's output feeds only bn3, so bn3's dx pass reduces that BatchNorm's backward partials
         identity = self.downsample(x, grad_box=box)
-        out = self.bn1(self.conv1(x, grad_sink=box, bn=self.bn1))
-        out = self.bn2(self.conv2(out, bn_link=True, bn=self.bn2))
-        return self.bn3(self.conv3(out, bn_link=True, bn=self.bn3), identity, residual_link=True)
+        out = self.bn1(self.conv1(x, grad_sink=box))
+        out = self.bn2(self.conv2(out, bn_link=True))
+        return self.bn3(self.conv3(out, bn_link=True), identity, residual_link=True)
 
 
 _DEFER_DOWN_BN = os.environ.get("PLX_DEFER_DOWN_BN", "1") != "0"  # A/B knob (scripts/gpu.sh ab)
@@ -69,7 +69,7 @@ class Downsample(nn.Module):
 
     def forward(self, x: torch.Tensor, grad_box: Optional[GradMailbox] = None) -> torch.Tensor:
         # the output feeds only bn3's residual add, which applies this BatchNorm's scale/bias itself
-        return self.bn(self.conv(x, grad_box=grad_box, bn=self.bn), defer_apply=_DEFER_DOWN_BN)
+        return self.bn(self.conv(x, grad_box=grad_box), defer_apply=_DEFER_DOWN_BN)
 
 
 class ResNet(nn.Module):

@@ -244,8 +244,6 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_bn_workspace": [_L, _I],
         "plx_bn_forward": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P],
         "plx_bn_apply": [_P, _P, _P, _L, _I, _P, _I, _P],
-        "plx_bn_apply_train": [_P, _P, _P, _L, _I, _P, _I, _P, _P, _P],
-        "plx_bn_dx": [_P, _P, _P, _P, _P, _L, _I, _P, _I, _P, _P],
         "plx_bn_l2_workspace": [_I, _I],
         "plx_bn_forward_from_partials": [_P, _P, _P, _L, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I, _P, _P,
                                          _I, _P, _P, _P],
@@ -287,7 +285,6 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P],
         "plx_gemm_nt_prologue": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
         "plx_gemm_nt_rows_per_block": [_I],
-        "plx_bn_fin_tickets": [_I, _I],
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
         "plx_set_tn_plan": [_I, _I],
         "plx_set_tn_sizes": [_I, _I],
@@ -314,7 +311,6 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_stem_conv_wgrad_workspace": [_I, _I, _I, _I],
         "plx_stem_conv_wgrad": [_P, _P, _P, _L, _L, _L, _L, _P, _I, _I, _I, _P, _I, _I, _P],
         "plx_conv_fwd": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
-        "plx_conv_fwd_bn": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
         "plx_conv_dgrad": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P],
         "plx_conv_dgrad_blocks": [_I, _I, _I, _I, _I, _I, _I],
         "plx_conv_wgrad_workspace": [_I, _I, _I, _I, _I, _I, _I, _I],
@@ -412,13 +408,9 @@ class ResBnArgs(ctypes.Structure):
 
 
 class BnBwdArgs(ctypes.Structure):
-    """Host image of ``BnBwd`` (csrc/conv_gemm.hip): fused BatchNorm-backward partials in a dgrad GEMM epilogue,
-    and (``l2`` set) the BatchNorm's finalize inside the GEMM's launch, forward or backward (``bn_fin_tail``)."""
+    """Host image of ``BnBwd`` (csrc/conv_gemm.hip): fused BatchNorm-backward partials in a dgrad GEMM epilogue."""
     _fields_ = [("x", _P), ("mask", _P), ("mean", _P), ("invstd", _P), ("part", _P), ("part_ld", _I),
-                ("blk_off", _I),
-                ("l2", _P), ("cnt", _P), ("count", ctypes.c_longlong), ("gamma", _P), ("beta", _P),
-                ("eps", ctypes.c_float), ("momentum", ctypes.c_float), ("running_mean", _P), ("running_var", _P),
-                ("out", _P), ("dgamma", _P), ("dbeta", _P), ("accumulate", _I)]
+                ("blk_off", _I)]
 
 
 def check(rc: int, what: str) -> None:

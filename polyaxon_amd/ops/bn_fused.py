@@ -71,10 +71,7 @@ class _BNAct(torch.autograd.Function):
         defer = bool(defer) and not relu and residual is None and link is not None
         y = None if defer else torch.empty_like(x, memory_format=torch.channels_last)
         yp = y.data_ptr() if y is not None else None
-        # ext[2]: the producing GEMM's launch already finalized (ops.conv1x1.bn_fin_fwd): its mean | invstd | scale |
-        # bias, running statistics updated -- only the apply pass is left
-        fin = ext[2] if ext is not None and len(ext) > 2 else None
-        stats = fin if fin is not None else torch.empty(4 * c, **f32)  # mean | invstd | scale | bias
+        stats = torch.empty(4 * c, **f32)  # mean | invstd | scale | bias
         res_sb = None
         if residual is not None:
             rl = getattr(residual, "_plx_bn_link", None)
@@ -86,14 +83,9 @@ class _BNAct(torch.autograd.Function):
         rv = running_var.data_ptr() if running_var is not None else None
         mask = torch.empty(m * c // 8, dtype=torch.uint8, device=x.device) if relu else None
         mp = mask.data_ptr() if mask is not None else None
-        if fin is not None:
-            if yp is not None:
-                rc = lib.plx_bn_apply_train(x.data_ptr(), res.data_ptr() if res is not None else None, yp, m, c,
-                                            stats[2 * c:].data_ptr(), int(relu), mp, rsp, _stream())
-                _native.check(rc, "plx_bn_apply_train")
-        elif ext is not None:
+        if ext is not None:
             # channel sums came from the producing conv's GEMM epilogue: no stats pass over x
-            part, nblk = ext[0], ext[1]
+            part, nblk = ext
             l2 = torch.empty(_native.size("plx_bn", "plx_bn_l2_workspace", nblk, c), **f32)
             rc = lib.plx_bn_forward_from_partials(
                 x.data_ptr(), res.data_ptr() if res is not None else None, yp, m, c, weight.data_ptr(),
@@ -123,7 +115,6 @@ class _BNAct(torch.autograd.Function):
         ctx.link = link
         if link is not None:
             link.x, link.mask, link.mean, link.invstd = x, mask, stats[:c], stats[c:2 * c]
-            link.weight, link.direct = weight, ctx.direct
             if defer:
                 link.affine = stats[2 * c:]
         # rlink: the residual came from a fused BatchNorm whose output nothing else consumes (a downsampling branch):
@@ -150,14 +141,14 @@ class _BNAct(torch.autograd.Function):
         masked_box = _MASKED_RESGRAD and ctx.box is not None and ctx.relu and mask is not None
         dres = (torch.empty_like(x, memory_format=torch.channels_last)
                 if ctx.has_res and not masked_box else None)
-        part, nblk, fin = ctx.link.take() if ctx.link is not None else (None, 0, None)
         if ctx.direct is not None:
             dg_ptr, db_ptr, acc = ctx.direct[0].data_ptr(), ctx.direct[1].data_ptr(), 1
             dgb = None
         else:
-            dgb = fin[1] if fin is not None else torch.empty(2 * c, **f32)
+            dgb = torch.empty(2 * c, **f32)
             dg_ptr, db_ptr, acc = dgb.data_ptr(), dgb[c:].data_ptr(), 0
-        coef = fin[0] if fin is not None else torch.empty(3 * c, **f32)
+        coef = torch.empty(3 * c, **f32)
+        part, nblk = ctx.link.take() if ctx.link is not None else (None, 0)
         rb = None
         if ctx.rlink is not None and dres is not None:
             rl = ctx.rlink
@@ -167,12 +158,7 @@ class _BNAct(torch.autograd.Function):
             rb = _native.ResBnArgs(rl.x.data_ptr(), rl.mask.data_ptr() if rl.mask is not None else None,
                                    rl.mean.data_ptr(), rl.invstd.data_ptr(), rl.part.data_ptr())
         rbp = ctypes.addressof(rb) if rb is not None else None
-        if fin is not None:  # the consumer's dgrad launch also finalized: dgamma / dbeta and coef are written
-            rc = lib.plx_bn_dx(x.data_ptr(), mask.data_ptr() if mask is not None else None, dy.data_ptr(),
-                               dx.data_ptr(), dres.data_ptr() if dres is not None else None, m, c, coef.data_ptr(),
-                               int(ctx.relu), rbp, _stream())
-            _native.check(rc, "plx_bn_dx")
-        elif part is not None:  # the consumer's dgrad epilogue already reduced dz and dz*xhat per block
+        if part is not None:  # the consumer's dgrad epilogue already reduced dz and dz*xhat per block
             l2 = torch.empty(_native.size("plx_bn", "plx_bn_l2_workspace", nblk, c), **f32)
             rc = lib.plx_bn_backward_from_partials(
                 x.data_ptr(), mask.data_ptr() if mask is not None else None, dy.data_ptr(), dx.data_ptr(),

@@ -23,8 +23,8 @@ import torch.nn.functional as F
 import ctypes
 
 from polyaxon_amd.ops import _native, side_stream, wcache
-from polyaxon_amd.ops.conv1x1 import (GradMailbox, _bf16_context, _num_cus, _stream, _zero_page, bn_fin_fwd,
-                                      bn_link_of, nt_stats_rows, unpack_relu_mask)
+from polyaxon_amd.ops.conv1x1 import (GradMailbox, _bf16_context, _num_cus, _stream, _zero_page, bn_link_of, nt_stats_rows,
+                                      unpack_relu_mask)
 from polyaxon_amd.ops.flat import direct_grad
 
 
@@ -48,7 +48,7 @@ def weight_prep_k(w: torch.Tensor):
 
 class _ConvK(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stats, stride, box, link, fin=None):
+    def forward(ctx, x, weight, stats, stride, box, link):
         lib = _native.lib("plx_conv")
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         n, cin, h, w = x.shape
@@ -56,15 +56,10 @@ class _ConvK(torch.autograd.Function):
         ho, wo = _out(h, k, stride), _out(w, k, stride)
         wf, wd = wcache.lookup(weight) or weight_prep_k(weight)
         y = torch.empty((n, cout, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-        sp = stats.data_ptr() if stats is not None else None
-        if fin is not None:  # the launch also finalizes the consuming BatchNorm (ops.conv1x1.bn_fin_fwd)
-            rc = lib.plx_conv_fwd_bn(x.data_ptr(), wf.data_ptr(), y.data_ptr(), n, h, w, cin, cout, k, stride,
-                                     _zero_page(x.device).data_ptr(), sp, ctypes.addressof(fin), _stream())
-            _native.check(rc, "plx_conv_fwd_bn")
-        else:
-            rc = lib.plx_conv_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), n, h, w, cin, cout, k, stride,
-                                  _zero_page(x.device).data_ptr(), sp, _stream())
-            _native.check(rc, "plx_conv_fwd")
+        rc = lib.plx_conv_fwd(x.data_ptr(), wf.data_ptr(), y.data_ptr(), n, h, w, cin, cout, k, stride,
+                              _zero_page(x.device).data_ptr(), stats.data_ptr() if stats is not None else None,
+                              _stream())
+        _native.check(rc, "plx_conv_fwd")
         ctx.save_for_backward(x, wd)
         ctx.wshape = weight.shape
         ctx.stride = stride
@@ -101,7 +96,7 @@ class _ConvK(torch.autograd.Function):
             bnr = None
             if ctx.link is not None and (ctx.box is None or extra is not None):
                 nblk = _native.size("plx_conv", "plx_conv_dgrad_blocks", n, h, w, cin, cout, k, s)
-                bnr = ctx.link.request(nblk, fin=s == 1)  # stride 2: 4 launches, the BatchNorm finalizes
+                bnr = ctx.link.request(nblk)
             rc = lib.plx_conv_dgrad(dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), n, h, w, cin, cout, k, s, zero,
                                     add.data_ptr() if add is not None else None,
                                     ctypes.addressof(bnr) if bnr is not None else None, _stream())
@@ -123,7 +118,7 @@ class _ConvK(torch.autograd.Function):
                 wgrad()
             if not direct:
                 dw = g.permute(0, 3, 1, 2)  # [co][ci][kh][kw] view with channels_last strides
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -135,23 +130,21 @@ def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
 
 
 def conv_k(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, with_stats: bool = False,
-           grad_box: GradMailbox = None, bn_link: bool = False, bn=None) -> torch.Tensor:
+           grad_box: GradMailbox = None, bn_link: bool = False) -> torch.Tensor:
     """``grad_box``: add the box's deferred gradient into dx (see ops.conv1x1.GradMailbox); ``bn_link``: dx is the
-    complete gradient of ``x`` — serve the producing BatchNorm its backward partials (ops.conv1x1.BnLink);
-    ``bn``: the consuming BatchNorm module, finalized inside the launch (ops.conv1x1.conv1x1)."""
-    stats = fin = None
+    complete gradient of ``x`` — serve the producing BatchNorm its backward partials (ops.conv1x1.BnLink)."""
+    stats = None
     if with_stats:
         n, _, h, w = x.shape
         k = weight.shape[2]
         m, cout = n * _out(h, k, stride) * _out(w, k, stride), weight.shape[0]
         nblk = -(-m // nt_stats_rows(cout))
         stats = torch.empty(2 * nblk * cout, dtype=torch.float32, device=x.device)
-        fin = bn_fin_fwd(bn, m, cout, nblk, x.device)
     if grad_box is not None:
         grad_box.armed = True
-    y = _ConvK.apply(x, weight, stats, stride, grad_box, bn_link_of(x, bn_link), fin[0] if fin is not None else None)
+    y = _ConvK.apply(x, weight, stats, stride, grad_box, bn_link_of(x, bn_link))
     if stats is not None:
-        y._plx_channel_stats = (stats, nblk, fin[1] if fin is not None else None)
+        y._plx_channel_stats = (stats, nblk)
     return y
 
 
@@ -165,10 +158,10 @@ class ConvKxK(nn.Conv2d):
         self.native = native
         self.bn_stats = bn_stats
 
-    def forward(self, x: torch.Tensor, grad_box: GradMailbox = None, bn_link: bool = False, bn=None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, grad_box: GradMailbox = None, bn_link: bool = False) -> torch.Tensor:
         if self.native and supported(x, self):
             return conv_k(x, self.weight, self.stride[0], with_stats=self.bn_stats and self.training,
-                          grad_box=grad_box, bn_link=bn_link, bn=bn)
+                          grad_box=grad_box, bn_link=bn_link)
         return F.conv2d(x, self.weight, None, self.stride, self.padding)
 
 

@@ -15,7 +15,6 @@ gradient comes back in fp32, so autocast's bf16 weight copy and its backward cas
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Dict
 
 import torch
@@ -172,56 +171,15 @@ def unpack_relu_mask(g: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
     return (g * keep).contiguous(memory_format=torch.channels_last)
 
 
-# PLX_BN_FIN_GEMM=0: the BatchNorm keeps its own reduce + finalize launch after the GEMM that produced its partials
-# (A/B knob; default: the GEMM's launch finalizes, csrc/conv_gemm.hip bn_fin_tail)
-FIN_IN_GEMM = os.environ.get("PLX_BN_FIN_GEMM", "1") != "0"
-_TICKETS = {}
-
-
-def fin_tickets(dev: torch.device, m: int, n: int) -> int:
-    """Zeroed ticket words for an in-launch BatchNorm finalize of an m x n GEMM (bn_fin_tail), one array per
-    (device, stream): launches sharing it are stream-ordered and each leaves it zeroed again."""
-    need = (n // 64) * (-(-(-(-m // nt_stats_rows(n))) // 64) + 1)
-    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
-    t = _TICKETS.get(key)
-    if t is None or t.numel() < need:
-        t = _TICKETS[key] = torch.zeros(max(need, 8192), dtype=torch.int32, device=dev)
-    return t.data_ptr()
-
-
-def fin_l2(nblk: int, c: int, dev: torch.device) -> torch.Tensor:
-    """Level-2 rows of an in-launch finalize: fp32 [2][ceil(nblk / 64)][c]."""
-    return torch.empty(2 * (-(-nblk // 64)) * c, dtype=torch.float32, device=dev)
-
-
-def bn_fin_fwd(bn, m: int, cout: int, nblk: int, dev: torch.device):
-    """In-launch forward finalize for the BatchNorm module ``bn`` (ops.norm.BatchNormAct) that consumes an m x cout
-    convolution output with channel stats: (BnBwdArgs, fp32 [4][cout] mean | invstd | scale | bias, l2), or None
-    when ``bn`` is not a training fused BatchNorm.  The launch also updates ``bn``'s running statistics."""
-    g = cout // 8
-    if (bn is None or not FIN_IN_GEMM or not getattr(bn, "fused", False) or not bn.training or bn.momentum is None
-            or bn.running_mean is None or g & (g - 1)):
-        return None
-    out = torch.empty(4 * cout, dtype=torch.float32, device=dev)
-    l2 = fin_l2(nblk, cout, dev)
-    a = _native.BnBwdArgs()
-    a.l2, a.cnt, a.count = l2.data_ptr(), fin_tickets(dev, m, cout), m
-    a.gamma, a.beta, a.eps, a.momentum = bn.weight.data_ptr(), bn.bias.data_ptr(), float(bn.eps), float(bn.momentum)
-    a.running_mean, a.running_var, a.out = bn.running_mean.data_ptr(), bn.running_var.data_ptr(), out.data_ptr()
-    return a, out, l2
-
-
 class BnLink:
     """A fused BatchNorm(+ReLU)'s output → the convolution whose data gradient is that output's COMPLETE gradient.
 
     The BatchNorm forward attaches one to its output (``y._plx_bn_link``) holding what its backward reduction
-    reads (x, ReLU mask, mean, invstd, and gamma plus its gradient slots for the finalize).  A consumer conv that
-    the model marks as the sole gradient source (``bn_link=True``) ``request``s a partials buffer and its dgrad
-    GEMM epilogue writes the per-block Σdz and Σdz·x̂ (csrc/conv_gemm.hip ``BnBwd``); the BatchNorm backward then
-    skips its reduce pass.  With ``fin`` (one GEMM launch writes all the partial rows) the same launch also
-    finalizes: it leaves dγ, dβ and the dx coefficients, and the BatchNorm backward runs its dx pass only."""
+    reads (x, ReLU mask, mean, invstd).  A consumer conv that the model marks as the sole gradient source
+    (``bn_link=True``) ``request``s a partials buffer and its dgrad GEMM epilogue writes the per-block
+    Σdz and Σdz·x̂ (csrc/conv_gemm.hip ``BnBwd``); the BatchNorm backward then skips its reduce pass."""
 
-    __slots__ = ("x", "mask", "mean", "invstd", "part", "nblk", "_args", "affine", "weight", "direct", "fin")
+    __slots__ = ("x", "mask", "mean", "invstd", "part", "nblk", "_args", "affine")
 
     def __init__(self, x=None, mask=None, mean=None, invstd=None):
         self.x, self.mask, self.mean, self.invstd = x, mask, mean, invstd
@@ -229,35 +187,19 @@ class BnLink:
         self.part = None
         self.nblk = 0
         self._args = None
-        self.weight = None  # gamma, and its direct (flat-slot) gradients or None: set by the BatchNorm forward
-        self.direct = None
-        self.fin = None
 
-    def request(self, nblk: int, fin: bool = False) -> "_native.BnBwdArgs":
-        n, c, h, w = self.x.shape
-        dev = self.x.device
-        self.part = torch.empty(2 * nblk * c, dtype=torch.float32, device=dev)
+    def request(self, nblk: int) -> "_native.BnBwdArgs":
+        c = self.x.shape[1]
+        self.part = torch.empty(2 * nblk * c, dtype=torch.float32, device=self.x.device)
         self.nblk = nblk
-        a = _native.BnBwdArgs(self.x.data_ptr(), self.mask.data_ptr() if self.mask is not None else None,
-                              self.mean.data_ptr(), self.invstd.data_ptr(), self.part.data_ptr(), nblk, 0)
-        self.fin = None
-        if fin and FIN_IN_GEMM and self.weight is not None:
-            coef = torch.empty(3 * c, dtype=torch.float32, device=dev)
-            dgb = None if self.direct is not None else torch.empty(2 * c, dtype=torch.float32, device=dev)
-            dg, db = (self.direct[0], self.direct[1]) if self.direct is not None else (dgb[:c], dgb[c:])
-            l2 = fin_l2(nblk, c, dev)
-            a.l2, a.cnt, a.count = l2.data_ptr(), fin_tickets(dev, n * h * w, c), n * h * w
-            a.gamma, a.out, a.dgamma, a.dbeta = self.weight.data_ptr(), coef.data_ptr(), dg.data_ptr(), db.data_ptr()
-            a.accumulate = 1 if self.direct is not None else 0
-            self.fin = (coef, dgb, l2)
-        self._args = a
-        return a
+        self._args = _native.BnBwdArgs(self.x.data_ptr(), self.mask.data_ptr() if self.mask is not None else None,
+                                       self.mean.data_ptr(), self.invstd.data_ptr(), self.part.data_ptr(), nblk, 0)
+        return self._args
 
     def take(self):
-        """(partials, nblk, fin): fin = (coef, dgamma|dbeta or None, l2) when the GEMM finalized, else None."""
-        part, nblk, fin = self.part, self.nblk, self.fin
-        self.part, self._args, self.fin = None, None, None
-        return part, nblk, fin
+        part, nblk = self.part, self.nblk
+        self.part, self._args = None, None
+        return part, nblk
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -273,7 +215,7 @@ def bn_link_of(x: torch.Tensor, want: bool):
 
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stats, box, sink, link, fin=None):
+    def forward(ctx, x, weight, stats, box, sink, link):
         x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         ctx.box = box
         ctx.sink = sink if (sink is not None and sink.armed) else None
@@ -285,7 +227,7 @@ class _Conv1x1(torch.autograd.Function):
         cout = weight.shape[0]
         wb, wt = wcache.lookup(weight) or weight_prep(weight)
         y = torch.empty((n, cout, h, w), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
-        gemm_nt(_rows(x), wb, _rows(y), stats, bnr=fin)
+        gemm_nt(_rows(x), wb, _rows(y), stats)
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
         ctx.wdtype = weight.dtype
@@ -309,7 +251,7 @@ class _Conv1x1(torch.autograd.Function):
             # the link is only served when dx (+ the box's gradient) is the whole gradient of x: with a box, the
             # producer must actually have deferred into it; a sink means dx is only part of it
             if ctx.link is not None and ctx.sink is None and (ctx.box is None or extra is not None):
-                bnr = ctx.link.request(-(-(n * h * w) // nt_stats_rows(cin)), fin=True)
+                bnr = ctx.link.request(-(-(n * h * w) // nt_stats_rows(cin)))
             gemm_nt(_rows(dy), wt, _rows(dx), add=_rows(extra) if extra is not None else None, bnr=bnr,
                     add_mask=extra_mask)
             if ctx.sink is not None:  # the downsample conv's dgrad adds this gradient in its epilogue
@@ -322,7 +264,7 @@ class _Conv1x1(torch.autograd.Function):
                 side_stream.run(lambda: gemm_tn(_rows(dy), _rows(x), out=slot, accumulate=True), (dy, x), x.device)
             else:
                 dw = gemm_tn(_rows(dy), _rows(x)).view(ctx.wshape).to(ctx.wdtype)
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def _bf16_context(x: torch.Tensor) -> bool:
@@ -339,28 +281,23 @@ def supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, with_stats: bool = False,
-            grad_box: "GradMailbox" = None, grad_sink: "GradMailbox" = None, bn_link: bool = False,
-            bn=None) -> torch.Tensor:
+            grad_box: "GradMailbox" = None, grad_sink: "GradMailbox" = None, bn_link: bool = False) -> torch.Tensor:
     """With ``with_stats`` the output carries ``_plx_channel_stats`` = (fp32 [2][nblk][Cout] per-block channel
-    sums / sums of squares, nblk, fin), which a following fused BatchNorm uses instead of its own stats pass;
-    ``bn`` (that BatchNorm module): the GEMM's launch also finalizes it (:func:`bn_fin_fwd`), fin = its
-    mean | invstd | scale | bias (else None).
+    sums / sums of squares, nblk), which a following fused BatchNorm uses instead of its own stats pass.
     ``grad_box``: add the box's deferred gradient into dx; ``grad_sink``: defer dx into that (armed) box;
     ``bn_link``: dx (+ ``grad_box``'s gradient) is the complete gradient of ``x`` — serve the BatchNorm that
     produced ``x`` its backward partials (:class:`BnLink`)."""
-    stats = fin = None
+    stats = None
     if with_stats:
         n, _, h, w = x.shape
         m, cout = n * h * w, weight.shape[0]
         nblk = -(-m // nt_stats_rows(cout))
         stats = torch.empty(2 * nblk * cout, dtype=torch.float32, device=x.device)
-        fin = bn_fin_fwd(bn, m, cout, nblk, x.device)
     if grad_box is not None:
         grad_box.armed = True
-    y = _Conv1x1.apply(x, weight, stats, grad_box, grad_sink, bn_link_of(x, bn_link),
-                       fin[0] if fin is not None else None)
+    y = _Conv1x1.apply(x, weight, stats, grad_box, grad_sink, bn_link_of(x, bn_link))
     if stats is not None:
-        y._plx_channel_stats = (stats, nblk, fin[1] if fin is not None else None)
+        y._plx_channel_stats = (stats, nblk)
     return y
 
 
@@ -374,8 +311,8 @@ class Conv1x1(nn.Conv2d):
         self.bn_stats = bn_stats  # emit channel stats for the BatchNorm that follows (training only)
 
     def forward(self, x: torch.Tensor, grad_box: GradMailbox = None, grad_sink: GradMailbox = None,
-                bn_link: bool = False, bn=None) -> torch.Tensor:
+                bn_link: bool = False) -> torch.Tensor:
         if self.native and supported(x, self):
             return conv1x1(x, self.weight, with_stats=self.bn_stats and self.training, grad_box=grad_box,
-                           grad_sink=grad_sink, bn_link=bn_link, bn=bn)
+                           grad_sink=grad_sink, bn_link=bn_link)
         return F.conv2d(x, self.weight, None, self.stride)
