@@ -103,6 +103,10 @@ struct BnBwd {
     const float* invstd;
     float* part;           // nullptr: disabled
     int part_ld, blk_off;
+    // skip_w > 0 (dense GEMM rows = pixels of [n][skip_h][skip_w] images): rows of even-even pixels add nothing --
+    // a strided 1x1 data gradient adds to exactly those pixels afterwards and reduces their final values itself
+    // (ResNet downsampling block: conv1's dgrad here, the downsample conv's in the rows from blk_off on)
+    int skip_h, skip_w;
 };
 
 __device__ __forceinline__ void row_coords(int m, int Hr, int Wr, int& n, int& r, int& c) {
@@ -524,6 +528,13 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         } else {
 #pragma unroll
             for (int it = 0; it < ITERS; ++it) mpre[it] = 0xffu;
+        }
+        if (bnr.skip_w > 0) {
+#pragma unroll
+            for (int it = 0; it < ITERS; ++it) {
+                const int gm = m0 + r0 + it * RSTEP, q = gm / bnr.skip_w;
+                if (((gm - q * bnr.skip_w) | (q % bnr.skip_h)) % 2 == 0) mpre[it] = 0u;
+            }
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -1845,7 +1856,9 @@ int plx_conv_fwd(const void* x, const void* wf, void* y, int Nb, int H, int W, i
 int plx_conv_dgrad(const void* dy, const void* wd, void* dx, int Nb, int H, int W, int Cin, int Cout, int K, int S,
                    const void* zero, const void* D, const BnBwd* bnr, void* stream) {
     if (Nb <= 0 || Cin % 64 || Cout % 64 || (K != 1 && K != 3) || (S != 1 && S != 2)) return -1;
-    if (bnr != nullptr && (S == 2 && K == 1)) return -1;
+    // a strided 1x1 writes the even-even pixels only: its partials can only continue a buffer whose other rows
+    // (blk_off before it) cover the rest (BnBwd::skip_w)
+    if (bnr != nullptr && (S == 2 && K == 1) && bnr->blk_off == 0) return -1;
     hipStream_t st = (hipStream_t)stream;
     BnBwd b = bnr != nullptr ? *bnr : BnBwd{};
     const int rpb = nt_rows_per_block(Cin);

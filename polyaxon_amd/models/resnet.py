@@ -50,7 +50,7 @@ class Bottleneck(nn.Module):
         # downsampling block: conv1's data gradient is deferred into the downsample conv's dgrad epilogue, and the
         # downsample BatchNorm's output feeds only bn3, so bn3's dx pass reduces that BatchNorm's backward partials
         identity = self.downsample(x, grad_box=box)
-        out = self.bn1(self.conv1(x, grad_sink=box))
+        out = self.bn1(self.conv1(x, grad_sink=box, bn_link=True))
         out = self.bn2(self.conv2(out, bn_link=True))
         return self.bn3(self.conv3(out, bn_link=True), identity, residual_link=True)
 
@@ -69,7 +69,9 @@ class Downsample(nn.Module):
 
     def forward(self, x: torch.Tensor, grad_box: Optional[GradMailbox] = None) -> torch.Tensor:
         # the output feeds only bn3's residual add, which applies this BatchNorm's scale/bias itself
-        return self.bn(self.conv(x, grad_box=grad_box), defer_apply=_DEFER_DOWN_BN)
+        # bn_link: the conv's dgrad (+ the box's conv1 gradient) is x's whole gradient -- it serves the BatchNorm that
+        # produced x its backward partials (with conv1's dgrad when strided, ops.conv1x1.BnLink.request_split)
+        return self.bn(self.conv(x, grad_box=grad_box, bn_link=True), defer_apply=_DEFER_DOWN_BN)
 
 
 class ResNet(nn.Module):

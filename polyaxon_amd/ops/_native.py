@@ -410,7 +410,7 @@ class ResBnArgs(ctypes.Structure):
 class BnBwdArgs(ctypes.Structure):
     """Host image of ``BnBwd`` (csrc/conv_gemm.hip): fused BatchNorm-backward partials in a dgrad GEMM epilogue."""
     _fields_ = [("x", _P), ("mask", _P), ("mean", _P), ("invstd", _P), ("part", _P), ("part_ld", _I),
-                ("blk_off", _I)]
+                ("blk_off", _I), ("skip_h", _I), ("skip_w", _I)]
 
 
 def check(rc: int, what: str) -> None:

@@ -64,7 +64,9 @@ class _ConvK(torch.autograd.Function):
         ctx.wshape = weight.shape
         ctx.stride = stride
         ctx.box = box
-        ctx.link = link if not (stride == 2 and k == 1) else None  # that dgrad never writes the odd pixels
+        # a strided 1x1 dgrad never writes the odd pixels: it only finishes a split link (BnLink.request_split)
+        ctx.s2k1 = stride == 2 and k == 1
+        ctx.link = link
         g = direct_grad(weight)
         ctx.wgrad = g if (g is not None and g.stride() == (k * k * cin, 1, k * cin, cin)) else None
         return y
@@ -94,7 +96,10 @@ class _ConvK(torch.autograd.Function):
                 # a strided 1x1 only reaches the even-even pixels: the rest of dx is zero
                 dx = (torch.zeros_like if (s == 2 and k == 1) else torch.empty_like)(x, memory_format=torch.channels_last)
             bnr = None
-            if ctx.link is not None and (ctx.box is None or extra is not None):
+            if ctx.link is not None and ctx.s2k1:
+                if extra is not None and ctx.link.split and ctx.link.part is not None:
+                    bnr = ctx.link.request_rest()
+            elif ctx.link is not None and (ctx.box is None or extra is not None):
                 nblk = _native.size("plx_conv", "plx_conv_dgrad_blocks", n, h, w, cin, cout, k, s)
                 bnr = ctx.link.request(nblk)
             rc = lib.plx_conv_dgrad(dy.data_ptr(), wd.data_ptr(), dx.data_ptr(), n, h, w, cin, cout, k, s, zero,
@@ -142,6 +147,7 @@ def conv_k(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, with_stats: b
         stats = torch.empty(2 * nblk * cout, dtype=torch.float32, device=x.device)
     if grad_box is not None:
         grad_box.armed = True
+        grad_box.s2k1 = stride == 2 and weight.shape[2] == 1
     y = _ConvK.apply(x, weight, stats, stride, grad_box, bn_link_of(x, bn_link))
     if stats is not None:
         y._plx_channel_stats = (stats, nblk)

@@ -15,6 +15,7 @@ gradient comes back in fp32, so autocast's bf16 weight copy and its backward cas
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict
 
 import torch
@@ -116,6 +117,10 @@ def weight_prep(w: torch.Tensor):
     return wb, wt
 
 
+# PLX_SPLIT_LINK=0: the BatchNorm feeding a ResNet downsampling block reduces its own backward partials (A/B knob)
+_SPLIT_LINK = os.environ.get("PLX_SPLIT_LINK", "1") != "0"
+
+
 class GradMailbox:
     """Hands a gradient from a later op's backward to an earlier op's backward that consumes the same tensor.
 
@@ -129,13 +134,14 @@ class GradMailbox:
     autograd sequence number first) runs the producer's backward before the consumer's; ``take`` fails loudly
     if that ever does not hold instead of silently dropping a gradient."""
 
-    __slots__ = ("armed", "grad", "mask", "expect")
+    __slots__ = ("armed", "grad", "mask", "expect", "s2k1")
 
     def __init__(self):
         self.armed = False
         self.grad = None
         self.mask = None
         self.expect = False
+        self.s2k1 = False  # the consumer is a stride-2 1x1 conv (its dgrad adds to the even-even pixels only)
 
     def put(self, g: torch.Tensor) -> None:
         if self.grad is not None:
@@ -179,7 +185,7 @@ class BnLink:
     (``bn_link=True``) ``request``s a partials buffer and its dgrad GEMM epilogue writes the per-block
     Σdz and Σdz·x̂ (csrc/conv_gemm.hip ``BnBwd``); the BatchNorm backward then skips its reduce pass."""
 
-    __slots__ = ("x", "mask", "mean", "invstd", "part", "nblk", "_args", "affine")
+    __slots__ = ("x", "mask", "mean", "invstd", "part", "nblk", "_args", "affine", "split")
 
     def __init__(self, x=None, mask=None, mean=None, invstd=None):
         self.x, self.mask, self.mean, self.invstd = x, mask, mean, invstd
@@ -187,18 +193,44 @@ class BnLink:
         self.part = None
         self.nblk = 0
         self._args = None
+        self.split = 0  # > 0: the first of two GEMMs wrote rows [0, split); the strided 1x1 dgrad still owes the rest
+
+    def _args_for(self, nblk_total: int, blk_off: int) -> "_native.BnBwdArgs":
+        return _native.BnBwdArgs(self.x.data_ptr(), self.mask.data_ptr() if self.mask is not None else None,
+                                 self.mean.data_ptr(), self.invstd.data_ptr(), self.part.data_ptr(), nblk_total,
+                                 blk_off)
 
     def request(self, nblk: int) -> "_native.BnBwdArgs":
         c = self.x.shape[1]
         self.part = torch.empty(2 * nblk * c, dtype=torch.float32, device=self.x.device)
-        self.nblk = nblk
-        self._args = _native.BnBwdArgs(self.x.data_ptr(), self.mask.data_ptr() if self.mask is not None else None,
-                                       self.mean.data_ptr(), self.invstd.data_ptr(), self.part.data_ptr(), nblk, 0)
+        self.nblk, self.split = nblk, 0
+        self._args = self._args_for(nblk, 0)
         return self._args
+
+    def request_split(self, nblk1: int, nblk2: int) -> "_native.BnBwdArgs":
+        """ResNet downsampling block: x feeds conv1 (stride-1 1x1, dgrad deferred into the box) and the stride-2 1x1
+        downsample conv (dgrad adds the box's gradient at the even-even pixels).  conv1's dgrad epilogue reduces
+        the pixels the strided one never touches (rows [0, nblk1), even-even pixels skipped), and the strided
+        dgrad the even-even ones with their final value (rows from nblk1, :meth:`request_rest`)."""
+        n, c, h, w = self.x.shape
+        self.part = torch.empty(2 * (nblk1 + nblk2) * c, dtype=torch.float32, device=self.x.device)
+        self.nblk, self.split = nblk1 + nblk2, nblk1
+        a = self._args_for(nblk1 + nblk2, 0)
+        a.skip_h, a.skip_w = h, w
+        self._args = a
+        return a
+
+    def request_rest(self) -> "_native.BnBwdArgs":
+        a = self._args_for(self.nblk, self.split)
+        self.split = 0
+        self._args = a
+        return a
 
     def take(self):
         part, nblk = self.part, self.nblk
-        self.part, self._args = None, None
+        if self.split:  # the second GEMM never ran: the rows are incomplete, the BatchNorm reduces itself
+            part, nblk = None, 0
+        self.part, self._args, self.split = None, None, 0
         return part, nblk
 
 
@@ -249,9 +281,13 @@ class _Conv1x1(torch.autograd.Function):
                 extra = extra.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
             bnr = None
             # the link is only served when dx (+ the box's gradient) is the whole gradient of x: with a box, the
-            # producer must actually have deferred into it; a sink means dx is only part of it
+            # producer must actually have deferred into it; a sink means dx is only part of it -- except where the
+            # sink's consumer is a strided 1x1, which only adds to the even-even pixels (BnLink.request_split)
+            rows = nt_stats_rows(cin)
             if ctx.link is not None and ctx.sink is None and (ctx.box is None or extra is not None):
-                bnr = ctx.link.request(-(-(n * h * w) // nt_stats_rows(cin)))
+                bnr = ctx.link.request(-(-(n * h * w) // rows))
+            elif ctx.link is not None and ctx.sink is not None and ctx.sink.s2k1 and extra is None and _SPLIT_LINK:
+                bnr = ctx.link.request_split(-(-(n * h * w) // rows), -(-(n * ((h + 1) // 2) * ((w + 1) // 2)) // rows))
             gemm_nt(_rows(dy), wt, _rows(dx), add=_rows(extra) if extra is not None else None, bnr=bnr,
                     add_mask=extra_mask)
             if ctx.sink is not None:  # the downsample conv's dgrad adds this gradient in its epilogue

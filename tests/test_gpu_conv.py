@@ -635,3 +635,49 @@ def test_global_avg_pool_kernels_match_fp32(cuda, shape):
     torch.testing.assert_close(y.float(), yr, rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(xa.grad.float(), xr.grad, rtol=1e-2, atol=1e-3)
     assert xa.grad.is_contiguous(memory_format=torch.channels_last)
+
+
+def _downsample_chain(cuda, split, monkeypatch, shape=(4, 256, 28, 30), width=128, seed=21):
+    """x -> fused BN+ReLU (bn0) -> ResNet downsampling Bottleneck (stride 2) -> sum(g * y): grads of x and bn0."""
+    from polyaxon_amd.models.resnet import Bottleneck, Downsample
+    from polyaxon_amd.ops import conv1x1
+    from polyaxon_amd.ops.norm import BatchNormAct
+
+    monkeypatch.setattr(conv1x1, "_SPLIT_LINK", split)
+    served = {}
+    take = conv1x1.BnLink.take
+
+    def spy(self):
+        part, nblk = take(self)
+        served[id(self)] = part is not None
+        return part, nblk
+    monkeypatch.setattr(conv1x1.BnLink, "take", spy)
+    torch.manual_seed(seed)
+    cin = shape[1]
+    bn0 = BatchNormAct(cin, act=True).to(cuda)
+    blk = Bottleneck(cin, width, 2, Downsample(cin, width * 4, 2)).to(cuda).to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        bn0.weight.uniform_(0.5, 1.5)
+        bn0.bias.uniform_(-0.2, 0.2)
+        for m in blk.modules():
+            if isinstance(m, BatchNormAct):
+                m.weight.uniform_(0.5, 1.5)
+    x = (torch.randn(shape, device=cuda) + 0.2).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        h = bn0(x)
+        y = blk(h)
+    g = torch.randn_like(y.float()).to(torch.bfloat16)
+    y.backward(g)
+    return (x.grad.float(), bn0.weight.grad.clone(), bn0.bias.grad.clone()), served.get(id(h._plx_bn_link))
+
+
+def test_downsampling_block_serves_its_input_batchnorm(cuda, monkeypatch):
+    """The BatchNorm feeding a downsampling block gets its backward partials from conv1's dgrad (all but the
+    even-even pixels) and the strided downsample conv's dgrad (those, with conv1's gradient added) instead of its
+    own reduce pass (ops.conv1x1.BnLink.request_split): same gradients, and the link is actually served."""
+    ref, served_ref = _downsample_chain(cuda, False, monkeypatch)
+    got, served = _downsample_chain(cuda, True, monkeypatch)
+    assert served is True and served_ref is False, (served, served_ref)  # bn0's link, by its backward
+    for a, b, name in zip(got, ref, ("dx", "dgamma", "dbeta")):
+        torch.testing.assert_close(a, b, rtol=1e-2, atol=1e-2 * float(b.abs().max()), msg=name)
