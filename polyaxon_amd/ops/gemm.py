@@ -212,6 +212,10 @@ def forward(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]
 
 
 _GELU_EPILOGUE = os.environ.get("PLX_GELU_EPILOGUE", "1") != "0"  # A/B knob: 0 = GEMM then a separate F.gelu
+# In `auto`, a forward with the GELU epilogue runs on the kernel (one launch, the activation a second store) instead
+# of hipBLASLt + a separate GELU pass: equal in the GPT-2 step (717.8k / 719.9k vs 717.8k / 718.2k tokens/s,
+# profiles/r5_gelu_native_ab.jsonl), one launch and one activation read fewer.  PLX_GELU_NATIVE=0: the table decides.
+_GELU_NATIVE = os.environ.get("PLX_GELU_NATIVE", "1") != "0"
 
 
 def forward_gelu(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None):
@@ -219,7 +223,8 @@ def forward_gelu(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Te
     epilogue (no separate pass reading h back); on hipBLASLt addmm then F.gelu."""
     T, fin = x2.shape
     N = weight.shape[0]
-    if _GELU_EPILOGUE and x2.is_cuda and supported(T, N, fin) and _use_native(T, N, fin, True, True):
+    native = _use_native(T, N, fin, True, True) or (_GELU_NATIVE and mode() == "auto")
+    if _GELU_EPILOGUE and x2.is_cuda and supported(T, N, fin) and native:
         h = torch.empty(T, N, dtype=torch.bfloat16, device=x2.device)
         a = torch.empty_like(h)
         gemm(x2, weight, T, N, fin, True, True, out=h, bias=bias, gelu_out=a)
