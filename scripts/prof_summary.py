@@ -11,11 +11,15 @@ import csv
 import sys
 
 CLASSES = [
-    ("conv GEMM (plx MFMA: 1x1, 3x3 implicit, wgrad slabs)", ("gemm_nt_kernel", "gemm_tn_kernel", "slab_partial", "slab_final",
-                                                           "weight_prep")),
-    ("pool (plx)", ("maxpool_fwd", "maxpool_bwd")),
+    ("conv GEMM (plx MFMA: 1x1, 3x3 implicit, wgrad slabs)", ("gemm_nt_kernel", "gemm_tn_kernel", "wgrad_kernel",
+                                                           "slab_partial", "slab_final", "weight_prep",
+                                                           "stem_pack", "stem_unpack")),
+    ("fused BN+add+ReLU (plx)", ("bn_stats", "bn_apply", "bn_bwd", "bn_fwd", "bn_partial", "stem_apply_pool",
+                                 "stem_pool_bn")),
+    ("pool (plx)", ("maxpool_fwd", "maxpool_bwd", "gap_fwd", "gap_bwd")),
+    ("loss (plx class cross entropy)", ("xent_fwd", "xent_bwd")),
+    ("data (plx synthetic batch)", ("synth_images", "counter_add")),
     ("conv (MIOpen igemm/CK/naive)", ("igemm", "conv", "ck::tensor_operation", "naive_conv", "gtcx")),
-    ("fused BN+add+ReLU (plx)", ("bn_stats", "bn_apply", "bn_bwd", "bn_fwd", "bn_partial")),
     ("BN (MIOpen)", ("MIOpenBatchNorm",)),
     ("optimizer / trial kernels (plx)", ("sgd_flat", "adamw_flat", "record_metric", "commit_metric", "init_flat",
                                          "zero_kernel")),

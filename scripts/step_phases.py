@@ -30,7 +30,7 @@ def union(iv):
 
 def kind(name):
     n = name
-    if "gemm_tn_kernel" in n or "slab_" in n or "stem_unpack_wgrad" in n:
+    if "gemm_tn_kernel" in n or "wgrad_kernel" in n or "slab_" in n or "stem_unpack_wgrad" in n:
         return "wgrad"
     if "gemm_nt_kernel" in n:
         return "nt(fwd/dgrad)"
@@ -44,7 +44,8 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--marker", default="sgd_flat_kernel")
-    ap.add_argument("--loss", default="nll_loss_forward")
+    # the loss kernel ends the forward: torch's NLL, or the fused class cross entropy (ops/lm.py class_xent)
+    ap.add_argument("--loss", default="nll_loss_forward,xent_fwd_kernel")
     ap.add_argument("--markdown", action="store_true")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
@@ -57,7 +58,7 @@ def main():
     n = 0
     for k in range(len(marks) - 1):
         step = rows[marks[k] + 1:marks[k + 1] + 1]
-        li = [i for i, r in enumerate(step) if a.loss in r["Kernel_Name"]]
+        li = [i for i, r in enumerate(step) if any(x in r["Kernel_Name"] for x in a.loss.split(","))]
         if not li:
             continue
         cut = int(step[li[0]]["End_Timestamp"])
