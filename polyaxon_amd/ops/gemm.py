@@ -223,7 +223,9 @@ def forward_gelu(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Te
     epilogue (no separate pass reading h back); on hipBLASLt addmm then F.gelu."""
     T, fin = x2.shape
     N = weight.shape[0]
-    native = _use_native(T, N, fin, True, True) or (_GELU_NATIVE and mode() == "auto")
+    native = _use_native(T, N, fin, True, True)
+    if not native and _GELU_NATIVE and mode() == "auto" and _GELU_EPILOGUE and supported(T, N, fin):
+        _seen[(T, N, fin, True, True)] = native = _LAYOUT_SCHEDULE[_FWD]  # decisions() reports what runs
     if _GELU_EPILOGUE and x2.is_cuda and supported(T, N, fin) and native:
         h = torch.empty(T, N, dtype=torch.bfloat16, device=x2.device)
         a = torch.empty_like(h)

@@ -15,6 +15,7 @@ thread-local.  JSON columns are stored as TEXT and decoded on read.
 from __future__ import annotations
 
 import json
+import math
 import os
 import sqlite3
 import threading
@@ -103,8 +104,23 @@ def _now() -> float:
     return time.time()
 
 
+def _json_safe(v: Any) -> Any:
+    """``v`` with every non-finite float replaced by the string "NaN" / "Infinity" / "-Infinity".  json.dumps writes
+    bare NaN / Infinity tokens, which are not JSON: SQLite's JSON functions reject the whole document as malformed,
+    so one diverged trial's loss made every ``metric.*`` query and sort over its group fail."""
+    if isinstance(v, float):
+        if math.isfinite(v):
+            return v
+        return "NaN" if v != v else ("Infinity" if v > 0 else "-Infinity")
+    if isinstance(v, dict):
+        return {k: _json_safe(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return [_json_safe(x) for x in v]
+    return v
+
+
 def _enc(v: Any) -> Any:
-    return json.dumps(v) if v is not None else None
+    return json.dumps(_json_safe(v)) if v is not None else None
 
 
 class StoreError(RuntimeError):
@@ -317,7 +333,7 @@ class Store:
             try:
                 c.executemany('INSERT INTO experiment_metrics (experiment_id, step, "values", created_at) '
                               "VALUES (?, ?, ?, ?)",
-                              [(x, s, json.dumps({k: float(v) for k, v in vals.items()}), ts or now)
+                              [(x, s, json.dumps(_json_safe({k: float(v) for k, v in vals.items()})), ts or now)
                                for x, vals, s, ts in rows])
                 for xid, vals in merged.items():
                     r = c.execute("SELECT last_metric FROM experiments WHERE id = ?", (xid,)).fetchone()
@@ -326,7 +342,7 @@ class Store:
                     last = json.loads(r["last_metric"] or "{}")
                     last.update(vals)
                     c.execute("UPDATE experiments SET last_metric = ?, updated_at = ? WHERE id = ?",
-                              (json.dumps(last), now, xid))
+                              (json.dumps(_json_safe(last)), now, xid))
                 c.execute("COMMIT")
             except Exception:
                 c.execute("ROLLBACK")
@@ -377,7 +393,8 @@ class Store:
             return []
         rows = self.execute(f"SELECT id, json_extract(last_metric, ?) AS m FROM experiments WHERE id IN "
                             f"({', '.join('?' * len(ids))}) ORDER BY id", [f'$."{metric}"'] + ids).fetchall()
-        return [(r["id"], r["m"]) for r in rows]
+        # a non-finite value (stored as a string, _json_safe) ranks nothing: reported as missing
+        return [(r["id"], r["m"] if isinstance(r["m"], (int, float)) else None) for r in rows]
 
     # ------------------------------------------------------------------ experiment jobs (replicas)
     def create_experiment_job(self, xid: int, role: str, index: int, definition: Optional[Dict[str, Any]] = None,

@@ -237,7 +237,9 @@ class BaseQuery:
                 raise QueryError(f"cannot sort by `{name}`")
             else:
                 expr = f"{a}.{col}"
-            parts.append(f"{expr} IS NULL, {expr} {'DESC' if desc else 'ASC'}")
+            # metrics: a missing or non-finite value (a string, store/db.py _json_safe) sorts last either way
+            last = f"typeof({expr}) NOT IN ('integer', 'real')" if col == "last_metric" else f"{expr} IS NULL"
+            parts.append(f"{last}, {expr} {'DESC' if desc else 'ASC'}")
         parts.append(f"{self.TABLE_ALIAS}.id ASC")
         return ", ".join(parts)
 

@@ -71,6 +71,26 @@ def test_metrics_last_metric_merge(store):
     assert store.experiments_metrics([x], "loss") == [(x, 0.25)]
 
 
+def test_non_finite_metrics_keep_metric_queries_working(store):
+    """A diverged trial's NaN / inf loss is stored as valid JSON ("NaN" / "Infinity"): metric sorts and filters over
+    its group still run (bare NaN made SQLite reject the document as malformed JSON), the value sorts last in both
+    directions and ranks nothing for the search managers."""
+    p = store.create_project("proj")
+    g = store.create_group(p["id"], {}, {})
+    xs = [store.create_experiment(p["id"], group_id=g) for _ in range(4)]
+    store.add_metrics(xs[0], {"loss": 0.5}, step=1)
+    store.add_metrics(xs[1], {"loss": float("nan")}, step=1)
+    store.add_metrics_batch([(xs[2], {"loss": float("inf")}, 1, None), (xs[3], {"loss": 0.25}, 1, None)])
+    asc = [x["id"] for x in store.list_experiments(group_id=g, sort="metric.loss")]
+    desc = [x["id"] for x in store.list_experiments(group_id=g, sort="-metric.loss")]
+    assert asc[:2] == [xs[3], xs[0]] and set(asc[2:]) == {xs[1], xs[2]}
+    assert desc[:2] == [xs[0], xs[3]] and set(desc[2:]) == {xs[1], xs[2]}
+    assert [x["id"] for x in store.list_experiments(group_id=g, query="metric.loss:<0.4")] == [xs[3]]
+    assert store.get_experiment(xs[1])["last_metric"] == {"loss": "NaN"}
+    assert store.get_metrics(xs[2])[0]["values"] == {"loss": "Infinity"}
+    assert dict(store.experiments_metrics(xs, "loss")) == {xs[0]: 0.5, xs[1]: None, xs[2]: None, xs[3]: 0.25}
+
+
 def test_query_dsl(store):
     p = store.create_project("proj")
     g = store.create_group(p["id"], {}, {})

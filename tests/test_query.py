@@ -115,8 +115,10 @@ def test_builder_proxies_and_errors():
 
 def test_sort_expressions():
     q = ExperimentQuery()
-    assert q.order_by("-metric.loss").startswith("json_extract(e.last_metric, '$.\"loss\"') IS NULL, "
-                                                 "json_extract(e.last_metric, '$.\"loss\"') DESC")
+    # a missing or non-finite metric (stored as a string) sorts last either way
+    assert q.order_by("-metric.loss").startswith("typeof(json_extract(e.last_metric, '$.\"loss\"')) NOT IN "
+                                                 "('integer', 'real'), json_extract(e.last_metric, '$.\"loss\"') DESC")
+    assert q.order_by("created_at").startswith("e.created_at IS NULL, e.created_at ASC")
     assert q.order_by("created_at, -id").endswith("e.id ASC")
     for bad in ("bogus", "tags", "metric", "metric.a'b", "independent"):
         with pytest.raises(QueryError):
