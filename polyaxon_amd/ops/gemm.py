@@ -213,8 +213,9 @@ def forward(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]
 
 _GELU_EPILOGUE = os.environ.get("PLX_GELU_EPILOGUE", "1") != "0"  # A/B knob: 0 = GEMM then a separate F.gelu
 # In `auto`, a forward with the GELU epilogue runs on the kernel (one launch, the activation a second store) instead
-# of hipBLASLt + a separate GELU pass: equal in the GPT-2 step (717.8k / 719.9k vs 717.8k / 718.2k tokens/s,
-# profiles/r5_gelu_native_ab.jsonl), one launch and one activation read fewer.  PLX_GELU_NATIVE=0: the table decides.
+# of hipBLASLt + a separate GELU pass.  In the GPT-2 step that was equal on one box (717.8k / 719.9k vs 717.8k /
+# 718.2k tokens/s) and +0.2-0.3 % on another (706.6k / 705.8k vs 704.5k / 704.5k), profiles/r5_gelu_native_ab.jsonl.
+# PLX_GELU_NATIVE=0: the table decides.
 _GELU_NATIVE = os.environ.get("PLX_GELU_NATIVE", "1") != "0"
 
 
