@@ -36,30 +36,6 @@ def capturing() -> bool:
     return torch.cuda.is_current_stream_capturing()
 
 
-# PLX_WGRAD_CUS=n: the side stream is created with a CU mask of n compute units (hipExtStreamCreateWithCUMask), spread
-# evenly over the mask bits, so the weight gradients cannot occupy the CUs (and their LDS) that the data-gradient
-# chain on the main stream needs; unset: an ordinary stream on every CU
-_WGRAD_CUS = int(os.environ.get("PLX_WGRAD_CUS", "0") or 0)
-
-
-def _masked_stream(idx: int, ncu: int) -> "torch.cuda.Stream":
-    import ctypes
-
-    total = torch.cuda.get_device_properties(idx).multi_processor_count
-    ncu = max(1, min(ncu, total))
-    bits = sorted({(i * total) // ncu for i in range(ncu)})
-    words = (ctypes.c_uint32 * ((total + 31) // 32))()
-    for b in bits:
-        words[b // 32] |= 1 << (b % 32)
-    hip = ctypes.CDLL("libamdhip64.so")
-    handle = ctypes.c_void_p()
-    with torch.cuda.device(idx):
-        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(len(words)), words)
-    if rc != 0:
-        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-    return torch.cuda.ExternalStream(handle.value, device=torch.device("cuda", idx))
-
-
 def priority_stream(idx: int, priority: int) -> "torch.cuda.Stream":
     """A HIP stream created with ``hipStreamCreateWithPriority`` (lower = higher priority; HIP maps -1 / 0 / 1 to
     the high / normal / low hardware-queue priority, which the command processor uses when it picks the next queue
@@ -91,9 +67,10 @@ def _stream_for(dev: torch.device) -> "torch.cuda.Stream":
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     s = _side.get(idx)
     if s is None:
-        if _WGRAD_CUS > 0:
-            s = _masked_stream(idx, _WGRAD_CUS)
-        elif _WGRAD_PRIORITY:
+        # (a CU-masked side stream, hipExtStreamCreateWithCUMask, was removed in round 5: it cannot take a priority,
+        # so it shares the compute stream's hardware queue and serialises with it, -29 %,
+        # profiles/r5_wgrad_cumask_ab.jsonl; round 3 measured it slower too)
+        if _WGRAD_PRIORITY:
             s = priority_stream(idx, int(_WGRAD_PRIORITY))
         else:
             s = torch.cuda.Stream(device=idx)
