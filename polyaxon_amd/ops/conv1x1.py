@@ -253,7 +253,9 @@ class _Conv1x1(torch.autograd.Function):
         ctx.sink = sink if (sink is not None and sink.armed) else None
         if ctx.sink is not None:
             ctx.sink.expect = True
-        ctx.link = link
+        # a sink nobody drains (its consumer is not on the native path) means x has another gradient source that
+        # autograd adds: dx is then never x's whole gradient, so the link must not be served
+        ctx.link = link if (sink is None or sink.armed) else None
         ctx.wgrad = direct_grad(weight)
         n, cin, h, w = x.shape
         cout = weight.shape[0]
