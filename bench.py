@@ -70,6 +70,9 @@ def _args(argv=None):
                     help="gpt2_bo: BASELINE config 4 on one node -- a Bayesian-GP search over GPT-2 125M AdamW "
                          "hyper-parameters on resident executors (each timed step = one BO group of "
                          "--bo-initial + --bo-iterations x --bo-concurrency trials per GPU)")
+    ap.add_argument("--trial-gpus", type=int, default=1,
+                    help="GPUs per trial: > 1 runs every trial data-parallel on a resident DP gang of that many ranks "
+                         "(FlatDDP over the framework RCCL communicator; BASELINE config 4: 2).  Must divide --gpus")
     ap.add_argument("--bo-initial", type=int, default=4)
     ap.add_argument("--bo-iterations", type=int, default=3)
     ap.add_argument("--bo-concurrency", type=int, default=4, help="trials per BO batch (constant liar) per GPU")
@@ -103,6 +106,8 @@ def _args(argv=None):
     args = ap.parse_args(argv)
     if args.target is None:
         args.target = 0.5 if args.config == "gpt2_bo" else 0.03
+    if args.trial_gpus < 1 or args.gpus % args.trial_gpus:
+        ap.error("--trial-gpus must divide --gpus")
     return args
 
 
@@ -123,7 +128,8 @@ def program_params(args):
 
 
 def bo_group_spec(seed: int, program: str, params: dict, args, world: int) -> dict:
-    """BASELINE config 4: GP-UCB over GPT-2's AdamW learning rate, weight decay and beta2."""
+    """BASELINE config 4: GP-UCB over GPT-2's AdamW learning rate, weight decay and beta2.  ``world``: executors (one
+    per GPU, or one per DP gang of ``--trial-gpus`` GPUs); every trial asks for ``--trial-gpus`` devices."""
     hp = {"seed": seed, "concurrency": args.bo_concurrency * world,
           "matrix": {"lr": {"loguniform": [math.log(1e-5), math.log(3e-3)]},
                      "weight_decay": {"uniform": [0.0, 0.2]},
@@ -135,13 +141,13 @@ def bo_group_spec(seed: int, program: str, params: dict, args, world: int) -> di
                                       "gaussian_process": {"kernel": "matern", "length_scale": 1.0, "nu": 2.5},
                                       "n_warmup": 10000, "n_iter": 8}}}
     return {"version": 1, "kind": "group", "project": "bench_gpt2_bo", "hptuning": hp,
-            "environment": {"resources": {"gpu": 1},
+            "environment": {"resources": {"gpu": args.trial_gpus},
                             "executor": {"kind": "resident", "program": program, "params": params,
                                          "max_active_brackets": args.max_active}}}
 
 
 def group_spec(seed: int, program: str, params: dict, concurrency: int, max_active: int, search: str = "hyperband",
-               asha_n: int = 29) -> dict:
+               asha_n: int = 29, trial_gpus: int = 1) -> dict:
     matrix = {"lr": {"loguniform": [math.log(0.02), math.log(1.0)]},
               "momentum": {"uniform": [0.8, 0.95]},
               "weight_decay": {"loguniform": [math.log(1e-5), math.log(1e-3)]}}
@@ -155,7 +161,7 @@ def group_spec(seed: int, program: str, params: dict, concurrency: int, max_acti
         hp = {"seed": seed, "concurrency": concurrency, "matrix": matrix,
               "hyperband": {"max_iter": MAX_ITER, "eta": ETA, "resource": resource, "metric": metric, "resume": True}}
     return {"version": 1, "kind": "group", "project": "bench_resnet50_" + search, "hptuning": hp,
-            "environment": {"resources": {"gpu": 1},
+            "environment": {"resources": {"gpu": trial_gpus},
                             "executor": {"kind": "resident", "program": program, "params": params,
                                          "max_active_brackets": max_active}}}
 
@@ -171,6 +177,7 @@ class ControlServer:
         from polyaxon_amd.polyflow.scheduler import Polyflow
 
         self.args, self.world = args, world
+        self.n_exec = world // args.trial_gpus  # resident executors: one per GPU, or one per DP gang
         self.program, self.params = program_params(args)
         self.log = log or (lambda m: print(f"[control +{time.perf_counter() - T0:.1f}s] {m}", file=sys.stderr,
                                            flush=True))
@@ -189,7 +196,7 @@ class ControlServer:
 
         execs = 0
         self.listener.settimeout(900)
-        while execs < self.world or self.bench is None:
+        while execs < self.n_exec or self.bench is None:
             sock, _ = self.listener.accept()
             sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             chan = Channel(sock)
@@ -199,13 +206,13 @@ class ControlServer:
             if hello.get("bench"):
                 self.bench = chan
                 continue
-            self.flow.attach_resident(chan, int(hello["rank"]), self.program, self.params,
-                                      max_active=self.args.max_active)
+            devices = hello.get("devices") or [int(hello["rank"])]  # a DP gang's leader brings the gang's devices
+            self.flow.attach_resident(chan, devices, self.program, self.params, max_active=self.args.max_active)
             execs += 1
         end = time.time() + 900
         while time.time() < end:
             snap = self.flow.call(lambda: self.flow.resident_pool().snapshot())
-            if sum(1 for w in snap if w["ready"]) == self.world:
+            if sum(1 for w in snap if w["ready"]) == self.n_exec:
                 return
             time.sleep(0.05)
         raise TimeoutError("resident executors did not become ready")
@@ -215,10 +222,10 @@ class ControlServer:
         n_groups = n // self.world if self.args.config == "gpt2_bo" else n  # one BO group spans every GPU
         for i in range(n_groups):
             if self.args.config == "gpt2_bo":
-                spec = bo_group_spec(seed0 + i, self.program, self.params, self.args, self.world)
+                spec = bo_group_spec(seed0 + i, self.program, self.params, self.args, self.n_exec)
             else:
-                spec = group_spec(seed0 + i, self.program, self.params, self.world, self.args.max_active,
-                                  self.args.search, self.args.asha_n)
+                spec = group_spec(seed0 + i, self.program, self.params, self.n_exec, self.args.max_active,
+                                  self.args.search, self.args.asha_n, self.args.trial_gpus)
             gids.append(self.flow.submit(spec)["id"])
         t_log = time.time()
         for g in gids:
@@ -241,7 +248,7 @@ class ControlServer:
 
     def _pause(self, tag: str) -> None:
         done = threading.Event()
-        left = [self.world]
+        left = [self.n_exec]
 
         def on_paused(_msg):
             left[0] -= 1
@@ -256,7 +263,8 @@ class ControlServer:
         rc = 0
         try:
             self._accept()
-            self.log(f"{self.world} resident executors ready; warm-up: {self.args.warmup} sweep(s)/GPU")
+            self.log(f"{self.n_exec} resident executors ready ({self.args.trial_gpus} GPU(s) each); warm-up: "
+                     f"{self.args.warmup} sweep(s)/GPU")
             if self.args.warmup:
                 self._sweeps(self.args.warmup * self.world, 10_000)
             base = self.flow.call(lambda: self.flow.resident_pool().snapshot())
@@ -340,6 +348,12 @@ class ControlServer:
         units = sum(1 for it in st.execute(
             f"SELECT data FROM experiment_group_iterations WHERE group_id IN ({q})", gids).fetchall()
             if json.loads(it["data"]).get("bracket_iteration") == 0)
+        # devices held by every trial's job (a DP=2 trial: both of its gang's devices)
+        trial_devices: dict = {}
+        for x in xs:
+            for j in st.experiment_jobs(x["id"]):
+                n = str(len(j.get("devices") or []))
+                trial_devices[n] = trial_devices.get(n, 0) + 1
         pool = self.flow.call(lambda: self.flow.resident_pool().snapshot())
         b = {w["wid"]: w for w in base}
         execs = []
@@ -364,7 +378,7 @@ class ControlServer:
                                   "suggest": [it["data"].get("suggest") for it in its[1:]]})
         return {"trials": trials, "succeeded": ok, "train_steps": steps, "ttt": ttt, "best": best, "per_sweep": per_sweep,
                 "bo_groups": bo_groups,
-                "per_units": per_units,
+                "per_units": per_units, "trial_devices": trial_devices,
                 "fsm_ok": fsm_ok, "resumed": resumed, "brackets": units, "groups": len(gids), "executors": execs,
                 "control_pid": os.getpid(), "control_device_footprint": device_footprint()}
 
@@ -485,7 +499,7 @@ def main() -> int:
     import torch
     import torch.distributed as dist
 
-    from polyaxon_amd.polyflow.resident import Channel, ResidentWorker
+    from polyaxon_amd.polyflow.resident import Channel, ResidentWorker, _FollowerChannel, _LeaderChannel
 
     def log(msg):
         if rank == 0:
@@ -507,6 +521,15 @@ def main() -> int:
         dist.broadcast_object_list(addr, src=0)
         ctl_addr = addr[0]
     host, _, port = ctl_addr.rpartition(":")
+    # --trial-gpus T > 1: ranks [g T, (g + 1) T) form DP gang g -- one resident executor whose trials train
+    # data-parallel over the gang's subgroup (FlatDDP on the gang's framework RCCL communicator); its rank 0 talks to
+    # the scheduler and re-broadcasts the control stream to the others (polyflow/resident.py _GangGroup)
+    tg = args.trial_gpus
+    gang_group = None
+    if tg > 1:
+        groups = [dist.new_group(list(range(g * tg, (g + 1) * tg))) for g in range(world // tg)]
+        gang_group = groups[rank // tg]
+    leader = rank % tg == 0
 
     def barrier():
         if dev.type == "cuda":
@@ -535,17 +558,26 @@ def main() -> int:
         except Exception as e:  # built again after the timed region (or gloo) rather than fail the run
             print(f"bench: early RCCL communicator unavailable ({e})", file=sys.stderr)
     worker = ResidentWorker(program, params, device=dev, max_active=args.max_active)
-    log(f"building {program} executors (batch {params['batch']}, image {params.get('image')}, config {args.config})")
+    if gang_group is not None:
+        worker.join_gang(rank % tg, tg, group=gang_group)
+    log(f"building {program} executors (batch {params['batch']}, image {params.get('image')}, config {args.config}, "
+        f"{tg} GPU(s) per trial)")
     worker._ready_info = worker.build()
     log(f"executor ready in {worker._ready_info['build_s']} s")
-    chan = Channel.connect(host, int(port), timeout=300)
-    chan.send({"rank": local if world > 1 else 0})
+    chan = ctl = None
+    if leader:
+        chan = Channel.connect(host, int(port), timeout=300)
+        first = local if world > 1 else 0
+        chan.send({"rank": first, "devices": list(range(first, first + tg))})
+        ctl = _LeaderChannel(chan, worker.gang) if worker.gang is not None else chan
+    else:
+        ctl = _FollowerChannel(worker.gang)
     bench = None
     if rank == 0:
         bench = Channel.connect(host, int(port), timeout=300)
         bench.send({"bench": 1})
 
-    r = worker.serve(chan)                      # warm-up sweeps, until paused
+    r = worker.serve(ctl)                       # warm-up sweeps, until paused
     if r != "pause:warm":
         raise RuntimeError(f"executor stopped during warm-up: {r}")
     s0 = dict(worker.stats)
@@ -554,13 +586,21 @@ def main() -> int:
     if bench is not None:
         bench.send({"op": "go", "t0": time.time()})
         log("timed region")
-    r = worker.serve(chan)                      # timed sweeps, until paused
+    r = worker.serve(ctl)                       # timed sweeps, until paused
     barrier()
     elapsed = time.perf_counter() - t0
     if r != "pause:timed":
         raise RuntimeError(f"executor stopped during the timed region: {r}")
+    ex = worker.program.executor
+    with torch.no_grad():  # fingerprint of the final weights: the ranks of one DP gang must hold identical ones
+        p64 = ex.flat.params.detach().double()
+        w_sum = float(p64.sum())
+        w_mix = float((p64 * torch.arange(p64.numel(), device=p64.device, dtype=torch.float64).remainder_(97).add_(1))
+                      .sum())
     mine = [elapsed, worker.stats["trials"] - s0["trials"], worker.stats["train_steps"] - s0["train_steps"],
-            float(os.getpid())] + [worker.stats[k] - s0[k] for k in ("idle_s", "round_s", "sync_s")]
+            float(os.getpid())] + [worker.stats[k] - s0[k] for k in ("idle_s", "round_s", "sync_s")] + [
+            float(ex.ddp.launched if ex.ddp is not None else 0),
+            float(ex.ddp._comm is not None) if ex.ddp is not None else 0.0, w_sum, w_mix]
     # framework-owned collective (csrc/rccl_comm.cpp) for the per-rank gather on the GPU path (the early communicator,
     # or one created now).
     comm = early_comm
@@ -591,14 +631,15 @@ def main() -> int:
             raise RuntimeError(f"control process failed: {msg}")
         res = msg["result"]
         value = res["trials"] / elapsed_max * 3600.0
+        n_exec = world // tg
         search = (f"hyperband max_iter={MAX_ITER} eta={ETA} resume=true, 3 brackets / 23 trials per sweep"
                   if args.search == "hyperband" else
                   f"asha min_resource=1 max_resource={ASHA_MAX} eta={ETA} resume=true, {args.asha_n} configs per sweep")
         gpt2 = args.config == "gpt2_bo"
         if gpt2:
             search = (f"bo (GP-UCB, matern 2.5, unit space: log-lr) over lr / weight_decay / beta2: "
-                      f"{args.bo_initial * world} random + "
-                      f"{args.bo_iterations} x {args.bo_concurrency * world} constant-liar suggestions per group, "
+                      f"{args.bo_initial * n_exec} random + "
+                      f"{args.bo_iterations} x {args.bo_concurrency * n_exec} constant-liar suggestions per group, "
                       f"{params['trial_units'] * params['unit_steps']} AdamW steps per trial")
         out = {
             "metric": METRIC_BO if gpt2 else METRIC,
@@ -623,10 +664,14 @@ def main() -> int:
                 "model": (("gpt2_125m" if dev.type == "cuda" else "gpt2 tiny (CPU rehearsal)") if gpt2 else
                           ("resnet50" if dev.type == "cuda" else "resnet18ish (CPU rehearsal)")),
                 "global_batch": params["batch"] * world,
-                "per_trial_batch": params["batch"],
+                "per_trial_batch": params["batch"] * tg,
+                "per_trial_world": tg,
                 "seq_len": params.get("seq"),
                 "image_size": params.get("image"),
-                "parallelism": f"trial-parallel x{world} (resident executor per GPU, brackets balanced by polyflow)",
+                "parallelism": (f"trial-parallel x{world} (resident executor per GPU, brackets balanced by polyflow)"
+                                if tg == 1 else
+                                f"trial-parallel x{n_exec}, each trial dp{tg} (resident executor per DP gang: FlatDDP "
+                                f"over the framework RCCL communicator)"),
                 "search": search,
                 "unit_steps": params["unit_steps"],
                 "step": "one complete sweep per GPU",
@@ -638,7 +683,8 @@ def main() -> int:
             "trials": res["trials"],
             "trials_succeeded": res["succeeded"],
             "trials_resumed": res["resumed"],
-            "train_images_per_s": round(res["train_steps"] * params["batch"] / elapsed_max, 1),
+            # every rank of a DP=T trial trains its own per-rank batch each step
+            "train_images_per_s": round(res["train_steps"] * params["batch"] * tg / elapsed_max, 1),
             "wall_clock_to_target_s": round(res["ttt"], 3) if res["ttt"] is not None else None,
             "target_loss": args.target,
             "best_loss": round(res["best"], 4) if res["best"] is not None else None,
@@ -666,7 +712,10 @@ def main() -> int:
             "hip_graph": bool(worker._ready_info.get("hip_graph")),
             "per_rank": [{"rank": i, "pid": int(p[3]), "elapsed_s": round(p[0], 3), "trials": int(p[1]),
                           "train_steps": int(p[2]), "idle_s": round(p[4], 3), "round_s": round(p[5], 3),
-                          "sync_s": round(p[6], 3)} for i, p in enumerate(per_rank)],
+                          "sync_s": round(p[6], 3), "gang": i // tg, "ddp_collectives": int(p[7]),
+                          "ddp_on_framework_comm": bool(p[8]), "weights_fingerprint": [p[9], p[10]]}
+                         for i, p in enumerate(per_rank)],
+            "trial_devices": res["trial_devices"],
             "executors": res["executors"],
             "control_pid": res["control_pid"],
             # the scheduler process (polyflow + BO GP requests to the executors) holds no GPU state
@@ -674,9 +723,11 @@ def main() -> int:
             "cpus_pinned": len(pinned),
         }
         print(json.dumps(out), file=result_out, flush=True)
-    chan.close()
+    if chan is not None:
+        chan.close()
     if bench is not None:
         bench.close()
+    worker.close_gang()
     if comm is not None:
         if comm is early_comm and world > 1:
             from polyaxon_amd.parallel import comm as _comm

@@ -256,7 +256,8 @@ __global__ __launch_bounds__(kBlock) void xent_fwd_kernel(const uint16_t* __rest
     const float l = m + __logf(sum);
     const int64_t t = CLS ? tokens[r] : tokens[lrow + 1];
     lse[r] = l;
-    loss[r] = l - bf2f(row[t]);
+    // a label outside [0, V) (ignore_index -100, or a bad label) contributes nothing and is never read
+    loss[r] = (t >= 0 && t < V) ? l - bf2f(row[t]) : 0.f;
   }
 }
 
@@ -273,7 +274,8 @@ __global__ __launch_bounds__(kBlock) void xent_bwd_kernel(const uint16_t* __rest
   bf16x8* gbase = (bf16x8*)(q0 & ~(uintptr_t)15);
   const int head = (int)((q0 & 15) >> 1);       // logits and grad share the layout (same offsets)
   const int nch = (head + V + 7) >> 3;
-  if (!CLS && s == S - 1) {                      // the last position predicts nothing: zero gradient
+  const int64_t tl = CLS ? tokens[lrow] : (s < S - 1 ? tokens[(int64_t)lrow + 1] : 0);
+  if ((!CLS && s == S - 1) || tl < 0 || tl >= V) {  // predicts nothing (last position, ignored label): zero gradient
     for (int c = threadIdx.x; c < nch; c += kBlock) {
       if (c * 8 - head >= 0 && c * 8 - head + 8 <= V) {
         gbase[c] = bf16x8{};
@@ -289,7 +291,7 @@ __global__ __launch_bounds__(kBlock) void xent_bwd_kernel(const uint16_t* __rest
   }
   const int r = CLS ? lrow : b * (S - 1) + s;
   const float l = lse[r], g = dloss[0] * inv_rows;
-  const int64_t t = CLS ? tokens[lrow] : tokens[(int64_t)lrow + 1];
+  const int64_t t = tl;
   const bf16x8* base = (const bf16x8*)((uintptr_t)(logits + (int64_t)lrow * V) & ~(uintptr_t)15);
   for (int c = threadIdx.x; c < nch; c += kBlock) {
     const bf16x8 v = base[c];
@@ -477,12 +479,13 @@ PLX_API int plx_xent_cls_fwd(const void* logits, const int64_t* labels, float* l
   return (int)hipGetLastError();
 }
 
-// grad bf16 [N][V] = (softmax - onehot(label)) * dloss / N; dloss: device scalar gradient of the mean loss
+// grad bf16 [N][V] = (softmax - onehot(label)) * dloss * scale (scale <= 0: 1 / N, the mean over all rows); rows whose
+// label is outside [0, V) get a zero gradient; dloss: device scalar gradient of the loss
 PLX_API int plx_xent_cls_bwd(const void* logits, const int64_t* labels, const float* lse, const float* dloss,
-                             void* grad, int N, int V, hipStream_t stream) {
+                             void* grad, int N, int V, float scale, hipStream_t stream) {
   if (N <= 0 || V <= 0) return 1;
   hipLaunchKernelGGL(xent_bwd_kernel<true>, dim3(N), dim3(kBlock), 0, stream, (const uint16_t*)logits, labels, lse,
-                     dloss, (uint16_t*)grad, 1, V, 1.f / (float)N);
+                     dloss, (uint16_t*)grad, 1, V, scale > 0.f ? scale : 1.f / (float)N);
   return (int)hipGetLastError();
 }
 

@@ -1,8 +1,12 @@
 """Health / status checks (reference polyaxon/checks/*.py: Postgres, Redis, RabbitMQ and a round-trip
 health task per Celery queue).  Here: the store, the scheduler thread (round-trip through its command
-queue), the native libraries, the HIP devices and RCCL availability."""
+queue), the native libraries, the HIP devices and a real RCCL round trip in a child process (this process stays GPU-free)."""
 from __future__ import annotations
 
+import json
+import os
+import subprocess
+import sys
 import time
 from typing import Any, Dict
 
@@ -44,13 +48,39 @@ def check_devices(flow) -> Dict[str, Any]:
     return _result(not unhealthy, f"unhealthy: {unhealthy}" if unhealthy else "", n_devices=len(devs))
 
 
-def check_rccl() -> Dict[str, Any]:
-    try:
-        import torch.distributed as dist
+_RCCL_CACHE: Dict[str, Any] = {}
+RCCL_CACHE_S = 60.0
 
-        return _result(dist.is_available() and dist.is_nccl_available(), backend="nccl (RCCL)")
+
+def check_rccl(timeout: float = 90.0, max_age: float = RCCL_CACHE_S) -> Dict[str, Any]:
+    """A real RCCL round trip (obs/rccl_probe.py) in a short-lived child process: this process -- the API /
+    scheduler -- never imports torch or maps the HIP runtime.  The result is cached for ``max_age`` seconds so a
+    polled ``/_status`` does not start a GPU process per request.  "skipped" (no device visible) counts as healthy."""
+    now = time.monotonic()
+    hit = _RCCL_CACHE.get("result")
+    if hit is not None and now - _RCCL_CACHE.get("at", 0.0) < max_age:
+        return dict(hit, cached=True)
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    pp = os.environ.get("PYTHONPATH")
+    env = dict(os.environ, PYTHONPATH=root + (os.pathsep + pp if pp else ""))
+    t = time.perf_counter()
+    try:
+        out = subprocess.run([sys.executable, "-m", "polyaxon_amd.obs.rccl_probe"], capture_output=True, text=True,
+                             timeout=timeout, env=env, cwd=root)
+        lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+        res = json.loads(lines[-1]) if lines else {"status": "error",
+                                                   "message": f"probe exited {out.returncode}: {out.stderr[-300:]}"}
+    except subprocess.TimeoutExpired:
+        res = {"status": "error", "message": f"RCCL probe did not finish within {timeout:.0f} s"}
     except Exception as e:
-        return _result(False, str(e))
+        res = {"status": "error", "message": f"{type(e).__name__}: {e}"}
+    res["probe_ms"] = round((time.perf_counter() - t) * 1000, 1)
+    healthy = res.get("status") in ("ok", "skipped")
+    result = _result(healthy, res.get("message", ""), **{k: v for k, v in res.items() if k not in ("status", "message")})
+    if res.get("status") == "skipped":
+        result["skipped"] = True
+    _RCCL_CACHE.update(result=result, at=now)
+    return dict(result, cached=False)
 
 
 def run_checks(flow) -> Dict[str, Any]:

@@ -36,7 +36,7 @@ LIBRARIES: Dict[str, dict] = {
     "plx_lm": {"sources": ["lm_kernels.hip"], "kind": "hip", "link": []},
     "plx_gemm": {"sources": ["gemm256.hip"], "kind": "hip", "link": []},
     "plx_attn": {"sources": ["attn_kernels.hip"], "kind": "hip", "link": []},
-    "plx_rccl": {"sources": ["rccl_comm.cpp"], "kind": "hip_host", "link": ["-lrccl"]},
+    "plx_rccl": {"sources": ["rccl_comm.cpp"], "kind": "hip_host", "link": ["-lrccl", "-pthread"]},
 }
 
 _lock = threading.Lock()
@@ -324,7 +324,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_xent_fwd": [_P, _P, _P, _P, _I, _I, _I, _P],
         "plx_xent_bwd": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
         "plx_xent_cls_fwd": [_P, _P, _P, _P, _I, _I, _P],
-        "plx_xent_cls_bwd": [_P, _P, _P, _P, _P, _I, _I, _P],
+        "plx_xent_cls_bwd": [_P, _P, _P, _P, _P, _I, _I, _F, _P],
         "plx_colsum_splits": [_L, _I],
         "plx_colsum": [_P, _L, _I, _P, _P, _P, _I, _P],
         "plx_gelu_bwd_colsum": [_P, _P, _P, _L, _I, _P, _P, _P, _I, _P],
@@ -372,13 +372,17 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
     },
     "plx_rccl": {
         "plx_rccl_unique_id": [ctypes.c_char_p],
-        "plx_rccl_init": [ctypes.c_char_p, _I, _I, _I, ctypes.POINTER(_I)],
+        "plx_rccl_init": [ctypes.c_char_p, _I, _I, _I, _L, _L, ctypes.POINTER(_I)],
         "plx_rccl_all_reduce": [_P, _P, _P, _L, _I, _I, _P],
         "plx_rccl_all_gather": [_P, _P, _P, _L, _I, _P],
         "plx_rccl_reduce_scatter": [_P, _P, _P, _L, _I, _I, _P],
         "plx_rccl_broadcast": [_P, _P, _P, _L, _I, _I, _P],
         "plx_rccl_bus_bw": [_P, _P, _L, _I, _P, ctypes.POINTER(_D), ctypes.POINTER(_D)],
         "plx_rccl_destroy": [_P],
+        "plx_rccl_status": [_P],
+        "plx_rccl_pending": [_P],
+        "plx_rccl_set_timeout": [_P, _L],
+        "plx_rccl_abort": [_P],
         "plx_rccl_error": [_I],
     },
     "plx_polytune": {

@@ -28,9 +28,11 @@ def _stream() -> int:
     return _native.current_stream()
 
 
-def supported(features: torch.Tensor, fc: nn.Module, labels: torch.Tensor) -> bool:
+def supported(features: torch.Tensor, fc: nn.Module, labels: torch.Tensor, labels_in_range: bool = False) -> bool:
+    """``labels_in_range``: the caller guarantees 0 <= label < fc.out_features for every row (the executor's own
+    synthetic data); the fused step has no ignore-index handling of its own (its mean divides by every row)."""
     n, c = features.shape[:2]
-    return (features.is_cuda and features.dtype == torch.bfloat16 and features.dim() == 4 and c % 8 == 0
+    return (labels_in_range and features.is_cuda and features.dtype == torch.bfloat16 and features.dim() == 4 and c % 8 == 0
             and features.is_contiguous(memory_format=torch.channels_last) and features.data_ptr() % 16 == 0
             and isinstance(fc, nn.Linear) and fc.bias is not None and fc.in_features == c
             and fc.weight.grad is not None and fc.bias.grad is not None
@@ -63,7 +65,7 @@ def classifier_head_step(features: torch.Tensor, fc: nn.Linear, labels: torch.Te
         ones = torch.ones(1, dtype=torch.float32, device=dev)
     dlogits = torch.empty_like(logits)
     _native.check(lm.plx_xent_cls_bwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), ones.data_ptr(),
-                                      dlogits.data_ptr(), n, v, _stream()), "plx_xent_cls_bwd")
+                                      dlogits.data_ptr(), n, v, 0.0, _stream()), "plx_xent_cls_bwd")
     fc.weight.grad.add_(torch.mm(dlogits.t(), pooled))
     fc.bias.grad.add_(dlogits.sum(0))
     dpooled = torch.mm(dlogits, wb)

@@ -169,37 +169,49 @@ def next_token_xent(logits: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
 class _ClassXent(torch.autograd.Function):
     """mean over rows of lse(logits[r]) - logits[r, labels[r]] from bf16 logits [N][V] (csrc/lm_kernels.hip
     plx_xent_cls_fwd / plx_xent_cls_bwd): replaces F.cross_entropy(logits.float(), labels)'s fp32 cast, log-softmax,
-    NLL and their three backward kernels with one kernel each way (the ResNet head, polyflow/executor.py)."""
+    NLL and their three backward kernels with one kernel each way (the ResNet head, polyflow/executor.py).
+
+    Rows whose label lies outside [0, V) (F.cross_entropy's ignore_index -100) contribute no loss and no gradient;
+    unless the caller guarantees every label is in range (``in_range``: the executor's own synthetic data), the mean
+    divides by the number of valid rows, as F.cross_entropy does (two extra small reductions)."""
 
     @staticmethod
-    def forward(ctx, logits, labels):
+    def forward(ctx, logits, labels, in_range):
         lib = _native.lib("plx_lm")
         N, V = logits.shape
         lse = torch.empty(N, dtype=torch.float32, device=logits.device)
         loss = torch.empty(N, dtype=torch.float32, device=logits.device)
         _native.check(lib.plx_xent_cls_fwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), loss.data_ptr(), N, V,
                                            _stream()), "plx_xent_cls_fwd")
-        ctx.save_for_backward(logits, labels, lse)
-        return loss.mean()
+        nvalid = None if in_range else ((labels >= 0) & (labels < V)).sum().clamp_min(1).to(torch.float32)
+        ctx.save_for_backward(logits, labels, lse, nvalid if nvalid is not None else lse.new_ones(()))
+        ctx.in_range = in_range
+        return loss.mean() if in_range else loss.sum() / nvalid
 
     @staticmethod
     def backward(ctx, g):
         lib = _native.lib("plx_lm")
-        logits, labels, lse = ctx.saved_tensors
+        logits, labels, lse, nvalid = ctx.saved_tensors
         N, V = logits.shape
         grad = torch.empty_like(logits)
-        g = g.detach().to(torch.float32).reshape(1).contiguous()
+        g = g.detach().to(torch.float32).reshape(1)
+        if not ctx.in_range:
+            g = g / nvalid  # scale 1: the kernel multiplies by dloss only
+        g = g.contiguous()
         _native.check(lib.plx_xent_cls_bwd(logits.data_ptr(), labels.data_ptr(), lse.data_ptr(), g.data_ptr(),
-                                           grad.data_ptr(), N, V, _stream()), "plx_xent_cls_bwd")
-        return grad, None
+                                           grad.data_ptr(), N, V, 0.0 if ctx.in_range else 1.0, _stream()),
+                      "plx_xent_cls_bwd")
+        return grad, None, None
 
 
-def class_xent(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-    """Classification cross entropy, mean over the N rows: the fused HIP pair on bf16 CUDA logits [N, V] (contiguous)
-    with int64 labels [N]; F.cross_entropy on fp32 logits otherwise."""
+def class_xent(logits: torch.Tensor, labels: torch.Tensor, in_range: bool = False) -> torch.Tensor:
+    """Classification cross entropy, mean over the rows with a label in [0, V) (F.cross_entropy semantics, ignore
+    index -100 included): the fused HIP pair on bf16 CUDA logits [N, V] (contiguous) with int64 labels [N];
+    F.cross_entropy on fp32 logits otherwise.  ``in_range``: the caller guarantees 0 <= label < V for every row
+    (skips the valid-row count)."""
     if (logits.is_cuda and logits.dtype == torch.bfloat16 and logits.dim() == 2 and logits.is_contiguous()
             and labels.dtype == torch.int64 and labels.is_contiguous() and labels.shape == logits.shape[:1]):
-        return _ClassXent.apply(logits, labels)
+        return _ClassXent.apply(logits, labels, bool(in_range))
     return F.cross_entropy(logits.float(), labels)
 
 

@@ -55,17 +55,22 @@ def init_from_env(backend: Optional[str] = None, device: Optional[torch.device] 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    explicit = backend is not None
     if backend is None:  # the rendezvous: device collectives go through parallel/comm.py's communicator
         backend = "gloo"
     if device is None:
-        device = torch.device("cuda", local) if (backend == "nccl" or torch.cuda.is_available()) else torch.device("cpu")
+        # the GPU only when the caller asks for it (nccl, or no backend named on a GPU host): an explicit gloo backend
+        # keeps the CPU, so CPU data-parallel runs on a GPU host never initialise HIP
+        cuda = backend == "nccl" or (not explicit and torch.cuda.is_available())
+        device = torch.device("cuda", local) if cuda else torch.device("cpu")
     if device.type == "cuda":
         torch.cuda.set_device(device)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {"device_id": device} if backend == "nccl" else {}
-        # collective watchdog: polyflow sets PLX_COLLECTIVE_TIMEOUT_S (+ TORCH_NCCL_ASYNC_ERROR_HANDLING) for
-        # multi-rank trials so a dead peer fails this rank instead of hanging it (polyflow/env.py)
+        # the rendezvous' own deadline: polyflow sets PLX_COLLECTIVE_TIMEOUT_S for multi-rank trials
+        # (polyflow/env.py), so a dead peer fails this rank's gloo control traffic instead of hanging it; the device
+        # collectives' deadline is the framework communicator's watchdog (csrc/rccl_comm.cpp), same variable
         timeout = float(os.environ.get("PLX_COLLECTIVE_TIMEOUT_S", "0") or 0)
         if timeout > 0:
             kw["timeout"] = datetime.timedelta(seconds=timeout)
@@ -151,6 +156,13 @@ class FlatDDP:
         self.force = bool(force_collectives) and dist.is_initialized()
         self.coll = self.world > 1 or self.force            # collectives run (world > 1, or forced at world 1)
         self.nccl = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
+        pg_mode = os.environ.get("PLX_DDP_COMM", "comm") == "pg"
+        if pg_mode and self.coll and flat.params.is_cuda and not self.nccl:
+            # the torch.distributed A/B path on the GPU needs ProcessGroupNCCL: the trial's process group is the gloo
+            # rendezvous, so build an nccl group over the same ranks (collective: every rank constructs FlatDDP here)
+            ranks = dist.get_process_group_ranks(process_group) if process_group is not None else None
+            self.pg = process_group = dist.new_group(ranks=ranks, backend="nccl")
+            self.nccl = True
         self.overlap = (overlap and self.coll) or optimizer is not None
         self.launched = 0
         # Every collective of the trial -- bucket all-reduces, ZeRO-1's reduce-scatter / all-gather, the parameter
@@ -158,9 +170,10 @@ class FlatDDP:
         # shim on the CPU, so the CPU tests execute this same path).  GPU bucket all-reduces run on a stream of their
         # own, event-ordered after the bucket's gradient: through ProcessGroupNCCL's work objects the GPT-2 step lost
         # 35 % at world 1 to a host / dispatch stall, this way 3.4 % (profiles/r4_gpt2_world1_collectives.md).
-        # PLX_DDP_COMM=pg: torch.distributed's own collectives over the process group (A/B).
+        # PLX_DDP_COMM=pg: torch.distributed's own collectives (ProcessGroupNCCL on the GPU, built above; gloo on the
+        # CPU) -- the reference path the CPU tests compare the communicator branch with (A/B).
         self._comm = self._comm_stream = None
-        if self.coll and os.environ.get("PLX_DDP_COMM", "comm") != "pg":
+        if self.coll and not pg_mode:
             from polyaxon_amd.parallel import comm as _comm
 
             self._comm = _comm.acquire(process_group, flat.device)

@@ -26,18 +26,45 @@ class RcclError(RuntimeError):
     pass
 
 
+TIMEOUT = 1000  # plx_rccl status: the watchdog aborted the communicator on its deadline (csrc/rccl_comm.cpp)
+
+
+def _env_seconds(name: str, default: float) -> float:
+    try:
+        return float(os.environ.get(name, "") or default)
+    except ValueError:
+        return default
+
+
 class RcclComm:
+    """One RCCL communicator, created non-blocking and watched (csrc/rccl_comm.cpp).
+
+    ``init_timeout_s``: every rank must join within it, else RcclError (default PLX_RCCL_INIT_TIMEOUT_S, else
+    PLX_COLLECTIVE_TIMEOUT_S, else 600 s).  ``timeout_s``: a collective not complete that long after it was enqueued
+    makes the process's watchdog thread abort the communicator -- RCCL's kernels in flight exit, and every later call
+    raises RcclError, so the rank fails and polyflow tears its gang down (default PLX_COLLECTIVE_TIMEOUT_S, which
+    polyflow sets for multi-rank trials, polyflow/env.py; 0 = no deadline, asynchronous RCCL errors still abort).
+    Reference behaviour: the reference stops every job of an experiment when one fails
+    (/root/reference/polyaxon/signals/experiments.py:252-281)."""
+
     synchronous = False  # collectives are enqueued on the current HIP stream
     # RCCL's AVG (a pre-multiplied sum) vs SUM + the caller's 1/W scale (PLX_DDP_AVG=0, A/B)
     native_avg = os.environ.get("PLX_DDP_AVG", "1") != "0"
 
-    def __init__(self, unique_id: bytes, nranks: int, rank: int, device: int):
+    def __init__(self, unique_id: bytes, nranks: int, rank: int, device: int, timeout_s: float = None,
+                 init_timeout_s: float = None):
         self.lib = _native.lib("plx_rccl")
+        coll = _env_seconds("PLX_COLLECTIVE_TIMEOUT_S", 0.0) if timeout_s is None else float(timeout_s)
+        if init_timeout_s is None:
+            init_timeout_s = _env_seconds("PLX_RCCL_INIT_TIMEOUT_S", coll if coll > 0 else 600.0)
         err = ctypes.c_int(0)
-        self.h = self.lib.plx_rccl_init(unique_id, nranks, rank, device, ctypes.byref(err))
+        self.h = self.lib.plx_rccl_init(unique_id, nranks, rank, device, int(init_timeout_s * 1000), int(coll * 1000),
+                                        ctypes.byref(err))
         if not self.h:
-            raise RcclError(f"ncclCommInitRank failed: {err.value}")
+            raise RcclError(f"RCCL communicator init (rank {rank} of {nranks}) failed: "
+                            f"{self.lib.plx_rccl_error(err.value).decode()}")
         self.nranks, self.rank, self.device = nranks, rank, device
+        self.timeout_s = coll
 
     @staticmethod
     def new_unique_id() -> bytes:
@@ -68,6 +95,27 @@ class RcclComm:
             raise RcclError(f"{what}: communicator is closed")
         if rc != 0:
             raise RcclError(f"{what}: {self.lib.plx_rccl_error(rc).decode()}")
+
+    def status(self) -> int:
+        """0 while healthy, else the error code that aborted the communicator (:data:`TIMEOUT`: the watchdog)."""
+        return int(self.lib.plx_rccl_status(self.h)) if self.h else 0
+
+    def check(self) -> None:
+        """Raise RcclError if the watchdog (or an asynchronous RCCL error) aborted the communicator."""
+        self._check(self.status(), "communicator")
+
+    def pending(self) -> int:
+        """Collectives enqueued and not yet seen complete by the watchdog."""
+        return int(self.lib.plx_rccl_pending(self.h)) if self.h else 0
+
+    def set_timeout(self, seconds: float) -> None:
+        self._check(self.lib.plx_rccl_set_timeout(self.h, int(seconds * 1000)), "set_timeout")
+        self.timeout_s = float(seconds)
+
+    def abort(self) -> None:
+        """Abort now (in-flight RCCL kernels exit; later calls raise)."""
+        if self.h:
+            self.lib.plx_rccl_abort(self.h)
 
     @staticmethod
     def _stream() -> int:

@@ -131,9 +131,12 @@ def trial_env(*, base_env: Optional[Dict[str, str]] = None, experiment: Dict[str
     hw_queue_env(env)
     n_ranks = sum(len(v) for v in cluster.values()) if cluster else 1
     if n_ranks > 1:
-        # RCCL watchdog: a rank that dies or hangs inside a collective tears the process group
-        # down after PLX_COLLECTIVE_TIMEOUT_S (parallel/ddp.init_from_env) instead of blocking its peers forever;
-        # the scheduler then sees the failure and tears down the surviving ranks.
+        # Collective deadlines, one variable for both planes:
+        # * the framework RCCL communicator's watchdog (csrc/rccl_comm.cpp) aborts it when a peer does not join within
+        #   PLX_COLLECTIVE_TIMEOUT_S or a collective stays incomplete that long: the rank raises RcclError and exits;
+        # * the gloo rendezvous group carries the same timeout (parallel/ddp.init_from_env);
+        # * a user program's own ProcessGroupNCCL gets torch's async error handling.
+        # The scheduler sees the failed rank and tears down the surviving ones.
         env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         env.setdefault("PLX_COLLECTIVE_TIMEOUT_S", "600")
         # RCCL channel count of the DP ranks' communicators (several channels spread a ring

@@ -76,10 +76,16 @@ class ResidentTrialExecutor:
         # class_xent: no fp32 logits copy, log-softmax or NLL kernels between the head GEMM and its backward, where the
         # host launching them was the bottleneck of the forward -> backward hand-off).  PLX_CLASS_XENT=0: F.cross_entropy
         default_loss = loss_fn is None
+        # labels guaranteed inside [0, classes): the executor's own synthetic source with no more classes than the
+        # head has outputs -- the fused kernels then skip F.cross_entropy's valid-row count
+        fc = getattr(model, "fc", None)
+        self._labels_in_range = (hasattr(batch, "next") and isinstance(getattr(batch, "classes", None), int)
+                                 and isinstance(fc, nn.Linear) and batch.classes <= fc.out_features)
         if loss_fn is None and os.environ.get("PLX_CLASS_XENT", "1") != "0":
             from polyaxon_amd.ops.lm import class_xent
 
-            loss_fn = class_xent
+            in_range = self._labels_in_range
+            loss_fn = lambda out, y: class_xent(out, y, in_range=in_range)  # noqa: E731
         self.loss_fn = loss_fn or (lambda out, y: F.cross_entropy(out.float(), y))
         # Fused classifier head (ops/head.py): a model with forward_features / forward_head and an nn.Linear fc, the
         # default cross entropy and bf16 autocast on the GPU run the head's forward and backward in the forward
@@ -128,13 +134,13 @@ class ResidentTrialExecutor:
             self.wcache = cache if len(cache) else None
         self.model.train()
 
-    def enable_dp(self, bucket_mb="auto") -> None:
-        """Data parallel over the default process group (a resident DP gang, polyflow/resident.py): bucketed,
-        backward-overlapped gradient all-reduce (parallel/ddp.py FlatDDP) before every optimizer step; the DP step
-        runs eagerly."""
+    def enable_dp(self, bucket_mb="auto", process_group=None) -> None:
+        """Data parallel over ``process_group`` (default: the default group; a resident DP gang, polyflow/resident.py):
+        bucketed, backward-overlapped gradient all-reduce (parallel/ddp.py FlatDDP) before every optimizer step; the
+        DP step runs eagerly."""
         from polyaxon_amd.parallel.ddp import FlatDDP
 
-        self.ddp = FlatDDP(self.flat, bucket_mb=bucket_mb)
+        self.ddp = FlatDDP(self.flat, process_group=process_group, bucket_mb=bucket_mb)
         self.use_graph = False
         self._prefetch = False
 
@@ -180,12 +186,14 @@ class ResidentTrialExecutor:
         if self.wcache is not None:
             self.wcache.activate()
         try:
-            if self._fused_head:
+            # not under DP: the fused head writes fc's gradient slots itself, so FlatDDP's post-accumulate hooks for fc
+            # would never fire and its bucket would only launch in finish(), without overlap
+            if self._fused_head and self.ddp is None:
                 from polyaxon_amd.ops import head
 
                 with torch.autocast("cuda", dtype=self.amp_dtype):
                     feats = self.model.forward_features(self.x)
-                if head.supported(feats, self.model.fc, self.y):
+                if head.supported(feats, self.model.fc, self.y, self._labels_in_range):
                     loss, dfeat = head.classifier_head_step(feats.detach(), self.model.fc, self.y, self._ones)
                     feats.backward(dfeat)
                     self.fused_head_steps += 1

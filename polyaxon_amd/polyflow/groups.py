@@ -439,14 +439,15 @@ class ResidentDriver(GroupDriver):
             self._arm_dispatch()
             return
         self._waiting_since = None
-        alive = {w.wid for w in pool.workers_for(self.program_key)}
+        world = pool.dp_world(self.gpu)
+        alive = {w.wid for w in pool.workers_for(self.program_key) if len(w.devices) == world}
         self.used_workers &= alive  # dead executors never count against the group's concurrency
         while self.pending_keys:
             key = self.pending_keys[0]
             br = self.brackets[key]
             msg = self.unit_message(key, br)
             allowed = sorted(self.used_workers) if len(self.used_workers) >= self.concurrency else None
-            w = pool.assign(self, msg, br["units"], allowed=allowed, key=self.program_key)
+            w = pool.assign(self, msg, br["units"], allowed=allowed, key=self.program_key, world=world)
             if w is None:
                 break
             self.used_workers.add(w.wid)

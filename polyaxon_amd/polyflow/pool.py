@@ -86,10 +86,18 @@ class ResidentPool:
                  "pid": w.proc.pid if w.proc else w.info.get("pid")} for w in self.workers.values()]
 
     # ------------------------------------------------------------------ creation
+    @staticmethod
+    def dp_world(gpu: float) -> int:
+        """Devices of one executor for a ``resources.gpu`` request: a DP gang for an integer > 1, else one."""
+        return int(round(gpu)) if gpu > 1.0 + 1e-9 else 1
+
     def ensure(self, key: str, program: str, params: Dict[str, Any], want: int, gpu: float = 1.0,
                hbm_gb: float = 0.0, max_active: int = 8) -> List[WorkerHandle]:
-        """Make sure up to ``want`` workers run ``program`` (spawning on free devices); returns the live ones."""
-        have = self.workers_for(key)
+        """Make sure up to ``want`` workers run ``program`` on ``dp_world(gpu)`` devices each (spawning on free
+        devices); returns the live ones.  An executor of another DP world never serves the request (a DP=2 trial
+        must not silently train on one device)."""
+        world = self.dp_world(gpu)
+        have = [w for w in self.workers_for(key) if len(w.devices) == world]
         self.placement_error = None
         while len(have) < want:
             h = self._spawn(key, program, params, gpu, hbm_gb, max_active)
@@ -254,18 +262,20 @@ class ResidentPool:
 
         threading.Thread(target=reader, name=f"resident-peer-{h.wid}", daemon=True).start()
 
-    def attach(self, chan: Channel, device: int, program: str, params: Optional[Dict[str, Any]] = None,
+    def attach(self, chan: Channel, device, program: str, params: Optional[Dict[str, Any]] = None,
                max_active: int = 8, gpu: float = 1.0) -> WorkerHandle:
         """Register an already running worker (it was built by another launcher, e.g. a bench.py rank) that owns
-        ``device``.  Runs on the scheduler thread."""
+        ``device`` -- one index, or the list of a DP gang's devices (its leader attaches; the other ranks follow
+        the leader's control stream).  Runs on the scheduler thread."""
         from polyaxon_amd.polyflow.programs import program_key
 
+        devices = [int(d) for d in device] if isinstance(device, (list, tuple)) else [int(device)]
         wid = self._next
         self._next += 1
         owner = f"resident:{wid}"
-        if self.flow.alloc.allocate_on(owner, [device], gpu) is None:
-            raise RuntimeError(f"device {device} is not free for a resident executor")
-        h = WorkerHandle(wid, program_key(program, params), program, dict(params or {}), [device], chan,
+        if self.flow.alloc.allocate_on(owner, devices, gpu) is None:
+            raise RuntimeError(f"devices {devices} are not free for a resident executor")
+        h = WorkerHandle(wid, program_key(program, params), program, dict(params or {}), devices, chan,
                          external=True)
         self.workers[wid] = h
         chan.send({"op": "init", "program": program, "params": params or {}, "max_active": max_active})
@@ -274,9 +284,10 @@ class ResidentPool:
 
     # ------------------------------------------------------------------ dispatch
     def assign(self, driver, msg: Dict[str, Any], units: float,
-               allowed: Optional[List[int]] = None, key: Optional[str] = None) -> Optional[WorkerHandle]:
+               allowed: Optional[List[int]] = None, key: Optional[str] = None,
+               world: Optional[int] = None) -> Optional[WorkerHandle]:
         cands = [w for w in self.workers.values() if w.alive and (key is None or w.key == key)
-                 and (allowed is None or w.wid in allowed)]
+                 and (allowed is None or w.wid in allowed) and (world is None or len(w.devices) == world)]
         if not cands:
             return None
         w = min(cands, key=lambda h: (h.load, h.wid))

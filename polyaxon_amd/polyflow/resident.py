@@ -242,16 +242,17 @@ class ResidentWorker:
         self._shutdown: Optional[str] = None
         self.gang: Optional[_GangGroup] = None
 
-    def join_gang(self, rank: int, world: int) -> None:
+    def join_gang(self, rank: int, world: int, group=None) -> None:
         """Become rank ``rank`` of a DP gang (before ``build``): the program trains with FlatDDP over the gang,
-        each rank on its own slice of the data stream."""
+        each rank on its own slice of the data stream.  ``group``: an existing process (sub)group of the ``world``
+        ranks (bench.py's gangs inside its own world group); None: the gang's own rendezvous from the pool's env."""
         import torch
 
         if self.device is None:
             self.device = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
         if torch.device(self.device).type == "cuda":
             torch.cuda.set_device(self.device)
-        self.gang = _GangGroup(rank, world, self.device)
+        self.gang = _GangGroup(rank, world, self.device, group=group)
 
     def close_gang(self) -> None:
         """Release the gang's framework communicator (the executor's FlatDDP hold and the metric mean's) and the
@@ -284,7 +285,7 @@ class ResidentWorker:
             params["graph"] = False  # the DP step runs eagerly (its collectives ride RCCL's own streams)
         self.program = build_program(self.program_name, params, self.device)
         if self.gang is not None:
-            self.program.executor.enable_dp()
+            self.program.executor.enable_dp(process_group=self.gang.group)
         self.program.warm()
         ex = self.program.executor
         self.metrics = BracketMetrics(self.max_active, 32, ex.device)
@@ -346,7 +347,10 @@ class ResidentWorker:
         elif op == "ping":
             chan.send({"ev": "pong", "stats": dict(self.stats)})
         elif op == "bo_suggest":
-            chan.send(self._bo_suggest(msg))
+            # a DP gang's followers see every control message too, but only the leader's reply reaches the scheduler:
+            # only rank 0 fits the GP and searches the acquisition
+            if self.gang is None or self.gang.rank == 0:
+                chan.send(self._bo_suggest(msg))
         elif op == "init":
             if msg.get("program") != self.program_name:
                 chan.send({"ev": "error", "fatal": True,
@@ -791,7 +795,7 @@ class _GangGroup:
     order -- and ships the RCCL unique id.  Every device collective (the executor's gradient buckets, the metric-table
     mean before each rung decision) runs on the process's one framework communicator (parallel/comm.py)."""
 
-    def __init__(self, rank: int, world: int, device):
+    def __init__(self, rank: int, world: int, device, group=None):
         import datetime
 
         import torch
@@ -799,6 +803,15 @@ class _GangGroup:
 
         self.rank, self.world = rank, world
         self.device = torch.device(device)
+        self.comm = None  # acquired on first use (collective: every rank reaches it at the same program point)
+        if group is not None:  # a subgroup of an existing world (bench.py): its rank 0 leads, as a GLOBAL rank
+            from polyaxon_amd.parallel.comm import group_rank0
+
+            if dist.get_world_size(group) != world or dist.get_rank(group) != rank:
+                raise ValueError("gang group does not match (rank, world)")
+            self.group, self.src, self.owns = group, group_rank0(group), False
+            return
+        self.group, self.src, self.owns = None, 0, True
         long = datetime.timedelta(days=7)  # an idle executor blocks in the control broadcast between groups
         # rank 0 serves the store on the pool's already-listening socket (polyflow/pool.py _spawn_gang); every rank
         # builds its store explicitly so all of them see the same (unprefixed) key space
@@ -807,13 +820,12 @@ class _GangGroup:
         store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]), world,
                               rank == 0, timeout=long, **kw)
         dist.init_process_group("gloo", store=store, rank=rank, world_size=world, timeout=long)
-        self.comm = None  # acquired on first use (collective: every rank reaches it at the same program point)
 
     def broadcast(self, obj):
         import torch.distributed as dist
 
         box = [obj]
-        dist.broadcast_object_list(box, src=0)
+        dist.broadcast_object_list(box, src=self.src, group=self.group)
         return box[0]
 
     def mean_(self, t) -> None:
@@ -821,7 +833,7 @@ class _GangGroup:
         from polyaxon_amd.parallel import comm as _comm
 
         if self.comm is None:
-            self.comm = _comm.acquire(None, t.device)
+            self.comm = _comm.acquire(self.group, t.device)
         if self.comm.native_avg:
             self.comm.all_reduce(t, op="avg")
         else:
@@ -835,7 +847,7 @@ class _GangGroup:
         if self.comm is not None:
             _comm.release(self.comm)
             self.comm = None
-        if dist.is_initialized():
+        if self.owns and dist.is_initialized():
             dist.destroy_process_group()
 
 

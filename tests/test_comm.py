@@ -178,3 +178,58 @@ def test_auto_buckets_are_planned_from_a_measured_link_and_agree_across_ranks():
     assert a["plan"]["source"] == "measured", a["plan"]
     assert a["plan"] == b["plan"] and a["buckets"] == b["buckets"]
     assert a["plan"]["busbw_GBps"] > 0 and a["plan"]["bucket_bytes"] >= 4 * 2 ** 20
+
+
+def _missing_peer_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), PLX_COLLECTIVE_TIMEOUT_S="3")
+    import time
+
+    import torch.distributed as dist
+
+    from polyaxon_amd.parallel import comm
+    from polyaxon_amd.parallel.ddp import init_from_env
+
+    init_from_env("gloo")
+    c = comm.acquire(None, torch.device("cpu"))
+    out = {"rank": rank}
+    if rank == 0:  # rank 1 never joins the collective: rank 0 must fail within the deadline, not hang
+        t0 = time.monotonic()
+        try:
+            c.all_reduce(torch.ones(4), op="sum")
+            out["raised"] = False
+        except RuntimeError as e:  # gloo's timeout surfaces as a RuntimeError (DistBackendError)
+            out["raised"], out["msg"] = True, str(e)[:200]
+        out["elapsed"] = time.monotonic() - t0
+    else:
+        time.sleep(8)
+    q.put(out)
+    q.close()
+    q.join_thread()  # flush the result before skipping the broken group's teardown
+    os._exit(0)
+
+
+def test_gloo_shim_collective_with_a_missing_peer_fails_within_the_timeout():
+    """The CPU twin of the RCCL watchdog (csrc/rccl_comm.cpp): a DP rank whose peer stops issuing collectives gets an
+    error after PLX_COLLECTIVE_TIMEOUT_S (the rendezvous group's deadline, parallel/ddp.init_from_env) instead of
+    blocking forever; polyflow then tears the gang down."""
+    res = _run(_missing_peer_worker, 2, timeout=60)
+    r0 = res[0]
+    assert r0["raised"], r0
+    assert 2.0 <= r0["elapsed"] < 8.0, r0
+
+
+def test_init_from_env_keeps_an_explicit_gloo_backend_on_the_cpu(monkeypatch):
+    """an explicit gloo backend means the CPU even on a GPU host (no HIP initialisation, no device ordinal
+    taken from LOCAL_RANK); only nccl or an unnamed backend on a GPU host selects cuda:LOCAL_RANK."""
+    from polyaxon_amd.parallel import ddp
+
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    set_to = []
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: set_to.append(d))
+    assert ddp.init_from_env("gloo")["device"].type == "cpu"
+    assert set_to == []
+    assert ddp.init_from_env()["device"] == torch.device("cuda", 5)
+    assert ddp.init_from_env("nccl")["device"] == torch.device("cuda", 5)

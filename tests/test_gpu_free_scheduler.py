@@ -83,3 +83,51 @@ def test_device_detection_without_hip_matches_the_runtime():
     assert out.returncode == 0, out.stderr[-2000:]
     mine, hip = json.loads(out.stdout.strip().splitlines()[-1])
     assert mine == hip >= 1
+
+
+STATUS_API = r"""
+import json, os, sys
+from fastapi.testclient import TestClient
+from polyaxon_amd.api.server import create_app
+from polyaxon_amd.polyflow.scheduler import Polyflow
+from polyaxon_amd.polyflow.devices import Device, DeviceAllocator
+
+flow = Polyflow(sys.argv[1], allocator=DeviceAllocator([Device(0)]), reconcile_s=0).start()
+client = TestClient(create_app(flow, admin_token="t"))
+first = client.get("/_status").json()
+second = client.get("/_status").json()
+flow.shutdown()
+maps = open("/proc/self/maps").read()
+print(json.dumps({"first": first, "second": second["checks"]["rccl"], "hip_mapped": "libamdhip64" in maps,
+                  "torch_imported": "torch" in sys.modules}))
+"""
+
+
+def _status_api(tmp_path, env_extra):
+    env = dict(os.environ, PYTHONPATH=REPO, **env_extra)
+    out = subprocess.run([sys.executable, "-c", STATUS_API, str(tmp_path)], capture_output=True, text=True,
+                         timeout=240, env=env, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_status_endpoint_keeps_the_api_process_gpu_free(tmp_path):
+    """``/_status``'s RCCL check runs in a child process (obs/rccl_probe.py): the API process never imports torch
+    nor maps the HIP runtime, and a second poll is served from the check's cache.  On this CPU box the probe
+    reports "skipped" (no device), which counts as healthy."""
+    r = _status_api(tmp_path, {"OMP_NUM_THREADS": "2"})
+    rccl = r["first"]["checks"]["rccl"]
+    assert rccl["status"] == "ok" and rccl["cached"] is False, r
+    assert r["second"]["cached"] is True, r
+    assert not r["torch_imported"] and not r["hip_mapped"], r
+
+
+@pytest.mark.gpu
+def test_status_endpoint_runs_a_real_rccl_round_trip(tmp_path):
+    """On the GPU box the check is a real RCCL all-reduce on the framework communicator, in a child process: status
+    ok with a measured latency, and still no HIP runtime in the API process (reference
+    /root/reference/polyaxon/checks/worker.py:16-45)."""
+    r = _status_api(tmp_path, {})
+    rccl = r["first"]["checks"]["rccl"]
+    assert rccl["status"] == "ok" and not rccl.get("skipped") and rccl["all_reduce_us"] > 0, r
+    assert not r["torch_imported"] and not r["hip_mapped"], r

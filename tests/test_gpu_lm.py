@@ -168,6 +168,34 @@ def test_class_xent_matches_fp32(cuda, N, V):
     torch.testing.assert_close(g, gr, rtol=1e-2, atol=1e-2 * float(gr.abs().max()))
 
 
+@pytest.mark.parametrize("in_range", [False, True])
+def test_class_xent_ignored_and_out_of_range_labels(cuda, in_range):
+    """labels outside [0, V) (ignore_index -100, or V itself) are never read; they add no loss and no
+    gradient.  Default: the mean is over the valid rows as in F.cross_entropy(ignore_index=-100); ``in_range``
+    (caller-guaranteed labels) divides by every row -- checked here on all-valid labels."""
+    from polyaxon_amd.ops.lm import class_xent
+
+    N, V = 64, 1000
+    torch.manual_seed(3)
+    logits = (torch.randn(N, V, device=cuda) * 3).to(torch.bfloat16).requires_grad_()
+    labels = torch.randint(0, V, (N,), device=cuda)
+    if not in_range:
+        labels[::5] = -100
+        labels[3] = V  # out of range: treated as ignored (torch would raise)
+    loss = class_xent(logits, labels, in_range=in_range)
+    (loss * 0.9).backward()
+    ref_in = logits.detach().float().requires_grad_()
+    ref_labels = labels.clone()
+    ref_labels[ref_labels >= V] = -100
+    ref = F.cross_entropy(ref_in, ref_labels, ignore_index=-100)
+    (ref * 0.9).backward()
+    assert abs(float(loss) - float(ref)) < 1e-4 * max(1.0, abs(float(ref)))
+    g, gr = logits.grad.float(), ref_in.grad
+    torch.testing.assert_close(g, gr, rtol=1e-2, atol=1e-2 * float(gr.abs().max()))
+    if not in_range:
+        assert float(g[::5].abs().max()) == 0.0 and float(g[3].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("T,N", [(16384, 768), (16384, 3072), (1000, 2304), (37, 264), (1, 8)])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_bias_grad_colsum_matches_fp32(cuda, T, N, dtype):

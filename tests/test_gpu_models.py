@@ -221,10 +221,11 @@ def _head_grads(cuda, fused: bool, monkeypatch):
     monkeypatch.setenv("PLX_FUSED_HEAD", "1" if fused else "0")
     torch.manual_seed(0)
     model = resnet18ish(num_classes=1000)
-    g = torch.Generator(device=cuda).manual_seed(1)
-    x = torch.randn(16, 3, 64, 64, device=cuda, generator=g)
-    y = torch.randint(0, 1000, (16,), device=cuda, generator=g)
-    ex = ResidentTrialExecutor(model, (x, y), cuda, use_graph=False)
+    # the executor's own synthetic source: labels guaranteed in [0, 1000), which the fused head requires
+    from polyaxon_amd.ops.synth import SyntheticImages
+
+    src = SyntheticImages(16, 64, cuda, classes=1000, active_classes=100, seed=1)
+    ex = ResidentTrialExecutor(model, src, cuda, use_graph=False)
     ex.reset(seed=3)
     ex.opt.step_ = lambda: None  # keep this step's gradients in the flat buffer
     ex._train_step()

@@ -204,3 +204,68 @@ def test_zero1_on_rccl_backend_world1_matches_unsharded():
     assert res["losses_equal"] and res["master_equal"] and res["lp_equal"], res
     assert res["buckets"] > 1 and res["launched"] == 3 * res["buckets"]
     assert res["state"] == res["numel"]  # world 1: the slice is the whole bucket
+
+
+def test_rccl_init_with_a_peer_that_never_joins_fails_within_the_deadline():
+    """SURVEY.md §5.3 watchdog: a 2-rank communicator whose peer never calls init raises RcclError after the init
+    deadline (non-blocking ncclCommInitRankConfig polled, then ncclCommAbort) instead of blocking the rank forever."""
+    res = _run("""
+        import json, time, torch
+        from polyaxon_amd.parallel.rccl import RcclComm, RcclError
+        torch.cuda.set_device(0)
+        uid = RcclComm.new_unique_id()
+        t0 = time.monotonic()
+        out = {"raised": False}
+        try:
+            RcclComm(uid, 2, 0, 0, timeout_s=5, init_timeout_s=4)
+        except RcclError as e:
+            out = {"raised": True, "msg": str(e)}
+        out["elapsed"] = time.monotonic() - t0
+        print(json.dumps(out))
+    """, timeout=120)
+    assert res["raised"] and "timed out" in res["msg"], res
+    assert 3.5 <= res["elapsed"] < 40, res
+
+
+def test_rccl_watchdog_aborts_a_collective_that_does_not_complete():
+    """The progress half of the watchdog: an all-reduce queued behind a 3 s kernel is still incomplete after the
+    communicator's 1 s deadline, so the watchdog aborts the communicator; the stream still drains and the NEXT call
+    raises RcclError.  With no deadline hit, completed collectives are retired (pending drains to 0)."""
+    res = _run("""
+        import json, time, torch
+        from polyaxon_amd.parallel.rccl import RcclComm, RcclError, TIMEOUT
+        torch.cuda.set_device(0)
+        comm = RcclComm(RcclComm.new_unique_id(), 1, 0, 0, timeout_s=30)
+        x = torch.ones(1024, device="cuda")
+        for _ in range(8):
+            comm.all_reduce(x)
+        torch.cuda.synchronize()
+        t0 = time.monotonic()
+        while comm.pending() and time.monotonic() - t0 < 5:
+            time.sleep(0.02)
+        out = {"drained": comm.pending(), "ok_status": comm.status(), "x": float(x[0])}
+        comm.set_timeout(1.0)
+        # ~3 s of GPU spin ahead of the collective (clock cycles at ~100 MHz for s_memrealtime-based sleep is not
+        # portable: calibrate by timing a short sleep first)
+        torch.cuda._sleep(1000000)
+        torch.cuda.synchronize()
+        t = time.monotonic()
+        torch.cuda._sleep(1000000)
+        torch.cuda.synchronize()
+        per = max(time.monotonic() - t, 1e-4) / 1000000
+        torch.cuda._sleep(int(3.0 / per))
+        comm.all_reduce(x)
+        torch.cuda.synchronize()
+        out["spin_s"] = time.monotonic() - t
+        out["status"] = comm.status()
+        try:
+            comm.all_reduce(x)
+            out["raised"] = False
+        except RcclError as e:
+            out["raised"], out["msg"] = True, str(e)
+        out["timeout_code"] = TIMEOUT
+        print(json.dumps(out))
+    """, timeout=120)
+    assert res["drained"] == 0 and res["ok_status"] == 0 and res["x"] == 1.0, res
+    assert res["spin_s"] > 1.5, res
+    assert res["status"] == res["timeout_code"] and res["raised"] and "timed out" in res["msg"], res

@@ -691,3 +691,24 @@ def test_asha_drops_snapshots_of_configs_that_can_no_longer_be_promoted():
     sh2.snap_rung[0] = 0
     w._drop_hopeless_snapshots(sh2)
     assert sh2.snap_rung == {0: 0}
+
+
+def test_bench_cpu_config4_trials_are_dp2_gangs():
+    """BASELINE config 4 ("each trial DP=2 on RCCL over xGMI") through bench.py: ``--config gpt2_bo --gpus 4
+    --trial-gpus 2`` builds two resident DP gangs of two ranks; every trial's job holds 2 devices, every rank launched
+    FlatDDP bucket collectives on the framework communicator (the gloo shim here, RCCL on the GPU), the two ranks of
+    a gang end with identical weights (the gangs differ), and the scheduler process stays device-free."""
+    res = _bench("--config", "gpt2_bo", "--gpus", "4", "--trial-gpus", "2", "--steps", "1", "--warmup", "0",
+                 threads="2")
+    assert res["config"]["per_trial_world"] == 2 and "dp2" in res["config"]["parallelism"]
+    assert res["trials"] == res["trials_succeeded"] > 0
+    assert res["trial_devices"] == {"2": res["trials"]}, res["trial_devices"]
+    ranks = res["per_rank"]
+    assert [r["gang"] for r in ranks] == [0, 0, 1, 1]
+    assert all(r["ddp_collectives"] > 0 and r["ddp_on_framework_comm"] for r in ranks), ranks
+    assert ranks[0]["weights_fingerprint"] == ranks[1]["weights_fingerprint"]
+    assert ranks[2]["weights_fingerprint"] == ranks[3]["weights_fingerprint"]
+    assert ranks[0]["weights_fingerprint"] != ranks[2]["weights_fingerprint"]
+    assert len(res["executors"]) == 2 and all(len(e["devices"]) == 2 for e in res["executors"])
+    fp = res["control_device_footprint"]
+    assert not fp["torch_imported"] and not fp["hip_mapped"] and not fp["kfd_open"], fp
