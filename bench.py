@@ -458,9 +458,8 @@ def _pin_cpus(local_rank: int, world: int) -> list:
     """Bind this rank to the CPUs local to its GPU (NUMA node of the PCIe root) before torch starts its threads."""
     from polyaxon_amd.polyflow.devices import device_cpus
 
-    mode = os.environ.get("PLX_BENCH_PIN", "1")  # A/B knob: 0 never, force = KFD index = local rank (round-3 default)
-    phys = local_rank if mode == "force" else _physical_gpu(local_rank, world)
-    if phys is None or mode == "0":
+    phys = _physical_gpu(local_rank, world)
+    if phys is None:
         return []
     cpus = device_cpus(phys)
     if cpus:
@@ -515,7 +514,7 @@ def main() -> int:
     if world > 1:
         # The process group is the gloo rendezvous: the ranks' control traffic (control address, barriers around the
         # timed region) and the RCCL unique id; the per-rank gather runs on the framework RCCL communicator
-        # (parallel/comm.py), alive for the whole run by default (PLX_BENCH_RCCL below).
+        # (parallel/comm.py), alive for the whole run (below).
         dist.init_process_group("gloo")
         addr = [ctl_addr]
         dist.broadcast_object_list(addr, src=0)
@@ -539,13 +538,11 @@ def main() -> int:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
-    # PLX_BENCH_RCCL: "early" (default) -- the framework's RCCL communicator is alive for the whole run, as in a DP
-    # trial (round 4: with 4 hardware queues its streams pushed the side stream onto the compute stream's queue,
-    # -17 %, profiles/r4_rccl_slowdown.md; the side stream now has a queue of its own, profiles/r5_hw_queues.md);
-    # "late" / "1" -- created after the timed region; "0" -- gloo only
-    rccl_mode = os.environ.get("PLX_BENCH_RCCL", "early")
+    # The framework's RCCL communicator is alive for the whole run, as in a DP trial (round 4: with 4 hardware queues
+    # its streams pushed the side stream onto the compute stream's queue, -17 %, profiles/r4_rccl_slowdown.md; the
+    # side stream now has a queue of its own, profiles/r5_hw_queues.md)
     early_comm = None
-    if dev.type == "cuda" and rccl_mode == "early":
+    if dev.type == "cuda":
         from polyaxon_amd.parallel.rccl import RcclComm
 
         try:
@@ -604,7 +601,7 @@ def main() -> int:
     # framework-owned collective (csrc/rccl_comm.cpp) for the per-rank gather on the GPU path (the early communicator,
     # or one created now).
     comm = early_comm
-    if comm is None and dev.type == "cuda" and rccl_mode != "0":
+    if comm is None and dev.type == "cuda":
         from polyaxon_amd.parallel.rccl import RcclComm
 
         try:

@@ -319,7 +319,7 @@ __device__ __forceinline__ bool reduce_l2_last(const float* __restrict__ part, i
 // 1024 threads: 16 row groups make both the level-1 rows (4 per thread) and the S level-2 rows (<= 8 per thread
 // up to S = 128) a single L2 round trip each; with 256 threads they were 2 and up to 4 dependent trips
 constexpr int kFinNT = 1024;
-static int g_fin_nt = kFinNT;  // plx_set_bn_fin_threads(256) restores the 256-thread variant (A/B)
+// (round 6 removed the 256-thread finalize variant: -0.5 %, profiles/r5_knob_recheck_ab.jsonl)
 template <int NT>
 __global__ __launch_bounds__(NT) void bn_fwd_reduce_finalize_kernel(const float* __restrict__ part, int nblk, float* l2,
                                                                     int S, unsigned* cnt, FwdFin f) {
@@ -657,16 +657,14 @@ inline void reduce_finalize_fwd(hipStream_t stream, const float* part, int nblk,
                                 const FwdFin& f) {
   const int C = f.C, S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
   if (cnt != nullptr) {
-    auto k = g_fin_nt == 256 ? bn_fwd_reduce_finalize_kernel<256> : bn_fwd_reduce_finalize_kernel<kFinNT>;
-    hipLaunchKernelGGL(k, dim3((C + 63) / 64, S), dim3(g_fin_nt == 256 ? 256 : kFinNT), 0, stream, part, nblk, l2, S,
+    hipLaunchKernelGGL(bn_fwd_reduce_finalize_kernel<kFinNT>, dim3((C + 63) / 64, S), dim3(kFinNT), 0, stream, part, nblk, l2, S,
                        cnt, f);
     return;
   }
-  const int nt = g_fin_nt == 256 ? 256 : kFinNT;
-  hipLaunchKernelGGL(nt == 256 ? bn_partial_reduce_kernel<256> : bn_partial_reduce_kernel<kFinNT>,
-                     dim3((C + 63) / 64, S, 2), dim3(nt), 0, stream, part, nblk, C, l2, S);
-  hipLaunchKernelGGL(nt == 256 ? bn_fwd_finalize_kernel<256> : bn_fwd_finalize_kernel<kFinNT>, dim3((C + 63) / 64),
-                     dim3(nt), 0, stream, l2, l2 + (int64_t)S * C, S,
+  hipLaunchKernelGGL(bn_partial_reduce_kernel<kFinNT>,
+                     dim3((C + 63) / 64, S, 2), dim3(kFinNT), 0, stream, part, nblk, C, l2, S);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel<kFinNT>, dim3((C + 63) / 64),
+                     dim3(kFinNT), 0, stream, l2, l2 + (int64_t)S * C, S,
                      f.x_row0, C, f.M, f.gamma, f.beta, f.eps, f.momentum, f.running_mean, f.running_var, f.save_mean,
                      f.save_invstd, f.scale, f.bias);
 }
@@ -675,16 +673,14 @@ inline void reduce_finalize_bwd(hipStream_t stream, const float* part, int nblk,
                                 const BwdFin& f) {
   const int C = f.C, S = (nblk + kRowsPerSplit - 1) / kRowsPerSplit;
   if (cnt != nullptr) {
-    auto k = g_fin_nt == 256 ? bn_bwd_reduce_finalize_kernel<256> : bn_bwd_reduce_finalize_kernel<kFinNT>;
-    hipLaunchKernelGGL(k, dim3((C + 63) / 64, S), dim3(g_fin_nt == 256 ? 256 : kFinNT), 0, stream, part, nblk, l2, S,
+    hipLaunchKernelGGL(bn_bwd_reduce_finalize_kernel<kFinNT>, dim3((C + 63) / 64, S), dim3(kFinNT), 0, stream, part, nblk, l2, S,
                        cnt, f);
     return;
   }
-  const int nt = g_fin_nt == 256 ? 256 : kFinNT;
-  hipLaunchKernelGGL(nt == 256 ? bn_partial_reduce_kernel<256> : bn_partial_reduce_kernel<kFinNT>,
-                     dim3((C + 63) / 64, S, 2), dim3(nt), 0, stream, part, nblk, C, l2, S);
-  hipLaunchKernelGGL(nt == 256 ? bn_bwd_finalize_kernel<256> : bn_bwd_finalize_kernel<kFinNT>, dim3((C + 63) / 64),
-                     dim3(nt), 0, stream, l2, l2 + (int64_t)S * C, S, C,
+  hipLaunchKernelGGL(bn_partial_reduce_kernel<kFinNT>,
+                     dim3((C + 63) / 64, S, 2), dim3(kFinNT), 0, stream, part, nblk, C, l2, S);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<kFinNT>, dim3((C + 63) / 64),
+                     dim3(kFinNT), 0, stream, l2, l2 + (int64_t)S * C, S, C,
                      f.M, f.gamma, f.mean, f.invstd, f.dgamma, f.dbeta, f.coef, f.accumulate);
 }
 
@@ -893,8 +889,8 @@ __global__ __launch_bounds__(256) void stem_pool_bn_bwd_kernel(const bf16x8* __r
 }
 
 // over quad rows: pass 1 (partials) a few per block (rows_y <= g_stem_bwd_cap bounds the level-1 partials: 4096 rows
-// ~4 MB at the stem's shape), pass 2 (dx) one per block.  A/B knob plx_set_stem_bwd_cap.
-int g_stem_bwd_cap = 4096;
+// ~4 MB at the stem's shape), pass 2 (dx) one per block.
+constexpr int g_stem_bwd_cap = 4096;
 
 inline dim3 stem_bwd_grid(int N, int H, int W, int G, bool dx) {
   const int rows = N * ((H + 1) / 2), cap = dx ? 65535 : g_stem_bwd_cap;
@@ -1046,8 +1042,6 @@ PLX_API int plx_stem_bn_pool_forward(const void* x, void* y, void* idx, int N, i
 }
 
 // A/B knob: quad rows of the stem backward's partials pass (1 .. 65535; set before sizing the workspace)
-PLX_API void plx_set_stem_bwd_cap(int cap) { g_stem_bwd_cap = cap < 1 ? 1 : (cap > 65535 ? 65535 : cap); }
-PLX_API void plx_set_bn_fin_threads(int n) { g_fin_nt = n == 256 ? 256 : kFinNT; }
 
 // floats of workspace plx_stem_bn_pool_backward needs: level-1 [2][nblk][C] + level-2 [2][S][C]
 PLX_API int64_t plx_stem_bn_pool_bwd_workspace(int N, int H, int W, int C) {

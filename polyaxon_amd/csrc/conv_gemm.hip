@@ -45,8 +45,6 @@ struct ConvGeom {
     // per-tap byte offsets for the NT GEMM's staging (filled by finish_geom): A row shift (offh*W + offw)*C*2
     // and B column start btap*C*2 -- dword arrays so a uniform tap index reads them with scalar loads
     int tap_a[9], tap_b[9];
-    // halo mode (stride-1 3x3 on the same grid): flattened pixel shift of tap t, offh[t] * W + offw[t]
-    int tap_shift[9];
     // x / Wr and q / Hr as __umulhi(x, m): m = floor(2^32 / d) + 1 is exact while x * d < 2^32, which holds for
     // pixel indices (< 2^24) and row-grid sides (<= 255); m = 0 marks d == 1
     uint32_t mWr, mHr;
@@ -77,7 +75,6 @@ inline ConvGeom finish_geom(ConvGeom g) {
     for (int t = 0; t < 9; ++t) {
         g.tap_a[t] = t < g.ntaps ? (g.offh[t] * g.W + g.offw[t]) * g.C * 2 : 0;
         g.tap_b[t] = t < g.ntaps ? g.btap[t] * g.C * 2 : 0;
-        g.tap_shift[t] = t < g.ntaps ? g.offh[t] * g.W + g.offw[t] : 0;
         if (t >= g.ntaps) continue;
         int i = 0, j = 0;
         while (i < g.nh && g.hv[i] != g.offh[t]) ++i;
@@ -181,12 +178,10 @@ __device__ __forceinline__ int nt_swz(int row) { return (row >> 1) & 7; }
 // and 4 blocks per CU, whose interleaving hides the staging instead (MINB = blocks per CU the registers allow)
 // BWD: the data-gradient epilogue (D add, ReLU-masked D, BatchNorm-backward partials); !BWD: the forward one (channel
 // stats).  Compile-time so each kernel only holds the epilogue registers it uses.
-// MODE: 0 dense rows, 1 implicit-GEMM convolution (ConvGeom gather), 2 the ResNet stem (see plx_stem_conv_fwd),
-// 3 halo convolution: a stride-1 3x3 convolution on the same row grid whose input rows are staged ONCE per 64-channel
-// chunk as a halo (the block's BM output pixels +- (W + 1) flattened pixels) and read by all 9 taps from LDS at a
-// per-tap row shift; only the weights are staged per tap.  Mode 1 re-stages the gathered A rows for every tap: 9x the
-// input bytes through the per-CU LDS-DMA path, which bounds those layers (~52 GB/s per CU, 34 % of MFMA peak).
-// (Round 5 removed the 8-wave 3-stage ring variant (NBUF 3) and the 4-5 stage software pipeline (NBUF 4-5): both
+// MODE: 0 dense rows, 1 implicit-GEMM convolution (ConvGeom gather), 2 the ResNet stem (see plx_stem_conv_fwd).
+// (Round 6 removed the halo mode (3: input rows staged once per channel chunk for all 9 taps; 0.99-1.17x the gather
+// mode's time, profiles/r3_negative_results.md) and the BatchNorm-apply prologue prototype (4: -159 us per step,
+// profiles/r5_bn_fusion_bound.md).  Round 5 removed the 8-wave 3-stage ring variant (NBUF 3) and the 4-5 stage software pipeline (NBUF 4-5): both
 // measured slower in the training step than these lock-step kernels, profiles/r4_conv3x3_scratch_fix_ring_ab.jsonl,
 // r4_conv3x3_swp_ab.jsonl, r4_bench_swp4_conv.json.)
 template <int BM, int BN, int WGM, int WGN, int MODE, int MINB = 2, int NBUF = 2, bool BWD = false, int NTH = NTHREADS>
@@ -195,10 +190,8 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                int M, int N, int K, int lda, int ldb, int ldc, const __bf16* __restrict__ zero,
                float* __restrict__ stats, ConvGeom geo, const __bf16* __restrict__ D, int ldd, BnBwd bnr,
                const uint8_t* __restrict__ dmask) {
-    // MODE 4: dense rows whose A operand is a BatchNorm output not yet applied: every A fragment becomes
-    // relu(a * scale[k] + bias[k]) between the LDS read and the MFMA (scale / bias = bnr.mean / bnr.invstd in this
-    // forward-only mode).  Prototype of the BN-apply prologue fusion (plx_gemm_nt_prologue).
-    constexpr bool CONV = MODE == 1 || MODE == 3, STEM = MODE == 2, HALO = MODE == 3, PRO = MODE == 4;
+    constexpr bool CONV = MODE == 1, STEM = MODE == 2;
+    static_assert(MODE >= 0 && MODE <= 2, "dense, gather or stem");
     constexpr int NW = NTH / 64;                           // waves
     static_assert(WGM * WGN == NW, "one wave per wave tile");
     static_assert(NTH == 256 && NBUF >= 1 && NBUF <= 2, "4-wave kernels, one or two K stages");
@@ -224,7 +217,7 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
     int a_off[AI];                                          // byte offsets
     uint32_t a_ok[AI];
 #pragma unroll
-    for (int i = 0; i < (HALO ? 0 : AI); ++i) {
+    for (int i = 0; i < AI; ++i) {
         const int row = (i * NW + wave) * 8 + (lane >> 3);
         const int lc = (lane & 7) ^ nt_swz(row);
         const int gm = m0 + row;
@@ -310,89 +303,6 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         for (int b = 0; b < RM; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const int fr = lane & 15, fq = lane >> 4;
-    if constexpr (HALO) {
-        // ---- halo mode: LDS = [HR halo rows x 128 B] then 2 weight stages [BN x 128 B]
-        const int W = geo.W, hoff = W + 1;
-        const int HR = (BM + 2 * W + 2 + 31) & ~31;
-        char* hal = smem;
-        char* bsm = smem + HR * 128;
-        const int m_lo = m0 - hoff;                         // flattened pixel of halo row 0 (may be < 0: zeros)
-        const int nck = geo.C / BK;
-        auto stage_halo = [&](int ck) {
-            for (int i = 0; i < HR / 32; ++i) {
-                const int row = (i * 4 + wave) * 8 + (lane >> 3);
-                const int p = m_lo + row;
-                const int lc = (lane & 7) ^ nt_swz(row);
-                const uint32_t off = (unsigned)p < (unsigned)M ? (uint32_t)((p * lda + ck * BK + lc * 8) * 2) : OOB;
-                blds16(ra, off, hal + (i * 4 + wave) * 1024);
-            }
-        };
-        auto stage_bt = [&](int buf, int ck, int t) {
-            const int bk0 = geo.tap_b[t] + ck * BK * 2;
-#pragma unroll
-            for (int i = 0; i < BN / 32; ++i) blds16(rb, (uint32_t)(b_off[i] + bk0), bsm + buf * B_BYTES + (i * 4 + wave) * 1024);
-        };
-        // tap validity of this lane's fragment rows (bit t: the tap's source pixel is inside the image): the halo
-        // holds the flattened neighbours, which cross image rows / images at the borders -- those taps read zero
-        uint32_t vb[RM];
-#pragma unroll
-        for (int rm = 0; rm < RM; ++rm) {
-            const int gm = m0 + wm * WTM + rm * 16 + fr;
-            int n, r, c;
-            row_coords(gm, geo, n, r, c);
-            uint32_t ok = 0;
-#pragma unroll
-            for (int t = 0; t < 9; ++t)
-                ok |= ((unsigned)(r + geo.offh[t]) < (unsigned)geo.H && (unsigned)(c + geo.offw[t]) < (unsigned)geo.W)
-                          ? 1u << t : 0u;
-            vb[rm] = gm < M ? ok : 0u;
-        }
-        stage_halo(0);
-        stage_bt(0, 0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const bf16x8 zero8 = {};
-        int ck = 0, t = 0;
-        const int nsteps = nck * 9;
-        for (int st = 0; st < nsteps; ++st) {
-            const int cur = st & 1;
-            if (st + 1 < nsteps) stage_bt(cur ^ 1, t == 8 ? ck + 1 : ck, t == 8 ? 0 : t + 1);
-            const int shift = hoff + geo.tap_shift[t];
-            const char* Bs = bsm + cur * B_BYTES;
-#pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
-                bf16x8 fa[RN], fb[RM];
-#pragma unroll
-                for (int rn = 0; rn < RN; ++rn) {
-                    const int row = wn * WTN + rn * 16 + fr;
-                    const int pc = (kk * 4 + fq) ^ nt_swz(row);
-                    fa[rn] = *(const bf16x8*)(Bs + row * 128 + pc * 16);
-                }
-#pragma unroll
-                for (int rm = 0; rm < RM; ++rm) {
-                    const int hrow = wm * WTM + rm * 16 + fr + shift;
-                    const int pc = (kk * 4 + fq) ^ nt_swz(hrow);
-                    const bf16x8 v = *(const bf16x8*)(hal + hrow * 128 + pc * 16);
-                    fb[rm] = (vb[rm] >> t) & 1u ? v : zero8;
-                }
-#pragma unroll
-                for (int rn = 0; rn < RN; ++rn)
-#pragma unroll
-                    for (int rm = 0; rm < RM; ++rm)
-                        acc[rn][rm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[rn], fb[rm], acc[rn][rm], 0, 0, 0);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (++t == 9) {
-                t = 0;
-                if (++ck < nck) {                           // next channel chunk: restage the halo (all reads done)
-                    stage_halo(ck);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __syncthreads();
-                }
-            }
-        }
-    } else {
     const int nk = K / BK;
     const int cdim = CONV ? geo.C : K;                      // channels per tap
     int st = 0, sc = 0;                                     // (tap, channel offset) of the next stage
@@ -437,18 +347,6 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
                 const int pc = (kk * 4 + fq) ^ nt_swz(row);
                 fb[rm] = *(const bf16x8*)(As + row * 128 + pc * 16);
             }
-            if constexpr (PRO) {
-                const int kb = kt * BK + (kk * 4 + fq) * 8;    // this lane's 8 channels
-                const f32x4 s0 = *(const f32x4*)(bnr.mean + kb), s1 = *(const f32x4*)(bnr.mean + kb + 4);
-                const f32x4 b0 = *(const f32x4*)(bnr.invstd + kb), b1 = *(const f32x4*)(bnr.invstd + kb + 4);
-#pragma unroll
-                for (int rm = 0; rm < RM; ++rm)
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        const float sc = e < 4 ? s0[e & 3] : s1[e & 3], bi = e < 4 ? b0[e & 3] : b1[e & 3];
-                        fb[rm][e] = (__bf16)fmaxf(fmaf((float)fb[rm][e], sc, bi), 0.f);
-                    }
-            }
 #pragma unroll
             for (int rn = 0; rn < RN; ++rn)
 #pragma unroll
@@ -458,7 +356,6 @@ gemm_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, __bf1
         if (NBUF == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    }  // !HALO
     // Epilogue through LDS (the k-loop's last barrier freed it): D[n][m] has column m = fr and rows
     // n = 4*fq + r in each lane, i.e. 4 consecutive channels of one pixel.  Stage the bf16 tile as [m][n] rows
     // padded by 16 B, then store whole output rows with 16 B per lane (a wave instruction writes contiguous
@@ -898,10 +795,16 @@ __global__ void slab_final_kernel(const float* __restrict__ S, float* __restrict
 // its partner's DMA issue, gather address math and wait.  A group refills a slot right after the barrier that follows
 // its own last read of it.  A 64-column sub-image lies inside one tap of a 3x3 gather (C % 64 == 0), so tiles may span
 // taps: the gathered B tile of a C = 64 layer is 3 taps wide.
-template <int NA, int NB, int KS, int CONV, int BKT, int RING>
+//
+// ATOMIC: instead of a slab per slice (summed by the slab reducer's two extra launches), each block adds its tile into
+// the fp32 output C (ldc) with no-return float atomics, which execute at the memory side (MI355X_MICROARCH.md, Global
+// float atomics: ~1.3 TB/s of added bytes chip-wide, full rate for 256 contiguous bytes per wave instruction).  The
+// finished tile goes through LDS (XOR-swizzled, conflict-free both ways) so every atomic instruction covers one 64-float
+// row, and all NW waves of the block issue them.  The caller zeroes C first unless it accumulates.
+template <int NA, int NB, int KS, int CONV, int BKT, int RING, bool ATOMIC = false>
 __global__ void __launch_bounds__(64 * KS * NA * NB, 1)
 wgrad_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float* __restrict__ W, int M, int N1, int N2,
-             int lda, int ldb, int kchunk, ConvGeom geo) {
+             int lda, int ldb, int kchunk, ConvGeom geo, int ldc) {
     constexpr int GW = NA * NB;                      // waves per group
     constexpr int NW = KS * GW;
     constexpr int R2 = RING / KS;                    // slots per group
@@ -1099,16 +1002,43 @@ wgrad_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B, float* 
                 for (int r = 0; r < 4; ++r) dst[((a * 4 + b) * 4 + r) * 64] = acc[a][b][r];
     }
     __syncthreads();
-    if (grp > 0) return;
+    if (!ATOMIC && grp > 0) return;
+    if (grp == 0) {
 #pragma unroll 1
-    for (int g = 1; g < KS; ++g) {
-        const float* src = red + ((g - 1) * GW + wg) * 4096 + lane;
+        for (int g = 1; g < KS; ++g) {
+            const float* src = red + ((g - 1) * GW + wg) * 4096 + lane;
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < 4; ++a)
 #pragma unroll
-            for (int b = 0; b < 4; ++b)
+                for (int b = 0; b < 4; ++b)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[a][b][r] += src[((a * 4 + b) * 4 + r) * 64];
+                    for (int r = 0; r < 4; ++r) acc[a][b][r] += src[((a * 4 + b) * 4 + r) * 64];
+        }
+    }
+    if constexpr (ATOMIC) {
+        // group 0's sub-tiles -> LDS [wg][row][col ^ swz(row)], then every wave adds whole 64-float rows into C
+        __syncthreads();  // every group-0 wave is done reading the hand-off area it now overwrites
+        if (grp == 0) {
+            float* t = red + wg * 4096;
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = a * 16 + 4 * g4 + r, col = b * 16 + gi;
+                        t[row * 64 + (col ^ (((row >> 2) & 3) << 4))] = acc[a][b][r];
+                    }
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int j = wave; j < GW * 64; j += NW) {
+            const int tw = j >> 6, row = j & 63;
+            const float v = red[tw * 4096 + row * 64 + (lane ^ (((row >> 2) & 3) << 4))];
+            float* dst = W + (size_t)(n10 + (tw / NB) * 64 + row) * ldc + n20 + (tw % NB) * 64 + lane;
+            __hip_atomic_fetch_add(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
     }
     // D[n1][n2]: lane holds column n2 = lane & 15, rows n1 = 4 (lane >> 4) + r
     float* slab = W + (size_t)slice * N1 * N2;
@@ -1180,106 +1110,36 @@ int launch_nt(const void* A, const void* B, void* C, int M, int N, int K, int ld
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-// Halo convolution (MODE 3): LDS = the halo image (rows rounded to 32) + two weight stages, or the epilogue tile if
-// larger; the halo depends on the image width, so the size is a launch argument (attribute set to the maximum).
-template <int BM, int BN, int WGM, int WGN, int MINB>
-int launch_halo(const void* A, const void* B, void* C, int M, int N, int lda, int ldb, int ldc, const void* zero,
-                float* stats, hipStream_t s, const ConvGeom& geo, const void* D, int ldd, BnBwd bnr) {
-    constexpr int TILE = BM * (BN * 2 + 16), RED = NTHREADS * 17 * 4;
-    constexpr int EPI = TILE > RED ? TILE : RED;
-    const int HR = (BM + 2 * geo.W + 2 + 31) & ~31;
-    int lds = HR * 128 + 2 * BN * BK * 2;
-    if (lds < EPI) lds = EPI;
-    if (lds > 160 * 1024) return -4;
-    auto kf = gemm_nt_kernel<BM, BN, WGM, WGN, 3, MINB, 2, false>;
-    auto kb = gemm_nt_kernel<BM, BN, WGM, WGN, 3, MINB, 2, true>;
-    static int attr = set_lds(kf, 160 * 1024) | set_lds(kb, 160 * 1024);
-    if (attr) return attr;
-    const bool bwd = D != nullptr || bnr.part != nullptr;
-    if (bwd && stats != nullptr) return -1;
-    auto k = bwd ? kb : kf;
-    const int nwg = ((M + BM - 1) / BM) * (N / BN);
-    hipLaunchKernelGGL(k, dim3(nwg), dim3(NTHREADS), lds, s, (const __bf16*)A, (const __bf16*)B, (__bf16*)C, M, N,
-                       9 * geo.C, lda, ldb, ldc, (const __bf16*)zero, stats, geo, (const __bf16*)D, ldd, bnr,
-                       (const uint8_t*)nullptr);
-    return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
-// stride-1 3x3 convolutions on the same grid can run in halo mode (A/B knob plx_set_halo / PLX_HALO: 0 off, 1 on).
-// Off by default: measured 0.99-1.17x the gather mode's time on the ResNet-50 3x3 layers (the halo image costs
-// occupancy: 2 blocks/CU instead of 4), see profiles/r3_negative_results.md.
-int g_halo = 0;
-
-// reduction order of the implicit-GEMM convolutions (A/B knob plx_set_tap_inner): see ConvGeom::tap_inner
-int g_tap_inner = 1;
-
-inline bool halo_ok(const ConvGeom& g) {
-    if (!g_halo || g.ntaps != 9 || g.S != 1 || g.OS != 0 || g.Hr != g.H || g.Wr != g.W || g.C % BK) return false;
-    for (int t = 0; t < 9; ++t)
-        if (g.offh[t] < -1 || g.offh[t] > 1 || g.offw[t] < -1 || g.offw[t] > 1) return false;
-    return true;
-}
-
 // Single-buffer NT GEMM (NBUF = 1) or double-buffered.  The single-buffer kernels run 4 blocks per CU (3 for the
 // 256x64 conv tile), which hides the staging better than double buffering at 2 blocks -- when the grid has the
 // blocks to fill them (>= 3 per CU), or when K == BK leaves nothing to double-buffer.  Measured on the ResNet-50
-// shapes (scripts/ab_modes.sh, profiles/r2_nt_single_buffer_ab.md).  Modes (A/B knob): 0 never, 1 K == BK only
-// (plain GEMMs), 2 every plain GEMM, 3 every GEMM, 4 forward-epilogue GEMMs by the rule, 5 (default) the rule.
-int g_nt_single_stage = 5;
+// shapes (scripts/ab_modes.sh, profiles/r2_nt_single_buffer_ab.md): single-buffered when the grid has >= 3 blocks per
+// CU, or for plain GEMMs with K == BK.
 
-// Tall tiles (A/B knob plx_set_nt_tall): 256 pixel rows x 128 channels per block (4 waves of 128 x 64) instead of
-// 128 x 128 for N % 128 == 0 -- 85 instead of 64 FLOP per staged byte and a quarter fewer LDS fragment reads per MFMA,
-// for the compute-bound GEMMs (reduction depth K >= g_nt_tall_k: the 3x3 layers and the wide 1x1s; the HBM-bound
-// shallow ones lose the 4-blocks-per-CU latency hiding).  0 off, 1 forward GEMMs, 2 forward and data-gradient GEMMs;
-// only when the grid still fills the CUs.
-int g_nt_tall = 0, g_nt_tall_k = 1024;
-
-inline bool nt_tall(bool bwd, int M, int N, int K) {
-    if (g_nt_tall == 0 || N % 128 || K < g_nt_tall_k || (bwd && g_nt_tall < 2)) return false;
-    return ((M + 255) / 256) * (N / 128) >= 256;
-}
-
-inline bool nt_single(bool bwd, bool conv, int K, int nwg) {
-    switch (g_nt_single_stage) {
-        case 0: return false;
-        case 1: return !conv && K == BK;
-        case 2: return !conv;
-        case 3: return true;
-        case 5: return nwg >= 768 || (!conv && K == BK);
-        default: return (!bwd && nwg >= 768) || (!conv && K == BK);
-    }
-}
+inline bool nt_single(bool conv, int K, int nwg) { return nwg >= 768 || (!conv && K == BK); }
 
 // m-slicing of the weight-gradient GEMM
 struct TnPlan { int kchunk, slices, groups, per_group, blocks, bn1, bn2; };
 
-// Wide weight-gradient tiles (plx_set_tn_wide): 256 x 128 (or 128 x 256) outputs per 4-wave block with 32-row
-// double-buffered stages -- 48 KB of LDS (the 128 x 128 double buffer takes 64 KB) and 85 instead of 64 MFMA FLOP
-// per staged byte, so the side stream moves a quarter fewer L2 -> LDS bytes beside the data-gradient chain.  Only
-// where the wide plan still launches at least min(CUs, narrow plan's blocks) blocks.
-int g_tn_wide = 0;
-
-inline void tn_tile(int N1, int N2, int& bn1, int& bn2, bool wide = false) {
-    if (wide && N1 % 256 == 0 && N2 % 128 == 0) { bn1 = 256; bn2 = 128; return; }
-    if (wide && N2 % 256 == 0 && N1 % 128 == 0) { bn1 = 128; bn2 = 256; return; }
+inline void tn_tile(int N1, int N2, int& bn1, int& bn2) {
     bn1 = N1 % 128 == 0 ? 128 : 64;
     bn2 = N2 % 128 == 0 ? 128 : 64;
 }
 
-// slicing knobs (plx_set_tn_plan): target resident blocks per CU, cap on the fp32 slab bytes
-// Swept in isolation (scripts/diag_wgrad_plan.py) 3 / 32 MB was best; in the training step the weight gradients run on
+// v1 slicing: target resident blocks per CU, cap on the fp32 slab bytes.  (v1 serves the stem's weight gradient, alone
+// at the end of the backward with 4 blocks per CU, and the v1 variant of the tests.)  Swept in isolation (scripts/diag_wgrad_plan.py) 3 / 32 MB was best; in the training step the weight gradients run on
 // the side stream beside the data-gradient chain, and there fewer slices (less slab traffic competing with the main
 // stream) win, except for the 56x56 layers whose gradients finish the backward: 0 = by size (tn_plan), 16 MB.  Same-box
-// bench, 2 interleaved rounds (PLX_TN_PLAN): 3/32 11.61k, 11.70k; 1/16 11.71k, 11.75k; by size 11.85k, 11.87k trials/h.
+// bench, 2 interleaved rounds (blocks per CU / slab MB): 3/32 11.61k, 11.70k; 1/16 11.71k, 11.75k; by size 11.85k, 11.87k trials/h.
 // Slab cap under the by-size plan: 8 MB 10.62k / 10.60k (too few slices), 16 MB 11.92k / 11.93k, 32 MB 11.91k / 11.91k
-int g_tn_blocks_per_cu = 0;
-int g_tn_bpc_big = 3, g_tn_bpc_mid = 1;  // by-size plan: 56x56 layers, 28x28 layers (plx_set_tn_sizes)
-long g_tn_slab_bytes = 16l << 20;
+constexpr int g_tn_blocks_per_cu = 0;
+constexpr int g_tn_bpc_big = 3, g_tn_bpc_mid = 1;  // by-size plan: 56x56 layers, 28x28 layers
+constexpr long g_tn_slab_bytes = 16l << 20;
 
 // bpc > 0 overrides the blocks-per-CU target (the stem's weight gradient runs alone at the end of the backward)
-inline TnPlan tn_plan_tile(int M, int N1, int N2, int num_cus, int bpc, bool wide) {
+inline TnPlan tn_plan(int M, int N1, int N2, int num_cus, int bpc = 0) {
     int bn1, bn2;
-    tn_tile(N1, N2, bn1, bn2, wide);
+    tn_tile(N1, N2, bn1, bn2);
     const int ntiles = (N1 / bn1) * (N2 / bn2);
     const long plane = (long)N1 * N2;
     // ~4 blocks per CU (one 4-wave block per CU leaves each SIMD a single wave: latency-bound), >= 4
@@ -1310,26 +1170,6 @@ inline TnPlan tn_plan_tile(int M, int N1, int N2, int num_cus, int bpc, bool wid
     return {kchunk, slices, groups, per_group, blocks, bn1, bn2};
 }
 
-inline TnPlan tn_plan(int M, int N1, int N2, int num_cus, int bpc = 0) {
-    const TnPlan narrow = tn_plan_tile(M, N1, N2, num_cus, bpc, false);
-    if (!g_tn_wide || bpc > 0) return narrow;
-    const TnPlan wide = tn_plan_tile(M, N1, N2, num_cus, bpc, true);
-    if (wide.bn1 == narrow.bn1 && wide.bn2 == narrow.bn2) return narrow;
-    const long nb = (long)(N1 / narrow.bn1) * (N2 / narrow.bn2) * narrow.slices;
-    const long wb = (long)(N1 / wide.bn1) * (N2 / wide.bn2) * wide.slices;
-    const long floor_blocks = nb < (num_cus > 0 ? num_cus : 256) ? nb : (num_cus > 0 ? num_cus : 256);
-    return wb >= floor_blocks ? wide : narrow;
-}
-
-// Rows per stage of the weight-gradient GEMM (A/B knob plx_set_tn_stages' second argument: 64 or 32)
-int g_tn_bk = 64;
-
-// LDS ring depth of the weight-gradient GEMM (A/B knob plx_set_tn_stages: 2 = double buffering, 3 or 4).  Default 2:
-// in the training step the deeper rings measured slower (same box, 3-sweep bench: 2 stages 11.92k, 3 stages 11.60k,
-// 4 stages 11.36k trials/h) -- a 96-128 KB ring leaves no LDS on its CU for the data-gradient chain's blocks
-// (profiles/r3_negative_results.md)
-int g_tn_stages = 2;
-
 template <int BN1, int BN2, int WG1, int WG2, int CONV, int NST, int BKT = BK>
 int launch_tn_st(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
                  const void* zero, hipStream_t s, const ConvGeom& geo) {
@@ -1349,7 +1189,7 @@ int launch_tn_st(const void* A, const void* B, float* W, int M, int N1, int N2, 
 // 3/4 of the CUs' worth of blocks measured +0.7 % trials/h over v1 (4 runs each on 2 boxes); with a 128 KB ring or
 // one block on every CU it was 2-4 % slower, although faster in isolation (profiles/r5_wgrad_v2.md)
 int g_tn_v2 = 1;        // 1: wgrad_kernel (v2), 0: gemm_tn_kernel (v1), 2: v2 for the gathered convolutions only
-                        // (A/B knob plx_set_tn_v2)
+                        // (test hook plx_set_tn_v2)
 int g_tn2_lds_kb = 64;  // LDS ring budget of a v2 block: 128 KB (one block per CU) or 64 KB (two per CU, or room for the
                         // main stream's blocks beside it); configurations whose groups would get < 2 slots keep 128
 
@@ -1386,9 +1226,9 @@ inline void plan_reducer(TnPlan& p, long plane) {
 // per round of blocks + the slab bytes (s + 1 planes: written, read back by the reducer) when s > 1.  Rates are
 // round numbers from the v2 isolated runs (profiles/r5_wgrad_v2.md).
 constexpr double kTnCuFlops = 3.2e12, kTnBlockUs = 2.5;
-// slab bandwidth the plan prices (A/B knob plx_set_tn2_slab_bw): 4.5 TB/s is the isolated rate, but in the training
-// step the slab write + reduce passes compete with the main stream's memory-bound BatchNorm kernels
-double g_tn2_slab_bw = 4.5e12;
+// slab bandwidth the plan prices: 4.5 TB/s, the isolated rate of the slab write + reduce passes (with the in-kernel
+// atomic reduction the same plan is kept: the added bytes cost about what the slab round trip did)
+constexpr double g_tn2_slab_bw = 4.5e12;
 
 // ring slots of a v2 block within an LDS budget (a multiple of KS, <= 16); 0 when a group would get < 2 slots
 constexpr int tn2_ring(int na, int nb, int ks, int lds_kb) {
@@ -1402,18 +1242,23 @@ inline int tn2_ring_kb(const V2Cfg& c) {
 
 // blocks the v2 plan aims for: 1 or 2 per CU, or (> 2) a total block count; 0 (default): 3/4 of the CUs, which leaves
 // a quarter of the CUs whole to the main stream's kernels (in-step sweep over 128-256 blocks: 192 best, 176 / 208 /
-// 224 / 256 at or below v1; A/B knob plx_set_tn2_bpc)
-int g_tn2_bpc = 0;
+// 224 / 256 at or below v1)
+constexpr int g_tn2_bpc = 0;
 
 // the stem's weight gradient (CONV 2), which runs alone on the main stream at the very end of the backward: 0 v1
 // (gemm_tn_kernel, 4 blocks per CU), 1 v2 planned for 2 blocks on every CU, 2 v2 with the side stream's block target
-// (A/B knob plx_set_tn2_stem)
+// (test hook plx_set_tn2_stem)
 int g_tn2_stem = 0;
 
-// v2 for the 6-wave configuration (N1 = 64, N2 a multiple of 192: the C = 64 3x3 weight gradients); A/B knob
+// v2 for the 6-wave configuration (N1 = 64, N2 a multiple of 192: the C = 64 3x3 weight gradients); test hook
 // plx_set_tn2_c64
 int g_tn2_c64 = 1;
 constexpr int kStemV2Bpc = 2;
+
+// v2 weight gradients reduce their K slices in the kernel with float atomics into the output (wgrad_kernel ATOMIC) --
+// 1, default -- or through fp32 slabs and the slab reducer's launches (0; deterministic summation order).  A/B knob
+// plx_set_tn_atomic (PLX_WGRAD_ATOMIC)
+int g_tn_atomic = 1;
 
 // full_bpc > 0: plan for that many blocks on EVERY CU (the stem's weight gradient, alone on the GPU at the end of the
 // backward), whatever the block target
@@ -1447,41 +1292,47 @@ inline TnPlan tn2_plan(int M, int N1, int N2, int num_cus, const V2Cfg& c, int f
     return p;
 }
 
-template <int NA, int NB, int KS, int CONV, int LDSK>
+template <int NA, int NB, int KS, int CONV, int LDSK, bool ATOMIC>
 int launch_tn2_k(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
-                 hipStream_t s, const ConvGeom& geo) {
+                 hipStream_t s, const ConvGeom& geo, int ldc) {
     constexpr int BKT = 32, STAGE = (NA + NB) * BKT * 128;
     constexpr int RING = tn2_ring(NA, NB, KS, LDSK);
     static_assert(RING > 0, "ring budget too small for this configuration");
     constexpr int LDS = RING * STAGE;
-    auto k = wgrad_kernel<NA, NB, KS, CONV, BKT, RING>;
+    static_assert(!ATOMIC || NA * NB * 16384 <= LDS, "the atomic epilogue's tile image exceeds the ring");
+    auto k = wgrad_kernel<NA, NB, KS, CONV, BKT, RING, ATOMIC>;
     static int attr = set_lds(k, LDS);
     if (attr) return attr;
     const int ntiles = (N1 / (64 * NA)) * (N2 / (64 * NB));
     hipLaunchKernelGGL(k, dim3(ntiles * plan.slices), dim3(64 * NA * NB * KS), LDS, s, (const __bf16*)A,
-                       (const __bf16*)B, W, M, N1, N2, lda, ldb, plan.kchunk, geo);
+                       (const __bf16*)B, W, M, N1, N2, lda, ldb, plan.kchunk, geo, ldc);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-template <int NA, int NB, int KS, int CONV>
+template <int NA, int NB, int KS, int CONV, bool ATOMIC>
 int launch_tn2(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
-               hipStream_t s, const ConvGeom& geo) {
+               hipStream_t s, const ConvGeom& geo, int ldc) {
     if constexpr (tn2_ring(NA, NB, KS, 64) > 0) {
         if (tn2_ring_kb(V2Cfg{NA, NB, KS}) <= 64)
-            return launch_tn2_k<NA, NB, KS, CONV, 64>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo);
+            return launch_tn2_k<NA, NB, KS, CONV, 64, ATOMIC>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo, ldc);
     }
-    return launch_tn2_k<NA, NB, KS, CONV, 128>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo);
+    return launch_tn2_k<NA, NB, KS, CONV, 128, ATOMIC>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo, ldc);
 }
 
+// atomic: add into W = C (ldc) in the kernel (wgrad_kernel ATOMIC) instead of writing slabs (ld N2)
 template <int CONV>
 int dispatch_tn2(const V2Cfg& c, const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb,
-                 const TnPlan& plan, hipStream_t s, const ConvGeom& geo) {
+                 const TnPlan& plan, hipStream_t s, const ConvGeom& geo, bool atomic = false, int ldc = 0) {
     if constexpr (CONV == 2) {  // the stem: 64 x 256
-        if (c.na == 1 && c.nb == 4 && c.ks == 2) return launch_tn2<1, 4, 2, 2>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo);
+        if (c.na == 1 && c.nb == 4 && c.ks == 2)
+            return atomic ? launch_tn2<1, 4, 2, 2, true>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo, ldc)
+                          : launch_tn2<1, 4, 2, 2, false>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo, ldc);
         return -1;
     } else {
 #define PLX_TN2(a, b, k) \
-    if (c.na == a && c.nb == b && c.ks == k) return launch_tn2<a, b, k, CONV>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo);
+    if (c.na == a && c.nb == b && c.ks == k) \
+        return atomic ? launch_tn2<a, b, k, CONV, true>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo, ldc) \
+                      : launch_tn2<a, b, k, CONV, false>(A, B, W, M, N1, N2, lda, ldb, plan, s, geo, ldc);
         PLX_TN2(2, 2, 2) PLX_TN2(1, 4, 2) PLX_TN2(1, 3, 2) PLX_TN2(1, 2, 4) PLX_TN2(1, 1, 8) PLX_TN2(4, 1, 2)
         PLX_TN2(2, 1, 4)
 #undef PLX_TN2
@@ -1492,14 +1343,8 @@ int dispatch_tn2(const V2Cfg& c, const void* A, const void* B, float* W, int M, 
 template <int BN1, int BN2, int WG1, int WG2, int CONV = 0>
 int launch_tn(const void* A, const void* B, float* W, int M, int N1, int N2, int lda, int ldb, const TnPlan& plan,
               const void* zero, hipStream_t s, ConvGeom geo = {}) {
-    if (g_tn_bk == 32)  // half-size stages: a 3- or 4-deep ring in (at most) the double buffer's LDS
-        return g_tn_stages >= 4
-                   ? launch_tn_st<BN1, BN2, WG1, WG2, CONV, 4, 32>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo)
-                   : launch_tn_st<BN1, BN2, WG1, WG2, CONV, 3, 32>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo);
-    if (g_tn_stages >= 4)
-        return launch_tn_st<BN1, BN2, WG1, WG2, CONV, 4>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo);
-    if (g_tn_stages == 3)
-        return launch_tn_st<BN1, BN2, WG1, WG2, CONV, 3>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo);
+    // double buffering (deeper rings measured slower in the step: a 96-128 KB ring leaves no LDS on its CU for the
+    // data-gradient chain's blocks, profiles/r3_negative_results.md)
     return launch_tn_st<BN1, BN2, WG1, WG2, CONV, 2>(A, B, W, M, N1, N2, lda, ldb, plan, zero, s, geo);
 }
 
@@ -1522,106 +1367,43 @@ int plx_gemm_nt(const void* A, const void* B, void* C, int M, int N, int K, int 
     if (bnr != nullptr && (ldc != N || bnr->part == nullptr)) return -1;
     const BnBwd b = bnr != nullptr ? *bnr : BnBwd{};
     hipStream_t s = (hipStream_t)stream;
-    const bool bwd = D != nullptr || bnr != nullptr;
-    if (nt_tall(bwd, M, N, K))
-        return launch_nt<256, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
     if (N % 128 == 0) {
-        const bool one = nt_single(bwd, false, K, ((M + 127) / 128) * (N / 128));
+        const bool one = nt_single(false, K, ((M + 127) / 128) * (N / 128));
         return one ? launch_nt<128, 128, 2, 2, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b,
                                                          dmask)
                    : launch_nt<128, 128, 2, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
     }
-    const bool one = nt_single(bwd, false, K, ((M + 255) / 256) * (N / 64));
+    const bool one = nt_single(false, K, ((M + 255) / 256) * (N / 64));
     return one ? launch_nt<256, 64, 4, 1, false, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask)
                : launch_nt<256, 64, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, D, ldd, b, dmask);
 }
 
-// Prototype of the BatchNorm-apply prologue (MODE 4): C = relu(A * scale + bias) . B^T, the per-channel affine of A
-// (scale / bias fp32 [K], 16-byte aligned) applied to the MFMA fragments instead of a separate apply pass writing
-// relu(bn(A)).  Forward only, same tile selection as plx_gemm_nt; stats (nullable) as there.  Used by
-// scripts/diag_bn_prologue.py to price the fusion on the ResNet-50 1x1 shapes.
-int plx_gemm_nt_prologue(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
-                         const void* zero, const float* scale, const float* bias, float* stats, void* stream) {
-    if (M <= 0 || N % 64 || K % BK || lda % 8 || ldb % 8 || ldc % 8 || !scale || !bias) return -1;
-    if ((uintptr_t)scale % 16 || (uintptr_t)bias % 16) return -1;
-    BnBwd b{};
-    b.mean = scale;
-    b.invstd = bias;
-    hipStream_t s = (hipStream_t)stream;
-    if (N % 128 == 0) {
-        const bool one = nt_single(false, false, K, ((M + 127) / 128) * (N / 128));
-        return one ? launch_nt<128, 128, 2, 2, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, nullptr, 0, b)
-                   : launch_nt<128, 128, 2, 2, 4, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, nullptr, 0, b);
-    }
-    const bool one = nt_single(false, false, K, ((M + 255) / 256) * (N / 64));
-    return one ? launch_nt<256, 64, 4, 1, 4, 1>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, nullptr, 0, b)
-               : launch_nt<256, 64, 4, 1, 4, 2>(A, B, C, M, N, K, lda, ldb, ldc, zero, stats, s, {}, nullptr, 0, b);
-}
-
-// A/B knob: single-buffer NT GEMM mode (see nt_single)
-void plx_set_nt_single_stage(int mode) { g_nt_single_stage = mode; }
-
-// A/B knob: halo mode for the stride-1 3x3 convolutions (1 on, 0 the per-tap gather)
-void plx_set_halo(int on) { g_halo = on ? 1 : 0; }
-
-// A/B knob: tap-inner reduction order of the implicit-GEMM convolutions (1) or tap-major (0)
-void plx_set_tap_inner(int on) { g_tap_inner = on ? 1 : 0; }
-
-// A/B knob: 256 x 128 NT tiles (0 off, 1 forward, 2 forward + data gradient), see nt_tall
-void plx_set_nt_tall(int mode, int min_k) {
-    g_nt_tall = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
-    if (min_k > 0) g_nt_tall_k = min_k;
-}
-
-// A/B knob: LDS ring depth of the weight-gradient GEMM (2, 3 or 4 stages)
-void plx_set_tn_stages(int n, int bk) {
-    g_tn_stages = n < 2 ? 2 : (n > 4 ? 4 : n);
-    if (bk == 32 || bk == 64) g_tn_bk = bk;
-}
-
-// A/B knob: wide (256 x 128 / 128 x 256) weight-gradient tiles (see g_tn_wide); set before sizing workspaces
-void plx_set_tn_wide(int on) { g_tn_wide = on ? 1 : 0; }
-
-// A/B knob: weight-gradient kernel v2 (wgrad_kernel, 1) or v1 (gemm_tn_kernel, 0); lds_kb: v2's ring budget (64 or
-// 128, <= 0 keeps it; workspace queries size for every plan, so either may be toggled after sizing)
 // diagnostics: K slices (fp32 slabs) the weight-gradient plan of this problem uses (v2: wgrad_kernel's plan)
 int plx_tn_plan_slices(int M, int N1, int N2, int num_cus, int v2) {
     if (M <= 0 || N1 % 64 || N2 % 64) return -1;
     return v2 ? tn2_plan(M, N1, N2, num_cus, v2_cfg(N1, N2)).slices : tn_plan(M, N1, N2, num_cus).slices;
 }
 
+// Kernel selection hooks of the weight-gradient tests (tests/test_gpu_conv.py runs every variant against fp32; no
+// environment knob sets them): the C = 64 3x3 6-wave v2 configuration, the in-kernel atomic reduction (else slabs),
+// the stem's kernel (0 v1, 1 v2 on every CU, 2 v2 with the side-stream block target), v2 (1) or v1 (0) with v2's LDS
+// ring budget (64 or 128 KB, <= 0 keeps it; workspace queries size for every plan)
 void plx_set_tn2_c64(int on) { g_tn2_c64 = on ? 1 : 0; }
 
-void plx_set_tn2_stem(int mode) { g_tn2_stem = mode < 0 ? 0 : (mode > 2 ? 2 : mode); }
+void plx_set_tn_atomic(int on) { g_tn_atomic = on ? 1 : 0; }
 
-void plx_set_tn2_slab_bw(int gb_per_s) { if (gb_per_s > 0) g_tn2_slab_bw = gb_per_s * 1e9; }
-void plx_set_tn2_bpc(int bpc) { g_tn2_bpc = bpc < 0 ? 0 : (bpc > 4096 ? 4096 : bpc); }
+void plx_set_tn2_stem(int mode) { g_tn2_stem = mode < 0 ? 0 : (mode > 2 ? 2 : mode); }
 
 void plx_set_tn_v2(int on, int lds_kb) {
     g_tn_v2 = on < 0 ? 0 : (on > 2 ? 2 : on);
     if (lds_kb > 0) g_tn2_lds_kb = lds_kb <= 64 ? 64 : 128;
 }
 
-// weight-gradient slicing knobs; workspace sizes follow them, so set before sizing / launching
-void plx_set_tn_plan(int blocks_per_cu, int slab_mb) {
-    if (blocks_per_cu >= 0) g_tn_blocks_per_cu = blocks_per_cu;  // 0: by problem size (tn_plan)
-    if (slab_mb > 0) g_tn_slab_bytes = (long)slab_mb << 20;
-}
-
-// A/B knob: blocks per CU of the by-size plan for the 56x56 (big) and 28x28 (mid) weight gradients
-void plx_set_tn_sizes(int big, int mid) {
-    if (big > 0) g_tn_bpc_big = big;
-    if (mid > 0) g_tn_bpc_mid = mid;
-}
-
 // floats of slab workspace plx_gemm_tn needs for this problem
 long plx_gemm_tn_workspace(int M, int N1, int N2, int num_cus) {
     if (M <= 0 || N1 % 64 || N2 % 64) return -1;
-    // the larger of the narrow and wide plans, whatever the knob: a size memoised before plx_set_tn_wide still fits
-    const TnPlan a = tn_plan_tile(M, N1, N2, num_cus, 0, false), b = tn_plan_tile(M, N1, N2, num_cus, 0, true);
+    const TnPlan a = tn_plan(M, N1, N2, num_cus);
     long n = a.slices + (a.groups > 1 ? a.groups : 0);
-    const long nb = b.slices + (b.groups > 1 ? b.groups : 0);
-    if (nb > n) n = nb;
     for (int kb = 64; kb <= 128; kb += 64) {  // both v2 ring budgets, whatever the knob
         const int keep = g_tn2_lds_kb;
         g_tn2_lds_kb = kb;
@@ -1650,12 +1432,12 @@ int run_tn(const void* A, const void* B, float* C, float* ws, int M, int N1, int
     const TnPlan plan = v2 ? tn2_plan(M, N1, N2, num_cus, cfg, CONV == 2 && g_tn2_stem == 1 ? kStemV2Bpc : 0)
                            : tn_plan(M, N1, N2, num_cus, bpc);
     int rc;
+    if (v2 && g_tn_atomic) {  // in-kernel reduction: float atomics into C, no slabs, no reducer launches
+        if (!accumulate && hipMemset2DAsync(C, (size_t)ldc * 4, 0, (size_t)N2 * 4, N1, s) != hipSuccess) return -3;
+        return dispatch_tn2<CONV>(cfg, A, B, C, M, N1, N2, lda, ldb, plan, s, geo, true, ldc);
+    }
     if (v2)
         rc = dispatch_tn2<CONV>(cfg, A, B, ws, M, N1, N2, lda, ldb, plan, s, geo);
-    else if (plan.bn1 == 256)
-        rc = launch_tn_st<256, 128, 2, 2, CONV, 2, 32>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
-    else if (plan.bn2 == 256)
-        rc = launch_tn_st<128, 256, 2, 2, CONV, 2, 32>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
     else if (N1 % 128 == 0 && N2 % 128 == 0)
         rc = launch_tn<128, 128, 2, 2, CONV>(A, B, ws, M, N1, N2, lda, ldb, plan, zero, s, geo);
     else if (N1 % 128 == 0)
@@ -1779,21 +1561,13 @@ inline int nt_rows_per_block(int N) { return N % 128 == 0 ? 128 : 256; }
 int nt_conv_any(const void* A, const void* B, void* C, int M, int N, const ConvGeom& g_in, int ldb, int ldc,
                 const void* zero, float* stats, hipStream_t s, const void* D = nullptr, const BnBwd& bnr = {}) {
     ConvGeom g = g_in;
-    g.tap_inner = g_tap_inner;
-    const bool bwd = D != nullptr || bnr.part != nullptr;
+    g.tap_inner = 1;  // tap-inner reduction order (ConvGeom::tap_inner; tap-major measured slower)
     const int K = g.ntaps * g.C;
-    if (halo_ok(g)) {
-        const int ldd = D != nullptr ? ldc : 0;
-        if (N % 128 == 0)
-            return launch_halo<128, 128, 2, 2, 2>(A, B, C, M, N, g.C, ldb, ldc, zero, stats, s, g, D, ldd, bnr);
-        return launch_halo<256, 64, 4, 1, 2>(A, B, C, M, N, g.C, ldb, ldc, zero, stats, s, g, D, ldd, bnr);
-    }
-    if (nt_tall(bwd, M, N, K)) return nt_conv<256, 128, 2, 2, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
     if (N % 128 == 0)
-        return nt_single(bwd, true, K, ((M + 127) / 128) * (N / 128))
+        return nt_single(true, K, ((M + 127) / 128) * (N / 128))
                    ? nt_conv<128, 128, 2, 2, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr)
                    : nt_conv<128, 128, 2, 2, 2>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
-    return nt_single(bwd, true, K, ((M + 255) / 256) * (N / 64))
+    return nt_single(true, K, ((M + 255) / 256) * (N / 64))
                ? nt_conv<256, 64, 4, 1, 1>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr)
                : nt_conv<256, 64, 4, 1, 2>(A, B, C, M, N, g, ldb, ldc, zero, stats, s, D, bnr);
 }
@@ -2037,7 +1811,7 @@ int plx_stem_conv_fwd(const void* xp, const void* wp, void* y, int N, int H, int
     g.mWr = div_magic(g.Wr);
     g.mHr = div_magic(g.Hr);
     const int M = N * g.Hr * g.Wr;
-    return nt_single(false, true, 256, (M + 255) / 256)
+    return nt_single(true, 256, (M + 255) / 256)
                ? launch_nt<256, 64, 4, 1, 2, 1>(xp, wp, y, M, 64, 256, 8, 256, 64, zero, stats, (hipStream_t)stream, g)
                : launch_nt<256, 64, 4, 1, 2, 2>(xp, wp, y, M, 64, 256, 8, 256, 64, zero, stats, (hipStream_t)stream, g);
 }

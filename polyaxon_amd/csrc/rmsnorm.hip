@@ -503,11 +503,9 @@ PLX_API int plx_rms_backward(const void* x, const float* w, const void* dy, cons
 }
 
 // LayerNorm: mean / rstd fp32 [rows] saved for the backward
-static int g_ln_wave = 1;  // plx_set_ln_wave(0): the workgroup-per-row kernels for every width (A/B)
-PLX_API void plx_set_ln_wave(int on) { g_ln_wave = on != 0; }
 
 // wave-per-row path: 16-byte vectors per lane (1 or 2: d <= 1024), 0 = workgroup-per-row kernels
-static inline int ln_vpl(int d) { return !g_ln_wave ? 0 : d <= 512 ? 1 : d <= 1024 ? 2 : 0; }
+static inline int ln_vpl(int d) { return d <= 512 ? 1 : d <= 1024 ? 2 : 0; }
 
 PLX_API int plx_ln_forward(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
                            int64_t rows, int d, float eps, hipStream_t stream) {

@@ -33,7 +33,7 @@ inline int grid_for(int64_t n_vec, int cap = 2048) {
   return (int)g;
 }
 
-// Block cap of the AdamW launches (A/B knob plx_set_adamw_grid_cap, PLX_OPT_BWD_GRID for the update inside the
+// Block cap of the AdamW launches (plx_set_adamw_grid_cap; measured for the update inside the
 // backward, parallel/ddp.py FlatDDP(optimizer=...)).  That update is HBM-bound like the backward's elementwise
 // kernels: with the full grid those ran 2-40x slower beside it; capped at 32 / 64 / 128 / 256 blocks the update
 // outlasted the backward (Llama-3 8B 13.4k / 16.1k / 17.5k / 17.8k vs 17.8k tokens/s without it, same box).

@@ -8,7 +8,6 @@ map onto MFMA, bf16 autocast compute, fp32 master weights living in one flat buf
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional, Type
 
 import torch
@@ -55,9 +54,6 @@ class Bottleneck(nn.Module):
         return self.bn3(self.conv3(out, bn_link=True), identity, residual_link=True)
 
 
-_DEFER_DOWN_BN = os.environ.get("PLX_DEFER_DOWN_BN", "1") != "0"  # A/B knob (scripts/gpu.sh ab)
-_STEM_FUSED = os.environ.get("PLX_STEM_FUSED", "1") != "0"  # A/B knob: stem BN + ReLU + max-pool in one op
-_STEM_CONV = os.environ.get("PLX_STEM_CONV", "1") != "0"  # A/B knob: native stem convolution
 
 
 class Downsample(nn.Module):
@@ -71,7 +67,7 @@ class Downsample(nn.Module):
         # the output feeds only bn3's residual add, which applies this BatchNorm's scale/bias itself
         # bn_link: the conv's dgrad (+ the box's conv1 gradient) is x's whole gradient -- it serves the BatchNorm that
         # produced x its backward partials (with conv1's dgrad when strided, ops.conv1x1.BnLink.request_split)
-        return self.bn(self.conv(x, grad_box=grad_box, bn_link=True), defer_apply=_DEFER_DOWN_BN)
+        return self.bn(self.conv(x, grad_box=grad_box, bn_link=True), defer_apply=True)
 
 
 class ResNet(nn.Module):
@@ -79,7 +75,7 @@ class ResNet(nn.Module):
                  zero_init_residual: bool = True, fused: bool = True, native_conv: bool = True):
         super().__init__()
         # 3 -> 64: the MFMA stem GEMM with BN-stats epilogue (ops/stem.py); other widths: the library convolution
-        self.stem = (StemConv(3, width, native=native_conv and _STEM_CONV) if width == 64
+        self.stem = (StemConv(3, width, native=native_conv) if width == 64
                      else nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False))
         self.stem_bn = BatchNormAct(width, act=True, fused=fused)
         self.pool = MaxPool3s2(native=native_conv)
@@ -137,12 +133,11 @@ class ResNet(nn.Module):
         """Everything before the classifier head: the last stage's [N, C, H, W] output (channels_last on the GPU)."""
         x = self.stem(x)
         # BN + ReLU + max-pool fused (ops/stem.py): the 112x112 BatchNorm output is never materialised
-        x = stem_bn_relu_pool(x, self.stem_bn, self.pool) if _STEM_FUSED else self.pool(self.stem_bn(x))
+        x = stem_bn_relu_pool(x, self.stem_bn, self.pool)
         return self.stages(x)
 
     def forward_head(self, x: torch.Tensor) -> torch.Tensor:
-        """Global average pool + fc (the resident executor can instead run the head's forward AND backward in one
-        go, ops/head.py)."""
+        """Global average pool (NHWC kernel, ops/pool.py) + fc."""
         x = torch.flatten(x.mean((2, 3)), 1) if x.is_contiguous() else global_avg_pool(x)
         return self.fc(x)
 

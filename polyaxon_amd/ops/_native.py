@@ -170,50 +170,10 @@ def lib(name: str) -> ctypes.CDLL:
             build(name, force=os.environ.get("PLX_NATIVE_REBUILD") == "1")
         handle = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
         _declare(name, handle)
-        if name == "plx_conv" and os.environ.get("PLX_NT_SINGLE_STAGE"):  # A/B knob (csrc/conv_gemm.hip)
-            handle.plx_set_nt_single_stage(int(os.environ["PLX_NT_SINGLE_STAGE"]))
-        if name == "plx_conv" and os.environ.get("PLX_HALO"):  # A/B knob: halo mode of the 3x3 convolutions
-            handle.plx_set_halo(int(os.environ["PLX_HALO"]))
-        if name == "plx_conv" and os.environ.get("PLX_TAP_INNER"):  # A/B knob: tap-inner conv reduction order
-            handle.plx_set_tap_inner(int(os.environ["PLX_TAP_INNER"]))
-        if name == "plx_conv" and os.environ.get("PLX_TN_STAGES"):  # A/B knob: weight-gradient LDS ring depth
-            st, _, bk = os.environ["PLX_TN_STAGES"].partition(",")  # "stages[,rows per stage]"
-            handle.plx_set_tn_stages(int(st), int(bk or 0))
-        if name == "plx_train" and os.environ.get("PLX_ADAMW_WIDE"):  # A/B knob: 8-wide non-temporal AdamW
-            handle.plx_set_adamw_wide(int(os.environ["PLX_ADAMW_WIDE"]))
-        if name == "plx_conv" and os.environ.get("PLX_TN_V2"):  # A/B knob: "v2[,ring KB]" weight-gradient kernel
-            v2, _, kb = os.environ["PLX_TN_V2"].partition(",")
-            handle.plx_set_tn_v2(int(v2), int(kb) if kb else -1)
-        if name == "plx_conv" and os.environ.get("PLX_TN2_BPC"):  # A/B knob: v2 blocks per CU (plan)
-            handle.plx_set_tn2_bpc(int(os.environ["PLX_TN2_BPC"]))
-        if name == "plx_conv" and os.environ.get("PLX_TN2_C64"):  # A/B knob: v2 for the C = 64 3x3 wgrads
-            handle.plx_set_tn2_c64(int(os.environ["PLX_TN2_C64"]))
-        if name == "plx_conv" and os.environ.get("PLX_TN2_STEM"):  # A/B knob: the stem's weight-gradient kernel
-            handle.plx_set_tn2_stem(int(os.environ["PLX_TN2_STEM"]))
-        if name == "plx_conv" and os.environ.get("PLX_TN2_SLAB_BW"):  # A/B knob: slab GB/s the v2 plan prices
-            handle.plx_set_tn2_slab_bw(int(os.environ["PLX_TN2_SLAB_BW"]))
-        if name == "plx_conv" and os.environ.get("PLX_TN_WIDE"):  # A/B knob: 256x128 weight-gradient tiles
-            handle.plx_set_tn_wide(int(os.environ["PLX_TN_WIDE"]))
-        if name == "plx_bn" and os.environ.get("PLX_STEM_BWD_CAP"):  # A/B knob: stem backward partials-pass rows
-            handle.plx_set_stem_bwd_cap(int(os.environ["PLX_STEM_BWD_CAP"]))
-        if name == "plx_rms" and os.environ.get("PLX_LN_WAVE"):  # A/B knob: wave-per-row LayerNorm (d <= 1024)
-            handle.plx_set_ln_wave(int(os.environ["PLX_LN_WAVE"]))
-        if name == "plx_bn" and os.environ.get("PLX_BN_FIN_THREADS"):  # A/B knob: 256-thread BN finalize
-            handle.plx_set_bn_fin_threads(int(os.environ["PLX_BN_FIN_THREADS"]))
-        if name == "plx_conv" and os.environ.get("PLX_NT_TALL"):  # A/B knob: 256x128 NT tiles (0 / 1 fwd / 2 +dgrad)
-            handle.plx_set_nt_tall(int(os.environ["PLX_NT_TALL"]), int(os.environ.get("PLX_NT_TALL_K", "0")))
-        if name == "plx_gemm" and os.environ.get("PLX_GEMM_SPLIT_TARGET"):  # A/B knob: split-K planner target
-            handle.plx_gemm256_set_split_target(int(os.environ["PLX_GEMM_SPLIT_TARGET"]))
-        if name == "plx_gemm" and os.environ.get("PLX_GEMM_GROUP"):  # A/B knob: M-tiles per tile group
-            handle.plx_gemm256_set_group(int(os.environ["PLX_GEMM_GROUP"]))
+        if name == "plx_conv" and os.environ.get("PLX_WGRAD_ATOMIC"):  # A/B knob: 0 = slab reducer (deterministic)
+            handle.plx_set_tn_atomic(int(os.environ["PLX_WGRAD_ATOMIC"]))
         if name == "plx_gemm" and os.environ.get("PLX_GEMM_WAVES"):  # 8 = ping-pong kernel, 4 = AGPR 4-wave kernel
             handle.plx_gemm256_set_waves(int(os.environ["PLX_GEMM_WAVES"]))
-        if name == "plx_conv" and os.environ.get("PLX_TN_PLAN"):  # A/B knob: "blocks_per_cu,slab_mb"
-            bpc, mb = (int(v) for v in os.environ["PLX_TN_PLAN"].split(","))
-            handle.plx_set_tn_plan(bpc, mb)
-        if name == "plx_conv" and os.environ.get("PLX_TN_SIZES"):  # A/B knob: "big,mid" blocks per CU
-            big, mid = (int(v) for v in os.environ["PLX_TN_SIZES"].split(","))
-            handle.plx_set_tn_sizes(big, mid)
         _loaded[name] = handle
         return handle
 
@@ -254,8 +214,6 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_stem_bn_pool_forward": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _P, _I, _P,
                                      _P],
         "plx_stem_bn_pool_bwd_workspace": [_I, _I, _I, _I],
-        "plx_set_stem_bwd_cap": [_I],
-        "plx_set_bn_fin_threads": [_I],
         "plx_stem_bn_pool_backward": [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     },
     "plx_procmon": {
@@ -283,23 +241,13 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
     },
     "plx_conv": {
         "plx_gemm_nt": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P],
-        "plx_gemm_nt_prologue": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
         "plx_gemm_nt_rows_per_block": [_I],
         "plx_gemm_tn_workspace": [_I, _I, _I, _I],
-        "plx_set_tn_plan": [_I, _I],
-        "plx_set_tn_sizes": [_I, _I],
-        "plx_set_nt_single_stage": [_I],
-        "plx_set_halo": [_I],
-        "plx_set_tap_inner": [_I],
-        "plx_set_tn_stages": [_I, _I],
-        "plx_set_tn_wide": [_I],
         "plx_set_tn_v2": [_I, _I],
-        "plx_set_tn2_bpc": [_I],
-        "plx_set_tn2_slab_bw": [_I],
         "plx_set_tn2_stem": [_I],
         "plx_set_tn2_c64": [_I],
+        "plx_set_tn_atomic": [_I],
         "plx_tn_plan_slices": [_I, _I, _I, _I, _I],
-        "plx_set_nt_tall": [_I, _I],
         "plx_gemm_tn": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P],
         "plx_weight_prep": [_P, _P, _P, _I, _I, _P],
         "plx_weight_prepk": [_P, _L, _L, _L, _L, _P, _P, _I, _I, _I, _P],
@@ -363,7 +311,6 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_add_rms_forward": [_P, _P, _P, _P, _P, _P, _L, _I, _F, _P],
         "plx_add_rms_backward": [_P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
         "plx_add_ln_backward": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _L, _I, _P],
-        "plx_set_ln_wave": [_I],
         "plx_partial_colsum_workspace": [_I, _I, _I],
         "plx_partial_colsum": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _P],
         "plx_rms_backward": [_P, _P, _P, _P, _P, _P, _L, _I, _P],
@@ -394,7 +341,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_partial_colsum_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_sizes": None, "plx_set_tn_v2": None, "plx_set_tn2_bpc": None, "plx_set_tn2_slab_bw": None, "plx_set_tn2_stem": None, "plx_set_tn2_c64": None, "plx_set_tn_stages": None, "plx_set_nt_tall": None, "plx_set_tap_inner": None, "plx_set_stem_bwd_cap": None, "plx_set_bn_fin_threads": None, "plx_set_ln_wave": None, "plx_set_adamw_grid_cap": None, "plx_set_adamw_wide": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_partial_colsum_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_v2": None, "plx_set_tn2_stem": None, "plx_set_tn2_c64": None, "plx_set_tn_atomic": None, "plx_set_adamw_grid_cap": None, "plx_set_adamw_wide": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

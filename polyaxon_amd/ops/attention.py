@@ -15,7 +15,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 from typing import Optional
 
 import torch
@@ -88,20 +87,17 @@ def _reference(q, k, v, causal, scale):
     return o.transpose(1, 2)
 
 
-_KNOBS_SET = False
+_CHECKED = False
 
 
 def _lib():
-    """The attention library with its A/B knobs applied once (PLX_ATTN_FWD_WAVES / PLX_ATTN_DQ_WAVES /
-    PLX_ATTN_DKDV_WAVES: 8 (default) or 4 waves per forward / dQ / dK-dV workgroup)."""
-    global _KNOBS_SET
+    """The attention library, its argument-block layout checked once against this module's (8 waves per forward /
+    dQ / dK-dV workgroup; the 4-wave variants stay reachable for the tests through plx_attn_set_*_waves)."""
+    global _CHECKED
     lib = _native.lib("plx_attn")
-    if not _KNOBS_SET:
+    if not _CHECKED:
         _check(lib.plx_attn_args_size())
-        lib.plx_attn_set_fwd_waves(int(os.environ.get("PLX_ATTN_FWD_WAVES", "8")))
-        lib.plx_attn_set_dq_waves(int(os.environ.get("PLX_ATTN_DQ_WAVES", "8")))
-        lib.plx_attn_set_dkdv_waves(int(os.environ.get("PLX_ATTN_DKDV_WAVES", "8")))
-        _KNOBS_SET = True
+        _CHECKED = True
     return lib
 
 

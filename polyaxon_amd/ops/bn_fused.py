@@ -8,7 +8,6 @@ With ReLU the forward also writes a 1-bit-per-element mask (1/16 of ``y``); the 
 from __future__ import annotations
 
 import ctypes
-import os
 
 from typing import Optional
 
@@ -19,22 +18,16 @@ from polyaxon_amd.ops.conv1x1 import BnLink
 from polyaxon_amd.ops.flat import direct_grad
 
 
-_MASKED_RESGRAD = os.environ.get("PLX_MASKED_RESGRAD", "1") != "0"  # A/B knob (scripts/gpu.sh ab)
-
-
 def _stream() -> int:
     return _native.current_stream()
 
 
 _COUNTERS = {}
-_FUSED_FINALIZE = os.environ.get("PLX_BN_FUSED_FINALIZE", "1") != "0"  # A/B knob
 
 
 def _counters(dev: torch.device):
     """Zeroed ticket counters of the one-launch reduce + finalize (csrc/bn_kernels.hip ``reduce_l2_last``), one
     array per (device, stream): launches sharing it are stream-ordered and each leaves it zeroed again."""
-    if not _FUSED_FINALIZE:
-        return None
     key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
     t = _COUNTERS.get(key)
     if t is None:
@@ -138,7 +131,7 @@ class _BNAct(torch.autograd.Function):
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         # identity block: the residual's gradient dz = dy * mask is not written here; dy and the mask ride into
         # conv1's dgrad epilogue (GradMailbox.put_masked), which adds them
-        masked_box = _MASKED_RESGRAD and ctx.box is not None and ctx.relu and mask is not None
+        masked_box = ctx.box is not None and ctx.relu and mask is not None
         dres = (torch.empty_like(x, memory_format=torch.channels_last)
                 if ctx.has_res and not masked_box else None)
         if ctx.direct is not None:

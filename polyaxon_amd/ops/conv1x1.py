@@ -15,7 +15,6 @@ gradient comes back in fp32, so autocast's bf16 weight copy and its backward cas
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Dict
 
 import torch
@@ -115,10 +114,6 @@ def weight_prep(w: torch.Tensor):
     rc = _native.lib("plx_conv").plx_weight_prep(w32.data_ptr(), wb.data_ptr(), wt.data_ptr(), cout, cin, _stream())
     _native.check(rc, "plx_weight_prep")
     return wb, wt
-
-
-# PLX_SPLIT_LINK=0: the BatchNorm feeding a ResNet downsampling block reduces its own backward partials (A/B knob)
-_SPLIT_LINK = os.environ.get("PLX_SPLIT_LINK", "1") != "0"
 
 
 class GradMailbox:
@@ -288,7 +283,7 @@ class _Conv1x1(torch.autograd.Function):
             rows = nt_stats_rows(cin)
             if ctx.link is not None and ctx.sink is None and (ctx.box is None or extra is not None):
                 bnr = ctx.link.request(-(-(n * h * w) // rows))
-            elif ctx.link is not None and ctx.sink is not None and ctx.sink.s2k1 and extra is None and _SPLIT_LINK:
+            elif ctx.link is not None and ctx.sink is not None and ctx.sink.s2k1 and extra is None:
                 bnr = ctx.link.request_split(-(-(n * h * w) // rows), -(-(n * ((h + 1) // 2) * ((w + 1) // 2)) // rows))
             gemm_nt(_rows(dy), wt, _rows(dx), add=_rows(extra) if extra is not None else None, bnr=bnr,
                     add_mask=extra_mask)

@@ -211,7 +211,6 @@ def forward(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]
     return torch.addmm(bias.to(x2.dtype), x2, weight.t())
 
 
-_GELU_EPILOGUE = os.environ.get("PLX_GELU_EPILOGUE", "1") != "0"  # A/B knob: 0 = GEMM then a separate F.gelu
 # In `auto`, a forward with the GELU epilogue runs on the kernel (one launch, the activation a second store) instead
 # of hipBLASLt + a separate GELU pass.  In the GPT-2 step that was equal on one box (717.8k / 719.9k vs 717.8k /
 # 718.2k tokens/s) and +0.2-0.3 % on another (706.6k / 705.8k vs 704.5k / 704.5k), profiles/r5_gelu_native_ab.jsonl.
@@ -225,9 +224,9 @@ def forward_gelu(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Te
     T, fin = x2.shape
     N = weight.shape[0]
     native = _use_native(T, N, fin, True, True)
-    if not native and _GELU_NATIVE and mode() == "auto" and _GELU_EPILOGUE and supported(T, N, fin):
+    if not native and _GELU_NATIVE and mode() == "auto" and supported(T, N, fin):
         _seen[(T, N, fin, True, True)] = native = _LAYOUT_SCHEDULE[_FWD]  # decisions() reports what runs
-    if _GELU_EPILOGUE and x2.is_cuda and supported(T, N, fin) and native:
+    if x2.is_cuda and supported(T, N, fin) and native:
         h = torch.empty(T, N, dtype=torch.bfloat16, device=x2.device)
         a = torch.empty_like(h)
         gemm(x2, weight, T, N, fin, True, True, out=h, bias=bias, gelu_out=a)

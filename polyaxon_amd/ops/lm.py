@@ -216,7 +216,6 @@ def class_xent(logits: torch.Tensor, labels: torch.Tensor, in_range: bool = Fals
 
 
 # ---------------------------------------------------------------------------------------------- bias gradient
-_COLSUM = os.environ.get("PLX_COLSUM", "1") != "0"  # A/B knob: 0 = torch's column reduction
 
 
 def bias_grad(dy2: torch.Tensor, bias: torch.Tensor, gelu_h: Optional[torch.Tensor] = None):
@@ -237,7 +236,7 @@ def bias_grad(dy2: torch.Tensor, bias: torch.Tensor, gelu_h: Optional[torch.Tens
                                  and slot.device == dy2.device):
         slot = None
     acc = bool(bias._plx_flat.mark_written(slot)) if slot is not None else False
-    native = (_COLSUM and _native_ok(dy2) and dy2.is_contiguous() and N % 8 == 0 and dy2.data_ptr() % 16 == 0
+    native = (_native_ok(dy2) and dy2.is_contiguous() and N % 8 == 0 and dy2.data_ptr() % 16 == 0
               and T > 0 and (N + 63) // 64 <= 4096 and (slot is not None or bias.dtype in (torch.float32, torch.bfloat16)))
     if gelu_h is not None:
         native = (native and gelu_h.dtype == torch.bfloat16 and gelu_h.is_contiguous() and gelu_h.shape == dy2.shape

@@ -5,7 +5,6 @@ gather (each input pixel sums the dy of the <= 4 windows whose argmax it is), so
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
@@ -97,7 +96,6 @@ class _GlobalAvgPoolNHWC(torch.autograd.Function):
 def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
     """x.mean((2, 3)) for a 4-D tensor; the NHWC-native autograd function when x is channels_last (and not NCHW
     contiguous, i.e. C > 1 and H * W > 1)."""
-    if (x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)
-            and os.environ.get("PLX_NHWC_AVGPOOL", "1") != "0"):
+    if x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last):
         return _GlobalAvgPoolNHWC.apply(x)
     return x.mean((2, 3))

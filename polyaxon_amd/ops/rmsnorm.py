@@ -2,7 +2,6 @@
 statistics and parameters), PyTorch composition otherwise."""
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -19,9 +18,6 @@ def _stream() -> int:
     return _native.current_stream()
 
 
-_NORM_DIRECT = os.environ.get("PLX_NORM_DIRECT", "1") != "0"  # A/B knob: 0 = return the sums to autograd
-
-
 def _param_grads(parts, params, d: int):
     """Column sums of the backward kernel's fp32 [nb, d] partial matrices (one per parameter) in one launch
     (csrc/rmsnorm.hip plx_partial_colsum).  A parameter with a direct fp32 flat-gradient slot (ops/flat.py) gets its
@@ -35,7 +31,7 @@ def _param_grads(parts, params, d: int):
     nb = parts[0].shape[0]
     outs, accs, ret = [], [], []
     for p in params:
-        slot = direct_grad(p) if _NORM_DIRECT else None
+        slot = direct_grad(p)
         if (slot is not None and slot.dtype == torch.float32 and slot.is_contiguous() and slot.numel() == d
                 and slot.device == dev):
             accs.append(int(p._plx_flat.mark_written(slot)))
@@ -130,8 +126,7 @@ class _AddRMSNorm(torch.autograd.Function):
 def add_rms_norm(x: torch.Tensor, res: torch.Tensor, weight: torch.Tensor, eps: float = 1e-5):
     """(s, y) = (x + res, RMSNorm(s)): the pre-norm residual add fused into the next RMSNorm for bf16 GPU rows; the
     separate add and :func:`rms_norm` otherwise."""
-    if (supported(x) and res.dtype == x.dtype and res.shape == x.shape and x.is_contiguous() and res.is_contiguous()
-            and os.environ.get("PLX_ADD_LN", "1") != "0"):
+    if supported(x) and res.dtype == x.dtype and res.shape == x.shape and x.is_contiguous() and res.is_contiguous():
         return _AddRMSNorm.apply(x, res, weight, eps)
     s = x + res
     return s, rms_norm(s, weight, eps)
@@ -249,13 +244,10 @@ def add_layer_norm(x: torch.Tensor, res: torch.Tensor, weight: torch.Tensor, bia
     """(s, y) = (x + res, LayerNorm(s)): the pre-norm transformer's residual add fused into the next norm for bf16 GPU
     rows of d <= 1024 (one wave per row); the separate add and :func:`layer_norm` otherwise."""
     if (supported(x) and res.dtype == x.dtype and res.shape == x.shape and x.shape[-1] <= 1024 and x.is_contiguous()
-            and res.is_contiguous() and _LN_WAVE):
+            and res.is_contiguous()):
         return _AddLayerNorm.apply(x, res, weight, bias, eps)
     s = x + res
     return s, layer_norm(s, weight, bias, eps)
-
-
-_LN_WAVE = os.environ.get("PLX_LN_WAVE", "1") != "0" and os.environ.get("PLX_ADD_LN", "1") != "0"
 
 
 class LayerNorm(torch.nn.Module):

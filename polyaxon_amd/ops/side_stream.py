@@ -6,8 +6,8 @@ weight gradient is only needed by the optimizer at the end of the step.  The dir
 stream with an event, runs the launch on the device's side stream, and pins the operand tensors to that stream
 (``record_stream``) so the caching allocator does not recycle them early.  :func:`join`, queued as an autograd
 end-of-backward callback (and called again by the executor before the optimizer), makes the main stream wait
-for every side launch.  Inside hipGraph capture the fork and join are captured as graph edges (with
-``PLX_WGRAD_CAPTURE_FORK=0`` capture runs them inline); ``PLX_WGRAD_STREAM=0`` runs every launch inline.
+for every side launch.  Inside hipGraph capture the fork and join are captured as graph edges.  ``PLX_WGRAD_STREAM=0``
+runs every launch inline (A/B: the serialized backward, profiles/r5_backward_contention.md).
 """
 from __future__ import annotations
 
@@ -25,11 +25,6 @@ _ENABLED = os.environ.get("PLX_WGRAD_STREAM", "1") != "0"
 
 def enabled() -> bool:
     return _ENABLED
-
-
-# Inside hipGraph capture the fork / join is captured too (event edges between the two captured streams), so a
-# replayed step keeps the overlap; PLX_WGRAD_CAPTURE_FORK=0 runs the launches inline during capture instead.
-_CAPTURE_FORK = os.environ.get("PLX_WGRAD_CAPTURE_FORK", "1") != "0"
 
 
 def capturing() -> bool:
@@ -54,13 +49,12 @@ def priority_stream(idx: int, priority: int) -> "torch.cuda.Stream":
     return torch.cuda.ExternalStream(handle.value, device=torch.device("cuda", idx))
 
 
-# PLX_WGRAD_PRIORITY=p: the side stream is created with HIP priority p (1 = low, the default; -1 high; empty: the
-# default priority).  HIP keeps a hardware-queue pool per priority level, so a low-priority side stream gets a queue
+# The side stream is created with low HIP priority (1).  HIP keeps a hardware-queue pool per priority level, so a low-priority side stream gets a queue
 # of its own even when the compute stream, RCCL's streams and torch's share the box's 4 (GPU_MAX_HW_QUEUES) normal
 # queues: with a live communicator and 4 queues the default-priority side stream landed on the compute stream's queue
 # and the two serialised (ResNet-50 bench 10.65k / 10.68k trials/h), low priority 11.52k, 8 queues 11.54k
 # (profiles/r5_hw_queues.md)
-_WGRAD_PRIORITY = os.environ.get("PLX_WGRAD_PRIORITY", "1")
+_WGRAD_PRIORITY = 1
 
 
 def _stream_for(dev: torch.device) -> "torch.cuda.Stream":
@@ -70,11 +64,7 @@ def _stream_for(dev: torch.device) -> "torch.cuda.Stream":
         # (a CU-masked side stream, hipExtStreamCreateWithCUMask, was removed in round 5: it cannot take a priority,
         # so it shares the compute stream's hardware queue and serialises with it, -29 %,
         # profiles/r5_wgrad_cumask_ab.jsonl; round 3 measured it slower too)
-        if _WGRAD_PRIORITY:
-            s = priority_stream(idx, int(_WGRAD_PRIORITY))
-        else:
-            s = torch.cuda.Stream(device=idx)
-        _side[idx] = s
+        s = _side[idx] = priority_stream(idx, _WGRAD_PRIORITY)
     return s
 
 
@@ -84,7 +74,7 @@ def stream_for(dev: torch.device) -> "torch.cuda.Stream":
 
 
 def run(fn: Callable[[], None], tensors: Iterable[torch.Tensor], dev: torch.device) -> None:
-    if not enabled() or dev.type != "cuda" or (capturing() and not _CAPTURE_FORK):
+    if not enabled() or dev.type != "cuda":
         fn()
         return
     main = torch.cuda.current_stream(dev)

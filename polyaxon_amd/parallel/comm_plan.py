@@ -21,7 +21,7 @@ instead of a constant tuned for a switched fabric:
 * **Measured at start-up.**  With ``bucket_mb="auto"`` at world > 1, :class:`~polyaxon_amd.parallel.ddp.FlatDDP`
   first times a few all-reduces on the trial's own communicator (:func:`calibrate`: 1-64 MB on the GPU, ~0.1 s),
   averages the times over the ranks (so every rank fits the same numbers and cuts the same buckets) and plans with
-  that fit (``source: "measured"``).  ``PLX_COMM_CALIBRATE=0`` keeps the analytic link model.
+  that fit (``source: "measured"``).
 * **Measured table.**  ``python -m torch.distributed.run --nproc-per-node W -m polyaxon_amd.parallel.rccl``
   prints the node's all-reduce algbw per message size; :func:`fit_table` turns those rows into (alpha, busbw) by a
   least-squares fit of ``t(B) = a + b B``, and ``PLX_COMM_TABLE=<that JSON>`` makes :func:`plan` use the fit for

@@ -140,10 +140,6 @@ class FlatDDP:
         self.opt = optimizer
         if optimizer is not None:
             optimizer.in_backward = True
-            if flat.params.is_cuda:  # A/B knob: block cap of the in-backward update (csrc/train_kernels.hip)
-                from polyaxon_amd.ops import _native
-
-                _native.lib("plx_train").plx_set_adamw_grid_cap(int(os.environ.get("PLX_OPT_BWD_GRID", "2048")))
         self._side = torch.cuda.Stream(device=flat.device) if (optimizer is not None and flat.params.is_cuda) else None
         self.stepped = 0
         if flat.lp_params is None:
@@ -179,20 +175,19 @@ class FlatDDP:
             self._comm = _comm.acquire(process_group, flat.device)
             if not self._comm.synchronous and not shard_optimizer:
                 self._comm_stream = torch.cuda.Stream(device=flat.device)
-        # an average in the collective (RCCL's AVG: a pre-multiplied sum) vs SUM + our own 1/W scale; PLX_DDP_AVG=0
-        # selects the latter (A/B, read by RcclComm.native_avg)
+        # an average in the collective (RCCL's AVG: a pre-multiplied sum) where the backend has one, else SUM + our
+        # own 1/W scale (the gloo shim)
         if self._comm is not None:
             self.avg_supported = bool(self._comm.native_avg)
         else:
-            self.avg_supported = self.nccl and os.environ.get("PLX_DDP_AVG", "1") != "0"
+            self.avg_supported = self.nccl
         self.plan = None
         if bucket_mb is None or bucket_mb == "auto":
             from polyaxon_amd.parallel.comm_plan import plan as _plan
 
             elem = 2 if flat.lp_grads is not None else 4  # bytes per gradient element on the wire (bf16 / fp32)
             model = None
-            if (self.world > 1 and self._comm is not None and not os.environ.get("PLX_COMM_TABLE")
-                    and os.environ.get("PLX_COMM_CALIBRATE", "1") != "0"):
+            if self.world > 1 and self._comm is not None and not os.environ.get("PLX_COMM_TABLE"):
                 # the node's own link, timed on this trial's communicator (same fit on every rank)
                 from polyaxon_amd.parallel.comm_plan import calibrate
 

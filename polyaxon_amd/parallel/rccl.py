@@ -48,8 +48,7 @@ class RcclComm:
     (/root/reference/polyaxon/signals/experiments.py:252-281)."""
 
     synchronous = False  # collectives are enqueued on the current HIP stream
-    # RCCL's AVG (a pre-multiplied sum) vs SUM + the caller's 1/W scale (PLX_DDP_AVG=0, A/B)
-    native_avg = os.environ.get("PLX_DDP_AVG", "1") != "0"
+    native_avg = True  # RCCL's AVG (a pre-multiplied sum) rather than SUM + the caller's 1/W scale
 
     def __init__(self, unique_id: bytes, nranks: int, rank: int, device: int, timeout_s: float = None,
                  init_timeout_s: float = None):

@@ -21,14 +21,12 @@ The same class runs on CPU (no graph, reference kernels) for the unit tests.
 """
 from __future__ import annotations
 
-import os
 import time
 from dataclasses import dataclass
 from typing import Callable, Dict, Optional, Tuple
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from polyaxon_amd.ops import _native, side_stream
 from polyaxon_amd.ops.flat import FlatParams
@@ -74,28 +72,18 @@ class ResidentTrialExecutor:
             raise ValueError(f"unknown optimizer {optimizer!r}")
         # default: cross entropy of the fp32-cast logits; on the GPU in one fused HIP kernel each way (ops/lm.py
         # class_xent: no fp32 logits copy, log-softmax or NLL kernels between the head GEMM and its backward, where the
-        # host launching them was the bottleneck of the forward -> backward hand-off).  PLX_CLASS_XENT=0: F.cross_entropy
-        default_loss = loss_fn is None
+        # host launching them was the bottleneck of the forward -> backward hand-off; +0.1-0.2 %, r5_class_xent_ab.jsonl)
         # labels guaranteed inside [0, classes): the executor's own synthetic source with no more classes than the
         # head has outputs -- the fused kernels then skip F.cross_entropy's valid-row count
         fc = getattr(model, "fc", None)
         self._labels_in_range = (hasattr(batch, "next") and isinstance(getattr(batch, "classes", None), int)
                                  and isinstance(fc, nn.Linear) and batch.classes <= fc.out_features)
-        if loss_fn is None and os.environ.get("PLX_CLASS_XENT", "1") != "0":
+        if loss_fn is None:
             from polyaxon_amd.ops.lm import class_xent
 
             in_range = self._labels_in_range
             loss_fn = lambda out, y: class_xent(out, y, in_range=in_range)  # noqa: E731
-        self.loss_fn = loss_fn or (lambda out, y: F.cross_entropy(out.float(), y))
-        # Fused classifier head (ops/head.py): a model with forward_features / forward_head and an nn.Linear fc, the
-        # default cross entropy and bf16 autocast on the GPU run the head's forward and backward in the forward
-        # pass and start autograd at the features.  PLX_FUSED_HEAD=0: through autograd
-        self._fused_head = (default_loss and self.is_cuda and amp_dtype == torch.bfloat16
-                            and hasattr(model, "forward_features") and hasattr(model, "forward_head")
-                            and isinstance(getattr(model, "fc", None), nn.Linear)
-                            and os.environ.get("PLX_FUSED_HEAD", "1") != "0")
-        self._ones = torch.ones(1, dtype=torch.float32, device=self.device) if self._fused_head else None
-        self.fused_head_steps = 0
+        self.loss_fn = loss_fn
         # ``batch`` is either a fixed (x, y) pair or a data source with in-place ``next()`` (ops/synth.py) that the
         # step refills before every forward: a fresh device-generated batch per step, inside the captured graph
         self.data = batch if hasattr(batch, "next") else None
@@ -113,13 +101,10 @@ class ResidentTrialExecutor:
         # Eager device path: batch k+1 is generated on the side stream while step k's backward ends (the side
         # stream idles once its last weight gradient is done, beside the main stream's stem chain and optimizer),
         # into the other of two batch buffers; step k+1's forward waits on an event instead of running the
-        # generator.  A graph-captured step keeps the generator inside the graph.  PLX_PREFETCH_BATCH=0: off.
+        # generator.  A graph-captured step keeps the generator inside the graph.  (Queueing batch k+1 at the start of
+        # step k instead, beside the forward, measured no better; removed in round 6.)
         self._prefetch = (self.is_cuda and not self.use_graph and self.data is not None
-                          and hasattr(self.data, "next_into") and side_stream.enabled()
-                          and os.environ.get("PLX_PREFETCH_BATCH", "1") != "0")
-        # PLX_PREFETCH_AT=start: queue batch k+1 on the side stream at the start of step k (it runs beside the
-        # forward, where the side stream is otherwise idle) instead of after the backward (beside its tail)
-        self._prefetch_at_start = os.environ.get("PLX_PREFETCH_AT", "end") == "start"
+                          and hasattr(self.data, "next_into") and side_stream.enabled())
         self._bufs = None          # [(x, y), (x, y)] when prefetching
         self._cur = 0              # buffer the next step consumes
         self._ready = None         # event after the generator wrote self._bufs[self._cur], or None
@@ -127,9 +112,9 @@ class ResidentTrialExecutor:
         self.graph_rejected = False
         self.graph_check_error: Optional[float] = None
         self.snapshots: Dict[object, TrialState] = {}
-        # bf16 operands of every native conv from one launch per step (ops/wcache.py); PLX_WCACHE=0: per layer
+        # bf16 operands of every native conv from one launch per step (ops/wcache.py)
         self.wcache = None
-        if self.is_cuda and os.environ.get("PLX_WCACHE", "1") != "0":
+        if self.is_cuda:
             cache = ConvWeightCache(model, self.flat.params)
             self.wcache = cache if len(cache) else None
         self.model.train()
@@ -179,29 +164,12 @@ class ResidentTrialExecutor:
             # every earlier step's use of the other buffer is complete in main-stream order from here
             step_start = torch.cuda.Event()
             step_start.record(main)
-            if self._prefetch_at_start:
-                self._queue_next_batch(step_start)
         elif self.data is not None:
             self.data.next()
         if self.wcache is not None:
             self.wcache.activate()
         try:
-            # not under DP: the fused head writes fc's gradient slots itself, so FlatDDP's post-accumulate hooks for fc
-            # would never fire and its bucket would only launch in finish(), without overlap
-            if self._fused_head and self.ddp is None:
-                from polyaxon_amd.ops import head
-
-                with torch.autocast("cuda", dtype=self.amp_dtype):
-                    feats = self.model.forward_features(self.x)
-                if head.supported(feats, self.model.fc, self.y, self._labels_in_range):
-                    loss, dfeat = head.classifier_head_step(feats.detach(), self.model.fc, self.y, self._ones)
-                    feats.backward(dfeat)
-                    self.fused_head_steps += 1
-                else:
-                    with torch.autocast("cuda", dtype=self.amp_dtype):
-                        loss = self.loss_fn(self.model.forward_head(feats), self.y)
-                    loss.backward()
-            elif self.amp_dtype is not None:
+            if self.amp_dtype is not None:
                 with torch.autocast("cuda", dtype=self.amp_dtype):
                     out = self.model(self.x)
                     loss = self.loss_fn(out, self.y)
@@ -216,7 +184,7 @@ class ResidentTrialExecutor:
         side_stream.join(self.device)  # weight-gradient GEMMs overlapped on the side stream (ops/side_stream.py)
         if self.ddp is not None:
             self.ddp.finish()  # the gang's averaged gradients
-        if prefetch and not self._prefetch_at_start:
+        if prefetch:
             # queued after the join: the main stream does not wait for it before the optimizer
             self._queue_next_batch(step_start)
         self.opt.step_()
@@ -324,27 +292,12 @@ class ResidentTrialExecutor:
     def set_hparams(self, **hp) -> None:
         self.opt.set_hparams(**{k: v for k, v in hp.items() if k in self.opt.HP})
 
-    _main_stream = None
-
     def run(self, n_steps: int) -> None:
-        hp = os.environ.get("PLX_MAIN_PRIORITY", "")
-        if not (hp and self.is_cuda and self.graph is None):
-            for _ in range(n_steps):
-                if self.graph is not None:
-                    self.graph.replay()
-                else:
-                    self._train_step()
-            return
-        # PLX_MAIN_PRIORITY=p: the eager steps run on a stream of HIP priority p (-1 = high), forked from and joined
-        # back into the caller's stream, so the critical path's workgroups are dispatched ahead of the side stream's
-        if self._main_stream is None:
-            self._main_stream = side_stream.priority_stream(self.device.index or 0, int(hp))
-        cur = torch.cuda.current_stream(self.device)
-        self._main_stream.wait_stream(cur)
-        with torch.cuda.stream(self._main_stream):
-            for _ in range(n_steps):
+        for _ in range(n_steps):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
                 self._train_step()
-        cur.wait_stream(self._main_stream)
 
     def commit(self, out: torch.Tensor, slot: int, window: int = 10) -> None:
         """out[slot] = mean loss over the last ``window`` steps, computed on the device."""

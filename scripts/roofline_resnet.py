@@ -33,7 +33,6 @@ def main() -> None:
     ap.add_argument("--bn-apply-only", type=int, default=0, help="also time the apply pass alone")
     ap.add_argument("--bn-counters", type=int, default=1, help="A/B knob: 1 = fused BN reduce+finalize (ticket "
                     "counters), 0 = the two-launch path")
-    ap.add_argument("--nt-single-stage", type=int, default=5, help="A/B knob: NT GEMM single-buffer mode (conv_gemm.hip nt_single)")
     a = ap.parse_args()
     import torch
 
@@ -44,7 +43,6 @@ def main() -> None:
     conv = _native.lib("plx_conv")
     bn = _native.lib("plx_bn")
     cus = _num_cus(dev)
-    conv.plx_set_nt_single_stage(a.nt_single_stage)
     zero = _zero_page(dev).data_ptr()
     st = torch.cuda.current_stream().cuda_stream
     cnt = torch.zeros(64, dtype=torch.int32, device=dev)  # BatchNorm reduce + finalize tickets

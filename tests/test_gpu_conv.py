@@ -400,181 +400,45 @@ def test_stem_conv_matches_conv2d(cuda, shape):
     torch.testing.assert_close(conv.weight.grad, w.grad, rtol=3e-2, atol=3e-2 * float(w.grad.abs().max()))
 
 
-@pytest.mark.parametrize("shape,cout", [((2, 64, 56, 56), 64), ((2, 128, 28, 28), 128), ((3, 256, 14, 14), 256),
-                                        ((5, 512, 7, 7), 512), ((1, 64, 3, 17), 128), ((3, 192, 9, 5), 64)])
-def test_conv3x3_halo_matches_gather_and_fp32(cuda, shape, cout):
-    """Halo mode (the input rows staged once per 64-channel chunk, read by all 9 taps at a row shift) against the
-    per-tap gather and an fp32 F.conv2d: forward and data gradient, ResNet-50 stage shapes plus ragged ones (partial
-    last tile, images narrower than a tile, several chunks)."""
-    from polyaxon_amd.ops import _native
-    from polyaxon_amd.ops.conv import ConvKxK
-
-    lib = _native.lib("plx_conv")
-    torch.manual_seed(11)
-    conv = ConvKxK(shape[1], cout, 3, 1).to(cuda)
-    conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
-    x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    out = {}
-    try:
-        for halo in (1, 0):
-            lib.plx_set_halo(halo)
-            xa = x.clone().requires_grad_()
-            y = conv(xa)
-            g = torch.ones_like(y) * 0.01 + torch.randn(y.shape, device=cuda, generator=torch.Generator(
-                device=cuda).manual_seed(3)).to(y.dtype)
-            y.backward(g)
-            out[halo] = (y.float(), xa.grad.float(), g)
-    finally:
-        lib.plx_set_halo(int(os.environ.get("PLX_HALO", "0")))
-    xr = x.float().clone().requires_grad_()
-    yr = F.conv2d(xr, conv.weight.detach().to(torch.bfloat16).float(), padding=1)
-    yr.backward(out[1][2].float())
-    for halo in (1, 0):
-        torch.testing.assert_close(out[halo][0], yr, rtol=2e-2, atol=8e-2)
-        torch.testing.assert_close(out[halo][1], xr.grad, rtol=2e-2, atol=8e-2)
-    # same bf16 rounding points, different fp32 summation order: tight agreement between the two native paths
-    torch.testing.assert_close(out[1][0], out[0][0], rtol=1e-2, atol=2e-2)
-    torch.testing.assert_close(out[1][1], out[0][1], rtol=1e-2, atol=2e-2)
-
-
-def test_tall_nt_tiles_match_default_tiles(cuda):
-    """256x128 NT tiles (plx_set_nt_tall 2: forward and data gradient) against the default 128x128 tiles and fp32: the
-    plain GEMM with channel stats (partial rows stay in 128-row units: the tall block zero-fills its second row), a
-    3x3 convolution forward, and a conv -> BN chain whose BN-backward partials come from the dgrad epilogue."""
-    from polyaxon_amd.ops import _native
-    from polyaxon_amd.ops.conv import ConvKxK
-    from polyaxon_amd.ops.conv1x1 import gemm_nt, nt_stats_rows
-
-    lib = _native.lib("plx_conv")
-    torch.manual_seed(11)
-    m, n, k = 256 * 600 + 77, 128, 192  # >= 512 tall blocks, ragged last block
-    a, b = _bf(m, k, dev=cuda), _bf(n, k, dev=cuda)
-    rows = nt_stats_rows(n)
-    nblk = -(-m // rows)
-    res = {}
-    try:
-        for tall in (0, 2):
-            lib.plx_set_nt_tall(tall, 64)
-            stats = torch.full((2 * nblk * n,), float("nan"), device=cuda)
-            out = gemm_nt(a, b, stats=stats)
-            st = stats.view(2, nblk, n).sum(1)
-            # 32 x 64 x 64 pixels = 512 tall blocks: the 3x3 forward and its data gradient both take the tall tile
-            res[tall] = (out.float(), st, _bn_chain_grads(cuda, lambda: ConvKxK(128, 128, 3, 1), (32, 128, 64, 64),
-                                                          link=True))
-    finally:
-        lib.plx_set_nt_tall(0, 1024)
-    ref = a.float() @ b.float().t()
-    torch.testing.assert_close(res[2][0], ref, rtol=2e-2, atol=2e-2 * k ** 0.5)
-    torch.testing.assert_close(res[2][0], res[0][0], rtol=0, atol=0)  # same MFMA order per output element
-    o = res[2][0]
-    torch.testing.assert_close(res[2][1][0], o.sum(0), rtol=1e-4, atol=1e-1)
-    torch.testing.assert_close(res[2][1][1], o.square().sum(0), rtol=1e-4, atol=1e0)
-    for x2, x0, name in zip(res[2][2], res[0][2], ("dx", "dgamma", "dbeta", "dw")):
-        torch.testing.assert_close(x2, x0, rtol=1e-2, atol=1e-2 * float(x0.abs().max()), msg=name)
-
-
-@pytest.mark.parametrize("stages,bk", [(2, 64), (3, 64), (4, 64), (3, 32), (4, 32)])
-def test_gemm_tn_stage_rings(cuda, stages, bk):
-    """Every weight-gradient LDS ring (plx_set_tn_stages: depth 2-4, 64- or 32-row stages) against fp32, dense and
-    the 3x3 gather (conv wgrad), with ragged reductions."""
-    from polyaxon_amd.ops import _native
-    from polyaxon_amd.ops.conv import ConvKxK
-    from polyaxon_amd.ops.conv1x1 import gemm_tn
-
-    lib = _native.lib("plx_conv")
-    lib.plx_set_tn_stages(stages, bk)
-    try:
-        torch.manual_seed(2)
-        for m, n1, n2 in ((5000, 128, 128), (777, 64, 256), (20000, 256, 64)):
-            a, b = _bf(m, n1, dev=cuda), _bf(m, n2, dev=cuda)
-            torch.testing.assert_close(gemm_tn(a, b), a.float().t() @ b.float(), rtol=1e-3, atol=1e-3 * m ** 0.5)
-        conv = ConvKxK(64, 128, 3, 1).to(cuda)
-        x = torch.randn(4, 64, 17, 13, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        y = conv(x.requires_grad_())
-        g = torch.randn_like(y.float())
-        y.backward(g.to(torch.bfloat16))
-    finally:
-        lib.plx_set_tn_stages(2, 64)
-    w = conv.weight.detach().float().requires_grad_()
-    F.conv2d(x.detach().float(), w, None, 1, 1).backward(g)
-    torch.testing.assert_close(conv.weight.grad.float(), w.grad, rtol=2e-2, atol=2e-2 * float(w.grad.abs().max()))
-
-
-def test_gemm_tn_wide_tiles(cuda):
-    """Wide weight-gradient tiles (plx_set_tn_wide: 256x128 and 128x256 with 32-row stages) against fp32: dense shapes
-    that take each orientation (ragged reductions), and a 3x3 convolution weight gradient whose 256-channel taps take
-    the 128x256 tile through the gather."""
-    from polyaxon_amd.ops import _native
-    from polyaxon_amd.ops.conv import ConvKxK
-    from polyaxon_amd.ops.conv1x1 import gemm_tn
-
-    lib = _native.lib("plx_conv")
-    lib.plx_set_tn_wide(1)
-    try:
-        torch.manual_seed(3)
-        for m, n1, n2 in ((50000 + 37, 256, 128), (40000 + 5, 128, 512), (30000, 512, 256), (777, 256, 256)):
-            a, b = _bf(m, n1, dev=cuda), _bf(m, n2, dev=cuda)
-            torch.testing.assert_close(gemm_tn(a, b), a.float().t() @ b.float(), rtol=1e-3, atol=1e-3 * m ** 0.5)
-        conv = ConvKxK(256, 128, 3, 1).to(cuda)
-        x = torch.randn(8, 256, 30, 29, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        y = conv(x.requires_grad_())
-        g = torch.randn_like(y.float())
-        y.backward(g.to(torch.bfloat16))
-    finally:
-        lib.plx_set_tn_wide(0)
-    w = conv.weight.detach().float().requires_grad_()
-    F.conv2d(x.detach().float(), w, None, 1, 1).backward(g)
-    torch.testing.assert_close(conv.weight.grad.float(), w.grad, rtol=2e-2, atol=2e-2 * float(w.grad.abs().max()))
-
-
-
-
 @pytest.mark.parametrize("shape,cout,stride", [((2, 128, 28, 28), 128, 1), ((3, 256, 14, 14), 256, 1),
                                                ((5, 512, 7, 7), 512, 1), ((3, 128, 9, 11), 128, 1),
                                                ((2, 128, 14, 14), 128, 2), ((3, 256, 13, 9), 256, 2),
                                                ((2, 64, 9, 7), 128, 1), ((2, 128, 5, 5), 384, 2)])
-def test_conv_tap_order(cuda, shape, cout, stride):
-    """Both reduction orders of the implicit-GEMM convolutions (plx_set_tap_inner: channel block outer / tap inner,
-    the default, and tap-major) against fp32 F.conv2d: forward with the BN channel-stat epilogue, data gradient
-    (stride 2: the parity-class GEMMs with scattered rows) and ragged last tiles."""
-    from polyaxon_amd.ops import _native
+def test_conv_implicit_gemm_matches_fp32(cuda, shape, cout, stride):
+    """The implicit-GEMM 3x3 convolution (tap-inner reduction order) against fp32 F.conv2d: forward with the BN
+    channel-stat epilogue, data gradient (stride 2: the parity-class GEMMs with scattered rows) and ragged last tiles.
+    (Round 6 removed the tap-major order, measured slower.)"""
     from polyaxon_amd.ops.conv import ConvKxK, conv_k
 
-    lib = _native.lib("plx_conv")
     torch.manual_seed(13)
     conv = ConvKxK(shape[1], cout, 3, stride).to(cuda)
     conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
     x = torch.randn(shape, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     g = torch.randn((shape[0], cout, (shape[2] - 1) // stride + 1, (shape[3] - 1) // stride + 1), device=cuda)
     g = g.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    res = {}
-    try:
-        for ti in (1, 0):
-            lib.plx_set_tap_inner(ti)
-            xa = x.clone().requires_grad_()
-            y = conv_k(xa, conv.weight, stride, with_stats=True)
-            st, nblk = y._plx_channel_stats
-            y.backward(g)
-            res[ti] = (y.float(), st.view(2, nblk, cout).sum(1), xa.grad.float())
-    finally:
-        lib.plx_set_tap_inner(int(os.environ.get("PLX_TAP_INNER", "1")))
+    xa = x.clone().requires_grad_()
+    y = conv_k(xa, conv.weight, stride, with_stats=True)
+    st, nblk = y._plx_channel_stats
+    y.backward(g)
+    y, st, dx = y.float(), st.view(2, nblk, cout).sum(1), xa.grad.float()
     xr = x.float().clone().requires_grad_()
     yr = F.conv2d(xr, conv.weight.detach().to(torch.bfloat16).float(), stride=stride, padding=1)
     yr.backward(g.float())
-    for key, (y, st, dx) in res.items():
-        torch.testing.assert_close(y, yr, rtol=2e-2, atol=8e-2, msg=str(key))
-        torch.testing.assert_close(dx, xr.grad, rtol=2e-2, atol=8e-2, msg=str(key))
-        yf = y.permute(0, 2, 3, 1).reshape(-1, cout)
-        torch.testing.assert_close(st[0], yf.sum(0), rtol=1e-3, atol=1e-1, msg=str(key))
-        torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1, msg=str(key))
+    torch.testing.assert_close(y, yr, rtol=2e-2, atol=8e-2)
+    torch.testing.assert_close(dx, xr.grad, rtol=2e-2, atol=8e-2)
+    yf = y.permute(0, 2, 3, 1).reshape(-1, cout)
+    torch.testing.assert_close(st[0], yf.sum(0), rtol=1e-3, atol=1e-1)
+    torch.testing.assert_close(st[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
 
 
-@pytest.mark.parametrize("variant", [(0, -1), (1, 64), (1, 128)], ids=["v1", "v2_64k", "v2_128k"])
+@pytest.mark.parametrize("variant", [(0, -1, 1), (1, 64, 1), (1, 128, 1), (1, 64, 0)],
+                         ids=["v1", "v2_64k_atomic", "v2_128k_atomic", "v2_64k_slabs"])
 def test_wgrad_kernels_every_class(cuda, variant):
-    """Both weight-gradient kernels (plx_set_tn_v2: v1 gemm_tn_kernel; v2 wgrad_kernel with a 64 or 128 KB LDS ring)
-    on every ResNet-50 wgrad class against fp32 F.conv2d weight gradients: dense 1x1 (ragged pixel counts), 3x3
-    stride 1 and 2 (the row gather, taps at the image border), 1x1 stride 2 (downsample), and the 7x7 stem (its own
-    knob plx_set_tn2_stem: v1, v2 on every CU, v2 with the side-stream block target)."""
+    """Both weight-gradient kernels (plx_set_tn_v2: v1 gemm_tn_kernel; v2 wgrad_kernel with a 64 or 128 KB LDS ring,
+    its K slices reduced in the kernel by float atomics or through fp32 slabs + the slab reducer) on every ResNet-50
+    wgrad class against fp32 F.conv2d weight gradients: dense 1x1 (ragged pixel counts, and 56x56 batches planned
+    into ~190 K slices), 3x3 stride 1 and 2 (the row gather, taps at the image border), 1x1 stride 2 (downsample), and
+    the 7x7 stem (its own knob plx_set_tn2_stem: v1, v2 on every CU, v2 with the side-stream block target)."""
     from polyaxon_amd.ops import _native
     from polyaxon_amd.ops.conv import ConvKxK
     from polyaxon_amd.ops.conv1x1 import Conv1x1
@@ -583,10 +447,12 @@ def test_wgrad_kernels_every_class(cuda, variant):
     cases = [("1x1", (4, 256, 14, 14), 64, 1), ("1x1", (3, 64, 17, 11), 256, 1), ("1x1", (2, 512, 7, 9), 1024, 1),
              ("3x3", (2, 64, 28, 28), 64, 1), ("3x3", (3, 128, 13, 9), 128, 1), ("3x3", (2, 256, 14, 14), 256, 2),
              ("3x3", (5, 512, 7, 7), 512, 1), ("1x1", (2, 256, 14, 14), 512, 2), ("1x1", (3, 512, 9, 7), 1024, 2),
-             ("stem", (2, 3, 64, 48), 64, 2)]
+             ("stem", (2, 3, 64, 48), 64, 2), ("1x1", (32, 256, 56, 56), 64, 1), ("1x1", (32, 64, 56, 56), 256, 1),
+             ("3x3", (16, 64, 56, 56), 64, 1), ("3x3", (32, 128, 28, 28), 128, 1)]
     lib = _native.lib("plx_conv")
-    lib.plx_set_tn_v2(*variant)
-    lib.plx_set_tn2_stem({(0, -1): 0, (1, 64): 1, (1, 128): 2}[variant])  # the stem's own kernel choice, all three
+    lib.plx_set_tn_v2(*variant[:2])
+    lib.plx_set_tn_atomic(variant[2])
+    lib.plx_set_tn2_stem({(0, -1): 0, (1, 64): 1, (1, 128): 2}[variant[:2]])  # the stem's own kernel choice, all three
     lib.plx_set_tn2_c64(1 if variant[0] else 0)  # v2's 6-wave configuration (C = 64 3x3) too
     try:
         for kind, shape, cout, stride in cases:
@@ -610,11 +476,38 @@ def test_wgrad_kernels_every_class(cuda, variant):
             got = conv.weight.grad.float()
             torch.testing.assert_close(got, w.grad, rtol=2e-2, atol=2e-2 * float(w.grad.abs().max()),
                                        msg=f"{kind} {shape} -> {cout} s{stride}")
+    finally:  # the defaults
+        lib.plx_set_tn_v2(1, 64)
+        lib.plx_set_tn2_stem(0)
+        lib.plx_set_tn2_c64(1)
+        lib.plx_set_tn_atomic(int(os.environ.get("PLX_WGRAD_ATOMIC", "1")))
+
+
+@pytest.mark.parametrize("atomic", [1, 0])
+def test_wgrad_accumulates_into_a_strided_fp32_slot(cuda, atomic):
+    """plx_gemm_tn with accumulate (the flat fp32 gradient slot the training step adds into): the in-kernel atomic
+    reduction and the slab reducer both add the product to what the slot holds, through a row stride (ldc > N2), and
+    leave the padding columns alone; fp32 reference a.float().T @ b.float()."""
+    from polyaxon_amd.ops import _native
+    from polyaxon_amd.ops.conv1x1 import gemm_tn
+
+    lib = _native.lib("plx_conv")
+    lib.plx_set_tn_atomic(atomic)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(11)
+        for m, n1, n2 in ((200704, 256, 64), (12544, 512, 2048), (1000, 64, 128)):
+            a = torch.randn(m, n1, device="cuda", generator=g).to(torch.bfloat16)
+            b = torch.randn(m, n2, device="cuda", generator=g).to(torch.bfloat16)
+            base = torch.randn(n1, n2 + 64, device="cuda", generator=g)
+            out = base.clone()
+            gemm_tn(a, b, out=out[:, :n2], accumulate=True)
+            torch.cuda.synchronize()
+            ref = base[:, :n2] + a.float().t() @ b.float()
+            torch.testing.assert_close(out[:, :n2], ref, rtol=1e-3, atol=1e-3 * float(ref.abs().max()),
+                                       msg=f"{m}x{n1}x{n2} atomic={atomic}")
+            assert torch.equal(out[:, n2:], base[:, n2:])
     finally:
-        v2, _, kb = os.environ.get("PLX_TN_V2", "1,64").partition(",")
-        lib.plx_set_tn_v2(int(v2), int(kb) if kb else 64)
-        lib.plx_set_tn2_stem(int(os.environ.get("PLX_TN2_STEM", "0")))
-        lib.plx_set_tn2_c64(int(os.environ.get("PLX_TN2_C64", "1")))
+        lib.plx_set_tn_atomic(int(os.environ.get("PLX_WGRAD_ATOMIC", "1")))
 
 
 @pytest.mark.parametrize("shape", [(256, 2048, 7, 7), (3, 64, 5, 9), (2, 8, 1, 1)])

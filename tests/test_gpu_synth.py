@@ -64,12 +64,11 @@ def test_executor_batch_prefetch_matches_inline(cuda):
     from polyaxon_amd.polyflow.executor import ResidentTrialExecutor
 
     out = {}
-    for mode in ("inline", "end", "start"):  # PLX_PREFETCH_AT: after the backward (default) / at the step's start
+    for mode in ("inline", "end"):  # generated inline / prefetched after the backward
         torch.manual_seed(0)
         data = SyntheticImages(4, 64, cuda, classes=1000, active_classes=100, grid=7, signal=0.5, seed=5)
         ex = ResidentTrialExecutor(resnet50(), data, cuda, use_graph=False)
         ex._prefetch = mode != "inline"
-        ex._prefetch_at_start = mode == "start"
         ex.reset(seed=1)
         ex.set_hparams(lr=0.05, momentum=0.9, weight_decay=1e-4)
         ex.run(4)
@@ -78,7 +77,7 @@ def test_executor_batch_prefetch_matches_inline(cuda):
         if mode != "inline":
             assert ex._ready is not None and ex._bufs is not None  # the prefetch path really ran
         del ex
-    for mode in ("end", "start"):
+    for mode in ("end",):
         assert out[mode][2] == out["inline"][2] + 1  # one batch generated ahead
         torch.testing.assert_close(out[mode][0], out["inline"][0], rtol=1e-5, atol=1e-5)
         torch.testing.assert_close(out[mode][1], out["inline"][1], rtol=1e-4, atol=1e-5)
