@@ -530,17 +530,44 @@ def test_global_avg_pool_kernels_match_fp32(cuda, shape):
     assert xa.grad.is_contiguous(memory_format=torch.channels_last)
 
 
-def _bn_ref(x, bn, relu=True):
-    y = F.batch_norm(x, None, None, bn.weight.float(), bn.bias.float(), training=True, eps=bn.eps)
-    return F.relu(y) if relu else y
+class _Bf16Store(torch.autograd.Function):
+    """Identity that rounds the value AND its gradient to bf16: emulates a bf16-stored activation in an fp32 graph."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+def _bottleneck_ref(x0, bn0, blk, g, store):
+    """bn0 -> ReLU -> downsampling Bottleneck in fp32 torch ops (F.batch_norm, F.conv2d) with ``store`` applied to
+    every stored activation; returns y and the grads of x, bn0.weight, bn0.bias for sum(g * y)."""
+    def bn(x, m, relu=True):
+        y = F.batch_norm(x, None, None, m.weight.detach().float(), m.bias.detach().float(), training=True, eps=m.eps)
+        return F.relu(y) if relu else y
+    w = lambda conv: conv.weight.detach().to(torch.bfloat16).float()  # noqa: E731
+    xr = x0.float().requires_grad_()
+    g0, b0 = bn0.weight.detach().clone().requires_grad_(), bn0.bias.detach().clone().requires_grad_()
+    hr = store(F.relu(F.batch_norm(xr, None, None, g0, b0, training=True, eps=bn0.eps)))
+    o = store(bn(store(F.conv2d(hr, w(blk.conv1))), blk.bn1))
+    o = store(bn(store(F.conv2d(o, w(blk.conv2), stride=2, padding=1)), blk.bn2))
+    o = bn(store(F.conv2d(o, w(blk.conv3))), blk.bn3, relu=False)
+    d = bn(store(F.conv2d(hr, w(blk.downsample.conv), stride=2)), blk.downsample.bn, relu=False)
+    yr = store(F.relu(o + d))
+    yr.backward(g.float())
+    return yr.detach(), (xr.grad, g0.grad, b0.grad)
 
 
 def test_downsampling_block_serves_its_input_batchnorm(cuda, monkeypatch):
     """The BatchNorm feeding a downsampling block gets its backward partials from conv1's dgrad (all but the
     even-even pixels) and the strided downsample conv's dgrad (those, with conv1's gradient added) instead of its
     own reduce pass (ops.conv1x1.BnLink.request_split): the link is actually served, and the whole fused chain --
-    bn0 -> ReLU -> Bottleneck(stride 2) with its downsample branch, forward and backward -- matches an fp32
-    F.batch_norm + F.conv2d reference of the same parameters."""
+    bn0 -> ReLU -> Bottleneck(stride 2) with its downsample branch, forward and backward -- is as close to an fp32
+    F.batch_norm + F.conv2d reference of the same parameters as the same torch ops with every activation and
+    gradient stored in bf16 are (the precision the native chain keeps)."""
     from polyaxon_amd.models.resnet import Bottleneck, Downsample
     from polyaxon_amd.ops import conv1x1
     from polyaxon_amd.ops.norm import BatchNormAct
@@ -572,18 +599,10 @@ def test_downsampling_block_serves_its_input_batchnorm(cuda, monkeypatch):
     g = torch.randn_like(y.float()).to(torch.bfloat16)
     y.backward(g)
     assert served.get(id(h._plx_bn_link)) is True, served  # bn0's link, by its backward
-    # fp32 reference with the same (bf16-representable) weights
-    w = lambda conv: conv.weight.detach().to(torch.bfloat16).float()  # noqa: E731
-    xr = x0.float().requires_grad_()
-    g0, b0 = bn0.weight.detach().clone().requires_grad_(), bn0.bias.detach().clone().requires_grad_()
-    hr = F.relu(F.batch_norm(xr, None, None, g0, b0, training=True, eps=bn0.eps))
-    o = _bn_ref(F.conv2d(hr, w(blk.conv1)), blk.bn1)
-    o = _bn_ref(F.conv2d(o, w(blk.conv2), stride=2, padding=1), blk.bn2)
-    o = _bn_ref(F.conv2d(o, w(blk.conv3)), blk.bn3, relu=False)
-    d = _bn_ref(F.conv2d(hr, w(blk.downsample.conv), stride=2), blk.downsample.bn, relu=False)
-    yr = F.relu(o + d)
-    yr.backward(g.float())
+    y32, ref = _bottleneck_ref(x0, bn0, blk, g, lambda t: t)
+    y16, emu = _bottleneck_ref(x0, bn0, blk, g, _Bf16Store.apply)
     rel = lambda a, b: float((a.float() - b).norm() / (b.norm() + 1e-12))  # noqa: E731
-    assert rel(y.float(), yr.detach()) < 2e-2, rel(y.float(), yr.detach())
-    for a, b, name in ((x.grad, xr.grad, "dx"), (bn0.weight.grad, g0.grad, "dgamma"), (bn0.bias.grad, b0.grad, "dbeta")):
-        assert rel(a, b) < 4e-2, (name, rel(a, b))
+    assert rel(y.float(), y32) < 2e-2, rel(y.float(), y32)
+    for a, r, e, name in zip((x.grad, bn0.weight.grad, bn0.bias.grad), ref, emu, ("dx", "dgamma", "dbeta")):
+        err, floor = rel(a, r), rel(e, r)
+        assert err <= 1.5 * floor + 5e-3, (name, err, floor)
