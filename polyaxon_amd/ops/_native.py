@@ -128,16 +128,34 @@ _SIZES: Dict[tuple, int] = {}
 _COUNTERS: Dict[tuple, object] = {}
 
 
+def capturing() -> bool:
+    """Is the current HIP stream being captured into a hipGraph?"""
+    import torch
+
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def cached(cache: dict, key, make, ok=None):
+    """``cache[key]`` (when ``ok(value)`` holds), else ``make()``.  A device buffer allocated while a stream is being
+    captured comes from that graph's private memory pool and dangles once the graph is freed, so such a value is
+    never stored: during capture a cached buffer is reused when present, else a fresh one serves this launch only
+    (its allocation and initialisation are part of the graph).  Long-lived buffers -- zero pages, last-arriver
+    tickets, workspaces -- therefore always live in the default pool."""
+    v = cache.get(key)
+    if v is not None and (ok is None or ok(v)):
+        return v
+    v = make()
+    if not capturing():
+        cache[key] = v
+    return v
+
+
 def counters(device, key: str, n: int = 4096):
     """A zeroed int32 counter array per (device, op) for the last-arriver kernels: each arriver that finishes a
     reduction resets its own counter, so the array is reused by every stream-ordered launch of that op."""
     import torch
 
-    k = (str(device), key)
-    c = _COUNTERS.get(k)
-    if c is None:
-        c = _COUNTERS[k] = torch.zeros(n, dtype=torch.int32, device=device)
-    return c
+    return cached(_COUNTERS, (str(device), key), lambda: torch.zeros(n, dtype=torch.int32, device=device))
 
 
 def current_stream() -> int:

@@ -42,10 +42,7 @@ _ZERO = {}
 
 
 def _zero_page(dev) -> torch.Tensor:
-    z = _ZERO.get(dev)
-    if z is None:
-        z = _ZERO[dev] = torch.zeros(64, dtype=torch.bfloat16, device=dev)
-    return z
+    return _native.cached(_ZERO, dev, lambda: torch.zeros(64, dtype=torch.bfloat16, device=dev))
 
 
 def _bhs(t: torch.Tensor, layout: str) -> _Strides:

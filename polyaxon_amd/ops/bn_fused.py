@@ -29,10 +29,8 @@ def _counters(dev: torch.device):
     """Zeroed ticket counters of the one-launch reduce + finalize (csrc/bn_kernels.hip ``reduce_l2_last``), one
     array per (device, stream): launches sharing it are stream-ordered and each leaves it zeroed again."""
     key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
-    t = _COUNTERS.get(key)
-    if t is None:
-        t = _COUNTERS[key] = torch.zeros(64, dtype=torch.int32, device=dev)  # >= ceil(2048 / 64) groups
-    return t.data_ptr()
+    # >= ceil(2048 / 64) groups
+    return _native.cached(_COUNTERS, key, lambda: torch.zeros(64, dtype=torch.int32, device=dev)).data_ptr()
 
 
 def _cl(t: torch.Tensor) -> torch.Tensor:

@@ -30,10 +30,7 @@ _CUS: Dict[int, int] = {}
 
 def _zero_page(dev: torch.device) -> torch.Tensor:
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
-    z = _ZERO.get(idx)
-    if z is None:
-        z = _ZERO[idx] = torch.zeros(256, dtype=torch.bfloat16, device=dev)
-    return z
+    return _native.cached(_ZERO, idx, lambda: torch.zeros(256, dtype=torch.bfloat16, device=dev))
 
 
 def _num_cus(dev: torch.device) -> int:

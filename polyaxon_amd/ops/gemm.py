@@ -140,11 +140,9 @@ def supported(M: int, N: int, K: int) -> bool:
 
 
 def _workspace(device: torch.device, floats: int) -> torch.Tensor:
-    key = (device.type, device.index or 0)
-    w = _ws.get(key)
-    if w is None or w.numel() < floats:
-        w = _ws[key] = torch.empty(max(floats, 1 << 20), dtype=torch.float32, device=device)
-    return w
+    return _native.cached(_ws, (device.type, device.index or 0),
+                          lambda: torch.empty(max(floats, 1 << 20), dtype=torch.float32, device=device),
+                          ok=lambda w: w.numel() >= floats)
 
 
 def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool,
