@@ -82,9 +82,13 @@ def run(fn: Callable[[], None], tensors: Iterable[torch.Tensor], dev: torch.devi
     side.wait_stream(main)  # operands (dy, x) and the gradient slot are ready in main-stream order
     with torch.cuda.stream(side):
         fn()
-    if not capturing():  # a captured graph owns its memory pool: nothing is recycled under it
-        for t in tensors:
-            t.record_stream(side)
+    # the operands must not be recycled before the side stream has read them -- during hipGraph capture too: the
+    # capture's private pool DOES hand a block freed by the main stream to a later allocation of the same capture, and
+    # in the graph that later kernel then overwrote dy / x under the concurrently replayed weight gradient (garbage
+    # gradients, the graph check's NaN since round 3).  A recorded block freed during capture is held until the
+    # capture ends (the allocator defers its reuse), which is what the graph needs.
+    for t in tensors:
+        t.record_stream(side)
     idx = side.device.index
     if not _pending.get(idx):
         _pending[idx] = True
