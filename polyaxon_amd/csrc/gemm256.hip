@@ -37,6 +37,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "handoff.h"
+
 #define PLX_API extern "C" __attribute__((visibility("default")))
 
 namespace {
@@ -44,6 +46,7 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int BM = 256, BN = 256, BK = 64, NTH = 512;
@@ -111,6 +114,26 @@ __device__ __forceinline__ uint32_t src_off(int sub, int piece, int lane, int ld
   }
 }
 
+// src_off(sub, wave + 8 pc, lane) = v(lane, wave) + s(sub, pc, wave): the lane-dependent part (K-major: row
+// lane >> 3 and the swizzled chunk, whose swizzle depends on the piece only through wave & 1; MN-major: k-row
+// lane >> 4 and the chunk, through (wave >> 1) & 1) is the same for every quarter and piece of a wave, the rest is
+// uniform.  v = the offset of (sub 0, piece wave); s = each piece's difference, taken at lane 0.
+template <bool IS_A, bool KMAJ>
+__device__ __forceinline__ void src_split(int wave, int lane, int ld, uint32_t& v, uint32_t (&s0)[2],
+                                          uint32_t (&s1)[2]) {
+  v = src_off<IS_A, KMAJ>(0, wave, lane, ld);
+  const uint32_t base = src_off<IS_A, KMAJ>(0, wave, 0, ld);
+#pragma unroll
+  for (int pc = 0; pc < 2; ++pc) {
+    s0[pc] = src_off<IS_A, KMAJ>(0, wave + 8 * pc, 0, ld) - base;
+    s1[pc] = src_off<IS_A, KMAJ>(1, wave + 8 * pc, 0, ld) - base;
+  }
+}
+
+__device__ __forceinline__ void glds2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, void* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)l, 16, voff, soff, 0, 0);
+}
+
 // Fragment addresses.  An MFMA fragment holds row r = c0 + (lane & 15) of a quarter image (c0 = 16-aligned quarter
 // position), k = 32 s + 8 (lane >> 4) + j.  The per-lane byte offset is computed once; the rest of the address is a
 // compile-time constant, so every ds_read in the loop is "base VGPR + immediate" (computing the XOR-swizzled
@@ -148,6 +171,10 @@ struct FragB {
 template <int V>
 struct IC {
   static constexpr int value = V;
+};
+template <bool V>
+struct IB {
+  static constexpr bool value = V;
 };
 
 struct Gemm256Args {
@@ -239,19 +266,35 @@ __device__ __forceinline__ void store_pair(const Gemm256Args& p, f32x4 a, f32x4 
   }
 }
 
-// ACC: C += alpha * AB (bf16 read-modify-write); SLAB: write fp32 partials (split K)
-template <bool AK, bool BKM, bool ACC, bool SLAB>
-__global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int ntn = p.N / BN, ntm = p.M / BM;
-  int tm, tn;
-  tile_of(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, p.group, tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kt0 = blockIdx.y * p.kt_per_split;
-  const int nk = min(p.kt_per_split, p.K / BK - kt0);
+// One output tile's K loop, K-tiles [kt0, kt0 + nk), accumulated into acc (callers zero it): the 256 x 256 x 64
+// ping-pong schedule described in the file header.  Leaves every DMA retired and every LDS read of the tile done
+// (all waves past the same barriers), so the caller may restage the LDS right away.
+//
+// pre: the caller already issued this tile's first two K-tiles (gemm256_prologue, or the previous tile's chained
+// ring) and then `extra` more vector-memory ops (the previous tile's epilogue stores, 0 / 16 / 32): the waits of the
+// first six phases count them in, so those stores drain behind the fill instead of before it (vmcnt retires loads
+// and stores in issue order).
+// chain (persistent kernel; nk even, the next piece >= 2 K-tiles): the ring does not drain at the end of this tile
+// but goes on with the next piece's K-tiles 0 and 1 (and wave 0 its bias), into the same slots: the next tile starts
+// with its first two K-tiles landed.  nk even keeps the slot parity: the next piece's K-tile j lands where this
+// tile's K-tile nk + j would have.
+struct Chain {
+  int m0, n0, kt0;
+  float* bias_lds;
+};
+
+template <bool AK, bool BKM>
+__device__ __forceinline__ void gemm256_prologue(const Gemm256Args& p, int m0, int n0, int kt0, int nk, char* smem,
+                                                 int wave, int lane, float* bias_lds = nullptr);
+
+// MODE 0: standalone (issues its own fill, drains at the end); 1: persistent, fill issued by the caller, drains;
+// 2: persistent and chained (the last K-tile pair peeled, the chain decided at compile time: a runtime chain check
+// in every phase, with the chained operands' buffer resources live across the K loop, had 2.6x the branches and ran
+// 13 % slower on Llama's 4096^3 projection).
+template <bool AK, bool BKM, int MODE = 0>
+__device__ __forceinline__ void gemm256_tile(const Gemm256Args& p, int m0, int n0, int kt0, int nk, f32x4 (&acc)[4][8],
+                                             char* smem, int wave, int lane, int wm, int wn, int extra = 0,
+                                             const Chain& chain = Chain{0, 0, 0, nullptr}) {
   const size_t k0 = (size_t)kt0 * BK;
 
   // buffer resources anchored at this block's tile origin (offsets stay 32-bit for any matrix size)
@@ -261,32 +304,34 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
   const uint32_t astep = AK ? BK * 2 : (uint32_t)(BK * p.lda * 2);
   const uint32_t bstep = BKM ? BK * 2 : (uint32_t)(BK * p.ldb * 2);
 
-  // per-lane source offsets of the two pieces (wave, wave + 8) of each quarter, in issue order:
-  // 0 = A-mi0, 1 = B-ni0, 2 = B-ni1, 3 = A-mi1
-  uint32_t src[4][2];
-#pragma unroll
-  for (int pc = 0; pc < 2; ++pc) {
-    src[0][pc] = src_off<true, AK>(0, wave + 8 * pc, lane, p.lda);
-    src[1][pc] = src_off<false, BKM>(0, wave + 8 * pc, lane, p.ldb);
-    src[2][pc] = src_off<false, BKM>(1, wave + 8 * pc, lane, p.ldb);
-    src[3][pc] = src_off<true, AK>(1, wave + 8 * pc, lane, p.lda);
-  }
-  auto issue = [&](int buf, int kt, int q) {
+  // Source offsets of the two pieces (wave, wave + 8) of each quarter, in issue order 0 = A-mi0, 1 = B-ni0,
+  // 2 = B-ni1, 3 = A-mi1, split as one per-lane VGPR per operand + a wave-uniform SGPR part (src_split): 2 VGPRs
+  // instead of 8 next to the 128 accumulators.
+  uint32_t va, vb, sof[4][2];
+  src_split<true, AK>(wave, lane, p.lda, va, sof[0], sof[3]);
+  src_split<false, BKM>(wave, lane, p.ldb, vb, sof[1], sof[2]);
+  auto issue_from = [&](__amdgpu_buffer_rsrc_t ra_, __amdgpu_buffer_rsrc_t rb_, int buf, int kt, int q) {
     // LDS placement: A-mi0 at 0, A-mi1 at QUARTER, B-ni0 at 2 QUARTER, B-ni1 at 3 QUARTER
     const int qoff = q == 0 ? 0 : q == 3 ? QUARTER : q == 1 ? 2 * QUARTER : 3 * QUARTER;
     char* dst = smem + buf * BUF + qoff;
     const bool isa = q == 0 || q == 3;
     const uint32_t koff = (uint32_t)kt * (isa ? astep : bstep);
-    const __amdgpu_buffer_rsrc_t r = isa ? ra : rb;
-    glds(r, src[q][0] + koff, dst + wave * 1024);
-    glds(r, src[q][1] + koff, dst + (wave + 8) * 1024);
+    const __amdgpu_buffer_rsrc_t r = isa ? ra_ : rb_;
+    glds2(r, isa ? va : vb, sof[q][0] + koff, dst + wave * 1024);
+    glds2(r, isa ? va : vb, sof[q][1] + koff, dst + (wave + 8) * 1024);
+  };
+  auto issue = [&](int buf, int kt, int q) { issue_from(ra, rb, buf, kt, q); };
+  // the chained next piece's operands (same strides)
+  // (built where used: the chain's origin goes through an opaque move so its buffer resources are not hoisted out of
+  // the K loop, where 8 more live SGPRs pushed SGPRs into VGPR lanes)
+  auto chain_issue = [&](int buf, int j, int q) {
+    int cm = chain.m0, cn = chain.n0, ck = chain.kt0;
+    asm volatile("" : "+s"(cm), "+s"(cn), "+s"(ck));
+    const size_t nk0 = (size_t)ck * BK;
+    issue_from(rsrc(AK ? p.A + (size_t)cm * p.lda + nk0 : p.A + nk0 * p.lda + cm),
+               rsrc(BKM ? p.B + (size_t)cn * p.ldb + nk0 : p.B + nk0 * p.ldb + cn), buf, j, q);
   };
 
-  f32x4 acc[4][8];  // [n tile: 4 x 16 = the wave's 64 columns][m tile: 8 x 16 = its 128 rows]
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // per-lane fragment offsets inside a quarter image (K-major: [s]; MN-major: [t])
   int aoff[4], boff[2];
@@ -351,18 +396,36 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
     else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   };
-  // issue seq g + 8 (tile kt + 2, kind P, into this tile's buffer CB) and wait for seq g + 2
-  auto ring = [&](auto cb, auto ph, int kt) {
+  // steady-state wait for seq g + 2: 12 DMAs younger -- plus, in the persistent modes' first K-tile pair, the
+  // previous tile's stores while they are younger than it (phases 0 .. 5: seq 2 .. 7 were issued before the stores)
+  auto wait12 = [&](auto first, int g) {
+    if constexpr (decltype(first)::value) {
+      if (g < 6 && extra >= 32) asm volatile("s_waitcnt vmcnt(44)" ::: "memory");
+      else if (g < 6 && extra >= 16) asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    }
+  };
+  // Issue seq g + 8 (tile kt + 2, kind P, into this tile's buffer CB) and wait for seq g + 2.  Past this tile's last
+  // K-tile, MODE 2 issues the chained piece's K-tile kt + 2 - nk instead (wave 0 also stages that piece's bias) and
+  // the other modes drain the ring.
+  auto ring = [&](auto cb, auto ph, auto first, int kt) {
     constexpr int CB = decltype(cb)::value, P = decltype(ph)::value;
     const int g = 4 * kt + P;
     if (g + 8 < S) {
       issue(CB, kt + 2, P);
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      wait12(first, g);
+    } else if constexpr (MODE == 2) {
+      if (P == 0 && kt == nk - 2 && wave == 0 && p.bias != nullptr && chain.bias_lds != nullptr)
+        glds(rsrc(p.bias + chain.n0), lane * 16, chain.bias_lds);
+      chain_issue(CB, kt + 2 - nk, P);
+      wait12(first, g);
     } else {
       wait_vm(2 * ((S - 1) - (g + 2)));
     }
   };
-  auto tile = [&](auto cb, int kt, FragA& a0) {
+  auto tile = [&](auto cb, auto first, int kt, FragA& a0) {
     constexpr int CB = decltype(cb)::value;
     const char* qa1 = smem + CB * BUF + QUARTER;
     const char* qb0 = smem + CB * BUF + 2 * QUARTER;
@@ -370,31 +433,39 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
     const char* qa0_next = smem + (1 - CB) * BUF;
     // phase 0: quadrant (0,0); reads B-ni0
     const FragB b0 = read_b(qb0);
-    ring(cb, IC<0>{}, kt);
+    ring(cb, IC<0>{}, first, kt);
     mfma_phase(a0, b0, 0, 0);
     // phase 1: quadrant (0,1); reads B-ni1
     const FragB b1 = read_b(qb1);
-    ring(cb, IC<1>{}, kt);
+    ring(cb, IC<1>{}, first, kt);
     mfma_phase(a0, b1, 0, 1);
     // phase 2: quadrant (1,1); reads A-mi1
     const FragA a1 = read_a(qa1);
-    ring(cb, IC<2>{}, kt);
+    ring(cb, IC<2>{}, first, kt);
     mfma_phase(a1, b1, 1, 1);
     // phase 3: quadrant (1,0) from registers; reads the next tile's A-mi0
     if (kt + 1 < nk) a0 = read_a(qa0_next);
-    ring(cb, IC<3>{}, kt);
+    ring(cb, IC<3>{}, first, kt);
     mfma_phase(a1, b0, 1, 0);
   };
 
   // prologue: seq 0 .. min(7, S - 1) (tiles 0 and 1); retire seq 0, 1 and read tile 0's A-mi0
+  if constexpr (MODE == 0) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) issue(0, 0, q);
+    for (int q = 0; q < 4; ++q) issue(0, 0, q);
+    if (nk > 1) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) issue(1, 1, q);
+    }
+  }
   if (nk > 1) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) issue(1, 1, q);
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    if (extra >= 32) asm volatile("s_waitcnt vmcnt(44)" ::: "memory");
+    else if (extra >= 16) asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   } else {
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (extra >= 32) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+    else if (extra >= 16) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
   FragA a0 = read_a(smem);
@@ -403,10 +474,107 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
   if (wm == 1) __builtin_amdgcn_s_barrier();
 
   for (int kt = 0; kt < nk; kt += 2) {
-    tile(IC<0>{}, kt, a0);
-    if (kt + 1 < nk) tile(IC<1>{}, kt + 1, a0);
+    tile(IC<0>{}, IB<MODE != 0>{}, kt, a0);
+    if (kt + 1 < nk) tile(IC<1>{}, IB<MODE != 0>{}, kt + 1, a0);
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // every wave executes the same number of barriers
+
+}
+
+// bf16 epilogue of one tile (bias / GELU / accumulate per the args): column-adjacent tile pairs regrouped to 16-byte
+// stores (pair_permute)
+// (bias: load_bias16 of the tile, or zeros when accumulating); 16 stores per lane, 32 with the GELU output
+template <bool ACC>
+__device__ __forceinline__ void gemm256_store(const Gemm256Args& p, f32x4 (&acc)[4][8], int m0, int n0, int lane, int wm,
+                                              int wn, const f32x4 (&bias)[2][2]) {
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int np = 0; np < 2; ++np) {
+    const int n8 = n0 + wn * 64 + np * 32 + 8 * fq;
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+      f32x4 a = acc[2 * np][mt], b = acc[2 * np + 1][mt];
+      pair_permute(a, b);
+      store_pair<ACC>(p, a, b, m0 + wm * 128 + mt * 16 + fr, n8, bias[np][0], bias[np][1]);
+    }
+  }
+}
+
+// the bias of this lane's 16 columns of the tile at n0 (gemm256_store's column pairs)
+__device__ __forceinline__ void load_bias16(const Gemm256Args& p, int n0, int lane, int wn, f32x4 (&bias)[2][2]) {
+#pragma unroll
+  for (int np = 0; np < 2; ++np) load_bias8(p, n0 + wn * 64 + np * 32 + 8 * (lane >> 4), bias[np][0], bias[np][1]);
+}
+
+// bias_lds: when the GEMM has a bias, wave 0 also stages the tile's 256 bias values there (one 1 KiB DMA, older than
+// every ring DMA, so the ring's first wait retires it)
+// load_bias16 from the tile's bias staged in LDS by gemm256_prologue (zeros without a bias)
+__device__ __forceinline__ void lds_bias16(const Gemm256Args& p, const float* bias_lds, int lane, int wn,
+                                           f32x4 (&bias)[2][2]) {
+#pragma unroll
+  for (int np = 0; np < 2; ++np) {
+    if (p.bias != nullptr) {
+      const float* b = bias_lds + wn * 64 + np * 32 + 8 * (lane >> 4);
+      bias[np][0] = *(const f32x4*)b;
+      bias[np][1] = *(const f32x4*)(b + 4);
+    } else {
+      bias[np][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bias[np][1] = bias[np][0];
+    }
+  }
+}
+
+template <bool AK, bool BKM>
+__device__ __forceinline__ void gemm256_prologue(const Gemm256Args& p, int m0, int n0, int kt0, int nk, char* smem,
+                                                 int wave, int lane, float* bias_lds) {
+  if (bias_lds != nullptr && p.bias != nullptr && wave == 0) glds(rsrc(p.bias + n0), lane * 16, bias_lds);
+  const size_t k0 = (size_t)kt0 * BK;
+  const __bf16* abase = AK ? p.A + (size_t)m0 * p.lda + k0 : p.A + k0 * p.lda + m0;
+  const __bf16* bbase = BKM ? p.B + (size_t)n0 * p.ldb + k0 : p.B + k0 * p.ldb + n0;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(abase), rb = rsrc(bbase);
+  const uint32_t astep = AK ? BK * 2 : (uint32_t)(BK * p.lda * 2);
+  const uint32_t bstep = BKM ? BK * 2 : (uint32_t)(BK * p.ldb * 2);
+  // the same quarter order and placement as gemm256_tile's `issue`
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    if (kt == 1 && nk < 2) break;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int qoff = q == 0 ? 0 : q == 3 ? QUARTER : q == 1 ? 2 * QUARTER : 3 * QUARTER;
+      char* dst = smem + kt * BUF + qoff;
+      const bool isa = q == 0 || q == 3;
+      const int sub = q == 0 || q == 1 ? 0 : 1;
+      const uint32_t koff = (uint32_t)kt * (isa ? astep : bstep);
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const uint32_t off = isa ? src_off<true, AK>(sub, wave + 8 * pc, lane, p.lda)
+                                 : src_off<false, BKM>(sub, wave + 8 * pc, lane, p.ldb);
+        glds(isa ? ra : rb, off + koff, dst + (wave + 8 * pc) * 1024);
+      }
+    }
+  }
+}
+
+// ACC: C += alpha * AB (bf16 read-modify-write); SLAB: write fp32 partials (split K)
+template <bool AK, bool BKM, bool ACC, bool SLAB>
+__global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int ntn = p.N / BN, ntm = p.M / BM;
+  int tm, tn;
+  tile_of(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, p.group, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kt0 = blockIdx.y * p.kt_per_split;
+  const int nk = min(p.kt_per_split, p.K / BK - kt0);
+
+  f32x4 acc[4][8];  // [n tile: 4 x 16 = the wave's 64 columns][m tile: 8 x 16 = its 128 rows]
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  gemm256_tile<AK, BKM>(p, m0, n0, kt0, nk, acc, smem, wave, lane, wm, wn);
 
   // epilogue: acc[nt][mt] is a 16 x 16 tile D[n][m]: m = lane & 15, n = 4 (lane >> 4) + j, j = 0..3
   const int fr = lane & 15, fq = lane >> 4;
@@ -420,20 +588,188 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
         *(f32x4*)((float*)p.C + ((size_t)blockIdx.y * p.M + m) * p.N + n) = acc[nt][mt];
       }
   } else {
-#pragma unroll
-    for (int np = 0; np < 2; ++np) {  // column-adjacent tile pairs (nt, nt + 1), 16-byte stores (pair_permute)
-      const int n8 = n0 + wn * 64 + np * 32 + 8 * fq;
-      f32x4 ba, bb;
-      load_bias8(p, n8, ba, bb);
-#pragma unroll
-      for (int mt = 0; mt < 8; ++mt) {
-        f32x4 a = acc[2 * np][mt], b = acc[2 * np + 1][mt];
-        pair_permute(a, b);
-        store_pair<ACC>(p, a, b, m0 + wm * 128 + mt * 16 + fr, n8, ba, bb);
-      }
-    }
+    f32x4 bias[2][2];
+    load_bias16(p, n0, lane, wn, bias);
+    gemm256_store<ACC>(p, acc, m0, n0, lane, wm, wn, bias);
   }
 }
+
+// ---------------------------------------------------------------------------------------------------------------
+// Persistent stream-K variant of the 8-wave kernel (schedule 9).  One workgroup per CU (G = the CU count) walks
+//   1. its contiguous share (ipb iterations) of the "stream-K" iteration space -- the first sk_tiles tiles x their
+//      K-tiles, flattened tile-major -- so the partial wave of tiles that would leave CUs idle (T % G of them, or all
+//      of them when T < G) is split along K over every CU, then
+//   2. the remaining (T - sk_tiles, a multiple of G) tiles data-parallel, tile sk_tiles + blk, + G, ...
+// A tile split over several workgroups is finished by the last of them to arrive (the hand-off of csrc/handoff.h:
+// sc1 fp32 partials per workgroup slot, one relaxed agent-scope ticket per tile, reset by the last arriver, so
+// back-to-back and graph-replayed launches reuse the zeroed tickets): nobody waits on anybody, so a workgroup that
+// is not yet resident (another kernel holding CUs) can never stall the others.  A workgroup's partial pieces are its
+// first (a tile's tail, slot 0) and its last SK piece (a tile's head, slot 1), so 2 G slots of 256 x 256 fp32.
+// Between data-parallel tiles the next tile's ring fill is issued before the finished tile's epilogue stores and the
+// fill's first wait counts the stores in (gemm256_tile's `extra`): the 128 KiB store of one tile drains under the
+// next tile's first loads, and the workgroups' tile ends drift apart instead of all 256 CUs hitting HBM with 32 MB
+// of stores at once (the per-tile fixed cost of profiles/r5_lm_gemm.md).
+struct SkArgs {
+  float* part;        // fp32 [2 G][65536]: per-workgroup partial slots (lane-linear f32x4 layout)
+  unsigned* tickets;  // [G], zero between launches
+  int sk_tiles;       // tiles in the stream-K phase (ids 0 .. sk_tiles - 1)
+  int ipb;            // stream-K iterations (K-tiles) per workgroup
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slot_rsrc(float* part, int slot) {
+  return rsrc(part + (size_t)slot * 65536);
+}
+
+template <bool AK, bool BKM>
+__global__ void __launch_bounds__(NTH, 1) gemm256_sk_kernel(Gemm256Args p, SkArgs s) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ __attribute__((aligned(16))) float s_bias[2][BN];  // per-tile bias, double-buffered across tiles
+  __shared__ int s_last;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int G = gridDim.x, blk = xcd_remap(blockIdx.x, G);
+  const int ntn = p.N / BN, ntm = p.M / BM, T = ntm * ntn, nk = p.K / BK;
+  const int sk_total = s.sk_tiles * nk;
+  int it = min(sk_total, blk * s.ipb);
+  const int it_end = min(sk_total, it + s.ipb);
+  int dp = s.sk_tiles + blk;
+
+  int tile = 0, kb = 0, ke = 0;
+  auto next = [&]() -> bool {
+    if (it < it_end) {
+      tile = it / nk;
+      kb = it - tile * nk;
+      ke = min(nk, kb + (it_end - it));
+      it += ke - kb;
+      return true;
+    }
+    if (dp < T) {
+      tile = dp;
+      kb = 0;
+      ke = nk;
+      dp += G;
+      return true;
+    }
+    return false;
+  };
+  auto origin = [&](int t, int& m0, int& n0) {
+    int tm, tn;
+    tile_of(t, ntm, ntn, p.group, tm, tn);
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+  if (!next()) return;
+  int ctile = tile, ckb = kb, cke = ke, cm0, cn0;  // the current item; tile / kb / ke: the one after it
+  origin(ctile, cm0, cn0);
+  gemm256_prologue<AK, BKM>(p, cm0, cn0, ckb, cke - ckb, smem, wave, lane, s_bias[0]);
+  // An even K-tile count (>= 4) makes every piece even and >= 4 (ipb is even and >= 4 then): every tile chains into
+  // the next one, the last into a dummy re-read of itself (drained before the exit).  Other counts drain the ring
+  // per tile (MODE 1).
+  auto run = [&](auto chain_tag) {
+    constexpr bool CHAIN = decltype(chain_tag)::value;
+    int extra = 0;
+    for (int slot = 0;; slot ^= 1) {
+      const bool more = next();
+      int m0 = cm0, n0 = cn0;
+      if (more) origin(tile, m0, n0);
+      const Chain ch{m0, n0, more ? kb : ckb, more ? s_bias[slot ^ 1] : nullptr};
+      // The lane index is laundered once per tile so that the K loop's per-lane LDS / DMA offsets are recomputed
+      // per tile instead of hoisted out of the tile loop: hoisted, they stayed live through the epilogue next to
+      // the 128 accumulator VGPRs and the kernel spilled (136 VGPRs).
+      int ln;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+      f32x4 acc[4][8];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      gemm256_tile<AK, BKM, CHAIN ? 2 : 1>(p, cm0, cn0, ckb, cke - ckb, acc, smem, wave, ln, wm, wn, extra, ch);
+      // every LDS read of this tile done; unless chained, every DMA retired and the ring free
+    bool store = ckb == 0 && cke == nk;
+    if (!store) {
+      // pieces of tile ctile: workgroups bf .. bl (the iteration space is split at multiples of ipb); the one that
+      // arrives last adds the others' partials and stores the tile.  A piece that already sees every other piece's
+      // ticket is last without writing its own partial.
+      const int bf = (ctile * nk) / s.ipb, bl = (ctile * nk + nk - 1) / s.ipb;
+      const int np = bl - bf + 1;
+      if (tid == 0)
+        s_last = __hip_atomic_load(s.tickets + bf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(np - 1);
+      __syncthreads();
+      int last = s_last;
+      if (!last) {
+        const __amdgpu_buffer_rsrc_t r = slot_rsrc(s.part, 2 * blk + (ckb == 0 ? 1 : 0));
+#pragma unroll
+        for (int i = 0; i < 32; ++i)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i >> 3][i & 7]), r, tid * 16,
+                                                 i * NTH * 16, 16 /* sc1 */);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+          plx_handoff_release();
+          const unsigned old = __hip_atomic_fetch_add(s.tickets + bf, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_last = old == (unsigned)(np - 1);
+          if (s_last) plx_handoff_acquire();
+        }
+        __syncthreads();
+        last = s_last;
+      }
+      if (last) {
+        // Sum the pieces in workgroup order bf .. bl whoever arrived last (this piece from registers, the others
+        // from their slots), so the result is bitwise independent of the arrival order.  8 f32x4 at a time: all 32
+        // loads in flight next to the 128 accumulators spilled.
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 t[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) t[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+          for (int b = bf; b <= bl; ++b) {
+            if (b == blk) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) t[u] += acc[g][u];
+            } else {
+              const __amdgpu_buffer_rsrc_t r = slot_rsrc(s.part, 2 * b + (b == bf ? 1 : 0));
+              f32x4 v[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u)
+                v[u] = __builtin_bit_cast(
+                    f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16, (g * 8 + u) * NTH * 16, 16 /* sc1 */));
+#pragma unroll
+              for (int u = 0; u < 8; ++u) t[u] += v[u];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc[g][u] = t[u];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (tid == 0) __hip_atomic_store(s.tickets + bf, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        store = true;
+      }
+    }
+    // Unless the ring chained into it, the next tile's fill (and its bias, into the other LDS slot) goes out before
+    // this tile's stores; the stores take their bias from LDS, so nothing in the epilogue waits on vmcnt behind the
+    // fill.  ln2: a fresh laundered lane, so the fill's offsets are not kept live from the K loop through the epilogue.
+    int ln2;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln2) : "v"(lane));
+    if (!CHAIN && more) gemm256_prologue<AK, BKM>(p, m0, n0, kb, ke - kb, smem, wave, ln2, s_bias[slot ^ 1]);
+    if (store) {
+      f32x4 bias[2][2];
+      lds_bias16(p, s_bias[slot], ln2, wn, bias);
+      gemm256_store<false>(p, acc, cm0, cn0, ln2, wm, wn, bias);
+    }
+    extra = store ? (p.C2 != nullptr ? 32 : 16) : 0;
+    if (!more) break;
+    ctile = tile;
+    ckb = kb;
+    cke = ke;
+    cm0 = m0;
+    cn0 = n0;
+    }
+    if (CHAIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy fill lands before the LDS is released
+  };
+  run(IB<true>{});  // the host launches this kernel for even K-tile counts >= 4 only
+}
+
 
 // ---------------------------------------------------------------------------------------------------------------
 // 4-wave variant: the same 256 x 256 x 64 tile, LDS layout and DMA engine, but 4 waves as 2 (M) x 2 (N), each
@@ -717,7 +1053,100 @@ int plan_kt_per_split(int M, int N, int K) {
   return (nk + splits - 1) / splits;
 }
 
+// Stream-K plan for G persistent workgroups.  The partial wave of tiles (T % G; all of them when T < G) is split along
+// K only when that pays: a split tile costs its pieces' fp32 partials (256 KiB each, written and read back: all
+// workgroups at once, so HBM-bound -- the GPT-2 768-wide projections, 192 tiles of 12 K-tiles split in two, ran
+// 0.041 ms against 0.027 unsplit, r6_lm_gemm_sk.jsonl), so only long reductions (>= 32 K-tiles) whose split saves
+// >= 16 K-tiles per workgroup are split, e.g. Llama-3's 384-tile QKV forward.  Pieces are >= 4 K-tiles and, for an
+// even K-tile count, even (the chained ring needs even pieces).
+int g_sk_force = 0;  // 1: split every partial wave (tests: the split paths on small shapes); plx_gemm256_set_sk_force
+
+void sk_plan(int M, int N, int K, int G, int& sk_tiles, int& ipb) {
+  const int T = (M / BM) * (N / BN), nk = K / BK;
+  const int rem = T % G;
+  ipb = rem ? max((rem * nk + G - 1) / G, min(nk, 4)) : 1;
+  if (nk % 2 == 0) ipb += ipb & 1;
+  sk_tiles = rem && (g_sk_force || (nk >= 32 && nk - ipb >= 16)) ? rem : 0;
+  if (!sk_tiles) ipb = 1;
+}
+
+int cu_count() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {
+    int n = 0;
+    cus[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }
+  return cus[dev];
+}
+
+template <bool AK, bool BKM>
+int launch_sk(const Gemm256Args& a, const SkArgs& sk, int G, hipStream_t st) {
+  auto k = gemm256_sk_kernel<AK, BKM>;
+  static const int attr =
+      hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES) == hipSuccess ? 0 : -4;
+  if (attr) return attr;
+  hipLaunchKernelGGL(k, dim3(G), dim3(NTH), LDS_BYTES, st, a, sk);
+  return 0;
+}
+
 }  // namespace
+
+// fp32 workspace floats plx_gemm256_sk needs for this shape on the current device (0: no tile is split)
+// (sized for any plan of the shape, so a memoised answer stays valid when plx_gemm256_set_sk_force changes)
+PLX_API long long plx_gemm256_sk_ws(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return -1;
+  const int G = cu_count();
+  return (M / BM) * (N / BN) % G ? 2LL * G * 65536 : 0;
+}
+
+// test knob: 1 splits every partial wave of tiles along K (the split / last-arriver paths on small shapes), 0 the
+// cost rule of sk_plan; returns the previous value
+PLX_API int plx_gemm256_set_sk_force(int force) {
+  const int prev = g_sk_force;
+  g_sk_force = force ? 1 : 0;
+  return prev;
+}
+
+// workgroups / stream-K tiles / iterations per workgroup of the plan (tests and the bench report it)
+PLX_API int plx_gemm256_sk_plan(int M, int N, int K, int* sk_tiles, int* ipb) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return -1;
+  const int G = cu_count();
+  sk_plan(M, N, K, G, *sk_tiles, *ipb);
+  return G;
+}
+
+// C[M][N] = alpha * A . B (+ bias) (gelu_out as plx_gemm256_exv) on the persistent stream-K kernel: one workgroup per
+// CU.  K must be an even multiple of 64, >= 256 (-1 otherwise: ops/gemm.py runs the 8-wave kernel then).  ws: plx_gemm256_sk_ws floats (may be null when that is 0); tickets: >= CU-count zeroed uint32 that the kernel
+// leaves zeroed (one array per device, launches on one stream at a time).  No accumulate.
+PLX_API int plx_gemm256_sk(const void* A, const void* B, void* C, void* ws, void* tickets, int M, int N, int K, int lda,
+                           int ldb, int ldc, int a_kmajor, int b_kmajor, float alpha, const float* bias,
+                           void* gelu_out, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return -1;
+  if ((K / BK) % 2 || K / BK < 4) return -1;  // the chained ring needs an even K-tile count >= 4
+  if (bias != nullptr && (uintptr_t)bias % 16) return -1;
+  if (gelu_out != nullptr && (uintptr_t)gelu_out % 16) return -1;
+  if (lda % 8 || ldb % 8 || ldc % 8 || (uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return -1;
+  const long long aspan = a_kmajor ? (long long)BM * lda * 2 : (long long)K * lda * 2;
+  const long long bspan = b_kmajor ? (long long)BN * ldb * 2 : (long long)K * ldb * 2;
+  if (aspan >= 0x7ffffff0LL || bspan >= 0x7ffffff0LL) return -2;
+  int G = cu_count();
+  SkArgs sk{(float*)ws, (unsigned*)tickets, 0, 1};
+  sk_plan(M, N, K, G, sk.sk_tiles, sk.ipb);
+  if (!sk.sk_tiles) G = min(G, (M / BM) * (N / BN));  // data-parallel only: no idle workgroups
+  if (sk.sk_tiles && (!ws || !tickets)) return -5;
+  Gemm256Args a{(const __bf16*)A, (const __bf16*)B, C, M, N, K, lda, ldb, ldc, 0, alpha, bias, gelu_out,
+                g_group > 0 ? g_group : 1};
+  hipStream_t st = (hipStream_t)stream;
+  int rc;
+  if (a_kmajor && b_kmajor) rc = launch_sk<true, true>(a, sk, G, st);
+  else if (a_kmajor) rc = launch_sk<true, false>(a, sk, G, st);
+  else if (b_kmajor) rc = launch_sk<false, true>(a, sk, G, st);
+  else rc = launch_sk<false, false>(a, sk, G, st);
+  if (rc) return rc;
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 
 // Split-K plan: number of K splits (blockIdx.y) the kernel uses for this shape (1 = no workspace needed);
 // the fp32 workspace must hold splits * M * N floats

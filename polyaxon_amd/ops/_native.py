@@ -305,6 +305,10 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gemm256_set_waves": [_I],
         "plx_gemm256_set_group": [_I],
         "plx_gemm256_tile": [],
+        "plx_gemm256_sk_ws": [_I, _I, _I],
+        "plx_gemm256_sk_plan": [_I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)],
+        "plx_gemm256_set_sk_force": [_I],
+        "plx_gemm256_sk": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P],
     },
     "plx_attn": {
         "plx_attn_fwd": [_P, _I, _P],
@@ -359,7 +363,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
 }
 
 
-RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_partial_colsum_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_v2": None, "plx_set_tn2_stem": None, "plx_set_tn2_c64": None, "plx_set_tn_atomic": None, "plx_set_adamw_grid_cap": None, "plx_set_adamw_wide": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
+RESTYPES: Dict[str, object] = {"plx_attn_bwd_workspace": ctypes.c_longlong, "plx_conv_wgrad_workspace": _L, "plx_bn_workspace": _L, "plx_bn_l2_workspace": _L, "plx_partial_colsum_workspace": _L, "plx_stem_bn_pool_bwd_workspace": _L, "plx_gemm_tn_workspace": _L, "plx_gemm256_sk_ws": ctypes.c_longlong, "plx_stem_conv_wgrad_workspace": _L, "plx_pm_create": _P, "plx_pm_destroy": None, "plx_set_tn_v2": None, "plx_set_tn2_stem": None, "plx_set_tn2_c64": None, "plx_set_tn_atomic": None, "plx_set_adamw_grid_cap": None, "plx_set_adamw_wide": None, "plx_attn_set_fwd_waves": None, "plx_attn_set_dq_waves": None, "plx_attn_set_dkdv_waves": None, "plx_gemm256_set_split_target": None,
                                "plx_pm_wake": None, "plx_rccl_init": _P, "plx_rccl_error": ctypes.c_char_p}
 
 

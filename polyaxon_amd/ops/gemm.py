@@ -56,11 +56,14 @@ SCHEDULE: Dict[Tuple[int, int, int, bool, bool], int] = {
 
 # A/B override of the schedule for every kernel call (scripts/gemm_bench.py --waves); 0 = the table
 FORCE_SCHEDULE = 0
+SK = 9  # the persistent stream-K schedule (no accumulate: such calls run the 8-wave kernel)
 
-# schedule of a kernel call outside the table, by layout (PLX_LM_GEMM=1, split-K shapes): the 8-wave ping-pong kernel
-# for the forward (both operands K-major: 4.63 vs 4.91 ms per GPT-2 step, 42.3 vs 47.1 Llama), the 4-wave one for the
-# data and weight gradients (4.40 vs 5.09, 45.2 vs 51.5; profiles/r5_lm_gemm.md).  PLX_GEMM_WAVES overrides it.
-_LAYOUT_SCHEDULE = {_FWD: 8, _DGRAD: 5, _WGRAD: 5}
+# schedule of a kernel call outside the table, by layout (PLX_LM_GEMM=1, split-K shapes): the persistent stream-K
+# kernel for the forward (both operands K-major: 2.98 vs 3.10 ms over one call of each of the 9 forward shapes in
+# profiles/r6_lm_gemm_sk.jsonl; it was the 8-wave ping-pong kernel, 4.63 vs 4.91 ms per GPT-2 step against the
+# 4-wave one), the 4-wave one for the data and weight gradients (4.40 vs 5.09, 45.2 vs 51.5; profiles/r5_lm_gemm.md).
+# PLX_GEMM_WAVES overrides it.
+_LAYOUT_SCHEDULE = {_FWD: SK, _DGRAD: 5, _WGRAD: 5}
 
 
 def _schedule_of(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> int:
@@ -176,17 +179,50 @@ def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: boo
                                  or gelu_out.stride() != out.stride() or gelu_out.data_ptr() % 16):
         raise ValueError("gelu_out must be a bf16 tensor laid out like out (and no accumulate)")
     lib = _native.lib("plx_gemm")
+    v = _schedule_of(M, N, K, a_kmajor, b_kmajor)
+    if v == SK:
+        if not accumulate and sk_supported(M, N, K):
+            return _gemm_sk(lib, a, b, out, M, N, K, a_kmajor, b_kmajor, alpha, bias, gelu_out)
+        v = 8  # accumulating calls and odd / short K: the 8-wave kernel
     ns = splits(M, N, K)
     ws = _workspace(a.device, ns * M * N).data_ptr() if ns > 1 else None
     lda = K if a_kmajor else M
     ldb = K if b_kmajor else N
-    v = _schedule_of(M, N, K, a_kmajor, b_kmajor)
     rc = lib.plx_gemm256_exv(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, M, N, K, lda, ldb, out.stride(0),
                              int(a_kmajor), int(b_kmajor), float(alpha), int(accumulate),
                              bias.data_ptr() if bias is not None else None,
                              gelu_out.data_ptr() if gelu_out is not None else None, v, _native.current_stream())
     if rc != 0:
         raise RuntimeError(f"plx_gemm256 failed ({rc}) for {M}x{N}x{K} a_kmajor={a_kmajor} b_kmajor={b_kmajor}")
+    return out
+
+
+def sk_supported(M: int, N: int, K: int) -> bool:
+    """schedule 9 takes the kernel's shapes with an even K-tile count >= 4 (the chained ring)"""
+    return supported(M, N, K) and (K // 64) % 2 == 0 and K >= 256
+
+
+def sk_plan(M: int, N: int, K: int) -> Tuple[int, int, int]:
+    """(persistent workgroups, stream-K tiles, K-tiles per workgroup in the stream-K phase) of schedule 9"""
+    import ctypes
+    t, i = ctypes.c_int(0), ctypes.c_int(0)
+    g = _native.lib("plx_gemm").plx_gemm256_sk_plan(M, N, K, ctypes.byref(t), ctypes.byref(i))
+    return g, t.value, i.value
+
+
+def _gemm_sk(lib, a, b, out, M, N, K, a_kmajor, b_kmajor, alpha, bias, gelu_out):
+    """schedule 9: the persistent stream-K kernel (csrc/gemm256.hip gemm256_sk_kernel)"""
+    floats = _native.size("plx_gemm", "plx_gemm256_sk_ws", M, N, K)
+    if floats < 0:
+        raise ValueError(f"gemm256_sk does not take {M}x{N}x{K}")
+    ws = _workspace(a.device, floats).data_ptr() if floats else None
+    tickets = _native.counters(a.device, "plx_gemm256_sk", 1024)
+    rc = lib.plx_gemm256_sk(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, tickets.data_ptr(), M, N, K,
+                            K if a_kmajor else M, K if b_kmajor else N, out.stride(0), int(a_kmajor), int(b_kmajor),
+                            float(alpha), bias.data_ptr() if bias is not None else None,
+                            gelu_out.data_ptr() if gelu_out is not None else None, _native.current_stream())
+    if rc != 0:
+        raise RuntimeError(f"plx_gemm256_sk failed ({rc}) for {M}x{N}x{K} a_kmajor={a_kmajor} b_kmajor={b_kmajor}")
     return out
 
 

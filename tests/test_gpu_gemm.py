@@ -280,3 +280,103 @@ def test_gemm256_gelu_epilogue(cuda, M, N, K):
     _check(h, a.float() @ b.float().t() + bias, K)
     ref = F.gelu(h.float(), approximate="tanh")
     torch.testing.assert_close(g.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.fixture(params=[1, 0], ids=["split_all", "cost_rule"])
+def stream_k(cuda, request):
+    """schedule 9 with every partial wave split along K (the split / last-arriver paths on small shapes), and with
+    the planner's cost rule (mostly the chained data-parallel loop)"""
+    from polyaxon_amd.ops import gemm
+
+    lib = gemm._native.lib("plx_gemm")
+    prev, prev_force = gemm.FORCE_SCHEDULE, lib.plx_gemm256_set_sk_force(request.param)
+    gemm.FORCE_SCHEDULE = gemm.SK
+    yield gemm
+    gemm.FORCE_SCHEDULE = prev
+    lib.plx_gemm256_set_sk_force(prev_force)
+
+
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [
+    (512, 768, 1408),   # 6 tiles < the CU count: 22 K-tiles in pieces of 4, 2-K-tile pieces across tile boundaries
+    (512, 768, 1344),   # 21 K-tiles (odd): the 8-wave kernel runs instead
+    (256, 256, 8192),   # one tile over 32 workgroups
+    (512, 512, 64),     # one K-tile: the 8-wave kernel
+    (4352, 4096, 768),  # 272 tiles = one data-parallel wave + 16 stream-K tiles
+    (1536, 4096, 4096),  # 96 tiles, 64 K-tiles: split by the cost rule too
+    (8192, 8192, 512),   # 1024 tiles = 4 chained data-parallel tiles per workgroup
+])
+def test_gemm256_stream_k_matches_fp32(stream_k, cuda, a_kmajor, b_kmajor, M, N, K):
+    """Schedule 9 (gemm256_sk_kernel): tile counts that do not divide the persistent grid, pieces that cross tile
+    boundaries, every operand layout, against fp32 torch."""
+    gemm = stream_k
+    g, skt, ipb = gemm.sk_plan(M, N, K)
+    assert g >= 1 and 0 <= skt <= (M // 256) * (N // 256) and ipb >= 1
+    a = _rand((M, K) if a_kmajor else (K, M), cuda, 21)
+    b = _rand((N, K) if b_kmajor else (K, N), cuda, 22)
+    out = gemm.gemm(a, b, M, N, K, a_kmajor, b_kmajor)
+    af = a.float() if a_kmajor else a.float().t()
+    bf = b.float() if b_kmajor else b.float().t()
+    torch.cuda.synchronize()
+    _check(out, af @ bf.t(), K)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 3072, 768), (4352, 4096, 768), (256, 512, 4096)])
+def test_gemm256_stream_k_epilogues_deterministic(stream_k, cuda, M, N, K):
+    """Bias + GELU on the persistent kernel (data-parallel tiles and last-arriver tiles), alpha, a strided output, and
+    30 back-to-back launches bitwise equal: the split tiles' partials are summed in workgroup order whichever
+    workgroup arrives last, and the tickets are left zeroed for the next launch."""
+    gemm = stream_k
+    a, b = _rand((M, K), cuda, 23), _rand((N, K), cuda, 24)
+    bias = torch.randn(N, device=cuda)
+    h = torch.empty(M, N, dtype=torch.bfloat16, device=cuda)
+    g = torch.empty_like(h)
+    gemm.gemm(a, b, M, N, K, True, True, out=h, bias=bias, gelu_out=g)
+    ref = a.float() @ b.float().t()
+    torch.cuda.synchronize()
+    _check(h, ref + bias, K)
+    torch.testing.assert_close(g.float(), F.gelu(h.float(), approximate="tanh"), rtol=1e-2, atol=1e-2)
+    wide = torch.zeros(M, N + 256, dtype=torch.bfloat16, device=cuda)
+    gemm.gemm(a, b, M, N, K, True, True, out=wide[:, 256:], alpha=0.5)
+    torch.cuda.synchronize()
+    _check(wide[:, 256:], 0.5 * ref, K)
+    assert wide[:, :256].abs().max().item() == 0
+    first = gemm.gemm(a, b, M, N, K, True, True)
+    for _ in range(30):
+        assert torch.equal(first, gemm.gemm(a, b, M, N, K, True, True))
+    tickets = gemm._native.counters(cuda, "plx_gemm256_sk", 1024)
+    torch.cuda.synchronize()
+    assert int(tickets.abs().sum().item()) == 0
+
+
+def test_gemm256_stream_k_accumulate_falls_back(stream_k, cuda):
+    """accumulate=True under schedule 9 runs the 8-wave kernel's read-modify-write epilogue (same numbers)."""
+    gemm = stream_k
+    M, N, K = 512, 512, 1024
+    a, b = _rand((M, K), cuda, 25), _rand((N, K), cuda, 26)
+    c0 = _rand((M, N), cuda, 27)
+    out = c0.clone()
+    gemm.gemm(a, b, M, N, K, True, True, out=out, accumulate=True)
+    torch.cuda.synchronize()
+    _check(out, a.float() @ b.float().t() + c0.float(), K)
+
+
+def test_gemm256_stream_k_in_graph(stream_k, cuda):
+    """Captured into a hipGraph and replayed: the tickets the kernel resets make every replay start from zero."""
+    gemm = stream_k
+    M, N, K = 512, 768, 1408
+    a, b = _rand((M, K), cuda, 28), _rand((N, K), cuda, 29)
+    out = gemm.gemm(a, b, M, N, K, True, True)  # warm: workspace + tickets allocated outside the capture
+    ref = out.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            gemm.gemm(a, b, M, N, K, True, True, out=out)
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(5):
+        out.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
