@@ -143,7 +143,9 @@ def supported(M: int, N: int, K: int) -> bool:
 
 
 def _workspace(device: torch.device, floats: int) -> torch.Tensor:
-    return _native.cached(_ws, (device.type, device.index or 0),
+    """fp32 scratch (split-K slabs, stream-K partials) per (device, stream): launches on two streams of one device
+    (trials sharing a GPU) never share one"""
+    return _native.cached(_ws, (device.type, device.index or 0, _native.current_stream()),
                           lambda: torch.empty(max(floats, 1 << 20), dtype=torch.float32, device=device),
                           ok=lambda w: w.numel() >= floats)
 
@@ -216,7 +218,7 @@ def _gemm_sk(lib, a, b, out, M, N, K, a_kmajor, b_kmajor, alpha, bias, gelu_out)
     if floats < 0:
         raise ValueError(f"gemm256_sk does not take {M}x{N}x{K}")
     ws = _workspace(a.device, floats).data_ptr() if floats else None
-    tickets = _native.counters(a.device, "plx_gemm256_sk", 1024)
+    tickets = _native.counters(a.device, f"plx_gemm256_sk:{_native.current_stream()}", 1024)
     rc = lib.plx_gemm256_sk(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, tickets.data_ptr(), M, N, K,
                             K if a_kmajor else M, K if b_kmajor else N, out.stride(0), int(a_kmajor), int(b_kmajor),
                             float(alpha), bias.data_ptr() if bias is not None else None,

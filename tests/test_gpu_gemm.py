@@ -344,7 +344,7 @@ def test_gemm256_stream_k_epilogues_deterministic(stream_k, cuda, M, N, K):
     first = gemm.gemm(a, b, M, N, K, True, True)
     for _ in range(30):
         assert torch.equal(first, gemm.gemm(a, b, M, N, K, True, True))
-    tickets = gemm._native.counters(cuda, "plx_gemm256_sk", 1024)
+    tickets = gemm._native.counters(cuda, f"plx_gemm256_sk:{gemm._native.current_stream()}", 1024)
     torch.cuda.synchronize()
     assert int(tickets.abs().sum().item()) == 0
 
