@@ -73,7 +73,7 @@ def _schedule_of(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> int:
     if v:
         return v
     if os.environ.get("PLX_GEMM_WAVES"):
-        return 0  # the library's global knob
+        return SK if os.environ["PLX_GEMM_WAVES"] == "9" else 0  # 9: stream-K; 8 / 5: the library's global knob
     return _LAYOUT_SCHEDULE.get((bool(a_kmajor), bool(b_kmajor)), 0)
 
 
