@@ -248,9 +248,9 @@ def forward(x2: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor]
 
 
 # In `auto`, a forward with the GELU epilogue runs on the kernel (one launch, the activation a second store) instead
-# of hipBLASLt + a separate GELU pass.  In the GPT-2 step that was equal on one box (717.8k / 719.9k vs 717.8k /
-# 718.2k tokens/s) and +0.2-0.3 % on another (706.6k / 705.8k vs 704.5k / 704.5k), profiles/r5_gelu_native_ab.jsonl.
-# PLX_GELU_NATIVE=0: the table decides.
+# of hipBLASLt + a separate GELU pass.  On the stream-K schedule that is +0.8 % on the GPT-2 step (709.2-711.3k vs
+# 703.7-706.2k tokens/s, 3 alternating pairs, profiles/r6_gelu_native_sk_ab.jsonl; it was neutral on the 8-wave
+# kernel, r5_gelu_native_ab.jsonl).  PLX_GELU_NATIVE=0: the table decides.
 _GELU_NATIVE = os.environ.get("PLX_GELU_NATIVE", "1") != "0"
 
 
