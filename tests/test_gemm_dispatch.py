@@ -90,3 +90,38 @@ def test_auto_dispatch_is_a_pure_function_of_the_shape(monkeypatch):
     d = gemm.decisions()
     assert d["2304x768x16384:MN"] == {"native": True, "schedule": 5} and d["16384x3072x768:KK"]["native"] is False
     gemm._seen.clear()
+
+
+def test_stream_k_plan_and_routing(monkeypatch):
+    """Schedule 9's host side on the CPU (the planner and the routing; no launch): the partial wave is split along K
+    only for long reductions whose split saves >= 16 K-tiles per workgroup, pieces are even for an even K-tile count,
+    odd / short K and accumulating calls fall back to the 8-wave kernel, PLX_GEMM_WAVES=9 selects it."""
+    lib = gemm._native.lib("plx_gemm")
+    prev = lib.plx_gemm256_set_sk_force(0)
+    try:
+        g, skt, ipb = gemm.sk_plan(4096, 6144, 4096)     # Llama QKV forward: 384 tiles, 64 K-tiles
+        assert skt == 384 % g and ipb % 2 == 0 and 4 <= ipb <= 64 - 16
+        g, skt, ipb = gemm.sk_plan(16384, 50432, 768)    # GPT-2 head: K too short to split
+        assert skt == 0 and ipb == 1
+        g, skt, ipb = gemm.sk_plan(4096, 4096, 4096)     # a full wave on a 256-CU chip: nothing to split
+        assert (skt == 0) == (256 % g == 0)
+        lib.plx_gemm256_set_sk_force(1)                  # tests split every partial wave
+        g, skt, ipb = gemm.sk_plan(512, 768, 1408)
+        assert skt == 6 and ipb >= 4 and ipb % 2 == 0
+    finally:
+        lib.plx_gemm256_set_sk_force(prev)
+    # the workspace is sized for any plan of the shape (memoised sizes stay valid when the force knob changes)
+    assert gemm._native.size("plx_gemm", "plx_gemm256_sk_ws", 512, 768, 1408) > 0
+    # shape checks happen before any device call: odd / short K is refused, ops/gemm.py runs schedule 8 instead
+    assert lib.plx_gemm256_sk(None, None, None, None, None, 512, 768, 1344, 1344, 1344, 768, 1, 1, 1.0, None, None,
+                              None) == -1
+    assert not gemm.sk_supported(512, 768, 1344) and not gemm.sk_supported(512, 512, 128)
+    assert gemm.sk_supported(512, 768, 1408) and gemm.sk_supported(16384, 50432, 768)
+    monkeypatch.setattr(gemm, "FORCE_SCHEDULE", 0)
+    monkeypatch.delenv("PLX_GEMM_WAVES", raising=False)
+    assert gemm._schedule_of(16384, 3072, 768, True, True) == gemm.SK      # forward layout default
+    assert gemm._schedule_of(16384, 768, 3072, True, False) == 5           # data gradient
+    monkeypatch.setenv("PLX_GEMM_WAVES", "9")
+    assert gemm._schedule_of(16384, 768, 3072, True, False) == gemm.SK
+    monkeypatch.setenv("PLX_GEMM_WAVES", "8")
+    assert gemm._schedule_of(16384, 3072, 768, True, True) == 0            # the library's global knob
