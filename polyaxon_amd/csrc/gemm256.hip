@@ -473,9 +473,15 @@ __device__ __forceinline__ void gemm256_tile(const Gemm256Args& p, int m0, int n
   // one wave's MFMAs (priority 1) overlap the other wave's ds_reads and DMA issue.
   if (wm == 1) __builtin_amdgcn_s_barrier();
 
-  for (int kt = 0; kt < nk; kt += 2) {
-    tile(IC<0>{}, IB<MODE != 0>{}, kt, a0);
-    if (kt + 1 < nk) tile(IC<1>{}, IB<MODE != 0>{}, kt + 1, a0);
+  int kt = 0;
+  if constexpr (MODE != 0) {  // peeled first pair: the only phases whose waits count the previous tile's stores
+    tile(IC<0>{}, IB<true>{}, 0, a0);
+    if (1 < nk) tile(IC<1>{}, IB<true>{}, 1, a0);
+    kt = 2;
+  }
+  for (; kt < nk; kt += 2) {
+    tile(IC<0>{}, IB<false>{}, kt, a0);
+    if (kt + 1 < nk) tile(IC<1>{}, IB<false>{}, kt + 1, a0);
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();  // every wave executes the same number of barriers
 

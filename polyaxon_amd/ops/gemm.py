@@ -14,8 +14,9 @@ Shapes the kernel does not take (a dimension not a multiple of 256, or K of 64) 
 :func:`supported` says which; on a GPU box a missing library raises instead of falling back (ops/_native.py).  The
 LM trainers' shapes all fit (GPT-2's vocabulary is padded to 50432 rows, models/transformer.py).
 
-Dispatch (``PLX_LM_GEMM``): ``auto`` (default) runs the kernel where it wins on every MI355X box measured and
-hipBLASLt elsewhere; ``1`` always the kernel (the GPU tests), ``0`` always hipBLASLt.  Round 4 measured the kernel
+Dispatch (``PLX_LM_GEMM``): ``auto`` (default) runs the kernel where it wins or ties on every MI355X box measured
+(since round 6 every GEMM of the GPT-2 125M step) and hipBLASLt elsewhere; ``1`` always the kernel (the GPU tests),
+``0`` always hipBLASLt.  Round 4 measured the kernel
 and hipBLASLt on three boxes / cache states (profiles/r4_lm_gemm.md): the split-K weight gradients of the narrow
 GPT-2 layers (and the tied head's) win 1.05-1.95x everywhere, a few Llama-3 8B weight / data gradients win by a few
 percent, and the large forward / data-gradient shapes swing between 1.05x and 0.79x with the box (the kernel is
@@ -50,6 +51,14 @@ SCHEDULE: Dict[Tuple[int, int, int, bool, bool], int] = {
         # GPT-2: every weight gradient (split-K), the tied head's, the attention projection's data gradient
         (2304, 768, 16384, _WGRAD, 5), (768, 768, 16384, _WGRAD, 5), (3072, 768, 16384, _WGRAD, 5),
         (768, 3072, 16384, _WGRAD, 5), (50432, 768, 16384, _WGRAD, 5), (16384, 768, 768, _DGRAD, 5),
+        # ... and, since round 6, every other GPT-2 linear: the forwards on the stream-K schedule, the data gradients
+        # on the 4-wave one.  The whole GPT-2 step on the kernel ties the mixed dispatch (708.9k vs 708.7k tokens/s
+        # over 4 + 3 alternating runs, 702.5 / 697.3k vs 697.4 / 705.2k over 2 + 2 on another box;
+        # profiles/r6_lm_step_gpt2_kernel_only_ab.jsonl), so no GPT-2 GEMM goes to hipBLASLt.
+        (16384, 2304, 768, _FWD, 9), (16384, 768, 768, _FWD, 9), (16384, 3072, 768, _FWD, 9),
+        (16384, 768, 3072, _FWD, 9), (16384, 50432, 768, _FWD, 9),
+        (16384, 768, 2304, _DGRAD, 5), (16384, 768, 3072, _DGRAD, 5), (16384, 3072, 768, _DGRAD, 5),
+        (16384, 768, 50432, _DGRAD, 5),
         # Llama-3 8B: the weight gradients and the QKV data gradient
         (6144, 4096, 4096, _WGRAD, 5), (4096, 4096, 4096, _WGRAD, 5), (28672, 4096, 4096, _WGRAD, 5),
         (4096, 14336, 4096, _WGRAD, 5), (4096, 4096, 6144, _DGRAD, 5))}
@@ -59,7 +68,7 @@ FORCE_SCHEDULE = 0
 SK = 9  # the persistent stream-K schedule (no accumulate: such calls run the 8-wave kernel)
 
 # schedule of a kernel call outside the table, by layout (PLX_LM_GEMM=1, split-K shapes): the persistent stream-K
-# kernel for the forward (both operands K-major: 2.98 vs 3.10 ms over one call of each of the 9 forward shapes in
+# kernel for the forward (both operands K-major: 2.85 vs 3.10 ms over one call of each of the 9 forward shapes in
 # profiles/r6_lm_gemm_sk.jsonl; it was the 8-wave ping-pong kernel, 4.63 vs 4.91 ms per GPT-2 step against the
 # 4-wave one), the 4-wave one for the data and weight gradients (4.40 vs 5.09, 45.2 vs 51.5; profiles/r5_lm_gemm.md).
 # PLX_GEMM_WAVES overrides it.

@@ -21,8 +21,12 @@ CLASSES = [
     ("data (plx synthetic batch)", ("synth_images", "counter_add")),
     ("conv (MIOpen igemm/CK/naive)", ("igemm", "conv", "ck::tensor_operation", "naive_conv", "gtcx")),
     ("BN (MIOpen)", ("MIOpenBatchNorm",)),
-    ("optimizer / trial kernels (plx)", ("sgd_flat", "adamw_flat", "record_metric", "commit_metric", "init_flat",
-                                         "zero_kernel")),
+    ("optimizer / trial kernels (plx)", ("sgd_flat", "adamw_flat", "adamw_mixed", "record_metric", "commit_metric",
+                                         "init_flat", "zero_kernel")),
+    ("LM GEMM (plx MFMA gemm256: 8-wave, 4-wave, stream-K, split-K reduce)", ("gemm256",)),
+    ("attention (plx flash fwd / dq / dkdv)", ("attn_fwd", "attn_bwd")),
+    ("LM fused elementwise (plx LayerNorm / RMSNorm, RoPE, SwiGLU, GELU + column sums)",
+     ("ln_fwd", "ln_bwd", "rms_", "qkv_rope", "swiglu", "colsum", "partial_colsum")),
     ("GEMM (hipBLASLt/rocBLAS)", ("Cijk", "gemm", "Gemm")),
     ("pool", ("pool",)),
     ("elementwise/other torch", ("at::native",)),

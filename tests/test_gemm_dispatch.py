@@ -75,10 +75,17 @@ def test_auto_dispatch_is_a_pure_function_of_the_shape(monkeypatch):
     (schedule 0 = library default), the rest on hipBLASLt (-1).  No timing, no CUDA call: reproducible across runs
     and identical on every DP rank."""
     monkeypatch.setenv("PLX_LM_GEMM", "auto")
-    assert set(gemm.SCHEDULE.values()) <= {4, 5, 6, 7, 8}
+    assert set(gemm.SCHEDULE.values()) <= {4, 5, 6, 7, 8, 9}
     assert gemm.schedule(2304, 768, 16384, False, False) == 5      # GPT-2 qkv wgrad (split-K)
     assert gemm.schedule(50432, 768, 16384, False, False) == 5     # GPT-2 tied head wgrad
-    assert gemm.schedule(16384, 768, 3072, True, True) == -1       # GPT-2 down fwd: hipBLASLt
+    assert gemm.schedule(16384, 768, 3072, True, True) == 9        # GPT-2 down fwd: stream-K
+    assert gemm.schedule(16384, 768, 50432, True, False) == 5      # GPT-2 head dgrad: 4-wave
+    # the whole GPT-2 125M step (bs 16 x 1024) is on the kernel
+    for fin, fout in ((768, 2304), (768, 768), (768, 3072), (3072, 768), (768, 50432)):
+        assert gemm.schedule(16384, fout, fin, True, True) >= 0
+        assert gemm.schedule(16384, fin, fout, True, False) >= 0
+        assert gemm.schedule(fout, fin, 16384, False, False) >= 0
+    assert gemm.schedule(4096, 3072, 768, True, True) == -1        # the same linear at another token count
     assert gemm.schedule(4096, 28672, 4096, True, True) == -1      # Llama up fwd: hipBLASLt
     assert gemm.schedule(28672, 4096, 4096, False, False) == 5     # Llama up wgrad
     assert gemm.splits(256, 256, 8192) > 1 and gemm.schedule(256, 256, 8192, False, False) == 0
@@ -86,9 +93,9 @@ def test_auto_dispatch_is_a_pure_function_of_the_shape(monkeypatch):
     for (M, N, K, ak, bk) in gemm.SCHEDULE:
         assert gemm.supported(M, N, K)
     gemm._seen.clear()
-    assert gemm._use_native(2304, 768, 16384, False, False) and not gemm._use_native(16384, 3072, 768, True, True)
+    assert gemm._use_native(2304, 768, 16384, False, False) and not gemm._use_native(4096, 3072, 768, True, True)
     d = gemm.decisions()
-    assert d["2304x768x16384:MN"] == {"native": True, "schedule": 5} and d["16384x3072x768:KK"]["native"] is False
+    assert d["2304x768x16384:MN"] == {"native": True, "schedule": 5} and d["4096x3072x768:KK"]["native"] is False
     gemm._seen.clear()
 
 
@@ -119,9 +126,11 @@ def test_stream_k_plan_and_routing(monkeypatch):
     assert gemm.sk_supported(512, 768, 1408) and gemm.sk_supported(16384, 50432, 768)
     monkeypatch.setattr(gemm, "FORCE_SCHEDULE", 0)
     monkeypatch.delenv("PLX_GEMM_WAVES", raising=False)
-    assert gemm._schedule_of(16384, 3072, 768, True, True) == gemm.SK      # forward layout default
-    assert gemm._schedule_of(16384, 768, 3072, True, False) == 5           # data gradient
+    # outside the table (4096 tokens): the layout defaults, or the PLX_GEMM_WAVES override
+    assert gemm._schedule_of(4096, 3072, 768, True, True) == gemm.SK       # forward layout default
+    assert gemm._schedule_of(4096, 768, 3072, True, False) == 5            # data gradient
     monkeypatch.setenv("PLX_GEMM_WAVES", "9")
-    assert gemm._schedule_of(16384, 768, 3072, True, False) == gemm.SK
+    assert gemm._schedule_of(4096, 768, 3072, True, False) == gemm.SK
     monkeypatch.setenv("PLX_GEMM_WAVES", "8")
-    assert gemm._schedule_of(16384, 3072, 768, True, True) == 0            # the library's global knob
+    assert gemm._schedule_of(4096, 3072, 768, True, True) == 0             # the library's global knob
+    assert gemm._schedule_of(16384, 3072, 768, True, True) == gemm.SK      # the table wins over the override

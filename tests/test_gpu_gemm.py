@@ -232,14 +232,14 @@ def test_auto_dispatch_runs_both_paths_and_matches(cuda, monkeypatch):
 
     monkeypatch.setenv("PLX_LM_GEMM", "auto")
     gemm._seen.clear()
-    T, fin, fout = 16384, 768, 2304
+    T, fin, fout = 4096, 768, 2304  # outside the table: the forward goes to hipBLASLt
     x, w = _rand((T, fin), cuda, 17), _rand((fout, fin), cuda, 18)
     dy = _rand((T, fout), cuda, 19)
     y = gemm.forward(x, w)
     dw = gemm.wgrad(dy, x)
     dec = gemm.decisions()
     assert dec[f"{T}x{fout}x{fin}:KK"]["native"] is False
-    assert dec[f"{fout}x{fin}x{T}:MN"] == {"native": True, "schedule": 5}
+    assert dec[f"{fout}x{fin}x{T}:MN"]["native"] is True  # split-K weight gradient
     torch.cuda.synchronize()
     _check(y, x.float() @ w.float().t(), fin)
     _check(dw, dy.float().t() @ x.float(), T)
