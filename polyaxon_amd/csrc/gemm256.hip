@@ -267,17 +267,16 @@ __device__ __forceinline__ void store_pair(const Gemm256Args& p, f32x4 a, f32x4 
 }
 
 // One output tile's K loop, K-tiles [kt0, kt0 + nk), accumulated into acc (callers zero it): the 256 x 256 x 64
-// ping-pong schedule described in the file header.  Leaves every DMA retired and every LDS read of the tile done
-// (all waves past the same barriers), so the caller may restage the LDS right away.
+// ping-pong schedule described in the file header.  Leaves every LDS read of the tile done (all waves past the same
+// barriers) and, standalone, every DMA retired, so the caller may restage the LDS right away.
 //
-// pre: the caller already issued this tile's first two K-tiles (gemm256_prologue, or the previous tile's chained
-// ring) and then `extra` more vector-memory ops (the previous tile's epilogue stores, 0 / 16 / 32): the waits of the
-// first six phases count them in, so those stores drain behind the fill instead of before it (vmcnt retires loads
-// and stores in issue order).
-// chain (persistent kernel; nk even, the next piece >= 2 K-tiles): the ring does not drain at the end of this tile
-// but goes on with the next piece's K-tiles 0 and 1 (and wave 0 its bias), into the same slots: the next tile starts
-// with its first two K-tiles landed.  nk even keeps the slot parity: the next piece's K-tile j lands where this
-// tile's K-tile nk + j would have.
+// Chained (the persistent kernel; nk even, the next piece >= 2 K-tiles): the tile's first two K-tiles were issued
+// before it (gemm256_prologue, or the previous tile's chained ring), followed by `extra` more vector-memory ops (the
+// previous tile's epilogue stores, 0 / 16 / 32): the waits of the first six phases count them in, so those stores
+// drain behind the fill instead of before it (vmcnt retires loads and stores in issue order).  The ring does not
+// drain at the end of the tile but goes on with `chain`'s K-tiles 0 and 1 (and wave 0 its bias), into the same
+// slots: the next tile starts with its first two K-tiles landed.  nk even keeps the slot parity: the next piece's
+// K-tile j lands where this tile's K-tile nk + j would have.
 struct Chain {
   int m0, n0, kt0;
   float* bias_lds;
@@ -287,11 +286,13 @@ template <bool AK, bool BKM>
 __device__ __forceinline__ void gemm256_prologue(const Gemm256Args& p, int m0, int n0, int kt0, int nk, char* smem,
                                                  int wave, int lane, float* bias_lds = nullptr);
 
-// MODE 0: standalone (issues its own fill, drains at the end); 1: persistent, fill issued by the caller, drains;
-// 2: persistent and chained (the last K-tile pair peeled, the chain decided at compile time: a runtime chain check
-// in every phase, with the chained operands' buffer resources live across the K loop, had 2.6x the branches and ran
-// 13 % slower on Llama's 4096^3 projection).
-template <bool AK, bool BKM, int MODE = 0>
+// CHAINED = false: standalone (issues its own fill, drains at the end).  CHAINED = true (the persistent kernel): the
+// fill was issued by the previous tile's chained ring (or the caller's prologue), the first K-tile pair is peeled
+// (only its waits count the previous tile's stores: with that runtime check in every phase the GPT-2 head forward
+// took 1.38 ms instead of 1.27), and the chain is a compile-time branch of the ring (a runtime chain check in every
+// phase, with the chained operands' buffer resources live across the K loop, had 2.6x the branches and ran 13 %
+// slower on Llama's 4096^3 projection).
+template <bool AK, bool BKM, bool CHAINED = false>
 __device__ __forceinline__ void gemm256_tile(const Gemm256Args& p, int m0, int n0, int kt0, int nk, f32x4 (&acc)[4][8],
                                              char* smem, int wave, int lane, int wm, int wn, int extra = 0,
                                              const Chain& chain = Chain{0, 0, 0, nullptr}) {
@@ -408,7 +409,7 @@ __device__ __forceinline__ void gemm256_tile(const Gemm256Args& p, int m0, int n
     }
   };
   // Issue seq g + 8 (tile kt + 2, kind P, into this tile's buffer CB) and wait for seq g + 2.  Past this tile's last
-  // K-tile, MODE 2 issues the chained piece's K-tile kt + 2 - nk instead (wave 0 also stages that piece's bias) and
+  // K-tile, the chained kernel issues the next piece's K-tile kt + 2 - nk instead (wave 0 also stages that piece's bias) and
   // the other modes drain the ring.
   auto ring = [&](auto cb, auto ph, auto first, int kt) {
     constexpr int CB = decltype(cb)::value, P = decltype(ph)::value;
@@ -416,7 +417,7 @@ __device__ __forceinline__ void gemm256_tile(const Gemm256Args& p, int m0, int n
     if (g + 8 < S) {
       issue(CB, kt + 2, P);
       wait12(first, g);
-    } else if constexpr (MODE == 2) {
+    } else if constexpr (CHAINED) {
       if (P == 0 && kt == nk - 2 && wave == 0 && p.bias != nullptr && chain.bias_lds != nullptr)
         glds(rsrc(p.bias + chain.n0), lane * 16, chain.bias_lds);
       chain_issue(CB, kt + 2 - nk, P);
@@ -450,7 +451,7 @@ __device__ __forceinline__ void gemm256_tile(const Gemm256Args& p, int m0, int n
   };
 
   // prologue: seq 0 .. min(7, S - 1) (tiles 0 and 1); retire seq 0, 1 and read tile 0's A-mi0
-  if constexpr (MODE == 0) {
+  if constexpr (!CHAINED) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) issue(0, 0, q);
     if (nk > 1) {
@@ -474,7 +475,7 @@ __device__ __forceinline__ void gemm256_tile(const Gemm256Args& p, int m0, int n
   if (wm == 1) __builtin_amdgcn_s_barrier();
 
   int kt = 0;
-  if constexpr (MODE != 0) {  // peeled first pair: the only phases whose waits count the previous tile's stores
+  if constexpr (CHAINED) {  // peeled first pair: the only phases whose waits count the previous tile's stores
     tile(IC<0>{}, IB<true>{}, 0, a0);
     if (1 < nk) tile(IC<1>{}, IB<true>{}, 1, a0);
     kt = 2;
@@ -611,10 +612,11 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_kernel(Gemm256Args p) {
 // back-to-back and graph-replayed launches reuse the zeroed tickets): nobody waits on anybody, so a workgroup that
 // is not yet resident (another kernel holding CUs) can never stall the others.  A workgroup's partial pieces are its
 // first (a tile's tail, slot 0) and its last SK piece (a tile's head, slot 1), so 2 G slots of 256 x 256 fp32.
-// Between data-parallel tiles the next tile's ring fill is issued before the finished tile's epilogue stores and the
-// fill's first wait counts the stores in (gemm256_tile's `extra`): the 128 KiB store of one tile drains under the
-// next tile's first loads, and the workgroups' tile ends drift apart instead of all 256 CUs hitting HBM with 32 MB
-// of stores at once (the per-tile fixed cost of profiles/r5_lm_gemm.md).
+// The DMA ring never drains between items: a tile's last two K-tiles issue the next item's first two (gemm256_tile
+// CHAINED), the finished tile's stores follow, and the next tile's first waits count them in (`extra`): the 128 KiB
+// store of one tile drains under the next tile's first loads and the workgroups' tile ends drift apart instead of
+// all 256 CUs paying the ring fill and a 32 MB store burst at once (the per-tile fixed cost of
+// profiles/r5_lm_gemm.md; profiles/r6_lm_gemm.md).
 struct SkArgs {
   float* part;        // fp32 [2 G][65536]: per-workgroup partial slots (lane-linear f32x4 layout)
   unsigned* tickets;  // [G], zero between launches
@@ -669,29 +671,27 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_sk_kernel(Gemm256Args p, SkArg
   int ctile = tile, ckb = kb, cke = ke, cm0, cn0;  // the current item; tile / kb / ke: the one after it
   origin(ctile, cm0, cn0);
   gemm256_prologue<AK, BKM>(p, cm0, cn0, ckb, cke - ckb, smem, wave, lane, s_bias[0]);
-  // An even K-tile count (>= 4) makes every piece even and >= 4 (ipb is even and >= 4 then): every tile chains into
-  // the next one, the last into a dummy re-read of itself (drained before the exit).  Other counts drain the ring
-  // per tile (MODE 1).
-  auto run = [&](auto chain_tag) {
-    constexpr bool CHAIN = decltype(chain_tag)::value;
-    int extra = 0;
-    for (int slot = 0;; slot ^= 1) {
-      const bool more = next();
-      int m0 = cm0, n0 = cn0;
-      if (more) origin(tile, m0, n0);
-      const Chain ch{m0, n0, more ? kb : ckb, more ? s_bias[slot ^ 1] : nullptr};
-      // The lane index is laundered once per tile so that the K loop's per-lane LDS / DMA offsets are recomputed
-      // per tile instead of hoisted out of the tile loop: hoisted, they stayed live through the epilogue next to
-      // the 128 accumulator VGPRs and the kernel spilled (136 VGPRs).
-      int ln;
-      asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
-      f32x4 acc[4][8];
+  // The host launches this kernel for an even K-tile count >= 4 only, so every piece is even and >= 2 (ipb is even
+  // then): every tile's ring chains into the next item, the last one into a dummy re-read of itself that is drained
+  // before the exit.
+  int extra = 0;
+  for (int slot = 0;; slot ^= 1) {
+    const bool more = next();
+    int m0 = cm0, n0 = cn0;
+    if (more) origin(tile, m0, n0);
+    const Chain ch{m0, n0, more ? kb : ckb, more ? s_bias[slot ^ 1] : nullptr};
+    // The lane index is laundered once per tile so that the K loop's per-lane LDS / DMA offsets are recomputed per
+    // tile instead of hoisted out of the tile loop: hoisted, they stayed live through the epilogue next to the 128
+    // accumulator VGPRs and the kernel spilled (136 VGPRs).
+    int ln;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+    f32x4 acc[4][8];
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-      gemm256_tile<AK, BKM, CHAIN ? 2 : 1>(p, cm0, cn0, ckb, cke - ckb, acc, smem, wave, ln, wm, wn, extra, ch);
-      // every LDS read of this tile done; unless chained, every DMA retired and the ring free
+      for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gemm256_tile<AK, BKM, true>(p, cm0, cn0, ckb, cke - ckb, acc, smem, wave, ln, wm, wn, extra, ch);
+    // every LDS read of this tile done; the next item's first two K-tiles (and its bias) are in flight
     bool store = ckb == 0 && cke == nk;
     if (!store) {
       // pieces of tile ctile: workgroups bf .. bl (the iteration space is split at multiples of ipb); the one that
@@ -752,12 +752,10 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_sk_kernel(Gemm256Args p, SkArg
         store = true;
       }
     }
-    // Unless the ring chained into it, the next tile's fill (and its bias, into the other LDS slot) goes out before
-    // this tile's stores; the stores take their bias from LDS, so nothing in the epilogue waits on vmcnt behind the
-    // fill.  ln2: a fresh laundered lane, so the fill's offsets are not kept live from the K loop through the epilogue.
+    // The stores go out after the next item's fill and take their bias from LDS, so nothing in the epilogue waits on
+    // vmcnt behind the fill.  ln2: a fresh laundered lane (the epilogue's offsets are not kept live across the K loop).
     int ln2;
     asm volatile("v_mov_b32 %0, %1" : "=v"(ln2) : "v"(lane));
-    if (!CHAIN && more) gemm256_prologue<AK, BKM>(p, m0, n0, kb, ke - kb, smem, wave, ln2, s_bias[slot ^ 1]);
     if (store) {
       f32x4 bias[2][2];
       lds_bias16(p, s_bias[slot], ln2, wn, bias);
@@ -770,10 +768,8 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_sk_kernel(Gemm256Args p, SkArg
     cke = ke;
     cm0 = m0;
     cn0 = n0;
-    }
-    if (CHAIN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy fill lands before the LDS is released
-  };
-  run(IB<true>{});  // the host launches this kernel for even K-tile counts >= 4 only
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy fill lands before the workgroup's LDS is released
 }
 
 
