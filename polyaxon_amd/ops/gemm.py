@@ -57,8 +57,10 @@ SCHEDULE: Dict[Tuple[int, int, int, bool, bool], int] = {
         # profiles/r6_lm_step_gpt2_kernel_only_ab.jsonl), so no GPT-2 GEMM goes to hipBLASLt.
         (16384, 2304, 768, _FWD, 9), (16384, 768, 768, _FWD, 9), (16384, 3072, 768, _FWD, 9),
         (16384, 768, 3072, _FWD, 9), (16384, 50432, 768, _FWD, 9),
-        (16384, 768, 2304, _DGRAD, 5), (16384, 768, 3072, _DGRAD, 5), (16384, 3072, 768, _DGRAD, 5),
-        (16384, 768, 50432, _DGRAD, 5),
+        (16384, 768, 2304, _DGRAD, 5), (16384, 768, 3072, _DGRAD, 5), (16384, 768, 50432, _DGRAD, 5),
+        # the MLP down-projection's data gradient (N = 3072 wide, K = 768) is the one data gradient where the
+        # stream-K 8-wave kernel beats the 4-wave one: 0.076-0.081 vs 0.086-0.088 ms (r6_lm_gemm_sk*.jsonl, r5)
+        (16384, 3072, 768, _DGRAD, 9),
         # Llama-3 8B: the weight gradients and the QKV data gradient
         (6144, 4096, 4096, _WGRAD, 5), (4096, 4096, 4096, _WGRAD, 5), (28672, 4096, 4096, _WGRAD, 5),
         (4096, 14336, 4096, _WGRAD, 5), (4096, 4096, 6144, _DGRAD, 5))}
