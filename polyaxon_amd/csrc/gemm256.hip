@@ -187,6 +187,8 @@ struct Gemm256Args {
   const float* bias;  // fp32 [N] added after alpha in the bf16 epilogue (the Linear bias), or null
   void* C2;           // bf16 [M][ldc]: gelu_tanh of the stored (bf16-rounded) C, or null (GPT-2's up-projection)
   int group;          // M-tiles per tile group (tile_of)
+  const __bf16* gelu_h;  // bf16 [M][ldc] or null: the epilogue stores bf16(C) * gelu_tanh'(gelu_h) instead of C (the
+                         // GELU backward of an MLP fused into the down-projection's data gradient); no bias / C2
 };
 
 // GELU, tanh approximation, of the bf16-rounded value (what a separate activation pass reading C would compute);
@@ -197,6 +199,15 @@ __device__ __forceinline__ float gelu_tanh(float h) {
 }
 
 __device__ __forceinline__ float bf16_round(float f) { return (float)(__bf16)f; }
+
+// d/dh gelu_tanh(h): the formula of csrc/lm_kernels.hip gelu_tanh_grad (bit-identical results), so the fused GELU
+// backward equals the separate pass over the stored data gradient
+__device__ __forceinline__ float gelu_tanh_grad(float h) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float e = __expf(2.f * k0 * fmaf(k1 * h * h, h, h));
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
+  return fmaf(0.5f, 1.f + t, 0.5f * h * (1.f - t * t) * k0 * fmaf(3.f * k1, h * h, 1.f));
+}
 
 // Epilogue store layout.  An MFMA tile's lane holds 4 consecutive columns of one row, so storing tiles one by one
 // writes 8 bytes per lane and 32 contiguous bytes per row: the memory side then sees 32-byte partial-line writes
@@ -232,7 +243,9 @@ __device__ __forceinline__ void load_bias8(const Gemm256Args& p, int n8, f32x4& 
 
 // bf16 epilogue of one permuted tile pair at row m, columns n8..n8+7 (n8 % 8 == 0: 16-byte aligned stores);
 // ba / bb: load_bias8 of n8 (ignored when accumulating)
-template <bool ACC>
+// GB: the kernel supports the fused GELU backward (p.gelu_h; the persistent kernel only, so the other kernels'
+// epilogues do not carry its registers)
+template <bool ACC, bool GB = false>
 __device__ __forceinline__ void store_pair(const Gemm256Args& p, f32x4 a, f32x4 b, int m, int n8, const f32x4& ba,
                                            const f32x4& bb) {
   __bf16* dst = (__bf16*)p.C + (size_t)m * p.ldc + n8;
@@ -249,6 +262,17 @@ __device__ __forceinline__ void store_pair(const Gemm256Args& p, f32x4 a, f32x4 
   } else {
     a = a * p.alpha + ba;
     b = b * p.alpha + bb;
+    if (GB && p.gelu_h != nullptr) {  // uniform branch: dh = bf16(dA) * gelu'(h), dA rounded as a stored C would be
+      const uint4 hv = *(const uint4*)(p.gelu_h + (size_t)m * p.ldc + n8);
+      a[0] = bf16_round(a[0]) * gelu_tanh_grad(__uint_as_float(hv.x << 16));
+      a[1] = bf16_round(a[1]) * gelu_tanh_grad(__uint_as_float(hv.x & 0xffff0000u));
+      a[2] = bf16_round(a[2]) * gelu_tanh_grad(__uint_as_float(hv.y << 16));
+      a[3] = bf16_round(a[3]) * gelu_tanh_grad(__uint_as_float(hv.y & 0xffff0000u));
+      b[0] = bf16_round(b[0]) * gelu_tanh_grad(__uint_as_float(hv.z << 16));
+      b[1] = bf16_round(b[1]) * gelu_tanh_grad(__uint_as_float(hv.z & 0xffff0000u));
+      b[2] = bf16_round(b[2]) * gelu_tanh_grad(__uint_as_float(hv.w << 16));
+      b[3] = bf16_round(b[3]) * gelu_tanh_grad(__uint_as_float(hv.w & 0xffff0000u));
+    }
   }
   uint4 packed;
   packed.x = pack_bf16x2(a[0], a[1]);
@@ -491,7 +515,7 @@ __device__ __forceinline__ void gemm256_tile(const Gemm256Args& p, int m0, int n
 // bf16 epilogue of one tile (bias / GELU / accumulate per the args): column-adjacent tile pairs regrouped to 16-byte
 // stores (pair_permute)
 // (bias: load_bias16 of the tile, or zeros when accumulating); 16 stores per lane, 32 with the GELU output
-template <bool ACC>
+template <bool ACC, bool GB = false>
 __device__ __forceinline__ void gemm256_store(const Gemm256Args& p, f32x4 (&acc)[4][8], int m0, int n0, int lane, int wm,
                                               int wn, const f32x4 (&bias)[2][2]) {
   const int fr = lane & 15, fq = lane >> 4;
@@ -502,7 +526,7 @@ __device__ __forceinline__ void gemm256_store(const Gemm256Args& p, f32x4 (&acc)
     for (int mt = 0; mt < 8; ++mt) {
       f32x4 a = acc[2 * np][mt], b = acc[2 * np + 1][mt];
       pair_permute(a, b);
-      store_pair<ACC>(p, a, b, m0 + wm * 128 + mt * 16 + fr, n8, bias[np][0], bias[np][1]);
+      store_pair<ACC, GB>(p, a, b, m0 + wm * 128 + mt * 16 + fr, n8, bias[np][0], bias[np][1]);
     }
   }
 }
@@ -759,7 +783,7 @@ __global__ void __launch_bounds__(NTH, 1) gemm256_sk_kernel(Gemm256Args p, SkArg
     if (store) {
       f32x4 bias[2][2];
       lds_bias16(p, s_bias[slot], ln2, wn, bias);
-      gemm256_store<false>(p, acc, cm0, cn0, ln2, wm, wn, bias);
+      gemm256_store<false, true>(p, acc, cm0, cn0, ln2, wm, wn, bias);
     }
     extra = store ? (p.C2 != nullptr ? 32 : 16) : 0;
     if (!more) break;
@@ -1122,13 +1146,16 @@ PLX_API int plx_gemm256_sk_plan(int M, int N, int K, int* sk_tiles, int* ipb) {
 // C[M][N] = alpha * A . B (+ bias) (gelu_out as plx_gemm256_exv) on the persistent stream-K kernel: one workgroup per
 // CU.  K must be an even multiple of 64, >= 256 (-1 otherwise: ops/gemm.py runs the 8-wave kernel then).  ws: plx_gemm256_sk_ws floats (may be null when that is 0); tickets: >= CU-count zeroed uint32 that the kernel
 // leaves zeroed (one array per device, launches on one stream at a time).  No accumulate.
+// gelu_h: bf16 [M][ldc] (16-byte aligned) or null: C = bf16(alpha A.B) * gelu_tanh'(gelu_h), the GELU backward
+// fused into the data gradient (not with bias / gelu_out)
 PLX_API int plx_gemm256_sk(const void* A, const void* B, void* C, void* ws, void* tickets, int M, int N, int K, int lda,
                            int ldb, int ldc, int a_kmajor, int b_kmajor, float alpha, const float* bias,
-                           void* gelu_out, void* stream) {
+                           void* gelu_out, const void* gelu_h, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return -1;
   if ((K / BK) % 2 || K / BK < 4) return -1;  // the chained ring needs an even K-tile count >= 4
   if (bias != nullptr && (uintptr_t)bias % 16) return -1;
   if (gelu_out != nullptr && (uintptr_t)gelu_out % 16) return -1;
+  if (gelu_h != nullptr && ((uintptr_t)gelu_h % 16 || bias != nullptr || gelu_out != nullptr)) return -1;
   if (lda % 8 || ldb % 8 || ldc % 8 || (uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return -1;
   const long long aspan = a_kmajor ? (long long)BM * lda * 2 : (long long)K * lda * 2;
   const long long bspan = b_kmajor ? (long long)BN * ldb * 2 : (long long)K * ldb * 2;
@@ -1139,7 +1166,7 @@ PLX_API int plx_gemm256_sk(const void* A, const void* B, void* C, void* ws, void
   if (!sk.sk_tiles) G = min(G, (M / BM) * (N / BN));  // data-parallel only: no idle workgroups
   if (sk.sk_tiles && (!ws || !tickets)) return -5;
   Gemm256Args a{(const __bf16*)A, (const __bf16*)B, C, M, N, K, lda, ldb, ldc, 0, alpha, bias, gelu_out,
-                g_group > 0 ? g_group : 1};
+                g_group > 0 ? g_group : 1, (const __bf16*)gelu_h};
   hipStream_t st = (hipStream_t)stream;
   int rc;
   if (a_kmajor && b_kmajor) rc = launch_sk<true, true>(a, sk, G, st);

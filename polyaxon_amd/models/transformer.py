@@ -155,8 +155,8 @@ class MLP(nn.Module):
     def forward(self, x):
         if self.kind == "swiglu":
             h = lm_ops.swiglu(lm_ops.linear(x, self.up.weight, self.up.bias))
-        else:  # GELU inside the op: its backward and the up-projection's bias gradient are one pass
-            h = lm_ops.linear(x, self.up.weight, self.up.bias, act="gelu_tanh")
+        else:  # GELU inside the op, its backward in the down-projection's data-gradient epilogue (ops/lm.py gelu_mlp)
+            return lm_ops.gelu_mlp(x, self.up.weight, self.up.bias, self.down.weight, self.down.bias)
         return lm_ops.linear(h, self.down.weight, self.down.bias)
 
 

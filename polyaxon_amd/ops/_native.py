@@ -308,7 +308,7 @@ SIGNATURES: Dict[str, Dict[str, list]] = {
         "plx_gemm256_sk_ws": [_I, _I, _I],
         "plx_gemm256_sk_plan": [_I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)],
         "plx_gemm256_set_sk_force": [_I],
-        "plx_gemm256_sk": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P],
+        "plx_gemm256_sk": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P],
     },
     "plx_attn": {
         "plx_attn_fwd": [_P, _I, _P],

@@ -163,13 +163,17 @@ def _workspace(device: torch.device, floats: int) -> torch.Tensor:
 
 def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool,
          out: Optional[torch.Tensor] = None, accumulate: bool = False, alpha: float = 1.0,
-         bias: Optional[torch.Tensor] = None, gelu_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+         bias: Optional[torch.Tensor] = None, gelu_out: Optional[torch.Tensor] = None,
+         gelu_h: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[M][N] (bf16, row-major, may be a strided view with unit column stride) = alpha * A . B (+ bias) (+ out).
 
     ``a`` is A[M][K] when ``a_kmajor`` else A stored [K][M]; ``b`` is B[N][K] when ``b_kmajor`` else [K][N].
     Both are contiguous bf16 (leading dimension = their row length).  ``bias``: [N], added in fp32 by the epilogue
     (cast to a contiguous fp32 copy if it is not one); not with ``accumulate``.  ``gelu_out``: a bf16 tensor shaped
-    like ``out`` that also receives gelu_tanh(out) from the same epilogue (GPT-2's up-projection + activation)."""
+    like ``out`` that also receives gelu_tanh(out) from the same epilogue (GPT-2's up-projection + activation).
+    ``gelu_h``: a bf16 tensor laid out like ``out``; the epilogue stores bf16(A.B) * gelu_tanh'(gelu_h) instead (an
+    MLP's GELU backward fused into the down-projection's data gradient; the stream-K schedule only, see
+    :func:`gelu_bwd_supported`)."""
     if not supported(M, N, K):
         raise ValueError(f"gemm256 needs M, N % 256 == 0 and K % 64 == 0 (got {M}x{N}x{K})")
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not (a.is_contiguous() and b.is_contiguous()):
@@ -193,9 +197,15 @@ def gemm(a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, a_kmajor: boo
         raise ValueError("gelu_out must be a bf16 tensor laid out like out (and no accumulate)")
     lib = _native.lib("plx_gemm")
     v = _schedule_of(M, N, K, a_kmajor, b_kmajor)
+    if gelu_h is not None:
+        if (v != SK or accumulate or bias is not None or gelu_out is not None or not sk_supported(M, N, K)
+                or gelu_h.dtype != torch.bfloat16 or gelu_h.shape != out.shape or gelu_h.stride() != out.stride()
+                or gelu_h.data_ptr() % 16):
+            raise ValueError("gelu_h needs the stream-K schedule, no bias / gelu_out / accumulate, and a bf16 tensor "
+                             "laid out like out")
     if v == SK:
         if not accumulate and sk_supported(M, N, K):
-            return _gemm_sk(lib, a, b, out, M, N, K, a_kmajor, b_kmajor, alpha, bias, gelu_out)
+            return _gemm_sk(lib, a, b, out, M, N, K, a_kmajor, b_kmajor, alpha, bias, gelu_out, gelu_h)
         v = 8  # accumulating calls and odd / short K: the 8-wave kernel
     ns = splits(M, N, K)
     ws = _workspace(a.device, ns * M * N).data_ptr() if ns > 1 else None
@@ -223,7 +233,7 @@ def sk_plan(M: int, N: int, K: int) -> Tuple[int, int, int]:
     return g, t.value, i.value
 
 
-def _gemm_sk(lib, a, b, out, M, N, K, a_kmajor, b_kmajor, alpha, bias, gelu_out):
+def _gemm_sk(lib, a, b, out, M, N, K, a_kmajor, b_kmajor, alpha, bias, gelu_out, gelu_h=None):
     """schedule 9: the persistent stream-K kernel (csrc/gemm256.hip gemm256_sk_kernel)"""
     floats = _native.size("plx_gemm", "plx_gemm256_sk_ws", M, N, K)
     if floats < 0:
@@ -233,10 +243,19 @@ def _gemm_sk(lib, a, b, out, M, N, K, a_kmajor, b_kmajor, alpha, bias, gelu_out)
     rc = lib.plx_gemm256_sk(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws, tickets.data_ptr(), M, N, K,
                             K if a_kmajor else M, K if b_kmajor else N, out.stride(0), int(a_kmajor), int(b_kmajor),
                             float(alpha), bias.data_ptr() if bias is not None else None,
-                            gelu_out.data_ptr() if gelu_out is not None else None, _native.current_stream())
+                            gelu_out.data_ptr() if gelu_out is not None else None,
+                            gelu_h.data_ptr() if gelu_h is not None else None, _native.current_stream())
     if rc != 0:
         raise RuntimeError(f"plx_gemm256_sk failed ({rc}) for {M}x{N}x{K} a_kmajor={a_kmajor} b_kmajor={b_kmajor}")
     return out
+
+
+def gelu_bwd_supported(T: int, d_ff: int, d: int) -> bool:
+    """Can the data gradient dA[T][d_ff] = dy[T][d] . W_down[d][d_ff] carry the GELU backward in its epilogue (the
+    dispatch runs it on the stream-K schedule)?"""
+    if not (supported(T, d_ff, d) and sk_supported(T, d_ff, d)) or mode() == "0":
+        return False
+    return _use_native(T, d_ff, d, True, False) and _schedule_of(T, d_ff, d, True, False) == SK
 
 
 def linear_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:

@@ -121,7 +121,11 @@ def test_stream_k_plan_and_routing(monkeypatch):
     assert gemm._native.size("plx_gemm", "plx_gemm256_sk_ws", 512, 768, 1408) > 0
     # shape checks happen before any device call: odd / short K is refused, ops/gemm.py runs schedule 8 instead
     assert lib.plx_gemm256_sk(None, None, None, None, None, 512, 768, 1344, 1344, 1344, 768, 1, 1, 1.0, None, None,
+                              None, None) == -1
+    # the fused GELU backward is refused with a bias (before any device call)
+    assert lib.plx_gemm256_sk(None, None, None, None, None, 512, 768, 1408, 1408, 1408, 768, 1, 0, 1.0, 16, None, 16,
                               None) == -1
+    assert not gemm.gelu_bwd_supported(512, 3072, 96)
     assert not gemm.sk_supported(512, 768, 1344) and not gemm.sk_supported(512, 512, 128)
     assert gemm.sk_supported(512, 768, 1408) and gemm.sk_supported(16384, 50432, 768)
     monkeypatch.setattr(gemm, "FORCE_SCHEDULE", 0)

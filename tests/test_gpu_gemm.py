@@ -380,3 +380,72 @@ def test_gemm256_stream_k_in_graph(stream_k, cuda):
         graph.replay()
         torch.cuda.synchronize()
         assert torch.equal(out, ref)
+
+
+def _gelu_grad_ref(h):
+    """d/dh gelu_tanh(h) in fp32 (torch's own formula, through autograd)"""
+    hh = h.float().detach().requires_grad_()
+    F.gelu(hh, approximate="tanh").sum().backward()
+    return hh.grad
+
+
+def test_gemm256_stream_k_gelu_backward_epilogue(stream_k, cuda):
+    """gelu_h: the data gradient's epilogue stores bf16(dy . W) * gelu_tanh'(h) -- against the fp32 chain, and against
+    the separate pass it replaces (the stored bf16 data gradient, then plx_gelu_bwd_colsum's dh) to one bf16 rounding
+    step: the same formula, but the two kernels' instruction sequences may differ in the last fp32 bit before the
+    bf16 rounding."""
+    gemm = stream_k
+    from polyaxon_amd.ops import lm
+
+    T, d, d_ff = 512, 768, 3072
+    dy = _rand((T, d), cuda, 31)
+    w = (_rand((d, d_ff), cuda, 32).float() * 0.05).to(torch.bfloat16)  # W_down [out = d][in = d_ff]
+    h = _rand((T, d_ff), cuda, 33)
+    dh = gemm.gemm(dy, w, T, d_ff, d, True, False, gelu_h=h)
+    da = gemm.gemm(dy, w, T, d_ff, d, True, False)  # the unfused data gradient
+    torch.cuda.synchronize()
+    ref = (dy.float() @ w.float()) * _gelu_grad_ref(h)
+    _check(dh, ref, d)
+    b = torch.zeros(d_ff, device=cuda, requires_grad=True)
+    dh2, _ = lm.bias_grad(da, b, gelu_h=h)  # the separate pass
+    torch.cuda.synchronize()
+    diff = (dh.float() - dh2.float()).abs()
+    assert bool((diff <= dh2.float().abs() * 2.0 ** -7 + 1e-30).all()), diff.max().item()
+    assert (diff > 0).float().mean().item() < 0.01
+    with pytest.raises(ValueError):
+        gemm.gemm(dy, w, T, d_ff, d, True, False, gelu_h=h, bias=torch.zeros(d_ff, device=cuda))
+
+
+@pytest.mark.parametrize("T", [512, 16384])
+def test_gelu_mlp_fused_backward_matches_fp32(cuda, monkeypatch, T):
+    """ops.lm.gelu_mlp (GPT-2's MLP as one op, the GELU backward in the down-projection's data-gradient epilogue):
+    output, dx, both weight and bias gradients against fp32 autograd of linear -> gelu_tanh -> linear.  T = 16384 is
+    GPT-2's bs 16 x 1024 (the table routes its down-projection data gradient to the stream-K schedule); T = 512
+    forces that schedule through PLX_LM_GEMM=1 and PLX_GEMM_WAVES=9."""
+    from polyaxon_amd.ops import lm
+
+    monkeypatch.setenv("PLX_LM_GEMM", "auto")
+    if T != 16384:  # every GEMM on the kernel, the stream-K schedule outside the table
+        monkeypatch.setenv("PLX_LM_GEMM", "1")
+        monkeypatch.setenv("PLX_GEMM_WAVES", "9")
+    d, d_ff = 768, 3072
+    x = _rand((T, d), cuda, 34).requires_grad_()
+    wu = (_rand((d_ff, d), cuda, 35).float() * 0.03).to(torch.bfloat16).requires_grad_()
+    bu = (_rand((d_ff,), cuda, 36).float() * 0.1).to(torch.bfloat16).requires_grad_()
+    wd = (_rand((d, d_ff), cuda, 37).float() * 0.03).to(torch.bfloat16).requires_grad_()
+    bd = (_rand((d,), cuda, 38).float() * 0.1).to(torch.bfloat16).requires_grad_()
+    y = lm.gelu_mlp(x, wu, bu, wd, bd)
+    assert "GeluMlpMfma" in type(y.grad_fn).__name__
+    dy = _rand((T, d), cuda, 39)
+    y.backward(dy)
+    ref = [t.detach().float().requires_grad_() for t in (x, wu, bu, wd, bd)]
+    yr = F.linear(F.gelu(F.linear(ref[0], ref[1], ref[2]), approximate="tanh"), ref[3], ref[4])
+    yr.backward(dy.float())
+    torch.cuda.synchronize()
+    _check(y, yr.detach(), d_ff)
+    _check(x.grad, ref[0].grad, d_ff)
+    _check(wu.grad, ref[1].grad, T)
+    _check(wd.grad, ref[3].grad, T)
+    # bias gradients: column sums of T bf16-rounded gradient rows, so the error grows like sqrt(T): relative to scale
+    _check(bu.grad, ref[2].grad, T)
+    _check(bd.grad, ref[4].grad, T)
