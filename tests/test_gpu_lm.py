@@ -127,11 +127,12 @@ def test_optimizer_in_backward_matches_monolithic_step_on_gpu(cuda, arch):
     assert len(d.buckets) > 3 and d.stepped == 4 * len(d.buckets)
 
 
-@pytest.mark.parametrize("B,S,V", [(2, 5, 50257), (3, 17, 256), (1, 2, 1000), (4, 33, 130001)])
+@pytest.mark.parametrize("B,S,V", [(2, 5, 50257), (3, 17, 256), (1, 2, 1000), (4, 33, 130001), (2, 9, 50432),
+                                   (1, 4, 65536)])
 def test_next_token_xent_matches_fp32(cuda, B, S, V):
     """The fused cross entropy (csrc/lm_kernels.hip plx_xent_fwd / _bwd) on bf16 logits -- odd vocabularies whose rows
-    start mid-chunk included -- against F.cross_entropy of the same logits in fp32: loss and logits gradient (the
-    last position of every sequence gets a zero gradient), with a non-unit incoming gradient."""
+    start mid-chunk included, GPT-2's padded 50432 -- against F.cross_entropy of the same logits in fp32: loss and
+    logits gradient (the last position of every sequence gets a zero gradient), with a non-unit incoming gradient."""
     from polyaxon_amd.ops.lm import next_token_xent
 
     torch.manual_seed(0)
@@ -145,6 +146,34 @@ def test_next_token_xent_matches_fp32(cuda, B, S, V):
     assert abs(float(loss) - float(ref)) < 1e-4 * max(1.0, abs(float(ref)))
     g, gr = logits.grad.float(), ref_in.grad
     assert float(g[:, -1].abs().max()) == 0.0
+    torch.testing.assert_close(g, gr, rtol=1e-2, atol=1e-2 * float(gr.abs().max()))
+
+
+def test_next_token_xent_unit_gradient_and_ignored_tokens(cuda):
+    """Targets outside [0, V) (-100 and > V) give zero loss rows and zero gradient rows, with the usual unit incoming
+    gradient, against F.cross_entropy with ignore_index -- whose mean skips the ignored rows, so the reference is
+    rescaled to the fused mean over all rows.  (A one-pass forward+gradient kernel holding each row in registers was
+    measured neutral on the GPT-2 step, 711.9-715.0k vs 712.4-715.3k tokens/s, profiles/r6_xent_onepass_ab.jsonl,
+    and removed.)"""
+    from polyaxon_amd.ops.lm import next_token_xent
+
+    torch.manual_seed(1)
+    B, S, V = 2, 12, 50432
+    logits = (torch.randn(B, S, V, device=cuda) * 3).to(torch.bfloat16).requires_grad_()
+    tokens = torch.randint(0, V, (B, S), device=cuda)
+    tokens[0, 3] = -100
+    tokens[1, 7] = V + 5
+    loss = next_token_xent(logits, tokens)
+    loss.backward()
+    tgt = tokens[:, 1:].reshape(-1).clone()
+    valid = (tgt >= 0) & (tgt < V)
+    tgt[~valid] = -100
+    ref_in = logits.detach().float().requires_grad_()
+    ref = F.cross_entropy(ref_in[:, :-1].reshape(-1, V), tgt, ignore_index=-100, reduction="sum") / tgt.numel()
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 1e-4 * max(1.0, abs(float(ref)))
+    g, gr = logits.grad.float(), ref_in.grad
+    assert float(g[:, -1].abs().max()) == 0.0 and float(g[0, 2].abs().max()) == 0.0 and float(g[1, 6].abs().max()) == 0.0
     torch.testing.assert_close(g, gr, rtol=1e-2, atol=1e-2 * float(gr.abs().max()))
 
 
