@@ -116,6 +116,18 @@ prof)
     fi
     echo "== [$v]"; head -25 ${O}_${i}_phases.md
   done ;;
+apitrace)  # HIP API + kernel trace of bench.py: which API calls block the host, and the host's lead (api_blockers.py)
+  rm -rf /tmp/plx_api
+  timeout -k 10 ${LIMIT:-600} rocprofv3 --hip-trace --kernel-trace -d /tmp/plx_api -o run --output-format csv \
+    -- python3 bench.py ${BENCH_ARGS:---steps 1 --warmup 0} > ${O}.log 2>&1 || fail "apitrace" $? ${O}.log
+  api=$(find /tmp/plx_api -name 'run_hip_api_trace.csv' | head -1)
+  trace=$(find /tmp/plx_api -name 'run_kernel_trace.csv' | head -1)
+  timeout -k 10 300 python3 scripts/api_blockers.py "$api" "$trace" > ${O}_blockers.jsonl || fail blockers $? ${O}.log
+  if [ -n "${WINDOW:-}" ]; then
+    python3 scripts/trace_window.py "$trace" --api "$api" --match "$WINDOW" --occurrence ${WOCC:--2} \
+      --before ${WBEFORE:-20} --after ${WAFTER:-40} > ${O}_window.txt
+  fi
+  cut -c1-300 ${O}_blockers.jsonl ;;
 pmc)
   SETS=${COUNTER_SETS:-"SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT;SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_WAVES TCC_HIT_sum TCC_MISS_sum;TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE"}
   IFS=';' read -ra CS <<< "$SETS"; i=0
