@@ -1071,12 +1071,21 @@ int g_group = 4;  // M-tiles per tile group (tile_of; plx_gemm256_set_group, 1 =
 int g_split_target = 256;  // blocks the split-K planner aims for (one per CU: splitting a grid that already
                            // fills the chip measured slower); plx_gemm256_set_split_target
 
-// K-tiles per split so that tiles x splits reaches ~g_split_target blocks while every split keeps >= 8 K-tiles
+// K-tiles per split: the most blocks (tiles x splits) up to g_split_target, every split >= 8 K-tiles and even.
+// Any split count, not only powers of two: GPT-2's 36-tile MLP weight gradients took 4 splits = 144 blocks (56 % of
+// the CUs) under the power-of-two rule and take 7 = 252 now; the 9-tile projection 16 -> 26 splits.
 int plan_kt_per_split(int M, int N, int K) {
   const int tiles = (M / BM) * (N / BN), nk = K / BK;
-  int splits = 1;
-  while (tiles * splits * 2 <= g_split_target && nk / (splits * 2) >= 8) splits *= 2;
-  return (nk + splits - 1) / splits;
+  int best = nk, best_blocks = tiles;
+  for (int s = 2; 2 * tiles <= g_split_target && s <= nk / 8; ++s) {
+    int kps = (nk + s - 1) / s;
+    kps += kps & 1;
+    if (kps < 8) break;
+    const int blocks = tiles * ((nk + kps - 1) / kps);
+    if (blocks > g_split_target) break;
+    if (blocks > best_blocks) best = kps, best_blocks = blocks;
+  }
+  return best;
 }
 
 // Stream-K plan for G persistent workgroups.  The partial wave of tiles (T % G; all of them when T < G) is split along

@@ -14,6 +14,7 @@
 #                            after a '|' ("PLX_X=1|--zero1")
 #   ablib                    the same, swapping two builds of one library in place: LIB=plx_bn expects
 #                            polyaxon_amd/_native/lib<LIB>_{new,old}.so, runs TESTS with "new", then new/old x ROUNDS
+#                            (CMD as for ab)
 #   prof                     rocprofv3 kernel trace of bench.py (BENCH_ARGS), summarised on the box: steady-state
 #                            kernel table (prof_summary.py) and step phases (step_phases.py); AB_LIST as for ab;
 #                            WINDOW=<kernel substring>: the launch sequence around it (trace_window.py); the
@@ -91,7 +92,7 @@ ablib)
   for r in $(seq ${ROUNDS:-2}); do
     for v in new old; do
       cp $D/lib${LIB}_$v.so $D/lib${LIB}.so
-      timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 13 --warmup 2} > ${O}_${r}_$v.json 2> ${O}_${r}_$v.err \
+      timeout -k 10 600 python -u ${CMD:-bench.py ${BENCH_ARGS:---steps 13 --warmup 2}} > ${O}_${r}_$v.json 2> ${O}_${r}_$v.err \
         || fail "bench [$v]" $? ${O}_${r}_$v.err
       bench_line "$v" ${O}_${r}_$v.json >> $O.jsonl
       tail -1 $O.jsonl
