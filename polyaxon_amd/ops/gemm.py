@@ -50,16 +50,19 @@ SCHEDULE: Dict[Tuple[int, int, int, bool, bool], int] = {
     (M, N, K) + lay: v for (M, N, K, lay, v) in (
         # GPT-2: every weight gradient (split-K), the tied head's, the attention projection's data gradient
         (2304, 768, 16384, _WGRAD, 5), (768, 768, 16384, _WGRAD, 5), (3072, 768, 16384, _WGRAD, 5),
-        (768, 3072, 16384, _WGRAD, 5), (50432, 768, 16384, _WGRAD, 5), (16384, 768, 768, _DGRAD, 5),
-        # ... and, since round 6, every other GPT-2 linear: the forwards on the stream-K schedule, the data gradients
-        # on the 4-wave one.  The whole GPT-2 step on the kernel ties the mixed dispatch (708.9k vs 708.7k tokens/s
-        # over 4 + 3 alternating runs, 702.5 / 697.3k vs 697.4 / 705.2k over 2 + 2 on another box;
-        # profiles/r6_lm_step_gpt2_kernel_only_ab.jsonl), so no GPT-2 GEMM goes to hipBLASLt.
+        (768, 3072, 16384, _WGRAD, 5), (50432, 768, 16384, _WGRAD, 5), (16384, 768, 768, _DGRAD, 9),
+        # ... and, since round 6, every other GPT-2 linear: the forwards on the stream-K schedule.  The whole GPT-2
+        # step on the kernel ties the mixed dispatch (708.9k vs 708.7k tokens/s over 4 + 3 alternating runs,
+        # 702.5 / 697.3k vs 697.4 / 705.2k over 2 + 2 on another box; profiles/r6_lm_step_gpt2_kernel_only_ab.jsonl),
+        # so no GPT-2 GEMM goes to hipBLASLt.
         (16384, 2304, 768, _FWD, 9), (16384, 768, 768, _FWD, 9), (16384, 3072, 768, _FWD, 9),
         (16384, 768, 3072, _FWD, 9), (16384, 50432, 768, _FWD, 9),
-        (16384, 768, 2304, _DGRAD, 5), (16384, 768, 3072, _DGRAD, 5), (16384, 768, 50432, _DGRAD, 5),
-        # the MLP down-projection's data gradient (N = 3072 wide, K = 768) is the one data gradient where the
-        # stream-K 8-wave kernel beats the 4-wave one: 0.076-0.081 vs 0.086-0.088 ms (r6_lm_gemm_sk*.jsonl, r5)
+        # data gradients: the stream-K kernel everywhere but the head's (K = 50432, where the 4-wave one is 1.19 vs
+        # 1.47 ms).  On the 192-tile N = 768 grids it beats the 4-wave one: QKV 0.064 vs 0.075 ms, MLP up 0.077 vs
+        # 0.080, projection 0.027 vs 0.028 (profiles/r6_gemm_sched_gpt2.jsonl), +0.25 % on the step over 3
+        # alternating pairs (r6_dgrad_sk_gpt2_step_ab.jsonl); the MLP down-projection's (N = 3072, K = 768):
+        # 0.076-0.081 vs 0.086-0.088 ms (r6_lm_gemm_sk*.jsonl, r5)
+        (16384, 768, 2304, _DGRAD, 9), (16384, 768, 3072, _DGRAD, 9), (16384, 768, 50432, _DGRAD, 5),
         (16384, 3072, 768, _DGRAD, 9),
         # Llama-3 8B: the weight gradients and the QKV data gradient
         (6144, 4096, 4096, _WGRAD, 5), (4096, 4096, 4096, _WGRAD, 5), (28672, 4096, 4096, _WGRAD, 5),

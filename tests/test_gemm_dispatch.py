@@ -80,6 +80,7 @@ def test_auto_dispatch_is_a_pure_function_of_the_shape(monkeypatch):
     assert gemm.schedule(50432, 768, 16384, False, False) == 5     # GPT-2 tied head wgrad
     assert gemm.schedule(16384, 768, 3072, True, True) == 9        # GPT-2 down fwd: stream-K
     assert gemm.schedule(16384, 768, 50432, True, False) == 5      # GPT-2 head dgrad: 4-wave
+    assert gemm.schedule(16384, 768, 2304, True, False) == 9       # GPT-2 qkv dgrad (192 tiles): stream-K
     # the whole GPT-2 125M step (bs 16 x 1024) is on the kernel
     for fin, fout in ((768, 2304), (768, 768), (768, 3072), (3072, 768), (768, 50432)):
         assert gemm.schedule(16384, fout, fin, True, True) >= 0
