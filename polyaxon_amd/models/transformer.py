@@ -124,7 +124,7 @@ class Attention(nn.Module):
         B, S, _ = x.shape
         cfg = self.cfg
         hd = cfg.head_dim
-        qkv = lm_ops.linear(x, self.qkv.weight, self.qkv.bias)
+        qkv = lm_ops.linear(x, self.qkv.weight, self.qkv.bias, side=True)
         if qkv.dtype == torch.bfloat16 and qkv.is_cuda:
             # one HIP pass: split + RoPE + head-major relayout (ops/lm.py)
             q, k, v = lm_ops.qkv_rope(qkv, B, S, cfg.n_heads, cfg.kv_heads, hd, rope)
@@ -139,7 +139,7 @@ class Attention(nn.Module):
         # hand-written CDNA4 flash attention (ops/attention.py, csrc/attn_kernels.hip): GQA straight into the
         # kernel (no repeat_interleave of K/V), output written in [B, S, H, D] so the projection reads it as is
         y = flash_attention(q, k, v, causal=True)
-        return lm_ops.linear(y.reshape(B, S, cfg.n_heads * hd), self.proj.weight, self.proj.bias)
+        return lm_ops.linear(y.reshape(B, S, cfg.n_heads * hd), self.proj.weight, self.proj.bias, side=True)
 
 
 class MLP(nn.Module):
@@ -154,10 +154,10 @@ class MLP(nn.Module):
 
     def forward(self, x):
         if self.kind == "swiglu":
-            h = lm_ops.swiglu(lm_ops.linear(x, self.up.weight, self.up.bias))
+            h = lm_ops.swiglu(lm_ops.linear(x, self.up.weight, self.up.bias, side=True))
         else:  # GELU inside the op, its backward in the down-projection's data-gradient epilogue (ops/lm.py gelu_mlp)
             return lm_ops.gelu_mlp(x, self.up.weight, self.up.bias, self.down.weight, self.down.bias)
-        return lm_ops.linear(h, self.down.weight, self.down.bias)
+        return lm_ops.linear(h, self.down.weight, self.down.bias, side=True)
 
 
 class Block(nn.Module):

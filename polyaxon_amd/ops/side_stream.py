@@ -97,6 +97,18 @@ def run(fn: Callable[[], None], tensors: Iterable[torch.Tensor], dev: torch.devi
         torch.autograd.Variable._execution_engine.queue_callback(lambda d=dev: join(d))
 
 
+def fence(stream: "torch.cuda.Stream", dev: torch.device) -> None:
+    """``stream`` waits for every side-stream launch queued so far on this device, without stalling the main stream:
+    a consumer of flat-slot gradients that runs before the end-of-backward join (FlatDDP's bucket all-reduce, fired by
+    the parameter's post-accumulate hook as soon as the op that queued its weight gradient returns) must not read the
+    slot before the side stream has written it."""
+    if dev.type != "cuda":
+        return
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if _pending.get(idx):
+        stream.wait_stream(_side[idx])
+
+
 def join(dev: torch.device) -> None:
     """Main stream waits for every side-stream weight-gradient launch of this device."""
     if dev.type != "cuda":

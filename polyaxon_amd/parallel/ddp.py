@@ -44,6 +44,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from polyaxon_amd.ops import side_stream
 from polyaxon_amd.ops.flat import FlatParams
 
 
@@ -264,6 +265,12 @@ class FlatDDP:
                 self._launch(b)
         return hook
 
+    def _wait_grads(self, stream) -> None:
+        """``stream`` waits for the bucket's gradients: the main stream's, and the weight gradients that ops queued on
+        the side stream (ops/side_stream.py) before their parameters' hooks fired"""
+        stream.wait_stream(torch.cuda.current_stream(self.flat.device))
+        side_stream.fence(stream, self.flat.device)
+
     def _launch(self, b: int) -> None:
         if self.zero:
             self._launch_sharded(b)
@@ -275,11 +282,11 @@ class FlatDDP:
             self.launched += 1
             op = "avg" if self.avg_supported else "sum"
             if self._comm.synchronous:
+                side_stream.join(self.flat.device)  # the bucket's side-stream weight gradients (ops/side_stream.py)
                 self._comm.all_reduce(view.data, op=op)
                 div = None if self.avg_supported else view
             else:
-                cur = torch.cuda.current_stream(self.flat.device)
-                self._comm_stream.wait_stream(cur)
+                self._wait_grads(self._comm_stream)
                 with torch.cuda.stream(self._comm_stream):
                     self._comm.all_reduce(view.data, op=op)
                     if not self.avg_supported:
@@ -287,6 +294,7 @@ class FlatDDP:
                 h = _StreamWork(self._comm_stream)
         elif self.coll:
             self.launched += 1
+            side_stream.join(self.flat.device)  # the PG collective orders after the current stream only
             if self.avg_supported:
                 h = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)
             else:
@@ -304,7 +312,7 @@ class FlatDDP:
                 div.div_(self.world)
             self.opt.step_range_(lo, hi)
             return
-        self._side.wait_stream(torch.cuda.current_stream(self.flat.device))
+        self._wait_grads(self._side)
         with torch.cuda.stream(self._side):
             if h is not None:
                 h.wait()  # the optimizer stream waits for RCCL's stream (host does not block)
@@ -328,7 +336,7 @@ class FlatDDP:
         self.stepped += 1
         cuda = self._side is not None
         if cuda:
-            self._side.wait_stream(torch.cuda.current_stream(f.device))
+            self._wait_grads(self._side)
         ctx = torch.cuda.stream(self._side) if cuda else _nullcontext()
         c = self._comm
         with ctx:

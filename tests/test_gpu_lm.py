@@ -304,3 +304,31 @@ def test_gelu_backward_bias_fused_matches_fp32(cuda, T, N):
     ref = torch.ops.aten.gelu_backward(da.float(), h.float(), approximate="tanh")
     torch.testing.assert_close(dh.float(), ref, rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(db.double(), dh.double().sum(0), rtol=1e-5, atol=1e-4 * T ** 0.5)
+
+
+@pytest.mark.parametrize("arch", ["llama", "gpt2"])
+def test_side_stream_weight_gradients_are_bitwise_the_inline_ones(cuda, arch, monkeypatch):
+    """The transformer blocks' weight-gradient GEMMs on the side stream (ops/lm.py _WGRAD_SIDE, queued before the data
+    gradient they overlap) write the same flat-slot gradients, bit for bit, as the same kernels inline; the loss's
+    backward joins the side stream before it returns."""
+    from polyaxon_amd.models.transformer import Transformer, gpt2_125m, lm_loss, tiny_llama
+    from polyaxon_amd.ops import lm
+    from polyaxon_amd.ops.flat import FlatParams
+
+    grads = {}
+    for side in (False, True):
+        monkeypatch.setattr(lm, "_WGRAD_SIDE", side)
+        torch.manual_seed(0)
+        cfg = (tiny_llama(d_model=256, n_heads=2, n_kv_heads=1, d_ff=512, max_seq_len=256) if arch == "llama" else
+               gpt2_125m(vocab_size=512, n_layers=2, d_model=256, n_heads=2, d_ff=1024, max_seq_len=256))
+        with torch.device(cuda):
+            model = Transformer(cfg)
+        flat = FlatParams(model, cuda, channels_last=False, lp_dtype=torch.bfloat16)
+        flat.enable_direct_grads(True)
+        tok = torch.randint(0, 256, (2, 256), device=cuda, generator=torch.Generator(device=cuda).manual_seed(3))
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = lm_loss(model(tok), tok)
+        loss.backward()
+        grads[side] = torch.cat([flat.lp_grads.float(), flat.grads]).clone()
+    assert torch.isfinite(grads[True]).all() and float(grads[True].norm()) > 0
+    assert torch.equal(grads[True], grads[False])
