@@ -234,7 +234,7 @@ def class_xent(logits: torch.Tensor, labels: torch.Tensor, in_range: bool = Fals
 # ---------------------------------------------------------------------------------------------- bias gradient
 
 
-def bias_grad(dy2: torch.Tensor, bias: torch.Tensor, gelu_h: Optional[torch.Tensor] = None):
+def bias_grad(dy2: torch.Tensor, bias: torch.Tensor, gelu_h: Optional[torch.Tensor] = None, side: bool = False):
     """db = dy2.sum(0) for ``bias``.  With a direct fp32 flat-gradient slot (ops/flat.py) the sum is written -- or,
     for a slot already written this step, accumulated -- there and None is returned (no autograd ``grad += g``
     kernel; FlatDDP still sees the parameter through its post-accumulate hook); otherwise returned in the bias
@@ -243,7 +243,10 @@ def bias_grad(dy2: torch.Tensor, bias: torch.Tensor, gelu_h: Optional[torch.Tens
     contiguous bf16 CUDA [T, N] with N % 8 == 0, torch's reduction otherwise.
 
     ``gelu_h``: dy2 is the gradient of gelu_tanh(gelu_h); returns (dh, db) with dh = dy2 * gelu_tanh'(gelu_h)
-    computed in the same pass as its column sums (plx_gelu_bwd_colsum)."""
+    computed in the same pass as its column sums (plx_gelu_bwd_colsum).
+
+    ``side``: the bias belongs to this op only; a plain column sum into its (first-written) flat slot then runs on
+    the side stream (PLX_LM_WGRAD_STREAM), beside the compute-bound GEMMs that follow it on the main stream."""
     from polyaxon_amd.ops.flat import direct_grad
 
     T, N = dy2.shape
@@ -261,14 +264,22 @@ def bias_grad(dy2: torch.Tensor, bias: torch.Tensor, gelu_h: Optional[torch.Tens
     if native:
         lib = _native.lib("plx_lm")
         dev = dy2.device
-        part = torch.empty(lib.plx_colsum_splits(T, N), N, dtype=torch.float32, device=dev)
         out = slot if slot is not None else torch.empty(N, dtype=bias.dtype, device=dev)
         mode = (2 if acc else 1) if out.dtype == torch.float32 else 0
-        cnt = _native.counters(dev, "plx_colsum")
-        if gelu_h is None:
+
+        def colsum():  # partials and tickets of the stream it runs on
+            part = torch.empty(lib.plx_colsum_splits(T, N), N, dtype=torch.float32, device=dev)
+            cnt = _native.counters(dev, f"plx_colsum:{_stream()}")
             _native.check(lib.plx_colsum(dy2.data_ptr(), T, N, part.data_ptr(), cnt.data_ptr(), out.data_ptr(), mode,
                                          _stream()), "plx_colsum")
+        if gelu_h is None:
+            if side and _WGRAD_SIDE and slot is not None and not acc:  # +1.3 % on GPT-2, r6_lm_bias_side_ab.jsonl
+                side_stream.run(colsum, (dy2,), dev)
+            else:
+                colsum()
         else:
+            part = torch.empty(lib.plx_colsum_splits(T, N), N, dtype=torch.float32, device=dev)
+            cnt = _native.counters(dev, f"plx_colsum:{_stream()}")
             dh = torch.empty_like(dy2)
             _native.check(lib.plx_gelu_bwd_colsum(dy2.data_ptr(), gelu_h.data_ptr(), dh.data_ptr(), T, N,
                                                   part.data_ptr(), cnt.data_ptr(), out.data_ptr(), mode, _stream()),
@@ -293,7 +304,7 @@ def _act_backward(ctx, dy2: torch.Tensor, h2: Optional[torch.Tensor]):
         if ctx.has_bias:
             return bias_grad(dy2, ctx.bias, gelu_h=h2)
         return torch.ops.aten.gelu_backward(dy2, h2, approximate="tanh"), None
-    return dy2, (bias_grad(dy2, ctx.bias) if ctx.has_bias else None)
+    return dy2, (bias_grad(dy2, ctx.bias, side=getattr(ctx, "side", False)) if ctx.has_bias else None)
 
 
 # ---------------------------------------------------------------------------------------------- direct-grad Linear
@@ -413,14 +424,14 @@ class _GeluMlpMfma(torch.autograd.Function):
         T, d_ff = h.shape
         d = w_down.shape[0]
         dy2 = dy.reshape(-1, d).contiguous()
-        db_down = bias_grad(dy2, ctx.b_down) if ctx.has_b[1] else None
+        db_down = bias_grad(dy2, ctx.b_down, side=True) if ctx.has_b[1] else None
         # a side-stream weight gradient forks from the main stream as it stands: queue it before the data gradient
         # it should overlap, not after (it would wait for it)
         # both weight gradients go beside the MLP's data gradients when the narrow one (T x d) leaves CUs idle:
         # GPT-2 +3.6 % on the step (r6_lm_wgrad_side_ab.jsonl), both on the side stream 0.3 % ahead of dw_up alone
         dw_down = _wgrad_into(gemm, dy2, a, ctx.slots[1], ctx.flats[1], ctx.needs_input_grad[3], side=(T, d))
         dh = gemm.gemm(dy2, w_down, T, d_ff, d, True, False, gelu_h=h)  # dA . gelu'(h) in the epilogue
-        db_up = bias_grad(dh, ctx.b_up) if ctx.has_b[0] else None
+        db_up = bias_grad(dh, ctx.b_up, side=True) if ctx.has_b[0] else None
         dw_up = _wgrad_into(gemm, dh, x2, ctx.slots[0], ctx.flats[0], ctx.needs_input_grad[1], side=(T, d))
         dx = gemm.dgrad(dh, w_up).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         return dx, dw_up, db_up, dw_down, db_down, None, None, None, None
