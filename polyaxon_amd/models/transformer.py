@@ -216,6 +216,8 @@ class Transformer(nn.Module):
     def forward(self, tokens: torch.Tensor) -> torch.Tensor:
         B, S = tokens.shape
         x = self.embed(tokens)
+        if self.head is None:  # tied head: its weight gradient may run on the side stream (lm_ops.linear side)
+            x = lm_ops.join_before_backward(x)
         rope = None
         if self.pos is not None:
             x = x + self.pos(torch.arange(S, device=tokens.device))[None]
@@ -243,7 +245,9 @@ class Transformer(nn.Module):
         # tied: the head's weight gradient is written first (into the flat slot, or returned to autograd) and the
         # embedding's arrives after it through autograd's accumulation, so both paths add up
         w = self.embed.weight if self.head is None else self.head.weight
-        return lm_ops.linear(x, w, self.logit_mask)
+        # side: the head's weight gradient beside its 192-tile data gradient and the blocks below (GPT-2: +1.6 %,
+        # profiles/r6_lm_head_side_ab.jsonl); the embedding's backward waits for it (join_before_backward above)
+        return lm_ops.linear(x, w, self.logit_mask, side=True)
 
     @staticmethod
     def _add_norm(x, r, norm):

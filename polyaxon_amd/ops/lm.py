@@ -380,6 +380,28 @@ class _LinearMfma(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
+class _SideJoin(torch.autograd.Function):
+    """Identity whose backward makes the main stream wait for every side-stream launch so far (side_stream.join)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        side_stream.join(g.device)
+        return g
+
+
+def join_before_backward(x: torch.Tensor) -> torch.Tensor:
+    """Mark ``x`` (a tied embedding's output): the ops that consume its gradient -- the embedding's backward, whose
+    weight-gradient accumulation writes the slot the tied head's side-stream weight gradient wrote -- run after the
+    side stream has finished.  Identity on the CPU and outside autograd."""
+    if not (x.is_cuda and x.requires_grad and torch.is_grad_enabled()):
+        return x
+    return _SideJoin.apply(x)
+
+
 def _wgrad_into(gemm, dz2, x2, slot, flat, needs, side=None):
     """dW = dz^T x: written / accumulated into the flat slot when there is one (returns None), else returned.
     ``side`` = (M, N) of the data gradient queued next: the weight is used by this op only (no other op of the step
