@@ -2,10 +2,16 @@
 statistics and parameters), PyTorch composition otherwise."""
 from __future__ import annotations
 
+import os
 
 import torch
 
-from polyaxon_amd.ops import _native
+from polyaxon_amd.ops import _native, side_stream
+
+# the norms' parameter-gradient reduction on the side stream (ops/side_stream.py) when every parameter has a
+# first-written flat slot: only the optimizer / FlatDDP read those, after side_stream.join / fence
+# (PLX_LM_WGRAD_STREAM=0: inline, as ops/lm.py)
+_SIDE = os.environ.get("PLX_LM_WGRAD_STREAM", "1") != "0"
 
 
 def rms_norm_reference(x: torch.Tensor, weight: torch.Tensor, eps: float) -> torch.Tensor:
@@ -43,11 +49,17 @@ def _param_grads(parts, params, d: int):
             outs.append(t)
             ret.append(t)
     nz = len(parts)
-    l2 = torch.empty(int(lib.plx_partial_colsum_workspace(nb, d, nz)), dtype=torch.float32, device=dev)
-    cnt = _native.counters(dev, "plx_partial_colsum")
-    _native.check(lib.plx_partial_colsum(parts[0].data_ptr(), parts[-1].data_ptr(), nb, d, nz, l2.data_ptr(),
-                                         cnt.data_ptr(), outs[0].data_ptr(), outs[-1].data_ptr(), accs[0], accs[-1],
-                                         _stream()), "plx_partial_colsum")
+
+    def reduce():  # workspace and tickets of the stream it runs on
+        l2 = torch.empty(int(lib.plx_partial_colsum_workspace(nb, d, nz)), dtype=torch.float32, device=dev)
+        cnt = _native.counters(dev, f"plx_partial_colsum:{_stream()}")
+        _native.check(lib.plx_partial_colsum(parts[0].data_ptr(), parts[-1].data_ptr(), nb, d, nz, l2.data_ptr(),
+                                             cnt.data_ptr(), outs[0].data_ptr(), outs[-1].data_ptr(), accs[0],
+                                             accs[-1], _stream()), "plx_partial_colsum")
+    if _SIDE and all(r is None for r in ret) and not any(accs):  # GPT-2 +0.4 %, r6_lm_norm_side_ab.jsonl
+        side_stream.run(reduce, parts, dev)
+    else:
+        reduce()
     return [r if r is None else r.to(p.dtype) for r, p in zip(ret, params)]
 
 
