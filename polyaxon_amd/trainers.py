@@ -279,6 +279,7 @@ def train_lm(argv=None) -> float:
                 xp.log_metrics(step=it + 1, loss=loss_mean[0])
             if it == args.steps - 1:
                 loss_val = float(loss_mean[0])
+    t_host = time.time() - t0  # the host has queued every step (a host time ~ dt: the GPU waited for launches)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     dt = time.time() - t0
@@ -291,6 +292,8 @@ def train_lm(argv=None) -> float:
 
         dec = _gemm.decisions()
         print(json.dumps({"loss": loss_val, "tokens_per_s": round(tok_s, 1), "world": info["world"],
+                          "ms_per_step": round(dt / max(1, args.steps - skip) * 1e3, 3),
+                          "host_ms_per_step": round(t_host / max(1, args.steps - skip) * 1e3, 3),
                           "world1_collectives": args.world1_collectives if force else "", "zero1": zero1, "bucket_launches": ddp.launched,
                           "buckets": len(ddp.buckets), "bucket_plan": ddp.plan,
                           "params_m": round(sum(s.numel for s in flat.segments) / 1e6, 1),
