@@ -410,6 +410,8 @@ def _wgrad_into(gemm, dz2, x2, slot, flat, needs, side=None):
     if slot is not None:
         acc = bool(flat.mark_written(slot))
         if side is not None and _WGRAD_SIDE and not acc and _idle_cus(dz2.device, *side):
+            # (the planner's full 256-block split on the side stream too: a 128-block target tied, 64 was -23 %,
+            # profiles/r6_lm_side_split_target_ab.jsonl)
             side_stream.run(lambda: gemm.wgrad(dz2, x2, out=slot, accumulate=False), (dz2, x2), dz2.device)
         else:
             gemm.wgrad(dz2, x2, out=slot, accumulate=acc)
