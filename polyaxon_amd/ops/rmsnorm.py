@@ -9,7 +9,8 @@ import torch
 from polyaxon_amd.ops import _native, side_stream
 
 # the norms' parameter-gradient reduction on the side stream (ops/side_stream.py) when every parameter has a
-# first-written flat slot: only the optimizer / FlatDDP read those, after side_stream.join / fence
+# first-written flat slot and the side stream is in use this backward: only the optimizer / FlatDDP read those, after
+# side_stream.join / fence
 # (PLX_LM_WGRAD_STREAM=0: inline, as ops/lm.py)
 _SIDE = os.environ.get("PLX_LM_WGRAD_STREAM", "1") != "0"
 
@@ -56,7 +57,10 @@ def _param_grads(parts, params, d: int):
         _native.check(lib.plx_partial_colsum(parts[0].data_ptr(), parts[-1].data_ptr(), nb, d, nz, l2.data_ptr(),
                                              cnt.data_ptr(), outs[0].data_ptr(), outs[-1].data_ptr(), accs[0],
                                              accs[-1], _stream()), "plx_partial_colsum")
-    if _SIDE and all(r is None for r in ret) and not any(accs):  # GPT-2 +0.4 %, r6_lm_norm_side_ab.jsonl
+    # only beside side-stream work this backward already queued (GPT-2's weight gradients: +0.4 %,
+    # r6_lm_norm_side_ab.jsonl); alone on it (Llama-3 8B, whose weight gradients stay inline) it cost 0.8 %
+    # (r6_lm_norm_side_llama_ab.jsonl)
+    if _SIDE and side_stream.busy(dev) and all(r is None for r in ret) and not any(accs):
         side_stream.run(reduce, parts, dev)
     else:
         reduce()

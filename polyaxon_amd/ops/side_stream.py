@@ -97,6 +97,13 @@ def run(fn: Callable[[], None], tensors: Iterable[torch.Tensor], dev: torch.devi
         torch.autograd.Variable._execution_engine.queue_callback(lambda d=dev: join(d))
 
 
+def busy(dev: torch.device) -> bool:
+    """Has this backward queued side-stream work that the end-of-backward join has not yet covered?"""
+    if dev.type != "cuda":
+        return False
+    return bool(_pending.get(dev.index if dev.index is not None else torch.cuda.current_device()))
+
+
 def fence(stream: "torch.cuda.Stream", dev: torch.device) -> None:
     """``stream`` waits for every side-stream launch queued so far on this device, without stalling the main stream:
     a consumer of flat-slot gradients that runs before the end-of-backward join (FlatDDP's bucket all-reduce, fired by
