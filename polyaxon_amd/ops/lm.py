@@ -412,6 +412,8 @@ def _wgrad_into(gemm, dz2, x2, slot, flat, needs, side=None):
         if side is not None and _WGRAD_SIDE and not acc and _idle_cus(dz2.device, *side):
             # (the planner's full 256-block split on the side stream too: a 128-block target tied, 64 was -23 %,
             # profiles/r6_lm_side_split_target_ab.jsonl)
+            # (token chunks for the unsplit tied head, so its long workgroups free CUs sooner: neutral,
+            # profiles/r6_lm_head_wgrad_chunk_ab.jsonl)
             side_stream.run(lambda: gemm.wgrad(dz2, x2, out=slot, accumulate=False), (dz2, x2), dz2.device)
         else:
             gemm.wgrad(dz2, x2, out=slot, accumulate=acc)
